@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""bench.py -- resimulated session-frames/s of the batched SyncTest rollback program on MI355X.
+
+Workload (BASELINE.json configs[1]): ex_game state x 4096 independent
+sessions per GPU, an 8-frame rollback every frame (SyncTestSession with check_distance 8,
+max_prediction 9), 2 players, held-key synthetic inputs.  One step = one fused launch running
+`--frames-per-step` SyncTest frames on every session: per frame and session 1 LoadGameState,
+8 resimulated AdvanceFrames (the metric's unit), 8 SaveGameStates with fused Fletcher-16, the
+checksum comparisons, and the new frame's AdvanceFrame.
+
+Multi-GPU: one process per GPU (torch.distributed.run); sessions are sharded across ranks with no
+data-path collective (SyncTest has no exchange step), so scaling is weak and `value` is the sum
+of all ranks' resimulated session-frames over the max-over-ranks wall time.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--frames-per-step F]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def bytes_per_synctest_call(P, cd):
+    """Algorithmic HBM bytes one lane moves per SyncTest frame (DESIGN.md "Roofline"): load one
+    state, cd saves of state + u16 checksum, the first-seen checksum, 2 u16 reads per comparison
+    (cd - 1 of them), one input byte per player for each of the cd + 1 advances."""
+    S = 4 + 20 * P
+    return S + cd * (S + 2) + 2 + 4 * (cd - 1) + (cd + 1) * P
+
+
+def pmc_traffic(workload):
+    """Per-launch HBM bytes from the committed rocprofv3 PMC summary, if one exists for this
+    workload (profiles/pmc_<workload>.json written by tools/profile_pmc.py), else None."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as fh:
+            return float(json.load(fh)["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames-per-step", type=int, default=128)
+    ap.add_argument("--lanes", type=int, default=4096, help="sessions per GPU (config 2: 4096)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores available)")
+    ap.add_argument("--cpu-frames", type=int, default=100000, help="SyncTest frames per CPU thread")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and rank == 0:
+        print(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world} rank(s)", file=sys.stderr)
+
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from ggrs_amd import Engine
+    from ggrs_amd import synth
+
+    P, maxp, cd, delay = 2, 9, 8, 0
+    lanes, fps = args.lanes, args.frames_per_step
+    total_frames = (args.warmup + args.steps) * fps
+    assert args.warmup * fps > cd, "warm-up must cover the first check_distance frames"
+    trace_cap = min(256, total_frames)
+
+    inputs = synth.gen_inputs(rank * lanes, lanes, total_frames, P, synth.MODEL_HELD)
+    eng = Engine(lanes, P, maxp, cd, delay, input_capacity=total_frames + cd + delay + 2,
+                 device=local_rank, trace_capacity=trace_cap)
+    eng.add_local_inputs(0, inputs)  # resident in HBM before anything is timed
+    eng.synchronize()
+
+    def barrier():
+        eng.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        eng.synctest_advance_frames(fps)
+    barrier()
+    eng.timing_reset()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.synctest_advance_frames(fps)
+    barrier()
+    t1 = time.perf_counter()
+    kernel_ms, launches = eng.timing_read()
+    elapsed = t1 - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    status, _, _ = eng.mismatches()
+    halted = int((status != 0).sum())  # a halted lane would stop resimulating: must be none
+    resim_per_rank = lanes * cd * fps * args.steps
+    total_resim = resim_per_rank * world
+    value = total_resim / elapsed
+
+    # roofline of the one kernel that runs in the timed region (synctest_kernel<2>)
+    per_call = bytes_per_synctest_call(P, cd)
+    bytes_per_launch = lanes * fps * per_call
+    avg_launch_s = kernel_ms / 1e3 / max(launches, 1)
+    achieved = bytes_per_launch / avg_launch_s / 1e9
+    workload = f"config2_l{lanes}_f{fps}"
+    roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(workload),
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+                "note": "VALU-bound (f32 step + f64 glibc sincosf); working set fits L2/MALL"}
+
+    parity = None
+    cpu_baseline = None
+    if rank == 0:
+        try:
+            from oracle import oracle as O  # checker + CPU baseline only
+            O.build()
+            ref = O.synctest_run(inputs[:, 0, :], P, maxp, cd, delay)
+            parity = {"lane0_final_state_bit_exact": bytes(eng.state(0)) == bytes(ref["final_state"]),
+                      "lane0_trace_bit_exact": bool(
+                          (eng.trace(total_frames - trace_cap, trace_cap)[:, 0] ==
+                           ref["cksum"][total_frames - trace_cap:]).all())}
+            if world == 1 and not args.no_cpu_baseline:
+                try:
+                    avail = len(os.sched_getaffinity(0))
+                except AttributeError:
+                    avail = os.cpu_count() or 1
+                threads = args.cpu_threads or min(16, avail)
+                frames = max(args.cpu_frames, total_frames)
+                n, wall, ck0 = O.synctest_bench(threads, frames, warmup=0, num_players=P,
+                                                max_prediction=maxp, check_distance=cd,
+                                                input_delay=delay, model=O.MODEL_HELD,
+                                                seed_base=synth.SEED_BASE)
+                gpu_tr = eng.trace(total_frames - trace_cap, trace_cap)[:, 0]
+                cpu_baseline = {
+                    "value": round(n / wall, 1), "unit": "session-frames/s", "cores": threads,
+                    "kind": "port",
+                    "sample": f"{threads} threads x {frames} SyncTest frames (1 session/thread, "
+                              f"cd {cd}, 2 players, held-key inputs), C restatement of the "
+                              f"reference loop (oracle/ggrs_oracle.c)",
+                    "wall_s": round(wall, 3),
+                    "thread0_matches_gpu_lane0": bool((ck0[total_frames - trace_cap:total_frames] == gpu_tr).all()),
+                }
+        except Exception as exc:  # the oracle is optional on the measurement path
+            parity = {"error": repr(exc)}
+
+    if rank == 0:
+        line = {
+            "metric": "resimulated session-frames/sec (node)",
+            "value": round(value, 1),
+            "unit": "session-frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {"workload": "config2: ex_game x 4096 sessions/GPU, SyncTest 8-frame rollback "
+                                   "every frame (check_distance 8, max_prediction 9), 2 players, "
+                                   "held-key inputs",
+                       "sessions_per_gpu": lanes, "global_sessions": lanes * world,
+                       "frames_per_step": fps, "players": P, "check_distance": cd,
+                       "max_prediction": maxp, "parallelism": f"sessions sharded over {world} GPU(s)"},
+            "roofline": roofline,
+            "cpu_baseline": cpu_baseline,
+            "halted_lanes": halted,
+            "parity": parity,
+        }
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,113 @@
+"""ctypes binding of the engine's C ABI (include/ggrs_amd.h) -- libggrs_amd.so, built in-tree.
+
+There is no fallback: if the HIP library is missing or fails to load, every entry point raises.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libggrs_amd.so")
+
+GGRS_OK = 0
+GGRS_E_INVALID = -1
+GGRS_E_PRECONDITION = -2
+GGRS_E_HIP = -3
+GGRS_E_STATE = -4
+NULL_FRAME = -1
+REQ_SAVE, REQ_LOAD, REQ_ADVANCE = 0, 1, 2
+STATUS_CONFIRMED, STATUS_PREDICTED, STATUS_DISCONNECTED = 0, 1, 2
+LANE_RUNNING, LANE_MISMATCH = 0, 1
+
+# every symbol include/ggrs_amd.h declares (tests check the library exports all of them)
+EXPORTS = (
+    "ggrs_abi_version", "ggrs_last_error", "ggrs_engine_create", "ggrs_engine_destroy",
+    "ggrs_engine_config", "ggrs_add_local_inputs", "ggrs_add_local_inputs_device",
+    "ggrs_synctest_advance_frames", "ggrs_handle_requests", "ggrs_synchronize",
+    "ggrs_current_frame", "ggrs_read_mismatches", "ggrs_read_save_checksums", "ggrs_read_state",
+    "ggrs_read_ring", "ggrs_read_trace", "ggrs_debug_corrupt_on_load", "ggrs_last_launch_ms",
+    "ggrs_timing_reset", "ggrs_timing_read",
+)
+
+
+class Config(ctypes.Structure):
+    _fields_ = [
+        ("num_lanes", ctypes.c_int32),
+        ("num_players", ctypes.c_int32),
+        ("max_prediction", ctypes.c_int32),
+        ("check_distance", ctypes.c_int32),
+        ("input_delay", ctypes.c_int32),
+        ("input_capacity", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("trace_capacity", ctypes.c_int32),
+    ]
+
+
+class Request(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("frame", ctypes.c_int32)]
+
+
+class GgrsError(Exception):
+    """Mirror of GgrsError (src/error.rs:31-57) for errors the engine reports."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+class InvalidRequest(GgrsError):
+    """GgrsError::InvalidRequest (error.rs:39-43)."""
+
+
+class PreconditionError(GgrsError):
+    """A condition on which the reference panics (assert!), reported instead of unwinding."""
+
+
+_lib = None
+
+
+def lib():
+    """Load libggrs_amd.so (raises OSError if it has not been built: no CPU fallback exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f"{LIB_PATH} not built: run `python -m ggrs_amd.build` "
+                          "(the engine has no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.POINTER
+        vp = ctypes.c_void_p
+        L.ggrs_abi_version.restype = ctypes.c_int32
+        L.ggrs_last_error.restype = ctypes.c_char_p
+        L.ggrs_engine_create.argtypes = [P(Config), P(vp)]
+        L.ggrs_engine_destroy.argtypes = [vp]
+        L.ggrs_engine_config.argtypes = [vp, P(Config)]
+        L.ggrs_add_local_inputs.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp]
+        L.ggrs_add_local_inputs_device.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp]
+        L.ggrs_synctest_advance_frames.argtypes = [vp, ctypes.c_int32]
+        L.ggrs_handle_requests.argtypes = [vp, P(Request), ctypes.c_int32, vp, vp]
+        L.ggrs_synchronize.argtypes = [vp]
+        L.ggrs_current_frame.argtypes = [vp, P(ctypes.c_int32)]
+        L.ggrs_read_mismatches.argtypes = [vp, vp, vp, vp]
+        L.ggrs_read_save_checksums.argtypes = [vp, ctypes.c_int32, vp]
+        L.ggrs_read_state.argtypes = [vp, ctypes.c_int32, vp]
+        L.ggrs_read_ring.argtypes = [vp, ctypes.c_int32, vp, vp, vp]
+        L.ggrs_read_trace.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp]
+        L.ggrs_debug_corrupt_on_load.argtypes = [vp, ctypes.c_int32, ctypes.c_int32]
+        L.ggrs_last_launch_ms.argtypes = [vp, P(ctypes.c_float)]
+        L.ggrs_timing_reset.argtypes = [vp]
+        L.ggrs_timing_read.argtypes = [vp, P(ctypes.c_float), P(ctypes.c_int32)]
+        for name in EXPORTS:
+            if name not in ("ggrs_abi_version", "ggrs_last_error"):
+                getattr(L, name).restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc == GGRS_OK:
+        return
+    msg = lib().ggrs_last_error().decode(errors="replace")
+    if rc == GGRS_E_INVALID:
+        raise InvalidRequest(rc, msg)
+    if rc == GGRS_E_PRECONDITION:
+        raise PreconditionError(rc, msg)
+    raise GgrsError(rc, msg)

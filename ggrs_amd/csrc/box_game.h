@@ -1,0 +1,184 @@
+// ex_game box-game state, step and fused Fletcher-16, for one lane per (session, branch).
+//
+// Reference: examples/ex_game/ex_game.rs
+//   constants              :10-26
+//   fletcher16             :45-55   (over bincode::serialize(&State), :105-106 and :121-122)
+//   State                  :236-243 (frame, num_players, positions, velocities, rotations)
+//   State::new             :246-269
+//   State::advance         :271-333
+// Bit-exactness rules: separately rounded f32 ops in the reference's order
+// (compile with -ffp-contract=off; Rust never contracts), correctly rounded f32 sqrt and division
+// (hipcc's default), f32 denormals kept (hipcc's default), glibc's own sinf/cosf algorithm
+// (glibc_sincosf.h), exact fmodf for rem_euclid.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "glibc_sincosf.h"
+
+#pragma clang fp contract(off)
+
+namespace ggrs {
+
+constexpr float kWindowHeight = 800.0f;
+constexpr float kWindowWidth = 600.0f;
+constexpr float kMovementSpeed = 15.0f / 60.0f;  // 15.0 / FPS as f32
+constexpr float kRotationSpeed = 2.5f / 60.0f;   // 2.5 / FPS as f32 (0x1.555556p-5)
+constexpr float kMaxSpeed = 7.0f;
+constexpr float kFriction = 0.98f;
+constexpr float kPi = 3.14159265358979323846f;   // std::f32::consts::PI
+constexpr float kTwoPi = 2.0f * kPi;             // 2.0 * PI evaluated in f32
+constexpr uint32_t kInputUp = 1u, kInputDown = 2u, kInputLeft = 4u, kInputRight = 8u;
+
+// Number of 32-bit fields of the SoA state: frame + (x, y, vx, vy, rot) per player.
+__host__ __device__ constexpr int state_fields(int p) { return 1 + 5 * p; }
+// bincode size of State (fixint LE): i32 + u64 + 3 * (u64 len) + 20 * P.
+__host__ __device__ constexpr int bincode_bytes(int p) { return 36 + 20 * p; }
+
+// SoA field index, in bincode order: frame, (x_i, y_i)*, (vx_i, vy_i)*, rot_i*.
+__host__ __device__ constexpr int fld_frame() { return 0; }
+__host__ __device__ constexpr int fld_x(int p, int i) { return 1 + 2 * i; }
+__host__ __device__ constexpr int fld_y(int p, int i) { return 2 + 2 * i; }
+__host__ __device__ constexpr int fld_vx(int p, int i) { return 1 + 2 * p + 2 * i; }
+__host__ __device__ constexpr int fld_vy(int p, int i) { return 2 + 2 * p + 2 * i; }
+__host__ __device__ constexpr int fld_rot(int p, int i) { return 1 + 4 * p + i; }
+// byte offset of SoA field k inside the bincode encoding
+__host__ __device__ constexpr int fld_offset(int p, int k) {
+  return k == 0 ? 0 : (k <= 2 * p ? 20 + 4 * (k - 1) : (k <= 4 * p ? 28 + 4 * (k - 1) : 36 + 4 * (k - 1)));
+}
+
+template <int P>
+struct BoxState {
+  uint32_t w[state_fields(P)];  // raw bits; w[0] is the i32 frame
+  __device__ __host__ float f(int k) const { return __builtin_bit_cast(float, w[k]); }
+  __device__ __host__ void set(int k, float v) { w[k] = __builtin_bit_cast(uint32_t, v); }
+};
+
+// f32::rem_euclid: r = a % b (fmodf, exact); if r < 0 { r + |b| } else { r }.
+// The fast path is exact fmod for |a| < 2|b| (Sterbenz), which covers rot +- ROTATION_SPEED for
+// every rot in [0, 2*pi]; anything else takes the library fmodf (exact as well).
+__device__ inline float rem_euclid(float a, float b) {
+  float aa = __builtin_fabsf(a), ab = __builtin_fabsf(b);
+  float r;
+  if (aa < ab) r = a;
+  else if (aa < 2.0f * ab) r = __builtin_copysignf(aa - ab, a);
+  else r = fmodf(a, b);
+  return r < 0.0f ? r + ab : r;
+}
+
+// One player of State::advance (ex_game.rs:276-331).  `input` is Input.inp, already mapped to 4
+// for InputStatus::Disconnected by the caller (ex_game.rs:277-281).
+__device__ inline void advance_player(float& x, float& y, float& vx, float& vy, float& rot,
+                                      uint32_t input) {
+  float vel_x = vx * kFriction;
+  float vel_y = vy * kFriction;
+  const bool up = (input & kInputUp) != 0, down = (input & kInputDown) != 0;
+  const bool left = (input & kInputLeft) != 0, right = (input & kInputRight) != 0;
+  if (up != down) {  // thrust (up && !down) or brake (!up && down), both with the OLD rot
+    float s, c;
+    if (__builtin_fabsf(rot) < 120.0f) {
+      glibc_sincosf_small(rot, &s, &c);
+    } else {
+      s = glibc_sinf(rot);
+      c = glibc_cosf(rot);
+    }
+    const float dx = kMovementSpeed * c, dy = kMovementSpeed * s;
+    if (up) {
+      vel_x = vel_x + dx;
+      vel_y = vel_y + dy;
+    } else {
+      vel_x = vel_x - dx;
+      vel_y = vel_y - dy;
+    }
+  }
+  if (left && !right) rot = rem_euclid(rot - kRotationSpeed, kTwoPi);
+  if (!left && right) rot = rem_euclid(rot + kRotationSpeed, kTwoPi);
+  const float magnitude = __builtin_sqrtf(vel_x * vel_x + vel_y * vel_y);
+  if (magnitude > kMaxSpeed) {
+    vel_x = (vel_x * kMaxSpeed) / magnitude;
+    vel_y = (vel_y * kMaxSpeed) / magnitude;
+  }
+  float nx = x + vel_x, ny = y + vel_y;
+  nx = __builtin_fmaxf(nx, 0.0f);
+  nx = __builtin_fminf(nx, kWindowWidth);
+  ny = __builtin_fmaxf(ny, 0.0f);
+  ny = __builtin_fminf(ny, kWindowHeight);
+  x = nx;
+  y = ny;
+  vx = vel_x;
+  vy = vel_y;
+}
+
+// State::advance for all players.  `inputs` packs player i's Input.inp in byte i; a set bit i of
+// `disconnected` marks InputStatus::Disconnected (the player spins: input 4).
+template <int P>
+__device__ inline void advance_state(BoxState<P>& s, uint32_t inputs, uint32_t disconnected) {
+  s.w[0] = (uint32_t)((int32_t)s.w[0] + 1);
+#pragma unroll
+  for (int i = 0; i < P; i++) {
+    uint32_t in = (disconnected >> i) & 1u ? 4u : (inputs >> (8 * i)) & 0xffu;
+    float x = s.f(fld_x(P, i)), y = s.f(fld_y(P, i)), vx = s.f(fld_vx(P, i)), vy = s.f(fld_vy(P, i));
+    float rot = s.f(fld_rot(P, i));
+    advance_player(x, y, vx, vy, rot, in);
+    s.set(fld_x(P, i), x);
+    s.set(fld_y(P, i), y);
+    s.set(fld_vx(P, i), vx);
+    s.set(fld_vy(P, i), vy);
+    s.set(fld_rot(P, i), rot);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fletcher-16 of the bincode encoding, without materialising the bytes.
+// fletcher16 reduces mod 255 after every byte; since x -> x mod 255 is a ring homomorphism,
+//   sum1 = sum_j d_j (mod 255),  sum2 = sum_j (n - j) d_j (mod 255)  over the n = 36+20P bytes.
+// A 32-bit field at byte offset o contributes dot4(w, [1,1,1,1]) to sum1 and
+// dot4(w, [n-o, n-o-1, n-o-2, n-o-3]) to sum2 (weights <= 116 fit a byte): two v_dot4_u32_u8.
+// The u64 length prefixes (= P) are constants folded into kSum1Const / kSum2Const.
+__host__ __device__ constexpr uint32_t weights_at(int n, int o) {
+  return (uint32_t)(n - o) | ((uint32_t)(n - o - 1) << 8) | ((uint32_t)(n - o - 2) << 16) |
+         ((uint32_t)(n - o - 3) << 24);
+}
+template <int P>
+struct Fletcher {
+  static constexpr int n = bincode_bytes(P);
+  // num_players u64 at 4, positions len at 12, velocities len at 20+8P, rotations len at 28+16P:
+  // each has low byte P and seven zero bytes.
+  static constexpr uint32_t kSum1Const = 4u * P;
+  static constexpr uint32_t kSum2Const =
+      (uint32_t)P * ((n - 4) + (n - 12) + (n - (20 + 8 * P)) + (n - (28 + 16 * P)));
+};
+
+__device__ inline uint32_t dot4_u8(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_udot4(a, b, c, false);
+}
+
+template <int P>
+__device__ inline uint16_t fletcher16_state(const BoxState<P>& s) {
+  constexpr int n = Fletcher<P>::n;
+  uint32_t s1 = Fletcher<P>::kSum1Const, s2 = Fletcher<P>::kSum2Const;
+#pragma unroll
+  for (int k = 0; k < state_fields(P); k++) {
+    s1 = dot4_u8(s.w[k], 0x01010101u, s1);
+    s2 = dot4_u8(s.w[k], weights_at(n, fld_offset(P, k)), s2);
+  }
+  return (uint16_t)(((s2 % 255u) << 8) | (s1 % 255u));
+}
+
+// Host mirror of the same closed form (used by the C ABI's host-side helpers/tests).
+template <int P>
+inline uint16_t fletcher16_state_host(const uint32_t* w) {
+  constexpr int n = Fletcher<P>::n;
+  uint64_t s1 = Fletcher<P>::kSum1Const, s2 = Fletcher<P>::kSum2Const;
+  for (int k = 0; k < state_fields(P); k++) {
+    uint32_t wt = weights_at(n, fld_offset(P, k));
+    for (int b = 0; b < 4; b++) {
+      uint32_t byte = (w[k] >> (8 * b)) & 0xff;
+      s1 += byte;
+      s2 += byte * ((wt >> (8 * b)) & 0xff);
+    }
+  }
+  return (uint16_t)(((s2 % 255u) << 8) | (s1 % 255u));
+}
+
+}  // namespace ggrs

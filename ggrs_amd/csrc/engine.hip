@@ -1,0 +1,765 @@
+// engine.hip -- the MI355X batched rollback-resimulation engine: HBM-resident SoA state ring,
+// fused SyncTest / request-program kernels (one lane per (session, branch)), C ABI.
+//
+// Reference path (caspark/ggrs 0.10.2): SyncTestSession::advance_frame
+// (src/sessions/sync_test_session.rs:85-150) driving SyncLayer (src/sync_layer.rs:144-375) and the
+// user's request handler Game::handle_requests (examples/ex_game/ex_game.rs:79-127).  The C ABI is
+// declared in include/ggrs_amd.h (each entry point cites the reference interface it replaces).
+//
+// HBM layout (lane-fastest structure of arrays, every access coalesced across a wavefront):
+//   cur      [F][L]     u32  current game state; F = 1 + 5P fields in bincode order
+//   ring     [R][F][L]  u32  saved-state ring, slot = frame % R (SavedStates::get_cell :161-166)
+//   ring_ck  [R][L]     u16  checksum stored with each saved cell (GameStateCell.checksum)
+//   first_ck [R][L]     u16  SyncTest checksum_history: first checksum seen for each frame
+//   inputs   [C][L][Pp] u8   input queue, slot = queue frame % C (InputQueue, input_queue.rs:10-37)
+//   trace    [T][L]     u16  optional per-frame display checksum (ex_game.rs:121-126)
+// Frame bookkeeping (current frame, which frame each ring slot holds) is identical for all lanes
+// of an engine -- lanes run the same request program -- so it lives on the host and reaches the
+// kernels as scalars; only halted lanes (MismatchedChecksum) leave the common program.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ggrs_amd.h"
+#include "box_game.h"
+
+#pragma clang fp contract(off)
+
+using namespace ggrs;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int set_error(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                       \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess) return set_error(GGRS_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+constexpr int kWave = 64;
+
+inline int padded_players(int p) { return p <= 1 ? 1 : (p == 2 ? 2 : 4); }
+
+// ------------------------------------------------------------------------------ device helpers
+template <int P>
+struct InputWord;
+template <>
+struct InputWord<1> { using T = uint8_t; };
+template <>
+struct InputWord<2> { using T = uint16_t; };
+template <>
+struct InputWord<3> { using T = uint32_t; };
+template <>
+struct InputWord<4> { using T = uint32_t; };
+
+template <int P>
+__device__ inline uint32_t load_inputs(const uint8_t* base, int64_t idx) {
+  using T = typename InputWord<P>::T;
+  return (uint32_t)reinterpret_cast<const T*>(base)[idx];
+}
+
+template <int P>
+__device__ inline void load_state(BoxState<P>& s, const uint32_t* base, int64_t L) {
+#pragma unroll
+  for (int k = 0; k < state_fields(P); k++) s.w[k] = base[k * L];
+}
+template <int P>
+__device__ inline void store_state(const BoxState<P>& s, uint32_t* base, int64_t L) {
+#pragma unroll
+  for (int k = 0; k < state_fields(P); k++) base[k * L] = s.w[k];
+}
+
+// exact fmod for |a| < 2|b| (Sterbenz), library fmodf otherwise
+__device__ inline float fmod_exact(float a, float b) {
+  float aa = __builtin_fabsf(a), ab = __builtin_fabsf(b);
+  if (aa < ab) return a;
+  if (aa < 2.0f * ab) return __builtin_copysignf(aa - ab, a);
+  return fmodf(a, b);
+}
+
+// ------------------------------------------------------------------------------ kernels
+// State::new(P) for every lane (ex_game.rs:246-269)
+template <int P>
+__global__ __launch_bounds__(256) void init_states_kernel(uint32_t* cur, int64_t L) {
+  const int64_t lane = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= L) return;
+  BoxState<P> s;
+  s.w[0] = 0;
+  const float r = kWindowWidth / 4.0f;
+#pragma unroll
+  for (int i = 0; i < P; i++) {
+    float rot = (float)i / (float)P * 2.0f * kPi;
+    s.set(fld_x(P, i), kWindowWidth / 2.0f + r * glibc_cosf(rot));
+    s.set(fld_y(P, i), kWindowHeight / 2.0f + r * glibc_sinf(rot));
+    s.set(fld_vx(P, i), 0.0f);
+    s.set(fld_vy(P, i), 0.0f);
+    s.set(fld_rot(P, i), fmod_exact(rot + kPi, 2.0f * kPi));
+  }
+  store_state<P>(s, cur + lane, L);
+}
+
+struct SyncTestParams {
+  int64_t L;
+  int32_t R, cd, f0, n, cap, trace_cap;
+  int32_t corrupt_lane, corrupt_frame;
+  uint32_t* cur;
+  uint32_t* ring;
+  uint16_t* ring_ck;
+  uint16_t* first_ck;
+  const uint8_t* inputs;
+  int32_t* lane_status;
+  int32_t* mis_frame;
+  uint64_t* mis_mask;
+  uint16_t* trace;
+};
+
+template <int P>
+__device__ inline uint16_t save_cell(const SyncTestParams& p, const BoxState<P>& s, int slot,
+                                     int64_t lane) {
+  store_state<P>(s, p.ring + (int64_t)slot * state_fields(P) * p.L + lane, p.L);
+  const uint16_t ck = fletcher16_state<P>(s);
+  p.ring_ck[(int64_t)slot * p.L + lane] = ck;
+  return ck;
+}
+
+// n SyncTest frames for every running lane, each: [checksums_consistent over f-cd..f]
+// [Load f-cd, (Advance, Save)..., Advance]  Save f, Advance  -- sync_test_session.rs:85-150.
+// Which cells and history entries exist is a pure function of (f, cd, R) for a session driven
+// only by this program since frame 0 (see DESIGN.md "SyncTest bookkeeping"):
+//   * at call f the ring holds every frame in [f-R, f-1], so each frame in [f-cd, f-1] is present
+//     and frame f is not;
+//   * frame fc enters checksum_history at call max(fc+1, cd+1) with the checksum of its first
+//     save (call fc's "save current state"), kept in first_ck; it is compared against the cell at
+//     every later call while fc >= f-cd, i.e. at call f >= cd+2 for fc in [f-cd, f-2].
+template <int P>
+__global__ __launch_bounds__(kWave) void synctest_kernel(SyncTestParams p) {
+  const int64_t lane = (int64_t)blockIdx.x * kWave + threadIdx.x;
+  if (lane >= p.L) return;
+  if (p.lane_status[lane] != GGRS_LANE_RUNNING) return;
+  const int64_t L = p.L;
+  BoxState<P> s;
+  load_state<P>(s, p.cur + lane, L);
+  const int32_t cd = p.cd, R = p.R;
+  for (int32_t f = p.f0; f < p.f0 + p.n; ++f) {
+    if (cd > 0 && f > cd) {
+      if (f >= cd + 2) {
+        uint64_t mism = 0;
+        for (int32_t fc = f - cd; fc <= f - 2; ++fc) {
+          const int64_t o = (int64_t)(fc % R) * L + lane;
+          if (p.ring_ck[o] != p.first_ck[o]) mism |= 1ull << (fc - (f - cd));
+        }
+        if (mism) {  // GgrsError::MismatchedChecksum: the session stops before the rollback
+          p.lane_status[lane] = GGRS_LANE_MISMATCH;
+          p.mis_frame[lane] = f;
+          p.mis_mask[lane] = mism;
+          break;
+        }
+      }
+      int32_t g = f - cd;  // adjust_gamestate(f - cd): Load, then cd x (Save unless first, Advance)
+      load_state<P>(s, p.ring + (int64_t)(g % R) * state_fields(P) * L + lane, L);
+      if (lane == p.corrupt_lane && f == p.corrupt_frame) s.w[fld_x(P, 0)] ^= 1u;
+      for (int32_t i = 0; i < cd; ++i, ++g) {
+        if (i > 0) save_cell<P>(p, s, g % R, lane);
+        advance_state<P>(s, load_inputs<P>(p.inputs, (int64_t)(g % p.cap) * L + lane), 0u);
+      }
+    }
+    if (cd > 0) {  // save_current_state + its first sighting in checksum_history
+      const uint16_t ck = save_cell<P>(p, s, f % R, lane);
+      p.first_ck[(int64_t)(f % R) * L + lane] = ck;
+    }
+    advance_state<P>(s, load_inputs<P>(p.inputs, (int64_t)(f % p.cap) * L + lane), 0u);
+    if (p.trace) p.trace[(int64_t)(f % p.trace_cap) * L + lane] = fletcher16_state<P>(s);
+  }
+  store_state<P>(s, p.cur + lane, L);
+}
+
+struct RequestParams {
+  int64_t L;
+  int32_t R, n_reqs, trace_cap;
+  const int32_t* reqs;        // [n_reqs][2] kind, frame
+  const uint8_t* inputs;      // [n_adv][L][Pp]
+  const uint8_t* status;      // [n_adv][L][Pp] or null
+  uint32_t* cur;
+  uint32_t* ring;
+  uint16_t* ring_ck;
+  uint16_t* trace;
+};
+
+// Game::handle_requests (ex_game.rs:79-99) for one ordered request list on every lane.
+template <int P>
+__global__ __launch_bounds__(kWave) void requests_kernel(RequestParams p) {
+  const int64_t lane = (int64_t)blockIdx.x * kWave + threadIdx.x;
+  if (lane >= p.L) return;
+  const int64_t L = p.L;
+  BoxState<P> s;
+  load_state<P>(s, p.cur + lane, L);
+  int64_t adv = 0;
+  for (int32_t r = 0; r < p.n_reqs; ++r) {
+    const int32_t kind = p.reqs[2 * r], frame = p.reqs[2 * r + 1];
+    const int32_t slot = frame % p.R;
+    if (kind == GGRS_REQ_LOAD) {
+      load_state<P>(s, p.ring + (int64_t)slot * state_fields(P) * L + lane, L);
+    } else if (kind == GGRS_REQ_SAVE) {
+      store_state<P>(s, p.ring + (int64_t)slot * state_fields(P) * L + lane, L);
+      p.ring_ck[(int64_t)slot * L + lane] = fletcher16_state<P>(s);
+    } else {
+      const int64_t idx = adv * L + lane;
+      uint32_t disc = 0;
+      if (p.status) {
+        const uint32_t st = load_inputs<P>(p.status, idx);
+#pragma unroll
+        for (int i = 0; i < P; i++)
+          if (((st >> (8 * i)) & 0xffu) == GGRS_STATUS_DISCONNECTED) disc |= 1u << i;
+      }
+      advance_state<P>(s, load_inputs<P>(p.inputs, idx), disc);
+      if (p.trace) p.trace[(int64_t)((int32_t)s.w[0] - 1) % p.trace_cap * L + lane] = fletcher16_state<P>(s);
+      ++adv;
+    }
+  }
+  store_state<P>(s, p.cur + lane, L);
+}
+
+// Repack [n][L][P] user inputs into the [C][L][Pp] queue at queue frames q0.. (wrapping).
+__global__ void pack_inputs_kernel(const uint8_t* src, uint8_t* dst, int64_t L, int32_t P,
+                                   int32_t Pp, int32_t n, int32_t q0, int32_t cap) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)n * L) return;
+  const int64_t fr = i / L, lane = i % L;
+  const int64_t q = ((int64_t)q0 + fr) % cap;
+  for (int k = 0; k < Pp; k++) dst[(q * L + lane) * Pp + k] = k < P ? src[i * P + k] : 0;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------ engine object
+struct ggrs_engine {
+  ggrs_config_t cfg{};
+  int Pp = 1, F = 1, R = 1, cap = 128;
+  int mode = 0;  // 0 fresh, 1 synctest program, 2 request program
+  hipStream_t stream = nullptr;
+  uint32_t* cur = nullptr;
+  uint32_t* ring = nullptr;
+  uint16_t* ring_ck = nullptr;
+  uint16_t* first_ck = nullptr;
+  uint8_t* inputs = nullptr;
+  int32_t* lane_status = nullptr;
+  int32_t* mis_frame = nullptr;
+  uint64_t* mis_mask = nullptr;
+  uint16_t* trace = nullptr;
+  uint8_t* staging = nullptr;  // device scratch for request inputs / status / request list
+  size_t staging_bytes = 0;
+  // host-side (lane-uniform) bookkeeping
+  int32_t current_frame = 0;
+  int32_t next_user_frame = 0;  // next user frame add_local_inputs expects
+  std::vector<int32_t> ring_tag;
+  int32_t corrupt_lane = -1, corrupt_frame = -1;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+  // per-launch event pairs collected between ggrs_timing_reset and ggrs_timing_read
+  std::vector<hipEvent_t> tev;
+  size_t tev_used = 0;
+  bool collecting = false;
+  hipEvent_t ev_last0 = nullptr, ev_last1 = nullptr;
+};
+
+namespace {
+
+int ensure_staging(ggrs_engine* e, size_t bytes) {
+  if (bytes <= e->staging_bytes) return GGRS_OK;
+  if (e->staging) HIP_TRY(hipFree(e->staging));
+  e->staging = nullptr;
+  e->staging_bytes = 0;
+  HIP_TRY(hipMalloc(&e->staging, bytes));
+  e->staging_bytes = bytes;
+  return GGRS_OK;
+}
+
+// Brackets one fused launch with HIP events on the engine's stream (the stream the kernel runs
+// on), so ggrs_last_launch_ms / ggrs_timing_read report device time of exactly that kernel.
+template <typename K>
+int launch_timed(ggrs_engine* e, K&& launch) {
+  hipEvent_t a = e->ev0, b = e->ev1;
+  if (e->collecting) {
+    while (e->tev.size() < e->tev_used + 2) {
+      hipEvent_t ev;
+      HIP_TRY(hipEventCreate(&ev));
+      e->tev.push_back(ev);
+    }
+    a = e->tev[e->tev_used];
+    b = e->tev[e->tev_used + 1];
+    e->tev_used += 2;
+  }
+  HIP_TRY(hipEventRecord(a, e->stream));
+  launch();
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(b, e->stream));
+  if (e->collecting) {  // keep last-launch queries valid too
+    e->ev_last0 = a;
+    e->ev_last1 = b;
+  } else {
+    e->ev_last0 = e->ev0;
+    e->ev_last1 = e->ev1;
+  }
+  e->timed = true;
+  return GGRS_OK;
+}
+
+int64_t grid_of(int64_t n, int64_t block) { return (n + block - 1) / block; }
+
+}  // namespace
+
+extern "C" {
+
+int32_t ggrs_abi_version(void) { return GGRS_ABI_VERSION; }
+
+const char* ggrs_last_error(void) { return g_last_error.c_str(); }
+
+int ggrs_engine_destroy(ggrs_engine_t* e) {
+  if (!e) return GGRS_OK;
+  (void)hipSetDevice(e->cfg.device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  void* bufs[] = {e->cur, e->ring, e->ring_ck, e->first_ck, e->inputs, e->lane_status,
+                  e->mis_frame, e->mis_mask, e->trace, e->staging};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  for (hipEvent_t ev : e->tev) (void)hipEventDestroy(ev);
+  if (e->ev0) (void)hipEventDestroy(e->ev0);
+  if (e->ev1) (void)hipEventDestroy(e->ev1);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+  return GGRS_OK;
+}
+
+int ggrs_engine_create(const ggrs_config_t* cfg, ggrs_engine_t** out) {
+  if (!cfg || !out) return set_error(GGRS_E_INVALID, "null argument");
+  *out = nullptr;
+  const ggrs_config_t c = *cfg;
+  if (c.num_lanes < 1) return set_error(GGRS_E_INVALID, "num_lanes must be >= 1");
+  if (c.num_players < 1 || c.num_players > 4)
+    return set_error(GGRS_E_INVALID, "num_players must be in 1..4 (ex_game.rs:70)");
+  if (c.max_prediction < 1 || c.max_prediction > 63)
+    return set_error(GGRS_E_INVALID, "max_prediction must be in 1..63");
+  if (c.check_distance < 0 || c.check_distance >= c.max_prediction)
+    return set_error(GGRS_E_INVALID, "Check distance too big. (check_distance must be < max_prediction)");
+  if (c.input_delay < 0 || c.input_delay > 1024) return set_error(GGRS_E_INVALID, "bad input_delay");
+  if (c.input_capacity < 0 || c.trace_capacity < 0) return set_error(GGRS_E_INVALID, "negative capacity");
+  ggrs_engine* e = new ggrs_engine();
+  e->cfg = c;
+  e->Pp = padded_players(c.num_players);
+  e->F = state_fields(c.num_players);
+  e->R = c.max_prediction + 1;
+  e->cap = c.input_capacity ? c.input_capacity : 128;
+  if (e->cap < c.input_delay + c.check_distance + 2) {
+    delete e;
+    return set_error(GGRS_E_INVALID, "input_capacity must be >= input_delay + check_distance + 2");
+  }
+  e->ring_tag.assign(e->R, GGRS_NULL_FRAME);
+  e->cfg.input_capacity = e->cap;
+  auto fail = [&](int rc) {
+    std::string msg = g_last_error;
+    ggrs_engine_destroy(e);
+    g_last_error = msg;
+    return rc;
+  };
+#define CTRY(expr)                                                                      \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) return fail(set_error(GGRS_E_HIP, "%s: %s", #expr, hipGetErrorString(e_))); \
+  } while (0)
+  const int64_t L = c.num_lanes;
+  CTRY(hipSetDevice(c.device));
+  CTRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+  CTRY(hipEventCreate(&e->ev0));
+  CTRY(hipEventCreate(&e->ev1));
+  CTRY(hipMalloc(&e->cur, sizeof(uint32_t) * e->F * L));
+  CTRY(hipMalloc(&e->ring, sizeof(uint32_t) * (size_t)e->R * e->F * L));
+  CTRY(hipMalloc(&e->ring_ck, sizeof(uint16_t) * (size_t)e->R * L));
+  CTRY(hipMalloc(&e->first_ck, sizeof(uint16_t) * (size_t)e->R * L));
+  CTRY(hipMalloc(&e->inputs, (size_t)e->cap * L * e->Pp));
+  CTRY(hipMalloc(&e->lane_status, sizeof(int32_t) * L));
+  CTRY(hipMalloc(&e->mis_frame, sizeof(int32_t) * L));
+  CTRY(hipMalloc(&e->mis_mask, sizeof(uint64_t) * L));
+  if (c.trace_capacity > 0) CTRY(hipMalloc(&e->trace, sizeof(uint16_t) * (size_t)c.trace_capacity * L));
+  CTRY(hipMemsetAsync(e->ring, 0, sizeof(uint32_t) * (size_t)e->R * e->F * L, e->stream));
+  CTRY(hipMemsetAsync(e->ring_ck, 0, sizeof(uint16_t) * (size_t)e->R * L, e->stream));
+  CTRY(hipMemsetAsync(e->first_ck, 0, sizeof(uint16_t) * (size_t)e->R * L, e->stream));
+  // default input (Input::default(), inp = 0) for every queue frame, covering frames < delay
+  CTRY(hipMemsetAsync(e->inputs, 0, (size_t)e->cap * L * e->Pp, e->stream));
+  CTRY(hipMemsetAsync(e->lane_status, 0, sizeof(int32_t) * L, e->stream));
+  CTRY(hipMemsetAsync(e->mis_frame, 0xff, sizeof(int32_t) * L, e->stream));
+  CTRY(hipMemsetAsync(e->mis_mask, 0, sizeof(uint64_t) * L, e->stream));
+  if (e->trace) CTRY(hipMemsetAsync(e->trace, 0, sizeof(uint16_t) * (size_t)c.trace_capacity * L, e->stream));
+  const int64_t grid = grid_of(L, 256);
+  switch (c.num_players) {
+    case 1: init_states_kernel<1><<<grid, 256, 0, e->stream>>>(e->cur, L); break;
+    case 2: init_states_kernel<2><<<grid, 256, 0, e->stream>>>(e->cur, L); break;
+    case 3: init_states_kernel<3><<<grid, 256, 0, e->stream>>>(e->cur, L); break;
+    default: init_states_kernel<4><<<grid, 256, 0, e->stream>>>(e->cur, L); break;
+  }
+  CTRY(hipGetLastError());
+  CTRY(hipStreamSynchronize(e->stream));
+#undef CTRY
+  *out = e;
+  return GGRS_OK;
+}
+
+int ggrs_engine_config(const ggrs_engine_t* e, ggrs_config_t* out) {
+  if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
+  *out = e->cfg;
+  return GGRS_OK;
+}
+
+static int add_inputs_common(ggrs_engine_t* e, int32_t first_frame, int32_t n, const void* src,
+                             bool device) {
+  if (!e || (!src && n > 0)) return set_error(GGRS_E_INVALID, "null argument");
+  if (n < 0) return set_error(GGRS_E_INVALID, "n_frames must be >= 0");
+  if (first_frame != e->next_user_frame)
+    return set_error(GGRS_E_INVALID,
+                     "inputs must be added sequentially (expected frame %d, got %d; input_queue.rs:171-177)",
+                     e->next_user_frame, first_frame);
+  if (n == 0) return GGRS_OK;
+  const int32_t delay = e->cfg.input_delay;
+  // oldest queue frame a later call still reads: the rollback start current - cd
+  const int64_t oldest_needed = (int64_t)e->current_frame - e->cfg.check_distance;
+  const int64_t newest = (int64_t)first_frame + n - 1 + delay;
+  if (newest - oldest_needed >= e->cap)
+    return set_error(GGRS_E_INVALID,
+                     "input queue full: frames up to %lld would overwrite frame %lld still needed (capacity %d)",
+                     (long long)newest, (long long)oldest_needed, e->cap);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const int64_t L = e->cfg.num_lanes;
+  const int P = e->cfg.num_players;
+  const size_t bytes = (size_t)n * L * P;
+  const uint8_t* dsrc = (const uint8_t*)src;
+  if (!device) {
+    int rc = ensure_staging(e, bytes);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(e->staging, src, bytes, hipMemcpyHostToDevice, e->stream));
+    dsrc = e->staging;
+  }
+  const int64_t total = (int64_t)n * L;
+  pack_inputs_kernel<<<grid_of(total, 256), 256, 0, e->stream>>>(dsrc, e->inputs, L, P, e->Pp, n,
+                                                                 (first_frame + delay) % e->cap, e->cap);
+  HIP_TRY(hipGetLastError());
+  if (!device) HIP_TRY(hipStreamSynchronize(e->stream));  // staging is reused by the next call
+  e->next_user_frame = first_frame + n;
+  return GGRS_OK;
+}
+
+int ggrs_add_local_inputs(ggrs_engine_t* e, int32_t first_frame, int32_t n, const uint8_t* inputs) {
+  return add_inputs_common(e, first_frame, n, inputs, false);
+}
+
+int ggrs_add_local_inputs_device(ggrs_engine_t* e, int32_t first_frame, int32_t n, const void* inputs) {
+  return add_inputs_common(e, first_frame, n, inputs, true);
+}
+
+int ggrs_synctest_advance_frames(ggrs_engine_t* e, int32_t n) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  if (n < 0) return set_error(GGRS_E_INVALID, "n_frames must be >= 0");
+  if (e->mode == 2) return set_error(GGRS_E_STATE, "engine already driven by ggrs_handle_requests");
+  if (n == 0) return GGRS_OK;
+  // every frame run needs its (delayed) input queued: SyncTestSession requires input for all
+  // players before advance_frame ("Missing local input", sync_test_session.rs:110-114)
+  const int64_t last_needed_user = (int64_t)e->current_frame + n - 1 - e->cfg.input_delay;
+  if (last_needed_user >= e->next_user_frame)
+    return set_error(GGRS_E_INVALID,
+                     "Missing local input while calling advance_frame(): frame %lld not added",
+                     (long long)last_needed_user);
+  e->mode = 1;
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  SyncTestParams p;
+  p.L = e->cfg.num_lanes;
+  p.R = e->R;
+  p.cd = e->cfg.check_distance;
+  p.f0 = e->current_frame;
+  p.n = n;
+  p.cap = e->cap;
+  p.trace_cap = e->cfg.trace_capacity;
+  p.corrupt_lane = e->corrupt_lane;
+  p.corrupt_frame = e->corrupt_frame;
+  p.cur = e->cur;
+  p.ring = e->ring;
+  p.ring_ck = e->ring_ck;
+  p.first_ck = e->first_ck;
+  p.inputs = e->inputs;
+  p.lane_status = e->lane_status;
+  p.mis_frame = e->mis_frame;
+  p.mis_mask = e->mis_mask;
+  p.trace = e->trace;
+  const int64_t grid = grid_of(p.L, kWave);
+  int rc = launch_timed(e, [&] {
+    switch (e->cfg.num_players) {
+      case 1: synctest_kernel<1><<<grid, kWave, 0, e->stream>>>(p); break;
+      case 2: synctest_kernel<2><<<grid, kWave, 0, e->stream>>>(p); break;
+      case 3: synctest_kernel<3><<<grid, kWave, 0, e->stream>>>(p); break;
+      default: synctest_kernel<4><<<grid, kWave, 0, e->stream>>>(p); break;
+    }
+  });
+  if (rc) return rc;
+  // lane-uniform bookkeeping: after call f the ring holds, in slot s, the newest frame <= f
+  // congruent to s (every frame 0..f has been saved; cd == 0 saves nothing)
+  e->current_frame += n;
+  if (e->cfg.check_distance > 0)
+    for (int s = 0; s < e->R; s++) {
+      int32_t last = e->current_frame - 1;
+      int32_t fr = last - (((last - s) % e->R) + e->R) % e->R;
+      e->ring_tag[s] = fr >= 0 ? fr : GGRS_NULL_FRAME;
+    }
+  return GGRS_OK;
+}
+
+int ggrs_handle_requests(ggrs_engine_t* e, const ggrs_request_t* reqs, int32_t n_reqs,
+                         const uint8_t* inputs, const uint8_t* status) {
+  if (!e || (!reqs && n_reqs > 0)) return set_error(GGRS_E_INVALID, "null argument");
+  if (e->mode == 1) return set_error(GGRS_E_STATE, "engine already driven by ggrs_synctest_advance_frames");
+  if (n_reqs <= 0) return GGRS_OK;
+  // validate the whole list against the lane-uniform cell bookkeeping before touching the device
+  std::vector<int32_t> tags = e->ring_tag;
+  int32_t frame = e->current_frame;
+  int32_t n_adv = 0;
+  for (int32_t r = 0; r < n_reqs; r++) {
+    const int32_t k = reqs[r].kind, f = reqs[r].frame;
+    if (k == GGRS_REQ_SAVE) {
+      if (f == GGRS_NULL_FRAME) return set_error(GGRS_E_PRECONDITION, "request %d: save of NULL_FRAME (sync_layer.rs:20)", r);
+      if (f != frame) return set_error(GGRS_E_PRECONDITION, "request %d: save frame %d != state frame %d (ex_game.rs:104)", r, f, frame);
+      tags[f % e->R] = f;
+    } else if (k == GGRS_REQ_LOAD) {
+      if (f < 0 || tags[f % e->R] != f)
+        return set_error(GGRS_E_PRECONDITION, "request %d: no saved state for frame %d (sync_layer.rs:248, ex_game.rs:112)", r, f);
+      frame = f;
+    } else if (k == GGRS_REQ_ADVANCE) {
+      frame += 1;
+      n_adv++;
+    } else {
+      return set_error(GGRS_E_INVALID, "request %d: unknown kind %d", r, k);
+    }
+  }
+  if (n_adv > 0 && !inputs) return set_error(GGRS_E_INVALID, "inputs required for AdvanceFrame requests");
+  if (e->trace && n_adv > e->cfg.trace_capacity) return set_error(GGRS_E_INVALID, "more advances than trace_capacity");
+  e->mode = 2;
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const int64_t L = e->cfg.num_lanes;
+  const int P = e->cfg.num_players, Pp = e->Pp;
+  const size_t req_bytes = sizeof(int32_t) * 2 * n_reqs;
+  const size_t in_bytes = (size_t)n_adv * L * Pp;
+  const size_t raw_bytes = (size_t)n_adv * L * P;
+  const size_t total = req_bytes + 2 * in_bytes + 2 * raw_bytes + 64;
+  int rc = ensure_staging(e, total);
+  if (rc) return rc;
+  uint8_t* d_reqs = e->staging;
+  uint8_t* d_in = d_reqs + ((req_bytes + 15) & ~(size_t)15);
+  uint8_t* d_st = d_in + in_bytes;
+  uint8_t* d_raw = d_st + in_bytes;
+  std::vector<int32_t> flat(2 * n_reqs);
+  for (int32_t r = 0; r < n_reqs; r++) {
+    flat[2 * r] = reqs[r].kind;
+    flat[2 * r + 1] = reqs[r].frame;
+  }
+  HIP_TRY(hipMemcpyAsync(d_reqs, flat.data(), req_bytes, hipMemcpyHostToDevice, e->stream));
+  if (n_adv > 0) {
+    HIP_TRY(hipMemcpyAsync(d_raw, inputs, raw_bytes, hipMemcpyHostToDevice, e->stream));
+    pack_inputs_kernel<<<grid_of((int64_t)n_adv * L, 256), 256, 0, e->stream>>>(d_raw, d_in, L, P, Pp, n_adv, 0, n_adv);
+    HIP_TRY(hipGetLastError());
+    if (status) {
+      HIP_TRY(hipMemcpyAsync(d_raw + raw_bytes, status, raw_bytes, hipMemcpyHostToDevice, e->stream));
+      pack_inputs_kernel<<<grid_of((int64_t)n_adv * L, 256), 256, 0, e->stream>>>(d_raw + raw_bytes, d_st, L, P, Pp, n_adv, 0, n_adv);
+      HIP_TRY(hipGetLastError());
+    }
+  }
+  RequestParams p;
+  p.L = L;
+  p.R = e->R;
+  p.n_reqs = n_reqs;
+  p.trace_cap = e->cfg.trace_capacity;
+  p.reqs = (const int32_t*)d_reqs;
+  p.inputs = d_in;
+  p.status = status ? d_st : nullptr;
+  p.cur = e->cur;
+  p.ring = e->ring;
+  p.ring_ck = e->ring_ck;
+  p.trace = e->trace;
+  const int64_t grid = grid_of(L, kWave);
+  rc = launch_timed(e, [&] {
+    switch (P) {
+      case 1: requests_kernel<1><<<grid, kWave, 0, e->stream>>>(p); break;
+      case 2: requests_kernel<2><<<grid, kWave, 0, e->stream>>>(p); break;
+      case 3: requests_kernel<3><<<grid, kWave, 0, e->stream>>>(p); break;
+      default: requests_kernel<4><<<grid, kWave, 0, e->stream>>>(p); break;
+    }
+  });
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(e->stream));  // staging reuse
+  e->ring_tag = tags;
+  e->current_frame = frame;
+  return GGRS_OK;
+}
+
+int ggrs_synchronize(ggrs_engine_t* e) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return GGRS_OK;
+}
+
+int ggrs_current_frame(const ggrs_engine_t* e, int32_t* out) {
+  if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
+  *out = e->current_frame;
+  return GGRS_OK;
+}
+
+int ggrs_read_mismatches(ggrs_engine_t* e, int32_t* st, int32_t* mf, uint64_t* mm) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const size_t L = e->cfg.num_lanes;
+  if (st) HIP_TRY(hipMemcpyAsync(st, e->lane_status, 4 * L, hipMemcpyDeviceToHost, e->stream));
+  if (mf) HIP_TRY(hipMemcpyAsync(mf, e->mis_frame, 4 * L, hipMemcpyDeviceToHost, e->stream));
+  if (mm) HIP_TRY(hipMemcpyAsync(mm, e->mis_mask, 8 * L, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return GGRS_OK;
+}
+
+int ggrs_read_save_checksums(ggrs_engine_t* e, int32_t frame, uint16_t* out) {
+  if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
+  if (frame < 0 || e->ring_tag[frame % e->R] != frame)
+    return set_error(GGRS_E_PRECONDITION, "no saved cell for frame %d", frame);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const size_t L = e->cfg.num_lanes;
+  HIP_TRY(hipMemcpyAsync(out, e->ring_ck + (size_t)(frame % e->R) * L, 2 * L, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return GGRS_OK;
+}
+
+static void serialize_state(const uint32_t* w, int P, uint8_t* out) {
+  // bincode: i32 frame, u64 P, u64 P + (x,y)*P, u64 P + (vx,vy)*P, u64 P + rot*P
+  uint8_t* o = out;
+  auto u32 = [&](uint32_t v) { memcpy(o, &v, 4); o += 4; };
+  auto u64 = [&](uint64_t v) { memcpy(o, &v, 8); o += 8; };
+  u32(w[0]);
+  u64((uint64_t)P);
+  u64((uint64_t)P);
+  for (int k = 1; k <= 2 * P; k++) u32(w[k]);
+  u64((uint64_t)P);
+  for (int k = 2 * P + 1; k <= 4 * P; k++) u32(w[k]);
+  u64((uint64_t)P);
+  for (int k = 4 * P + 1; k <= 5 * P; k++) u32(w[k]);
+}
+
+static int gather_lane(ggrs_engine_t* e, const uint32_t* base, int32_t lane, uint32_t* w) {
+  const size_t L = e->cfg.num_lanes;
+  for (int k = 0; k < e->F; k++)
+    HIP_TRY(hipMemcpyAsync(&w[k], base + (size_t)k * L + lane, 4, hipMemcpyDeviceToHost, e->stream));
+  return GGRS_OK;
+}
+
+int ggrs_read_state(ggrs_engine_t* e, int32_t lane, uint8_t* out) {
+  if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
+  if (lane < 0 || lane >= e->cfg.num_lanes) return set_error(GGRS_E_INVALID, "lane out of range");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  uint32_t w[32];
+  int rc = gather_lane(e, e->cur, lane, w);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  serialize_state(w, e->cfg.num_players, out);
+  return GGRS_OK;
+}
+
+int ggrs_read_ring(ggrs_engine_t* e, int32_t lane, int32_t* frames, uint16_t* cks, uint8_t* states) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  if (lane < 0 || lane >= e->cfg.num_lanes) return set_error(GGRS_E_INVALID, "lane out of range");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const size_t L = e->cfg.num_lanes;
+  const int sb = bincode_bytes(e->cfg.num_players);
+  std::vector<uint32_t> w((size_t)e->R * e->F);
+  std::vector<uint16_t> c(e->R);
+  for (int s = 0; s < e->R; s++) {
+    int rc = gather_lane(e, e->ring + (size_t)s * e->F * L, lane, &w[(size_t)s * e->F]);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(&c[s], e->ring_ck + (size_t)s * L + lane, 2, hipMemcpyDeviceToHost, e->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  for (int s = 0; s < e->R; s++) {
+    const bool has = e->ring_tag[s] != GGRS_NULL_FRAME;
+    if (frames) frames[s] = e->ring_tag[s];
+    if (cks) cks[s] = has ? c[s] : 0;
+    if (states) {
+      if (has) serialize_state(&w[(size_t)s * e->F], e->cfg.num_players, states + (size_t)s * sb);
+      else memset(states + (size_t)s * sb, 0, sb);
+    }
+  }
+  return GGRS_OK;
+}
+
+int ggrs_read_trace(ggrs_engine_t* e, int32_t first_frame, int32_t n, uint16_t* out) {
+  if (!e || (!out && n > 0)) return set_error(GGRS_E_INVALID, "null argument");
+  if (!e->trace) return set_error(GGRS_E_STATE, "engine created with trace_capacity = 0");
+  const int32_t T = e->cfg.trace_capacity;
+  if (n < 0 || first_frame < 0 || first_frame + n > e->current_frame || first_frame < e->current_frame - T)
+    return set_error(GGRS_E_INVALID, "trace frames [%d, %d) not held (current %d, capacity %d)", first_frame,
+                     first_frame + n, e->current_frame, T);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const size_t L = e->cfg.num_lanes;
+  for (int32_t i = 0; i < n; i++)
+    HIP_TRY(hipMemcpyAsync(out + (size_t)i * L, e->trace + (size_t)((first_frame + i) % T) * L, 2 * L,
+                           hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return GGRS_OK;
+}
+
+int ggrs_debug_corrupt_on_load(ggrs_engine_t* e, int32_t lane, int32_t frame) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  e->corrupt_lane = lane;
+  e->corrupt_frame = frame;
+  return GGRS_OK;
+}
+
+int ggrs_last_launch_ms(ggrs_engine_t* e, float* ms) {
+  if (!e || !ms) return set_error(GGRS_E_INVALID, "null argument");
+  if (!e->timed) return set_error(GGRS_E_STATE, "no fused launch yet");
+  HIP_TRY(hipEventSynchronize(e->ev_last1));
+  HIP_TRY(hipEventElapsedTime(ms, e->ev_last0, e->ev_last1));
+  return GGRS_OK;
+}
+
+int ggrs_timing_reset(ggrs_engine_t* e) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  e->tev_used = 0;
+  e->collecting = true;
+  return GGRS_OK;
+}
+
+int ggrs_timing_read(ggrs_engine_t* e, float* total_ms, int32_t* launches) {
+  if (!e || !total_ms || !launches) return set_error(GGRS_E_INVALID, "null argument");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  float sum = 0.0f;
+  for (size_t i = 0; i + 1 < e->tev_used; i += 2) {
+    float ms = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&ms, e->tev[i], e->tev[i + 1]));
+    sum += ms;
+  }
+  *total_ms = sum;
+  *launches = (int32_t)(e->tev_used / 2);
+  e->collecting = false;
+  e->tev_used = 0;
+  return GGRS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,151 @@
+/*
+ * ggrs_amd.h -- C ABI of the MI355X batched rollback-resimulation engine.
+ *
+ * One engine owns L lanes.  A lane is one (session, branch): its own ex_game State, its own
+ * saved-state ring and its own input stream.  All lanes of an engine execute the same request
+ * program (the request kinds and frames a GGRS session emits are identical for sessions in
+ * lockstep; only inputs differ), so every call below acts on all lanes at once.
+ *
+ * Replaces (caspark/ggrs 0.10.2, file:line):
+ *   ggrs_engine_create         SessionBuilder::start_synctest_session (src/sessions/builder.rs:346-358)
+ *                              + SyncLayer::new / SavedStates::new (src/sync_layer.rs:149-159,183-198)
+ *                              + Game::new / State::new (examples/ex_game/ex_game.rs:67-76,246-269)
+ *   ggrs_add_local_inputs      SyncTestSession::add_local_input (src/sessions/sync_test_session.rs:61-74)
+ *                              feeding InputQueue::add_input (src/input_queue.rs:170-186) with the
+ *                              session's input delay (src/input_queue.rs:233-265)
+ *   ggrs_synctest_advance_frames
+ *                              n x { SyncTestSession::advance_frame (sync_test_session.rs:85-150)
+ *                              incl. checksums_consistent (:173-190) and adjust_gamestate (:192-217),
+ *                              then Game::handle_requests (ex_game.rs:79-99) }
+ *   ggrs_handle_requests       Game::handle_requests (ex_game.rs:79-99) for an ordered
+ *                              Vec<GgrsRequest> (src/lib.rs:171-195): SaveGameState -> save_game_state
+ *                              (ex_game.rs:103-108), LoadGameState -> load_game_state (:111-113),
+ *                              AdvanceFrame -> advance_frame (:115-127)
+ *   ggrs_read_save_checksums   the `Some(checksum)` a handler passes to GameStateCell::save
+ *                              (sync_layer.rs:18-24), so a GGRS session can keep `data = None`
+ *                              cells while the states live in HBM
+ *   ggrs_read_mismatches       GgrsError::MismatchedChecksum { current_frame, mismatched_frames }
+ *                              (src/error.rs:44-50), per lane
+ *
+ * Errors: every function returns GGRS_OK (0) or a negative GGRS_E_* code; ggrs_last_error() gives
+ * the message.  The reference panics (assert!) on precondition violations (sync_layer.rs:20,
+ * 231-248; ex_game.rs:104); this ABI never unwinds and reports them as GGRS_E_PRECONDITION
+ * without touching device state.  A checksum mismatch is data, not an error code.
+ *
+ * Threading: an engine is used by one host thread at a time; work is enqueued on the engine's
+ * own HIP stream and the read functions synchronise with it.  No torch types cross this ABI.
+ */
+#ifndef GGRS_AMD_H
+#define GGRS_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GGRS_ABI_VERSION 1
+
+#define GGRS_OK 0
+#define GGRS_E_INVALID (-1)      /* GgrsError::InvalidRequest: bad argument or configuration */
+#define GGRS_E_PRECONDITION (-2) /* a reference assert! would have panicked */
+#define GGRS_E_HIP (-3)          /* HIP runtime error (message from hipGetErrorString) */
+#define GGRS_E_STATE (-4)        /* call not valid in the engine's current mode */
+
+#define GGRS_NULL_FRAME (-1) /* src/lib.rs:47 */
+
+/* GgrsRequest kinds (src/lib.rs:171-195) */
+#define GGRS_REQ_SAVE 0
+#define GGRS_REQ_LOAD 1
+#define GGRS_REQ_ADVANCE 2
+
+/* InputStatus (src/lib.rs:106-113) as carried per player in the status bytes of an advance */
+#define GGRS_STATUS_CONFIRMED 0
+#define GGRS_STATUS_PREDICTED 1
+#define GGRS_STATUS_DISCONNECTED 2
+
+/* per-lane status */
+#define GGRS_LANE_RUNNING 0
+#define GGRS_LANE_MISMATCH 1 /* halted: SyncTestSession::advance_frame returned MismatchedChecksum */
+
+typedef struct ggrs_config {
+  int32_t num_lanes;      /* L >= 1: independent (session, branch) lanes */
+  int32_t num_players;    /* 1..4 (ex_game.rs:70) */
+  int32_t max_prediction; /* ring holds max_prediction + 1 saved states (sync_layer.rs:149-159) */
+  int32_t check_distance; /* SyncTest check distance; must be < max_prediction (builder.rs:347) */
+  int32_t input_delay;    /* local input delay in frames (builder.rs:154-158) */
+  int32_t input_capacity; /* frames of queued input per lane; 0 = 128 (INPUT_QUEUE_LENGTH) */
+  int32_t device;         /* HIP device ordinal */
+  int32_t trace_capacity; /* frames of per-frame checksum trace kept on device; 0 = none */
+} ggrs_config_t;
+
+typedef struct ggrs_engine ggrs_engine_t;
+
+typedef struct ggrs_request {
+  int32_t kind;  /* GGRS_REQ_* */
+  int32_t frame; /* Save/Load: the request's frame; Advance: ignored */
+} ggrs_request_t;
+
+int32_t ggrs_abi_version(void);
+const char* ggrs_last_error(void);
+
+int ggrs_engine_create(const ggrs_config_t* cfg, ggrs_engine_t** out);
+int ggrs_engine_destroy(ggrs_engine_t* eng);
+int ggrs_engine_config(const ggrs_engine_t* eng, ggrs_config_t* out);
+
+/* Queue user inputs for frames [first_frame, first_frame + n_frames) of every lane.
+ * inputs: [n_frames][num_lanes][num_players] bytes (Input.inp).  Frames must be added in order
+ * starting at 0 (input_queue.rs:171-177); they enter the queue at frame + input_delay, frames
+ * below the delay hold the default input (input_queue.rs:251-257).  `_device` takes a device
+ * pointer (same layout) readable on the engine's stream. */
+int ggrs_add_local_inputs(ggrs_engine_t* eng, int32_t first_frame, int32_t n_frames,
+                          const uint8_t* inputs);
+int ggrs_add_local_inputs_device(ggrs_engine_t* eng, int32_t first_frame, int32_t n_frames,
+                                 const void* inputs_device);
+
+/* Run n_frames SyncTest frames on every running lane (fused: one kernel launch). */
+int ggrs_synctest_advance_frames(ggrs_engine_t* eng, int32_t n_frames);
+
+/* Execute an ordered request list on every lane (fused: one kernel launch).
+ * inputs: [n_advance][num_lanes][num_players] Input.inp bytes, status: same shape InputStatus
+ * bytes (NULL = all confirmed), one slice per AdvanceFrame in order.  Save checksums are kept on
+ * device; read them with ggrs_read_save_checksums. */
+int ggrs_handle_requests(ggrs_engine_t* eng, const ggrs_request_t* reqs, int32_t n_reqs,
+                         const uint8_t* inputs, const uint8_t* status);
+
+/* Block until all work queued on the engine's stream has finished. */
+int ggrs_synchronize(ggrs_engine_t* eng);
+/* Frame the engine's session is at (SyncTestSession::current_frame, sync_test_session.rs:153). */
+int ggrs_current_frame(const ggrs_engine_t* eng, int32_t* out);
+/* Per-lane status / mismatch: each array has num_lanes entries (any may be NULL).  mask bit k
+ * set <=> frame (mismatch_frame - check_distance + k) mismatched. */
+int ggrs_read_mismatches(ggrs_engine_t* eng, int32_t* lane_status, int32_t* mismatch_frame,
+                         uint64_t* mismatch_mask);
+/* Checksum stored with the saved cell of `frame` for every lane (num_lanes u16). */
+int ggrs_read_save_checksums(ggrs_engine_t* eng, int32_t frame, uint16_t* out);
+/* Current game state of one lane as bincode bytes (36 + 20 * num_players). */
+int ggrs_read_state(ggrs_engine_t* eng, int32_t lane, uint8_t* out);
+/* Saved-state ring of one lane: frames[R], checksums[R], states[R][36 + 20 * num_players]. */
+int ggrs_read_ring(ggrs_engine_t* eng, int32_t lane, int32_t* frames, uint16_t* checksums,
+                   uint8_t* states);
+/* Per-frame display checksum trace (fletcher16 of the state after each frame's final
+ * AdvanceFrame, ex_game.rs:121-126) for frames [first_frame, first_frame + n_frames):
+ * out[n_frames][num_lanes].  Requires trace_capacity > 0 and frames still held. */
+int ggrs_read_trace(ggrs_engine_t* eng, int32_t first_frame, int32_t n_frames, uint16_t* out);
+
+/* Fault injection (tests): after the LoadGameState of SyncTest call `frame`, flip the lowest
+ * bit of player 0's x on `lane` -- a non-deterministic simulation the SyncTest must catch. */
+int ggrs_debug_corrupt_on_load(ggrs_engine_t* eng, int32_t lane, int32_t frame);
+
+/* Timing of the last fused launch on the engine's stream, from HIP events around it (ms). */
+int ggrs_last_launch_ms(ggrs_engine_t* eng, float* ms);
+/* Collect HIP-event device times of every fused launch from now on; _read synchronises, returns
+ * the summed milliseconds and the launch count, and stops collecting. */
+int ggrs_timing_reset(ggrs_engine_t* eng);
+int ggrs_timing_read(ggrs_engine_t* eng, float* total_ms, int32_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GGRS_AMD_H */

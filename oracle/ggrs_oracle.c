@@ -1,0 +1,819 @@
+/*
+ * ggrs_oracle.c -- CPU restatement of the GGRS rollback hot path.  TEST INFRASTRUCTURE ONLY.
+ *
+ * This file is the parity oracle and the CPU baseline.  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it (as oracle/_build/libggrs_oracle.so); the product path
+ * (ggrs_amd/) never links, calls or falls back to it.
+ *
+ * The reference (caspark/ggrs 0.10.2, Rust) cannot be compiled in this image (no Rust toolchain,
+ * SURVEY.md finding 1), so this is a line-by-line restatement in C of:
+ *   examples/ex_game/ex_game.rs      State (236-243), State::new (246-269), State::advance
+ *                                    (271-333), fletcher16 (45-55), bincode layout of State
+ *                                    (serde derive, bincode 1.x fixint LE), Game::handle_requests
+ *                                    / save / load / advance (79-127)
+ *   src/input_queue.rs               InputQueue (10-266)
+ *   src/sync_layer.rs                GameStateCell (14-89), SavedStates (144-166), SyncLayer
+ *                                    (168-375)
+ *   src/sessions/sync_test_session.rs SyncTestSession::add_local_input (61-74), advance_frame
+ *                                    (85-150), checksums_consistent (173-190), adjust_gamestate
+ *                                    (192-217)
+ *   src/sessions/builder.rs          defaults (13-27), start_synctest_session check (346-358)
+ *   src/lib.rs                       NULL_FRAME (47), InputStatus (106-113), PredictRepeatLast
+ *                                    (390-395), PredictDefault (402-406)
+ * Floating point: compiled with -O2 -ffp-contract=off (Rust never contracts) and linked against
+ * this image's glibc 2.35 libm, whose sinf/cosf/fmodf are what Rust's f32::sin/cos/% call.
+ *
+ * Parity pinning: the reference holds no numeric golden vectors.  This
+ * restatement is pinned by (a) the reference's own structural tests restated in
+ * tests/test_oracle.py (request counts 1/2/6/16 and order, frame advance, random checksums ->
+ * MismatchedChecksum, input-delay semantics) and (b) an independent pure-Python restatement
+ * (oracle/pyoracle.py) that generated the committed fixtures in tests/golden/.
+ */
+#include <math.h>
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#define NULL_FRAME (-1)                  /* src/lib.rs:47 */
+#define INPUT_QUEUE_LENGTH 128           /* src/input_queue.rs:6 */
+#define MAX_PLAYERS 4                    /* ex_game.rs:70 asserts num_players <= 4 */
+
+enum { STATUS_CONFIRMED = 0, STATUS_PREDICTED = 1, STATUS_DISCONNECTED = 2 }; /* lib.rs:106-113 */
+enum { REQ_SAVE = 0, REQ_LOAD = 1, REQ_ADVANCE = 2 };                         /* lib.rs:171-195 */
+enum { PREDICT_REPEAT_LAST = 0, PREDICT_DEFAULT = 1 };                        /* lib.rs:390-406 */
+
+/* ---------------------------------------------------------------- ex_game constants (10-26) */
+#define WINDOW_HEIGHT 800.0f
+#define WINDOW_WIDTH 600.0f
+#define INPUT_UP (1u << 0)
+#define INPUT_DOWN (1u << 1)
+#define INPUT_LEFT (1u << 2)
+#define INPUT_RIGHT (1u << 3)
+static float movement_speed(void) { volatile float a = 15.0f, b = 60.0f; return a / b; } /* 15.0 / FPS as f32 */
+static float rotation_speed(void) { volatile float a = 2.5f, b = 60.0f; return a / b; }  /* 2.5 / FPS as f32 */
+#define MAX_SPEED 7.0f
+#define FRICTION 0.98f
+#define PI_F32 3.14159265358979323846264338327950288f /* std::f32::consts::PI */
+
+/* ---------------------------------------------------------------- State (ex_game.rs:236-243)
+ * Rust holds three Vecs on the heap; the restatement keeps them heap-allocated too so that the
+ * CPU baseline pays the same clone/alloc pattern per save and load (ex_game.rs:107,112). */
+typedef struct {
+  int32_t frame;
+  uint64_t num_players;
+  float* positions;  /* Vec<(f32, f32)>, 2*P */
+  float* velocities; /* Vec<(f32, f32)>, 2*P */
+  float* rotations;  /* Vec<f32>, P */
+} State;
+
+static void state_alloc(State* s, uint64_t p) {
+  s->num_players = p;
+  s->positions = (float*)malloc(sizeof(float) * 2 * p);
+  s->velocities = (float*)malloc(sizeof(float) * 2 * p);
+  s->rotations = (float*)malloc(sizeof(float) * p);
+}
+static void state_free(State* s) {
+  free(s->positions); free(s->velocities); free(s->rotations);
+  s->positions = s->velocities = s->rotations = NULL;
+}
+static void state_clone(State* dst, const State* src) { /* #[derive(Clone)] */
+  state_alloc(dst, src->num_players);
+  dst->frame = src->frame;
+  memcpy(dst->positions, src->positions, sizeof(float) * 2 * src->num_players);
+  memcpy(dst->velocities, src->velocities, sizeof(float) * 2 * src->num_players);
+  memcpy(dst->rotations, src->rotations, sizeof(float) * src->num_players);
+}
+
+/* State::new (ex_game.rs:246-269) */
+static void state_new(State* s, uint64_t num_players) {
+  state_alloc(s, num_players);
+  s->frame = 0;
+  const float r = WINDOW_WIDTH / 4.0f;
+  for (int32_t i = 0; i < (int32_t)num_players; i++) {
+    float rot = (float)i / (float)num_players * 2.0f * PI_F32; /* left to right, all f32 */
+    float x = WINDOW_WIDTH / 2.0f + r * cosf(rot);
+    float y = WINDOW_HEIGHT / 2.0f + r * sinf(rot);
+    s->positions[2 * i] = x;
+    s->positions[2 * i + 1] = y;
+    s->velocities[2 * i] = 0.0f;
+    s->velocities[2 * i + 1] = 0.0f;
+    s->rotations[i] = fmodf(rot + PI_F32, 2.0f * PI_F32); /* `%` on f32 is fmodf; not rem_euclid */
+  }
+}
+
+/* f32::rem_euclid (Rust std): r = self % rhs; if r < 0 { r + rhs.abs() } else { r } */
+static float rem_euclid_f32(float a, float b) {
+  float r = fmodf(a, b);
+  return r < 0.0f ? r + fabsf(b) : r;
+}
+
+/* State::advance (ex_game.rs:271-333).  inputs[i] = Input.inp, status[i] = InputStatus */
+static void state_advance(State* s, const uint8_t* inputs, const uint8_t* status) {
+  const float MS = movement_speed(), RS = rotation_speed();
+  s->frame += 1;
+  for (uint64_t i = 0; i < s->num_players; i++) {
+    uint8_t input = status[i] == STATUS_DISCONNECTED ? 4 : inputs[i]; /* disconnected spin */
+    float old_x = s->positions[2 * i], old_y = s->positions[2 * i + 1];
+    float old_vel_x = s->velocities[2 * i], old_vel_y = s->velocities[2 * i + 1];
+    float rot = s->rotations[i];
+    float vel_x = old_vel_x * FRICTION;
+    float vel_y = old_vel_y * FRICTION;
+    /* Rust: `input & INPUT_UP != 0` parses as `(input & INPUT_UP) != 0` */
+    if ((input & INPUT_UP) != 0 && (input & INPUT_DOWN) == 0) {
+      vel_x += MS * cosf(rot);
+      vel_y += MS * sinf(rot);
+    }
+    if ((input & INPUT_UP) == 0 && (input & INPUT_DOWN) != 0) {
+      vel_x -= MS * cosf(rot);
+      vel_y -= MS * sinf(rot);
+    }
+    if ((input & INPUT_LEFT) != 0 && (input & INPUT_RIGHT) == 0)
+      rot = rem_euclid_f32(rot - RS, 2.0f * PI_F32);
+    if ((input & INPUT_LEFT) == 0 && (input & INPUT_RIGHT) != 0)
+      rot = rem_euclid_f32(rot + RS, 2.0f * PI_F32);
+    float magnitude = sqrtf(vel_x * vel_x + vel_y * vel_y);
+    if (magnitude > MAX_SPEED) {
+      vel_x = (vel_x * MAX_SPEED) / magnitude;
+      vel_y = (vel_y * MAX_SPEED) / magnitude;
+    }
+    float x = old_x + vel_x;
+    float y = old_y + vel_y;
+    x = fmaxf(x, 0.0f); /* f32::max / f32::min are IEEE maxNum / minNum = fmaxf / fminf */
+    x = fminf(x, WINDOW_WIDTH);
+    y = fmaxf(y, 0.0f);
+    y = fminf(y, WINDOW_HEIGHT);
+    s->positions[2 * i] = x;
+    s->positions[2 * i + 1] = y;
+    s->velocities[2 * i] = vel_x;
+    s->velocities[2 * i + 1] = vel_y;
+    s->rotations[i] = rot;
+  }
+}
+
+/* bincode 1.x (DefaultOptions for serialize(): fixint, little endian) of #[derive(Serialize)]
+ * State: i32, u64 (usize), then each Vec as u64 length + elements.  36 + 20*P bytes. */
+static size_t put_u32(uint8_t* b, uint32_t v) { for (int k = 0; k < 4; k++) b[k] = (uint8_t)(v >> (8 * k)); return 4; }
+static size_t put_u64(uint8_t* b, uint64_t v) { for (int k = 0; k < 8; k++) b[k] = (uint8_t)(v >> (8 * k)); return 8; }
+static size_t put_f32(uint8_t* b, float f) { uint32_t u; memcpy(&u, &f, 4); return put_u32(b, u); }
+
+size_t oracle_state_serialize(const State* s, uint8_t* out) {
+  size_t o = 0;
+  uint64_t p = s->num_players;
+  o += put_u32(out + o, (uint32_t)s->frame);
+  o += put_u64(out + o, p);
+  o += put_u64(out + o, p);
+  for (uint64_t i = 0; i < 2 * p; i++) o += put_f32(out + o, s->positions[i]);
+  o += put_u64(out + o, p);
+  for (uint64_t i = 0; i < 2 * p; i++) o += put_f32(out + o, s->velocities[i]);
+  o += put_u64(out + o, p);
+  for (uint64_t i = 0; i < p; i++) o += put_f32(out + o, s->rotations[i]);
+  return o;
+}
+
+/* fletcher16 (ex_game.rs:45-55), byte loop exactly as the reference */
+uint16_t oracle_fletcher16(const uint8_t* data, size_t n) {
+  uint16_t sum1 = 0, sum2 = 0;
+  for (size_t i = 0; i < n; i++) {
+    sum1 = (uint16_t)((sum1 + data[i]) % 255);
+    sum2 = (uint16_t)((sum2 + sum1) % 255);
+  }
+  return (uint16_t)((sum2 << 8) | sum1);
+}
+
+/* bincode::serialize(&state) + fletcher16 (ex_game.rs:105-106); Rust allocates the buffer */
+static uint16_t state_checksum(const State* s) {
+  uint8_t* buf = (uint8_t*)malloc(36 + 20 * s->num_players);
+  size_t n = oracle_state_serialize(s, buf);
+  uint16_t c = oracle_fletcher16(buf, n);
+  free(buf);
+  return c;
+}
+
+/* ---------------------------------------------------------------- PlayerInput (frame_info.rs:28-53) */
+typedef struct { int32_t frame; uint8_t input; } PlayerInput;
+
+/* ---------------------------------------------------------------- InputQueue (input_queue.rs:10-266) */
+typedef struct {
+  size_t head, tail, length;
+  int first_frame;
+  int32_t last_added_frame, first_incorrect_frame, last_requested_frame;
+  size_t frame_delay;
+  PlayerInput inputs[INPUT_QUEUE_LENGTH];
+  PlayerInput prediction;
+  int predictor;
+} InputQueue;
+
+#define ORACLE_ASSERT(c, msg)                                                              \
+  do {                                                                                     \
+    if (!(c)) { fprintf(stderr, "oracle panic (%s:%d): %s\n", __FILE__, __LINE__, msg); abort(); } \
+  } while (0)
+
+static void iq_new(InputQueue* q, int predictor) { /* :40-53 */
+  q->head = q->tail = q->length = 0;
+  q->frame_delay = 0;
+  q->first_frame = 1;
+  q->last_added_frame = q->first_incorrect_frame = q->last_requested_frame = NULL_FRAME;
+  q->prediction.frame = NULL_FRAME; q->prediction.input = 0;
+  for (int i = 0; i < INPUT_QUEUE_LENGTH; i++) { q->inputs[i].frame = NULL_FRAME; q->inputs[i].input = 0; }
+  q->predictor = predictor;
+}
+static void iq_reset_prediction(InputQueue* q) { /* :63-67 */
+  q->prediction.frame = NULL_FRAME;
+  q->first_incorrect_frame = NULL_FRAME;
+  q->last_requested_frame = NULL_FRAME;
+}
+__attribute__((unused)) static PlayerInput iq_confirmed_input(const InputQueue* q, int32_t requested_frame) { /* :71-80 */
+  size_t offset = (size_t)requested_frame % INPUT_QUEUE_LENGTH;
+  ORACLE_ASSERT(q->inputs[offset].frame == requested_frame, "no confirmed input for the requested frame");
+  return q->inputs[offset];
+}
+static void iq_discard_confirmed_frames(InputQueue* q, int32_t frame) { /* :83-101 */
+  if (q->last_requested_frame != NULL_FRAME && q->last_requested_frame < frame) frame = q->last_requested_frame;
+  if (frame >= q->last_added_frame) {
+    q->tail = q->head;
+    q->length = 1;
+  } else if (frame <= q->inputs[q->tail].frame) {
+  } else {
+    size_t offset = (size_t)(frame - q->inputs[q->tail].frame);
+    q->tail = (q->tail + offset) % INPUT_QUEUE_LENGTH;
+    q->length -= offset;
+  }
+}
+static uint8_t predict(int predictor, uint8_t previous) { /* lib.rs:390-406 */
+  return predictor == PREDICT_DEFAULT ? 0 : previous;
+}
+/* input() (:104-167): returns input, sets *status */
+static uint8_t iq_input(InputQueue* q, int32_t requested_frame, uint8_t* status) {
+  ORACLE_ASSERT(q->first_incorrect_frame == NULL_FRAME, "input requested with a known misprediction");
+  q->last_requested_frame = requested_frame;
+  ORACLE_ASSERT(requested_frame >= q->inputs[q->tail].frame, "requested frame no longer exists");
+  if (q->prediction.frame < 0) {
+    size_t offset = (size_t)(requested_frame - q->inputs[q->tail].frame);
+    if (offset < q->length) {
+      offset = (offset + q->tail) % INPUT_QUEUE_LENGTH;
+      ORACLE_ASSERT(q->inputs[offset].frame == requested_frame, "queue frame mismatch");
+      *status = STATUS_CONFIRMED;
+      return q->inputs[offset].input;
+    }
+    const PlayerInput* prev = NULL;
+    if (!(requested_frame == 0 || q->last_added_frame == NULL_FRAME)) {
+      size_t pp = q->head == 0 ? INPUT_QUEUE_LENGTH - 1 : q->head - 1;
+      prev = &q->inputs[pp];
+    }
+    uint8_t pred = prev ? predict(q->predictor, prev->input) : 0; /* unwrap_or_default */
+    int32_t frame_num = prev ? prev->frame : q->prediction.frame;
+    q->prediction.frame = frame_num;
+    q->prediction.input = pred;
+    q->prediction.frame += 1;
+  }
+  ORACLE_ASSERT(q->prediction.frame != NULL_FRAME, "prediction frame is null");
+  *status = STATUS_PREDICTED;
+  return q->prediction.input;
+}
+static void iq_add_input_by_frame(InputQueue* q, PlayerInput input, int32_t frame_number) { /* :190-230 */
+  size_t pp = q->head == 0 ? INPUT_QUEUE_LENGTH - 1 : q->head - 1;
+  ORACLE_ASSERT(q->last_added_frame == NULL_FRAME || frame_number == q->last_added_frame + 1, "non-sequential add");
+  ORACLE_ASSERT(frame_number == 0 || q->inputs[pp].frame == frame_number - 1, "queue gap");
+  int prediction_matches_input = q->prediction.input == input.input; /* equal(_, input_only=true) */
+  q->inputs[q->head] = input;
+  q->inputs[q->head].frame = frame_number;
+  q->head = (q->head + 1) % INPUT_QUEUE_LENGTH;
+  q->length += 1;
+  ORACLE_ASSERT(q->length <= INPUT_QUEUE_LENGTH, "input queue overflow");
+  q->first_frame = 0;
+  q->last_added_frame = frame_number;
+  if (q->prediction.frame != NULL_FRAME) {
+    ORACLE_ASSERT(frame_number == q->prediction.frame, "prediction frame mismatch");
+    if (q->first_incorrect_frame == NULL_FRAME && !prediction_matches_input) q->first_incorrect_frame = frame_number;
+    if (q->prediction.frame == q->last_requested_frame && q->first_incorrect_frame == NULL_FRAME)
+      q->prediction.frame = NULL_FRAME;
+    else
+      q->prediction.frame += 1;
+  }
+}
+static int32_t iq_advance_queue_head(InputQueue* q, int32_t input_frame) { /* :233-265 */
+  size_t pp = q->head == 0 ? INPUT_QUEUE_LENGTH - 1 : q->head - 1;
+  int32_t expected_frame = q->first_frame ? 0 : q->inputs[pp].frame + 1;
+  input_frame += (int32_t)q->frame_delay;
+  if (expected_frame > input_frame) return NULL_FRAME;
+  while (expected_frame < input_frame) {
+    PlayerInput rep = q->inputs[pp];
+    iq_add_input_by_frame(q, rep, expected_frame);
+    expected_frame += 1;
+  }
+  pp = q->head == 0 ? INPUT_QUEUE_LENGTH - 1 : q->head - 1;
+  ORACLE_ASSERT(input_frame == 0 || input_frame == q->inputs[pp].frame + 1, "queue head mismatch");
+  return input_frame;
+}
+static int32_t iq_add_input(InputQueue* q, PlayerInput input) { /* :170-186 */
+  if (q->last_added_frame != NULL_FRAME && input.frame + (int32_t)q->frame_delay != q->last_added_frame + 1)
+    return NULL_FRAME;
+  int32_t new_frame = iq_advance_queue_head(q, input.frame);
+  if (new_frame != NULL_FRAME) iq_add_input_by_frame(q, input, new_frame);
+  return new_frame;
+}
+
+/* ---------------------------------------------------------------- GameStateCell / SavedStates */
+typedef struct {
+  int32_t frame;       /* GameState.frame (frame_info.rs:6-23), NULL_FRAME by default */
+  int has_data;
+  State data;
+  int has_checksum;
+  uint16_t checksum;   /* Option<u128> holding a fletcher16 */
+} Cell;
+
+static void cell_save(Cell* c, int32_t frame, const State* data, int has_cs, uint16_t cs) { /* sync_layer.rs:18-24 */
+  ORACLE_ASSERT(frame != NULL_FRAME, "save of NULL_FRAME");
+  c->frame = frame;
+  if (c->has_data) state_free(&c->data);
+  c->has_data = data != NULL;
+  if (data) c->data = *data; /* ownership moves in */
+  c->has_checksum = has_cs;
+  c->checksum = cs;
+}
+
+/* ---------------------------------------------------------------- SyncLayer (sync_layer.rs:168-375) */
+typedef struct {
+  size_t num_players, max_prediction;
+  size_t num_cells;
+  Cell* cells;
+  int32_t last_confirmed_frame, last_saved_frame, current_frame;
+  InputQueue queues[MAX_PLAYERS];
+} SyncLayer;
+
+static void sl_new(SyncLayer* sl, size_t num_players, size_t max_prediction, int predictor) {
+  sl->num_players = num_players;
+  sl->max_prediction = max_prediction;
+  sl->last_confirmed_frame = sl->last_saved_frame = NULL_FRAME;
+  sl->current_frame = 0;
+  sl->num_cells = max_prediction + 1; /* SavedStates::new :149-159 */
+  sl->cells = (Cell*)calloc(sl->num_cells, sizeof(Cell));
+  for (size_t i = 0; i < sl->num_cells; i++) sl->cells[i].frame = NULL_FRAME;
+  for (size_t i = 0; i < num_players; i++) iq_new(&sl->queues[i], predictor);
+}
+static void sl_free(SyncLayer* sl) {
+  for (size_t i = 0; i < sl->num_cells; i++) if (sl->cells[i].has_data) state_free(&sl->cells[i].data);
+  free(sl->cells);
+}
+static size_t sl_cell_index(const SyncLayer* sl, int32_t frame) { /* get_cell :161-166 */
+  ORACLE_ASSERT(frame >= 0, "negative frame");
+  return (size_t)frame % sl->num_cells;
+}
+
+typedef struct {
+  int kind;
+  int32_t frame;
+  size_t cell;
+  uint8_t inputs[MAX_PLAYERS];
+  uint8_t status[MAX_PLAYERS];
+} Request;
+
+typedef struct { Request* v; size_t n, cap; } RequestVec;
+static void rv_push(RequestVec* rv, Request r) {
+  if (rv->n == rv->cap) { rv->cap = rv->cap ? 2 * rv->cap : 4; rv->v = (Request*)realloc(rv->v, rv->cap * sizeof(Request)); }
+  rv->v[rv->n++] = r;
+}
+
+static Request sl_save_current_state(SyncLayer* sl) { /* :208-215 */
+  sl->last_saved_frame = sl->current_frame;
+  Request r; memset(&r, 0, sizeof r);
+  r.kind = REQ_SAVE; r.frame = sl->current_frame; r.cell = sl_cell_index(sl, sl->current_frame);
+  return r;
+}
+static Request sl_load_frame(SyncLayer* sl, int32_t frame_to_load) { /* :229-255 */
+  ORACLE_ASSERT(frame_to_load != NULL_FRAME, "cannot load null frame");
+  ORACLE_ASSERT(frame_to_load < sl->current_frame, "must load frame in the past");
+  ORACLE_ASSERT(frame_to_load >= sl->current_frame - (int32_t)sl->max_prediction, "cannot load frame outside of prediction window");
+  size_t ci = sl_cell_index(sl, frame_to_load);
+  ORACLE_ASSERT(sl->cells[ci].frame == frame_to_load, "cell frame != frame to load");
+  sl->current_frame = frame_to_load;
+  Request r; memset(&r, 0, sizeof r);
+  r.kind = REQ_LOAD; r.frame = frame_to_load; r.cell = ci;
+  return r;
+}
+static void sl_reset_prediction(SyncLayer* sl) { for (size_t i = 0; i < sl->num_players; i++) iq_reset_prediction(&sl->queues[i]); }
+static int32_t sl_add_local_input(SyncLayer* sl, size_t handle, PlayerInput in) { /* :259-267 */
+  ORACLE_ASSERT(in.frame == sl->current_frame, "local input frame != current frame");
+  return iq_add_input(&sl->queues[handle], in);
+}
+/* synchronized_inputs (:280-293); connect_status: disconnected[i], last_frame[i] */
+static void sl_synchronized_inputs(SyncLayer* sl, const int* disconnected, const int32_t* last_frame, Request* adv) {
+  for (size_t i = 0; i < sl->num_players; i++) {
+    if (disconnected[i] && last_frame[i] < sl->current_frame) {
+      adv->inputs[i] = 0; adv->status[i] = STATUS_DISCONNECTED;
+    } else {
+      adv->inputs[i] = iq_input(&sl->queues[i], sl->current_frame, &adv->status[i]);
+    }
+  }
+}
+static void sl_set_last_confirmed_frame(SyncLayer* sl, int32_t frame, int sparse_saving) { /* :313-340 */
+  int32_t first_incorrect = NULL_FRAME;
+  for (size_t h = 0; h < sl->num_players; h++)
+    if (sl->queues[h].first_incorrect_frame > first_incorrect) first_incorrect = sl->queues[h].first_incorrect_frame;
+  if (sparse_saving && sl->last_saved_frame < frame) frame = sl->last_saved_frame;
+  if (sl->current_frame < frame) frame = sl->current_frame;
+  ORACLE_ASSERT(first_incorrect == NULL_FRAME || first_incorrect >= frame, "confirmed beyond first incorrect");
+  sl->last_confirmed_frame = frame;
+  if (sl->last_confirmed_frame > 0)
+    for (size_t i = 0; i < sl->num_players; i++) iq_discard_confirmed_frames(&sl->queues[i], frame - 1);
+}
+static const Cell* sl_saved_state_by_frame(const SyncLayer* sl, int32_t frame) { /* :356-364 */
+  const Cell* c = &sl->cells[sl_cell_index(sl, frame)];
+  return c->frame == frame ? c : NULL;
+}
+
+/* ---------------------------------------------------------------- SyncTestSession */
+typedef struct { int32_t frame; int has; uint16_t cs; } HistEntry;
+
+typedef struct {
+  size_t num_players, max_prediction, check_distance;
+  SyncLayer sl;
+  int disconnected[MAX_PLAYERS];
+  int32_t last_frame[MAX_PLAYERS];
+  HistEntry hist[256]; /* HashMap<Frame, Option<u128>>; holds <= check_distance + 1 keys */
+  size_t hist_n;
+  int has_local[MAX_PLAYERS];
+  PlayerInput local[MAX_PLAYERS];
+} SyncTestSession;
+
+/* SessionBuilder::start_synctest_session (builder.rs:346-358): returns 0 or -1 (InvalidRequest) */
+int synctest_new(SyncTestSession* s, size_t num_players, size_t max_prediction, size_t check_distance,
+                 size_t input_delay, int predictor) {
+  if (check_distance >= max_prediction) return -1; /* "Check distance too big." */
+  if (num_players < 1 || num_players > MAX_PLAYERS) return -2;
+  memset(s, 0, sizeof *s);
+  s->num_players = num_players; s->max_prediction = max_prediction; s->check_distance = check_distance;
+  sl_new(&s->sl, num_players, max_prediction, predictor);
+  for (size_t i = 0; i < num_players; i++) { s->sl.queues[i].frame_delay = input_delay; s->disconnected[i] = 0; s->last_frame[i] = NULL_FRAME; }
+  return 0;
+}
+static void synctest_free(SyncTestSession* s) { sl_free(&s->sl); }
+
+static int synctest_add_local_input(SyncTestSession* s, size_t handle, uint8_t input) { /* :61-74 */
+  if (handle >= s->num_players) return -1;
+  s->local[handle].frame = s->sl.current_frame;
+  s->local[handle].input = input;
+  s->has_local[handle] = 1;
+  return 0;
+}
+
+/* checksums_consistent (:173-190) */
+static int synctest_checksums_consistent(SyncTestSession* s, int32_t frame_to_check) {
+  int32_t oldest_allowed = s->sl.current_frame - (int32_t)s->check_distance;
+  size_t w = 0;
+  for (size_t i = 0; i < s->hist_n; i++) if (s->hist[i].frame >= oldest_allowed) s->hist[w++] = s->hist[i];
+  s->hist_n = w;
+  const Cell* c = sl_saved_state_by_frame(&s->sl, frame_to_check);
+  if (!c) return 1;
+  for (size_t i = 0; i < s->hist_n; i++)
+    if (s->hist[i].frame == c->frame)
+      return s->hist[i].has == c->has_checksum && (!c->has_checksum || s->hist[i].cs == c->checksum);
+  ORACLE_ASSERT(s->hist_n < 256, "checksum history overflow");
+  s->hist[s->hist_n].frame = c->frame; s->hist[s->hist_n].has = c->has_checksum; s->hist[s->hist_n].cs = c->checksum;
+  s->hist_n++;
+  return 1;
+}
+
+static void synctest_adjust_gamestate(SyncTestSession* s, int32_t frame_to, RequestVec* rv) { /* :192-217 */
+  int32_t start_frame = s->sl.current_frame;
+  int32_t count = start_frame - frame_to;
+  rv_push(rv, sl_load_frame(&s->sl, frame_to));
+  sl_reset_prediction(&s->sl);
+  ORACLE_ASSERT(s->sl.current_frame == frame_to, "load did not move the cursor");
+  for (int32_t i = 0; i < count; i++) {
+    Request adv; memset(&adv, 0, sizeof adv); adv.kind = REQ_ADVANCE;
+    sl_synchronized_inputs(&s->sl, s->disconnected, s->last_frame, &adv);
+    if (i > 0) rv_push(rv, sl_save_current_state(&s->sl));
+    s->sl.current_frame += 1;
+    rv_push(rv, adv);
+  }
+  ORACLE_ASSERT(s->sl.current_frame == start_frame, "replay did not return to start frame");
+}
+
+/* advance_frame (:85-150).  Returns 0 ok, 1 MismatchedChecksum (mismatch_mask bit k = frame
+ * (current - cd + k)), -1 InvalidRequest (missing local input). */
+int synctest_advance_frame(SyncTestSession* s, RequestVec* rv, int32_t* mismatch_frame, uint64_t* mismatch_mask) {
+  rv->n = 0;
+  int32_t current_frame = s->sl.current_frame;
+  if (s->check_distance > 0 && current_frame > (int32_t)s->check_distance) {
+    int32_t oldest = current_frame - (int32_t)s->check_distance;
+    uint64_t mask = 0;
+    for (int32_t f = oldest; f <= current_frame; f++)
+      if (!synctest_checksums_consistent(s, f)) mask |= 1ull << (f - oldest);
+    if (mask) { *mismatch_frame = current_frame; *mismatch_mask = mask; return 1; }
+    synctest_adjust_gamestate(s, s->sl.current_frame - (int32_t)s->check_distance, rv);
+  }
+  for (size_t h = 0; h < s->num_players; h++) if (!s->has_local[h]) return -1;
+  /* HashMap iteration order is irrelevant: each handle has its own queue */
+  for (size_t h = 0; h < s->num_players; h++) sl_add_local_input(&s->sl, h, s->local[h]);
+  for (size_t h = 0; h < s->num_players; h++) s->has_local[h] = 0;
+  if (s->check_distance > 0) rv_push(rv, sl_save_current_state(&s->sl));
+  Request adv; memset(&adv, 0, sizeof adv); adv.kind = REQ_ADVANCE;
+  sl_synchronized_inputs(&s->sl, s->disconnected, s->last_frame, &adv);
+  rv_push(rv, adv);
+  s->sl.current_frame += 1;
+  int32_t safe_frame = s->sl.current_frame - (int32_t)s->check_distance;
+  sl_set_last_confirmed_frame(&s->sl, safe_frame, 0);
+  for (size_t i = 0; i < s->num_players; i++) s->last_frame[i] = s->sl.current_frame;
+  return 0;
+}
+
+/* ---------------------------------------------------------------- Game (ex_game.rs:58-127) */
+typedef struct {
+  State game_state;
+  int32_t last_checksum_frame;
+  uint16_t last_checksum;
+  int random_checksums;   /* tests/stubs.rs RandomChecksumGameStub analogue (fault injector) */
+  uint64_t rng;
+} Game;
+
+static uint64_t splitmix64(uint64_t* st) {
+  uint64_t z = (*st += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+/* corrupt_after_load: fault injection for tests -- flip the lowest bit of player 0's x right
+ * after a LoadGameState (a non-deterministic simulation the SyncTest must catch). */
+static void game_handle_requests(Game* g, SyncLayer* sl, const RequestVec* rv, int corrupt_after_load) { /* :79-99 */
+  for (size_t k = 0; k < rv->n; k++) {
+    const Request* r = &rv->v[k];
+    Cell* c = &sl->cells[r->cell];
+    if (r->kind == REQ_LOAD) { /* load_game_state :111-113 */
+      ORACLE_ASSERT(c->has_data, "No data found.");
+      State st; state_clone(&st, &c->data);
+      state_free(&g->game_state);
+      g->game_state = st;
+      if (corrupt_after_load) {
+        uint32_t u; memcpy(&u, &g->game_state.positions[0], 4); u ^= 1u; memcpy(&g->game_state.positions[0], &u, 4);
+      }
+    } else if (r->kind == REQ_SAVE) { /* save_game_state :103-108 */
+      ORACLE_ASSERT(g->game_state.frame == r->frame, "save frame != state frame");
+      uint16_t cs = g->random_checksums ? (uint16_t)splitmix64(&g->rng) : state_checksum(&g->game_state);
+      State st; state_clone(&st, &g->game_state);
+      cell_save(c, r->frame, &st, 1, cs);
+    } else { /* advance_frame :115-127 */
+      state_advance(&g->game_state, r->inputs, r->status);
+      g->last_checksum = state_checksum(&g->game_state);
+      g->last_checksum_frame = g->game_state.frame;
+    }
+  }
+}
+
+/* ---------------------------------------------------------------- synthetic inputs
+ * Session s draws from splitmix64 seeded with seed; one draw per (frame, player) in order.
+ * model 0 (uniform): inp = r & 15.  model 1 ("held key"): keep the previous
+ * input of that player unless ((r >> 8) & 7) == 0, then inp = r & 15. */
+void oracle_gen_inputs(uint64_t seed, int64_t frames, int64_t players, int model, uint8_t* out) {
+  uint64_t st = seed;
+  uint8_t prev[MAX_PLAYERS] = {0, 0, 0, 0};
+  for (int64_t f = 0; f < frames; f++)
+    for (int64_t p = 0; p < players; p++) {
+      uint64_t r = splitmix64(&st);
+      uint8_t v = (uint8_t)(r & 15);
+      if (model == 1 && ((r >> 8) & 7) != 0) v = prev[p];
+      prev[p] = v;
+      out[f * players + p] = v;
+    }
+}
+
+/* ---------------------------------------------------------------- exported entry points */
+typedef struct {
+  int32_t num_players, max_prediction, check_distance, input_delay;
+  int32_t predictor, random_checksums;
+  uint64_t rng_seed;
+  int32_t corrupt_frame; /* SyncTest call whose Load is corrupted (-1: none) */
+  int32_t pad_;
+} OracleSyncTestCfg;
+
+typedef struct {
+  int32_t status;            /* 0 ok; 1 MismatchedChecksum; -1 InvalidRequest at build */
+  int32_t frames_done;       /* advance_frame calls that returned Ok */
+  int32_t mismatch_frame;    /* current_frame of the Err */
+  uint64_t mismatch_mask;    /* bit k <=> frame (mismatch_frame - cd + k) mismatched */
+  int64_t n_load, n_save, n_advance, n_resim; /* request counts; resim = advances inside adjust_gamestate */
+} OracleSyncTestResult;
+
+/* Run `frames` SyncTest frames of ex_game with user inputs inputs[frames][P] and statuses all
+ * local.  Outputs (any may be NULL):
+ *   cksum_trace[f]    fletcher16 of the state after call f's final AdvanceFrame (= the display
+ *                     checksum ex_game.rs:121-126, state.frame == f+1)
+ *   req_trace         concatenated request kinds of every call (cap req_cap), req_len[f] per call
+ *   final_state       bincode bytes of the game state after the last call (36+20P)
+ *   ring_frames[R], ring_cksums[R], ring_states[R][36+20P]  the saved-state ring at the end   */
+int oracle_synctest_run(const OracleSyncTestCfg* cfg, int32_t frames, const uint8_t* inputs,
+                        uint16_t* cksum_trace, uint8_t* req_trace, int64_t req_cap, int32_t* req_len,
+                        uint8_t* final_state, int32_t* ring_frames, uint16_t* ring_cksums,
+                        uint8_t* ring_states, OracleSyncTestResult* res) {
+  memset(res, 0, sizeof *res);
+  SyncTestSession s;
+  int rc = synctest_new(&s, (size_t)cfg->num_players, (size_t)cfg->max_prediction,
+                        (size_t)cfg->check_distance, (size_t)cfg->input_delay, cfg->predictor);
+  if (rc) { res->status = -1; return rc; }
+  Game g; memset(&g, 0, sizeof g);
+  state_new(&g.game_state, (uint64_t)cfg->num_players);
+  g.last_checksum_frame = NULL_FRAME;
+  g.random_checksums = cfg->random_checksums; g.rng = cfg->rng_seed;
+  RequestVec rv = {0};
+  int64_t rt = 0;
+  size_t P = (size_t)cfg->num_players;
+  for (int32_t f = 0; f < frames; f++) {
+    for (size_t p = 0; p < P; p++) synctest_add_local_input(&s, p, inputs[(size_t)f * P + p]);
+    int32_t mf = 0; uint64_t mm = 0;
+    int st = synctest_advance_frame(&s, &rv, &mf, &mm);
+    if (st == 1) { res->status = 1; res->mismatch_frame = mf; res->mismatch_mask = mm; break; }
+    if (st < 0) { res->status = -1; break; }
+    int seen_load = 0;
+    for (size_t k = 0; k < rv.n; k++) {
+      int kind = rv.v[k].kind;
+      if (kind == REQ_LOAD) { res->n_load++; seen_load = 1; }
+      else if (kind == REQ_SAVE) res->n_save++;
+      else { res->n_advance++; if (seen_load && k + 1 < rv.n) res->n_resim++; }
+      if (req_trace && rt < req_cap) req_trace[rt] = (uint8_t)kind;
+      rt++;
+    }
+    if (req_len) req_len[f] = (int32_t)rv.n;
+    game_handle_requests(&g, &s.sl, &rv, f == cfg->corrupt_frame);
+    if (cksum_trace) cksum_trace[f] = g.last_checksum;
+    res->frames_done = f + 1;
+  }
+  if (final_state) oracle_state_serialize(&g.game_state, final_state);
+  for (size_t i = 0; i < s.sl.num_cells; i++) {
+    const Cell* c = &s.sl.cells[i];
+    if (ring_frames) ring_frames[i] = c->frame;
+    if (ring_cksums) ring_cksums[i] = c->has_checksum ? c->checksum : 0;
+    if (ring_states) {
+      uint8_t* dst = ring_states + i * (36 + 20 * P);
+      if (c->has_data) oracle_state_serialize(&c->data, dst); else memset(dst, 0, 36 + 20 * P);
+    }
+  }
+  free(rv.v);
+  state_free(&g.game_state);
+  synctest_free(&s);
+  return 0;
+}
+
+/* State::new(P) serialized, and one State::advance step on bincode bytes (for KATs). */
+void oracle_state_new_bytes(int32_t p, uint8_t* out) {
+  State s; state_new(&s, (uint64_t)p); oracle_state_serialize(&s, out); state_free(&s);
+}
+static void state_from_bytes(State* s, const uint8_t* b) {
+  uint64_t p; memcpy(&p, b + 4, 8);
+  state_alloc(s, p);
+  memcpy(&s->frame, b, 4);
+  memcpy(s->positions, b + 20, 8 * p);
+  memcpy(s->velocities, b + 28 + 8 * p, 8 * p);
+  memcpy(s->rotations, b + 36 + 16 * p, 4 * p);
+}
+void oracle_state_advance_bytes(const uint8_t* in, const uint8_t* inputs, const uint8_t* status, uint8_t* out) {
+  State s; state_from_bytes(&s, in); state_advance(&s, inputs, status); oracle_state_serialize(&s, out); state_free(&s);
+}
+float oracle_sinf(float x) { return sinf(x); }
+float oracle_cosf(float x) { return cosf(x); }
+float oracle_fmodf(float a, float b) { return fmodf(a, b); }
+
+/* libm sinf/cosf bits over an inclusive f32 bit range, written to out_sin/out_cos (u32). */
+void oracle_sincos_range(uint32_t lo, uint32_t hi, uint32_t* out_sin, uint32_t* out_cos) {
+  for (uint64_t u = lo; u <= hi; u++) {
+    float f; uint32_t w = (uint32_t)u; memcpy(&f, &w, 4);
+    float s = sinf(f), c = cosf(f);
+    memcpy(&out_sin[u - lo], &s, 4); memcpy(&out_cos[u - lo], &c, 4);
+  }
+}
+
+/* Order-independent digest of libm sinf/cosf over an inclusive bit range:
+ * sum over u of mix64((u << 32) | bits(sinf(u))) + mix64(((u << 32) | bits(cosf(u))) ^ C).  */
+static uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+typedef struct { uint32_t lo, hi; uint64_t acc; } DigestJob;
+static void* digest_worker(void* a) {
+  DigestJob* j = (DigestJob*)a;
+  uint64_t acc = 0;
+  for (uint64_t u = j->lo; u <= j->hi; u++) {
+    float f; uint32_t w = (uint32_t)u; memcpy(&f, &w, 4);
+    float s = sinf(f), c = cosf(f);
+    uint32_t sb, cb; memcpy(&sb, &s, 4); memcpy(&cb, &c, 4);
+    acc += mix64((u << 32) | sb) + mix64(((u << 32) | cb) ^ 0xC05C05C05C05C05Cull);
+  }
+  j->acc = acc;
+  return NULL;
+}
+uint64_t oracle_sincos_digest(uint32_t lo, uint32_t hi, int threads) {
+  if (threads < 1) threads = 1;
+  if (threads > 64) threads = 64;
+  pthread_t th[64]; DigestJob jobs[64];
+  uint64_t n = (uint64_t)hi - lo + 1, per = (n + threads - 1) / threads;
+  int used = 0;
+  for (int t = 0; t < threads; t++) {
+    uint64_t a = lo + (uint64_t)t * per;
+    if (a > hi) break;
+    uint64_t b = a + per - 1; if (b > hi) b = hi;
+    jobs[t].lo = (uint32_t)a; jobs[t].hi = (uint32_t)b;
+    pthread_create(&th[t], NULL, digest_worker, &jobs[t]);
+    used++;
+  }
+  uint64_t acc = 0;
+  for (int t = 0; t < used; t++) { pthread_join(th[t], NULL); acc += jobs[t].acc; }
+  return acc;
+}
+
+/* ---------------------------------------------------------------- CPU baseline
+ * The reference loop (ex_game_synctest.rs:69-82: add_local_input for every player, advance_frame,
+ * handle_requests) for one session per thread, inputs drawn on the fly with the same generator
+ * (seed = seed_base + session).  Returns wall seconds of the timed frames; thread 0's per-frame
+ * display checksums go to cksum0 (length frames, after warmup). */
+typedef struct {
+  OracleSyncTestCfg cfg; int model; uint64_t seed; int32_t warmup, frames;
+  uint16_t* cksum; int64_t resim; int failed;
+  pthread_barrier_t* bar; double t0, t1;
+} BenchJob;
+
+static double now_s(void) { struct timespec ts; clock_gettime(CLOCK_MONOTONIC, &ts); return ts.tv_sec + 1e-9 * ts.tv_nsec; }
+
+static void* bench_worker(void* a) {
+  BenchJob* j = (BenchJob*)a;
+  SyncTestSession s;
+  size_t P = (size_t)j->cfg.num_players;
+  if (synctest_new(&s, P, (size_t)j->cfg.max_prediction, (size_t)j->cfg.check_distance, (size_t)j->cfg.input_delay, j->cfg.predictor)) { j->failed = 1; return NULL; }
+  Game g; memset(&g, 0, sizeof g);
+  state_new(&g.game_state, P);
+  RequestVec rv = {0};
+  uint64_t st = j->seed; uint8_t prev[MAX_PLAYERS] = {0, 0, 0, 0};
+  int64_t resim = 0;
+  for (int32_t f = 0; f < j->warmup + j->frames; f++) {
+    if (f == j->warmup) { pthread_barrier_wait(j->bar); j->t0 = now_s(); }
+    for (size_t p = 0; p < P; p++) { /* the local_input() of ex_game.rs:177-221, synthetic */
+      uint64_t r = splitmix64(&st);
+      uint8_t v = (uint8_t)(r & 15);
+      if (j->model == 1 && ((r >> 8) & 7) != 0) v = prev[p];
+      prev[p] = v;
+      synctest_add_local_input(&s, p, v);
+    }
+    int32_t mf; uint64_t mm;
+    if (synctest_advance_frame(&s, &rv, &mf, &mm) != 0) { j->failed = 1; break; }
+    if (f >= j->warmup) {
+      int seen_load = 0;
+      for (size_t k = 0; k < rv.n; k++) {
+        if (rv.v[k].kind == REQ_LOAD) seen_load = 1;
+        else if (rv.v[k].kind == REQ_ADVANCE && seen_load && k + 1 < rv.n) resim++;
+      }
+    }
+    game_handle_requests(&g, &s.sl, &rv, 0);
+    if (f >= j->warmup && j->cksum) j->cksum[f - j->warmup] = g.last_checksum;
+  }
+  j->t1 = now_s();
+  j->resim = resim;
+  free(rv.v);
+  state_free(&g.game_state);
+  synctest_free(&s);
+  return NULL;
+}
+
+/* Returns resimulated session-frames over all threads; *wall = max thread wall seconds. */
+int64_t oracle_synctest_bench(const OracleSyncTestCfg* cfg, int model, uint64_t seed_base, int32_t threads,
+                              int32_t warmup, int32_t frames, uint16_t* cksum0, double* wall) {
+  if (threads < 1) threads = 1;
+  BenchJob* jobs = (BenchJob*)calloc((size_t)threads, sizeof(BenchJob));
+  pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+  pthread_barrier_t bar; pthread_barrier_init(&bar, NULL, (unsigned)threads);
+  for (int t = 0; t < threads; t++) {
+    jobs[t].cfg = *cfg; jobs[t].model = model; jobs[t].seed = seed_base + (uint64_t)t;
+    jobs[t].warmup = warmup; jobs[t].frames = frames; jobs[t].cksum = t == 0 ? cksum0 : NULL; jobs[t].bar = &bar;
+    pthread_create(&th[t], NULL, bench_worker, &jobs[t]);
+  }
+  int64_t total = 0; double t0 = 1e300, t1 = 0; int failed = 0;
+  for (int t = 0; t < threads; t++) {
+    pthread_join(th[t], NULL);
+    total += jobs[t].resim; failed |= jobs[t].failed;
+    if (jobs[t].t0 < t0) t0 = jobs[t].t0;
+    if (jobs[t].t1 > t1) t1 = jobs[t].t1;
+  }
+  pthread_barrier_destroy(&bar);
+  free(jobs); free(th);
+  *wall = t1 - t0;
+  return failed ? -1 : total;
+}
+
+/* ---------------------------------------------------------------- InputQueue unit pins
+ * Restates the reference's input_queue.rs tests (:298-353): add inputs[i] for frames i (with the
+ * given delay), returning add_input's frame in added[i] and input(i) read back right after each
+ * add in read[i] (only when do_read). */
+void oracle_input_queue_sequence(int32_t delay, int32_t n, const int32_t* frames, const uint8_t* inputs,
+                                 int do_read, int32_t* added, uint8_t* read, int32_t* length) {
+  InputQueue q;
+  iq_new(&q, PREDICT_REPEAT_LAST);
+  q.frame_delay = (size_t)delay;
+  for (int32_t i = 0; i < n; i++) {
+    PlayerInput in = {frames[i], inputs[i]};
+    added[i] = iq_add_input(&q, in);
+    if (length) length[i] = (int32_t)q.length;
+    if (do_read) { uint8_t st; read[i] = iq_input(&q, frames[i], &st); }
+  }
+}

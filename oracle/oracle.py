@@ -1,0 +1,198 @@
+"""ctypes binding of the C oracle (oracle/ggrs_oracle.c).  TEST INFRASTRUCTURE ONLY.
+
+Loaded only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the checker
+or the CPU baseline.  The product (ggrs_amd/) never imports this module.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "libggrs_oracle.so")
+
+REQ_SAVE, REQ_LOAD, REQ_ADVANCE = 0, 1, 2
+MODEL_UNIFORM, MODEL_HELD = 0, 1
+
+
+class SyncTestCfg(ctypes.Structure):
+    _fields_ = [
+        ("num_players", ctypes.c_int32),
+        ("max_prediction", ctypes.c_int32),
+        ("check_distance", ctypes.c_int32),
+        ("input_delay", ctypes.c_int32),
+        ("predictor", ctypes.c_int32),
+        ("random_checksums", ctypes.c_int32),
+        ("rng_seed", ctypes.c_uint64),
+        ("corrupt_frame", ctypes.c_int32),
+        ("pad_", ctypes.c_int32),
+    ]
+
+
+class SyncTestResult(ctypes.Structure):
+    _fields_ = [
+        ("status", ctypes.c_int32),
+        ("frames_done", ctypes.c_int32),
+        ("mismatch_frame", ctypes.c_int32),
+        ("mismatch_mask", ctypes.c_uint64),
+        ("n_load", ctypes.c_int64),
+        ("n_save", ctypes.c_int64),
+        ("n_advance", ctypes.c_int64),
+        ("n_resim", ctypes.c_int64),
+    ]
+
+
+def build():
+    """Compile the oracle with its Makefile (gcc; seconds)."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.POINTER
+        u8p, u16p, i32p = P(ctypes.c_uint8), P(ctypes.c_uint16), P(ctypes.c_int32)
+        L.oracle_synctest_run.argtypes = [P(SyncTestCfg), ctypes.c_int32, u8p, u16p, u8p,
+                                          ctypes.c_int64, i32p, u8p, i32p, u16p, u8p,
+                                          P(SyncTestResult)]
+        L.oracle_synctest_run.restype = ctypes.c_int
+        L.oracle_gen_inputs.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64,
+                                        ctypes.c_int, u8p]
+        L.oracle_fletcher16.argtypes = [u8p, ctypes.c_size_t]
+        L.oracle_fletcher16.restype = ctypes.c_uint16
+        L.oracle_state_new_bytes.argtypes = [ctypes.c_int32, u8p]
+        L.oracle_state_advance_bytes.argtypes = [u8p, u8p, u8p, u8p]
+        for fn in ("oracle_sinf", "oracle_cosf"):
+            getattr(L, fn).argtypes = [ctypes.c_float]
+            getattr(L, fn).restype = ctypes.c_float
+        L.oracle_sincos_digest.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int]
+        L.oracle_sincos_digest.restype = ctypes.c_uint64
+        L.oracle_sincos_range.argtypes = [ctypes.c_uint32, ctypes.c_uint32, P(ctypes.c_uint32),
+                                          P(ctypes.c_uint32)]
+        L.oracle_synctest_bench.argtypes = [P(SyncTestCfg), ctypes.c_int, ctypes.c_uint64,
+                                            ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, u16p,
+                                            P(ctypes.c_double)]
+        L.oracle_synctest_bench.restype = ctypes.c_int64
+        L.oracle_input_queue_sequence.argtypes = [ctypes.c_int32, ctypes.c_int32, i32p, u8p,
+                                                  ctypes.c_int, i32p, u8p, i32p]
+        _lib = L
+    return _lib
+
+
+def _ptr(a, ct):
+    return a.ctypes.data_as(ctypes.POINTER(ct)) if a is not None else None
+
+
+def state_bytes(p):
+    return 36 + 20 * p
+
+
+def gen_inputs(seed, frames, players, model=MODEL_UNIFORM):
+    out = np.zeros((frames, players), np.uint8)
+    lib().oracle_gen_inputs(seed, frames, players, model, _ptr(out, ctypes.c_uint8))
+    return out
+
+
+def session_seed(session, base=0x6767525300000000):
+    return (base + session) & 0xFFFFFFFFFFFFFFFF
+
+
+def fletcher16(b):
+    a = np.frombuffer(bytes(b), np.uint8).copy()
+    return int(lib().oracle_fletcher16(_ptr(a, ctypes.c_uint8), a.size))
+
+
+def state_new(p):
+    out = np.zeros(state_bytes(p), np.uint8)
+    lib().oracle_state_new_bytes(p, _ptr(out, ctypes.c_uint8))
+    return out
+
+
+def state_advance(state, inputs, status=None):
+    state = np.ascontiguousarray(state, np.uint8)
+    p = (state.size - 36) // 20
+    inp = np.ascontiguousarray(inputs, np.uint8)
+    st = np.zeros(p, np.uint8) if status is None else np.ascontiguousarray(status, np.uint8)
+    out = np.zeros_like(state)
+    lib().oracle_state_advance_bytes(_ptr(state, ctypes.c_uint8), _ptr(inp, ctypes.c_uint8),
+                                     _ptr(st, ctypes.c_uint8), _ptr(out, ctypes.c_uint8))
+    return out
+
+
+def synctest_run(inputs, num_players=2, max_prediction=8, check_distance=2, input_delay=0,
+                 random_checksums=False, rng_seed=1, req_cap=None, corrupt_frame=-1):
+    """Run the restated SyncTest loop; returns a dict of numpy arrays and the result struct."""
+    inputs = np.ascontiguousarray(inputs, np.uint8).reshape(-1, num_players)
+    frames = inputs.shape[0]
+    R = max_prediction + 1
+    sb = state_bytes(num_players)
+    cfg = SyncTestCfg(num_players, max_prediction, check_distance, input_delay, 0,
+                      1 if random_checksums else 0, rng_seed, corrupt_frame, 0)
+    res = SyncTestResult()
+    req_cap = req_cap if req_cap is not None else frames * (2 * check_distance + 3)
+    out = dict(
+        cksum=np.zeros(frames, np.uint16),
+        req=np.zeros(max(req_cap, 1), np.uint8),
+        req_len=np.zeros(frames, np.int32),
+        final_state=np.zeros(sb, np.uint8),
+        ring_frames=np.zeros(R, np.int32),
+        ring_cksums=np.zeros(R, np.uint16),
+        ring_states=np.zeros((R, sb), np.uint8),
+    )
+    rc = lib().oracle_synctest_run(
+        ctypes.byref(cfg), frames, _ptr(inputs, ctypes.c_uint8), _ptr(out["cksum"], ctypes.c_uint16),
+        _ptr(out["req"], ctypes.c_uint8), req_cap, _ptr(out["req_len"], ctypes.c_int32),
+        _ptr(out["final_state"], ctypes.c_uint8), _ptr(out["ring_frames"], ctypes.c_int32),
+        _ptr(out["ring_cksums"], ctypes.c_uint16), _ptr(out["ring_states"], ctypes.c_uint8),
+        ctypes.byref(res))
+    out["rc"] = rc
+    out["result"] = res
+    return out
+
+
+def input_queue_sequence(delay, frames, inputs, read=True):
+    """Add (frame, input) pairs to one InputQueue; returns (add_input results, input(frame)
+    read back after each add, queue length after each add)."""
+    fr = np.ascontiguousarray(frames, np.int32)
+    ins = np.ascontiguousarray(inputs, np.uint8)
+    n = fr.size
+    added, got, length = np.zeros(n, np.int32), np.zeros(n, np.uint8), np.zeros(n, np.int32)
+    lib().oracle_input_queue_sequence(delay, n, _ptr(fr, ctypes.c_int32), _ptr(ins, ctypes.c_uint8),
+                                      1 if read else 0, _ptr(added, ctypes.c_int32),
+                                      _ptr(got, ctypes.c_uint8), _ptr(length, ctypes.c_int32))
+    return added, got, length
+
+
+def sincos_digest(lo, hi, threads=8):
+    return int(lib().oracle_sincos_digest(lo, hi, threads))
+
+
+def sincos_range(lo, hi):
+    n = hi - lo + 1
+    s = np.zeros(n, np.uint32)
+    c = np.zeros(n, np.uint32)
+    lib().oracle_sincos_range(lo, hi, _ptr(s, ctypes.c_uint32), _ptr(c, ctypes.c_uint32))
+    return s, c
+
+
+def synctest_bench(threads, frames, warmup=1000, num_players=2, max_prediction=8,
+                   check_distance=7, input_delay=2, model=MODEL_UNIFORM,
+                   seed_base=0x6767525300000000):
+    """CPU baseline: the reference SyncTest loop, one session per thread.
+
+    Returns (resim_frames_total, wall_seconds, thread0_checksums)."""
+    cfg = SyncTestCfg(num_players, max_prediction, check_distance, input_delay, 0, 0, 0, -1, 0)
+    ck = np.zeros(frames, np.uint16)
+    wall = ctypes.c_double(0)
+    n = lib().oracle_synctest_bench(ctypes.byref(cfg), model, seed_base, threads, warmup, frames,
+                                    _ptr(ck, ctypes.c_uint16), ctypes.byref(wall))
+    if n < 0:
+        raise RuntimeError("oracle bench session failed")
+    return int(n), wall.value, ck

@@ -1,0 +1,49 @@
+"""GPU KAT of the product sinf/cosf restatement: the order-independent digest of every f32 in
+[0, 2*pi] (each reachable ship rotation is in there, SURVEY.md finding 3) must equal the digest of
+glibc libm's values pinned in tests/golden/golden.json; both the separate and the fused form."""
+import ctypes
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+GOLDEN = json.load(open(os.path.join(HERE, "golden", "golden.json")))
+
+
+@pytest.fixture(scope="module")
+def katlib(tmp_path_factory):
+    so = os.path.join(HERE, "native", "libsincosf_kat_device.so")
+    src = os.path.join(HERE, "native", "sincosf_kat_device.hip")
+    if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+        subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-ffp-contract=off",
+                        "-fPIC", "-shared", "-std=c++17", "-I", os.path.join(ROOT, "ggrs_amd", "csrc"),
+                        src, "-o", so], check=True)
+    L = ctypes.CDLL(so)
+    L.kat_digest.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
+    L.kat_values.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    return L
+
+
+@pytest.mark.parametrize("fused", [0, 1])
+def test_device_digest_0_2pi(katlib, fused):
+    g = GOLDEN["sincos_digest_0_2pi"]
+    out = ctypes.c_uint64()
+    assert katlib.kat_digest(g["lo"], g["hi"], fused, ctypes.byref(out)) == 0
+    assert out.value == g["digest"]
+
+
+def test_device_values(katlib):
+    xs = np.array([s["x"] for s in GOLDEN["sincos"]], np.uint32)
+    sv, cv = np.zeros_like(xs), np.zeros_like(xs)
+    assert katlib.kat_values(ctypes.c_void_p(xs.ctypes.data), xs.size, ctypes.c_void_p(sv.ctypes.data),
+                             ctypes.c_void_p(cv.ctypes.data)) == 0
+    for i, s in enumerate(GOLDEN["sincos"]):
+        if s["x"] in (0x7F800000,):
+            continue
+        assert (int(sv[i]), int(cv[i])) == (s["sin"], s["cos"]), hex(s["x"])
