@@ -1,0 +1,66 @@
+"""Summarise a tools/profile.sh run (gpurun_out/<tag>) into profiles/<tag>/: the rocprofv3
+kernel-stats CSV, per-kernel PMC averages, and pmc_<workload>.json (per-launch HBM bytes of the
+SyncTest kernel, read by bench.py's roofline.traffic).
+
+HBM bytes follow MI355X_MICROARCH.md "HBM": FETCH_SIZE / WRITE_SIZE are KiB from the L2's
+memory-side request counters (TCC_EA0_RDREQ/WRREQ); on gfx950 FETCH_SIZE reports exactly half the
+bytes of a wide streaming read, so the corrected figure doubles it.  Both are kept.
+
+    python tools/summarize_profile.py r01 config2_l4096_f128
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def pmc_means(path, kernel_substr):
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if kernel_substr in r["Kernel_Name"]:
+            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}, {k: len(v) for k, v in agg.items()}
+
+
+def main(tag, workload, kernel="synctest_kernel"):
+    src = os.path.join(ROOT, "gpurun_out", tag)
+    dst = os.path.join(ROOT, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "trace_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(dst, "kernel_stats.csv")))}
+    kname = next(n for n in stats if kernel in n)
+    avg_ns = float(stats[kname]["AverageNs"])
+    out = {"tag": tag, "workload": workload, "kernel": kname, "calls": int(stats[kname]["Calls"]),
+           "avg_duration_ns": avg_ns}
+    for group in ("pmc_fetch", "pmc_write", "pmc_sq"):
+        p = os.path.join(src, group, "pmc_counter_collection.csv")
+        if os.path.exists(p):
+            means, counts = pmc_means(p, kernel)
+            out[group] = means
+    fetch_kib = out.get("pmc_fetch", {}).get("FETCH_SIZE")
+    write_kib = out.get("pmc_write", {}).get("WRITE_SIZE")
+    if fetch_kib is not None and write_kib is not None:
+        out["hbm_bytes_per_launch_raw"] = (fetch_kib + write_kib) * 1024
+        out["hbm_bytes_per_launch"] = (2 * fetch_kib + write_kib) * 1024  # gfx950 FETCH x2
+    sq = out.get("pmc_sq", {})
+    if sq.get("SQ_WAVES"):
+        out["valu_insts_per_wave"] = sq["SQ_INSTS_VALU"] / sq["SQ_WAVES"]
+    with open(os.path.join(dst, "summary.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+    if "hbm_bytes_per_launch" in out:
+        with open(os.path.join(ROOT, "profiles", f"pmc_{workload}.json"), "w") as fh:
+            json.dump({"tag": tag, "kernel": kname, "hbm_bytes_per_launch": out["hbm_bytes_per_launch"],
+                       "hbm_bytes_per_launch_raw": out["hbm_bytes_per_launch_raw"],
+                       "avg_duration_ns": avg_ns}, fh, indent=1)
+    for f in ("bench_trace.log",):
+        if os.path.exists(os.path.join(src, f)):
+            shutil.copy(os.path.join(src, f), os.path.join(dst, f))
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
