@@ -57,6 +57,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores available)")
     ap.add_argument("--cpu-frames", type=int, default=100000, help="SyncTest frames per CPU thread")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--path", choices=["pipelined", "sequential"], default="pipelined",
+                    help="SyncTest kernel (DESIGN.md section 3)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -84,6 +86,7 @@ def main():
     inputs = synth.gen_inputs(rank * lanes, lanes, total_frames, P, synth.MODEL_HELD)
     eng = Engine(lanes, P, maxp, cd, delay, input_capacity=total_frames + cd + delay + 2,
                  device=local_rank, trace_capacity=trace_cap)
+    eng.set_synctest_path(0 if args.path == "pipelined" else 1)
     eng.add_local_inputs(0, inputs)  # resident in HBM before anything is timed
     eng.synchronize()
 
@@ -180,7 +183,8 @@ def main():
                                    "held-key inputs",
                        "sessions_per_gpu": lanes, "global_sessions": lanes * world,
                        "frames_per_step": fps, "players": P, "check_distance": cd,
-                       "max_prediction": maxp, "parallelism": f"sessions sharded over {world} GPU(s)"},
+                       "max_prediction": maxp, "kernel_path": args.path,
+                       "parallelism": f"sessions sharded over {world} GPU(s)"},
             "roofline": roofline,
             "cpu_baseline": cpu_baseline,
             "halted_lanes": halted,

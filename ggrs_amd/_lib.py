@@ -17,6 +17,7 @@ NULL_FRAME = -1
 REQ_SAVE, REQ_LOAD, REQ_ADVANCE = 0, 1, 2
 STATUS_CONFIRMED, STATUS_PREDICTED, STATUS_DISCONNECTED = 0, 1, 2
 LANE_RUNNING, LANE_MISMATCH = 0, 1
+PATH_PIPELINED, PATH_SEQUENTIAL = 0, 1
 
 # every symbol include/ggrs_amd.h declares (tests check the library exports all of them)
 EXPORTS = (
@@ -25,7 +26,7 @@ EXPORTS = (
     "ggrs_synctest_advance_frames", "ggrs_handle_requests", "ggrs_synchronize",
     "ggrs_current_frame", "ggrs_read_mismatches", "ggrs_read_save_checksums", "ggrs_read_state",
     "ggrs_read_ring", "ggrs_read_trace", "ggrs_debug_corrupt_on_load", "ggrs_last_launch_ms",
-    "ggrs_timing_reset", "ggrs_timing_read",
+    "ggrs_timing_reset", "ggrs_timing_read", "ggrs_set_synctest_path",
 )
 
 
@@ -94,6 +95,7 @@ def lib():
         L.ggrs_debug_corrupt_on_load.argtypes = [vp, ctypes.c_int32, ctypes.c_int32]
         L.ggrs_last_launch_ms.argtypes = [vp, P(ctypes.c_float)]
         L.ggrs_timing_reset.argtypes = [vp]
+        L.ggrs_set_synctest_path.argtypes = [vp, ctypes.c_int32]
         L.ggrs_timing_read.argtypes = [vp, P(ctypes.c_float), P(ctypes.c_int32)]
         for name in EXPORTS:
             if name not in ("ggrs_abi_version", "ggrs_last_error"):

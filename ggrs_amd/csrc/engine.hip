@@ -20,6 +20,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -188,6 +189,110 @@ __global__ __launch_bounds__(kWave) void synctest_kernel(SyncTestParams p) {
   store_state<P>(s, p.cur + lane, L);
 }
 
+// ------------------------------------------------------------------------------------------
+// Pipelined SyncTest program (the fast path for calls f > cd).
+//
+// Call c's replay (adjust_gamestate, sync_test_session.rs:192-217) loads the cell of frame c-cd,
+// which call c-1 saved right after its FIRST replayed advance; everything else call c does hangs
+// off that state as a chain of cd+1 advances (cd-1 re-saves, the save of frame c, the new frame's
+// advance).  So with K = cd+1 lanes per session, chain c runs on lane c mod K over time steps
+// t = c .. c+cd (step i = t-c), and the K chains of a session advance in lockstep:
+//   * at step t every chain holds (its own replay of) frame t-cd, advances it with input t-cd
+//     (one input load per session), and - unless it just loaded - saves it first;
+//   * the chain starting at t (i = 0) takes the state chain t-1 is about to save (the cell of
+//     frame t-cd, i.e. its LoadGameState) from that lane's registers; the first chain of a launch
+//     loads it from the HBM ring, where the previous launch saved it;
+//   * chain t-cd saves frame t-cd as "current" (its first-seen checksum, first_ck) in the same
+//     step in which chains t-cd+1 .. t-1 re-save it, so their comparison against the first-seen
+//     value (checksums_consistent at their next call) is a register broadcast.
+// Every Load, Save (state + Fletcher-16 into the ring) and AdvanceFrame of the reference program
+// is executed; only the schedule changes.  A chain whose re-saves mismatch records the launch in
+// *fail_f0; the host then restores the checkpoint taken before the launch and replays it with the
+// sequential kernel above, which reproduces the reference's Err state exactly (stop at the first
+// failing call, ring and state as the reference leaves them).
+struct PipeParams {
+  int64_t L;
+  int32_t R, cd, K, spw, f0, n, cap, trace_cap;
+  int32_t corrupt_lane, corrupt_frame;
+  uint32_t* cur;
+  uint32_t* ring;
+  uint16_t* ring_ck;
+  uint16_t* first_ck;
+  const uint8_t* inputs;
+  const int32_t* lane_status;
+  int32_t* fail_f0;
+  uint16_t* trace;
+};
+
+template <int P>
+__global__ __launch_bounds__(kWave) void synctest_pipelined_kernel(PipeParams p) {
+  if (*p.fail_f0 >= 0) return;  // an earlier launch failed: the host replays from its checkpoint
+  const int wl = threadIdx.x;
+  const int K = p.K, cd = p.cd, R = p.R;
+  const int g = wl / K, j = wl - g * K;
+  const int64_t L = p.L;
+  const int64_t s = (int64_t)blockIdx.x * p.spw + g;  // session of this lane
+  const bool valid = g < p.spw && s < L && p.lane_status[s] == GGRS_LANE_RUNNING;
+  const int64_t sl = valid ? s : 0;
+  const int base = g * K;
+  const int src_prev = base + (j == 0 ? K - 1 : j - 1);  // lane of chain c-1
+  constexpr int F = state_fields(P);
+  BoxState<P> st;
+#pragma unroll
+  for (int k = 0; k < F; k++) st.w[k] = 0;
+  uint64_t mask = 0;
+  const int32_t t_end = p.f0 + p.n + cd;
+  int32_t i = ((p.f0 - j) % K + K) % K;  // step of this lane's chain at t = f0
+  for (int32_t t = p.f0; t < t_end; ++t, i = (i + 1 == K ? 0 : i + 1)) {
+    const int32_t c = t - i;
+    const bool active = valid && c >= p.f0 && c < p.f0 + p.n;
+    const int32_t gf = t - cd;  // the frame every chain of the session holds at this step
+    const uint32_t in = load_inputs<P>(p.inputs, (int64_t)(gf % p.cap) * L + sl);
+    // LoadGameState of chain c: the cell chain c-1 is saving in this step
+    BoxState<P> from;
+#pragma unroll
+    for (int k = 0; k < F; k++) from.w[k] = __shfl(st.w[k], src_prev, kWave);
+    if (i == 0) {
+      if (c == p.f0) load_state<P>(st, p.ring + (int64_t)(gf % R) * F * L + sl, L);
+      else st = from;
+      if (s == p.corrupt_lane && c == p.corrupt_frame) st.w[fld_x(P, 0)] ^= 1u;
+      mask = 0;
+    }
+    const uint16_t ck = fletcher16_state<P>(st);
+    // first-seen checksum of frame gf: chain gf's save of it in this very step, when chain gf
+    // belongs to this launch; otherwise the value an earlier launch stored in first_ck
+    const int src_first = base + ((gf % K) + K) % K;
+    const uint16_t first_here = (uint16_t)__shfl((int)ck, src_first, kWave);
+    if (active && i > 0) {
+      store_state<P>(st, p.ring + (int64_t)(gf % R) * F * L + s, L);  // SaveGameState(gf)
+      p.ring_ck[(int64_t)(gf % R) * L + s] = ck;
+      if (i < cd) {
+        const uint16_t first = gf >= p.f0 ? first_here : p.first_ck[(int64_t)(gf % R) * L + s];
+        if (ck != first) mask |= 1ull << (i - 1);  // compared at call c+1 (frame c+1-cd+i-1)
+      } else {
+        p.first_ck[(int64_t)(gf % R) * L + s] = ck;
+      }
+    }
+    if (active) advance_state<P>(st, in, 0u);
+    if (active && i == cd) {
+      if (p.trace) p.trace[(int64_t)(c % p.trace_cap) * L + s] = fletcher16_state<P>(st);
+      if (c == p.f0 + p.n - 1) store_state<P>(st, p.cur + s, L);
+      if (mask) atomicCAS(p.fail_f0, -1, p.f0);
+    }
+  }
+}
+
+// Checkpoint / restore of everything a SyncTest launch writes (cur, ring, ring_ck, first_ck):
+// dir 0 copies live -> shadow unless a launch already failed (then the shadow must keep the
+// state from before the failing launch); dir 1 copies shadow -> live.
+__global__ void checkpoint_kernel(uint4* live, uint4* shadow, int64_t n16, const int32_t* fail_f0, int dir) {
+  if (dir == 0 && *fail_f0 >= 0) return;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n16; k += (int64_t)gridDim.x * blockDim.x) {
+    if (dir == 0) shadow[k] = live[k];
+    else live[k] = shadow[k];
+  }
+}
+
 struct RequestParams {
   int64_t L;
   int32_t R, n_reqs, trace_cap;
@@ -263,6 +368,13 @@ struct ggrs_engine {
   uint16_t* trace = nullptr;
   uint8_t* staging = nullptr;  // device scratch for request inputs / status / request list
   size_t staging_bytes = 0;
+  // cur | ring | ring_ck | first_ck live in one arena so a launch checkpoint is one copy
+  uint8_t* arena = nullptr;
+  uint8_t* shadow = nullptr;
+  size_t arena_bytes = 0;
+  int32_t* fail_f0 = nullptr;  // f0 of the first pipelined launch whose checks failed, or -1
+  bool unverified = false;     // pipelined launches enqueued since the last resolve()
+  int path = GGRS_PATH_PIPELINED;
   // host-side (lane-uniform) bookkeeping
   int32_t current_frame = 0;
   int32_t next_user_frame = 0;  // next user frame add_local_inputs expects
@@ -333,7 +445,7 @@ int ggrs_engine_destroy(ggrs_engine_t* e) {
   if (!e) return GGRS_OK;
   (void)hipSetDevice(e->cfg.device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
-  void* bufs[] = {e->cur, e->ring, e->ring_ck, e->first_ck, e->inputs, e->lane_status,
+  void* bufs[] = {e->arena, e->shadow, e->fail_f0, e->inputs, e->lane_status,
                   e->mis_frame, e->mis_mask, e->trace, e->staging};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -386,18 +498,27 @@ int ggrs_engine_create(const ggrs_config_t* cfg, ggrs_engine_t** out) {
   CTRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
   CTRY(hipEventCreate(&e->ev0));
   CTRY(hipEventCreate(&e->ev1));
-  CTRY(hipMalloc(&e->cur, sizeof(uint32_t) * e->F * L));
-  CTRY(hipMalloc(&e->ring, sizeof(uint32_t) * (size_t)e->R * e->F * L));
-  CTRY(hipMalloc(&e->ring_ck, sizeof(uint16_t) * (size_t)e->R * L));
-  CTRY(hipMalloc(&e->first_ck, sizeof(uint16_t) * (size_t)e->R * L));
+  {
+    auto up16 = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t b_cur = up16(sizeof(uint32_t) * e->F * L);
+    const size_t b_ring = up16(sizeof(uint32_t) * (size_t)e->R * e->F * L);
+    const size_t b_ck = up16(sizeof(uint16_t) * (size_t)e->R * L);
+    e->arena_bytes = b_cur + b_ring + 2 * b_ck;
+    CTRY(hipMalloc(&e->arena, e->arena_bytes));
+    CTRY(hipMalloc(&e->shadow, e->arena_bytes));
+    CTRY(hipMemsetAsync(e->arena, 0, e->arena_bytes, e->stream));
+    e->cur = (uint32_t*)e->arena;
+    e->ring = (uint32_t*)(e->arena + b_cur);
+    e->ring_ck = (uint16_t*)(e->arena + b_cur + b_ring);
+    e->first_ck = (uint16_t*)(e->arena + b_cur + b_ring + b_ck);
+  }
+  CTRY(hipMalloc(&e->fail_f0, sizeof(int32_t)));
+  CTRY(hipMemsetAsync(e->fail_f0, 0xff, sizeof(int32_t), e->stream));
   CTRY(hipMalloc(&e->inputs, (size_t)e->cap * L * e->Pp));
   CTRY(hipMalloc(&e->lane_status, sizeof(int32_t) * L));
   CTRY(hipMalloc(&e->mis_frame, sizeof(int32_t) * L));
   CTRY(hipMalloc(&e->mis_mask, sizeof(uint64_t) * L));
   if (c.trace_capacity > 0) CTRY(hipMalloc(&e->trace, sizeof(uint16_t) * (size_t)c.trace_capacity * L));
-  CTRY(hipMemsetAsync(e->ring, 0, sizeof(uint32_t) * (size_t)e->R * e->F * L, e->stream));
-  CTRY(hipMemsetAsync(e->ring_ck, 0, sizeof(uint16_t) * (size_t)e->R * L, e->stream));
-  CTRY(hipMemsetAsync(e->first_ck, 0, sizeof(uint16_t) * (size_t)e->R * L, e->stream));
   // default input (Input::default(), inp = 0) for every queue frame, covering frames < delay
   CTRY(hipMemsetAsync(e->inputs, 0, (size_t)e->cap * L * e->Pp, e->stream));
   CTRY(hipMemsetAsync(e->lane_status, 0, sizeof(int32_t) * L, e->stream));
@@ -424,6 +545,8 @@ int ggrs_engine_config(const ggrs_engine_t* e, ggrs_config_t* out) {
   return GGRS_OK;
 }
 
+static int resolve(ggrs_engine_t* e);
+
 static int add_inputs_common(ggrs_engine_t* e, int32_t first_frame, int32_t n, const void* src,
                              bool device) {
   if (!e || (!src && n > 0)) return set_error(GGRS_E_INVALID, "null argument");
@@ -433,6 +556,7 @@ static int add_inputs_common(ggrs_engine_t* e, int32_t first_frame, int32_t n, c
                      "inputs must be added sequentially (expected frame %d, got %d; input_queue.rs:171-177)",
                      e->next_user_frame, first_frame);
   if (n == 0) return GGRS_OK;
+  { int rc_ = resolve(e); if (rc_) return rc_; }  // oldest needed input is then current - cd
   const int32_t delay = e->cfg.input_delay;
   // oldest queue frame a later call still reads: the rollback start current - cd
   const int64_t oldest_needed = (int64_t)e->current_frame - e->cfg.check_distance;
@@ -469,25 +593,12 @@ int ggrs_add_local_inputs_device(ggrs_engine_t* e, int32_t first_frame, int32_t 
   return add_inputs_common(e, first_frame, n, inputs, true);
 }
 
-int ggrs_synctest_advance_frames(ggrs_engine_t* e, int32_t n) {
-  if (!e) return set_error(GGRS_E_INVALID, "null engine");
-  if (n < 0) return set_error(GGRS_E_INVALID, "n_frames must be >= 0");
-  if (e->mode == 2) return set_error(GGRS_E_STATE, "engine already driven by ggrs_handle_requests");
-  if (n == 0) return GGRS_OK;
-  // every frame run needs its (delayed) input queued: SyncTestSession requires input for all
-  // players before advance_frame ("Missing local input", sync_test_session.rs:110-114)
-  const int64_t last_needed_user = (int64_t)e->current_frame + n - 1 - e->cfg.input_delay;
-  if (last_needed_user >= e->next_user_frame)
-    return set_error(GGRS_E_INVALID,
-                     "Missing local input while calling advance_frame(): frame %lld not added",
-                     (long long)last_needed_user);
-  e->mode = 1;
-  HIP_TRY(hipSetDevice(e->cfg.device));
+static int launch_sequential(ggrs_engine_t* e, int32_t f0, int32_t n) {
   SyncTestParams p;
   p.L = e->cfg.num_lanes;
   p.R = e->R;
   p.cd = e->cfg.check_distance;
-  p.f0 = e->current_frame;
+  p.f0 = f0;
   p.n = n;
   p.cap = e->cap;
   p.trace_cap = e->cfg.trace_capacity;
@@ -503,7 +614,7 @@ int ggrs_synctest_advance_frames(ggrs_engine_t* e, int32_t n) {
   p.mis_mask = e->mis_mask;
   p.trace = e->trace;
   const int64_t grid = grid_of(p.L, kWave);
-  int rc = launch_timed(e, [&] {
+  return launch_timed(e, [&] {
     switch (e->cfg.num_players) {
       case 1: synctest_kernel<1><<<grid, kWave, 0, e->stream>>>(p); break;
       case 2: synctest_kernel<2><<<grid, kWave, 0, e->stream>>>(p); break;
@@ -511,16 +622,120 @@ int ggrs_synctest_advance_frames(ggrs_engine_t* e, int32_t n) {
       default: synctest_kernel<4><<<grid, kWave, 0, e->stream>>>(p); break;
     }
   });
+}
+
+static int checkpoint(ggrs_engine_t* e, int dir) {
+  const int64_t n16 = (int64_t)(e->arena_bytes / 16);
+  checkpoint_kernel<<<1024, 256, 0, e->stream>>>((uint4*)e->arena, (uint4*)e->shadow, n16, e->fail_f0, dir);
+  HIP_TRY(hipGetLastError());
+  return GGRS_OK;
+}
+
+static int launch_pipelined(ggrs_engine_t* e, int32_t f0, int32_t n) {
+  int rc = checkpoint(e, 0);
   if (rc) return rc;
+  PipeParams p;
+  p.L = e->cfg.num_lanes;
+  p.R = e->R;
+  p.cd = e->cfg.check_distance;
+  p.K = p.cd + 1;
+  p.spw = kWave / p.K;
+  p.f0 = f0;
+  p.n = n;
+  p.cap = e->cap;
+  p.trace_cap = e->cfg.trace_capacity;
+  p.corrupt_lane = e->corrupt_lane;
+  p.corrupt_frame = e->corrupt_frame;
+  p.cur = e->cur;
+  p.ring = e->ring;
+  p.ring_ck = e->ring_ck;
+  p.first_ck = e->first_ck;
+  p.inputs = e->inputs;
+  p.lane_status = e->lane_status;
+  p.fail_f0 = e->fail_f0;
+  p.trace = e->trace;
+  const int64_t grid = grid_of(p.L, p.spw);
+  e->unverified = true;
+  return launch_timed(e, [&] {
+    switch (e->cfg.num_players) {
+      case 1: synctest_pipelined_kernel<1><<<grid, kWave, 0, e->stream>>>(p); break;
+      case 2: synctest_pipelined_kernel<2><<<grid, kWave, 0, e->stream>>>(p); break;
+      case 3: synctest_pipelined_kernel<3><<<grid, kWave, 0, e->stream>>>(p); break;
+      default: synctest_pipelined_kernel<4><<<grid, kWave, 0, e->stream>>>(p); break;
+    }
+  });
+}
+
+// Settle pipelined launches: if one of them saw a checksum mismatch, roll every lane back to the
+// checkpoint taken before it and replay the frames since with the sequential kernel, which halts
+// lanes exactly where the reference returns MismatchedChecksum.
+static int resolve(ggrs_engine_t* e) {
+  if (!e->unverified) return GGRS_OK;
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  int32_t f = -1;
+  HIP_TRY(hipMemcpyAsync(&f, e->fail_f0, sizeof f, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  e->unverified = false;
+  if (f < 0) return GGRS_OK;
+  int rc = checkpoint(e, 1);
+  if (rc) return rc;
+  HIP_TRY(hipMemsetAsync(e->fail_f0, 0xff, sizeof(int32_t), e->stream));
+  rc = launch_sequential(e, f, e->current_frame - f);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return GGRS_OK;
+}
+
+int ggrs_synctest_advance_frames(ggrs_engine_t* e, int32_t n) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  if (n < 0) return set_error(GGRS_E_INVALID, "n_frames must be >= 0");
+  if (e->mode == 2) return set_error(GGRS_E_STATE, "engine already driven by ggrs_handle_requests");
+  if (n == 0) return GGRS_OK;
+  // every frame run needs its (delayed) input queued: SyncTestSession requires input for all
+  // players before advance_frame ("Missing local input", sync_test_session.rs:110-114)
+  const int64_t last_needed_user = (int64_t)e->current_frame + n - 1 - e->cfg.input_delay;
+  if (last_needed_user >= e->next_user_frame)
+    return set_error(GGRS_E_INVALID,
+                     "Missing local input while calling advance_frame(): frame %lld not added",
+                     (long long)last_needed_user);
+  e->mode = 1;
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const int32_t cd = e->cfg.check_distance;
+  int32_t f0 = e->current_frame, left = n;
+  // warm-up calls (f <= cd: no rollback yet) and cd == 0 / 1 take the sequential kernel
+  if (e->path == GGRS_PATH_SEQUENTIAL || cd <= 1) {
+    int rc = launch_sequential(e, f0, left);
+    if (rc) return rc;
+    left = 0;
+  } else if (f0 <= cd) {
+    const int32_t m = std::min(left, cd + 1 - f0);
+    int rc = launch_sequential(e, f0, m);
+    if (rc) return rc;
+    f0 += m;
+    left -= m;
+  }
+  if (left > 0) {
+    int rc = launch_pipelined(e, f0, left);
+    if (rc) return rc;
+  }
   // lane-uniform bookkeeping: after call f the ring holds, in slot s, the newest frame <= f
   // congruent to s (every frame 0..f has been saved; cd == 0 saves nothing)
   e->current_frame += n;
-  if (e->cfg.check_distance > 0)
+  if (cd > 0)
     for (int s = 0; s < e->R; s++) {
       int32_t last = e->current_frame - 1;
       int32_t fr = last - (((last - s) % e->R) + e->R) % e->R;
       e->ring_tag[s] = fr >= 0 ? fr : GGRS_NULL_FRAME;
     }
+  return GGRS_OK;
+}
+
+int ggrs_set_synctest_path(ggrs_engine_t* e, int32_t path) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  if (path != GGRS_PATH_PIPELINED && path != GGRS_PATH_SEQUENTIAL) return set_error(GGRS_E_INVALID, "unknown path %d", path);
+  int rc = resolve(e);
+  if (rc) return rc;
+  e->path = path;
   return GGRS_OK;
 }
 
@@ -612,6 +827,7 @@ int ggrs_handle_requests(ggrs_engine_t* e, const ggrs_request_t* reqs, int32_t n
 
 int ggrs_synchronize(ggrs_engine_t* e) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  { int rc_ = resolve(e); if (rc_) return rc_; }
   HIP_TRY(hipSetDevice(e->cfg.device));
   HIP_TRY(hipStreamSynchronize(e->stream));
   return GGRS_OK;
@@ -625,6 +841,7 @@ int ggrs_current_frame(const ggrs_engine_t* e, int32_t* out) {
 
 int ggrs_read_mismatches(ggrs_engine_t* e, int32_t* st, int32_t* mf, uint64_t* mm) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  { int rc_ = resolve(e); if (rc_) return rc_; }
   HIP_TRY(hipSetDevice(e->cfg.device));
   const size_t L = e->cfg.num_lanes;
   if (st) HIP_TRY(hipMemcpyAsync(st, e->lane_status, 4 * L, hipMemcpyDeviceToHost, e->stream));
@@ -636,6 +853,7 @@ int ggrs_read_mismatches(ggrs_engine_t* e, int32_t* st, int32_t* mf, uint64_t* m
 
 int ggrs_read_save_checksums(ggrs_engine_t* e, int32_t frame, uint16_t* out) {
   if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
+  { int rc_ = resolve(e); if (rc_) return rc_; }
   if (frame < 0 || e->ring_tag[frame % e->R] != frame)
     return set_error(GGRS_E_PRECONDITION, "no saved cell for frame %d", frame);
   HIP_TRY(hipSetDevice(e->cfg.device));
@@ -669,6 +887,7 @@ static int gather_lane(ggrs_engine_t* e, const uint32_t* base, int32_t lane, uin
 
 int ggrs_read_state(ggrs_engine_t* e, int32_t lane, uint8_t* out) {
   if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
+  { int rc_ = resolve(e); if (rc_) return rc_; }
   if (lane < 0 || lane >= e->cfg.num_lanes) return set_error(GGRS_E_INVALID, "lane out of range");
   HIP_TRY(hipSetDevice(e->cfg.device));
   uint32_t w[32];
@@ -681,6 +900,7 @@ int ggrs_read_state(ggrs_engine_t* e, int32_t lane, uint8_t* out) {
 
 int ggrs_read_ring(ggrs_engine_t* e, int32_t lane, int32_t* frames, uint16_t* cks, uint8_t* states) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  { int rc_ = resolve(e); if (rc_) return rc_; }
   if (lane < 0 || lane >= e->cfg.num_lanes) return set_error(GGRS_E_INVALID, "lane out of range");
   HIP_TRY(hipSetDevice(e->cfg.device));
   const size_t L = e->cfg.num_lanes;
@@ -707,6 +927,7 @@ int ggrs_read_ring(ggrs_engine_t* e, int32_t lane, int32_t* frames, uint16_t* ck
 
 int ggrs_read_trace(ggrs_engine_t* e, int32_t first_frame, int32_t n, uint16_t* out) {
   if (!e || (!out && n > 0)) return set_error(GGRS_E_INVALID, "null argument");
+  { int rc_ = resolve(e); if (rc_) return rc_; }
   if (!e->trace) return set_error(GGRS_E_STATE, "engine created with trace_capacity = 0");
   const int32_t T = e->cfg.trace_capacity;
   if (n < 0 || first_frame < 0 || first_frame + n > e->current_frame || first_frame < e->current_frame - T)

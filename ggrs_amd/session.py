@@ -100,6 +100,10 @@ class Engine:
     def synctest_advance_frames(self, n):
         _lib.check(self._L.ggrs_synctest_advance_frames(self._h, n))
 
+    def set_synctest_path(self, path):
+        """_lib.PATH_PIPELINED (default) or _lib.PATH_SEQUENTIAL."""
+        _lib.check(self._L.ggrs_set_synctest_path(self._h, path))
+
     def handle_requests(self, reqs, inputs=None, status=None):
         arr = (_lib.Request * len(reqs))(*[_lib.Request(k, f) for k, f in reqs])
         i = None if inputs is None else np.ascontiguousarray(inputs, np.uint8)

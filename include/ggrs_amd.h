@@ -64,6 +64,10 @@ extern "C" {
 #define GGRS_STATUS_PREDICTED 1
 #define GGRS_STATUS_DISCONNECTED 2
 
+/* SyncTest execution paths (ggrs_set_synctest_path) */
+#define GGRS_PATH_PIPELINED 0  /* default: cd+1 concurrent rollback chains per session */
+#define GGRS_PATH_SEQUENTIAL 1 /* one lane per session, calls in order */
+
 /* per-lane status */
 #define GGRS_LANE_RUNNING 0
 #define GGRS_LANE_MISMATCH 1 /* halted: SyncTestSession::advance_frame returned MismatchedChecksum */
@@ -103,8 +107,12 @@ int ggrs_add_local_inputs(ggrs_engine_t* eng, int32_t first_frame, int32_t n_fra
 int ggrs_add_local_inputs_device(ggrs_engine_t* eng, int32_t first_frame, int32_t n_frames,
                                  const void* inputs_device);
 
-/* Run n_frames SyncTest frames on every running lane (fused: one kernel launch). */
+/* Run n_frames SyncTest frames on every running lane (fused: one kernel launch; warm-up frames
+ * f <= check_distance take one extra launch). */
 int ggrs_synctest_advance_frames(ggrs_engine_t* eng, int32_t n_frames);
+/* Choose the SyncTest kernel: GGRS_PATH_PIPELINED (default; a mismatch found there is re-run on
+ * the sequential kernel from a checkpoint, so results are identical) or GGRS_PATH_SEQUENTIAL. */
+int ggrs_set_synctest_path(ggrs_engine_t* eng, int32_t path);
 
 /* Execute an ordered request list on every lane (fused: one kernel launch).
  * inputs: [n_advance][num_lanes][num_players] Input.inp bytes, status: same shape InputStatus

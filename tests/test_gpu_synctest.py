@@ -22,10 +22,15 @@ def lane_inputs(O, base_seed, lanes, frames, players, model):
                      for l in range(lanes)], axis=1)  # [frames][lanes][P]
 
 
-def make_engine(lanes, P, maxp, cd, d, frames, trace=True):
+PATHS = [0, 1]  # _lib.PATH_PIPELINED, _lib.PATH_SEQUENTIAL
+
+
+def make_engine(lanes, P, maxp, cd, d, frames, trace=True, path=0):
     from ggrs_amd import Engine
-    return Engine(lanes, P, maxp, cd, d, input_capacity=frames + d + cd + 2,
-                  trace_capacity=frames if trace else 0)
+    eng = Engine(lanes, P, maxp, cd, d, input_capacity=frames + d + cd + 2,
+                 trace_capacity=frames if trace else 0)
+    eng.set_synctest_path(path)
+    return eng
 
 
 def run_chunks(eng, inputs, chunks):
@@ -52,14 +57,15 @@ def check_lane(O, eng, inputs, lane, P, maxp, cd, d, frames, trace=None):
             assert int(ck[s]) == int(r["ring_cksums"][s]) and bytes(st[s]) == bytes(r["ring_states"][s])
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("name", sorted(CASES))
-def test_golden_cases(oracle, name):
+def test_golden_cases(oracle, name, path):
     c = CASES[name]
     P, maxp, cd, d, F = c["num_players"], c["max_prediction"], c["check_distance"], c["input_delay"], c["frames"]
     lanes = 130  # three waves, the last partial
     inputs = lane_inputs(oracle, c["seed"] + 1000, lanes, F, P, c["input_model"])
     inputs[:, 0, :] = oracle.gen_inputs(c["seed"], F, P, c["input_model"])  # lane 0 = the golden session
-    eng = make_engine(lanes, P, maxp, cd, d, F)
+    eng = make_engine(lanes, P, maxp, cd, d, F, path=path)
     run_chunks(eng, inputs, [1, 2, cd + 1, F - cd - 4])
     assert eng.current_frame() == F
     tr = eng.trace(0, F)
@@ -76,11 +82,12 @@ def test_golden_cases(oracle, name):
     assert (st == 0).all()
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("chunks", [[300], [1] * 20 + [280], [7, 13, 280], [150, 150]])
-def test_chunking_is_invisible(oracle, chunks):
+def test_chunking_is_invisible(oracle, chunks, path):
     P, maxp, cd, d, F, lanes = 2, 8, 7, 2, 300, 64
     inputs = lane_inputs(oracle, 77, lanes, F, P, 0)
-    eng = make_engine(lanes, P, maxp, cd, d, F)
+    eng = make_engine(lanes, P, maxp, cd, d, F, path=path)
     run_chunks(eng, inputs, chunks)
     tr = eng.trace(0, F)
     for lane in (0, 31, 63):
@@ -109,19 +116,29 @@ def test_streamed_inputs_small_queue(oracle):
         assert bytes(eng.state(lane)) == bytes(r["final_state"])
 
 
-def test_mismatch_detection_matches_reference(oracle):
+@pytest.mark.parametrize("path,chunk,call", [(0, 120, 40), (1, 120, 40), (0, 16, 40), (0, 16, 48),
+                                             (0, 7, 9), (1, 7, 9), (0, 120, 110)])
+def test_mismatch_detection_matches_reference(oracle, path, chunk, call):
     """A non-deterministic simulation on one lane: the SyncTest must report
-    MismatchedChecksum{current_frame, mismatched_frames} exactly as the reference session."""
+    MismatchedChecksum{current_frame, mismatched_frames} exactly as the reference session
+    (pipelined launches detect it and are replayed on the sequential kernel from a checkpoint;
+    chunk 16 puts the failure in a later launch, call 48 on a launch's first chain)."""
     from ggrs_amd import MismatchedChecksum, SessionBuilder
-    P, maxp, cd, d, F, lanes, bad_lane, call = 2, 8, 7, 2, 120, 70, 66, 40
+    P, maxp, cd, d, F, lanes, bad_lane = 2, 8, 7, 2, 120, 70, 66
     inputs = lane_inputs(oracle, 9, lanes, F, P, 0)
     sess = (SessionBuilder().with_num_players(P).with_max_prediction_window(maxp)
             .with_check_distance(cd).with_input_delay(d).with_num_lanes(lanes)
             .with_input_capacity(F + 16).start_synctest_session())
+    sess.engine.set_synctest_path(path)
     sess.engine.corrupt_on_load(bad_lane, call)
     sess.add_local_inputs(inputs)
     with pytest.raises(MismatchedChecksum) as ei:
-        sess.advance_frames(F)
+        done = 0
+        while done < F:
+            n = min(chunk, F - done)
+            sess.advance_frames(n, check=False)
+            done += n
+        sess.raise_on_mismatch()
     r = oracle.synctest_run(inputs[:, bad_lane, :], P, maxp, cd, d, corrupt_frame=call)
     assert r["result"].status == 1
     assert ei.value.current_frame == r["result"].mismatch_frame == call + 1
@@ -140,25 +157,28 @@ def test_mismatch_detection_matches_reference(oracle):
     check_lane(oracle, sess.engine, inputs, bad_lane - 1, P, maxp, cd, d, F)
 
 
-def test_full_size_config2(oracle):
+@pytest.mark.parametrize("path", PATHS)
+def test_full_size_config2(oracle, path):
     """Config 2 at full size: 4096 sessions, 8-frame rollback every frame (SyncTest cd 8,
-    max_prediction 9), held-key inputs; sampled lanes bit-exact plus a checksum of checksums."""
+    max_prediction 9), held-key inputs; sampled lanes bit-exact."""
+    from ggrs_amd import synth
     P, maxp, cd, d, F, lanes = 2, 9, 8, 0, 400, 4096
-    inputs = lane_inputs(oracle, 0x6767525300000000, lanes, F, P, 1)
-    eng = make_engine(lanes, P, maxp, cd, d, F)
+    inputs = synth.gen_inputs(0, lanes, F, P, synth.MODEL_HELD)
+    eng = make_engine(lanes, P, maxp, cd, d, F, path=path)
     run_chunks(eng, inputs, [F])
     tr = eng.trace(0, F)
     rng = np.random.default_rng(0)
-    for lane in sorted(set([0, 1, 2047, 4095] + rng.integers(0, lanes, 12).tolist())):
+    for lane in sorted(set([0, 1, 6, 7, 2047, 4095] + rng.integers(0, lanes, 12).tolist())):
         check_lane(oracle, eng, inputs, lane, P, maxp, cd, d, F, tr)
     st, _, _ = eng.mismatches()
     assert (st == 0).all()
 
 
-def test_max_ring_and_four_players(oracle):
+@pytest.mark.parametrize("path", PATHS)
+def test_max_ring_and_four_players(oracle, path):
     P, maxp, cd, d, F, lanes = 4, 63, 62, 0, 200, 64
     inputs = lane_inputs(oracle, 3, lanes, F, P, 0)
-    eng = make_engine(lanes, P, maxp, cd, d, F)
+    eng = make_engine(lanes, P, maxp, cd, d, F, path=path)
     run_chunks(eng, inputs, [F])
     tr = eng.trace(0, F)
     for lane in (0, 63):
