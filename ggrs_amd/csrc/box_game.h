@@ -156,12 +156,19 @@ __device__ inline uint32_t dot4_u8(uint32_t a, uint32_t b, uint32_t c) {
 template <int P>
 __device__ inline uint16_t fletcher16_state(const BoxState<P>& s) {
   constexpr int n = Fletcher<P>::n;
-  uint32_t s1 = Fletcher<P>::kSum1Const, s2 = Fletcher<P>::kSum2Const;
+  constexpr int F = state_fields(P);
+  // two independent accumulator pairs halve the dependent v_dot4 chain
+  uint32_t a1 = Fletcher<P>::kSum1Const, a2 = Fletcher<P>::kSum2Const, b1 = 0, b2 = 0;
 #pragma unroll
-  for (int k = 0; k < state_fields(P); k++) {
-    s1 = dot4_u8(s.w[k], 0x01010101u, s1);
-    s2 = dot4_u8(s.w[k], weights_at(n, fld_offset(P, k)), s2);
+  for (int k = 0; k < F; k += 2) {
+    a1 = dot4_u8(s.w[k], 0x01010101u, a1);
+    a2 = dot4_u8(s.w[k], weights_at(n, fld_offset(P, k)), a2);
+    if (k + 1 < F) {
+      b1 = dot4_u8(s.w[k + 1], 0x01010101u, b1);
+      b2 = dot4_u8(s.w[k + 1], weights_at(n, fld_offset(P, k + 1)), b2);
+    }
   }
+  const uint32_t s1 = a1 + b1, s2 = a2 + b2;
   return (uint16_t)(((s2 % 255u) << 8) | (s1 % 255u));
 }
 

@@ -243,11 +243,15 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_kernel(PipeParams p)
   uint64_t mask = 0;
   const int32_t t_end = p.f0 + p.n + cd;
   int32_t i = ((p.f0 - j) % K + K) % K;  // step of this lane's chain at t = f0
+  // input of frame t-cd, fetched one step ahead so its load is issued before this step's stores
+  // (loads and stores retire in order on one vmcnt: a load behind the stores would wait for them)
+  uint32_t in_next = load_inputs<P>(p.inputs, (int64_t)((p.f0 - cd) % p.cap) * L + sl);
   for (int32_t t = p.f0; t < t_end; ++t, i = (i + 1 == K ? 0 : i + 1)) {
     const int32_t c = t - i;
     const bool active = valid && c >= p.f0 && c < p.f0 + p.n;
     const int32_t gf = t - cd;  // the frame every chain of the session holds at this step
-    const uint32_t in = load_inputs<P>(p.inputs, (int64_t)(gf % p.cap) * L + sl);
+    const uint32_t in = in_next;
+    if (t + 1 < t_end) in_next = load_inputs<P>(p.inputs, (int64_t)((gf + 1) % p.cap) * L + sl);
     // LoadGameState of chain c: the cell chain c-1 is saving in this step
     BoxState<P> from;
 #pragma unroll
@@ -278,6 +282,195 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_kernel(PipeParams p)
       if (p.trace) p.trace[(int64_t)(c % p.trace_cap) * L + s] = fletcher16_state<P>(st);
       if (c == p.f0 + p.n - 1) store_state<P>(st, p.cur + s, L);
       if (mask) atomicCAS(p.fail_f0, -1, p.f0);
+    }
+  }
+}
+
+// The same pipelined program with the players of a chain on Pp adjacent lanes (Pp = P rounded
+// up to a power of two): each lane steps one player (State::advance's per-player loop body is
+// independent across players, ex_game.rs:275-332), so a wavefront issues half (P = 2) the
+// instructions per step and twice the wavefronts share the chip.  The frame counter lives in
+// every lane of a chain; the Fletcher-16 sums are per-lane partials over the lane's own fields
+// (player 0 adds the frame field and the constants), combined by an xor-butterfly across the Pp
+// lanes.  Used whenever (cd+1) * Pp <= 64.
+template <int P>
+__device__ inline void partial_fletcher(uint32_t frame, const uint32_t (&w)[5], int pl, uint32_t& s1,
+                                        uint32_t& s2) {
+  constexpr int n = Fletcher<P>::n;
+  s1 = 0;
+  s2 = 0;
+  if (pl >= P) return;
+  const int ks[5] = {fld_x(P, 0), fld_y(P, 0), fld_vx(P, 0), fld_vy(P, 0), fld_rot(P, 0)};
+  const int dk[5] = {2, 2, 2, 2, 1};  // field index stride per player
+#pragma unroll
+  for (int q = 0; q < 5; q++) {
+    const int k = ks[q] + dk[q] * pl;
+    const uint32_t wt = weights_at(n, fld_offset(P, k));
+    s1 = dot4_u8(w[q], 0x01010101u, s1);
+    s2 = dot4_u8(w[q], wt, s2);
+  }
+  if (pl == 0) {
+    s1 = dot4_u8(frame, 0x01010101u, s1 + Fletcher<P>::kSum1Const);
+    s2 = dot4_u8(frame, weights_at(n, 0), s2 + Fletcher<P>::kSum2Const);
+  }
+}
+
+template <int P, int Pp>
+__device__ inline uint16_t chain_fletcher(uint32_t frame, const uint32_t (&w)[5], int pl) {
+  uint32_t s1, s2;
+  partial_fletcher<P>(frame, w, pl, s1, s2);
+#pragma unroll
+  for (int m = 1; m < Pp; m <<= 1) {
+    s1 += (uint32_t)__shfl_xor((int)s1, m, kWave);
+    s2 += (uint32_t)__shfl_xor((int)s2, m, kWave);
+  }
+  return (uint16_t)(((s2 % 255u) << 8) | (s1 % 255u));
+}
+
+// LDS staging of the inputs: every chain of a session reads the same input byte per step, and a
+// global load inside the step loop would be waited on with vmcnt, which also counts the step's
+// ring stores (they retire in order) -- so inputs for kStageFrames frames at a time are copied to
+// LDS, and the loop body issues no global loads at all.
+constexpr int kStageFrames = 256;
+constexpr int kMaxRampFrames = 64;  // first-seen checksums of frames f0-cd .. f0-1 (cd <= 62)
+
+template <int P>
+__global__ __launch_bounds__(kWave) void synctest_pipelined_split_kernel(PipeParams p) {
+  constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
+  __shared__ uint8_t lds_in[kStageFrames * kWave];           // [frame][session-in-block][Pp]
+  __shared__ uint16_t lds_first[kMaxRampFrames * kWave];      // [ramp frame][session-in-block]
+  __shared__ uint32_t lds_cell[kWave * 6];                    // chain f0's LoadGameState, per lane
+  if (*p.fail_f0 >= 0) return;
+  const int wl = threadIdx.x;
+  const int K = p.K, cd = p.cd, R = p.R;
+  const int G = K * Pp;
+  const int g = wl / G, r = wl - g * G;
+  const int j = r / Pp, pl = r - j * Pp;  // chain slot, player
+  const int64_t L = p.L;
+  const int spw = p.spw;
+  const int64_t s0 = (int64_t)blockIdx.x * spw;  // first session of this block
+  const int64_t s = s0 + g;
+  const int nsess = (int)((L - s0) < spw ? (L - s0) : spw);
+  const bool valid = g < spw && s < L && p.lane_status[s] == GGRS_LANE_RUNNING;
+  const bool owner = valid && pl < P;
+  const int64_t sl = valid ? s : 0;
+  const int plc = pl < P ? pl : 0;
+  const int base = g * G;
+  const int src_prev = base + (j == 0 ? K - 1 : j - 1) * Pp + pl;
+  constexpr int F = state_fields(P);
+  const int kx = fld_x(P, plc), ky = fld_y(P, plc), kvx = fld_vx(P, plc), kvy = fld_vy(P, plc),
+            krot = fld_rot(P, plc);
+  const int32_t g0 = p.f0 - cd;  // first frame any chain of this launch steps
+  // first-seen checksums of the frames saved by the previous launch (frames g0 .. f0-1)
+  for (int q = wl; q < cd * nsess; q += kWave) {
+    const int gg = q / nsess, ss = q - gg * nsess;
+    lds_first[gg * kWave + ss] = p.first_ck[(int64_t)((g0 + gg) % R) * L + s0 + ss];
+  }
+  // the cell chain f0 loads: frame f0-cd, saved by the previous launch.  Parked in LDS so the
+  // loop reads it with ds_read: a register first used inside the loop would put a vmcnt wait in
+  // the loop body, and vmcnt also waits for the step's ring stores.
+  {
+    const uint32_t* cell = p.ring + (int64_t)(g0 % R) * F * L + sl;
+    lds_cell[wl * 6 + 0] = cell[0];
+    lds_cell[wl * 6 + 1] = cell[kx * L];
+    lds_cell[wl * 6 + 2] = cell[ky * L];
+    lds_cell[wl * 6 + 3] = cell[kvx * L];
+    lds_cell[wl * 6 + 4] = cell[kvy * L];
+    lds_cell[wl * 6 + 5] = cell[krot * L];
+  }
+  __syncthreads();
+  uint32_t frame = 0;
+  uint32_t w[5] = {0, 0, 0, 0, 0};  // x, y, vx, vy, rot of this lane's player
+  uint64_t mask = 0;
+  const int32_t t_end = p.f0 + p.n + cd;
+  int32_t i = ((p.f0 - j) % K + K) % K;
+  const int row = nsess * Pp;  // staged bytes per frame
+  for (int32_t t = p.f0; t < t_end; ++t, i = (i + 1 == K ? 0 : i + 1)) {
+    const int32_t c = t - i;
+    const bool active = valid && c >= p.f0 && c < p.f0 + p.n;
+    const int32_t gf = t - cd;
+    const int32_t rel = gf - g0;
+    if ((rel & (kStageFrames - 1)) == 0) {  // stage the next kStageFrames frames of input
+      __syncthreads();
+      const int nf = (t_end - t) < kStageFrames ? (t_end - t) : kStageFrames;
+      for (int q = wl; q < nf * row; q += kWave) {
+        const int ff = q / row, b = q - ff * row;
+        lds_in[ff * row + b] = p.inputs[((int64_t)((gf + ff) % p.cap) * L + s0) * Pp + b];
+      }
+      __syncthreads();
+    }
+    const uint32_t in = lds_in[(rel & (kStageFrames - 1)) * row + g * Pp + pl];
+    uint32_t from[6];
+    from[0] = (uint32_t)__shfl((int)frame, src_prev, kWave);
+#pragma unroll
+    for (int q = 0; q < 5; q++) from[q + 1] = (uint32_t)__shfl((int)w[q], src_prev, kWave);
+    if (i == 0) {  // LoadGameState(c - cd)
+      if (c == p.f0) {
+        frame = lds_cell[wl * 6];
+#pragma unroll
+        for (int q = 0; q < 5; q++) w[q] = lds_cell[wl * 6 + 1 + q];
+      } else {
+        frame = from[0];
+#pragma unroll
+        for (int q = 0; q < 5; q++) w[q] = from[q + 1];
+      }
+      if (s == p.corrupt_lane && c == p.corrupt_frame && pl == 0) w[0] ^= 1u;
+      mask = 0;
+    }
+    const uint16_t ck = chain_fletcher<P, Pp>(frame, w, pl);
+    const int src_first = base + (((gf % K) + K) % K) * Pp;
+    const uint16_t first_here = (uint16_t)__shfl((int)ck, src_first, kWave);
+    if (active && i > 0) {  // SaveGameState(gf)
+      uint32_t* cell = p.ring + (int64_t)(gf % R) * F * L + s;
+      if (owner) {
+        cell[kx * L] = w[0];
+        cell[ky * L] = w[1];
+        cell[kvx * L] = w[2];
+        cell[kvy * L] = w[3];
+        cell[krot * L] = w[4];
+      }
+      if (pl == 0) {
+        cell[0] = frame;
+        p.ring_ck[(int64_t)(gf % R) * L + s] = ck;
+        if (i < cd) {  // checksums_consistent(gf) at call c+1
+          const uint16_t first = gf >= p.f0 ? first_here : lds_first[rel * kWave + g];
+          if (ck != first) mask |= 1ull << (i - 1);
+        } else {
+          p.first_ck[(int64_t)(gf % R) * L + s] = ck;
+        }
+      }
+    }
+    if (active) {  // AdvanceFrame with the input of frame gf
+      frame = (uint32_t)((int32_t)frame + 1);
+      if (owner) {
+        float x = __builtin_bit_cast(float, w[0]), y = __builtin_bit_cast(float, w[1]);
+        float vx = __builtin_bit_cast(float, w[2]), vy = __builtin_bit_cast(float, w[3]);
+        float rot = __builtin_bit_cast(float, w[4]);
+        advance_player(x, y, vx, vy, rot, in);
+        w[0] = __builtin_bit_cast(uint32_t, x);
+        w[1] = __builtin_bit_cast(uint32_t, y);
+        w[2] = __builtin_bit_cast(uint32_t, vx);
+        w[3] = __builtin_bit_cast(uint32_t, vy);
+        w[4] = __builtin_bit_cast(uint32_t, rot);
+      }
+    }
+    if (p.trace) {  // uniform condition: the butterfly needs every lane
+      const uint16_t ck_new = chain_fletcher<P, Pp>(frame, w, pl);
+      if (active && i == cd && pl == 0) p.trace[(int64_t)(c % p.trace_cap) * L + s] = ck_new;
+    }
+    if (active && i == cd) {
+      if (c == p.f0 + p.n - 1) {
+        uint32_t* cur = p.cur + s;
+        if (owner) {
+          cur[kx * L] = w[0];
+          cur[ky * L] = w[1];
+          cur[kvx * L] = w[2];
+          cur[kvy * L] = w[3];
+          cur[krot * L] = w[4];
+        }
+        if (pl == 0) cur[0] = frame;
+      }
+      if (pl == 0 && mask) atomicCAS(p.fail_f0, -1, p.f0);
     }
   }
 }
@@ -654,8 +847,21 @@ static int launch_pipelined(ggrs_engine_t* e, int32_t f0, int32_t n) {
   p.lane_status = e->lane_status;
   p.fail_f0 = e->fail_f0;
   p.trace = e->trace;
-  const int64_t grid = grid_of(p.L, p.spw);
   e->unverified = true;
+  const int Pp = e->Pp;
+  if (e->path == GGRS_PATH_PIPELINED && p.K * Pp <= kWave) {
+    p.spw = kWave / (p.K * Pp);
+    const int64_t grid = grid_of(p.L, p.spw);
+    return launch_timed(e, [&] {
+      switch (e->cfg.num_players) {
+        case 1: synctest_pipelined_split_kernel<1><<<grid, kWave, 0, e->stream>>>(p); break;
+        case 2: synctest_pipelined_split_kernel<2><<<grid, kWave, 0, e->stream>>>(p); break;
+        case 3: synctest_pipelined_split_kernel<3><<<grid, kWave, 0, e->stream>>>(p); break;
+        default: synctest_pipelined_split_kernel<4><<<grid, kWave, 0, e->stream>>>(p); break;
+      }
+    });
+  }
+  const int64_t grid = grid_of(p.L, p.spw);
   return launch_timed(e, [&] {
     switch (e->cfg.num_players) {
       case 1: synctest_pipelined_kernel<1><<<grid, kWave, 0, e->stream>>>(p); break;
@@ -732,7 +938,8 @@ int ggrs_synctest_advance_frames(ggrs_engine_t* e, int32_t n) {
 
 int ggrs_set_synctest_path(ggrs_engine_t* e, int32_t path) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
-  if (path != GGRS_PATH_PIPELINED && path != GGRS_PATH_SEQUENTIAL) return set_error(GGRS_E_INVALID, "unknown path %d", path);
+  if (path != GGRS_PATH_PIPELINED && path != GGRS_PATH_SEQUENTIAL && path != GGRS_PATH_PIPELINED_WHOLE)
+    return set_error(GGRS_E_INVALID, "unknown path %d", path);
   int rc = resolve(e);
   if (rc) return rc;
   e->path = path;

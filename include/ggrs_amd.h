@@ -65,8 +65,10 @@ extern "C" {
 #define GGRS_STATUS_DISCONNECTED 2
 
 /* SyncTest execution paths (ggrs_set_synctest_path) */
-#define GGRS_PATH_PIPELINED 0  /* default: cd+1 concurrent rollback chains per session */
-#define GGRS_PATH_SEQUENTIAL 1 /* one lane per session, calls in order */
+#define GGRS_PATH_PIPELINED 0       /* default: cd+1 concurrent rollback chains per session, one
+                                       lane per (chain, player) when (cd+1) * players <= 64 */
+#define GGRS_PATH_SEQUENTIAL 1      /* one lane per session, calls in order */
+#define GGRS_PATH_PIPELINED_WHOLE 2 /* pipelined, one lane per chain (all players in one lane) */
 
 /* per-lane status */
 #define GGRS_LANE_RUNNING 0
