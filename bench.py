@@ -52,7 +52,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames-per-step", type=int, default=128)
+    ap.add_argument("--frames-per-step", type=int, default=512)
     ap.add_argument("--lanes", type=int, default=4096, help="sessions per GPU (config 2: 4096)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores available)")
     ap.add_argument("--cpu-frames", type=int, default=100000, help="SyncTest frames per CPU thread")

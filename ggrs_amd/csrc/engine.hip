@@ -385,7 +385,11 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_split_kernel(PipePar
   const int32_t t_end = p.f0 + p.n + cd;
   int32_t i = ((p.f0 - j) % K + K) % K;
   const int row = nsess * Pp;  // staged bytes per frame
-  for (int32_t t = p.f0; t < t_end; ++t, i = (i + 1 == K ? 0 : i + 1)) {
+  // wave-uniform slot counters of frame gf = t - cd, advanced by one per step (no divisions)
+  int32_t slot_r = g0 % R;       // ring slot of frame gf
+  int32_t slot_k = g0 % K;       // chain slot (lane group) of chain gf
+  int32_t slot_t = p.trace_cap ? (p.f0 - K) % p.trace_cap : 0;  // trace slot of chain t - K (f0 >= K)
+  for (int32_t t = p.f0; t < t_end; ++t) {
     const int32_t c = t - i;
     const bool active = valid && c >= p.f0 && c < p.f0 + p.n;
     const int32_t gf = t - cd;
@@ -400,11 +404,39 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_split_kernel(PipePar
       __syncthreads();
     }
     const uint32_t in = lds_in[(rel & (kStageFrames - 1)) * row + g * Pp + pl];
+    // Fletcher-16 of the registers as they stand: the cell this chain saves now (i >= 1) or, on a
+    // lane about to start a chain (i == 0), the final state of the chain that ended last step --
+    // its display checksum (ex_game.rs:121-126).
+    const uint16_t ck = chain_fletcher<P, Pp>(frame, w, pl);
+    const uint16_t first_here = (uint16_t)__shfl((int)ck, base + slot_k * Pp, kWave);
     uint32_t from[6];
     from[0] = (uint32_t)__shfl((int)frame, src_prev, kWave);
 #pragma unroll
     for (int q = 0; q < 5; q++) from[q + 1] = (uint32_t)__shfl((int)w[q], src_prev, kWave);
-    if (i == 0) {  // LoadGameState(c - cd)
+    if (active && i > 0) {  // SaveGameState(gf)
+      uint32_t* cell = p.ring + (int64_t)slot_r * F * L + s;
+      if (owner) {
+        cell[kx * L] = w[0];
+        cell[ky * L] = w[1];
+        cell[kvx * L] = w[2];
+        cell[kvy * L] = w[3];
+        cell[krot * L] = w[4];
+      }
+      if (pl == 0) {
+        cell[0] = frame;
+        p.ring_ck[(int64_t)slot_r * L + s] = ck;
+        if (i < cd) {  // checksums_consistent(gf) at call c+1
+          const uint16_t first = gf >= p.f0 ? first_here : lds_first[rel * kWave + g];
+          if (ck != first) mask |= 1ull << (i - 1);
+        } else {
+          p.first_ck[(int64_t)slot_r * L + s] = ck;
+        }
+      }
+    }
+    if (i == 0) {
+      if (p.trace && valid && pl == 0 && c - K >= p.f0 && c - K < p.f0 + p.n)
+        p.trace[(int64_t)slot_t * L + s] = ck;
+      // LoadGameState(c - cd): the cell chain c-1 saves in this step (HBM for a launch's first chain)
       if (c == p.f0) {
         frame = lds_cell[wl * 6];
 #pragma unroll
@@ -416,29 +448,6 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_split_kernel(PipePar
       }
       if (s == p.corrupt_lane && c == p.corrupt_frame && pl == 0) w[0] ^= 1u;
       mask = 0;
-    }
-    const uint16_t ck = chain_fletcher<P, Pp>(frame, w, pl);
-    const int src_first = base + (((gf % K) + K) % K) * Pp;
-    const uint16_t first_here = (uint16_t)__shfl((int)ck, src_first, kWave);
-    if (active && i > 0) {  // SaveGameState(gf)
-      uint32_t* cell = p.ring + (int64_t)(gf % R) * F * L + s;
-      if (owner) {
-        cell[kx * L] = w[0];
-        cell[ky * L] = w[1];
-        cell[kvx * L] = w[2];
-        cell[kvy * L] = w[3];
-        cell[krot * L] = w[4];
-      }
-      if (pl == 0) {
-        cell[0] = frame;
-        p.ring_ck[(int64_t)(gf % R) * L + s] = ck;
-        if (i < cd) {  // checksums_consistent(gf) at call c+1
-          const uint16_t first = gf >= p.f0 ? first_here : lds_first[rel * kWave + g];
-          if (ck != first) mask |= 1ull << (i - 1);
-        } else {
-          p.first_ck[(int64_t)(gf % R) * L + s] = ck;
-        }
-      }
     }
     if (active) {  // AdvanceFrame with the input of frame gf
       frame = (uint32_t)((int32_t)frame + 1);
@@ -453,25 +462,30 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_split_kernel(PipePar
         w[3] = __builtin_bit_cast(uint32_t, vy);
         w[4] = __builtin_bit_cast(uint32_t, rot);
       }
-    }
-    if (p.trace) {  // uniform condition: the butterfly needs every lane
-      const uint16_t ck_new = chain_fletcher<P, Pp>(frame, w, pl);
-      if (active && i == cd && pl == 0) p.trace[(int64_t)(c % p.trace_cap) * L + s] = ck_new;
-    }
-    if (active && i == cd) {
-      if (c == p.f0 + p.n - 1) {
-        uint32_t* cur = p.cur + s;
-        if (owner) {
-          cur[kx * L] = w[0];
-          cur[ky * L] = w[1];
-          cur[kvx * L] = w[2];
-          cur[kvy * L] = w[3];
-          cur[krot * L] = w[4];
+      if (i == cd) {
+        if (c == p.f0 + p.n - 1) {
+          uint32_t* cur = p.cur + s;
+          if (owner) {
+            cur[kx * L] = w[0];
+            cur[ky * L] = w[1];
+            cur[kvx * L] = w[2];
+            cur[kvy * L] = w[3];
+            cur[krot * L] = w[4];
+          }
+          if (pl == 0) cur[0] = frame;
         }
-        if (pl == 0) cur[0] = frame;
+        if (pl == 0 && mask) atomicCAS(p.fail_f0, -1, p.f0);
       }
-      if (pl == 0 && mask) atomicCAS(p.fail_f0, -1, p.f0);
     }
+    i = i + 1 == K ? 0 : i + 1;
+    slot_r = slot_r + 1 == R ? 0 : slot_r + 1;
+    slot_k = slot_k + 1 == K ? 0 : slot_k + 1;
+    if (p.trace_cap) slot_t = slot_t + 1 == p.trace_cap ? 0 : slot_t + 1;
+  }
+  if (p.trace) {  // display checksum of the launch's last chain (it ended at the last step)
+    const uint16_t ck = chain_fletcher<P, Pp>(frame, w, pl);
+    const int32_t last = p.f0 + p.n - 1;
+    if (valid && pl == 0 && j == last % K) p.trace[(int64_t)(last % p.trace_cap) * L + s] = ck;
   }
 }
 

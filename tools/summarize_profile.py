@@ -36,7 +36,7 @@ def main(tag, workload, kernel="synctest_kernel"):
     avg_ns = float(stats[kname]["AverageNs"])
     out = {"tag": tag, "workload": workload, "kernel": kname, "calls": int(stats[kname]["Calls"]),
            "avg_duration_ns": avg_ns}
-    for group in ("pmc_fetch", "pmc_write", "pmc_sq"):
+    for group in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_grbm"):
         p = os.path.join(src, group, "pmc_counter_collection.csv")
         if os.path.exists(p):
             means, counts = pmc_means(p, kernel)
@@ -49,6 +49,17 @@ def main(tag, workload, kernel="synctest_kernel"):
     sq = out.get("pmc_sq", {})
     if sq.get("SQ_WAVES"):
         out["valu_insts_per_wave"] = sq["SQ_INSTS_VALU"] / sq["SQ_WAVES"]
+    if sq.get("SQ_WAVE_CYCLES"):
+        # SQ_WAVE_CYCLES / SQ_ACTIVE_* / SQ_WAIT_* count quad-cycles (MI355X_MICROARCH.md)
+        wc = sq["SQ_WAVE_CYCLES"]
+        out["valu_active_frac_of_wave_cycles"] = sq.get("SQ_ACTIVE_INST_VALU", 0) / wc
+        out["wait_inst_frac"] = sq.get("SQ_WAIT_INST_ANY", 0) / wc
+        out["wait_any_frac"] = sq.get("SQ_WAIT_ANY", 0) / wc
+        out["active_any_frac"] = sq.get("SQ_ACTIVE_INST_ANY", 0) / wc
+    gr = out.get("pmc_grbm", {})
+    if gr.get("GRBM_GUI_ACTIVE"):
+        # effective clock ~= GRBM_GUI_ACTIVE / 8 (summed over XCDs) / kernel time
+        out["effective_clock_ghz"] = gr["GRBM_GUI_ACTIVE"] / 8 / avg_ns
     with open(os.path.join(dst, "summary.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     if "hbm_bytes_per_launch" in out:
