@@ -8,4 +8,6 @@ from ._lib import GgrsError, InvalidRequest, PreconditionError, NULL_FRAME  # no
 from .session import (AdvanceFrame, BoxGameHandler, Engine, LoadGameState,  # noqa: F401
                       MismatchedChecksum, SaveGameState, SessionBuilder, SyncTestSession)
 
+from .branch import BranchEngine  # noqa: F401
+
 __version__ = "0.1.0"

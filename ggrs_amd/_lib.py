@@ -27,6 +27,11 @@ EXPORTS = (
     "ggrs_current_frame", "ggrs_read_mismatches", "ggrs_read_save_checksums", "ggrs_read_state",
     "ggrs_read_ring", "ggrs_read_trace", "ggrs_debug_corrupt_on_load", "ggrs_last_launch_ms",
     "ggrs_timing_reset", "ggrs_timing_read", "ggrs_set_synctest_path",
+    "ggrs_branch_engine_create", "ggrs_branch_engine_destroy", "ggrs_branch_engine_config",
+    "ggrs_branch_add_inputs", "ggrs_branch_speculate", "ggrs_branch_confirm",
+    "ggrs_branch_report_bytes", "ggrs_branch_synchronize", "ggrs_branch_trunk_frame",
+    "ggrs_branch_read_report", "ggrs_branch_read_desync", "ggrs_branch_read_trunk",
+    "ggrs_branch_read_lane", "ggrs_branch_timing_reset", "ggrs_branch_timing_read",
 )
 
 

@@ -1,0 +1,175 @@
+"""Speculative branch rollback (P2P) over the engine's C ABI (include/ggrs_amd.h, ggrs_branch_*).
+
+One BranchEngine holds S sessions x B branches.  Each round: speculate() replays the window from
+each session's confirmed trunk with the branch generator's remote inputs (P2PSession::
+adjust_gamestate, src/sessions/p2p_session.rs:658-714, with InputQueue prediction replaced), then
+confirm() applies the confirmed remote inputs of the trunk frame: the trunk advances, each lane
+learns whether its branch survived, and the per-session checksum + survival bits form the report
+that a multi-GPU run all-gathers (the ChecksumReport exchange, p2p_session.rs:939-975).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import InvalidRequest
+
+
+class BranchConfig(ctypes.Structure):
+    _fields_ = [
+        ("num_sessions", ctypes.c_int32),
+        ("num_players", ctypes.c_int32),
+        ("remote_mask", ctypes.c_int32),
+        ("window", ctypes.c_int32),
+        ("branches", ctypes.c_int32),
+        ("alphabet", ctypes.c_int32),
+        ("input_capacity", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+    ]
+
+
+_bound = False
+
+
+def _bind(L):
+    global _bound
+    if _bound:
+        return
+    vp = ctypes.c_void_p
+    P = ctypes.POINTER
+    L.ggrs_branch_engine_create.argtypes = [P(BranchConfig), P(vp)]
+    L.ggrs_branch_engine_destroy.argtypes = [vp]
+    L.ggrs_branch_engine_config.argtypes = [vp, P(BranchConfig)]
+    L.ggrs_branch_add_inputs.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp]
+    L.ggrs_branch_speculate.argtypes = [vp]
+    L.ggrs_branch_confirm.argtypes = [vp, vp]
+    L.ggrs_branch_report_bytes.argtypes = [vp, P(ctypes.c_int64)]
+    L.ggrs_branch_synchronize.argtypes = [vp]
+    L.ggrs_branch_trunk_frame.argtypes = [vp, P(ctypes.c_int32)]
+    L.ggrs_branch_read_report.argtypes = [vp, vp, vp]
+    L.ggrs_branch_read_desync.argtypes = [vp, vp]
+    L.ggrs_branch_read_trunk.argtypes = [vp, ctypes.c_int32, vp]
+    L.ggrs_branch_read_lane.argtypes = [vp, ctypes.c_int64, ctypes.c_int32, P(ctypes.c_uint16), vp]
+    L.ggrs_branch_timing_reset.argtypes = [vp]
+    L.ggrs_branch_timing_read.argtypes = [vp, P(ctypes.c_float), P(ctypes.c_int32)]
+    for name in _lib.EXPORTS:
+        if name.startswith("ggrs_branch_"):
+            getattr(L, name).restype = ctypes.c_int
+    _bound = True
+
+
+def _vp(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+class BranchEngine:
+    def __init__(self, num_sessions, num_players=2, remote_mask=0b10, window=4, branches=1,
+                 alphabet=16, input_capacity=0, device=0):
+        self._L = _lib.lib()
+        _bind(self._L)
+        cfg = BranchConfig(num_sessions, num_players, remote_mask, window, branches, alphabet,
+                           input_capacity, device)
+        h = ctypes.c_void_p()
+        _lib.check(self._L.ggrs_branch_engine_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+        self.num_sessions, self.num_players = num_sessions, num_players
+        self.remote_mask, self.window, self.branches, self.alphabet = remote_mask, window, branches, alphabet
+        self.num_lanes = num_sessions * branches
+        self.ring_len = window + 1
+        self.state_bytes = 36 + 20 * num_players
+        n = ctypes.c_int64()
+        _lib.check(self._L.ggrs_branch_report_bytes(self._h, ctypes.byref(n)))
+        self.report_bytes = n.value
+        self.report_ck_bytes = (2 * num_sessions + 7) & ~7
+        self.report_words = (self.num_lanes + 63) // 64
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.ggrs_branch_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add_inputs(self, first_frame, inputs):
+        a = np.ascontiguousarray(inputs, np.uint8)
+        if a.ndim != 3 or a.shape[1:] != (self.num_sessions, self.num_players):
+            raise InvalidRequest(-1, f"inputs must be [n][{self.num_sessions}][{self.num_players}]")
+        _lib.check(self._L.ggrs_branch_add_inputs(self._h, first_frame, a.shape[0], _vp(a)))
+
+    def speculate(self):
+        _lib.check(self._L.ggrs_branch_speculate(self._h))
+
+    def confirm(self, report_device_ptr=None):
+        ptr = ctypes.c_void_p(report_device_ptr) if report_device_ptr else None
+        _lib.check(self._L.ggrs_branch_confirm(self._h, ptr))
+
+    def synchronize(self):
+        _lib.check(self._L.ggrs_branch_synchronize(self._h))
+
+    def trunk_frame(self):
+        v = ctypes.c_int32()
+        _lib.check(self._L.ggrs_branch_trunk_frame(self._h, ctypes.byref(v)))
+        return v.value
+
+    def report(self):
+        ck = np.zeros(self.num_sessions, np.uint16)
+        bits = np.zeros(self.report_words, np.uint64)
+        _lib.check(self._L.ggrs_branch_read_report(self._h, _vp(ck), _vp(bits)))
+        return ck, bits
+
+    def survivors(self):
+        _, bits = self.report()
+        return unpack_bits(bits, self.num_lanes)
+
+    def desync(self):
+        out = np.zeros(self.num_sessions, np.int32)
+        _lib.check(self._L.ggrs_branch_read_desync(self._h, _vp(out)))
+        return out
+
+    def trunk(self, session):
+        out = np.zeros(self.state_bytes, np.uint8)
+        _lib.check(self._L.ggrs_branch_read_trunk(self._h, session, _vp(out)))
+        return out
+
+    def lane_state(self, lane, frame):
+        out = np.zeros(self.state_bytes, np.uint8)
+        ck = ctypes.c_uint16()
+        _lib.check(self._L.ggrs_branch_read_lane(self._h, lane, frame, ctypes.byref(ck), _vp(out)))
+        return int(ck.value), out
+
+    def timing_reset(self):
+        _lib.check(self._L.ggrs_branch_timing_reset(self._h))
+
+    def timing_read(self):
+        ms, n = ctypes.c_float(), ctypes.c_int32()
+        _lib.check(self._L.ggrs_branch_timing_read(self._h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    # ---- the branch generator, restated on the host for checking and scheduling
+    def assumed_remote(self, branch, k, last_confirmed):
+        """Remote inputs lane `branch` plays on speculated frame k, per player (None = local)."""
+        out = []
+        first_remote = next(q for q in range(self.num_players) if self.remote_mask >> q & 1)
+        E = 0
+        v = 1
+        while v < self.branches:
+            v *= self.alphabet
+            E += 1
+        for q in range(self.num_players):
+            if not self.remote_mask >> q & 1:
+                out.append(None)
+            elif q == first_remote and self.branches > 1:
+                kk = min(k, E - 1)
+                out.append((branch // self.alphabet ** kk) % self.alphabet)
+            else:
+                out.append(int(last_confirmed[q]))
+        return out
+
+
+def unpack_bits(words, n):
+    bits = np.unpackbits(np.ascontiguousarray(words, "<u8").view(np.uint8), bitorder="little")
+    return bits[:n].astype(bool)

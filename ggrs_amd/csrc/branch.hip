@@ -1,0 +1,489 @@
+// branch.hip -- speculative branch rollback: the P2P rollback replay (P2PSession::adjust_gamestate,
+// src/sessions/p2p_session.rs:658-714, + the save of the current frame, :337) for every
+// (session, branch) lane, with InputQueue prediction (src/input_queue.rs:104-167,
+// src/lib.rs:390-395) replaced by a branch generator:
+//   * B == 1: PredictRepeatLast -- every remote player plays its last confirmed input;
+//   * B == A^E: branch b assumes the first remote player plays digit_k = (b / A^k) % A on the
+//     k-th speculated frame (k < E; held at digit_{E-1} afterwards); other remote players repeat.
+// A round is speculate (each lane: Load the session trunk, W x (Advance, Save) into its own ring)
+// then confirm (the remote inputs of the trunk frame arrive: the trunk is replayed one frame with
+// them -- the rollback to first_incorrect GGRS performs -- and each lane learns whether its branch
+// survived, i.e. assumed exactly those inputs).  The next speculate checks that every surviving
+// lane's saved state for the new trunk frame has the trunk's checksum (desync detection).
+//
+// HBM layout (lane = session * B + branch, lane-fastest SoA):
+//   trunk    [F][S]     u32  confirmed state of each session at trunk_frame
+//   ring     [R][F][L]  u32  R = W + 1 saved states per lane, slot = frame % R
+//   ring_ck  [R][L]     u16
+//   inputs   [C][S][Pp] u8   true inputs of every player (remote ones are read only once confirmed)
+//   report   [S] u16 trunk checksum | pad | [ceil(L/64)] u64 survival bits  -- the all-gather payload
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+using namespace ggrs;
+
+namespace {
+
+struct SpecParams {
+  int64_t S, L;
+  int32_t B, W, R, A, E, cap, P;
+  int32_t f_c;          // trunk frame
+  uint32_t remote_mask; // bit p: player p is remote
+  int32_t first_remote; // index of the enumerated remote player (-1: none)
+  int32_t check_prev;   // 1: verify survivors of the previous confirm
+  const uint32_t* trunk;
+  uint32_t* ring;
+  uint16_t* ring_ck;
+  const uint8_t* inputs;
+  const uint64_t* prev_survive;  // survival bits of the previous confirm
+  const uint16_t* trunk_ck;      // checksum of the current trunk (previous confirm's report)
+  int32_t* desync;               // per session: first frame whose survivor disagreed, or -1
+};
+
+// The remote-input byte of branch b on speculated frame k for the enumerated player.
+__device__ inline uint32_t branch_digit(int32_t b, int32_t k, int32_t A, int32_t E) {
+  int32_t kk = k < E ? k : E - 1;
+  int32_t v = b;
+  for (int32_t q = 0; q < kk; q++) v /= A;
+  return (uint32_t)(v % A);
+}
+
+// Inputs lane (s, b) plays on frame f_c + k: local players from the queue, remote players
+// predicted.  GGRS predicts from the last input added to the player's queue (input_queue.rs:
+// 128-161), i.e. the confirmed input of frame f_c - 1, or the default input before frame 0.
+template <int P>
+__device__ inline uint32_t branch_inputs(const SpecParams& p, int64_t s, int32_t b, int32_t k) {
+  const uint32_t truth = load_inputs<P>(p.inputs, (int64_t)((p.f_c + k) % p.cap) * p.S + s);
+  const uint32_t last = p.f_c > 0 ? load_inputs<P>(p.inputs, (int64_t)((p.f_c - 1) % p.cap) * p.S + s) : 0u;
+  uint32_t in = 0;
+#pragma unroll
+  for (int q = 0; q < P; q++) {
+    uint32_t v;
+    if (!((p.remote_mask >> q) & 1u)) v = (truth >> (8 * q)) & 0xffu;          // local: confirmed
+    else if (q == p.first_remote && p.B > 1) v = branch_digit(b, k, p.A, p.E);  // enumerated
+    else v = (last >> (8 * q)) & 0xffu;                                         // repeat last
+    in |= v << (8 * q);
+  }
+  return in;
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void speculate_kernel(SpecParams p) {
+  const int64_t lane = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= p.L) return;
+  const int64_t s = lane / p.B;
+  const int32_t b = (int32_t)(lane - s * p.B);
+  constexpr int F = state_fields(P);
+  if (p.check_prev && ((p.prev_survive[lane >> 6] >> (lane & 63)) & 1ull)) {
+    // a surviving branch already saved the new trunk frame: it must match the replayed trunk
+    const uint16_t mine = p.ring_ck[(int64_t)(p.f_c % p.R) * p.L + lane];
+    if (mine != p.trunk_ck[s]) atomicCAS(&p.desync[s], -1, p.f_c);
+  }
+  BoxState<P> st;
+  load_state<P>(st, p.trunk + s, p.S);  // LoadGameState(f_c)
+  for (int32_t k = 0; k < p.W; ++k) {
+    advance_state<P>(st, branch_inputs<P>(p, s, b, k), 0u);  // AdvanceFrame(f_c + k)
+    const int32_t slot = (p.f_c + k + 1) % p.R;                 // SaveGameState(f_c + k + 1)
+    store_state<P>(st, p.ring + (int64_t)slot * F * p.L + lane, p.L);
+    p.ring_ck[(int64_t)slot * p.L + lane] = fletcher16_state<P>(st);
+  }
+}
+
+struct ConfirmParams {
+  int64_t S, L;
+  int32_t B, A, E, cap, P;
+  int32_t f_c;
+  uint32_t remote_mask;
+  int32_t first_remote;
+  uint32_t* trunk;
+  const uint8_t* inputs;
+  uint16_t* report_ck;   // [S]
+  uint64_t* report_bits; // [ceil(L/64)]
+};
+
+// The remote inputs of frame f_c have arrived.  Branch survival: the lane assumed exactly the
+// confirmed inputs for f_c (what add_input_by_frame checks, input_queue.rs:199-218).  Branch
+// lane 0 of each session replays frame f_c with them into the new trunk and reports its checksum.
+template <int P>
+__global__ __launch_bounds__(256) void confirm_kernel(ConfirmParams p) {
+  const int64_t lane = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool in_range = lane < p.L;
+  const int64_t s = in_range ? lane / p.B : 0;
+  const int32_t b = in_range ? (int32_t)(lane - s * p.B) : 0;
+  bool survive = false;
+  if (in_range) {
+    const uint32_t truth = load_inputs<P>(p.inputs, (int64_t)(p.f_c % p.cap) * p.S + s);
+    const uint32_t last = p.f_c > 0 ? load_inputs<P>(p.inputs, (int64_t)((p.f_c - 1) % p.cap) * p.S + s) : 0u;
+    survive = true;
+#pragma unroll
+    for (int q = 0; q < P; q++) {
+      if (!((p.remote_mask >> q) & 1u)) continue;
+      const uint32_t assumed = (q == p.first_remote && p.B > 1) ? branch_digit(b, 0, p.A, p.E)
+                                                                : (last >> (8 * q)) & 0xffu;
+      survive = survive && assumed == ((truth >> (8 * q)) & 0xffu);
+    }
+    if (b == 0) {
+      BoxState<P> st;
+      load_state<P>(st, p.trunk + s, p.S);
+      advance_state<P>(st, truth, 0u);
+      store_state<P>(st, p.trunk + s, p.S);
+      p.report_ck[s] = fletcher16_state<P>(st);
+    }
+  }
+  const uint64_t bits = __ballot(survive);
+  if (in_range && (threadIdx.x & 63) == 0) p.report_bits[lane >> 6] = bits;
+}
+
+}  // namespace
+
+struct ggrs_branch_engine {
+  ggrs_branch_config_t cfg{};
+  int Pp = 1, F = 1, R = 2, cap = 128, E = 0, first_remote = -1;
+  int64_t L = 0;
+  hipStream_t stream = nullptr;
+  uint32_t* trunk = nullptr;
+  uint32_t* ring = nullptr;
+  uint16_t* ring_ck = nullptr;
+  uint8_t* inputs = nullptr;
+  uint8_t* report = nullptr;  // report_bytes: [S] u16 | pad to 8 | [words] u64
+  size_t report_bytes = 0;
+  uint64_t* prev_bits = nullptr;
+  int32_t* desync = nullptr;
+  uint8_t* staging = nullptr;
+  size_t staging_bytes = 0;
+  int32_t trunk_frame = 0;
+  int32_t next_input_frame = 0;
+  bool have_prev = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::vector<hipEvent_t> tev;
+  size_t tev_used = 0;
+  bool collecting = false;
+};
+
+namespace {
+
+size_t report_ck_bytes(int64_t S) { return ((size_t)S * 2 + 7) & ~(size_t)7; }
+int64_t report_words(int64_t L) { return (L + 63) / 64; }
+
+template <typename K>
+int branch_launch_timed(ggrs_branch_engine* e, K&& launch) {
+  hipEvent_t a = e->ev0, b = e->ev1;
+  if (e->collecting) {
+    while (e->tev.size() < e->tev_used + 2) {
+      hipEvent_t ev;
+      HIP_TRY(hipEventCreate(&ev));
+      e->tev.push_back(ev);
+    }
+    a = e->tev[e->tev_used];
+    b = e->tev[e->tev_used + 1];
+    e->tev_used += 2;
+  }
+  HIP_TRY(hipEventRecord(a, e->stream));
+  launch();
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(b, e->stream));
+  return GGRS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ggrs_branch_engine_destroy(ggrs_branch_engine_t* e) {
+  if (!e) return GGRS_OK;
+  (void)hipSetDevice(e->cfg.device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  void* bufs[] = {e->trunk, e->ring, e->ring_ck, e->inputs, e->report, e->prev_bits, e->desync, e->staging};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  for (hipEvent_t ev : e->tev) (void)hipEventDestroy(ev);
+  if (e->ev0) (void)hipEventDestroy(e->ev0);
+  if (e->ev1) (void)hipEventDestroy(e->ev1);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+  return GGRS_OK;
+}
+
+int ggrs_branch_engine_create(const ggrs_branch_config_t* cfg, ggrs_branch_engine_t** out) {
+  if (!cfg || !out) return set_error(GGRS_E_INVALID, "null argument");
+  *out = nullptr;
+  const ggrs_branch_config_t c = *cfg;
+  if (c.num_sessions < 1) return set_error(GGRS_E_INVALID, "num_sessions must be >= 1");
+  if (c.num_players < 1 || c.num_players > 4) return set_error(GGRS_E_INVALID, "num_players must be in 1..4 (ex_game.rs:70)");
+  if ((c.remote_mask & ~((1 << c.num_players) - 1)) != 0 || c.remote_mask == 0)
+    return set_error(GGRS_E_INVALID, "remote_mask must name at least one of the session's players");
+  if (c.window < 1 || c.window > 62) return set_error(GGRS_E_INVALID, "window must be in 1..62");
+  if (c.branches < 1) return set_error(GGRS_E_INVALID, "branches must be >= 1");
+  if (c.alphabet < 2 || c.alphabet > 256) return set_error(GGRS_E_INVALID, "alphabet must be in 2..256");
+  int E = 0;
+  if (c.branches > 1) {
+    int64_t v = 1;
+    while (v < c.branches) { v *= c.alphabet; E++; }
+    if (v != c.branches) return set_error(GGRS_E_INVALID, "branches must be 1 or a power of the alphabet");
+    if (E > c.window) return set_error(GGRS_E_INVALID, "branches enumerate more frames than the window");
+  }
+  const int64_t L = (int64_t)c.num_sessions * c.branches;
+  if (L > ((int64_t)1 << 31)) return set_error(GGRS_E_INVALID, "too many lanes");
+  ggrs_branch_engine* e = new ggrs_branch_engine();
+  e->cfg = c;
+  e->L = L;
+  e->E = E;
+  e->Pp = padded_players(c.num_players);
+  e->F = state_fields(c.num_players);
+  e->R = c.window + 1;
+  e->cap = c.input_capacity ? c.input_capacity : 128;
+  e->cfg.input_capacity = e->cap;
+  for (int q = 0; q < c.num_players; q++)
+    if ((c.remote_mask >> q) & 1) { e->first_remote = q; break; }
+  if (e->cap < c.window + 2) {
+    delete e;
+    return set_error(GGRS_E_INVALID, "input_capacity must be >= window + 2");
+  }
+  auto fail = [&](int rc) {
+    std::string msg = ggrs_last_error();
+    ggrs_branch_engine_destroy(e);
+    set_error(rc, "%s", msg.c_str());
+    return rc;
+  };
+#define CTRY(expr)                                                                      \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) return fail(set_error(GGRS_E_HIP, "%s: %s", #expr, hipGetErrorString(e_))); \
+  } while (0)
+  const int64_t S = c.num_sessions;
+  CTRY(hipSetDevice(c.device));
+  CTRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+  CTRY(hipEventCreate(&e->ev0));
+  CTRY(hipEventCreate(&e->ev1));
+  CTRY(hipMalloc(&e->trunk, sizeof(uint32_t) * e->F * S));
+  CTRY(hipMalloc(&e->ring, sizeof(uint32_t) * (size_t)e->R * e->F * L));
+  CTRY(hipMalloc(&e->ring_ck, sizeof(uint16_t) * (size_t)e->R * L));
+  CTRY(hipMalloc(&e->inputs, (size_t)e->cap * S * e->Pp));
+  e->report_bytes = report_ck_bytes(S) + 8 * report_words(L);
+  CTRY(hipMalloc(&e->report, e->report_bytes));
+  CTRY(hipMalloc(&e->prev_bits, 8 * report_words(L)));
+  CTRY(hipMalloc(&e->desync, sizeof(int32_t) * S));
+  CTRY(hipMemsetAsync(e->ring, 0, sizeof(uint32_t) * (size_t)e->R * e->F * L, e->stream));
+  CTRY(hipMemsetAsync(e->ring_ck, 0, sizeof(uint16_t) * (size_t)e->R * L, e->stream));
+  CTRY(hipMemsetAsync(e->inputs, 0, (size_t)e->cap * S * e->Pp, e->stream));
+  CTRY(hipMemsetAsync(e->report, 0, e->report_bytes, e->stream));
+  CTRY(hipMemsetAsync(e->prev_bits, 0, 8 * report_words(L), e->stream));
+  CTRY(hipMemsetAsync(e->desync, 0xff, sizeof(int32_t) * S, e->stream));
+  dispatch_players(c.num_players, [&](auto PC) {
+    constexpr int P = decltype(PC)::value;
+    init_states_kernel<P><<<grid_of(S, 256), 256, 0, e->stream>>>(e->trunk, S);
+  });
+  CTRY(hipGetLastError());
+  CTRY(hipStreamSynchronize(e->stream));
+#undef CTRY
+  *out = e;
+  return GGRS_OK;
+}
+
+int ggrs_branch_engine_config(const ggrs_branch_engine_t* e, ggrs_branch_config_t* out) {
+  if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
+  *out = e->cfg;
+  return GGRS_OK;
+}
+
+int ggrs_branch_add_inputs(ggrs_branch_engine_t* e, int32_t first_frame, int32_t n, const uint8_t* inputs) {
+  if (!e || (!inputs && n > 0)) return set_error(GGRS_E_INVALID, "null argument");
+  if (n < 0) return set_error(GGRS_E_INVALID, "n_frames must be >= 0");
+  if (first_frame != e->next_input_frame)
+    return set_error(GGRS_E_INVALID, "inputs must be added sequentially (expected frame %d, got %d)",
+                     e->next_input_frame, first_frame);
+  if (n == 0) return GGRS_OK;
+  // the oldest frame still read is trunk_frame - 1 (the repeat-last prediction source)
+  if ((int64_t)first_frame + n - 1 - ((int64_t)e->trunk_frame - 1) >= e->cap)
+    return set_error(GGRS_E_INVALID, "input queue full (capacity %d)", e->cap);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const int64_t S = e->cfg.num_sessions;
+  const int P = e->cfg.num_players;
+  const size_t bytes = (size_t)n * S * P;
+  if (bytes > e->staging_bytes) {
+    if (e->staging) HIP_TRY(hipFree(e->staging));
+    e->staging = nullptr;
+    e->staging_bytes = 0;
+    HIP_TRY(hipMalloc(&e->staging, bytes));
+    e->staging_bytes = bytes;
+  }
+  HIP_TRY(hipMemcpyAsync(e->staging, inputs, bytes, hipMemcpyHostToDevice, e->stream));
+  pack_inputs_kernel<<<grid_of((int64_t)n * S, 256), 256, 0, e->stream>>>(e->staging, e->inputs, S, P, e->Pp, n,
+                                                                          first_frame % e->cap, e->cap);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  e->next_input_frame = first_frame + n;
+  return GGRS_OK;
+}
+
+int ggrs_branch_speculate(ggrs_branch_engine_t* e) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  const int32_t W = e->cfg.window;
+  if ((int64_t)e->trunk_frame + W - 1 >= e->next_input_frame)
+    return set_error(GGRS_E_INVALID, "local inputs for frames up to %d are not queued", e->trunk_frame + W - 1);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  SpecParams p;
+  p.S = e->cfg.num_sessions;
+  p.L = e->L;
+  p.B = e->cfg.branches;
+  p.W = W;
+  p.R = e->R;
+  p.A = e->cfg.alphabet;
+  p.E = e->E;
+  p.cap = e->cap;
+  p.P = e->cfg.num_players;
+  p.f_c = e->trunk_frame;
+  p.remote_mask = (uint32_t)e->cfg.remote_mask;
+  p.first_remote = e->first_remote;
+  p.check_prev = e->have_prev ? 1 : 0;
+  p.trunk = e->trunk;
+  p.ring = e->ring;
+  p.ring_ck = e->ring_ck;
+  p.inputs = e->inputs;
+  p.prev_survive = e->prev_bits;
+  p.trunk_ck = (const uint16_t*)e->report;
+  p.desync = e->desync;
+  return branch_launch_timed(e, [&] {
+    dispatch_players(p.P, [&](auto PC) {
+      constexpr int P = decltype(PC)::value;
+      speculate_kernel<P><<<grid_of(p.L, 256), 256, 0, e->stream>>>(p);
+    });
+  });
+}
+
+int ggrs_branch_confirm(ggrs_branch_engine_t* e, void* report_device) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  if (e->trunk_frame >= e->next_input_frame)
+    return set_error(GGRS_E_INVALID, "inputs of frame %d are not queued", e->trunk_frame);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  ConfirmParams p;
+  p.S = e->cfg.num_sessions;
+  p.L = e->L;
+  p.B = e->cfg.branches;
+  p.A = e->cfg.alphabet;
+  p.E = e->E;
+  p.cap = e->cap;
+  p.P = e->cfg.num_players;
+  p.f_c = e->trunk_frame;
+  p.remote_mask = (uint32_t)e->cfg.remote_mask;
+  p.first_remote = e->first_remote;
+  p.trunk = e->trunk;
+  p.inputs = e->inputs;
+  p.report_ck = (uint16_t*)e->report;
+  p.report_bits = (uint64_t*)(e->report + report_ck_bytes(p.S));
+  int rc = branch_launch_timed(e, [&] {
+    dispatch_players(p.P, [&](auto PC) {
+      constexpr int P = decltype(PC)::value;
+      confirm_kernel<P><<<grid_of(p.L, 256), 256, 0, e->stream>>>(p);
+    });
+  });
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(e->prev_bits, p.report_bits, 8 * report_words(p.L), hipMemcpyDeviceToDevice, e->stream));
+  if (report_device)
+    HIP_TRY(hipMemcpyAsync(report_device, e->report, e->report_bytes, hipMemcpyDeviceToDevice, e->stream));
+  e->trunk_frame += 1;
+  e->have_prev = true;
+  return GGRS_OK;
+}
+
+int ggrs_branch_report_bytes(const ggrs_branch_engine_t* e, int64_t* out) {
+  if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
+  *out = (int64_t)e->report_bytes;
+  return GGRS_OK;
+}
+
+int ggrs_branch_synchronize(ggrs_branch_engine_t* e) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return GGRS_OK;
+}
+
+int ggrs_branch_trunk_frame(const ggrs_branch_engine_t* e, int32_t* out) {
+  if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
+  *out = e->trunk_frame;
+  return GGRS_OK;
+}
+
+int ggrs_branch_read_report(ggrs_branch_engine_t* e, uint16_t* checksums, uint64_t* survive_bits) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const int64_t S = e->cfg.num_sessions;
+  if (checksums) HIP_TRY(hipMemcpyAsync(checksums, e->report, 2 * S, hipMemcpyDeviceToHost, e->stream));
+  if (survive_bits)
+    HIP_TRY(hipMemcpyAsync(survive_bits, e->report + report_ck_bytes(S), 8 * report_words(e->L),
+                           hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return GGRS_OK;
+}
+
+int ggrs_branch_read_desync(ggrs_branch_engine_t* e, int32_t* first_frame) {
+  if (!e || !first_frame) return set_error(GGRS_E_INVALID, "null argument");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipMemcpyAsync(first_frame, e->desync, 4 * e->cfg.num_sessions, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return GGRS_OK;
+}
+
+int ggrs_branch_read_trunk(ggrs_branch_engine_t* e, int32_t session, uint8_t* out) {
+  if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
+  if (session < 0 || session >= e->cfg.num_sessions) return set_error(GGRS_E_INVALID, "session out of range");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  std::vector<uint32_t> w(e->F);
+  for (int k = 0; k < e->F; k++)
+    HIP_TRY(hipMemcpyAsync(&w[k], e->trunk + (size_t)k * e->cfg.num_sessions + session, 4, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  serialize_state_bytes(w.data(), e->cfg.num_players, out);
+  return GGRS_OK;
+}
+
+int ggrs_branch_read_lane(ggrs_branch_engine_t* e, int64_t lane, int32_t frame, uint16_t* checksum, uint8_t* out) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  if (lane < 0 || lane >= e->L) return set_error(GGRS_E_INVALID, "lane out of range");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const int slot = ((frame % e->R) + e->R) % e->R;
+  std::vector<uint32_t> w(e->F);
+  for (int k = 0; k < e->F; k++)
+    HIP_TRY(hipMemcpyAsync(&w[k], e->ring + ((size_t)slot * e->F + k) * e->L + lane, 4, hipMemcpyDeviceToHost, e->stream));
+  uint16_t ck = 0;
+  HIP_TRY(hipMemcpyAsync(&ck, e->ring_ck + (size_t)slot * e->L + lane, 2, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (checksum) *checksum = ck;
+  if (out) serialize_state_bytes(w.data(), e->cfg.num_players, out);
+  return GGRS_OK;
+}
+
+int ggrs_branch_timing_reset(ggrs_branch_engine_t* e) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  e->tev_used = 0;
+  e->collecting = true;
+  return GGRS_OK;
+}
+
+int ggrs_branch_timing_read(ggrs_branch_engine_t* e, float* total_ms, int32_t* launches) {
+  if (!e || !total_ms || !launches) return set_error(GGRS_E_INVALID, "null argument");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  float sum = 0.0f;
+  for (size_t i = 0; i + 1 < e->tev_used; i += 2) {
+    float ms = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&ms, e->tev[i], e->tev[i + 1]));
+    sum += ms;
+  }
+  *total_ms = sum;
+  *launches = (int32_t)(e->tev_used / 2);
+  e->collecting = false;
+  e->tev_used = 0;
+  return GGRS_OK;
+}
+
+}  // extern "C"

@@ -25,14 +25,13 @@
 #include <string>
 #include <vector>
 
-#include "ggrs_amd.h"
-#include "box_game.h"
+#include "common.h"
 
 #pragma clang fp contract(off)
 
 using namespace ggrs;
 
-namespace {
+namespace ggrs {
 
 thread_local std::string g_last_error;
 
@@ -46,74 +45,11 @@ int set_error(int code, const char* fmt, ...) {
   return code;
 }
 
-#define HIP_TRY(expr)                                                                       \
-  do {                                                                                      \
-    hipError_t e_ = (expr);                                                                 \
-    if (e_ != hipSuccess) return set_error(GGRS_E_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
-  } while (0)
+}  // namespace ggrs
 
-constexpr int kWave = 64;
-
-inline int padded_players(int p) { return p <= 1 ? 1 : (p == 2 ? 2 : 4); }
-
-// ------------------------------------------------------------------------------ device helpers
-template <int P>
-struct InputWord;
-template <>
-struct InputWord<1> { using T = uint8_t; };
-template <>
-struct InputWord<2> { using T = uint16_t; };
-template <>
-struct InputWord<3> { using T = uint32_t; };
-template <>
-struct InputWord<4> { using T = uint32_t; };
-
-template <int P>
-__device__ inline uint32_t load_inputs(const uint8_t* base, int64_t idx) {
-  using T = typename InputWord<P>::T;
-  return (uint32_t)reinterpret_cast<const T*>(base)[idx];
-}
-
-template <int P>
-__device__ inline void load_state(BoxState<P>& s, const uint32_t* base, int64_t L) {
-#pragma unroll
-  for (int k = 0; k < state_fields(P); k++) s.w[k] = base[k * L];
-}
-template <int P>
-__device__ inline void store_state(const BoxState<P>& s, uint32_t* base, int64_t L) {
-#pragma unroll
-  for (int k = 0; k < state_fields(P); k++) base[k * L] = s.w[k];
-}
-
-// exact fmod for |a| < 2|b| (Sterbenz), library fmodf otherwise
-__device__ inline float fmod_exact(float a, float b) {
-  float aa = __builtin_fabsf(a), ab = __builtin_fabsf(b);
-  if (aa < ab) return a;
-  if (aa < 2.0f * ab) return __builtin_copysignf(aa - ab, a);
-  return fmodf(a, b);
-}
+namespace {
 
 // ------------------------------------------------------------------------------ kernels
-// State::new(P) for every lane (ex_game.rs:246-269)
-template <int P>
-__global__ __launch_bounds__(256) void init_states_kernel(uint32_t* cur, int64_t L) {
-  const int64_t lane = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (lane >= L) return;
-  BoxState<P> s;
-  s.w[0] = 0;
-  const float r = kWindowWidth / 4.0f;
-#pragma unroll
-  for (int i = 0; i < P; i++) {
-    float rot = (float)i / (float)P * 2.0f * kPi;
-    s.set(fld_x(P, i), kWindowWidth / 2.0f + r * glibc_cosf(rot));
-    s.set(fld_y(P, i), kWindowHeight / 2.0f + r * glibc_sinf(rot));
-    s.set(fld_vx(P, i), 0.0f);
-    s.set(fld_vy(P, i), 0.0f);
-    s.set(fld_rot(P, i), fmod_exact(rot + kPi, 2.0f * kPi));
-  }
-  store_state<P>(s, cur + lane, L);
-}
-
 struct SyncTestParams {
   int64_t L;
   int32_t R, cd, f0, n, cap, trace_cap;
@@ -546,16 +482,6 @@ __global__ __launch_bounds__(kWave) void requests_kernel(RequestParams p) {
   store_state<P>(s, p.cur + lane, L);
 }
 
-// Repack [n][L][P] user inputs into the [C][L][Pp] queue at queue frames q0.. (wrapping).
-__global__ void pack_inputs_kernel(const uint8_t* src, uint8_t* dst, int64_t L, int32_t P,
-                                   int32_t Pp, int32_t n, int32_t q0, int32_t cap) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (int64_t)n * L) return;
-  const int64_t fr = i / L, lane = i % L;
-  const int64_t q = ((int64_t)q0 + fr) % cap;
-  for (int k = 0; k < Pp; k++) dst[(q * L + lane) * Pp + k] = k < P ? src[i * P + k] : 0;
-}
-
 }  // namespace
 
 // ------------------------------------------------------------------------------ engine object
@@ -637,8 +563,6 @@ int launch_timed(ggrs_engine* e, K&& launch) {
   e->timed = true;
   return GGRS_OK;
 }
-
-int64_t grid_of(int64_t n, int64_t block) { return (n + block - 1) / block; }
 
 }  // namespace
 
@@ -1084,21 +1008,6 @@ int ggrs_read_save_checksums(ggrs_engine_t* e, int32_t frame, uint16_t* out) {
   return GGRS_OK;
 }
 
-static void serialize_state(const uint32_t* w, int P, uint8_t* out) {
-  // bincode: i32 frame, u64 P, u64 P + (x,y)*P, u64 P + (vx,vy)*P, u64 P + rot*P
-  uint8_t* o = out;
-  auto u32 = [&](uint32_t v) { memcpy(o, &v, 4); o += 4; };
-  auto u64 = [&](uint64_t v) { memcpy(o, &v, 8); o += 8; };
-  u32(w[0]);
-  u64((uint64_t)P);
-  u64((uint64_t)P);
-  for (int k = 1; k <= 2 * P; k++) u32(w[k]);
-  u64((uint64_t)P);
-  for (int k = 2 * P + 1; k <= 4 * P; k++) u32(w[k]);
-  u64((uint64_t)P);
-  for (int k = 4 * P + 1; k <= 5 * P; k++) u32(w[k]);
-}
-
 static int gather_lane(ggrs_engine_t* e, const uint32_t* base, int32_t lane, uint32_t* w) {
   const size_t L = e->cfg.num_lanes;
   for (int k = 0; k < e->F; k++)
@@ -1115,7 +1024,7 @@ int ggrs_read_state(ggrs_engine_t* e, int32_t lane, uint8_t* out) {
   int rc = gather_lane(e, e->cur, lane, w);
   if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(e->stream));
-  serialize_state(w, e->cfg.num_players, out);
+  serialize_state_bytes(w, e->cfg.num_players, out);
   return GGRS_OK;
 }
 
@@ -1139,7 +1048,7 @@ int ggrs_read_ring(ggrs_engine_t* e, int32_t lane, int32_t* frames, uint16_t* ck
     if (frames) frames[s] = e->ring_tag[s];
     if (cks) cks[s] = has ? c[s] : 0;
     if (states) {
-      if (has) serialize_state(&w[(size_t)s * e->F], e->cfg.num_players, states + (size_t)s * sb);
+      if (has) serialize_state_bytes(&w[(size_t)s * e->F], e->cfg.num_players, states + (size_t)s * sb);
       else memset(states + (size_t)s * sb, 0, sb);
     }
   }

@@ -154,6 +154,58 @@ int ggrs_last_launch_ms(ggrs_engine_t* eng, float* ms);
 int ggrs_timing_reset(ggrs_engine_t* eng);
 int ggrs_timing_read(ggrs_engine_t* eng, float* total_ms, int32_t* launches);
 
+/* ---------------------------------------------------------------------------------------------
+ * Speculative branch rollback (P2P).  Lane = (session, branch), lane = session * branches + branch.
+ * A round = ggrs_branch_speculate (every lane: LoadGameState(trunk frame) of its session, then
+ * window x (AdvanceFrame, SaveGameState) -- P2PSession::adjust_gamestate, p2p_session.rs:658-714,
+ * plus the save of the current frame, :337 -- with the remote players' inputs from the branch
+ * generator that replaces InputQueue prediction, input_queue.rs:104-167) followed by
+ * ggrs_branch_confirm (the remote inputs of the trunk frame arrive: the trunk replays that frame
+ * with them, every lane learns whether its branch survived -- assumed exactly those inputs,
+ * input_queue.rs:199-218 -- and the per-session checksum + survival bits form the report that
+ * multi-GPU runs all-gather, the ChecksumReport exchange of p2p_session.rs:939-975).
+ */
+typedef struct ggrs_branch_config {
+  int32_t num_sessions;   /* S >= 1 */
+  int32_t num_players;    /* 1..4 */
+  int32_t remote_mask;    /* bit p: player p is remote (inputs confirmed late); others local */
+  int32_t window;         /* W: frames speculated per round (1..62); ring = W + 1 saved states */
+  int32_t branches;       /* B per session: 1 = PredictRepeatLast (lib.rs:390-395); A^E =
+                             enumerate the first remote player over E frames, then hold */
+  int32_t alphabet;       /* A: remote input values enumerated (16 for ex_game's 4 buttons) */
+  int32_t input_capacity; /* frames of queued inputs per session; 0 = 128 */
+  int32_t device;
+} ggrs_branch_config_t;
+
+typedef struct ggrs_branch_engine ggrs_branch_engine_t;
+
+int ggrs_branch_engine_create(const ggrs_branch_config_t* cfg, ggrs_branch_engine_t** out);
+int ggrs_branch_engine_destroy(ggrs_branch_engine_t* eng);
+int ggrs_branch_engine_config(const ggrs_branch_engine_t* eng, ggrs_branch_config_t* out);
+/* True inputs of every player for frames [first_frame, first_frame + n_frames):
+ * [n_frames][num_sessions][num_players].  Remote players' values are only read once the frame
+ * is confirmed (and as the repeat-last prediction source for later frames). */
+int ggrs_branch_add_inputs(ggrs_branch_engine_t* eng, int32_t first_frame, int32_t n_frames,
+                           const uint8_t* inputs);
+int ggrs_branch_speculate(ggrs_branch_engine_t* eng);
+/* Confirm the trunk frame; if report_device != NULL the round's report is also copied there
+ * (device pointer, ggrs_branch_report_bytes bytes: [S] u16 checksums, padded to 8 bytes, then
+ * ceil(L/64) u64 survival words) on the engine's stream. */
+int ggrs_branch_confirm(ggrs_branch_engine_t* eng, void* report_device);
+int ggrs_branch_report_bytes(const ggrs_branch_engine_t* eng, int64_t* out);
+int ggrs_branch_synchronize(ggrs_branch_engine_t* eng);
+int ggrs_branch_trunk_frame(const ggrs_branch_engine_t* eng, int32_t* out);
+int ggrs_branch_read_report(ggrs_branch_engine_t* eng, uint16_t* checksums, uint64_t* survive_bits);
+/* per session: first trunk frame at which a surviving branch's saved state disagreed with the
+ * replayed trunk (a desync), or -1 */
+int ggrs_branch_read_desync(ggrs_branch_engine_t* eng, int32_t* first_frame);
+int ggrs_branch_read_trunk(ggrs_branch_engine_t* eng, int32_t session, uint8_t* out);
+/* the saved state (bincode) and checksum of `frame` in one lane's ring */
+int ggrs_branch_read_lane(ggrs_branch_engine_t* eng, int64_t lane, int32_t frame, uint16_t* checksum,
+                          uint8_t* out);
+int ggrs_branch_timing_reset(ggrs_branch_engine_t* eng);
+int ggrs_branch_timing_read(ggrs_branch_engine_t* eng, float* total_ms, int32_t* launches);
+
 #ifdef __cplusplus
 }
 #endif

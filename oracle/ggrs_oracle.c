@@ -817,3 +817,51 @@ void oracle_input_queue_sequence(int32_t delay, int32_t n, const int32_t* frames
     if (do_read) { uint8_t st; read[i] = iq_input(&q, frames[i], &st); }
   }
 }
+
+/* ---------------------------------------------------------------- P2P rollback replay
+ * P2PSession::adjust_gamestate (p2p_session.rs:658-714, non-sparse) followed by the save of the
+ * current frame (:337), executed by the ex_game handler.  The session's ring holds the cell of
+ * load_frame (state_in, saved as that frame); current frame = load_frame + count; the inputs the
+ * replay requests per frame are given explicitly (inputs[count][P], status[count][P]) -- they are
+ * what synchronized_inputs returns once InputQueue has confirmed or predicted them.
+ * Outputs the saved cells of frames load_frame+1 .. load_frame+count (states + checksums). */
+int oracle_p2p_replay(int32_t P, const uint8_t* state_in, int32_t load_frame, int32_t count,
+                      int32_t max_prediction, const uint8_t* inputs, const uint8_t* status,
+                      uint8_t* out_states, uint16_t* out_cksums, uint8_t* final_state) {
+  if (count < 1 || count > max_prediction) return -1;
+  SyncLayer sl;
+  sl_new(&sl, (size_t)P, (size_t)max_prediction, PREDICT_REPEAT_LAST);
+  Game g; memset(&g, 0, sizeof g);
+  state_from_bytes(&g.game_state, state_in);
+  ORACLE_ASSERT(g.game_state.frame == load_frame, "state_in frame != load_frame");
+  /* the cell of load_frame was saved when the session passed it */
+  sl.current_frame = load_frame;
+  RequestVec rv = {0};
+  rv_push(&rv, sl_save_current_state(&sl));
+  game_handle_requests(&g, &sl, &rv, 0);
+  sl.current_frame = load_frame + count;
+  /* adjust_gamestate */
+  rv.n = 0;
+  rv_push(&rv, sl_load_frame(&sl, load_frame));
+  for (int32_t i = 0; i < count; i++) {
+    Request adv; memset(&adv, 0, sizeof adv); adv.kind = REQ_ADVANCE;
+    for (int32_t p = 0; p < P; p++) { adv.inputs[p] = inputs[i * P + p]; adv.status[p] = status ? status[i * P + p] : 0; }
+    if (i > 0) rv_push(&rv, sl_save_current_state(&sl));
+    sl.current_frame += 1;
+    rv_push(&rv, adv);
+  }
+  rv_push(&rv, sl_save_current_state(&sl)); /* advance_frame: save the current frame (:337) */
+  game_handle_requests(&g, &sl, &rv, 0);
+  size_t sb = 36 + 20 * (size_t)P;
+  for (int32_t k = 1; k <= count; k++) {
+    const Cell* c = sl_saved_state_by_frame(&sl, load_frame + k);
+    ORACLE_ASSERT(c && c->has_data, "missing saved cell");
+    if (out_states) oracle_state_serialize(&c->data, out_states + (size_t)(k - 1) * sb);
+    if (out_cksums) out_cksums[k - 1] = c->checksum;
+  }
+  if (final_state) oracle_state_serialize(&g.game_state, final_state);
+  free(rv.v);
+  state_free(&g.game_state);
+  sl_free(&sl);
+  return 0;
+}

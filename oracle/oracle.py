@@ -80,6 +80,9 @@ def lib():
                                             ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, u16p,
                                             P(ctypes.c_double)]
         L.oracle_synctest_bench.restype = ctypes.c_int64
+        L.oracle_p2p_replay.argtypes = [ctypes.c_int32, u8p, ctypes.c_int32, ctypes.c_int32,
+                                         ctypes.c_int32, u8p, u8p, u8p, u16p, u8p]
+        L.oracle_p2p_replay.restype = ctypes.c_int
         L.oracle_input_queue_sequence.argtypes = [ctypes.c_int32, ctypes.c_int32, i32p, u8p,
                                                   ctypes.c_int, i32p, u8p, i32p]
         _lib = L
@@ -168,6 +171,27 @@ def input_queue_sequence(delay, frames, inputs, read=True):
                                       1 if read else 0, _ptr(added, ctypes.c_int32),
                                       _ptr(got, ctypes.c_uint8), _ptr(length, ctypes.c_int32))
     return added, got, length
+
+
+def p2p_replay(state, load_frame, inputs, max_prediction=None, status=None):
+    """P2PSession::adjust_gamestate from `state` (the cell of load_frame) over len(inputs) frames
+    + the save of the current frame; returns (saved states [count][sb], checksums [count], final)."""
+    state = np.ascontiguousarray(state, np.uint8)
+    P = (state.size - 36) // 20
+    inp = np.ascontiguousarray(inputs, np.uint8).reshape(-1, P)
+    count = inp.shape[0]
+    st = None if status is None else np.ascontiguousarray(status, np.uint8).reshape(-1, P)
+    mp = max_prediction or count
+    states = np.zeros((count, state.size), np.uint8)
+    cks = np.zeros(count, np.uint16)
+    final = np.zeros(state.size, np.uint8)
+    rc = lib().oracle_p2p_replay(P, _ptr(state, ctypes.c_uint8), load_frame, count, mp,
+                                 _ptr(inp, ctypes.c_uint8), _ptr(st, ctypes.c_uint8),
+                                 _ptr(states, ctypes.c_uint8), _ptr(cks, ctypes.c_uint16),
+                                 _ptr(final, ctypes.c_uint8))
+    if rc != 0:
+        raise ValueError("bad p2p replay arguments")
+    return states, cks, final
 
 
 def sincos_digest(lo, hi, threads=8):

@@ -1,0 +1,97 @@
+"""GPU parity of the speculative branch rollback (ggrs_branch_*): every lane's replay equals the
+oracle's P2PSession::adjust_gamestate (p2p_session.rs:658-714 + the save at :337) run with that
+branch's inputs; the trunk equals the confirmed-input replay; survival bits equal "assumed the
+confirmed inputs"; the report checksum is fletcher16 of the confirmed state.  Bit-exact."""
+import numpy as np
+import pytest
+
+# torch (plumbing for device buffers / RCCL) must load its bundled HIP runtime before the engine
+# library: both link libamdhip64.so.7, and whichever loads first serves the process.  bench.py
+# imports torch first for the same reason.
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+
+def branch_inputs(eng, truth, f_c, lane, W):
+    """[W][P] inputs lane `lane` plays from trunk frame f_c (host restatement of the generator)."""
+    s, b = divmod(lane, eng.branches)
+    last = truth[f_c - 1, s] if f_c > 0 else np.zeros(eng.num_players, np.uint8)
+    rows = []
+    for k in range(W):
+        assumed = eng.assumed_remote(b, k, last)
+        rows.append([truth[f_c + k, s, q] if a is None else a for q, a in enumerate(assumed)])
+    return np.array(rows, np.uint8)
+
+
+def run_rounds(oracle, eng, truth, rounds, lanes_to_check):
+    S, P, W = eng.num_sessions, eng.num_players, eng.window
+    trunks = {s: oracle.state_new(P) for s in set(l // eng.branches for l in lanes_to_check) | {0}}
+    for r in range(rounds):
+        f_c = eng.trunk_frame()
+        assert f_c == r
+        eng.speculate()
+        eng.synchronize()
+        for lane in lanes_to_check:
+            s = lane // eng.branches
+            states, cks, _ = oracle.p2p_replay(trunks[s], f_c, branch_inputs(eng, truth, f_c, lane, W))
+            for k in range(W):
+                ck, st = eng.lane_state(lane, f_c + k + 1)
+                assert ck == int(cks[k]) and bytes(st) == bytes(states[k]), (lane, r, k)
+        eng.confirm()
+        ck, bits = eng.report()
+        surv = eng.survivors()
+        for s in trunks:
+            trunks[s] = oracle.state_advance(trunks[s], truth[f_c, s])
+            assert bytes(eng.trunk(s)) == bytes(trunks[s])
+            assert int(ck[s]) == oracle.fletcher16(bytes(trunks[s]))
+        for lane in lanes_to_check:
+            s, b = divmod(lane, eng.branches)
+            want = branch_inputs(eng, truth, f_c, lane, 1)[0]
+            assert surv[lane] == bool((want == truth[f_c, s]).all()), (lane, r)
+    assert (eng.desync() == -1).all()
+
+
+def test_config3_enumeration(oracle):
+    """Config 3: 1 session x 16^4 branches over a 4-frame window, 2 players (1 remote)."""
+    from ggrs_amd import BranchEngine, synth
+    eng = BranchEngine(1, num_players=2, remote_mask=0b10, window=4, branches=16 ** 4, alphabet=16)
+    rounds = 6
+    truth = synth.gen_inputs(0, 1, rounds + 8, 2, synth.MODEL_HELD)
+    eng.add_inputs(0, truth)
+    rng = np.random.default_rng(3)
+    lanes = sorted(set([0, 1, 15, 16, 255, 4096, 65535] + rng.integers(0, 65536, 10).tolist()))
+    run_rounds(oracle, eng, truth, rounds, lanes)
+    # exactly the 16^3 branches whose digit 0 matched the confirmed input survive each round
+    surv = eng.survivors()
+    assert surv.sum() == 16 ** 3
+
+
+@pytest.mark.parametrize("branches,window,P,mask", [(1, 8, 4, 0b1110), (16, 8, 4, 0b0010), (16, 3, 2, 0b01),
+                                                    (256, 5, 3, 0b110)])
+def test_generators_many_sessions(oracle, branches, window, P, mask):
+    from ggrs_amd import BranchEngine, synth
+    S = 300
+    eng = BranchEngine(S, num_players=P, remote_mask=mask, window=window, branches=branches, alphabet=16)
+    rounds = 5
+    truth = synth.gen_inputs(7, S, rounds + window + 2, P, synth.MODEL_HELD)
+    eng.add_inputs(0, truth)
+    L = S * branches
+    lanes = sorted(set([0, 1, branches, L - 1, L // 2, 63, 64]))
+    run_rounds(oracle, eng, truth, rounds, lanes)
+
+
+def test_report_to_device_buffer(oracle):
+    """confirm() can copy the report into a caller-owned device buffer (the all-gather input)."""
+    from ggrs_amd import BranchEngine, synth
+    eng = BranchEngine(100, num_players=2, remote_mask=0b10, window=4, branches=16, alphabet=16)
+    truth = synth.gen_inputs(0, 100, 20, 2)
+    eng.add_inputs(0, truth)
+    buf = torch.zeros(eng.report_bytes, dtype=torch.uint8, device="cuda")
+    eng.speculate()
+    eng.confirm(buf.data_ptr())
+    eng.synchronize()
+    host = buf.cpu().numpy()
+    ck, bits = eng.report()
+    assert (host[:200].view(np.uint16) == ck).all()
+    assert (host[eng.report_ck_bytes:].view(np.uint64) == bits).all()
