@@ -13,6 +13,13 @@ data-path collective (SyncTest has no exchange step), so scaling is weak and `va
 of all ranks' resimulated session-frames over the max-over-ranks wall time.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--frames-per-step F]
+    python bench.py --config 3|4 ...   # speculative branch rollback
+
+Configs 3 and 4 (branch engine): a step is one round -- speculate (every (session, branch) lane
+replays the window from its session's confirmed trunk with the branch generator's remote inputs)
+then confirm (the trunk replays the confirmed frame; survival bits and checksums form the report)
+and, with more than one rank, the RCCL all-gather of the reports.  Resimulated session-frames per
+round = lanes x window + sessions.
 """
 import argparse
 import json
@@ -47,6 +54,116 @@ def pmc_traffic(workload):
         return None
 
 
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and rank == 0:
+        print(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world} rank(s)", file=sys.stderr)
+    import torch  # before the engine: torch's bundled HIP runtime must serve the process
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    return world, rank, local_rank, torch, dist
+
+
+BRANCH_CONFIGS = {
+    # sessions per GPU, branches, players, remote mask, window
+    3: dict(sessions=1, branches=16 ** 4, players=2, remote_mask=0b10, window=4,
+            text="config3: 1 session x 65,536 branches (16^4 remote-input sequences over a 4-frame "
+                 "window), 2 players, speculate + confirm per round"),
+    4: dict(sessions=8192, branches=16, players=4, remote_mask=0b1110, window=8,
+            text="config4: 4-player P2P, 8192 sessions x 16 branches = 131,072 lanes per GPU, "
+                 "window 8, RCCL all-gather of checksums + survival bits per confirmation"),
+}
+
+
+def run_branch(args):
+    world, rank, local_rank, torch, dist = setup_dist(args)
+    from ggrs_amd import BranchEngine, exchange, synth
+    c = BRANCH_CONFIGS[args.config]
+    S, B, P, W = c["sessions"], c["branches"], c["players"], c["window"]
+    rounds = args.warmup + args.steps
+    group = rank % (world // 2) if (args.peers and world >= 2) else rank
+    truth = synth.gen_inputs(group * S, S, rounds + W + 1, P, synth.MODEL_HELD)
+    eng = BranchEngine(S, num_players=P, remote_mask=c["remote_mask"], window=W, branches=B,
+                       alphabet=16, input_capacity=rounds + W + 3, device=local_rank)
+    eng.add_inputs(0, truth)
+    L = eng.num_lanes
+    report = torch.zeros(eng.report_bytes, dtype=torch.uint8, device=f"cuda:{local_rank}")
+    desyncs = []
+
+    def round_():
+        eng.speculate()
+        if dist is not None:
+            eng.confirm(report.data_ptr())
+            eng.synchronize()
+            g = exchange.allgather_reports(report)
+            if args.peers:
+                desyncs.extend(exchange.desyncs_against_peer(g, rank, world, eng.trunk_frame() - 1, S, L))
+        else:
+            eng.confirm()
+
+    for _ in range(args.warmup):
+        round_()
+    eng.synchronize()
+    if dist is not None:
+        dist.barrier()
+    eng.timing_reset()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        round_()
+    eng.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t1 = time.perf_counter()
+    kernel_ms, launches = eng.timing_read()
+    elapsed = t1 - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    resim_round = L * W + S
+    value = resim_round * args.steps * world / elapsed
+    Sp = 4 + 20 * P
+    bytes_round = L * (Sp + W * (Sp + 2) + W * P) + S * (2 * Sp + 2 + P) + 8 * ((L + 63) // 64)
+    avg_round_s = kernel_ms / 1e3 / max(launches, 1) * 2  # speculate + confirm launches per round
+    achieved = bytes_round / avg_round_s / 1e9
+    parity = None
+    if rank == 0:
+        try:
+            from oracle import oracle as O
+            O.build()
+            st = O.state_new(P)
+            for f in range(eng.trunk_frame()):
+                st = O.state_advance(st, truth[f, 0])
+            ck, _ = eng.report()
+            parity = {"session0_trunk_bit_exact": bytes(eng.trunk(0)) == bytes(st),
+                      "session0_checksum": int(ck[0]) == O.fletcher16(bytes(st)),
+                      "desyncs": int((eng.desync() >= 0).sum()) + len(desyncs)}
+        except Exception as exc:
+            parity = {"error": repr(exc)}
+        line = {
+            "metric": "resimulated session-frames/sec (node)", "value": round(value, 1),
+            "unit": "session-frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": c["text"], "sessions_per_gpu": S, "branches": B, "lanes_per_gpu": L,
+                       "players": P, "window": W, "peers": bool(args.peers),
+                       "parallelism": f"sessions sharded over {world} GPU(s), RCCL all-gather per round"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                         "algorithmic_bytes_per_round": bytes_round,
+                         "avg_kernel_ms_per_round": round(avg_round_s * 1e3, 4)},
+            "cpu_baseline": None, "parity": parity,
+        }
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -59,21 +176,16 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--path", choices=["pipelined", "sequential", "pipelined-whole"], default="pipelined",
                     help="SyncTest kernel (DESIGN.md section 3)")
+    ap.add_argument("--config", type=int, choices=[2, 3, 4], default=2,
+                    help="BASELINE.json config: 2 = SyncTest (default), 3/4 = branch rollback")
+    ap.add_argument("--peers", action="store_true",
+                    help="configs 3/4: rank r and r + world/2 replay the same sessions (the two "
+                         "machines of a match) and compare checksums after each all-gather")
     args = ap.parse_args()
+    if args.config != 2:
+        return run_branch(args)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and rank == 0:
-        print(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world} rank(s)", file=sys.stderr)
-
-    import torch
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-
+    world, rank, local_rank, torch, dist = setup_dist(args)
     from ggrs_amd import Engine
     from ggrs_amd import synth
 

@@ -1,0 +1,68 @@
+"""Cross-GPU exchange of confirmation reports: one all-gather per confirmation.
+
+A branch engine's report per confirmed frame is [S] u16 session checksums (padded to 8 bytes) +
+ceil(L/64) u64 survival words (ggrs_branch_confirm).  Every rank contributes its report and
+receives all of them: over RCCL (backend "nccl") the gather is all_gather_into_tensor on device
+buffers, over gloo (CPU tests) a list all_gather.  This replaces GGRS's per-peer ChecksumReport
+messages (src/network/protocol.rs:692-698 send, :663-682 receive) and the comparison in
+P2PSession::compare_local_checksums_against_peers (src/sessions/p2p_session.rs:904-937): with
+peer replicas (rank r and rank r + world/2 simulating the same sessions, like the two machines of
+a match), a differing checksum is a DesyncDetected event (src/lib.rs:158-167).
+"""
+from dataclasses import dataclass
+
+import numpy as np
+
+
+@dataclass
+class DesyncDetected:
+    """GgrsEvent::DesyncDetected (src/lib.rs:158-167); addr is the peer's rank."""
+    frame: int
+    session: int
+    local_checksum: int
+    remote_checksum: int
+    addr: int
+
+
+def report_layout(num_sessions, num_lanes):
+    ck_bytes = (2 * num_sessions + 7) & ~7
+    words = (num_lanes + 63) // 64
+    return ck_bytes, words, ck_bytes + 8 * words
+
+
+def split_report(buf, num_sessions, num_lanes):
+    """(checksums[S] u16, survival words u64) from one report's bytes (numpy uint8)."""
+    ck_bytes, words, total = report_layout(num_sessions, num_lanes)
+    b = np.ascontiguousarray(buf, np.uint8).reshape(-1)[:total]
+    return b[:2 * num_sessions].view(np.uint16), b[ck_bytes:ck_bytes + 8 * words].view(np.uint64)
+
+
+def allgather_reports(local, group=None):
+    """All-gather one report tensor (uint8, 1-D) from every rank -> [world, nbytes] tensor."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    if dist.get_backend(group) == "nccl":
+        out = torch.empty((world, local.numel()), dtype=local.dtype, device=local.device)
+        dist.all_gather_into_tensor(out.view(-1), local.contiguous(), group=group)
+        return out
+    parts = [torch.empty_like(local) for _ in range(world)]
+    dist.all_gather(parts, local.contiguous(), group=group)
+    return torch.stack(parts)
+
+
+def peer_of(rank, world):
+    """The rank simulating the same sessions as `rank` (the other machine of each match)."""
+    return (rank + world // 2) % world
+
+
+def desyncs_against_peer(gathered, rank, world, frame, num_sessions, num_lanes):
+    """Compare this rank's session checksums with its peer replica's (p2p_session.rs:904-937)."""
+    if world < 2:
+        return []
+    peer = peer_of(rank, world)
+    g = gathered.cpu().numpy() if hasattr(gathered, "cpu") else np.asarray(gathered)
+    mine, _ = split_report(g[rank], num_sessions, num_lanes)
+    theirs, _ = split_report(g[peer], num_sessions, num_lanes)
+    bad = np.nonzero(mine != theirs)[0]
+    return [DesyncDetected(frame, int(s), int(mine[s]), int(theirs[s]), peer) for s in bad]
