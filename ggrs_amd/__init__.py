@@ -9,5 +9,6 @@ from .session import (AdvanceFrame, BoxGameHandler, Engine, LoadGameState,  # no
                       MismatchedChecksum, SaveGameState, SessionBuilder, SyncTestSession)
 
 from .branch import BranchEngine  # noqa: F401
+from .particles import ParticleEngine  # noqa: F401
 
 __version__ = "0.1.0"

@@ -12,8 +12,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libggrs_amd.so")
-SOURCES = [os.path.join(CSRC, "engine.hip"), os.path.join(CSRC, "branch.hip")]
-HEADERS = [os.path.join(CSRC, h) for h in ("box_game.h", "glibc_sincosf.h", "common.h")] + [
+SOURCES = [os.path.join(CSRC, f) for f in ("engine.hip", "branch.hip", "particles.hip")]
+HEADERS = [os.path.join(CSRC, h) for h in ("box_game.h", "glibc_sincosf.h", "common.h", "particles.h")] + [
     os.path.join(ROOT, "include", "ggrs_amd.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

@@ -1,0 +1,523 @@
+// particles.hip -- the SyncTest rollback program (SyncTestSession::advance_frame,
+// src/sessions/sync_test_session.rs:85-150, same bookkeeping as synctest_kernel in engine.hip) on
+// the config-5 particle world (particles.h): ~1 MB states, so every Load/Save is an HBM stream.
+//
+// One workgroup per session.  Each thread owns entity quads (4 consecutive entities, 16-byte
+// loads/stores per field) for the whole launch and keeps a quad in registers across one call's
+// replay: Load (1 read of the quad), cd x (Save, Advance), Save of the current frame, the new
+// frame's Advance.  HBM per call and session = S (load) + cd * S (saves), S = 4 + 100 N bytes --
+// per resimulated frame S * (1 + 1/cd).  The Fletcher-16 of every saved frame is reduced in
+// registers (64-bit closed form), across the wavefront by shuffles and across the workgroup in LDS.
+//
+// HBM layout: ring [R][L][25][N] u32 (field-major, entity fastest), cur [L][25][N], frame counters
+// [R][L] / [L] i32, ring_ck / first_ck [R][L] u16, inputs [C][L] u32 (P input bytes per frame).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cstring>
+#include <utility>
+#include <vector>
+
+#include "common.h"
+#include "particles.h"
+
+#pragma clang fp contract(off)
+
+using namespace ggrs;
+using namespace ggrs::particles;
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kMaxCd = 62;
+
+struct PWParams {
+  int64_t L;
+  int32_t N, R, cd, f0, n, cap, P;
+  int32_t corrupt_lane, corrupt_frame;
+  uint32_t* cur;
+  int32_t* cur_frame;
+  uint32_t* ring;
+  int32_t* ring_frame;
+  uint16_t* ring_ck;
+  uint16_t* first_ck;
+  const uint32_t* inputs;
+  int32_t* lane_status;
+  int32_t* mis_frame;
+  uint64_t* mis_mask;
+};
+
+__global__ void pw_init_kernel(uint32_t* cur, int32_t* cur_frame, int64_t L, int32_t N, int64_t first_session) {
+  const int64_t s = blockIdx.y;
+  for (int32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < N; e += gridDim.x * blockDim.x) {
+    uint32_t* base = cur + (size_t)s * kFields * N + e;
+    const float r = kWindowWidth / 4.0f;
+    const float rot = (float)e / (float)N * 2.0f * kPi;
+    base[0] = __builtin_bit_cast(uint32_t, kWindowWidth / 2.0f + r * glibc_cosf(rot));
+    base[(size_t)N] = __builtin_bit_cast(uint32_t, kWindowHeight / 2.0f + r * glibc_sinf(rot));
+    base[(size_t)2 * N] = 0u;
+    base[(size_t)3 * N] = 0u;
+    base[(size_t)4 * N] = __builtin_bit_cast(uint32_t, fmod_exact(rot + kPi, 2.0f * kPi));
+    for (int k = 0; k < 20; k++)
+      base[(size_t)(5 + k) * N] = initial_payload((uint64_t)(first_session + s), (uint64_t)e, k);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) cur_frame[s] = 0;
+}
+
+__device__ inline void load_quad(uint32_t (&w)[4][kFields], const uint32_t* base, int32_t N, int32_t q) {
+#pragma unroll
+  for (int k = 0; k < kFields; k++) {
+    const uint4 v = *reinterpret_cast<const uint4*>(base + (size_t)k * N + 4 * q);
+    w[0][k] = v.x;
+    w[1][k] = v.y;
+    w[2][k] = v.z;
+    w[3][k] = v.w;
+  }
+}
+__device__ inline void store_quad(const uint32_t (&w)[4][kFields], uint32_t* base, int32_t N, int32_t q) {
+#pragma unroll
+  for (int k = 0; k < kFields; k++)
+    *reinterpret_cast<uint4*>(base + (size_t)k * N + 4 * q) = make_uint4(w[0][k], w[1][k], w[2][k], w[3][k]);
+}
+__device__ inline void advance_quad(uint32_t (&w)[4][kFields], uint32_t in_word, int32_t P, int32_t e0) {
+#pragma unroll
+  for (int j = 0; j < 4; j++) advance_entity(w[j], (in_word >> (8 * ((e0 + j) % P))) & 0xffu);
+}
+__device__ inline void fletcher_quad(FletcherAcc& a, const uint32_t (&w)[4][kFields], int32_t N, int32_t e0) {
+#pragma unroll
+  for (int j = 0; j < 4; j++) fletcher_entity(a, w[j], (uint64_t)kEntityBytes * (uint64_t)(N - (e0 + j)));
+}
+
+// Wavefront sum of one quad-frame's Fletcher partials, added by lane 0 to the wave's LDS slot of
+// that frame (each wave owns its slots: no atomics).  Every lane of the wave must call it.
+__device__ inline void wave_accumulate(const FletcherAcc& a, uint64_t* slot3) {
+  uint64_t s1 = a.s1, s2p = a.s2pos, s2n = a.s2neg;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    s1 += (uint64_t)__shfl_xor((long long)s1, m, 64);
+    s2p += (uint64_t)__shfl_xor((long long)s2p, m, 64);
+    s2n += (uint64_t)__shfl_xor((long long)s2n, m, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    slot3[0] += s1;
+    slot3[1] += s2p;
+    slot3[2] += s2n;
+  }
+}
+
+// checksum of one frame from the block totals plus the frame counter at byte offset 0
+__device__ inline uint16_t finish_checksum(uint64_t s1, uint64_t s2pos, uint64_t s2neg, int32_t frame, int32_t N) {
+  const uint64_t n = 4 + (uint64_t)kEntityBytes * N;
+  const uint32_t fw = (uint32_t)frame;
+  const uint32_t a = __builtin_amdgcn_udot4(fw, 0x01010101u, 0u, false);
+  const uint32_t b = __builtin_amdgcn_udot4(fw, 0x03020100u, 0u, false);
+  const uint64_t t1 = s1 + a;
+  const uint64_t t2 = s2pos + n * a - s2neg - b;  // sum_j (n - j) d_j >= 0
+  return (uint16_t)(((t2 % 255u) << 8) | (t1 % 255u));
+}
+
+constexpr int kWaves = kBlock / 64;
+
+__global__ __launch_bounds__(kBlock) void pw_synctest_kernel(PWParams p) {
+  __shared__ uint64_t lds_acc[kWaves][kMaxCd + 1][3];  // per wave, per saved frame: s1, s2+, s2-
+  __shared__ int32_t lds_stop;
+  const int64_t s = blockIdx.x;
+  if (p.lane_status[s] != GGRS_LANE_RUNNING) return;
+  const int32_t N = p.N, R = p.R, nq = N / 4, cd = p.cd;
+  const int64_t L = p.L;
+  const int wave = threadIdx.x >> 6;
+  const size_t rec = (size_t)kFields * N;  // u32 per session state
+  uint32_t* cur = p.cur + (size_t)s * rec;
+  for (int32_t f = p.f0; f < p.f0 + p.n; ++f) {
+    const bool replay = cd > 0 && f > cd;
+    if (replay && f >= cd + 2) {  // checksums_consistent over f-cd .. f (sync_test_session.rs:173-190)
+      if (threadIdx.x == 0) {
+        uint64_t mism = 0;
+        for (int32_t fc = f - cd; fc <= f - 2; ++fc) {
+          const int64_t o = (int64_t)(fc % R) * L + s;
+          if (p.ring_ck[o] != p.first_ck[o]) mism |= 1ull << (fc - (f - cd));
+        }
+        lds_stop = mism != 0;
+        if (mism) {
+          p.lane_status[s] = GGRS_LANE_MISMATCH;
+          p.mis_frame[s] = f;
+          p.mis_mask[s] = mism;
+        }
+      }
+      __syncthreads();
+      if (lds_stop) {
+        // Err(MismatchedChecksum): the session stops before the rollback, holding the state of
+        // call f-1's final AdvanceFrame -- the advance of the frame-(f-1) cell it saved.
+        const uint32_t in_prev = p.inputs[(int64_t)((f - 1) % p.cap) * L + s];
+        for (int32_t q = threadIdx.x; q < nq; q += kBlock) {
+          uint32_t w[4][kFields];
+          load_quad(w, p.ring + ((size_t)((f - 1) % R) * L + s) * rec, N, q);
+          advance_quad(w, in_prev, p.P, 4 * q);
+          store_quad(w, cur, N, q);
+        }
+        return;
+      }
+    }
+    for (int k = threadIdx.x; k < kWaves * (kMaxCd + 1) * 3; k += kBlock) (&lds_acc[0][0][0])[k] = 0;
+    __syncthreads();
+    const uint32_t in_cur = p.inputs[(int64_t)(f % p.cap) * L + s];
+    const int32_t g0 = replay ? f - cd : f;
+    const bool last_call = f == p.f0 + p.n - 1;
+    for (int32_t qb = 0; qb < nq; qb += kBlock) {  // wave-uniform trip count (shuffles inside)
+      const int32_t q = qb + threadIdx.x;
+      const bool on = q < nq;
+      const int32_t e0 = 4 * q;
+      uint32_t w[4][kFields];
+      if (on) {
+        if (replay) {  // LoadGameState(f - cd)
+          load_quad(w, p.ring + ((size_t)(g0 % R) * L + s) * rec, N, q);
+          if (s == p.corrupt_lane && f == p.corrupt_frame && q == 0) w[0][0] ^= 1u;
+        } else {
+          load_quad(w, cur, N, q);  // the handler's current state (warm-up calls)
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+#pragma unroll
+          for (int k = 0; k < kFields; k++) w[j][k] = 0;
+      }
+      const int32_t steps = replay ? cd : 0;
+      for (int32_t i = 0; i <= steps; ++i) {
+        const int32_t g = g0 + i;  // frame the quad holds
+        if (cd > 0 && (i > 0 || !replay)) {  // SaveGameState(g): the replay's saves, then save current
+          FletcherAcc a{0, 0, 0};
+          if (on) {
+            store_quad(w, p.ring + ((size_t)(g % R) * L + s) * rec, N, q);
+            fletcher_quad(a, w, N, e0);
+          }
+          wave_accumulate(a, lds_acc[wave][i]);
+        }
+        if (on) advance_quad(w, i < steps ? p.inputs[(int64_t)(g % p.cap) * L + s] : in_cur, p.P, e0);
+      }
+      // the game state after the call; a later call of this launch reloads from the ring, so
+      // only the last call's (or a warm-up call's) result has a reader
+      if (on && (!replay || last_call)) store_quad(w, cur, N, q);
+    }
+    __syncthreads();
+    if (cd > 0 && threadIdx.x == 0) {
+      for (int i = replay ? 1 : 0; i <= (replay ? cd : 0); i++) {
+        uint64_t t[3] = {0, 0, 0};
+        for (int wv = 0; wv < kWaves; wv++)
+          for (int c = 0; c < 3; c++) t[c] += lds_acc[wv][i][c];
+        const int32_t g = g0 + i;
+        const uint16_t ck = finish_checksum(t[0], t[1], t[2], g, N);
+        p.ring_ck[(int64_t)(g % R) * L + s] = ck;
+        p.ring_frame[(int64_t)(g % R) * L + s] = g;
+        if (g == f) p.first_ck[(int64_t)(f % R) * L + s] = ck;  // first sighting of frame f
+      }
+    }
+    if (threadIdx.x == 0) p.cur_frame[s] = f + 1;
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+struct ggrs_particle_engine {
+  ggrs_particle_config_t cfg{};
+  int R = 2, cap = 128;
+  hipStream_t stream = nullptr;
+  uint32_t* cur = nullptr;
+  int32_t* cur_frame = nullptr;
+  uint32_t* ring = nullptr;
+  int32_t* ring_frame = nullptr;
+  uint16_t* ring_ck = nullptr;
+  uint16_t* first_ck = nullptr;
+  uint32_t* inputs = nullptr;
+  int32_t* lane_status = nullptr;
+  int32_t* mis_frame = nullptr;
+  uint64_t* mis_mask = nullptr;
+  uint8_t* staging = nullptr;
+  size_t staging_bytes = 0;
+  int32_t current_frame = 0, next_input_frame = 0;
+  int32_t corrupt_lane = -1, corrupt_frame = -1;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::vector<hipEvent_t> tev;
+  size_t tev_used = 0;
+  bool collecting = false;
+};
+
+namespace {
+
+__global__ void pw_pack_inputs(const uint8_t* src, uint32_t* dst, int64_t L, int32_t P, int32_t n, int32_t q0, int32_t cap) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)n * L) return;
+  const int64_t fr = i / L, s = i % L;
+  uint32_t w = 0;
+  for (int k = 0; k < P; k++) w |= (uint32_t)src[i * P + k] << (8 * k);
+  dst[(((int64_t)q0 + fr) % cap) * L + s] = w;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ggrs_particle_engine_destroy(ggrs_particle_engine_t* e) {
+  if (!e) return GGRS_OK;
+  (void)hipSetDevice(e->cfg.device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  void* bufs[] = {e->cur, e->cur_frame, e->ring, e->ring_frame, e->ring_ck, e->first_ck, e->inputs,
+                  e->lane_status, e->mis_frame, e->mis_mask, e->staging};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  for (hipEvent_t ev : e->tev) (void)hipEventDestroy(ev);
+  if (e->ev0) (void)hipEventDestroy(e->ev0);
+  if (e->ev1) (void)hipEventDestroy(e->ev1);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+  return GGRS_OK;
+}
+
+int ggrs_particle_engine_create(const ggrs_particle_config_t* cfg, ggrs_particle_engine_t** out) {
+  if (!cfg || !out) return set_error(GGRS_E_INVALID, "null argument");
+  *out = nullptr;
+  const ggrs_particle_config_t c = *cfg;
+  if (c.num_sessions < 1) return set_error(GGRS_E_INVALID, "num_sessions must be >= 1");
+  if (c.num_entities < 4 || c.num_entities % 4 != 0 || c.num_entities > 160000)
+    return set_error(GGRS_E_INVALID, "num_entities must be a multiple of 4 in 4..160000");
+  if (c.num_players < 1 || c.num_players > 4) return set_error(GGRS_E_INVALID, "num_players must be in 1..4");
+  if (c.check_distance < 0 || c.check_distance > kMaxCd)
+    return set_error(GGRS_E_INVALID, "check_distance must be in 0..%d", kMaxCd);
+  if (c.check_distance >= c.max_prediction)
+    return set_error(GGRS_E_INVALID, "Check distance too big. (check_distance must be < max_prediction)");
+  if (c.max_prediction > 63) return set_error(GGRS_E_INVALID, "max_prediction must be <= 63");
+  ggrs_particle_engine* e = new ggrs_particle_engine();
+  e->cfg = c;
+  e->R = c.max_prediction + 1;
+  e->cap = c.input_capacity ? c.input_capacity : 128;
+  e->cfg.input_capacity = e->cap;
+  if (e->cap < c.check_distance + 2) {
+    delete e;
+    return set_error(GGRS_E_INVALID, "input_capacity must be >= check_distance + 2");
+  }
+  auto fail = [&](int rc) {
+    std::string msg = ggrs_last_error();
+    ggrs_particle_engine_destroy(e);
+    set_error(rc, "%s", msg.c_str());
+    return rc;
+  };
+#define CTRY(expr)                                                                      \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) return fail(set_error(GGRS_E_HIP, "%s: %s", #expr, hipGetErrorString(e_))); \
+  } while (0)
+  const int64_t L = c.num_sessions;
+  const size_t rec = (size_t)kFields * c.num_entities;
+  CTRY(hipSetDevice(c.device));
+  CTRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+  CTRY(hipEventCreate(&e->ev0));
+  CTRY(hipEventCreate(&e->ev1));
+  CTRY(hipMalloc(&e->cur, 4 * rec * L));
+  CTRY(hipMalloc(&e->cur_frame, 4 * L));
+  CTRY(hipMalloc(&e->ring, 4 * rec * L * e->R));
+  CTRY(hipMalloc(&e->ring_frame, 4 * (size_t)L * e->R));
+  CTRY(hipMalloc(&e->ring_ck, 2 * (size_t)L * e->R));
+  CTRY(hipMalloc(&e->first_ck, 2 * (size_t)L * e->R));
+  CTRY(hipMalloc(&e->inputs, 4 * (size_t)L * e->cap));
+  CTRY(hipMalloc(&e->lane_status, 4 * L));
+  CTRY(hipMalloc(&e->mis_frame, 4 * L));
+  CTRY(hipMalloc(&e->mis_mask, 8 * L));
+  CTRY(hipMemsetAsync(e->ring_frame, 0xff, 4 * (size_t)L * e->R, e->stream));
+  CTRY(hipMemsetAsync(e->ring_ck, 0, 2 * (size_t)L * e->R, e->stream));
+  CTRY(hipMemsetAsync(e->first_ck, 0, 2 * (size_t)L * e->R, e->stream));
+  CTRY(hipMemsetAsync(e->inputs, 0, 4 * (size_t)L * e->cap, e->stream));
+  CTRY(hipMemsetAsync(e->lane_status, 0, 4 * L, e->stream));
+  CTRY(hipMemsetAsync(e->mis_frame, 0xff, 4 * L, e->stream));
+  CTRY(hipMemsetAsync(e->mis_mask, 0, 8 * L, e->stream));
+  {
+    dim3 grid((unsigned)std::min<int64_t>(64, (c.num_entities + 255) / 256), (unsigned)L);
+    pw_init_kernel<<<grid, 256, 0, e->stream>>>(e->cur, e->cur_frame, L, c.num_entities, c.first_session_id);
+    CTRY(hipGetLastError());
+  }
+  CTRY(hipStreamSynchronize(e->stream));
+#undef CTRY
+  *out = e;
+  return GGRS_OK;
+}
+
+int ggrs_particle_add_local_inputs(ggrs_particle_engine_t* e, int32_t first_frame, int32_t n, const uint8_t* inputs) {
+  if (!e || (!inputs && n > 0)) return set_error(GGRS_E_INVALID, "null argument");
+  if (n < 0) return set_error(GGRS_E_INVALID, "n_frames must be >= 0");
+  if (first_frame != e->next_input_frame)
+    return set_error(GGRS_E_INVALID, "inputs must be added sequentially (expected frame %d, got %d)",
+                     e->next_input_frame, first_frame);
+  if (n == 0) return GGRS_OK;
+  const int64_t oldest_needed = (int64_t)e->current_frame - e->cfg.check_distance;
+  if ((int64_t)first_frame + n - 1 - oldest_needed >= e->cap)
+    return set_error(GGRS_E_INVALID, "input queue full (capacity %d)", e->cap);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const int64_t L = e->cfg.num_sessions;
+  const size_t bytes = (size_t)n * L * e->cfg.num_players;
+  if (bytes > e->staging_bytes) {
+    if (e->staging) HIP_TRY(hipFree(e->staging));
+    e->staging = nullptr;
+    e->staging_bytes = 0;
+    HIP_TRY(hipMalloc(&e->staging, bytes));
+    e->staging_bytes = bytes;
+  }
+  HIP_TRY(hipMemcpyAsync(e->staging, inputs, bytes, hipMemcpyHostToDevice, e->stream));
+  pw_pack_inputs<<<grid_of((int64_t)n * L, 256), 256, 0, e->stream>>>(e->staging, e->inputs, L, e->cfg.num_players, n,
+                                                                       first_frame % e->cap, e->cap);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  e->next_input_frame = first_frame + n;
+  return GGRS_OK;
+}
+
+int ggrs_particle_synctest_advance_frames(ggrs_particle_engine_t* e, int32_t n) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  if (n < 0) return set_error(GGRS_E_INVALID, "n_frames must be >= 0");
+  if (n == 0) return GGRS_OK;
+  if ((int64_t)e->current_frame + n - 1 >= e->next_input_frame)
+    return set_error(GGRS_E_INVALID, "Missing local input while calling advance_frame(): frame %d not added",
+                     e->current_frame + n - 1);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  PWParams p;
+  p.L = e->cfg.num_sessions;
+  p.N = e->cfg.num_entities;
+  p.R = e->R;
+  p.cd = e->cfg.check_distance;
+  p.f0 = e->current_frame;
+  p.n = n;
+  p.cap = e->cap;
+  p.P = e->cfg.num_players;
+  p.corrupt_lane = e->corrupt_lane;
+  p.corrupt_frame = e->corrupt_frame;
+  p.cur = e->cur;
+  p.cur_frame = e->cur_frame;
+  p.ring = e->ring;
+  p.ring_frame = e->ring_frame;
+  p.ring_ck = e->ring_ck;
+  p.first_ck = e->first_ck;
+  p.inputs = e->inputs;
+  p.lane_status = e->lane_status;
+  p.mis_frame = e->mis_frame;
+  p.mis_mask = e->mis_mask;
+  hipEvent_t a = e->ev0, b = e->ev1;
+  if (e->collecting) {
+    while (e->tev.size() < e->tev_used + 2) {
+      hipEvent_t ev;
+      HIP_TRY(hipEventCreate(&ev));
+      e->tev.push_back(ev);
+    }
+    a = e->tev[e->tev_used];
+    b = e->tev[e->tev_used + 1];
+    e->tev_used += 2;
+  }
+  HIP_TRY(hipEventRecord(a, e->stream));
+  pw_synctest_kernel<<<p.L, kBlock, 0, e->stream>>>(p);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(b, e->stream));
+  e->current_frame += n;
+  return GGRS_OK;
+}
+
+int ggrs_particle_synchronize(ggrs_particle_engine_t* e) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return GGRS_OK;
+}
+
+int ggrs_particle_current_frame(const ggrs_particle_engine_t* e, int32_t* out) {
+  if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
+  *out = e->current_frame;
+  return GGRS_OK;
+}
+
+int ggrs_particle_read_mismatches(ggrs_particle_engine_t* e, int32_t* st, int32_t* mf, uint64_t* mm) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const size_t L = e->cfg.num_sessions;
+  if (st) HIP_TRY(hipMemcpyAsync(st, e->lane_status, 4 * L, hipMemcpyDeviceToHost, e->stream));
+  if (mf) HIP_TRY(hipMemcpyAsync(mf, e->mis_frame, 4 * L, hipMemcpyDeviceToHost, e->stream));
+  if (mm) HIP_TRY(hipMemcpyAsync(mm, e->mis_mask, 8 * L, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return GGRS_OK;
+}
+
+// declared layout bytes of a SoA record: frame, then per entity 25 little-endian words
+static void pw_serialize(const std::vector<uint32_t>& soa, int32_t frame, int32_t N, uint8_t* out) {
+  memcpy(out, &frame, 4);
+  for (int32_t e2 = 0; e2 < N; e2++)
+    for (int k = 0; k < kFields; k++) memcpy(out + 4 + (size_t)kEntityBytes * e2 + 4 * k, &soa[(size_t)k * N + e2], 4);
+}
+
+int ggrs_particle_read_state(ggrs_particle_engine_t* e, int32_t session, uint8_t* out) {
+  if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
+  if (session < 0 || session >= e->cfg.num_sessions) return set_error(GGRS_E_INVALID, "session out of range");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const int32_t N = e->cfg.num_entities;
+  const size_t rec = (size_t)kFields * N;
+  std::vector<uint32_t> soa(rec);
+  int32_t frame = 0;
+  HIP_TRY(hipMemcpyAsync(soa.data(), e->cur + rec * session, 4 * rec, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(&frame, e->cur_frame + session, 4, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  pw_serialize(soa, frame, N, out);
+  return GGRS_OK;
+}
+
+int ggrs_particle_read_saved(ggrs_particle_engine_t* e, int32_t session, int32_t frame, uint16_t* checksum, uint8_t* out) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  if (session < 0 || session >= e->cfg.num_sessions) return set_error(GGRS_E_INVALID, "session out of range");
+  if (frame < 0) return set_error(GGRS_E_INVALID, "negative frame");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const int32_t N = e->cfg.num_entities;
+  const size_t rec = (size_t)kFields * N;
+  const int slot = frame % e->R;
+  int32_t tag = -1;
+  uint16_t ck = 0;
+  HIP_TRY(hipMemcpyAsync(&tag, e->ring_frame + (size_t)slot * e->cfg.num_sessions + session, 4, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(&ck, e->ring_ck + (size_t)slot * e->cfg.num_sessions + session, 2, hipMemcpyDeviceToHost, e->stream));
+  std::vector<uint32_t> soa(out ? rec : 0);
+  if (out)
+    HIP_TRY(hipMemcpyAsync(soa.data(), e->ring + ((size_t)slot * e->cfg.num_sessions + session) * rec, 4 * rec,
+                           hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  if (tag != frame) return set_error(GGRS_E_PRECONDITION, "no saved cell for frame %d (slot holds %d)", frame, tag);
+  if (checksum) *checksum = ck;
+  if (out) pw_serialize(soa, frame, N, out);
+  return GGRS_OK;
+}
+
+int ggrs_particle_debug_corrupt_on_load(ggrs_particle_engine_t* e, int32_t session, int32_t frame) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  e->corrupt_lane = session;
+  e->corrupt_frame = frame;
+  return GGRS_OK;
+}
+
+int ggrs_particle_timing_reset(ggrs_particle_engine_t* e) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  e->tev_used = 0;
+  e->collecting = true;
+  return GGRS_OK;
+}
+
+int ggrs_particle_timing_read(ggrs_particle_engine_t* e, float* total_ms, int32_t* launches) {
+  if (!e || !total_ms || !launches) return set_error(GGRS_E_INVALID, "null argument");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  float sum = 0.0f;
+  for (size_t i = 0; i + 1 < e->tev_used; i += 2) {
+    float ms = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&ms, e->tev[i], e->tev[i + 1]));
+    sum += ms;
+  }
+  *total_ms = sum;
+  *launches = (int32_t)(e->tev_used / 2);
+  e->collecting = false;
+  e->tev_used = 0;
+  return GGRS_OK;
+}
+
+}  // extern "C"

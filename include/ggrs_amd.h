@@ -206,6 +206,44 @@ int ggrs_branch_read_lane(ggrs_branch_engine_t* eng, int64_t lane, int32_t frame
 int ggrs_branch_timing_reset(ggrs_branch_engine_t* eng);
 int ggrs_branch_timing_read(ggrs_branch_engine_t* eng, float* total_ms, int32_t* launches);
 
+/* ---------------------------------------------------------------------------------------------
+ * Config-5 large-state stress game (defined by this build; ggrs_amd/csrc/particles.h):
+ * a session is one frame counter + num_entities x 100-byte entities (an ex_game ship + 80 bytes
+ * of integer payload), ~1 MB at 10k entities, so every Load/Save of the SyncTest program
+ * (sync_test_session.rs:85-150) is an HBM stream.  One engine = num_sessions sessions.
+ */
+typedef struct ggrs_particle_config {
+  int32_t num_sessions;
+  int32_t num_entities;     /* multiple of 4, <= 160000 */
+  int32_t num_players;      /* input bytes per frame; entity e plays player e % num_players */
+  int32_t max_prediction;   /* ring = max_prediction + 1 states per session */
+  int32_t check_distance;   /* 0..62, < max_prediction */
+  int32_t input_capacity;   /* frames of queued input; 0 = 128 */
+  int32_t device;
+  int32_t first_session_id; /* global id of session 0 (seeds the initial payload) */
+} ggrs_particle_config_t;
+
+typedef struct ggrs_particle_engine ggrs_particle_engine_t;
+
+int ggrs_particle_engine_create(const ggrs_particle_config_t* cfg, ggrs_particle_engine_t** out);
+int ggrs_particle_engine_destroy(ggrs_particle_engine_t* eng);
+/* inputs [n_frames][num_sessions][num_players], frames added in order from 0 (no input delay) */
+int ggrs_particle_add_local_inputs(ggrs_particle_engine_t* eng, int32_t first_frame, int32_t n_frames,
+                                   const uint8_t* inputs);
+int ggrs_particle_synctest_advance_frames(ggrs_particle_engine_t* eng, int32_t n_frames);
+int ggrs_particle_synchronize(ggrs_particle_engine_t* eng);
+int ggrs_particle_current_frame(const ggrs_particle_engine_t* eng, int32_t* out);
+int ggrs_particle_read_mismatches(ggrs_particle_engine_t* eng, int32_t* status, int32_t* mismatch_frame,
+                                  uint64_t* mismatch_mask);
+/* current state of one session in the declared layout (4 + 100 * num_entities bytes) */
+int ggrs_particle_read_state(ggrs_particle_engine_t* eng, int32_t session, uint8_t* out);
+/* the saved cell of `frame` (checksum and/or declared-layout bytes) */
+int ggrs_particle_read_saved(ggrs_particle_engine_t* eng, int32_t session, int32_t frame, uint16_t* checksum,
+                             uint8_t* out);
+int ggrs_particle_debug_corrupt_on_load(ggrs_particle_engine_t* eng, int32_t session, int32_t frame);
+int ggrs_particle_timing_reset(ggrs_particle_engine_t* eng);
+int ggrs_particle_timing_read(ggrs_particle_engine_t* eng, float* total_ms, int32_t* launches);
+
 #ifdef __cplusplus
 }
 #endif

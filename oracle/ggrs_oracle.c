@@ -110,46 +110,48 @@ static float rem_euclid_f32(float a, float b) {
   return r < 0.0f ? r + fabsf(b) : r;
 }
 
+/* One player of State::advance (ex_game.rs:276-331): in/out x, y, vx, vy, rot. */
+static void ship_step(float* px, float* py, float* pvx, float* pvy, float* prot, uint8_t input) {
+  const float MS = movement_speed(), RS = rotation_speed();
+  float old_x = *px, old_y = *py;
+  float old_vel_x = *pvx, old_vel_y = *pvy;
+  float rot = *prot;
+  float vel_x = old_vel_x * FRICTION;
+  float vel_y = old_vel_y * FRICTION;
+  /* Rust: `input & INPUT_UP != 0` parses as `(input & INPUT_UP) != 0` */
+  if ((input & INPUT_UP) != 0 && (input & INPUT_DOWN) == 0) {
+    vel_x += MS * cosf(rot);
+    vel_y += MS * sinf(rot);
+  }
+  if ((input & INPUT_UP) == 0 && (input & INPUT_DOWN) != 0) {
+    vel_x -= MS * cosf(rot);
+    vel_y -= MS * sinf(rot);
+  }
+  if ((input & INPUT_LEFT) != 0 && (input & INPUT_RIGHT) == 0)
+    rot = rem_euclid_f32(rot - RS, 2.0f * PI_F32);
+  if ((input & INPUT_LEFT) == 0 && (input & INPUT_RIGHT) != 0)
+    rot = rem_euclid_f32(rot + RS, 2.0f * PI_F32);
+  float magnitude = sqrtf(vel_x * vel_x + vel_y * vel_y);
+  if (magnitude > MAX_SPEED) {
+    vel_x = (vel_x * MAX_SPEED) / magnitude;
+    vel_y = (vel_y * MAX_SPEED) / magnitude;
+  }
+  float x = old_x + vel_x;
+  float y = old_y + vel_y;
+  x = fmaxf(x, 0.0f); /* f32::max / f32::min are IEEE maxNum / minNum = fmaxf / fminf */
+  x = fminf(x, WINDOW_WIDTH);
+  y = fmaxf(y, 0.0f);
+  y = fminf(y, WINDOW_HEIGHT);
+  *px = x; *py = y; *pvx = vel_x; *pvy = vel_y; *prot = rot;
+}
+
 /* State::advance (ex_game.rs:271-333).  inputs[i] = Input.inp, status[i] = InputStatus */
 static void state_advance(State* s, const uint8_t* inputs, const uint8_t* status) {
-  const float MS = movement_speed(), RS = rotation_speed();
   s->frame += 1;
   for (uint64_t i = 0; i < s->num_players; i++) {
     uint8_t input = status[i] == STATUS_DISCONNECTED ? 4 : inputs[i]; /* disconnected spin */
-    float old_x = s->positions[2 * i], old_y = s->positions[2 * i + 1];
-    float old_vel_x = s->velocities[2 * i], old_vel_y = s->velocities[2 * i + 1];
-    float rot = s->rotations[i];
-    float vel_x = old_vel_x * FRICTION;
-    float vel_y = old_vel_y * FRICTION;
-    /* Rust: `input & INPUT_UP != 0` parses as `(input & INPUT_UP) != 0` */
-    if ((input & INPUT_UP) != 0 && (input & INPUT_DOWN) == 0) {
-      vel_x += MS * cosf(rot);
-      vel_y += MS * sinf(rot);
-    }
-    if ((input & INPUT_UP) == 0 && (input & INPUT_DOWN) != 0) {
-      vel_x -= MS * cosf(rot);
-      vel_y -= MS * sinf(rot);
-    }
-    if ((input & INPUT_LEFT) != 0 && (input & INPUT_RIGHT) == 0)
-      rot = rem_euclid_f32(rot - RS, 2.0f * PI_F32);
-    if ((input & INPUT_LEFT) == 0 && (input & INPUT_RIGHT) != 0)
-      rot = rem_euclid_f32(rot + RS, 2.0f * PI_F32);
-    float magnitude = sqrtf(vel_x * vel_x + vel_y * vel_y);
-    if (magnitude > MAX_SPEED) {
-      vel_x = (vel_x * MAX_SPEED) / magnitude;
-      vel_y = (vel_y * MAX_SPEED) / magnitude;
-    }
-    float x = old_x + vel_x;
-    float y = old_y + vel_y;
-    x = fmaxf(x, 0.0f); /* f32::max / f32::min are IEEE maxNum / minNum = fmaxf / fminf */
-    x = fminf(x, WINDOW_WIDTH);
-    y = fmaxf(y, 0.0f);
-    y = fminf(y, WINDOW_HEIGHT);
-    s->positions[2 * i] = x;
-    s->positions[2 * i + 1] = y;
-    s->velocities[2 * i] = vel_x;
-    s->velocities[2 * i + 1] = vel_y;
-    s->rotations[i] = rot;
+    ship_step(&s->positions[2 * i], &s->positions[2 * i + 1], &s->velocities[2 * i],
+              &s->velocities[2 * i + 1], &s->rotations[i], input);
   }
 }
 
@@ -863,5 +865,135 @@ int oracle_p2p_replay(int32_t P, const uint8_t* state_in, int32_t load_frame, in
   free(rv.v);
   state_free(&g.game_state);
   sl_free(&sl);
+  return 0;
+}
+
+
+/* ================================================================ config-5 particle world
+ * The large-state stress game the build defines (ggrs_amd/csrc/particles.h has the spec): frame +
+ * N entities of (ex_game ship x, y, vx, vy, rot; u32 payload[20]).  Restated here for parity. */
+typedef struct { int32_t frame; int32_t N; float* ship; uint32_t* pay; } PState;
+
+static uint64_t pw_mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static void pstate_alloc(PState* s, int32_t N) {
+  s->N = N; s->ship = (float*)malloc(sizeof(float) * 5 * (size_t)N); s->pay = (uint32_t*)malloc(4 * 20 * (size_t)N);
+}
+static void pstate_free(PState* s) { free(s->ship); free(s->pay); s->ship = NULL; s->pay = NULL; }
+static void pstate_clone(PState* d, const PState* s) {
+  pstate_alloc(d, s->N); d->frame = s->frame;
+  memcpy(d->ship, s->ship, sizeof(float) * 5 * (size_t)s->N); memcpy(d->pay, s->pay, 4 * 20 * (size_t)s->N);
+}
+static void pstate_new(PState* s, int32_t N, uint64_t session) {
+  pstate_alloc(s, N);
+  s->frame = 0;
+  const float r = WINDOW_WIDTH / 4.0f;
+  for (int32_t e = 0; e < N; e++) {
+    float rot = (float)e / (float)N * 2.0f * PI_F32;
+    s->ship[5 * e + 0] = WINDOW_WIDTH / 2.0f + r * cosf(rot);
+    s->ship[5 * e + 1] = WINDOW_HEIGHT / 2.0f + r * sinf(rot);
+    s->ship[5 * e + 2] = 0.0f;
+    s->ship[5 * e + 3] = 0.0f;
+    s->ship[5 * e + 4] = fmodf(rot + PI_F32, 2.0f * PI_F32);
+    for (int k = 0; k < 20; k++) s->pay[20 * e + k] = (uint32_t)pw_mix64((session << 40) ^ ((uint64_t)e << 8) ^ (uint64_t)k);
+  }
+}
+static void pstate_advance(PState* s, const uint8_t* inputs, int32_t P) {
+  s->frame += 1;
+  for (int32_t e = 0; e < s->N; e++) {
+    uint8_t in = inputs[e % P];
+    float* sh = &s->ship[5 * e];
+    ship_step(&sh[0], &sh[1], &sh[2], &sh[3], &sh[4], in);
+    uint32_t* p = &s->pay[20 * e];
+    uint32_t old[20];
+    memcpy(old, p, sizeof old);
+    for (int k = 0; k < 20; k++) p[k] = old[k] * 0x9E3779B1u + (old[(k + 1) % 20] >> 7) + (uint32_t)in;
+  }
+}
+static size_t pstate_bytes(int32_t N) { return 4 + 100 * (size_t)N; }
+static void pstate_serialize(const PState* s, uint8_t* out) {
+  put_u32(out, (uint32_t)s->frame);
+  for (int32_t e = 0; e < s->N; e++) {
+    uint8_t* o = out + 4 + 100 * (size_t)e;
+    for (int k = 0; k < 5; k++) put_f32(o + 4 * k, s->ship[5 * e + k]);
+    for (int k = 0; k < 20; k++) put_u32(o + 20 + 4 * k, s->pay[20 * e + k]);
+  }
+}
+static uint16_t pstate_checksum(const PState* s) {
+  size_t n = pstate_bytes(s->N);
+  uint8_t* b = (uint8_t*)malloc(n);
+  pstate_serialize(s, b);
+  uint16_t c = oracle_fletcher16(b, n);
+  free(b);
+  return c;
+}
+
+/* The ex_game-style handler for the particle world: cells keep their frame/checksum in the
+ * SyncLayer (data = None, sync_layer.rs:18-24) and the particle states in store[cell]. */
+static void pw_handle_requests(PState* g, PState* store, int* has, SyncLayer* sl, const RequestVec* rv,
+                               int32_t P, int corrupt_after_load) {
+  for (size_t k = 0; k < rv->n; k++) {
+    const Request* r = &rv->v[k];
+    if (r->kind == REQ_LOAD) {
+      ORACLE_ASSERT(has[r->cell], "No data found.");
+      PState t; pstate_clone(&t, &store[r->cell]);
+      pstate_free(g); *g = t;
+      if (corrupt_after_load) { uint32_t u; memcpy(&u, &g->ship[0], 4); u ^= 1u; memcpy(&g->ship[0], &u, 4); }
+    } else if (r->kind == REQ_SAVE) {
+      ORACLE_ASSERT(g->frame == r->frame, "save frame != state frame");
+      if (has[r->cell]) pstate_free(&store[r->cell]);
+      pstate_clone(&store[r->cell], g);
+      has[r->cell] = 1;
+      cell_save(&sl->cells[r->cell], r->frame, NULL, 1, pstate_checksum(g));
+    } else {
+      pstate_advance(g, r->inputs, P);
+    }
+  }
+}
+
+/* SyncTest over the particle world for one session; outputs the checksum of every frame's first
+ * save (call f's save_current_state, ck_trace[f]; 0 when cd == 0), final state bytes, ring frames,
+ * checksums and state bytes ([R][4 + 100N]). */
+int oracle_particles_synctest_run(int32_t N, int32_t P, int32_t max_prediction, int32_t check_distance,
+                                  uint64_t session, int32_t frames, const uint8_t* inputs, int32_t corrupt_frame,
+                                  uint16_t* ck_trace, uint8_t* final_state, int32_t* ring_frames,
+                                  uint16_t* ring_cksums, uint8_t* ring_states, OracleSyncTestResult* res) {
+  memset(res, 0, sizeof *res);
+  SyncTestSession s;
+  if (synctest_new(&s, (size_t)P, (size_t)max_prediction, (size_t)check_distance, 0, PREDICT_REPEAT_LAST)) {
+    res->status = -1; return -1;
+  }
+  size_t R = s.sl.num_cells;
+  PState* store = (PState*)calloc(R, sizeof(PState));
+  int* has = (int*)calloc(R, sizeof(int));
+  PState g; pstate_new(&g, N, session);
+  RequestVec rv = {0};
+  for (int32_t f = 0; f < frames; f++) {
+    for (int32_t p = 0; p < P; p++) synctest_add_local_input(&s, (size_t)p, inputs[(size_t)f * P + p]);
+    int32_t mf = 0; uint64_t mm = 0;
+    int st = synctest_advance_frame(&s, &rv, &mf, &mm);
+    if (st == 1) { res->status = 1; res->mismatch_frame = mf; res->mismatch_mask = mm; break; }
+    if (st < 0) { res->status = -1; break; }
+    pw_handle_requests(&g, store, has, &s.sl, &rv, P, f == corrupt_frame);
+    if (ck_trace) {
+      const Cell* c = sl_saved_state_by_frame(&s.sl, f);
+      ck_trace[f] = c ? c->checksum : 0;
+    }
+    res->frames_done = f + 1;
+  }
+  if (final_state) pstate_serialize(&g, final_state);
+  size_t sb = pstate_bytes(N);
+  for (size_t i = 0; i < R; i++) {
+    if (ring_frames) ring_frames[i] = s.sl.cells[i].frame;
+    if (ring_cksums) ring_cksums[i] = s.sl.cells[i].has_checksum ? s.sl.cells[i].checksum : 0;
+    if (ring_states) { if (has[i]) pstate_serialize(&store[i], ring_states + i * sb); else memset(ring_states + i * sb, 0, sb); }
+    if (has[i]) pstate_free(&store[i]);
+  }
+  free(store); free(has); free(rv.v);
+  pstate_free(&g);
+  synctest_free(&s);
   return 0;
 }

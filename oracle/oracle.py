@@ -83,6 +83,11 @@ def lib():
         L.oracle_p2p_replay.argtypes = [ctypes.c_int32, u8p, ctypes.c_int32, ctypes.c_int32,
                                          ctypes.c_int32, u8p, u8p, u8p, u16p, u8p]
         L.oracle_p2p_replay.restype = ctypes.c_int
+        L.oracle_particles_synctest_run.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                                     ctypes.c_int32, ctypes.c_uint64, ctypes.c_int32,
+                                                     u8p, ctypes.c_int32, u16p, u8p, i32p, u16p, u8p,
+                                                     P(SyncTestResult)]
+        L.oracle_particles_synctest_run.restype = ctypes.c_int
         L.oracle_input_queue_sequence.argtypes = [ctypes.c_int32, ctypes.c_int32, i32p, u8p,
                                                   ctypes.c_int, i32p, u8p, i32p]
         _lib = L
@@ -192,6 +197,28 @@ def p2p_replay(state, load_frame, inputs, max_prediction=None, status=None):
     if rc != 0:
         raise ValueError("bad p2p replay arguments")
     return states, cks, final
+
+
+def particles_synctest_run(inputs, num_entities, num_players=2, max_prediction=17,
+                           check_distance=16, session=0, corrupt_frame=-1, ring_states=True):
+    """SyncTest over the config-5 particle world for one session (see particles.h for the game)."""
+    inputs = np.ascontiguousarray(inputs, np.uint8).reshape(-1, num_players)
+    frames = inputs.shape[0]
+    R = max_prediction + 1
+    sb = 4 + 100 * num_entities
+    res = SyncTestResult()
+    out = dict(ck_trace=np.zeros(frames, np.uint16), final_state=np.zeros(sb, np.uint8),
+               ring_frames=np.zeros(R, np.int32), ring_cksums=np.zeros(R, np.uint16),
+               ring_states=np.zeros((R, sb), np.uint8) if ring_states else None)
+    rc = lib().oracle_particles_synctest_run(
+        num_entities, num_players, max_prediction, check_distance, session, frames,
+        _ptr(inputs, ctypes.c_uint8), corrupt_frame, _ptr(out["ck_trace"], ctypes.c_uint16),
+        _ptr(out["final_state"], ctypes.c_uint8), _ptr(out["ring_frames"], ctypes.c_int32),
+        _ptr(out["ring_cksums"], ctypes.c_uint16), _ptr(out["ring_states"], ctypes.c_uint8),
+        ctypes.byref(res))
+    out["rc"] = rc
+    out["result"] = res
+    return out
 
 
 def sincos_digest(lo, hi, threads=8):
