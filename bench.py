@@ -164,6 +164,79 @@ def run_branch(args):
         dist.destroy_process_group()
 
 
+def run_particles(args):
+    """Config 5: SyncTest (check_distance 16, max_prediction 17) on 1 MB particle-world states;
+    one step = one SyncTest frame on every session (1 load + 16 resimulated advances with 16 saves
+    + the new advance), so every Load/Save streams through HBM."""
+    world, rank, local_rank, torch, dist = setup_dist(args)
+    from ggrs_amd import ParticleEngine, synth
+    S = args.sessions or 8192
+    N, P, maxp, cd = 10000, 2, 17, 16
+    warm = max(args.warmup, cd + 2)
+    frames = warm + args.steps
+    inputs = synth.gen_inputs(rank * S, S, frames, P, synth.MODEL_HELD)
+    eng = ParticleEngine(S, N, P, maxp, cd, input_capacity=frames + cd + 2, device=local_rank,
+                         first_session_id=rank * S)
+    eng.add_local_inputs(inputs)
+    for _ in range(warm):
+        eng.synctest_advance_frames(1)
+    eng.synchronize()
+    if dist is not None:
+        dist.barrier()
+    eng.timing_reset()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.synctest_advance_frames(1)
+    eng.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t1 = time.perf_counter()
+    kernel_ms, launches = eng.timing_read()
+    elapsed = t1 - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    st, _, _ = eng.mismatches()
+    value = S * cd * args.steps * world / elapsed
+    Sb = 4 + 100 * N
+    bytes_launch = S * (Sb + cd * (Sb + 2) + 2 + 4 * (cd - 1) + (cd + 1) * P)
+    avg_s = kernel_ms / 1e3 / max(launches, 1)
+    achieved = bytes_launch / avg_s / 1e9
+    parity = None
+    if rank == 0:
+        try:
+            from oracle import oracle as O
+            O.build()
+            r = O.particles_synctest_run(inputs[:, 0, :], N, P, maxp, cd, session=0, ring_states=False)
+            parity = {"session0_final_state_bit_exact": bytes(eng.state(0)) == bytes(r["final_state"]),
+                      "session0_ring_checksums": all(
+                          eng.saved(0, int(fr), with_state=False)[0] == int(ck)
+                          for fr, ck in zip(r["ring_frames"], r["ring_cksums"]) if fr >= 0)}
+        except Exception as exc:
+            parity = {"error": repr(exc)}
+        line = {
+            "metric": "resimulated session-frames/sec (node)", "value": round(value, 1),
+            "unit": "session-frames/s", "n_gpus": world, "steps": args.steps, "warmup": warm,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "config5: particle world, 10k entities x 100 B (~1 MB) per session, "
+                                   "SyncTest check_distance 16 / max_prediction 17 (ring 17 x 1 MB)",
+                       "sessions_per_gpu": S, "entities": N, "players": P, "check_distance": cd,
+                       "hbm_ring_gb_per_gpu": round(S * Sb * (maxp + 1) / 1e9, 2),
+                       "parallelism": f"sessions sharded over {world} GPU(s)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                         "traffic": pmc_traffic(f"config5_s{S}"),
+                         "algorithmic_bytes_per_launch": bytes_launch,
+                         "avg_launch_ms": round(avg_s * 1e3, 4)},
+            "cpu_baseline": None, "halted_lanes": int((st != 0).sum()), "parity": parity,
+        }
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -176,12 +249,16 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--path", choices=["pipelined", "sequential", "pipelined-whole"], default="pipelined",
                     help="SyncTest kernel (DESIGN.md section 3)")
-    ap.add_argument("--config", type=int, choices=[2, 3, 4], default=2,
-                    help="BASELINE.json config: 2 = SyncTest (default), 3/4 = branch rollback")
+    ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=2,
+                    help="BASELINE.json config: 2 = SyncTest (default), 3/4 = branch rollback, "
+                         "5 = 1 MB particle-world SyncTest")
+    ap.add_argument("--sessions", type=int, default=0, help="config 5: sessions per GPU (0 = 8192)")
     ap.add_argument("--peers", action="store_true",
                     help="configs 3/4: rank r and r + world/2 replay the same sessions (the two "
                          "machines of a match) and compare checksums after each all-gather")
     args = ap.parse_args()
+    if args.config == 5:
+        return run_particles(args)
     if args.config != 2:
         return run_branch(args)
 
