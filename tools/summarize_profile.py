@@ -6,7 +6,7 @@ HBM bytes follow MI355X_MICROARCH.md "HBM": FETCH_SIZE / WRITE_SIZE are KiB from
 memory-side request counters (TCC_EA0_RDREQ/WRREQ); on gfx950 FETCH_SIZE reports exactly half the
 bytes of a wide streaming read, so the corrected figure doubles it.  Both are kept.
 
-    python tools/summarize_profile.py r01 config2_l4096_f128
+    python tools/summarize_profile.py <tag> <workload> <kernel substring> [last K dispatches]
 """
 import collections
 import csv
@@ -18,28 +18,45 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def pmc_means(path, kernel_substr):
-    agg = collections.defaultdict(list)
+def pmc_means(path, kernel_substr, last=0):
+    """Per-counter mean over the kernel's dispatches (the last `last` ones if last > 0)."""
+    per = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         if kernel_substr in r["Kernel_Name"]:
-            agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in agg.items()}, {k: len(v) for k, v in agg.items()}
+            per[r["Counter_Name"]].append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
+    out, n = {}, {}
+    for k, v in per.items():
+        v.sort()
+        vals = [x for _, x in (v[-last:] if last else v)]
+        out[k], n[k] = sum(vals) / len(vals), len(vals)
+    return out, n
 
 
-def main(tag, workload, kernel="synctest_kernel"):
+def trace_mean_ns(path, kernel_substr, last=0):
+    rows = [r for r in csv.DictReader(open(path)) if kernel_substr in r["Kernel_Name"]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    if last:
+        rows = rows[-last:]
+    d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
+    return sum(d) / len(d), len(d)
+
+
+def main(tag, workload, kernel="synctest_kernel", last="0"):
+    last = int(last)
     src = os.path.join(ROOT, "gpurun_out", tag)
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "trace_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
     stats = {r["Name"]: r for r in csv.DictReader(open(os.path.join(dst, "kernel_stats.csv")))}
     kname = next(n for n in stats if kernel in n)
-    avg_ns = float(stats[kname]["AverageNs"])
-    out = {"tag": tag, "workload": workload, "kernel": kname, "calls": int(stats[kname]["Calls"]),
-           "avg_duration_ns": avg_ns}
+    avg_ns, ncalls = trace_mean_ns(os.path.join(src, "trace", "trace_kernel_trace.csv"), kernel, last)
+    out = {"tag": tag, "workload": workload, "kernel": kname, "calls_in_trace": int(stats[kname]["Calls"]),
+           "dispatches_averaged": ncalls, "avg_duration_ns": avg_ns,
+           "note": f"averages over the last {last} dispatches (the timed steps)" if last else "all dispatches"}
     for group in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_grbm"):
         p = os.path.join(src, group, "pmc_counter_collection.csv")
         if os.path.exists(p):
-            means, counts = pmc_means(p, kernel)
+            means, counts = pmc_means(p, kernel, last)
             out[group] = means
     fetch_kib = out.get("pmc_fetch", {}).get("FETCH_SIZE")
     write_kib = out.get("pmc_write", {}).get("WRITE_SIZE")
