@@ -325,6 +325,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_split_kernel(PipePar
   int32_t slot_r = g0 % R;       // ring slot of frame gf
   int32_t slot_k = g0 % K;       // chain slot (lane group) of chain gf
   int32_t slot_t = p.trace_cap ? (p.f0 - K) % p.trace_cap : 0;  // trace slot of chain t - K (f0 >= K)
+  const uint32_t corrupt_on = (p.corrupt_frame >= 0 && s == p.corrupt_lane && pl == 0) ? 1u : 0u;
   for (int32_t t = p.f0; t < t_end; ++t) {
     const int32_t c = t - i;
     const bool active = valid && c >= p.f0 && c < p.f0 + p.n;
@@ -339,17 +340,20 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_split_kernel(PipePar
       }
       __syncthreads();
     }
-    const uint32_t in = lds_in[(rel & (kStageFrames - 1)) * row + g * Pp + pl];
-    // Fletcher-16 of the registers as they stand: the cell this chain saves now (i >= 1) or, on a
-    // lane about to start a chain (i == 0), the final state of the chain that ended last step --
-    // its display checksum (ex_game.rs:121-126).
-    const uint16_t ck = chain_fletcher<P, Pp>(frame, w, pl);
-    const uint16_t first_here = (uint16_t)__shfl((int)ck, base + slot_k * Pp, kWave);
+    // (1) LoadGameState hand-off: the cell chain c-1 saves in this step, from its lane's registers
     uint32_t from[6];
     from[0] = (uint32_t)__shfl((int)frame, src_prev, kWave);
 #pragma unroll
     for (int q = 0; q < 5; q++) from[q + 1] = (uint32_t)__shfl((int)w[q], src_prev, kWave);
-    if (active && i > 0) {  // SaveGameState(gf)
+    const uint32_t in = lds_in[(rel & (kStageFrames - 1)) * row + g * Pp + pl];
+    // (2) Fletcher-16 of the registers as they stand: the cell this chain saves now (i >= 1) or, on
+    // a lane about to start a chain (i == 0), the final state of the chain that ended last step --
+    // its display checksum (ex_game.rs:121-126); plus chain gf's value: the first-seen checksum
+    const uint16_t ck = chain_fletcher<P, Pp>(frame, w, pl);
+    uint16_t first = (uint16_t)__shfl((int)ck, base + slot_k * Pp, kWave);
+    if (rel < cd) first = lds_first[rel * kWave + g];  // frame gf was saved by the previous launch
+    // (3) SaveGameState(gf) on every chain past its load
+    if (active && i > 0) {
       uint32_t* cell = p.ring + (int64_t)slot_r * F * L + s;
       if (owner) {
         cell[kx * L] = w[0];
@@ -361,57 +365,53 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_split_kernel(PipePar
       if (pl == 0) {
         cell[0] = frame;
         p.ring_ck[(int64_t)slot_r * L + s] = ck;
-        if (i < cd) {  // checksums_consistent(gf) at call c+1
-          const uint16_t first = gf >= p.f0 ? first_here : lds_first[rel * kWave + g];
-          if (ck != first) mask |= 1ull << (i - 1);
-        } else {
-          p.first_ck[(int64_t)slot_r * L + s] = ck;
-        }
+        if (i == cd) p.first_ck[(int64_t)slot_r * L + s] = ck;
       }
     }
-    if (i == 0) {
-      if (p.trace && valid && pl == 0 && c - K >= p.f0 && c - K < p.f0 + p.n)
-        p.trace[(int64_t)slot_t * L + s] = ck;
-      // LoadGameState(c - cd): the cell chain c-1 saves in this step (HBM for a launch's first chain)
-      if (c == p.f0) {
+    // checksums_consistent(gf) at call c+1 for the re-saves (i in 1..cd-1), branch-free
+    const bool cmp = active && pl == 0 && i > 0 && i < cd && ck != first;
+    mask = (i == 0 ? 0ull : mask) | ((uint64_t)cmp << ((i - 1) & 63));
+    if (i == 0 && p.trace && valid && pl == 0 && c - K >= p.f0 && c - K < p.f0 + p.n)
+      p.trace[(int64_t)slot_t * L + s] = ck;
+    // (4) the chain starting now takes the loaded cell (the launch's first chain: from HBM via LDS)
+    if (t == p.f0) {
+      if (i == 0) {
         frame = lds_cell[wl * 6];
 #pragma unroll
         for (int q = 0; q < 5; q++) w[q] = lds_cell[wl * 6 + 1 + q];
-      } else {
-        frame = from[0];
+      }
+    } else {
+      frame = i == 0 ? from[0] : frame;
 #pragma unroll
-        for (int q = 0; q < 5; q++) w[q] = from[q + 1];
-      }
-      if (s == p.corrupt_lane && c == p.corrupt_frame && pl == 0) w[0] ^= 1u;
-      mask = 0;
+      for (int q = 0; q < 5; q++) w[q] = i == 0 ? from[q + 1] : w[q];
     }
-    if (active) {  // AdvanceFrame with the input of frame gf
-      frame = (uint32_t)((int32_t)frame + 1);
-      if (owner) {
-        float x = __builtin_bit_cast(float, w[0]), y = __builtin_bit_cast(float, w[1]);
-        float vx = __builtin_bit_cast(float, w[2]), vy = __builtin_bit_cast(float, w[3]);
-        float rot = __builtin_bit_cast(float, w[4]);
-        advance_player(x, y, vx, vy, rot, in);
-        w[0] = __builtin_bit_cast(uint32_t, x);
-        w[1] = __builtin_bit_cast(uint32_t, y);
-        w[2] = __builtin_bit_cast(uint32_t, vx);
-        w[3] = __builtin_bit_cast(uint32_t, vy);
-        w[4] = __builtin_bit_cast(uint32_t, rot);
-      }
-      if (i == cd) {
-        if (c == p.f0 + p.n - 1) {
-          uint32_t* cur = p.cur + s;
-          if (owner) {
-            cur[kx * L] = w[0];
-            cur[ky * L] = w[1];
-            cur[kvx * L] = w[2];
-            cur[kvy * L] = w[3];
-            cur[krot * L] = w[4];
-          }
-          if (pl == 0) cur[0] = frame;
+    w[0] ^= (i == 0 && c == p.corrupt_frame) ? corrupt_on : 0u;
+    // (5) AdvanceFrame(gf) -- on every lane (idle lanes hold finite states; their result is unused)
+    frame = (uint32_t)((int32_t)frame + 1);
+    {
+      float x = __builtin_bit_cast(float, w[0]), y = __builtin_bit_cast(float, w[1]);
+      float vx = __builtin_bit_cast(float, w[2]), vy = __builtin_bit_cast(float, w[3]);
+      float rot = __builtin_bit_cast(float, w[4]);
+      advance_player(x, y, vx, vy, rot, in);
+      w[0] = __builtin_bit_cast(uint32_t, x);
+      w[1] = __builtin_bit_cast(uint32_t, y);
+      w[2] = __builtin_bit_cast(uint32_t, vx);
+      w[3] = __builtin_bit_cast(uint32_t, vy);
+      w[4] = __builtin_bit_cast(uint32_t, rot);
+    }
+    if (active && i == cd) {  // chain end
+      if (c == p.f0 + p.n - 1) {
+        uint32_t* cur = p.cur + s;
+        if (owner) {
+          cur[kx * L] = w[0];
+          cur[ky * L] = w[1];
+          cur[kvx * L] = w[2];
+          cur[kvy * L] = w[3];
+          cur[krot * L] = w[4];
         }
-        if (pl == 0 && mask) atomicCAS(p.fail_f0, -1, p.f0);
+        if (pl == 0) cur[0] = frame;
       }
+      if (pl == 0 && mask) atomicCAS(p.fail_f0, -1, p.f0);
     }
     i = i + 1 == K ? 0 : i + 1;
     slot_r = slot_r + 1 == R ? 0 : slot_r + 1;
