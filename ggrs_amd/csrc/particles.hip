@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <array>
+#include <cstdlib>
 #include <cstring>
 #include <utility>
 #include <vector>
@@ -36,6 +37,7 @@ struct PWParams {
   int64_t L;
   int32_t N, R, cd, f0, n, cap, P;
   int32_t corrupt_lane, corrupt_frame;
+  int32_t nt_saves;
   uint32_t* cur;
   int32_t* cur_frame;
   uint32_t* ring;
@@ -75,10 +77,19 @@ __device__ inline void load_quad(uint32_t (&w)[4][kFields], const uint32_t* base
     w[3][k] = v.w;
   }
 }
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ inline void store_quad(const uint32_t (&w)[4][kFields], uint32_t* base, int32_t N, int32_t q) {
 #pragma unroll
   for (int k = 0; k < kFields; k++)
     *reinterpret_cast<uint4*>(base + (size_t)k * N + 4 * q) = make_uint4(w[0][k], w[1][k], w[2][k], w[3][k]);
+}
+// ring saves are write-once-per-call streams far larger than any cache: non-temporal stores
+__device__ inline void store_quad_nt(const uint32_t (&w)[4][kFields], uint32_t* base, int32_t N, int32_t q) {
+#pragma unroll
+  for (int k = 0; k < kFields; k++) {
+    u32x4 v = {w[0][k], w[1][k], w[2][k], w[3][k]};
+    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(base + (size_t)k * N + 4 * q));
+  }
 }
 __device__ inline void advance_quad(uint32_t (&w)[4][kFields], uint32_t in_word, int32_t P, int32_t e0) {
 #pragma unroll
@@ -188,7 +199,8 @@ __global__ __launch_bounds__(kBlock) void pw_synctest_kernel(PWParams p) {
         if (cd > 0 && (i > 0 || !replay)) {  // SaveGameState(g): the replay's saves, then save current
           FletcherAcc a{0, 0, 0};
           if (on) {
-            store_quad(w, p.ring + ((size_t)(g % R) * L + s) * rec, N, q);
+            if (p.nt_saves) store_quad_nt(w, p.ring + ((size_t)(g % R) * L + s) * rec, N, q);
+            else store_quad(w, p.ring + ((size_t)(g % R) * L + s) * rec, N, q);
             fletcher_quad(a, w, N, e0);
           }
           wave_accumulate(a, lds_acc[wave][i]);
@@ -237,6 +249,7 @@ struct ggrs_particle_engine {
   size_t staging_bytes = 0;
   int32_t current_frame = 0, next_input_frame = 0;
   int32_t corrupt_lane = -1, corrupt_frame = -1;
+  int32_t nt_saves = 1;  // GGRS_PW_STORE=plain selects plain stores for the ring saves
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<hipEvent_t> tev;
   size_t tev_used = 0;
@@ -291,6 +304,7 @@ int ggrs_particle_engine_create(const ggrs_particle_config_t* cfg, ggrs_particle
   e->cfg = c;
   e->R = c.max_prediction + 1;
   e->cap = c.input_capacity ? c.input_capacity : 128;
+  if (const char* sp = getenv("GGRS_PW_STORE")) e->nt_saves = strcmp(sp, "plain") != 0;
   e->cfg.input_capacity = e->cap;
   if (e->cap < c.check_distance + 2) {
     delete e;
@@ -389,6 +403,7 @@ int ggrs_particle_synctest_advance_frames(ggrs_particle_engine_t* e, int32_t n) 
   p.P = e->cfg.num_players;
   p.corrupt_lane = e->corrupt_lane;
   p.corrupt_frame = e->corrupt_frame;
+  p.nt_saves = e->nt_saves;
   p.cur = e->cur;
   p.cur_frame = e->cur_frame;
   p.ring = e->ring;
