@@ -237,6 +237,116 @@ def run_particles(args):
         dist.destroy_process_group()
 
 
+def run_p2p(args):
+    """P2P rollback decision on the device (ggrs_p2p_*): S sessions of one peer, 2 players (one
+    remote, inputs arrive 4 frames late), max_prediction 8, held-key inputs.  One step = 64
+    advance_frame calls on every session: poll, misprediction check, rollback + resimulation
+    where the session's prediction failed, save, advance."""
+    world, rank, local_rank, torch, dist = setup_dist(args)
+    from ggrs_amd import P2PEngine, synth
+    S = args.sessions or 65536
+    P, D, maxp, calls = 2, 4, 8, 64
+    frames = (args.warmup + args.steps) * calls
+    rows = synth.gen_inputs(rank * S, S, frames, P, synth.MODEL_HELD)
+    eng = P2PEngine(S, num_players=P, local_players=(0,), input_delay=0, max_prediction=maxp,
+                    remote_latency=D, input_capacity=frames + D + 2, device=local_rank)
+    eng.add_inputs(0, rows)
+    eng.synchronize()
+    for _ in range(args.warmup):
+        eng.advance_frames(calls)
+    eng.synchronize()
+    rb0, rs0 = eng.stats()
+    if dist is not None:
+        dist.barrier()
+    eng.timing_reset()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.advance_frames(calls)
+    eng.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t1 = time.perf_counter()
+    kernel_ms, launches = eng.timing_read()
+    elapsed = t1 - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    rb1, rs1 = eng.stats()
+    resim = int((rs1 - rs0).sum())
+    rollbacks = int((rb1 - rb0).sum())
+    session_calls = S * calls * args.steps
+    value = session_calls * world / elapsed
+    F = 5 * P + 1
+    # HBM bytes per launch: the state in/out, every save (state + checksum), every rollback load,
+    # the queue words in/out and the input rows each call reads (arrival + its own, + replays)
+    bytes_launch = (2 * 4 * F * S + (session_calls // args.steps) * (4 * F + 2) * 1
+                    + (rollbacks // args.steps) * (4 * F + (D - 1) * (4 * F + 2))
+                    + 2 * 16 * P * S + (session_calls // args.steps) * 2 * 2 + (resim // args.steps) * 2 * 2)
+    avg_s = kernel_ms / 1e3 / max(launches, 1)
+    achieved = bytes_launch / avg_s / 1e9
+    parity = cpu_baseline = None
+    if rank == 0:
+        try:
+            from oracle import oracle as O
+            O.build()
+            ok = True
+            for s in (0, 1, S // 2, S - 1):
+                r = O.p2p_run(rows[:, s], num_players=P, local_mask=0b01, max_prediction=maxp, latency=D)
+                ok &= bytes(eng.state(s)) == bytes(r["final_state"]) and int(rb1[s]) == r["result"].rollbacks
+            parity = {"sessions_0_1_mid_last_bit_exact": bool(ok)}
+            if world == 1 and not args.no_cpu_baseline:
+                cpu_baseline = p2p_cpu_baseline(args, O, synth, P, D, maxp)
+        except Exception as exc:
+            parity = {"error": repr(exc)}
+        line = {
+            "metric": "P2P session-frames/sec (node)", "value": round(value, 1),
+            "unit": "session-frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"p2p: {S} sessions per GPU, 2 players (1 remote, inputs {D} frames "
+                                   f"late), max_prediction {maxp}, held-key inputs, {calls} calls per step",
+                       "sessions_per_gpu": S, "parallelism": f"sessions sharded over {world} GPU(s)"},
+            "rollbacks_per_session_frame": round(rollbacks / session_calls, 5),
+            "advances_per_sec": round((session_calls + resim) * world / elapsed, 1),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                         "traffic": pmc_traffic(f"p2p_s{S}"),
+                         "algorithmic_bytes_per_launch": bytes_launch,
+                         "avg_launch_ms": round(avg_s * 1e3, 4)},
+            "cpu_baseline": cpu_baseline, "parity": parity,
+        }
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def p2p_cpu_baseline(args, O, synth, P, D, maxp):
+    """The oracle's P2P session (C restatement of p2p_session.rs:265-426 + ex_game) on T host
+    threads, one session per thread (ctypes drops the GIL for the call)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import numpy as np
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    T = args.cpu_threads or min(16, avail)
+    frames = 2_000_000
+    rows = synth.gen_inputs(0, T, frames, P, synth.MODEL_HELD)
+    per = [np.ascontiguousarray(rows[:, t]) for t in range(T)]
+    del rows
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(T) as ex:
+        res = list(ex.map(lambda a: O.p2p_run(a, num_players=P, local_mask=0b01, max_prediction=maxp,
+                                              latency=D)["rc"], per))
+    wall = time.perf_counter() - t0
+    return {"value": round(T * frames / wall, 1), "unit": "session-frames/s", "cores": T, "kind": "port",
+            "sample": f"{T} threads x {frames} P2P advance_frame calls (1 session/thread, same game, "
+                      f"latency {D}, held-key inputs), C restatement oracle/ggrs_oracle.c oracle_p2p_run",
+            "wall_s": round(wall, 3), "all_ok": all(r == 0 for r in res)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -256,7 +366,11 @@ def main():
     ap.add_argument("--peers", action="store_true",
                     help="configs 3/4: rank r and r + world/2 replay the same sessions (the two "
                          "machines of a match) and compare checksums after each all-gather")
+    ap.add_argument("--workload", choices=["synctest", "p2p"], default="synctest",
+                    help="p2p: the device P2P rollback decision (SURVEY.md 8f), --sessions per GPU")
     args = ap.parse_args()
+    if args.workload == "p2p":
+        return run_p2p(args)
     if args.config == 5:
         return run_particles(args)
     if args.config != 2:

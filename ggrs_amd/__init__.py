@@ -10,5 +10,6 @@ from .session import (AdvanceFrame, BoxGameHandler, Engine, LoadGameState,  # no
 
 from .branch import BranchEngine  # noqa: F401
 from .particles import ParticleEngine  # noqa: F401
+from .p2p import P2PEngine  # noqa: F401
 
 __version__ = "0.1.0"

@@ -1,0 +1,528 @@
+// p2p.hip -- the P2P rollback decision on the device: one peer's P2PSession::advance_frame
+// (src/sessions/p2p_session.rs:265-426) for S independent sessions, one thread per session,
+// with the remote players' InputQueue prediction (src/input_queue.rs:104-230) kept per session in
+// registers.  Network model (the oracle's, oracle/ggrs_oracle.c oracle_p2p_run): the remote
+// players' input of frame g arrives at the start of call g + D (D = remote_latency); local
+// players' inputs enter every call with the session's input delay.
+//
+// What a call does for every session (rollback mode, sparse saving off, every player connected):
+//   1. poll: each remote queue gets frame g = f - D (add_input_by_frame, input_queue.rs:190-230):
+//      a prediction that disagrees sets first_incorrect_frame = g;
+//   2. f == 0: SaveGameState(0)  (:305-308);
+//   3. first_incorrect = min over queues (check_simulation_consistency, sync_layer.rs:343-353);
+//      if set: LoadGameState(first_incorrect), reset_prediction, then (Save unless first, Advance)
+//      for frames first_incorrect .. f-1 with synchronized_inputs (adjust_gamestate :658-714);
+//   4. SaveGameState(f) (:337);
+//   5. AdvanceFrame with synchronized_inputs(f): local inputs confirmed (queue frame f holds user
+//      input f - delay, the default input below the delay), remote inputs predicted.
+// D < max_prediction is required, so the prediction threshold (:400-421) never stops a call and
+// every confirmed frame the reference would discard is older than anything read again.
+//
+// Because the remote input of frame g arrives exactly at call g + D, a rollback always loads
+// frame f - D; which sessions roll back is decided per session by its own predictions.
+//
+// HBM layout (session-fastest SoA, as the SyncTest engine):
+//   cur      [F][S]     u32   state after the last call
+//   ring     [R][F][S]  u32   R = max_prediction + 1, slot = frame % R (sync_layer.rs:161-166)
+//   ring_ck  [R][S]     u16   fletcher16 handed to GameStateCell::save
+//   inputs   [C][S][Pp] u8    row g: local add_local_input of call g, remote inputs of frame g
+//   queue    [4][P][S]  i32   prediction.frame, prediction.input, first_incorrect, last_requested
+//   stats    rollbacks [S] i32, resim [S] i64
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.h"
+
+#pragma clang fp contract(off)
+
+using namespace ggrs;
+
+namespace {
+
+constexpr int32_t kNull = -1;  // NULL_FRAME (src/lib.rs:44)
+
+struct P2PParams {
+  int64_t S;
+  int32_t R, D, delay, cap, trace_cap, f0, n, predictor;
+  uint32_t local_mask;
+  uint32_t* cur;
+  uint32_t* ring;
+  uint16_t* ring_ck;
+  const uint8_t* inputs;
+  int32_t* queue;
+  int32_t* rollbacks;
+  int64_t* resim;
+  uint16_t* trace;
+};
+
+// The per-session state of every remote player's InputQueue that the P2P program reads.
+template <int P>
+struct RemoteQueues {
+  int32_t pred_frame[P];  // prediction.frame (NULL: not predicting)
+  uint32_t pred_in[P];    // prediction.input
+  int32_t first_inc[P];   // first_incorrect_frame
+  int32_t last_req[P];    // last_requested_frame
+};
+
+template <int P>
+__device__ inline void save_cell(const P2PParams& p, const BoxState<P>& s, int32_t frame, int64_t sess) {
+  const int32_t slot = frame % p.R;
+  store_state<P>(s, p.ring + (int64_t)slot * state_fields(P) * p.S + sess, p.S);
+  p.ring_ck[(int64_t)slot * p.S + sess] = fletcher16_state<P>(s);
+}
+
+template <int P>
+__device__ inline uint32_t input_row(const P2PParams& p, int32_t g, int64_t sess) {
+  return load_inputs<P>(p.inputs, (int64_t)(g % p.cap) * p.S + sess);
+}
+
+// synchronized_inputs(h) (sync_layer.rs:280-293) with InputQueue::input (input_queue.rs:104-167).
+// last_added: the remote queues' last_added_frame (f - D after this call's poll, or NULL).
+template <int P>
+__device__ inline uint32_t sync_inputs(const P2PParams& p, RemoteQueues<P>& q, int32_t h, int32_t last_added,
+                                       int64_t sess) {
+  uint32_t in = 0;
+  // local queues hold every frame <= f + delay: queue frame h is user input h - delay, and the
+  // frames below the delay replicate the default input (input_queue.rs:233-265)
+  const uint32_t local_row = (p.local_mask && h >= p.delay) ? input_row<P>(p, h - p.delay, sess) : 0u;
+  uint32_t confirmed_row = 0u, last_row = 0u;
+  const bool confirmed = last_added != kNull && h <= last_added;
+  if (confirmed) confirmed_row = input_row<P>(p, h, sess);
+  else if (last_added != kNull && h != 0) last_row = input_row<P>(p, last_added, sess);
+#pragma unroll
+  for (int k = 0; k < P; k++) {
+    uint32_t v;
+    if ((p.local_mask >> k) & 1u) {
+      v = (local_row >> (8 * k)) & 0xffu;
+    } else {
+      q.last_req[k] = h;
+      if (q.pred_frame[k] < 0) {
+        if (confirmed) {  // the queue holds frame h
+          in |= ((confirmed_row >> (8 * k)) & 0xffu) << (8 * k);
+          continue;
+        }
+        const bool prev = !(h == 0 || last_added == kNull);
+        const uint32_t last = (last_row >> (8 * k)) & 0xffu;
+        q.pred_in[k] = prev ? (p.predictor == 0 ? last : 0u) : 0u;  // lib.rs:390-406, unwrap_or_default
+        q.pred_frame[k] = (prev ? last_added : kNull) + 1;
+      }
+      v = q.pred_in[k];
+    }
+    in |= v << (8 * k);
+  }
+  return in;
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void p2p_kernel(P2PParams p) {
+  const int64_t sess = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (sess >= p.S) return;
+  const int64_t S = p.S;
+  BoxState<P> st;
+  load_state<P>(st, p.cur + sess, S);
+  RemoteQueues<P> q;
+#pragma unroll
+  for (int k = 0; k < P; k++) {
+    q.pred_frame[k] = p.queue[(0 * P + k) * S + sess];
+    q.pred_in[k] = (uint32_t)p.queue[(1 * P + k) * S + sess];
+    q.first_inc[k] = p.queue[(2 * P + k) * S + sess];
+    q.last_req[k] = p.queue[(3 * P + k) * S + sess];
+  }
+  int32_t rollbacks = 0;
+  int64_t resim = 0;
+  for (int32_t f = p.f0; f < p.f0 + p.n; ++f) {
+    // 1. poll_remote_clients: the remote input of frame g = f - D (add_input_by_frame)
+    const int32_t g = f - p.D;
+    const int32_t last_added = g >= 0 ? g : kNull;
+    if (g >= 0) {
+      const uint32_t row = input_row<P>(p, g, sess);
+#pragma unroll
+      for (int k = 0; k < P; k++) {
+        if ((p.local_mask >> k) & 1u) continue;
+        if (q.pred_frame[k] != kNull) {
+          const uint32_t v = (row >> (8 * k)) & 0xffu;
+          if (q.first_inc[k] == kNull && q.pred_in[k] != v) q.first_inc[k] = g;
+          if (q.pred_frame[k] == q.last_req[k] && q.first_inc[k] == kNull) q.pred_frame[k] = kNull;
+          else q.pred_frame[k] += 1;
+        }
+      }
+    }
+    // 2. the first frame's save
+    if (f == 0) save_cell<P>(p, st, 0, sess);
+    // 3. check_simulation_consistency + adjust_gamestate
+    int32_t first_inc = kNull;
+#pragma unroll
+    for (int k = 0; k < P; k++)
+      if (q.first_inc[k] != kNull && (first_inc == kNull || q.first_inc[k] < first_inc)) first_inc = q.first_inc[k];
+    if (first_inc != kNull) {
+      load_state<P>(st, p.ring + (int64_t)(first_inc % p.R) * state_fields(P) * S + sess, S);
+#pragma unroll
+      for (int k = 0; k < P; k++) {  // reset_prediction (input_queue.rs:63-67)
+        q.pred_frame[k] = kNull;
+        q.first_inc[k] = kNull;
+        q.last_req[k] = kNull;
+      }
+      for (int32_t h = first_inc; h < f; ++h) {
+        const uint32_t in = sync_inputs<P>(p, q, h, last_added, sess);
+        if (h > first_inc) save_cell<P>(p, st, h, sess);
+        advance_state<P>(st, in, 0u);
+      }
+      rollbacks += 1;
+      resim += f - first_inc;
+    }
+    // 4. save the current frame; 5. advance with synchronized inputs
+    save_cell<P>(p, st, f, sess);
+    const uint32_t in = sync_inputs<P>(p, q, f, last_added, sess);
+    advance_state<P>(st, in, 0u);
+    if (p.trace) p.trace[(int64_t)(f % p.trace_cap) * S + sess] = fletcher16_state<P>(st);
+  }
+  store_state<P>(st, p.cur + sess, S);
+#pragma unroll
+  for (int k = 0; k < P; k++) {
+    p.queue[(0 * P + k) * S + sess] = q.pred_frame[k];
+    p.queue[(1 * P + k) * S + sess] = (int32_t)q.pred_in[k];
+    p.queue[(2 * P + k) * S + sess] = q.first_inc[k];
+    p.queue[(3 * P + k) * S + sess] = q.last_req[k];
+  }
+  p.rollbacks[sess] += rollbacks;
+  p.resim[sess] += resim;
+}
+
+// every queue starts empty: prediction.frame, first_incorrect, last_requested = NULL, input 0
+__global__ void init_queue_kernel(int32_t* queue, int64_t n_per_field, int32_t P) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 4 * n_per_field) return;
+  const int64_t field = i / n_per_field;
+  queue[i] = field == 1 ? 0 : kNull;
+  (void)P;
+}
+
+}  // namespace
+
+struct ggrs_p2p_engine {
+  ggrs_p2p_config_t cfg{};
+  int Pp = 1, F = 1, R = 2, cap = 256;
+  hipStream_t stream = nullptr;
+  uint32_t* cur = nullptr;
+  uint32_t* ring = nullptr;
+  uint16_t* ring_ck = nullptr;
+  uint8_t* inputs = nullptr;
+  int32_t* queue = nullptr;
+  int32_t* rollbacks = nullptr;
+  int64_t* resim = nullptr;
+  uint16_t* trace = nullptr;
+  uint8_t* staging = nullptr;
+  size_t staging_bytes = 0;
+  int32_t current_frame = 0;
+  int32_t next_input_frame = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::vector<hipEvent_t> tev;
+  size_t tev_used = 0;
+  bool collecting = false;
+};
+
+namespace {
+
+template <typename K>
+int p2p_launch_timed(ggrs_p2p_engine* e, K&& launch) {
+  hipEvent_t a = e->ev0, b = e->ev1;
+  if (e->collecting) {
+    while (e->tev.size() < e->tev_used + 2) {
+      hipEvent_t ev;
+      HIP_TRY(hipEventCreate(&ev));
+      e->tev.push_back(ev);
+    }
+    a = e->tev[e->tev_used];
+    b = e->tev[e->tev_used + 1];
+    e->tev_used += 2;
+  }
+  HIP_TRY(hipEventRecord(a, e->stream));
+  launch();
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(b, e->stream));
+  return GGRS_OK;
+}
+
+// oldest input row a call at frame f still reads: user input (f - D) - delay of the local
+// players' replay, and the remote input f - D
+int32_t oldest_row(const ggrs_p2p_engine* e, int32_t f) {
+  return std::max(0, f - e->cfg.remote_latency - e->cfg.input_delay);
+}
+
+}  // namespace
+
+extern "C" {
+
+int ggrs_p2p_engine_destroy(ggrs_p2p_engine_t* e) {
+  if (!e) return GGRS_OK;
+  (void)hipSetDevice(e->cfg.device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  void* bufs[] = {e->cur, e->ring, e->ring_ck, e->inputs, e->queue, e->rollbacks, e->resim, e->trace, e->staging};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  for (hipEvent_t ev : e->tev) (void)hipEventDestroy(ev);
+  if (e->ev0) (void)hipEventDestroy(e->ev0);
+  if (e->ev1) (void)hipEventDestroy(e->ev1);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+  return GGRS_OK;
+}
+
+int ggrs_p2p_engine_create(const ggrs_p2p_config_t* cfg, ggrs_p2p_engine_t** out) {
+  if (!cfg || !out) return set_error(GGRS_E_INVALID, "null argument");
+  *out = nullptr;
+  ggrs_p2p_config_t c = *cfg;
+  if (c.num_sessions < 1) return set_error(GGRS_E_INVALID, "num_sessions must be >= 1");
+  if (c.num_players < 1 || c.num_players > 4) return set_error(GGRS_E_INVALID, "num_players must be in 1..4 (ex_game.rs:70)");
+  if ((c.local_mask & ~((1 << c.num_players) - 1)) != 0)
+    return set_error(GGRS_E_INVALID, "local_mask names a player the session does not have");
+  if (c.local_mask == (1 << c.num_players) - 1)
+    return set_error(GGRS_E_INVALID, "a P2P session needs at least one remote player");
+  if (c.input_delay < 0) return set_error(GGRS_E_INVALID, "input_delay must be >= 0");
+  if (c.max_prediction < 1)
+    return set_error(GGRS_E_INVALID, "max_prediction must be >= 1 (0 is lockstep mode, which never rolls back)");
+  if (c.remote_latency < 1 || c.remote_latency >= c.max_prediction)
+    return set_error(GGRS_E_INVALID, "remote_latency must be in 1..max_prediction-1 (else the prediction threshold stalls)");
+  if (c.predictor != 0 && c.predictor != 1) return set_error(GGRS_E_INVALID, "predictor must be 0 (repeat last) or 1 (default)");
+  if (c.input_capacity == 0) c.input_capacity = 256;
+  if (c.input_capacity < c.remote_latency + c.input_delay + 2)
+    return set_error(GGRS_E_INVALID, "input_capacity must be >= remote_latency + input_delay + 2");
+  if (c.trace_capacity < 0) return set_error(GGRS_E_INVALID, "trace_capacity must be >= 0");
+  ggrs_p2p_engine* e = new ggrs_p2p_engine();
+  e->cfg = c;
+  e->Pp = padded_players(c.num_players);
+  e->F = state_fields(c.num_players);
+  e->R = c.max_prediction + 1;
+  e->cap = c.input_capacity;
+  auto fail = [&](int rc) {
+    std::string msg = ggrs_last_error();
+    ggrs_p2p_engine_destroy(e);
+    set_error(rc, "%s", msg.c_str());
+    return rc;
+  };
+#define CTRY(expr)                                                                      \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) return fail(set_error(GGRS_E_HIP, "%s: %s", #expr, hipGetErrorString(e_))); \
+  } while (0)
+  const int64_t S = c.num_sessions;
+  const int P = c.num_players;
+  CTRY(hipSetDevice(c.device));
+  CTRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+  CTRY(hipEventCreate(&e->ev0));
+  CTRY(hipEventCreate(&e->ev1));
+  CTRY(hipMalloc(&e->cur, sizeof(uint32_t) * e->F * S));
+  CTRY(hipMalloc(&e->ring, sizeof(uint32_t) * (size_t)e->R * e->F * S));
+  CTRY(hipMalloc(&e->ring_ck, sizeof(uint16_t) * (size_t)e->R * S));
+  CTRY(hipMalloc(&e->inputs, (size_t)e->cap * S * e->Pp));
+  CTRY(hipMalloc(&e->queue, sizeof(int32_t) * 4 * P * S));
+  CTRY(hipMalloc(&e->rollbacks, sizeof(int32_t) * S));
+  CTRY(hipMalloc(&e->resim, sizeof(int64_t) * S));
+  if (c.trace_capacity > 0) CTRY(hipMalloc(&e->trace, sizeof(uint16_t) * (size_t)c.trace_capacity * S));
+  CTRY(hipMemsetAsync(e->ring, 0, sizeof(uint32_t) * (size_t)e->R * e->F * S, e->stream));
+  CTRY(hipMemsetAsync(e->ring_ck, 0, sizeof(uint16_t) * (size_t)e->R * S, e->stream));
+  CTRY(hipMemsetAsync(e->inputs, 0, (size_t)e->cap * S * e->Pp, e->stream));
+  CTRY(hipMemsetAsync(e->rollbacks, 0, sizeof(int32_t) * S, e->stream));
+  CTRY(hipMemsetAsync(e->resim, 0, sizeof(int64_t) * S, e->stream));
+  if (e->trace) CTRY(hipMemsetAsync(e->trace, 0, sizeof(uint16_t) * (size_t)c.trace_capacity * S, e->stream));
+  init_queue_kernel<<<grid_of(4 * P * S, 256), 256, 0, e->stream>>>(e->queue, (int64_t)P * S, P);
+  dispatch_players(P, [&](auto PC) {
+    constexpr int PP = decltype(PC)::value;
+    init_states_kernel<PP><<<grid_of(S, 256), 256, 0, e->stream>>>(e->cur, S);
+  });
+  CTRY(hipGetLastError());
+  CTRY(hipStreamSynchronize(e->stream));
+#undef CTRY
+  *out = e;
+  return GGRS_OK;
+}
+
+int ggrs_p2p_engine_config(const ggrs_p2p_engine_t* e, ggrs_p2p_config_t* out) {
+  if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
+  *out = e->cfg;
+  return GGRS_OK;
+}
+
+int ggrs_p2p_add_inputs(ggrs_p2p_engine_t* e, int32_t first_frame, int32_t n, const uint8_t* inputs) {
+  if (!e || (!inputs && n > 0)) return set_error(GGRS_E_INVALID, "null argument");
+  if (n < 0) return set_error(GGRS_E_INVALID, "n_frames must be >= 0");
+  if (first_frame != e->next_input_frame)
+    return set_error(GGRS_E_INVALID, "inputs must be added sequentially (expected frame %d, got %d)",
+                     e->next_input_frame, first_frame);
+  if (n == 0) return GGRS_OK;
+  if ((int64_t)first_frame + n - 1 - oldest_row(e, e->current_frame) >= e->cap)
+    return set_error(GGRS_E_INVALID, "input queue full (capacity %d)", e->cap);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const int64_t S = e->cfg.num_sessions;
+  const int P = e->cfg.num_players;
+  const size_t bytes = (size_t)n * S * P;
+  if (bytes > e->staging_bytes) {
+    if (e->staging) HIP_TRY(hipFree(e->staging));
+    e->staging = nullptr;
+    e->staging_bytes = 0;
+    HIP_TRY(hipMalloc(&e->staging, bytes));
+    e->staging_bytes = bytes;
+  }
+  HIP_TRY(hipMemcpyAsync(e->staging, inputs, bytes, hipMemcpyHostToDevice, e->stream));
+  pack_inputs_kernel<<<grid_of((int64_t)n * S, 256), 256, 0, e->stream>>>(e->staging, e->inputs, S, P, e->Pp, n,
+                                                                          first_frame % e->cap, e->cap);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  e->next_input_frame = first_frame + n;
+  return GGRS_OK;
+}
+
+int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  if (n < 0) return set_error(GGRS_E_INVALID, "n_frames must be >= 0");
+  if (n == 0) return GGRS_OK;
+  if ((int64_t)e->current_frame + n > e->next_input_frame)
+    return set_error(GGRS_E_INVALID, "Missing local input: inputs are queued up to frame %d, calls need up to %d",
+                     e->next_input_frame - 1, e->current_frame + n - 1);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  P2PParams p;
+  p.S = e->cfg.num_sessions;
+  p.R = e->R;
+  p.D = e->cfg.remote_latency;
+  p.delay = e->cfg.input_delay;
+  p.cap = e->cap;
+  p.trace_cap = e->cfg.trace_capacity;
+  p.f0 = e->current_frame;
+  p.n = n;
+  p.predictor = e->cfg.predictor;
+  p.local_mask = (uint32_t)e->cfg.local_mask;
+  p.cur = e->cur;
+  p.ring = e->ring;
+  p.ring_ck = e->ring_ck;
+  p.inputs = e->inputs;
+  p.queue = e->queue;
+  p.rollbacks = e->rollbacks;
+  p.resim = e->resim;
+  p.trace = e->trace;
+  // rows the calls read must still be in the ring: rows >= oldest_row(f0) up to f0 + n - 1
+  if ((int64_t)p.f0 + n - 1 - oldest_row(e, p.f0) >= e->cap)
+    return set_error(GGRS_E_INVALID, "advance of %d frames reads more input rows than input_capacity (%d)", n, e->cap);
+  int rc = p2p_launch_timed(e, [&] {
+    dispatch_players(e->cfg.num_players, [&](auto PC) {
+      constexpr int P = decltype(PC)::value;
+      p2p_kernel<P><<<grid_of(p.S, 256), 256, 0, e->stream>>>(p);
+    });
+  });
+  if (rc) return rc;
+  e->current_frame += n;
+  return GGRS_OK;
+}
+
+int ggrs_p2p_current_frame(const ggrs_p2p_engine_t* e, int32_t* out) {
+  if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
+  *out = e->current_frame;
+  return GGRS_OK;
+}
+
+int ggrs_p2p_synchronize(ggrs_p2p_engine_t* e) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return GGRS_OK;
+}
+
+static int read_record(ggrs_p2p_engine_t* e, const uint32_t* base, int64_t s, uint8_t* out) {
+  const int64_t S = e->cfg.num_sessions;
+  std::vector<uint32_t> w(e->F);
+  for (int k = 0; k < e->F; k++)
+    HIP_TRY(hipMemcpyAsync(&w[k], base + (int64_t)k * S + s, 4, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  serialize_state_bytes(w.data(), e->cfg.num_players, out);
+  return GGRS_OK;
+}
+
+int ggrs_p2p_read_state(ggrs_p2p_engine_t* e, int32_t session, uint8_t* out) {
+  if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
+  if (session < 0 || session >= e->cfg.num_sessions) return set_error(GGRS_E_INVALID, "session out of range");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  return read_record(e, e->cur, session, out);
+}
+
+int ggrs_p2p_read_ring(ggrs_p2p_engine_t* e, int32_t session, int32_t* frames, uint16_t* checksums, uint8_t* states) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  if (session < 0 || session >= e->cfg.num_sessions) return set_error(GGRS_E_INVALID, "session out of range");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const int64_t S = e->cfg.num_sessions;
+  const int32_t R = e->R, f = e->current_frame;
+  const size_t sb = 36 + 20 * (size_t)e->cfg.num_players;
+  for (int32_t slot = 0; slot < R; slot++) {
+    // after call f-1 the cells hold frames f-R .. f-1 (every call saves its current frame)
+    int32_t fr = kNull;
+    for (int32_t g = f - 1; g >= 0 && g >= f - R; g--)
+      if (g % R == slot) { fr = g; break; }
+    if (frames) frames[slot] = fr;
+    if (checksums) {
+      checksums[slot] = 0;
+      if (fr != kNull)
+        HIP_TRY(hipMemcpy(&checksums[slot], e->ring_ck + (int64_t)slot * S + session, 2, hipMemcpyDeviceToHost));
+    }
+    if (states) {
+      if (fr == kNull) {
+        std::memset(states + slot * sb, 0, sb);
+      } else {
+        int rc = read_record(e, e->ring + (int64_t)slot * e->F * S, session, states + slot * sb);
+        if (rc) return rc;
+      }
+    }
+  }
+  return GGRS_OK;
+}
+
+int ggrs_p2p_read_stats(ggrs_p2p_engine_t* e, int32_t* rollbacks, int64_t* resim_frames) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const int64_t S = e->cfg.num_sessions;
+  if (rollbacks) HIP_TRY(hipMemcpyAsync(rollbacks, e->rollbacks, 4 * S, hipMemcpyDeviceToHost, e->stream));
+  if (resim_frames) HIP_TRY(hipMemcpyAsync(resim_frames, e->resim, 8 * S, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return GGRS_OK;
+}
+
+int ggrs_p2p_read_trace(ggrs_p2p_engine_t* e, int32_t first_frame, int32_t n, uint16_t* out) {
+  if (!e || (!out && n > 0)) return set_error(GGRS_E_INVALID, "null argument");
+  if (!e->trace) return set_error(GGRS_E_PRECONDITION, "engine created with trace_capacity 0");
+  const int32_t T = e->cfg.trace_capacity;
+  if (n < 0 || first_frame < 0 || first_frame + n > e->current_frame || first_frame + T < e->current_frame)
+    return set_error(GGRS_E_INVALID, "trace frames out of the retained range");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const int64_t S = e->cfg.num_sessions;
+  for (int32_t i = 0; i < n; i++)
+    HIP_TRY(hipMemcpyAsync(out + (int64_t)i * S, e->trace + (int64_t)((first_frame + i) % T) * S, 2 * S,
+                           hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return GGRS_OK;
+}
+
+int ggrs_p2p_timing_reset(ggrs_p2p_engine_t* e) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  e->tev_used = 0;
+  e->collecting = true;
+  return GGRS_OK;
+}
+
+int ggrs_p2p_timing_read(ggrs_p2p_engine_t* e, float* total_ms, int32_t* launches) {
+  if (!e || !total_ms || !launches) return set_error(GGRS_E_INVALID, "null argument");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  float total = 0.0f;
+  for (size_t i = 0; i + 1 < e->tev_used; i += 2) {
+    float ms = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&ms, e->tev[i], e->tev[i + 1]));
+    total += ms;
+  }
+  *total_ms = total;
+  *launches = (int32_t)(e->tev_used / 2);
+  e->collecting = false;
+  return GGRS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,149 @@
+"""P2P rollback decision over the engine's C ABI (include/ggrs_amd.h, ggrs_p2p_*).
+
+One P2PEngine holds S sessions of one peer.  Each call of advance_frames(n) runs n x
+P2PSession::advance_frame (src/sessions/p2p_session.rs:265-426) + the ex_game handler for every
+session: the remote players' inputs of frame f - remote_latency arrive, mispredictions found by
+InputQueue (src/input_queue.rs:190-230) roll the session back (adjust_gamestate, :658-714), the
+current frame is saved and advanced with synchronized inputs (remote players predicted,
+src/lib.rs:390-406).  The device decides per session whether and how far to roll back.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import InvalidRequest
+
+PREDICT_REPEAT_LAST, PREDICT_DEFAULT = 0, 1
+
+
+class P2PConfig(ctypes.Structure):
+    _fields_ = [
+        ("num_sessions", ctypes.c_int32),
+        ("num_players", ctypes.c_int32),
+        ("local_mask", ctypes.c_int32),
+        ("input_delay", ctypes.c_int32),
+        ("max_prediction", ctypes.c_int32),
+        ("remote_latency", ctypes.c_int32),
+        ("predictor", ctypes.c_int32),
+        ("input_capacity", ctypes.c_int32),
+        ("trace_capacity", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+    ]
+
+
+_bound = False
+
+
+def _bind(L):
+    global _bound
+    if _bound:
+        return
+    vp = ctypes.c_void_p
+    P = ctypes.POINTER
+    i32 = ctypes.c_int32
+    L.ggrs_p2p_engine_create.argtypes = [P(P2PConfig), P(vp)]
+    L.ggrs_p2p_engine_destroy.argtypes = [vp]
+    L.ggrs_p2p_engine_config.argtypes = [vp, P(P2PConfig)]
+    L.ggrs_p2p_add_inputs.argtypes = [vp, i32, i32, vp]
+    L.ggrs_p2p_advance_frames.argtypes = [vp, i32]
+    L.ggrs_p2p_current_frame.argtypes = [vp, P(i32)]
+    L.ggrs_p2p_synchronize.argtypes = [vp]
+    L.ggrs_p2p_read_state.argtypes = [vp, i32, vp]
+    L.ggrs_p2p_read_ring.argtypes = [vp, i32, vp, vp, vp]
+    L.ggrs_p2p_read_stats.argtypes = [vp, vp, vp]
+    L.ggrs_p2p_read_trace.argtypes = [vp, i32, i32, vp]
+    L.ggrs_p2p_timing_reset.argtypes = [vp]
+    L.ggrs_p2p_timing_read.argtypes = [vp, P(ctypes.c_float), P(i32)]
+    for name in _lib.EXPORTS:
+        if name.startswith("ggrs_p2p_"):
+            getattr(L, name).restype = ctypes.c_int
+    _bound = True
+
+
+def _vp(a):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+class P2PEngine:
+    """S sessions of one peer: local players `local_players`, every other player remote."""
+
+    def __init__(self, num_sessions, num_players=2, local_players=(0,), input_delay=0,
+                 max_prediction=8, remote_latency=4, predictor=PREDICT_REPEAT_LAST,
+                 input_capacity=0, trace_capacity=0, device=0):
+        self._L = _lib.lib()
+        _bind(self._L)
+        mask = 0
+        for p in local_players:
+            mask |= 1 << p
+        cfg = P2PConfig(num_sessions, num_players, mask, input_delay, max_prediction, remote_latency,
+                        predictor, input_capacity, trace_capacity, device)
+        h = ctypes.c_void_p()
+        _lib.check(self._L.ggrs_p2p_engine_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+        self.num_sessions, self.num_players, self.local_mask = num_sessions, num_players, mask
+        self.input_delay, self.max_prediction = input_delay, max_prediction
+        self.remote_latency, self.predictor = remote_latency, predictor
+        self.ring_len = max_prediction + 1
+        self.state_bytes = 36 + 20 * num_players
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.ggrs_p2p_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add_inputs(self, first_frame, inputs):
+        """inputs [n][S][P]: row g = local players' add_local_input of call g, remote players'
+        input of frame g."""
+        a = np.ascontiguousarray(inputs, np.uint8)
+        if a.ndim != 3 or a.shape[1:] != (self.num_sessions, self.num_players):
+            raise InvalidRequest(-1, f"inputs must be [n][{self.num_sessions}][{self.num_players}]")
+        _lib.check(self._L.ggrs_p2p_add_inputs(self._h, first_frame, a.shape[0], _vp(a)))
+
+    def advance_frames(self, n=1):
+        _lib.check(self._L.ggrs_p2p_advance_frames(self._h, n))
+
+    def current_frame(self):
+        v = ctypes.c_int32()
+        _lib.check(self._L.ggrs_p2p_current_frame(self._h, ctypes.byref(v)))
+        return v.value
+
+    def synchronize(self):
+        _lib.check(self._L.ggrs_p2p_synchronize(self._h))
+
+    def state(self, session):
+        out = np.zeros(self.state_bytes, np.uint8)
+        _lib.check(self._L.ggrs_p2p_read_state(self._h, session, _vp(out)))
+        return out
+
+    def ring(self, session):
+        frames = np.zeros(self.ring_len, np.int32)
+        cks = np.zeros(self.ring_len, np.uint16)
+        states = np.zeros((self.ring_len, self.state_bytes), np.uint8)
+        _lib.check(self._L.ggrs_p2p_read_ring(self._h, session, _vp(frames), _vp(cks), _vp(states)))
+        return frames, cks, states
+
+    def stats(self):
+        rb = np.zeros(self.num_sessions, np.int32)
+        rs = np.zeros(self.num_sessions, np.int64)
+        _lib.check(self._L.ggrs_p2p_read_stats(self._h, _vp(rb), _vp(rs)))
+        return rb, rs
+
+    def trace(self, first_frame, n):
+        out = np.zeros((n, self.num_sessions), np.uint16)
+        _lib.check(self._L.ggrs_p2p_read_trace(self._h, first_frame, n, _vp(out)))
+        return out
+
+    def timing_reset(self):
+        _lib.check(self._L.ggrs_p2p_timing_reset(self._h))
+
+    def timing_read(self):
+        ms, n = ctypes.c_float(), ctypes.c_int32()
+        _lib.check(self._L.ggrs_p2p_timing_read(self._h, ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value

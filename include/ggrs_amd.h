@@ -244,6 +244,54 @@ int ggrs_particle_debug_corrupt_on_load(ggrs_particle_engine_t* eng, int32_t ses
 int ggrs_particle_timing_reset(ggrs_particle_engine_t* eng);
 int ggrs_particle_timing_read(ggrs_particle_engine_t* eng, float* total_ms, int32_t* launches);
 
+/* ---------------------------------------------------------------------------------------------
+ * P2P rollback decision: num_sessions independent P2PSessions of one peer,
+ * each call = P2PSession::advance_frame (src/sessions/p2p_session.rs:265-426) + the ex_game
+ * handler, with every remote player's InputQueue prediction (src/input_queue.rs:104-230) on the
+ * device.  Rollback mode, sparse saving off, every player connected.  Network model: the remote
+ * players' input of frame g arrives at the start of call g + remote_latency (poll_remote_clients
+ * :430-446 -> handle_event Event::Input :880-895 -> SyncLayer::add_remote_input,
+ * src/sync_layer.rs:271-277); the remote peer runs with input delay 0.
+ */
+typedef struct ggrs_p2p_config {
+  int32_t num_sessions;
+  int32_t num_players;     /* 1..4 (ex_game.rs:70) */
+  int32_t local_mask;      /* bit p: player p is local to this peer; at least one player is remote */
+  int32_t input_delay;     /* local players' frame delay (SessionBuilder::with_input_delay, builder.rs:150) */
+  int32_t max_prediction;  /* >= 1 (builder.rs with_max_prediction_window); ring = max_prediction + 1 */
+  int32_t remote_latency;  /* 1 .. max_prediction-1 frames */
+  int32_t predictor;       /* 0 PredictRepeatLast, 1 PredictDefault (src/lib.rs:390-406) */
+  int32_t input_capacity;  /* frames of queued input rows; 0 = 256 */
+  int32_t trace_capacity;  /* calls of display checksums kept (0: none) */
+  int32_t device;
+} ggrs_p2p_config_t;
+
+typedef struct ggrs_p2p_engine ggrs_p2p_engine_t;
+
+int ggrs_p2p_engine_create(const ggrs_p2p_config_t* cfg, ggrs_p2p_engine_t** out);
+int ggrs_p2p_engine_destroy(ggrs_p2p_engine_t* eng);
+int ggrs_p2p_engine_config(const ggrs_p2p_engine_t* eng, ggrs_p2p_config_t* out);
+/* inputs [n_frames][num_sessions][num_players]: row g holds the local players' add_local_input
+ * (p2p_session.rs:219-246) of call g and the remote players' input of frame g (what the remote
+ * peer sends, src/network/protocol.rs:564-642); rows are added in order from 0 */
+int ggrs_p2p_add_inputs(ggrs_p2p_engine_t* eng, int32_t first_frame, int32_t n_frames, const uint8_t* inputs);
+/* n_frames calls of advance_frame for every session; InvalidRequest when a call's row is missing */
+int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* eng, int32_t n_frames);
+int ggrs_p2p_current_frame(const ggrs_p2p_engine_t* eng, int32_t* out);
+int ggrs_p2p_synchronize(ggrs_p2p_engine_t* eng);
+int ggrs_p2p_read_state(ggrs_p2p_engine_t* eng, int32_t session, uint8_t* out);
+/* the session's saved-state ring (SavedStates, sync_layer.rs:144-166): per slot frame, checksum,
+ * bincode state (36 + 20 P bytes) */
+int ggrs_p2p_read_ring(ggrs_p2p_engine_t* eng, int32_t session, int32_t* frames, uint16_t* checksums,
+                       uint8_t* states);
+/* per session: number of rollbacks (adjust_gamestate calls) and resimulated frames so far */
+int ggrs_p2p_read_stats(ggrs_p2p_engine_t* eng, int32_t* rollbacks, int64_t* resim_frames);
+/* [n][num_sessions] fletcher16 of each session's state after the final AdvanceFrame of calls
+ * first_frame .. first_frame+n-1 (ex_game.rs:121-126) */
+int ggrs_p2p_read_trace(ggrs_p2p_engine_t* eng, int32_t first_frame, int32_t n, uint16_t* out);
+int ggrs_p2p_timing_reset(ggrs_p2p_engine_t* eng);
+int ggrs_p2p_timing_read(ggrs_p2p_engine_t* eng, float* total_ms, int32_t* launches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -43,6 +43,29 @@ class SyncTestResult(ctypes.Structure):
     ]
 
 
+class P2PCfg(ctypes.Structure):
+    _fields_ = [
+        ("num_players", ctypes.c_int32),
+        ("max_prediction", ctypes.c_int32),
+        ("input_delay", ctypes.c_int32),
+        ("latency", ctypes.c_int32),
+        ("local_mask", ctypes.c_int32),
+        ("predictor", ctypes.c_int32),
+    ]
+
+
+class P2PResult(ctypes.Structure):
+    _fields_ = [
+        ("status", ctypes.c_int32),
+        ("frames_done", ctypes.c_int32),
+        ("rollbacks", ctypes.c_int64),
+        ("resim", ctypes.c_int64),
+        ("n_load", ctypes.c_int64),
+        ("n_save", ctypes.c_int64),
+        ("n_advance", ctypes.c_int64),
+    ]
+
+
 def build():
     """Compile the oracle with its Makefile (gcc; seconds)."""
     subprocess.run(["make", "-s", "-C", HERE], check=True)
@@ -90,6 +113,9 @@ def lib():
         L.oracle_particles_synctest_run.restype = ctypes.c_int
         L.oracle_input_queue_sequence.argtypes = [ctypes.c_int32, ctypes.c_int32, i32p, u8p,
                                                   ctypes.c_int, i32p, u8p, i32p]
+        L.oracle_p2p_run.argtypes = [P(P2PCfg), ctypes.c_int32, u8p, u16p, i32p, u8p, ctypes.c_int64,
+                                     i32p, u8p, i32p, u16p, u8p, P(P2PResult)]
+        L.oracle_p2p_run.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -197,6 +223,31 @@ def p2p_replay(state, load_frame, inputs, max_prediction=None, status=None):
     if rc != 0:
         raise ValueError("bad p2p replay arguments")
     return states, cks, final
+
+
+def p2p_run(inputs, num_players=2, local_mask=0b01, input_delay=0, max_prediction=8, latency=4,
+            predictor=0, req_cap=0):
+    """One peer's P2P session over len(inputs) calls (oracle_p2p_run in ggrs_oracle.c):
+    inputs[g] = local add_local_input of call g / remote input of frame g."""
+    inputs = np.ascontiguousarray(inputs, np.uint8).reshape(-1, num_players)
+    frames = inputs.shape[0]
+    R = max_prediction + 1
+    sb = state_bytes(num_players)
+    cfg = P2PCfg(num_players, max_prediction, input_delay, latency, local_mask, predictor)
+    res = P2PResult()
+    out = dict(ck_trace=np.zeros(frames, np.uint16), rb_frame=np.zeros(frames, np.int32),
+               req_trace=np.zeros(max(req_cap, 1), np.uint8), req_len=np.zeros(frames, np.int32),
+               final_state=np.zeros(sb, np.uint8), ring_frames=np.zeros(R, np.int32),
+               ring_cksums=np.zeros(R, np.uint16), ring_states=np.zeros((R, sb), np.uint8))
+    rc = lib().oracle_p2p_run(
+        ctypes.byref(cfg), frames, _ptr(inputs, ctypes.c_uint8), _ptr(out["ck_trace"], ctypes.c_uint16),
+        _ptr(out["rb_frame"], ctypes.c_int32), _ptr(out["req_trace"], ctypes.c_uint8), req_cap,
+        _ptr(out["req_len"], ctypes.c_int32), _ptr(out["final_state"], ctypes.c_uint8),
+        _ptr(out["ring_frames"], ctypes.c_int32), _ptr(out["ring_cksums"], ctypes.c_uint16),
+        _ptr(out["ring_states"], ctypes.c_uint8), ctypes.byref(res))
+    out["rc"] = rc
+    out["result"] = res
+    return out
 
 
 def particles_synctest_run(inputs, num_entities, num_players=2, max_prediction=17,

@@ -49,6 +49,22 @@ def test_bad_config_rejected_without_device(engine_lib, kw, msg):
         Engine(**args)
 
 
+@pytest.mark.parametrize("kw,msg", [
+    (dict(remote_latency=8, max_prediction=8), "remote_latency"),
+    (dict(remote_latency=0), "remote_latency"),
+    (dict(local_players=(0, 1)), "remote player"),
+    (dict(local_players=(2,)), "local_mask"),
+    (dict(predictor=2), "predictor"),
+    (dict(max_prediction=0), "lockstep"),
+])
+def test_bad_p2p_config_rejected_without_device(engine_lib, kw, msg):
+    from ggrs_amd import InvalidRequest, P2PEngine
+    args = dict(num_players=2, remote_latency=3)
+    args.update(kw)
+    with pytest.raises(InvalidRequest, match=msg):
+        P2PEngine(4, **args)
+
+
 def test_builder_mirrors_reference_check(engine_lib):
     from ggrs_amd import InvalidRequest, SessionBuilder
     with pytest.raises(InvalidRequest, match="Check distance too big"):
