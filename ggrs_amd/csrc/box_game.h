@@ -67,9 +67,9 @@ __device__ inline float rem_euclid(float a, float b) {
 }
 
 // One player of State::advance (ex_game.rs:276-331).  `input` is Input.inp, already mapped to 4
-// for InputStatus::Disconnected by the caller (ex_game.rs:277-281).
-__device__ inline void advance_player(float& x, float& y, float& vx, float& vy, float& rot,
-                                      uint32_t input) {
+// for InputStatus::Disconnected by the caller (ex_game.rs:277-281).  General form: any rot.
+__device__ inline void advance_player_general(float& x, float& y, float& vx, float& vy, float& rot,
+                                              uint32_t input) {
   float vel_x = vx * kFriction;
   float vel_y = vy * kFriction;
   const bool up = (input & kInputUp) != 0, down = (input & kInputDown) != 0;
@@ -107,6 +107,57 @@ __device__ inline void advance_player(float& x, float& y, float& vx, float& vy, 
   y = ny;
   vx = vel_x;
   vy = vel_y;
+}
+
+// The same step, branch-free, for +0 <= rot <= 2*pi -- the only rotations a state can hold
+// (State::new starts there, rem_euclid keeps it there).  Every value is computed with the same
+// IEEE ops as the general form and the branches become selects:
+//   * sin/cos of the old rot: glibc_sincosf_domain (one reduction + both polynomials);
+//   * thrust/brake: both vel +- d are formed, the input picks one (or neither);
+//   * rotation: a = rot -+ ROTATION_SPEED lies in [-0.042, 2*pi + 0.042], so rem_euclid is the
+//     Sterbenz step (|a| < 2|b|) plus the negative fix-up, never fmodf; no rotation keeps rot.
+// Only the speed clamp (two correctly rounded divisions) stays a branch.
+__device__ inline void advance_player_domain(float& x, float& y, float& vx, float& vy, float& rot,
+                                             uint32_t input) {
+  float vel_x = vx * kFriction;
+  float vel_y = vy * kFriction;
+  const bool up = (input & kInputUp) != 0, down = (input & kInputDown) != 0;
+  const bool left = (input & kInputLeft) != 0, right = (input & kInputRight) != 0;
+  float s, c;
+  glibc_sincosf_domain(rot, &s, &c);
+  const float dx = kMovementSpeed * c, dy = kMovementSpeed * s;
+  const bool thrust = up && !down, brake = down && !up;
+  const float tx = vel_x + dx, ty = vel_y + dy, bx = vel_x - dx, by = vel_y - dy;
+  vel_x = thrust ? tx : (brake ? bx : vel_x);
+  vel_y = thrust ? ty : (brake ? by : vel_y);
+  const bool ccw = left && !right, cw = right && !left;
+  const float a = ccw ? rot - kRotationSpeed : rot + kRotationSpeed;
+  const float aa = __builtin_fabsf(a);
+  float r = aa < kTwoPi ? a : __builtin_copysignf(aa - kTwoPi, a);
+  r = r < 0.0f ? r + kTwoPi : r;
+  rot = (ccw || cw) ? r : rot;
+  const float magnitude = __builtin_sqrtf(vel_x * vel_x + vel_y * vel_y);
+  if (magnitude > kMaxSpeed) {
+    vel_x = (vel_x * kMaxSpeed) / magnitude;
+    vel_y = (vel_y * kMaxSpeed) / magnitude;
+  }
+  float nx = x + vel_x, ny = y + vel_y;
+  nx = __builtin_fmaxf(nx, 0.0f);
+  nx = __builtin_fminf(nx, kWindowWidth);
+  ny = __builtin_fmaxf(ny, 0.0f);
+  ny = __builtin_fminf(ny, kWindowHeight);
+  x = nx;
+  y = ny;
+  vx = vel_x;
+  vy = vel_y;
+}
+
+// Dispatch: the branch-free form when every active lane's rot is in the domain (always, for
+// states this engine produced), else the general form for the whole wave.
+__device__ inline void advance_player(float& x, float& y, float& vx, float& vy, float& rot, uint32_t input) {
+  const bool in_domain = __builtin_bit_cast(uint32_t, rot) <= kTwoPiBits;
+  if (__builtin_expect(__all(in_domain), 1)) advance_player_domain(x, y, vx, vy, rot, input);
+  else advance_player_general(x, y, vx, vy, rot, input);
 }
 
 // State::advance for all players.  `inputs` packs player i's Input.inp in byte i; a set bit i of

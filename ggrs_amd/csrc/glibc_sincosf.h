@@ -188,4 +188,25 @@ __host__ __device__ inline void glibc_sincosf_small(float y, float* sinp, float*
   *cosp = flip ? -cv : cv;
 }
 
+// Branch-free sin+cos for the ship-rotation domain +0 <= y <= 2*pi (bit patterns
+// 0x00000000 .. 0x40c90fdb), the only values rot takes (ex_game.rs:303-309 keeps it there by
+// rem_euclid; State::new starts it there).  On that domain glibc's small-argument paths agree
+// with the reduction path: for y < 0.75 (the |y| < pi/4 test of abstop12) reduce_fast yields
+// n = 0 and x - 0*hpi = x exactly, and the |y| < 2^-12 shortcut (sin = y, cos = 1) is what the
+// polynomials round to there.  Verified against libm on every f32 of the domain
+// (tests/native/sincosf_kat_host.cpp, bad_domain).
+__host__ __device__ inline void glibc_sincosf_domain(float y, float* sinp, float* cosp) {
+  int n;
+  const double x = reduce_fast((double)y, &n);
+  const double x2 = x * x;
+  const float S = (float)sin_poly(x, x2);
+  const float C = (float)cos_poly(x2);
+  const float sv = (n & 1) ? C : S;
+  const float cv = (n & 1) ? -S : C;
+  const bool flip = (n & 2) != 0;
+  *sinp = flip ? -sv : sv;
+  *cosp = flip ? -cv : cv;
+}
+constexpr uint32_t kTwoPiBits = 0x40c90fdbu;  // bits of (float)(2*pi)
+
 }  // namespace ggrs

@@ -25,7 +25,7 @@ def kat_binary(tmp_path_factory):
 def test_port_matches_libm_on_0_2pi(kat_binary):
     r = subprocess.run([kat_binary, "0", "40c90fdb", str(os.cpu_count() or 8)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "bad_sin 0 bad_cos 0 bad_fused 0" in r.stdout
+    assert "bad_sin 0 bad_cos 0 bad_fused 0 bad_domain 0" in r.stdout
 
 
 def test_port_matches_libm_on_all_f32(kat_binary):
