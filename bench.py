@@ -357,7 +357,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores available)")
     ap.add_argument("--cpu-frames", type=int, default=100000, help="SyncTest frames per CPU thread")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--path", choices=["pipelined", "sequential", "pipelined-whole"], default="pipelined",
+    ap.add_argument("--path", choices=["pipelined", "sequential", "pipelined-whole", "pipelined-split"], default="pipelined",
                     help="SyncTest kernel (DESIGN.md section 3)")
     ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=2,
                     help="BASELINE.json config: 2 = SyncTest (default), 3/4 = branch rollback, "
@@ -389,7 +389,7 @@ def main():
     inputs = synth.gen_inputs(rank * lanes, lanes, total_frames, P, synth.MODEL_HELD)
     eng = Engine(lanes, P, maxp, cd, delay, input_capacity=total_frames + cd + delay + 2,
                  device=local_rank, trace_capacity=trace_cap)
-    eng.set_synctest_path({"pipelined": 0, "sequential": 1, "pipelined-whole": 2}[args.path])
+    eng.set_synctest_path({"pipelined": 0, "sequential": 1, "pipelined-whole": 2, "pipelined-split": 3}[args.path])
     eng.add_local_inputs(0, inputs)  # resident in HBM before anything is timed
     eng.synchronize()
 

@@ -425,6 +425,256 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_split_kernel(PipePar
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Pipelined SyncTest, v3: the split kernel's schedule (chains on lanes, players split over Pp
+// lanes, LDS-staged inputs) with the step's latency chain shortened.  Per-wave counters showed the
+// split kernel latency-bound (one wave per SIMD, 34% of wave cycles parked on s_waitcnt, 81 SALU
+// per step), so:
+//   * the frame counter is wave-uniform (every chain of every session holds frame t - cd at step
+//     t), so it lives in a scalar and is never shuffled;
+//   * the Pp-lane Fletcher combine uses DPP quad permutes, not ds_bpermute;
+//   * the first-seen comparison's broadcast is consumed one step later (its LDS round trip
+//     overlaps the next step's hand-off), folded into the mask before the chain-end check;
+//   * ring / checksum / trace stores are buffer stores whose offset is pushed out of the
+//     descriptor's range on lanes that must not store (no exec-mask branches);
+//   * the steady state (every chain of the launch active, frame past the ramp) runs in a loop
+//     specialised for it; ramp and tail steps take the general body.
+// Requires every buffer the stores touch to be < 1 GiB (host falls back to the split kernel).
+constexpr uint32_t kOob = 0x40000000u;  // >= every descriptor's num_records; two of them never wrap
+
+__device__ inline __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+template <int Pp>
+__device__ inline uint32_t quad_sum(uint32_t v) {
+  if constexpr (Pp >= 2) v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // xor 1
+  if constexpr (Pp >= 4) v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // xor 2
+  return v;
+}
+
+template <int P>
+__global__ __launch_bounds__(kWave) void synctest_pipelined_v3_kernel(PipeParams p) {
+  constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
+  constexpr int F = state_fields(P);
+  constexpr int n_bytes = Fletcher<P>::n;
+  __shared__ uint8_t lds_in[kStageFrames * kWave];       // [frame][session-in-block][Pp]
+  __shared__ uint16_t lds_first[kMaxRampFrames * kWave];  // [ramp frame][session-in-block]
+  __shared__ uint32_t lds_cell[kWave * 5];                // chain f0's LoadGameState, per lane
+  if (*p.fail_f0 >= 0) return;
+  const int wl = threadIdx.x;
+  const int K = p.K, cd = p.cd, R = p.R;
+  const int G = K * Pp;
+  const int g = wl / G, r = wl - g * G;
+  const int j = r / Pp, pl = r - j * Pp;
+  const int64_t L = p.L;
+  const int spw = p.spw;
+  const int64_t s0 = (int64_t)blockIdx.x * spw;
+  const int64_t s = s0 + g;
+  const int nsess = (int)((L - s0) < spw ? (L - s0) : spw);
+  const bool valid = g < spw && s < L && p.lane_status[s] == GGRS_LANE_RUNNING;
+  const bool owner = valid && pl < P;
+  const bool lead = valid && pl == 0;
+  const int64_t sl = valid ? s : 0;
+  const int plc = pl < P ? pl : 0;
+  const int base = g * G;
+  const int src_prev = (base + (j == 0 ? K - 1 : j - 1) * Pp + pl) * 4;  // ds_bpermute byte address
+  const int kq[5] = {fld_x(P, plc), fld_y(P, plc), fld_vx(P, plc), fld_vy(P, plc), fld_rot(P, plc)};
+  // descriptors and per-lane byte offsets (kOob where the lane never stores)
+  const uint32_t slot_bytes = (uint32_t)(F * L * 4), ck_slot_bytes = (uint32_t)(L * 2);
+  const __amdgpu_buffer_rsrc_t rs_ring = make_rsrc(p.ring, slot_bytes * (uint32_t)R);
+  const __amdgpu_buffer_rsrc_t rs_ck = make_rsrc(p.ring_ck, ck_slot_bytes * (uint32_t)R);
+  const __amdgpu_buffer_rsrc_t rs_first = make_rsrc(p.first_ck, ck_slot_bytes * (uint32_t)R);
+  const __amdgpu_buffer_rsrc_t rs_trace =
+      make_rsrc(p.trace, p.trace ? ck_slot_bytes * (uint32_t)p.trace_cap : 0u);
+  uint32_t fo[5];
+#pragma unroll
+  for (int q = 0; q < 5; q++) fo[q] = owner ? (uint32_t)((kq[q] * L + s) * 4) : kOob;
+  const uint32_t fo_frame = lead ? (uint32_t)(s * 4) : kOob;
+  const uint32_t co = lead ? (uint32_t)(s * 2) : kOob;
+  // Fletcher weights of this lane's five fields (the frame's part is added by lane pl == 0)
+  uint32_t wt[5];
+#pragma unroll
+  for (int q = 0; q < 5; q++) wt[q] = owner ? weights_at(n_bytes, fld_offset(P, kq[q])) : 0u;
+  const uint32_t one4 = owner ? 0x01010101u : 0u;
+
+  const int32_t g0 = p.f0 - cd;
+  for (int q = wl; q < cd * nsess; q += kWave) {
+    const int gg = q / nsess, ss = q - gg * nsess;
+    lds_first[gg * kWave + ss] = p.first_ck[(int64_t)((g0 + gg) % R) * L + s0 + ss];
+  }
+  {
+    const uint32_t* cell = p.ring + (int64_t)(g0 % R) * F * L + sl;
+#pragma unroll
+    for (int q = 0; q < 5; q++) lds_cell[wl * 5 + q] = cell[kq[q] * L];
+  }
+  __syncthreads();
+
+  uint32_t w[5] = {0, 0, 0, 0, 0};
+  uint64_t mask = 0;
+  // the previous step's comparison, finished at the next step (its broadcast is still in flight)
+  uint32_t pend_ck = 0, pend_first = 0;
+  bool pend_cmp = false;
+  int pend_bit = 0;
+  const int32_t t_end = p.f0 + p.n + cd;
+  int32_t i = ((p.f0 - j) % K + K) % K;
+  const int row = nsess * Pp;
+  int32_t slot_r = g0 % R;
+  int32_t slot_k = g0 % K;
+  int32_t slot_t = p.trace_cap ? (p.f0 - K) % p.trace_cap : 0;
+  const uint32_t corrupt_on = (p.corrupt_frame >= 0 && s == p.corrupt_lane && pl == 0) ? 1u : 0u;
+  const int32_t ramp_end = min(p.f0 + cd, t_end);
+  const int32_t core_end = max(ramp_end, p.f0 + p.n);
+
+  auto stage = [&](int32_t t) {
+    __syncthreads();
+    const int32_t gf = t - cd;
+    const int nf = (t_end - t) < kStageFrames ? (t_end - t) : kStageFrames;
+    for (int q = wl; q < nf * row; q += kWave) {
+      const int ff = q / row, b = q - ff * row;
+      lds_in[ff * row + b] = p.inputs[((int64_t)((gf + ff) % p.cap) * L + s0) * Pp + b];
+    }
+    __syncthreads();
+  };
+
+  // One step t.  kCore: every chain of the launch is active, t > f0 + cd - 1 and t < f0 + n.
+  auto step = [&](auto core_tag, int32_t t) {
+    constexpr bool kCore = decltype(core_tag)::value;
+    const int32_t c = t - i;
+    const bool active = kCore ? valid : (valid && c >= p.f0 && c < p.f0 + p.n);
+    const int32_t gf = t - cd;
+    const int32_t rel = t - p.f0;
+    const uint32_t frame = (uint32_t)gf;
+    // (1) hand-off: the cell chain c-1 saves in this step, from its lane's registers
+    uint32_t from[5];
+#pragma unroll
+    for (int q = 0; q < 5; q++) from[q] = (uint32_t)__builtin_amdgcn_ds_bpermute(src_prev, (int)w[q]);
+    const uint32_t in = lds_in[(rel & (kStageFrames - 1)) * row + g * Pp + pl];
+    // previous step's comparison (checksums_consistent of its re-saves), now that its broadcast landed
+    mask |= (uint64_t)(pend_cmp && pend_ck != pend_first) << pend_bit;
+    // (2) Fletcher-16 of the registers: frame gf's cell (i >= 1) or the ended chain's final state
+    uint32_t s1 = 0, s2 = 0;
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+      s1 = dot4_u8(w[q], one4, s1);
+      s2 = dot4_u8(w[q], wt[q], s2);
+    }
+    if (pl == 0) {
+      s1 = dot4_u8(frame, 0x01010101u, s1 + Fletcher<P>::kSum1Const);
+      s2 = dot4_u8(frame, weights_at(n_bytes, 0), s2 + Fletcher<P>::kSum2Const);
+    }
+    s1 = quad_sum<Pp>(s1);
+    s2 = quad_sum<Pp>(s2);
+    const uint32_t ck = ((s2 % 255u) << 8) | (s1 % 255u);
+    uint32_t first = (uint32_t)__builtin_amdgcn_ds_bpermute((base + slot_k * Pp) * 4, (int)ck);
+    if (!kCore && rel < cd) first = lds_first[rel * kWave + g];
+    // (3) SaveGameState(gf) on every chain past its load; first-seen value on chain gf (i == cd)
+    {
+      const bool sv = active && i > 0;
+      const uint32_t so = sv ? (uint32_t)slot_r * slot_bytes : kOob;
+#pragma unroll
+      for (int q = 0; q < 5; q++) __builtin_amdgcn_raw_buffer_store_b32(w[q], rs_ring, fo[q] + so, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(frame, rs_ring, fo_frame + so, 0, 0);
+      const uint32_t cso = sv ? (uint32_t)slot_r * ck_slot_bytes : kOob;
+      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ck, co + cso, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_first, co + (i == cd ? cso : kOob), 0, 0);
+    }
+    // display checksum of the chain that ended last step (i == 0 lanes)
+    {
+      const bool tr = i == 0 && c - K >= p.f0 && c - K < p.f0 + p.n;
+      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_trace,
+                                            co + (tr ? (uint32_t)slot_t * ck_slot_bytes : kOob), 0, 0);
+    }
+    // this step's comparison, finished next step
+    pend_cmp = active && pl == 0 && i > 0 && i < cd;
+    pend_ck = ck;
+    pend_first = first;
+    pend_bit = (i - 1) & 63;
+    // (4) the chain starting now takes the loaded cell (the launch's first chain: via LDS)
+    if (!kCore && t == p.f0) {
+      if (i == 0) {
+#pragma unroll
+        for (int q = 0; q < 5; q++) w[q] = lds_cell[wl * 5 + q];
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 5; q++) w[q] = i == 0 ? from[q] : w[q];
+    }
+    if (i == 0) mask = 0;
+    w[0] ^= (i == 0 && c == p.corrupt_frame) ? corrupt_on : 0u;
+    // (5) AdvanceFrame(gf) on every lane
+    {
+      float x = __builtin_bit_cast(float, w[0]), y = __builtin_bit_cast(float, w[1]);
+      float vx = __builtin_bit_cast(float, w[2]), vy = __builtin_bit_cast(float, w[3]);
+      float rot = __builtin_bit_cast(float, w[4]);
+      advance_player(x, y, vx, vy, rot, in);
+      w[0] = __builtin_bit_cast(uint32_t, x);
+      w[1] = __builtin_bit_cast(uint32_t, y);
+      w[2] = __builtin_bit_cast(uint32_t, vx);
+      w[3] = __builtin_bit_cast(uint32_t, vy);
+      w[4] = __builtin_bit_cast(uint32_t, rot);
+    }
+    if (!kCore && active && i == cd && c == p.f0 + p.n - 1) {  // the launch's last chain: its state
+      uint32_t* cur = p.cur + s;
+      if (owner) {
+#pragma unroll
+        for (int q = 0; q < 5; q++) cur[kq[q] * L] = w[q];
+      }
+      if (pl == 0) cur[0] = frame + 1u;
+    }
+    i = i + 1 == K ? 0 : i + 1;
+    slot_r = slot_r + 1 == R ? 0 : slot_r + 1;
+    slot_k = slot_k + 1 == K ? 0 : slot_k + 1;
+    slot_t = slot_t + 1 == p.trace_cap ? 0 : slot_t + 1;
+  };
+
+  // chain ends: a chain's compares at i = 1..cd-1 are folded by the step where i == cd, so the
+  // mask is complete when it is tested (one step after the chain's last advance)
+  auto chain_end_check = [&]() {
+    if (pl == 0 && valid && i == 0 && mask) atomicCAS(p.fail_f0, -1, p.f0);
+  };
+
+  int32_t t = p.f0;
+  for (; t < ramp_end; ++t) {
+    if ((((t - p.f0)) & (kStageFrames - 1)) == 0) stage(t);
+    step(std::false_type(), t);
+    chain_end_check();
+  }
+  while (t < core_end) {
+    const int32_t rel = t - p.f0;
+    if ((rel & (kStageFrames - 1)) == 0) stage(t);
+    const int32_t chunk_end = min(core_end, t + (kStageFrames - (rel & (kStageFrames - 1))));
+    for (; t < chunk_end; ++t) {
+      step(std::true_type(), t);
+      chain_end_check();
+    }
+  }
+  for (; t < t_end; ++t) {
+    if ((((t - p.f0)) & (kStageFrames - 1)) == 0) stage(t);
+    step(std::false_type(), t);
+    chain_end_check();
+  }
+  // the last step's pending comparison belongs to a chain that does not end in this launch
+  if (p.trace) {  // display checksum of the launch's last chain (it ended at the last step)
+    uint32_t s1 = 0, s2 = 0;
+    const uint32_t frame = (uint32_t)(t_end - cd);
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+      s1 = dot4_u8(w[q], one4, s1);
+      s2 = dot4_u8(w[q], wt[q], s2);
+    }
+    if (pl == 0) {
+      s1 = dot4_u8(frame, 0x01010101u, s1 + Fletcher<P>::kSum1Const);
+      s2 = dot4_u8(frame, weights_at(n_bytes, 0), s2 + Fletcher<P>::kSum2Const);
+    }
+    s1 = quad_sum<Pp>(s1);
+    s2 = quad_sum<Pp>(s2);
+    const uint16_t ck = (uint16_t)(((s2 % 255u) << 8) | (s1 % 255u));
+    const int32_t last = p.f0 + p.n - 1;
+    if (valid && pl == 0 && j == last % K) p.trace[(int64_t)(last % p.trace_cap) * L + s] = ck;
+  }
+}
+
 // Checkpoint / restore of everything a SyncTest launch writes (cur, ring, ring_ck, first_ck):
 // dir 0 copies live -> shadow unless a launch already failed (then the shadow must keep the
 // state from before the failing launch); dir 1 copies shadow -> live.
@@ -787,7 +1037,22 @@ static int launch_pipelined(ggrs_engine_t* e, int32_t f0, int32_t n) {
   p.trace = e->trace;
   e->unverified = true;
   const int Pp = e->Pp;
-  if (e->path == GGRS_PATH_PIPELINED && p.K * Pp <= kWave) {
+  const uint64_t F4L = (uint64_t)e->F * 4 * p.L;
+  const bool fits_v3 = F4L * p.R < kOob && (uint64_t)2 * p.L * p.R < kOob &&
+                       (uint64_t)2 * p.L * (uint64_t)std::max(p.trace_cap, 0) < kOob;
+  if (e->path == GGRS_PATH_PIPELINED && p.K * Pp <= kWave && fits_v3) {
+    p.spw = kWave / (p.K * Pp);
+    const int64_t grid = grid_of(p.L, p.spw);
+    return launch_timed(e, [&] {
+      switch (e->cfg.num_players) {
+        case 1: synctest_pipelined_v3_kernel<1><<<grid, kWave, 0, e->stream>>>(p); break;
+        case 2: synctest_pipelined_v3_kernel<2><<<grid, kWave, 0, e->stream>>>(p); break;
+        case 3: synctest_pipelined_v3_kernel<3><<<grid, kWave, 0, e->stream>>>(p); break;
+        default: synctest_pipelined_v3_kernel<4><<<grid, kWave, 0, e->stream>>>(p); break;
+      }
+    });
+  }
+  if ((e->path == GGRS_PATH_PIPELINED || e->path == GGRS_PATH_PIPELINED_SPLIT) && p.K * Pp <= kWave) {
     p.spw = kWave / (p.K * Pp);
     const int64_t grid = grid_of(p.L, p.spw);
     return launch_timed(e, [&] {
@@ -876,7 +1141,8 @@ int ggrs_synctest_advance_frames(ggrs_engine_t* e, int32_t n) {
 
 int ggrs_set_synctest_path(ggrs_engine_t* e, int32_t path) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
-  if (path != GGRS_PATH_PIPELINED && path != GGRS_PATH_SEQUENTIAL && path != GGRS_PATH_PIPELINED_WHOLE)
+  if (path != GGRS_PATH_PIPELINED && path != GGRS_PATH_SEQUENTIAL && path != GGRS_PATH_PIPELINED_WHOLE &&
+      path != GGRS_PATH_PIPELINED_SPLIT)
     return set_error(GGRS_E_INVALID, "unknown path %d", path);
   int rc = resolve(e);
   if (rc) return rc;

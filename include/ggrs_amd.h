@@ -69,6 +69,8 @@ extern "C" {
                                        lane per (chain, player) when (cd+1) * players <= 64 */
 #define GGRS_PATH_SEQUENTIAL 1      /* one lane per session, calls in order */
 #define GGRS_PATH_PIPELINED_WHOLE 2 /* pipelined, one lane per chain (all players in one lane) */
+#define GGRS_PATH_PIPELINED_SPLIT 3 /* pipelined, players split over lanes (the round-1 v2 kernel;
+                                       the default path runs its v3 successor when buffers < 1 GiB) */
 
 /* per-lane status */
 #define GGRS_LANE_RUNNING 0

@@ -22,7 +22,7 @@ def lane_inputs(O, base_seed, lanes, frames, players, model):
                      for l in range(lanes)], axis=1)  # [frames][lanes][P]
 
 
-PATHS = [0, 1, 2]  # _lib.PATH_PIPELINED (split players), PATH_SEQUENTIAL, PATH_PIPELINED_WHOLE
+PATHS = [0, 1, 2, 3]  # PIPELINED (v3), SEQUENTIAL, PIPELINED_WHOLE, PIPELINED_SPLIT (v2)
 
 
 def make_engine(lanes, P, maxp, cd, d, frames, trace=True, path=0):
@@ -116,7 +116,7 @@ def test_streamed_inputs_small_queue(oracle):
         assert bytes(eng.state(lane)) == bytes(r["final_state"])
 
 
-@pytest.mark.parametrize("path,chunk,call", [(0, 120, 40), (1, 120, 40), (2, 120, 40), (0, 16, 40),
+@pytest.mark.parametrize("path,chunk,call", [(0, 120, 40), (1, 120, 40), (2, 120, 40), (3, 120, 40), (0, 16, 40),
                                              (0, 16, 48), (2, 16, 48), (0, 7, 9), (1, 7, 9),
                                              (0, 120, 110)])
 def test_mismatch_detection_matches_reference(oracle, path, chunk, call):
