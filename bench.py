@@ -54,6 +54,17 @@ def pmc_traffic(workload):
         return None
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for ln in fh:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -355,7 +366,8 @@ def main():
     ap.add_argument("--frames-per-step", type=int, default=512)
     ap.add_argument("--lanes", type=int, default=4096, help="sessions per GPU (config 2: 4096)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores available)")
-    ap.add_argument("--cpu-frames", type=int, default=100000, help="SyncTest frames per CPU thread")
+    ap.add_argument("--cpu-frames", type=int, default=3000000,
+                    help="SyncTest frames per CPU thread (default: ~10 s of host work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--path", choices=["pipelined", "sequential", "pipelined-whole", "pipelined-split"], default="pipelined",
                     help="SyncTest kernel (DESIGN.md section 3)")
@@ -461,7 +473,7 @@ def main():
                     "sample": f"{threads} threads x {frames} SyncTest frames (1 session/thread, "
                               f"cd {cd}, 2 players, held-key inputs), C restatement of the "
                               f"reference loop (oracle/ggrs_oracle.c)",
-                    "wall_s": round(wall, 3),
+                    "wall_s": round(wall, 3), "cpu": cpu_model(),
                     "thread0_matches_gpu_lane0": bool((ck0[total_frames - trace_cap:total_frames] == gpu_tr).all()),
                 }
         except Exception as exc:  # the oracle is optional on the measurement path
