@@ -17,7 +17,7 @@ NULL_FRAME = -1
 REQ_SAVE, REQ_LOAD, REQ_ADVANCE = 0, 1, 2
 STATUS_CONFIRMED, STATUS_PREDICTED, STATUS_DISCONNECTED = 0, 1, 2
 LANE_RUNNING, LANE_MISMATCH = 0, 1
-PATH_PIPELINED, PATH_SEQUENTIAL, PATH_PIPELINED_WHOLE = 0, 1, 2
+PATH_PIPELINED, PATH_SEQUENTIAL, PATH_PIPELINED_WHOLE, PATH_PIPELINED_SPLIT, PATH_PIPELINED_V3, PATH_PIPELINED_V4_DPP = 0, 1, 2, 3, 4, 5
 
 # every symbol include/ggrs_amd.h declares (tests check the library exports all of them)
 EXPORTS = (

@@ -152,6 +152,77 @@ __device__ inline void advance_player_domain(float& x, float& y, float& vx, floa
   vy = vel_y;
 }
 
+// Correctly rounded sqrtf for the speed clamp, where s > 49: hipcc's own correctly rounded
+// expansion (raw v_sqrt_f32, then the neighbour residual test) without its small-input scaling
+// (s < 2^-96) and zero/inf/NaN class fix-up, neither of which applies to s > 49.
+__device__ inline float sqrt_rn_above_49(float s) {
+  const float m = __builtin_amdgcn_sqrtf(s);
+  const uint32_t mb = __builtin_bit_cast(uint32_t, m);
+  const float dn = __builtin_bit_cast(float, mb - 1u), up = __builtin_bit_cast(float, mb + 1u);
+  const float rd = __builtin_fmaf(-dn, m, s);
+  const float ru = __builtin_fmaf(-up, m, s);
+  const float r = rd <= 0.0f ? dn : m;
+  return ru > 0.0f ? up : r;
+}
+
+// Correctly rounded f32 division a / m for the speed clamp, through binary64: a reciprocal of m
+// refined by two Newton steps (relative error < 2^-51) times a, rounded once to f32.  For f32
+// operands the exact quotient lies at least 2^-49 (relative) away from every f32 rounding
+// boundary (midpoint), so a binary64 value within 2^-50.5 of it rounds to the same f32 as the
+// exact quotient: RN32(q64) == RN32(a / m).  Checked against hipcc's correctly rounded division
+// on the GPU (tests/test_gpu_sincosf.py).  m is finite, > 7 here.
+__device__ inline double rcp_f64_refined(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-d, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+
+// advance_player_domain with fewer instructions and the same IEEE results (v4 SyncTest kernel):
+//   * thrust / brake / neither add d / -d / -0.0f: x - d == x + (-d) exactly and x + (-0) == x
+//     for every x, signed zeros included, so one add replaces two adds and a select;
+//   * the clamp test |v| > 7 is sqrtf(s) > 7 <=> s > 49, true for every f32 s (exhaustive host
+//     KAT, tests/native/step_kat_host.c), so the square root is only taken inside the clamp, and
+//     the clamp's two divisions share one refined binary64 reciprocal (rcp_f64_refined);
+//   * max(min(.)) clamps become v_med3_f32: equal for every non-NaN input without -0, and a
+//     position sum is never -0 (x >= +0, and x + v == 0 only as +0) nor NaN.
+__device__ inline void advance_player_lean(float& x, float& y, float& vx, float& vy, float& rot,
+                                           uint32_t input) {
+  float vel_x = vx * kFriction;
+  float vel_y = vy * kFriction;
+  float s, c;
+  glibc_sincosf_domain(rot, &s, &c);
+  const float dx = kMovementSpeed * c, dy = kMovementSpeed * s;
+  const uint32_t ud = input & (kInputUp | kInputDown), lr = input & (kInputLeft | kInputRight);
+  const bool thrust = ud == kInputUp, brake = ud == kInputDown;
+  vel_x = vel_x + (thrust ? dx : (brake ? -dx : -0.0f));
+  vel_y = vel_y + (thrust ? dy : (brake ? -dy : -0.0f));
+  const bool ccw = lr == kInputLeft, turn = ccw || lr == kInputRight;
+  const float a = rot + (ccw ? -kRotationSpeed : kRotationSpeed);
+  const float aa = __builtin_fabsf(a);
+  float r = aa < kTwoPi ? a : __builtin_copysignf(aa - kTwoPi, a);
+  r = r < 0.0f ? r + kTwoPi : r;
+  rot = turn ? r : rot;
+  const float mag2 = vel_x * vel_x + vel_y * vel_y;
+  if (mag2 > kMaxSpeed * kMaxSpeed) {
+    const float magnitude = sqrt_rn_above_49(mag2);
+    const double r = rcp_f64_refined((double)magnitude);
+    vel_x = (float)((double)(vel_x * kMaxSpeed) * r);
+    vel_y = (float)((double)(vel_y * kMaxSpeed) * r);
+  }
+  x = __builtin_amdgcn_fmed3f(x + vel_x, 0.0f, kWindowWidth);
+  y = __builtin_amdgcn_fmed3f(y + vel_y, 0.0f, kWindowHeight);
+  vx = vel_x;
+  vy = vel_y;
+}
+
+__device__ inline void advance_player_v4(float& x, float& y, float& vx, float& vy, float& rot, uint32_t input) {
+  const bool in_domain = __builtin_bit_cast(uint32_t, rot) <= kTwoPiBits;
+  if (__builtin_expect(__all(in_domain), 1)) advance_player_lean(x, y, vx, vy, rot, input);
+  else advance_player_general(x, y, vx, vy, rot, input);
+}
+
 // Dispatch: the branch-free form when every active lane's rot is in the domain (always, for
 // states this engine produced), else the general form for the whole wave.
 __device__ inline void advance_player(float& x, float& y, float& vx, float& vy, float& rot, uint32_t input) {
@@ -202,6 +273,23 @@ struct Fletcher {
 
 __device__ inline uint32_t dot4_u8(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_udot4(a, b, c, false);
+}
+
+// Fletcher-16 from DOUBLED sums d1 = 2*sum1, d2 = 2*sum2 (< 2^24; accumulated with doubled byte
+// weights, all <= 2*116 = 232 so they still fit v_dot4's u8 lanes).  Doubling lets the mod-255
+// run on full-rate 24-bit multiplies: q = floor(x/255) = (2x * 0x808081) >> 32 for x < 2^31/127
+// (0x808081 * 255 = 2^31 + 127), one v_mul_hi_u32_u24; 2r = 2x - 510 q, one v_mad_i32_i24;
+// then (r2 << 8) | r1 = (2 r2 << 7) | (2 r1 >> 1).  Replaces four quarter-rate 32-bit multiplies.
+__device__ inline uint32_t mulhi_u24(uint32_t a, uint32_t b) {
+  return (uint32_t)(((uint64_t)(a & 0xffffffu) * (uint64_t)(b & 0xffffffu)) >> 32);
+}
+__device__ inline uint32_t fletcher_from_doubled(uint32_t d1, uint32_t d2) {
+  const uint32_t q1 = mulhi_u24(d1, 0x808081u), q2 = mulhi_u24(d2, 0x808081u);
+  uint32_t r1, r2;
+  const int32_t m510 = -510;
+  asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r1) : "v"(q1), "s"(m510), "v"(d1));
+  asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r2) : "v"(q2), "s"(m510), "v"(d2));
+  return (r2 << 7) | (r1 >> 1);
 }
 
 template <int P>

@@ -446,6 +446,25 @@ __device__ inline __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t by
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 
+// x mod n for x < 2^32 / n (n >= 1): q = mulhi(x, floor(2^32 / n) + 1) is floor(x / n) there, since
+// the multiplier's excess over 2^32 / n is < 1 and so adds less than x / 2^32 < 1 / n to x / n.
+// Scalar when x and n are (s_mul_hi_u32).  The SyncTest launch caps x at n_frames + cd < 2^24.
+// Requires n >= 2 (for n == 1 the caller scales the result by 0).
+__host__ __device__ inline uint32_t magic_small(uint32_t n) {
+  return n <= 1 ? 0u : (uint32_t)(0xffffffffu / n) + 1u;
+}
+__device__ inline uint32_t mod_small(uint32_t x, uint32_t n, uint32_t magic) {
+  return x - __umulhi(x, magic) * n;
+}
+
+// v from the lane Pp below (DPP wave_shr:1, Pp times); lanes < Pp get garbage (callers select)
+template <int Pp>
+__device__ inline uint32_t wave_shr_lanes(uint32_t v) {
+#pragma unroll
+  for (int k = 0; k < Pp; k++) v = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, true);
+  return v;
+}
+
 template <int Pp>
 __device__ inline uint32_t quad_sum(uint32_t v) {
   if constexpr (Pp >= 2) v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // xor 1
@@ -673,6 +692,237 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v3_kernel(PipeParams
     const int32_t last = p.f0 + p.n - 1;
     if (valid && pl == 0 && j == last % K) p.trace[(int64_t)(last % p.trace_cap) * L + s] = ck;
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// Pipelined SyncTest, v4: static chain roles.  Same schedule and the same Loads, Saves and
+// AdvanceFrames as v3, re-indexed so that no lane's role changes from step to step:
+//   * lane role j (0..cd) always holds chain t - j at step t.  After every advance the chains move
+//     one lane up (role j takes role j-1's post-advance state, one ds_bpermute per field) and
+//     role 0 keeps its own: that state -- chain t-1 after its first replayed advance, the cell of
+//     frame t-cd -- is exactly what chain t loads at step t (and what chain t-1 saves at step t);
+//   * saves are issued by the producer: role j's post-advance state is the cell role j+1 saves at
+//     step t+1, so roles 0..cd-1 store it (and its Fletcher-16) right after their advance, role
+//     cd-1 also as the first-seen checksum, role cd's is the call's display checksum; the
+//     rotation's LDS round trip overlaps the Fletcher sums and stores instead of stalling them;
+//   * every per-lane predicate (save, first-seen, compare, trace) is static, so store offsets are
+//     precomputed per lane (kOob where the lane never stores) plus a wave-uniform slot offset in
+//     soffset, and the step has no exec-mask branches outside the ramp and tail;
+//   * a mismatching re-save only sets a wave-uniform flag (the host replays a failed launch on the
+//     sequential kernel anyway), folded into *fail_f0 once at the end;
+//   * step arithmetic: advance_player_lean (one add per thrust axis, clamp test s > 49, med3),
+//     Fletcher-16 mod 255 from doubled sums on 24-bit multiplies.
+// kDppRot: the rotation by DPP wave shifts (VALU) instead of ds_bpermute (LDS round trip).
+template <int P, bool kDppRot>
+__global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams p) {
+  constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
+  constexpr int F = state_fields(P);
+  constexpr int n_bytes = Fletcher<P>::n;
+  __shared__ uint8_t lds_in[kStageFrames * kWave];       // [frame][session-in-block][Pp]
+  __shared__ uint16_t lds_first[kMaxRampFrames * kWave];  // [ramp frame][session-in-block]
+  __shared__ uint32_t lds_cell[kWave * 5];                // chain f0's LoadGameState, per lane
+  if (*p.fail_f0 >= 0) return;
+  const int wl = threadIdx.x;
+  const int K = p.K, cd = p.cd, R = p.R;
+  const int G = K * Pp;
+  const int g = wl / G, r = wl - g * G;
+  const int j = r / Pp, pl = r - j * Pp;  // static role, player
+  const int64_t L = p.L;
+  const int spw = p.spw;
+  const int64_t s0 = (int64_t)blockIdx.x * spw;
+  const int64_t s = s0 + g;
+  const int nsess = (int)((L - s0) < spw ? (L - s0) : spw);
+  const bool valid = g < spw && s < L && p.lane_status[s] == GGRS_LANE_RUNNING;
+  const bool owner = valid && pl < P;
+  const int64_t sl = valid ? s : 0;
+  const int plc = pl < P ? pl : 0;
+  const int base = g * G;
+  const int src_first = ((base + (cd - 1) * Pp) & (kWave - 1)) * 4;
+  const uint32_t keep_own = j == 0 ? 0xffffffffu : 0u;  // role 0 keeps its state in the rotation
+  const int src_rot = (j == 0 ? wl : base + (j - 1) * Pp + pl) * 4;  // ds_bpermute form
+  const int kq[5] = {fld_x(P, plc), fld_y(P, plc), fld_vx(P, plc), fld_vy(P, plc), fld_rot(P, plc)};
+  const uint32_t slot_bytes = (uint32_t)(F * L * 4), ck_slot_bytes = (uint32_t)(L * 2);
+  // ring, ring_ck and first_ck are consecutive in the engine's arena: one descriptor from the
+  // ring's base covers all three (fewer live SGPRs keeps the slot counters scalar)
+  const uint32_t ck_base = (uint32_t)((const uint8_t*)p.ring_ck - (const uint8_t*)p.ring);
+  const uint32_t first_base = (uint32_t)((const uint8_t*)p.first_ck - (const uint8_t*)p.ring);
+  const __amdgpu_buffer_rsrc_t rs_ring = make_rsrc(p.ring, first_base + ck_slot_bytes * (uint32_t)R);
+  const __amdgpu_buffer_rsrc_t rs_trace =
+      make_rsrc(p.trace, p.trace ? ck_slot_bytes * (uint32_t)p.trace_cap : 0u);
+  // static store offsets: producers (roles 0..cd-1) save; role cd-1 also writes first_ck; role cd
+  // writes the display checksum
+  const bool producer = valid && j <= cd - 1;
+  uint32_t fo[5];
+#pragma unroll
+  for (int q = 0; q < 5; q++) fo[q] = (producer && pl < P) ? (uint32_t)((kq[q] * L + s) * 4) : kOob;
+  const uint32_t fo_frame = (producer && pl == 0) ? (uint32_t)(s * 4) : kOob;
+  const uint32_t co = (producer && pl == 0) ? ck_base + (uint32_t)(s * 2) : kOob;
+  const uint32_t co_first = (valid && pl == 0 && j == cd - 1) ? first_base + (uint32_t)(s * 2) : kOob;
+  const uint32_t co_trace = (valid && pl == 0 && j == cd) ? (uint32_t)(s * 2) : kOob;
+  // re-saves compared against the first-seen value: producers for roles 1..cd-1, player-0 lane
+  const uint64_t cmp_lanes = __ballot(valid && pl == 0 && j <= cd - 2);
+  // doubled Fletcher weights (fletcher_from_doubled); the frame field and the constant length
+  // prefixes go to the player-0 lane
+  uint32_t wt[5];
+#pragma unroll
+  for (int q = 0; q < 5; q++) wt[q] = owner ? 2u * weights_at(n_bytes, fld_offset(P, kq[q])) : 0u;
+  const uint32_t one2 = owner ? 0x02020202u : 0u;
+  const uint32_t wf1 = pl == 0 ? 0x02020202u : 0u, wf2 = pl == 0 ? 2u * weights_at(n_bytes, 0) : 0u;
+  const uint32_t c1 = pl == 0 ? 2u * Fletcher<P>::kSum1Const : 0u;
+  const uint32_t c2 = pl == 0 ? 2u * Fletcher<P>::kSum2Const : 0u;
+
+  const int32_t g0 = p.f0 - cd;
+  for (int q = wl; q < cd * nsess; q += kWave) {
+    const int gg = q / nsess, ss = q - gg * nsess;
+    lds_first[gg * kWave + ss] = p.first_ck[(int64_t)((g0 + gg) % R) * L + s0 + ss];
+  }
+  {
+    const uint32_t* cell = p.ring + (int64_t)(g0 % R) * F * L + sl;
+#pragma unroll
+    for (int q = 0; q < 5; q++) lds_cell[wl * 5 + q] = cell[kq[q] * L];
+  }
+  __syncthreads();
+  // every role starts from the loaded cell (roles > 0 hold chains of the previous launch, which
+  // this launch neither saves nor compares, but they must hold in-domain states)
+  uint32_t w[5];
+#pragma unroll
+  for (int q = 0; q < 5; q++) w[q] = lds_cell[wl * 5 + q];
+
+  uint64_t bad = 0;                 // wave-uniform: some re-save disagreed with its first-seen value
+  uint32_t pend_ck = 0, pend_first = 0;
+  uint64_t pend_lanes = 0;          // the previous step's comparison, finished one step later
+  const int32_t t_end = p.f0 + p.n + cd;
+  const int row = nsess * Pp;
+  const int in_lane = g * Pp + pl;
+  // ring slot of frame t-cd+1 and trace slot of chain t-cd, from the step index rel = t - f0
+  // (scalar multiply-high modulo: a loop-carried counter would be widened to a VGPR)
+  // (integer division runs on the VALU; readfirstlane brings the uniform results back to SGPRs,
+  // otherwise every buffer store using them as soffset would be waterfalled)
+  const uint32_t sr0 = (uint32_t)__builtin_amdgcn_readfirstlane((g0 + 1) % R);
+  const uint32_t st0 = (uint32_t)__builtin_amdgcn_readfirstlane(p.trace_cap ? g0 % p.trace_cap : 0);
+  const uint32_t magic_r = (uint32_t)__builtin_amdgcn_readfirstlane((int)magic_small(R));
+  const uint32_t magic_t = (uint32_t)__builtin_amdgcn_readfirstlane((int)magic_small(p.trace_cap));
+  const uint32_t tr_slot_bytes = p.trace_cap > 1 ? ck_slot_bytes : 0u;  // one trace slot: offset 0
+  const bool corrupt_here = p.corrupt_frame >= p.f0 && p.corrupt_frame < p.f0 + p.n;
+  const uint32_t corrupt_on = (corrupt_here && s == p.corrupt_lane && pl == 0 && j == 0) ? 1u : 0u;
+  const int32_t ramp_end = min(p.f0 + cd, t_end);
+  const int32_t core_end = corrupt_here ? ramp_end : max(ramp_end, p.f0 + p.n);
+
+  auto stage = [&](int32_t t) {
+    __syncthreads();
+    const int32_t gf = t - cd;
+    const int nf = (t_end - t) < kStageFrames ? (t_end - t) : kStageFrames;
+    for (int q = wl; q < nf * row; q += kWave) {
+      const int ff = q / row, b = q - ff * row;
+      lds_in[ff * row + b] = p.inputs[((int64_t)((gf + ff) % p.cap) * L + s0) * Pp + b];
+    }
+    __syncthreads();
+  };
+
+  // One step t.  kCore: every chain is active (t in [f0 + cd, f0 + n)) and no injected corruption.
+  auto step = [&](auto core_tag, int32_t t) {
+    constexpr bool kCore = decltype(core_tag)::value;
+    const int32_t rel = t - p.f0;
+    const int32_t c = t - j;  // this lane's chain
+    const bool active = kCore ? valid : (valid && c >= p.f0 && c < p.f0 + p.n);
+    const uint32_t in = lds_in[(rel & (kStageFrames - 1)) * row + in_lane];
+    bad |= __ballot(pend_ck != pend_first) & pend_lanes;
+    if (!kCore) w[0] ^= (t == p.corrupt_frame) ? corrupt_on : 0u;  // role 0 = chain t's load
+    // AdvanceFrame(t - cd) on every lane
+    {
+      float x = __builtin_bit_cast(float, w[0]), y = __builtin_bit_cast(float, w[1]);
+      float vx = __builtin_bit_cast(float, w[2]), vy = __builtin_bit_cast(float, w[3]);
+      float rot = __builtin_bit_cast(float, w[4]);
+      advance_player_v4(x, y, vx, vy, rot, in);
+      w[0] = __builtin_bit_cast(uint32_t, x);
+      w[1] = __builtin_bit_cast(uint32_t, y);
+      w[2] = __builtin_bit_cast(uint32_t, vx);
+      w[3] = __builtin_bit_cast(uint32_t, vy);
+      w[4] = __builtin_bit_cast(uint32_t, rot);
+    }
+    const uint32_t frame1 = (uint32_t)(t - cd + 1);
+    // rotation for step t+1: role j takes role j-1's state, Pp lanes down; two DPP wave_shr:1
+    // moves (VALU, no LDS round trip) and role 0 keeps its own
+    uint32_t nx[5];
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+      if constexpr (kDppRot) {
+        const uint32_t sh = wave_shr_lanes<Pp>(w[q]);
+        nx[q] = (w[q] & keep_own) | (sh & ~keep_own);  // a plain select here gets branched
+      } else {
+        nx[q] = (uint32_t)__builtin_amdgcn_ds_bpermute(src_rot, (int)w[q]);
+      }
+    }
+    if constexpr (!kDppRot) __builtin_amdgcn_sched_barrier(0);  // LDS latency behind the save
+    // Fletcher-16 of the post-advance state (frame t-cd+1): the cell role j+1 saves at step t+1
+    uint32_t d1 = dot4_u8(frame1, wf1, c1), d2 = dot4_u8(frame1, wf2, c2);
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+      d1 = dot4_u8(w[q], one2, d1);
+      d2 = dot4_u8(w[q], wt[q], d2);
+    }
+    if constexpr (Pp >= 2) {
+      d1 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d1, 0xB1, 0xF, 0xF, true);  // xor 1
+      d2 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d2, 0xB1, 0xF, 0xF, true);
+    }
+    if constexpr (Pp >= 4) {
+      d1 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d1, 0x4E, 0xF, 0xF, true);  // xor 2
+      d2 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d2, 0x4E, 0xF, 0xF, true);
+    }
+    const uint32_t ck = fletcher_from_doubled(d1, d2);
+    uint32_t first = (uint32_t)__builtin_amdgcn_ds_bpermute(src_first, (int)ck);
+    // the first save of frame t-cd+1 happened in the previous launch while its chain is not ours
+    if (!kCore && rel + 1 < cd) first = lds_first[(rel + 1) * kWave + g];
+    // SaveGameState(t-cd+1) for role j+1, first-seen, display checksum
+    const uint32_t sru = mod_small((uint32_t)rel + sr0, (uint32_t)R, magic_r);
+    const uint32_t stu = mod_small((uint32_t)rel + st0, (uint32_t)p.trace_cap, magic_t);
+    auto stores = [&]() {
+      const uint32_t so = sru * slot_bytes, cso = sru * ck_slot_bytes;
+#pragma unroll
+      for (int q = 0; q < 5; q++) __builtin_amdgcn_raw_buffer_store_b32(w[q], rs_ring, fo[q], so, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(frame1, rs_ring, fo_frame, so, 0);
+      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ring, co, cso, 0);
+      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ring, co_first, cso, 0);
+      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_trace, co_trace, stu * tr_slot_bytes, 0);
+    };
+    if (kCore) {
+      stores();
+      pend_lanes = cmp_lanes;
+    } else {
+      if (active) stores();
+      pend_lanes = cmp_lanes & __ballot(active);
+      if (active && j == cd && c == p.f0 + p.n - 1) {  // the launch's last call: current state
+        uint32_t* cur = p.cur + s;
+        if (owner) {
+#pragma unroll
+          for (int q = 0; q < 5; q++) cur[kq[q] * L] = w[q];
+        }
+        if (pl == 0) cur[0] = frame1;
+      }
+    }
+    pend_ck = ck;
+    pend_first = first;
+#pragma unroll
+    for (int q = 0; q < 5; q++) w[q] = nx[q];
+  };
+
+  int32_t t = p.f0;
+  for (; t < ramp_end; ++t) {
+    if (((t - p.f0) & (kStageFrames - 1)) == 0) stage(t);
+    step(std::false_type(), t);
+  }
+  while (t < core_end) {
+    const int32_t rel = t - p.f0;
+    if ((rel & (kStageFrames - 1)) == 0) stage(t);
+    const int32_t chunk_end = min(core_end, t + (kStageFrames - (rel & (kStageFrames - 1))));
+    for (; t < chunk_end; ++t) step(std::true_type(), t);
+  }
+  for (; t < t_end; ++t) {
+    if (((t - p.f0) & (kStageFrames - 1)) == 0) stage(t);
+    step(std::false_type(), t);
+  }
+  bad |= __ballot(pend_ck != pend_first) & pend_lanes;
+  if (bad && wl == __builtin_ctzll(bad)) atomicCAS(p.fail_f0, -1, p.f0);
 }
 
 // Checkpoint / restore of everything a SyncTest launch writes (cur, ring, ring_ck, first_ck):
@@ -1040,7 +1290,28 @@ static int launch_pipelined(ggrs_engine_t* e, int32_t f0, int32_t n) {
   const uint64_t F4L = (uint64_t)e->F * 4 * p.L;
   const bool fits_v3 = F4L * p.R < kOob && (uint64_t)2 * p.L * p.R < kOob &&
                        (uint64_t)2 * p.L * (uint64_t)std::max(p.trace_cap, 0) < kOob;
-  if (e->path == GGRS_PATH_PIPELINED && p.K * Pp <= kWave && fits_v3) {
+  // v4 addresses ring, ring_ck and first_ck from the ring's base (one descriptor)
+  const bool fits_v4 = fits_v3 && (uint8_t*)e->ring_ck > (uint8_t*)e->ring && (uint8_t*)e->first_ck > (uint8_t*)e->ring_ck &&
+                       (uint64_t)((uint8_t*)e->first_ck - (uint8_t*)e->ring) + (uint64_t)2 * p.L * p.R < kOob;
+  if ((e->path == GGRS_PATH_PIPELINED || e->path == GGRS_PATH_PIPELINED_V4_DPP) && p.K * Pp <= kWave && fits_v4) {
+    p.spw = kWave / (p.K * Pp);
+    const int64_t grid = grid_of(p.L, p.spw);
+    const bool dpp = e->path == GGRS_PATH_PIPELINED_V4_DPP;
+    return launch_timed(e, [&] {
+      switch (e->cfg.num_players * 2 + (dpp ? 1 : 0)) {
+        case 2: synctest_pipelined_v4_kernel<1, false><<<grid, kWave, 0, e->stream>>>(p); break;
+        case 3: synctest_pipelined_v4_kernel<1, true><<<grid, kWave, 0, e->stream>>>(p); break;
+        case 4: synctest_pipelined_v4_kernel<2, false><<<grid, kWave, 0, e->stream>>>(p); break;
+        case 5: synctest_pipelined_v4_kernel<2, true><<<grid, kWave, 0, e->stream>>>(p); break;
+        case 6: synctest_pipelined_v4_kernel<3, false><<<grid, kWave, 0, e->stream>>>(p); break;
+        case 7: synctest_pipelined_v4_kernel<3, true><<<grid, kWave, 0, e->stream>>>(p); break;
+        case 8: synctest_pipelined_v4_kernel<4, false><<<grid, kWave, 0, e->stream>>>(p); break;
+        default: synctest_pipelined_v4_kernel<4, true><<<grid, kWave, 0, e->stream>>>(p); break;
+      }
+    });
+  }
+  if ((e->path == GGRS_PATH_PIPELINED || e->path == GGRS_PATH_PIPELINED_V3 ||
+       e->path == GGRS_PATH_PIPELINED_V4_DPP) && p.K * Pp <= kWave && fits_v3) {
     p.spw = kWave / (p.K * Pp);
     const int64_t grid = grid_of(p.L, p.spw);
     return launch_timed(e, [&] {
@@ -1052,7 +1323,8 @@ static int launch_pipelined(ggrs_engine_t* e, int32_t f0, int32_t n) {
       }
     });
   }
-  if ((e->path == GGRS_PATH_PIPELINED || e->path == GGRS_PATH_PIPELINED_SPLIT) && p.K * Pp <= kWave) {
+  if ((e->path == GGRS_PATH_PIPELINED || e->path == GGRS_PATH_PIPELINED_SPLIT ||
+       e->path == GGRS_PATH_PIPELINED_V3 || e->path == GGRS_PATH_PIPELINED_V4_DPP) && p.K * Pp <= kWave) {
     p.spw = kWave / (p.K * Pp);
     const int64_t grid = grid_of(p.L, p.spw);
     return launch_timed(e, [&] {
@@ -1142,7 +1414,7 @@ int ggrs_synctest_advance_frames(ggrs_engine_t* e, int32_t n) {
 int ggrs_set_synctest_path(ggrs_engine_t* e, int32_t path) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
   if (path != GGRS_PATH_PIPELINED && path != GGRS_PATH_SEQUENTIAL && path != GGRS_PATH_PIPELINED_WHOLE &&
-      path != GGRS_PATH_PIPELINED_SPLIT)
+      path != GGRS_PATH_PIPELINED_SPLIT && path != GGRS_PATH_PIPELINED_V3 && path != GGRS_PATH_PIPELINED_V4_DPP)
     return set_error(GGRS_E_INVALID, "unknown path %d", path);
   int rc = resolve(e);
   if (rc) return rc;

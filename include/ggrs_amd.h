@@ -70,7 +70,10 @@ extern "C" {
 #define GGRS_PATH_SEQUENTIAL 1      /* one lane per session, calls in order */
 #define GGRS_PATH_PIPELINED_WHOLE 2 /* pipelined, one lane per chain (all players in one lane) */
 #define GGRS_PATH_PIPELINED_SPLIT 3 /* pipelined, players split over lanes (the round-1 v2 kernel;
-                                       the default path runs its v3 successor when buffers < 1 GiB) */
+                                       the default path runs its v4 successor when buffers < 1 GiB) */
+#define GGRS_PATH_PIPELINED_V3 4    /* pipelined v3 (rotating chain roles), kept for comparison */
+#define GGRS_PATH_PIPELINED_V4_DPP 5 /* pipelined v4 with the chain rotation by DPP wave shifts
+                                        (the default v4 path rotates through ds_bpermute) */
 
 /* per-lane status */
 #define GGRS_LANE_RUNNING 0

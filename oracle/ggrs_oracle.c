@@ -530,6 +530,8 @@ typedef struct {
   uint16_t last_checksum;
   int random_checksums;   /* tests/stubs.rs RandomChecksumGameStub analogue (fault injector) */
   uint64_t rng;
+  int32_t desync_frame;   /* fault injector: the advance FROM this frame flips x0's lowest bit,
+                             on every (re)simulation -- a deterministic desync of this peer; -1 off */
 } Game;
 
 static uint64_t splitmix64(uint64_t* st) {
@@ -559,7 +561,11 @@ static void game_handle_requests(Game* g, SyncLayer* sl, const RequestVec* rv, i
       State st; state_clone(&st, &g->game_state);
       cell_save(c, r->frame, &st, 1, cs);
     } else { /* advance_frame :115-127 */
+      const int32_t from = g->game_state.frame;
       state_advance(&g->game_state, r->inputs, r->status);
+      if (g->desync_frame >= 0 && from == g->desync_frame) {
+        uint32_t u; memcpy(&u, &g->game_state.positions[0], 4); u ^= 1u; memcpy(&g->game_state.positions[0], &u, 4);
+      }
       g->last_checksum = state_checksum(&g->game_state);
       g->last_checksum_frame = g->game_state.frame;
     }
@@ -617,6 +623,7 @@ int oracle_synctest_run(const OracleSyncTestCfg* cfg, int32_t frames, const uint
                         (size_t)cfg->check_distance, (size_t)cfg->input_delay, cfg->predictor);
   if (rc) { res->status = -1; return rc; }
   Game g; memset(&g, 0, sizeof g);
+  g.desync_frame = -1;
   state_new(&g.game_state, (uint64_t)cfg->num_players);
   g.last_checksum_frame = NULL_FRAME;
   g.random_checksums = cfg->random_checksums; g.rng = cfg->rng_seed;
@@ -745,6 +752,7 @@ static void* bench_worker(void* a) {
   size_t P = (size_t)j->cfg.num_players;
   if (synctest_new(&s, P, (size_t)j->cfg.max_prediction, (size_t)j->cfg.check_distance, (size_t)j->cfg.input_delay, j->cfg.predictor)) { j->failed = 1; return NULL; }
   Game g; memset(&g, 0, sizeof g);
+  g.desync_frame = -1;
   state_new(&g.game_state, P);
   RequestVec rv = {0};
   uint64_t st = j->seed; uint8_t prev[MAX_PLAYERS] = {0, 0, 0, 0};
@@ -834,6 +842,7 @@ int oracle_p2p_replay(int32_t P, const uint8_t* state_in, int32_t load_frame, in
   SyncLayer sl;
   sl_new(&sl, (size_t)P, (size_t)max_prediction, PREDICT_REPEAT_LAST);
   Game g; memset(&g, 0, sizeof g);
+  g.desync_frame = -1;
   state_from_bytes(&g.game_state, state_in);
   ORACLE_ASSERT(g.game_state.frame == load_frame, "state_in frame != load_frame");
   /* the cell of load_frame was saved when the session passed it */
@@ -877,6 +886,85 @@ int oracle_p2p_replay(int32_t P, const uint8_t* state_in, int32_t load_frame, in
  * assert, local_connect_status.last_frame, SyncLayer::add_remote_input, sync_layer.rs:271-277).
  * Local players' inputs enter with add_local_input (:219-246) before each call; their queues
  * carry the input delay (p2p_session.rs:183).  The remote peer runs with input delay 0. */
+/* ---------------------------------------------------------------- desync detection
+ * DesyncDetection::On { interval } (p2p_session.rs:281-291 call order, :904-975) and one remote
+ * endpoint's pending checksum reports (protocol.rs:27 MAX_CHECKSUM_HISTORY_SIZE, :663-682). */
+#define MAX_CHECKSUM_HISTORY_SIZE 32
+typedef struct { int32_t frame; uint16_t cs; } CsEntry;
+typedef struct { int32_t frame; uint16_t local_cs, remote_cs; } DesyncEvent;
+typedef struct {
+  int32_t interval;                                   /* 0: DesyncDetection::Off */
+  int32_t last_sent;                                  /* last_sent_checksum_frame */
+  CsEntry local[MAX_CHECKSUM_HISTORY_SIZE + 2];       /* local_checksum_history */
+  size_t n_local;
+  CsEntry pending[MAX_CHECKSUM_HISTORY_SIZE + 2];     /* remote.pending_checksums */
+  size_t n_pending;
+} Desync;
+
+static void cs_retain(CsEntry* v, size_t* n, int32_t oldest) { /* HashMap::retain(frame >= oldest) */
+  size_t k = 0;
+  for (size_t i = 0; i < *n; i++) if (v[i].frame >= oldest) v[k++] = v[i];
+  *n = k;
+}
+static void cs_insert(CsEntry* v, size_t* n, int32_t frame, uint16_t cs) { /* HashMap::insert */
+  for (size_t i = 0; i < *n; i++) if (v[i].frame == frame) { v[i].cs = cs; return; }
+  v[*n].frame = frame; v[*n].cs = cs; *n += 1;
+}
+
+/* on_checksum_report (protocol.rs:663-682) */
+static void ds_on_checksum_report(Desync* d, int32_t frame, uint16_t cs) {
+  if (d->n_pending >= MAX_CHECKSUM_HISTORY_SIZE)
+    cs_retain(d->pending, &d->n_pending, frame - (MAX_CHECKSUM_HISTORY_SIZE - 1) * d->interval);
+  cs_insert(d->pending, &d->n_pending, frame, cs);
+}
+
+/* check_checksum_send_interval (p2p_session.rs:939-975): returns 1 with the report sent. */
+static int ds_check_send(Desync* d, const SyncLayer* sl, int32_t* frame_out, uint16_t* cs_out) {
+  const int32_t fts = d->last_sent == NULL_FRAME ? d->interval : d->last_sent + d->interval;
+  int sent = 0;
+  if (fts <= sl->last_confirmed_frame && fts <= sl->last_saved_frame) {
+    const Cell* c = sl_saved_state_by_frame(sl, fts);
+    ORACLE_ASSERT(c != NULL, "cell not found!");
+    if (c->has_checksum) {
+      *frame_out = fts;
+      *cs_out = c->checksum;
+      sent = 1;
+      d->last_sent = fts;
+      cs_insert(d->local, &d->n_local, fts, c->checksum);
+    }
+    if (d->n_local > MAX_CHECKSUM_HISTORY_SIZE)
+      cs_retain(d->local, &d->n_local, fts - (MAX_CHECKSUM_HISTORY_SIZE - 1) * d->interval);
+  }
+  return sent;
+}
+
+/* compare_local_checksums_against_peers (p2p_session.rs:904-937).  HashMap iteration order is
+ * unspecified; pending reports are visited in frame order here. */
+static size_t ds_compare(Desync* d, int32_t last_confirmed, DesyncEvent* ev, size_t cap) {
+  size_t n_ev = 0;
+  int checked[MAX_CHECKSUM_HISTORY_SIZE + 2] = {0};
+  for (;;) { /* visit in ascending frame order */
+    size_t best = (size_t)-1;
+    for (size_t i = 0; i < d->n_pending; i++)
+      if (!checked[i] && (best == (size_t)-1 || d->pending[i].frame < d->pending[best].frame)) best = i;
+    if (best == (size_t)-1) break;
+    checked[best] = 1; /* visited */
+    const CsEntry r = d->pending[best];
+    if (r.frame >= last_confirmed) { checked[best] = 2; continue; } /* still waiting for inputs */
+    size_t li = (size_t)-1;
+    for (size_t i = 0; i < d->n_local; i++) if (d->local[i].frame == r.frame) li = i;
+    if (li == (size_t)-1) { checked[best] = 2; continue; }
+    if (d->local[li].cs != r.cs && n_ev < cap) {
+      ev[n_ev].frame = r.frame; ev[n_ev].local_cs = d->local[li].cs; ev[n_ev].remote_cs = r.cs; n_ev++;
+    }
+    checked[best] = 3; /* checked_frames: removed below */
+  }
+  size_t k = 0;
+  for (size_t i = 0; i < d->n_pending; i++) if (checked[i] != 3) d->pending[k++] = d->pending[i];
+  d->n_pending = k;
+  return n_ev;
+}
+
 typedef struct {
   size_t num_players, max_prediction;
   uint32_t local_mask;
@@ -888,6 +976,12 @@ typedef struct {
   PlayerInput local[MAX_PLAYERS];
   int has_local[MAX_PLAYERS];
   int64_t rollbacks, resim;
+  Desync* ds;                /* desync detection, NULL = Off */
+  int sent;                  /* this call's checksum report (frame, checksum), if sent */
+  int32_t sent_frame;
+  uint16_t sent_cs;
+  DesyncEvent events[8];     /* this call's DesyncDetected events */
+  size_t n_events;
 } P2PSession;
 
 /* confirmed_frame (:542-553) */
@@ -944,6 +1038,12 @@ static int p2p_advance_frame(P2PSession* s, RequestVec* rv, int* advanced) {
   *advanced = 0;
   for (size_t h = 0; h < s->num_players; h++)
     if (((s->local_mask >> h) & 1u) && !s->has_local[h]) return -1;
+  s->sent = 0;
+  s->n_events = 0;
+  if (s->ds && s->ds->interval > 0) {                                        /* :281-291 */
+    s->sent = ds_check_send(s->ds, &s->sl, &s->sent_frame, &s->sent_cs);
+    s->n_events = ds_compare(s->ds, s->sl.last_confirmed_frame, s->events, 8);
+  }
   if (s->sl.current_frame == 0) rv_push(rv, sl_save_current_state(&s->sl)); /* :305-308 */
   int32_t confirmed = p2p_confirmed_frame(s);                                /* :314 */
   int32_t first_incorrect = sl_check_simulation_consistency(&s->sl, s->disconnect_frame);
@@ -1009,6 +1109,7 @@ int oracle_p2p_run(const OracleP2PCfg* cfg, int32_t frames, const uint8_t* input
   }
   s.disconnect_frame = NULL_FRAME;
   Game g; memset(&g, 0, sizeof g);
+  g.desync_frame = -1;
   state_new(&g.game_state, (uint64_t)P);
   g.last_checksum_frame = NULL_FRAME;
   RequestVec rv = {0};
@@ -1060,6 +1161,81 @@ int oracle_p2p_run(const OracleP2PCfg* cfg, int32_t frames, const uint8_t* input
   state_free(&g.game_state);
   sl_free(&s.sl);
   return res->status;
+}
+
+/* ---------------------------------------------------------------- two peers with desync detection
+ * Both machines of one match, stepped call by call: peer k's local players are local_mask[k], every
+ * other player is remote; inputs[g][P] are all players' inputs of frame g (input delay 0 on both,
+ * so both peers simulate the same match).  Inputs and checksum reports a peer sends in call g are
+ * received by the other at the start of call g + latency (poll_remote_clients).  Peer
+ * `desync_peer` runs a deterministic desync from `desync_frame` (Game.desync_frame), -1 for none.
+ * Per peer k and call f: sent_frame[k][f] / sent_cs[k][f] = the checksum report sent (-1 none),
+ * and the DesyncDetected events raised (ev_* arrays, n_ev total; ev_peer / ev_call say where). */
+int oracle_p2p_desync_pair_run(int32_t num_players, int32_t max_prediction, int32_t latency,
+                               const int32_t* local_mask, int32_t predictor, int32_t interval,
+                               int32_t frames, const uint8_t* inputs, int32_t desync_peer,
+                               int32_t desync_frame, int32_t* sent_frame, uint16_t* sent_cs,
+                               int32_t ev_cap, int32_t* ev_peer, int32_t* ev_call, int32_t* ev_frame,
+                               uint16_t* ev_local, uint16_t* ev_remote, int32_t* n_ev,
+                               uint16_t* cksum_trace) {
+  const size_t P = (size_t)num_players;
+  *n_ev = 0;
+  if (P < 2 || P > MAX_PLAYERS || max_prediction < 1 || latency < 1 || latency >= max_prediction ||
+      interval < 0)
+    return -1;
+  for (int k = 0; k < 2; k++)
+    if ((local_mask[k] & ~((1 << P) - 1)) != 0 || local_mask[k] == 0) return -1;
+  P2PSession s[2];
+  Game g[2];
+  Desync ds[2];
+  RequestVec rv = {0};
+  memset(s, 0, sizeof s); memset(g, 0, sizeof g); memset(ds, 0, sizeof ds);
+  for (int k = 0; k < 2; k++) {
+    s[k].num_players = P; s[k].max_prediction = (size_t)max_prediction;
+    s[k].local_mask = (uint32_t)local_mask[k]; s[k].latency = latency;
+    sl_new(&s[k].sl, P, s[k].max_prediction, predictor);
+    for (size_t i = 0; i < P; i++) s[k].last_frame[i] = NULL_FRAME;
+    s[k].disconnect_frame = NULL_FRAME;
+    ds[k].interval = interval; ds[k].last_sent = NULL_FRAME;
+    s[k].ds = &ds[k];
+    state_new(&g[k].game_state, (uint64_t)P);
+    g[k].last_checksum_frame = NULL_FRAME;
+    g[k].desync_frame = k == desync_peer ? desync_frame : -1;
+  }
+  int rc = 0;
+  for (int32_t f = 0; f < frames && rc == 0; f++) {
+    for (int k = 0; k < 2; k++) {
+      P2PSession* me = &s[k];
+      const int other = 1 - k;
+      const int32_t arrive = f - latency; /* poll_remote_clients: what the other sent at call f - latency */
+      if (arrive >= 0) {
+        for (size_t i = 0; i < P; i++)
+          if (!((me->local_mask >> i) & 1u)) p2p_on_remote_input(me, i, arrive, inputs[(size_t)arrive * P + i]);
+        if (sent_frame[(size_t)other * frames + arrive] >= 0)
+          ds_on_checksum_report(&ds[k], sent_frame[(size_t)other * frames + arrive], sent_cs[(size_t)other * frames + arrive]);
+      }
+      for (size_t i = 0; i < P; i++)
+        if ((me->local_mask >> i) & 1u) {
+          me->local[i].frame = me->sl.current_frame; me->local[i].input = inputs[(size_t)f * P + i]; me->has_local[i] = 1;
+        }
+      int advanced = 0;
+      if (p2p_advance_frame(me, &rv, &advanced) < 0 || !advanced) { rc = -2; break; }
+      sent_frame[(size_t)k * frames + f] = me->sent ? me->sent_frame : -1;
+      sent_cs[(size_t)k * frames + f] = me->sent ? me->sent_cs : 0;
+      for (size_t e = 0; e < me->n_events; e++) {
+        if (*n_ev < ev_cap) {
+          ev_peer[*n_ev] = k; ev_call[*n_ev] = f; ev_frame[*n_ev] = me->events[e].frame;
+          ev_local[*n_ev] = me->events[e].local_cs; ev_remote[*n_ev] = me->events[e].remote_cs;
+        }
+        *n_ev += 1;
+      }
+      game_handle_requests(&g[k], &me->sl, &rv, 0);
+      if (cksum_trace) cksum_trace[(size_t)k * frames + f] = g[k].last_checksum;
+    }
+  }
+  free(rv.v);
+  for (int k = 0; k < 2; k++) { state_free(&g[k].game_state); sl_free(&s[k].sl); }
+  return rc;
 }
 
 /* ================================================================ config-5 particle world

@@ -1,6 +1,8 @@
-"""GPU KAT of the product sinf/cosf restatement: the order-independent digest of every f32 in
-[0, 2*pi] (each reachable ship rotation is in there, SURVEY.md finding 3) must equal the digest of
-glibc libm's values pinned in tests/golden/golden.json; both the separate and the fused form."""
+"""GPU KATs of the product step arithmetic.  The sinf/cosf restatement: the order-independent
+digest of every f32 in [0, 2*pi] (each reachable ship rotation is in there, SURVEY.md finding 3)
+must equal the digest of glibc libm's values pinned in tests/golden/golden.json, both the separate
+and the fused form.  The v4 step (advance_player_lean): its clamp square root on every f32 above
+49, and the whole player step against the v3 step on random states."""
 import ctypes
 import json
 import os
@@ -27,6 +29,9 @@ def katlib(tmp_path_factory):
     L = ctypes.CDLL(so)
     L.kat_digest.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
     L.kat_values.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    L.kat_sqrt49.argtypes = [ctypes.POINTER(ctypes.c_uint64)]
+    L.kat_lean_step.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
+    L.kat_clamp_div.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
     return L
 
 
@@ -47,3 +52,27 @@ def test_device_values(katlib):
         if s["x"] in (0x7F800000,):
             continue
         assert (int(sv[i]), int(cv[i])) == (s["sin"], s["cos"]), hex(s["x"])
+
+
+def test_clamp_sqrt_every_f32_above_49(katlib):
+    """The v4 step's square root (taken only when s > 49) equals hipcc's correctly rounded sqrtf
+    bit for bit on every f32 in (49, +inf]."""
+    bad = ctypes.c_uint64()
+    assert katlib.kat_sqrt49(ctypes.byref(bad)) == 0
+    assert bad.value == 0
+
+
+def test_lean_step_equals_domain_step(katlib):
+    """advance_player_lean (v4) == advance_player_domain (v3) bitwise on 2^25 random player
+    states x 16 inputs (edges, zero, -0 and subnormal velocities included)."""
+    bad = ctypes.c_uint64()
+    assert katlib.kat_lean_step(0x6767, 64, ctypes.byref(bad)) == 0
+    assert bad.value == 0
+
+
+def test_clamp_division_through_f64_reciprocal(katlib):
+    """RN32(a * refined 1/m in binary64) == a / m (correctly rounded) for every f32 divisor m in
+    (7, 16] x 1024 random numerators of every exponent below 2^8 (~9.4e9 divisions)."""
+    bad = ctypes.c_uint64()
+    assert katlib.kat_clamp_div(0x6767, 1024, ctypes.byref(bad)) == 0
+    assert bad.value == 0

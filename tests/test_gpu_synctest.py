@@ -22,7 +22,7 @@ def lane_inputs(O, base_seed, lanes, frames, players, model):
                      for l in range(lanes)], axis=1)  # [frames][lanes][P]
 
 
-PATHS = [0, 1, 2, 3]  # PIPELINED (v3), SEQUENTIAL, PIPELINED_WHOLE, PIPELINED_SPLIT (v2)
+PATHS = [0, 1, 2, 3, 4, 5]  # PIPELINED (v4), SEQUENTIAL, PIPELINED_WHOLE, PIPELINED_SPLIT (v2), V3, V4_DPP
 
 
 def make_engine(lanes, P, maxp, cd, d, frames, trace=True, path=0):
@@ -173,6 +173,20 @@ def test_full_size_config2(oracle, path):
         check_lane(oracle, eng, inputs, lane, P, maxp, cd, d, F, tr)
     st, _, _ = eng.mismatches()
     assert (st == 0).all()
+
+
+@pytest.mark.parametrize("path", PATHS)
+@pytest.mark.parametrize("lanes,P", [(67, 2), (37, 4), (10, 3)])
+def test_ragged_last_block_every_lane(oracle, path, lanes, P):
+    """Lane counts that leave the last workgroup partly empty (idle lanes there map past the
+    last session): every lane's trace and final state bit-exact, across an input restage."""
+    maxp, cd, d, F = 9, 8, 1, 300
+    inputs = lane_inputs(oracle, 11, lanes, F, P, 0)
+    eng = make_engine(lanes, P, maxp, cd, d, F, path=path)
+    run_chunks(eng, inputs, [F])
+    tr = eng.trace(0, F)
+    for lane in range(lanes):
+        check_lane(oracle, eng, inputs, lane, P, maxp, cd, d, F, tr)
 
 
 @pytest.mark.parametrize("path", PATHS)
