@@ -57,7 +57,16 @@ struct P2PParams {
   int32_t* rollbacks;
   int64_t* resim;
   uint16_t* trace;
+  // desync detection (p2p_session.rs:939-975): interval (0 off) and the local checksum history,
+  // [kHist][S] u16, slot (frame / interval) % kHist
+  int32_t desync_interval;
+  uint16_t* hist;
+  // debug: the advance FROM dbg_frame of session dbg_sess flips x0's lowest bit (every replay)
+  int64_t dbg_sess;
+  int32_t dbg_frame;
 };
+
+constexpr int kHist = 32;  // MAX_CHECKSUM_HISTORY_SIZE (protocol.rs:27)
 
 // The per-session state of every remote player's InputQueue that the P2P program reads.
 template <int P>
@@ -134,7 +143,22 @@ __global__ __launch_bounds__(256) void p2p_kernel(P2PParams p) {
   }
   int32_t rollbacks = 0;
   int64_t resim = 0;
+  const bool dbg = sess == p.dbg_sess;
+  auto advance = [&](uint32_t in) {
+    const uint32_t from = st.w[0];
+    advance_state<P>(st, in, 0u);
+    if (dbg && (int32_t)from == p.dbg_frame) st.w[fld_x(P, 0)] ^= 1u;
+  };
   for (int32_t f = p.f0; f < p.f0 + p.n; ++f) {
+    // 0. check_checksum_send_interval (p2p_session.rs:939-975), before any rollback of this call:
+    //    last_confirmed_frame = f - 1 - D and last_saved_frame = f - 1 here, so frame_to_send =
+    //    interval, 2 interval, ... goes out at call frame_to_send + D + 1; its cell is in the ring
+    //    (D + 1 < R), its checksum enters the local history
+    if (p.desync_interval > 0) {
+      const int32_t fts = f - 1 - p.D;
+      if (fts >= p.desync_interval && fts % p.desync_interval == 0)
+        p.hist[(int64_t)((fts / p.desync_interval) % kHist) * S + sess] = p.ring_ck[(int64_t)(fts % p.R) * S + sess];
+    }
     // 1. poll_remote_clients: the remote input of frame g = f - D (add_input_by_frame)
     const int32_t g = f - p.D;
     const int32_t last_added = g >= 0 ? g : kNull;
@@ -169,7 +193,7 @@ __global__ __launch_bounds__(256) void p2p_kernel(P2PParams p) {
       for (int32_t h = first_inc; h < f; ++h) {
         const uint32_t in = sync_inputs<P>(p, q, h, last_added, sess);
         if (h > first_inc) save_cell<P>(p, st, h, sess);
-        advance_state<P>(st, in, 0u);
+        advance(in);
       }
       rollbacks += 1;
       resim += f - first_inc;
@@ -177,7 +201,7 @@ __global__ __launch_bounds__(256) void p2p_kernel(P2PParams p) {
     // 4. save the current frame; 5. advance with synchronized inputs
     save_cell<P>(p, st, f, sess);
     const uint32_t in = sync_inputs<P>(p, q, f, last_added, sess);
-    advance_state<P>(st, in, 0u);
+    advance(in);
     if (p.trace) p.trace[(int64_t)(f % p.trace_cap) * S + sess] = fletcher16_state<P>(st);
   }
   store_state<P>(st, p.cur + sess, S);
@@ -190,6 +214,19 @@ __global__ __launch_bounds__(256) void p2p_kernel(P2PParams p) {
   }
   p.rollbacks[sess] += rollbacks;
   p.resim[sess] += resim;
+}
+
+// compare_local_checksums_against_peers for one report frame, every session at once: bit s of
+// mask = local[s] != remote[s] (p2p_session.rs:915-926), count = number of set bits.
+__global__ __launch_bounds__(256) void compare_checksums_kernel(const uint16_t* local, const uint16_t* remote, int64_t S,
+                                                                 uint64_t* mask, int32_t* count) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool differ = s < S && local[s] != remote[s];
+  const uint64_t bits = __ballot(differ);
+  if ((threadIdx.x & 63) == 0 && s < S) {
+    mask[s >> 6] = bits;
+    if (bits) atomicAdd(count, __popcll(bits));
+  }
 }
 
 // every queue starts empty: prediction.frame, first_incorrect, last_requested = NULL, input 0
@@ -219,6 +256,12 @@ struct ggrs_p2p_engine {
   size_t staging_bytes = 0;
   int32_t current_frame = 0;
   int32_t next_input_frame = 0;
+  int32_t desync_interval = 0;
+  uint16_t* hist = nullptr;     // [kHist][S] local checksum history
+  uint64_t* cmp_mask = nullptr; // [ceil(S/64)] compare result
+  int32_t* cmp_count = nullptr;
+  int64_t dbg_sess = -1;
+  int32_t dbg_frame = -1;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<hipEvent_t> tev;
   size_t tev_used = 0;
@@ -261,7 +304,8 @@ int ggrs_p2p_engine_destroy(ggrs_p2p_engine_t* e) {
   if (!e) return GGRS_OK;
   (void)hipSetDevice(e->cfg.device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
-  void* bufs[] = {e->cur, e->ring, e->ring_ck, e->inputs, e->queue, e->rollbacks, e->resim, e->trace, e->staging};
+  void* bufs[] = {e->cur, e->ring, e->ring_ck, e->inputs, e->queue, e->rollbacks, e->resim, e->trace, e->staging,
+                  e->hist, e->cmp_mask, e->cmp_count};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (hipEvent_t ev : e->tev) (void)hipEventDestroy(ev);
@@ -403,6 +447,10 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
   p.rollbacks = e->rollbacks;
   p.resim = e->resim;
   p.trace = e->trace;
+  p.desync_interval = e->desync_interval;
+  p.hist = e->hist;
+  p.dbg_sess = e->dbg_sess;
+  p.dbg_frame = e->dbg_frame;
   // rows the calls read must still be in the ring: rows >= oldest_row(f0) up to f0 + n - 1
   if ((int64_t)p.f0 + n - 1 - oldest_row(e, p.f0) >= e->cap)
     return set_error(GGRS_E_INVALID, "advance of %d frames reads more input rows than input_capacity (%d)", n, e->cap);
@@ -414,6 +462,85 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
   });
   if (rc) return rc;
   e->current_frame += n;
+  return GGRS_OK;
+}
+
+int ggrs_p2p_set_desync_detection(ggrs_p2p_engine_t* e, int32_t interval) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  if (interval < 0) return set_error(GGRS_E_INVALID, "interval must be >= 0 (0 = DesyncDetection::Off)");
+  if (e->current_frame != 0)
+    return set_error(GGRS_E_STATE, "desync detection is part of the session's configuration (set before the first frame)");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const int64_t S = e->cfg.num_sessions;
+  if (interval > 0 && !e->hist) {
+    HIP_TRY(hipMalloc(&e->hist, sizeof(uint16_t) * kHist * S));
+    HIP_TRY(hipMemsetAsync(e->hist, 0, sizeof(uint16_t) * kHist * S, e->stream));
+    HIP_TRY(hipMalloc(&e->cmp_mask, sizeof(uint64_t) * ((S + 63) / 64)));
+    HIP_TRY(hipMalloc(&e->cmp_count, sizeof(int32_t)));
+  }
+  e->desync_interval = interval;
+  return GGRS_OK;
+}
+
+int ggrs_p2p_debug_desync(ggrs_p2p_engine_t* e, int32_t session, int32_t frame) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  if (session >= e->cfg.num_sessions) return set_error(GGRS_E_INVALID, "session out of range");
+  e->dbg_sess = session;
+  e->dbg_frame = session < 0 ? -1 : frame;
+  return GGRS_OK;
+}
+
+// The local history row of report frame `frame`: sent at call frame + D + 1, kept while it is one
+// of the kHist newest reports (local_checksum_history retention, p2p_session.rs:965-970).
+static int hist_row(ggrs_p2p_engine_t* e, int32_t frame, const uint16_t** row) {
+  const int32_t I = e->desync_interval, D = e->cfg.remote_latency;
+  if (I <= 0) return set_error(GGRS_E_STATE, "desync detection is off");
+  if (frame < I || frame % I != 0) return set_error(GGRS_E_PRECONDITION, "frame %d is not a checksum report frame", frame);
+  const int32_t newest = e->current_frame - 2 - D;  // frame_to_send of the last call run
+  if (frame > newest) return set_error(GGRS_E_PRECONDITION, "frame %d not reported yet", frame);
+  if (frame <= newest - kHist * I) return set_error(GGRS_E_PRECONDITION, "frame %d left the checksum history", frame);
+  *row = e->hist + (int64_t)((frame / I) % kHist) * e->cfg.num_sessions;
+  return GGRS_OK;
+}
+
+int ggrs_p2p_local_checksums(ggrs_p2p_engine_t* e, int32_t frame, uint16_t* out, int32_t out_on_device) {
+  if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
+  const uint16_t* row = nullptr;
+  int rc = hist_row(e, frame, &row);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  HIP_TRY(hipMemcpyAsync(out, row, 2 * (size_t)e->cfg.num_sessions,
+                         out_on_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return GGRS_OK;
+}
+
+int ggrs_p2p_compare_checksums(ggrs_p2p_engine_t* e, int32_t frame, const uint16_t* remote, int32_t remote_on_device,
+                               uint64_t* mask, int32_t* n_differ) {
+  if (!e || !remote || !mask || !n_differ) return set_error(GGRS_E_INVALID, "null argument");
+  const uint16_t* row = nullptr;
+  int rc = hist_row(e, frame, &row);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const int64_t S = e->cfg.num_sessions;
+  const uint16_t* rdev = remote;
+  if (!remote_on_device) {
+    if ((size_t)2 * S > e->staging_bytes) {
+      if (e->staging) HIP_TRY(hipFree(e->staging));
+      e->staging = nullptr;
+      e->staging_bytes = 0;
+      HIP_TRY(hipMalloc(&e->staging, 2 * S));
+      e->staging_bytes = 2 * S;
+    }
+    HIP_TRY(hipMemcpyAsync(e->staging, remote, 2 * S, hipMemcpyHostToDevice, e->stream));
+    rdev = (const uint16_t*)e->staging;
+  }
+  HIP_TRY(hipMemsetAsync(e->cmp_count, 0, sizeof(int32_t), e->stream));
+  compare_checksums_kernel<<<grid_of(S, 256), 256, 0, e->stream>>>(row, rdev, S, e->cmp_mask, e->cmp_count);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(mask, e->cmp_mask, 8 * (size_t)((S + 63) / 64), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(n_differ, e->cmp_count, sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
   return GGRS_OK;
 }
 

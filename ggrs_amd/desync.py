@@ -1,0 +1,121 @@
+"""P2P desync detection for every session of a P2PEngine: the host-side bookkeeping of
+DesyncDetection::On{interval} around the device-resident checksum history.
+
+Reference semantics restated (caspark/ggrs 0.10.2):
+  * P2PSession::advance_frame runs check_checksum_send_interval, then
+    compare_local_checksums_against_peers, before any rollback of the call
+    (src/sessions/p2p_session.rs:281-291);
+  * check_checksum_send_interval (:939-975): frame_to_send = interval, 2 interval, ... once
+    <= last_confirmed_frame and last_saved_frame; the saved cell's checksum is sent to every remote
+    and kept in local_checksum_history, pruned to MAX_CHECKSUM_HISTORY_SIZE = 32 reports
+    (src/network/protocol.rs:27).  The device records it (ggrs_p2p_set_desync_detection); in the
+    engine's network model that is call frame_to_send + remote_latency + 1;
+  * UdpProtocol::on_checksum_report (protocol.rs:663-682) keeps received reports in
+    pending_checksums, pruned to frames >= frame - 31 interval once 32 are pending;
+  * compare_local_checksums_against_peers (:904-937): every pending report with
+    frame < last_confirmed_frame whose frame is in the local history is compared (on the device,
+    ggrs_p2p_compare_checksums), raising GgrsEvent::DesyncDetected per differing session, and is
+    removed; the others stay pending.
+Reports travel between peers like inputs: what a peer sends in call g is received at the start of
+call g + remote_latency.  Pending reports are visited in frame order (the reference iterates a
+HashMap, whose order is unspecified).
+"""
+from dataclasses import dataclass
+
+MAX_CHECKSUM_HISTORY_SIZE = 32  # src/network/protocol.rs:27
+
+
+@dataclass
+class DesyncDetected:
+    """GgrsEvent::DesyncDetected (src/lib.rs:158-167) for one session; `call` is the advance_frame
+    call that raised it, `addr` the remote peer."""
+    frame: int
+    session: int
+    local_checksum: int
+    remote_checksum: int
+    addr: object
+    call: int
+
+
+class DesyncDetector:
+    """One peer's desync detection against one remote peer, for all sessions of `engine`."""
+
+    def __init__(self, engine, interval, addr=None):
+        self.engine = engine
+        self.interval = interval
+        self.addr = addr
+        self.latency = engine.remote_latency
+        engine.set_desync_detection(interval)
+        self.local_history = []   # report frames held in the device history, oldest first
+        self.pending = {}         # frame -> remote report ([S] u16 numpy or device tensor)
+        self.arrivals = {}        # call -> [(frame, report)] received at the start of that call
+        self.processed = 0        # calls whose desync steps have been replayed on the host
+        self.sent = 0             # calls whose outgoing reports have been handed out
+
+    def _send_frame(self, call):
+        """frame_to_send that goes out in `call`, or None."""
+        fts = call - 1 - self.latency
+        return fts if self.interval > 0 and fts >= self.interval and fts % self.interval == 0 else None
+
+    def outgoing(self, device_out=None):
+        """Reports sent in the calls run since the last outgoing(): [(call, frame, report)]."""
+        out = []
+        current = self.engine.current_frame()
+        for call in range(self.sent, current):
+            fts = self._send_frame(call)
+            if fts is not None:
+                out.append((call, fts, self.engine.local_checksums(fts)))
+        self.sent = current
+        return out
+
+    def receive(self, sent_call, frame, report):
+        """The remote's report of `frame`, sent in its call `sent_call`: received at the start of
+        call sent_call + latency."""
+        self.arrivals.setdefault(sent_call + self.latency, []).append((frame, report))
+
+    def _on_checksum_report(self, frame, report):
+        if len(self.pending) >= MAX_CHECKSUM_HISTORY_SIZE:
+            oldest = frame - (MAX_CHECKSUM_HISTORY_SIZE - 1) * self.interval
+            self.pending = {f: r for f, r in self.pending.items() if f >= oldest}
+        self.pending[frame] = report
+
+    def poll(self):
+        """Replay the desync steps of every call run so far (arrivals, send, compare) and return
+        the DesyncDetected events they raise, in call order."""
+        events = []
+        current = self.engine.current_frame()
+        for call in range(self.processed, current):
+            for frame, report in self.arrivals.pop(call, []):          # poll_remote_clients
+                self._on_checksum_report(frame, report)
+            fts = self._send_frame(call)                               # check_checksum_send_interval
+            if fts is not None:
+                self.local_history.append(fts)
+                if len(self.local_history) > MAX_CHECKSUM_HISTORY_SIZE:
+                    oldest = fts - (MAX_CHECKSUM_HISTORY_SIZE - 1) * self.interval
+                    self.local_history = [f for f in self.local_history if f >= oldest]
+            last_confirmed = call - 1 - self.latency                   # compare_local_checksums...
+            checked = []
+            for frame in sorted(self.pending):
+                if frame >= last_confirmed or frame not in self.local_history:
+                    continue
+                report = self.pending[frame]
+                sessions = self.engine.compare_checksums(frame, report)
+                if len(sessions):
+                    local = self.engine.local_checksums(frame)
+                    remote = report.cpu().numpy() if hasattr(report, "cpu") else report
+                    for s in sessions:
+                        events.append(DesyncDetected(frame, int(s), int(local[s]), int(remote[s]),
+                                                     self.addr, call))
+                checked.append(frame)
+            for frame in checked:
+                del self.pending[frame]
+        self.processed = current
+        return events
+
+
+def exchange(a, b):
+    """Deliver each detector's outgoing reports to the other (the two peers of one match)."""
+    for call, frame, report in a.outgoing():
+        b.receive(call, frame, report)
+    for call, frame, report in b.outgoing():
+        a.receive(call, frame, report)

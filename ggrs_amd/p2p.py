@@ -55,6 +55,10 @@ def _bind(L):
     L.ggrs_p2p_read_trace.argtypes = [vp, i32, i32, vp]
     L.ggrs_p2p_timing_reset.argtypes = [vp]
     L.ggrs_p2p_timing_read.argtypes = [vp, P(ctypes.c_float), P(i32)]
+    L.ggrs_p2p_set_desync_detection.argtypes = [vp, i32]
+    L.ggrs_p2p_local_checksums.argtypes = [vp, i32, vp, i32]
+    L.ggrs_p2p_compare_checksums.argtypes = [vp, i32, vp, i32, vp, P(i32)]
+    L.ggrs_p2p_debug_desync.argtypes = [vp, i32, i32]
     for name in _lib.EXPORTS:
         if name.startswith("ggrs_p2p_"):
             getattr(L, name).restype = ctypes.c_int
@@ -147,3 +151,39 @@ class P2PEngine:
         ms, n = ctypes.c_float(), ctypes.c_int32()
         _lib.check(self._L.ggrs_p2p_timing_read(self._h, ctypes.byref(ms), ctypes.byref(n)))
         return ms.value, n.value
+
+    # ---- desync detection (include/ggrs_amd.h, ggrs_p2p_*_desync*/checksums)
+    def set_desync_detection(self, interval):
+        """DesyncDetection::On{interval} (0 = Off) for every session; before the first call."""
+        _lib.check(self._L.ggrs_p2p_set_desync_detection(self._h, interval))
+        self.desync_interval = interval
+
+    def local_checksums(self, frame, out=None):
+        """This peer's checksum report of `frame` for every session: numpy [S] u16, or into a
+        device tensor `out` (torch, uint16/int16, S elements)."""
+        if out is not None and hasattr(out, "data_ptr"):
+            _lib.check(self._L.ggrs_p2p_local_checksums(self._h, frame, ctypes.c_void_p(out.data_ptr()), 1))
+            return out
+        a = np.zeros(self.num_sessions, np.uint16)
+        _lib.check(self._L.ggrs_p2p_local_checksums(self._h, frame, _vp(a), 0))
+        return a
+
+    def compare_checksums(self, frame, remote):
+        """Sessions whose local report of `frame` differs from `remote` ([S] u16 numpy, or a device
+        tensor): numpy array of session indices (compared on the device)."""
+        words = np.zeros((self.num_sessions + 63) // 64, np.uint64)
+        n = ctypes.c_int32()
+        if hasattr(remote, "data_ptr"):
+            ptr, dev = ctypes.c_void_p(remote.data_ptr()), 1
+        else:
+            remote = np.ascontiguousarray(remote, np.uint16)
+            ptr, dev = _vp(remote), 0
+        _lib.check(self._L.ggrs_p2p_compare_checksums(self._h, frame, ptr, dev, _vp(words), ctypes.byref(n)))
+        if n.value == 0:
+            return np.zeros(0, np.int64)
+        bits = np.unpackbits(words.view(np.uint8), bitorder="little")[:self.num_sessions]
+        return np.nonzero(bits)[0]
+
+    def debug_desync(self, session, frame):
+        """Test hook: session's AdvanceFrame from `frame` flips a bit, on every (re)simulation."""
+        _lib.check(self._L.ggrs_p2p_debug_desync(self._h, session, frame))

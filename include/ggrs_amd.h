@@ -297,6 +297,29 @@ int ggrs_p2p_read_trace(ggrs_p2p_engine_t* eng, int32_t first_frame, int32_t n, 
 int ggrs_p2p_timing_reset(ggrs_p2p_engine_t* eng);
 int ggrs_p2p_timing_read(ggrs_p2p_engine_t* eng, float* total_ms, int32_t* launches);
 
+/* ---- P2P desync detection (SessionBuilder::with_desync_detection_mode, builder.rs:197-203;
+ * DesyncDetection::On { interval }, src/lib.rs:71-80).  Replaces P2PSession's
+ * check_checksum_send_interval (p2p_session.rs:939-975) for every session at once: at call
+ * frame_to_send + remote_latency + 1 (when last_confirmed_frame and last_saved_frame reach it) the
+ * saved cell's checksum of frame_to_send = interval, 2 interval, ... enters a device-resident
+ * local_checksum_history of MAX_CHECKSUM_HISTORY_SIZE = 32 reports (protocol.rs:27).  The host
+ * exchanges reports between peers (UdpProtocol::send_checksum_report, protocol.rs:692-698) and
+ * compares received ones (compare_local_checksums_against_peers, p2p_session.rs:904-937) with
+ * ggrs_p2p_compare_checksums; ggrs_amd/desync.py holds the pending-report bookkeeping. */
+/* interval 0 = Off.  Part of the session's configuration: only before the first call. */
+int ggrs_p2p_set_desync_detection(ggrs_p2p_engine_t* eng, int32_t interval);
+/* [num_sessions] u16: the local checksum report of `frame` (host or device destination);
+ * GGRS_E_PRECONDITION when `frame` is not a report frame sent so far or left the history */
+int ggrs_p2p_local_checksums(ggrs_p2p_engine_t* eng, int32_t frame, uint16_t* out, int32_t out_on_device);
+/* compare the local report of `frame` with a peer's [num_sessions] report: bit s of mask
+ * (ceil(num_sessions/64) u64, host) set where they differ -- a GgrsEvent::DesyncDetected
+ * (src/lib.rs:158-167) for session s; *n_differ = number of such sessions */
+int ggrs_p2p_compare_checksums(ggrs_p2p_engine_t* eng, int32_t frame, const uint16_t* remote,
+                               int32_t remote_on_device, uint64_t* mask, int32_t* n_differ);
+/* test hook: the AdvanceFrame from `frame` of `session` flips the lowest bit of player 0's x on
+ * every (re)simulation -- a deterministic desync of this peer (session -1: off) */
+int ggrs_p2p_debug_desync(ggrs_p2p_engine_t* eng, int32_t session, int32_t frame);
+
 #ifdef __cplusplus
 }
 #endif

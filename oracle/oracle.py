@@ -116,6 +116,11 @@ def lib():
         L.oracle_p2p_run.argtypes = [P(P2PCfg), ctypes.c_int32, u8p, u16p, i32p, u8p, ctypes.c_int64,
                                      i32p, u8p, i32p, u16p, u8p, P(P2PResult)]
         L.oracle_p2p_run.restype = ctypes.c_int
+        L.oracle_p2p_desync_pair_run.argtypes = [
+            ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, i32p, ctypes.c_int32, ctypes.c_int32,
+            ctypes.c_int32, u8p, ctypes.c_int32, ctypes.c_int32, i32p, u16p, ctypes.c_int32, i32p, i32p,
+            i32p, u16p, u16p, i32p, u16p]
+        L.oracle_p2p_desync_pair_run.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -248,6 +253,34 @@ def p2p_run(inputs, num_players=2, local_mask=0b01, input_delay=0, max_predictio
     out["rc"] = rc
     out["result"] = res
     return out
+
+
+def p2p_desync_pair_run(inputs, num_players=2, max_prediction=8, latency=2, local_masks=(0b01, 0b10),
+                        predictor=0, interval=10, desync_peer=-1, desync_frame=-1, ev_cap=4096):
+    """Both peers of one match with DesyncDetection::On{interval} (oracle_p2p_desync_pair_run):
+    per peer and call the checksum report sent, and the DesyncDetected events raised as
+    (peer, call, frame, local_checksum, remote_checksum), in call order."""
+    inputs = np.ascontiguousarray(inputs, np.uint8).reshape(-1, num_players)
+    frames = inputs.shape[0]
+    masks = np.array(local_masks, np.int32)
+    sent_frame = np.full((2, frames), -1, np.int32)
+    sent_cs = np.zeros((2, frames), np.uint16)
+    ev = {k: np.zeros(ev_cap, t) for k, t in (("peer", np.int32), ("call", np.int32), ("frame", np.int32),
+                                              ("local", np.uint16), ("remote", np.uint16))}
+    n_ev = ctypes.c_int32(0)
+    trace = np.zeros((2, frames), np.uint16)
+    rc = lib().oracle_p2p_desync_pair_run(
+        num_players, max_prediction, latency, _ptr(masks, ctypes.c_int32), predictor, interval, frames,
+        _ptr(inputs, ctypes.c_uint8), desync_peer, desync_frame, _ptr(sent_frame, ctypes.c_int32),
+        _ptr(sent_cs, ctypes.c_uint16), ev_cap, _ptr(ev["peer"], ctypes.c_int32),
+        _ptr(ev["call"], ctypes.c_int32), _ptr(ev["frame"], ctypes.c_int32),
+        _ptr(ev["local"], ctypes.c_uint16), _ptr(ev["remote"], ctypes.c_uint16), ctypes.byref(n_ev),
+        _ptr(trace, ctypes.c_uint16))
+    n = min(n_ev.value, ev_cap)
+    events = [(int(ev["peer"][i]), int(ev["call"][i]), int(ev["frame"][i]), int(ev["local"][i]),
+               int(ev["remote"][i])) for i in range(n)]
+    return dict(rc=rc, sent_frame=sent_frame, sent_cs=sent_cs, events=events, n_events=n_ev.value,
+                cksum_trace=trace)
 
 
 def particles_synctest_run(inputs, num_entities, num_players=2, max_prediction=17,
