@@ -21,7 +21,8 @@ def run_pair(S, frames, D, mp, interval, chunk, desync=None):
     from ggrs_amd import P2PEngine
     from ggrs_amd.desync import DesyncDetector, exchange
     rows = stream(S, frames, 2)
-    engs = [P2PEngine(S, num_players=2, local_players=(k,), max_prediction=mp, remote_latency=D)
+    engs = [P2PEngine(S, num_players=2, local_players=(k,), max_prediction=mp, remote_latency=D,
+                      input_capacity=frames + 16)
             for k in (0, 1)]
     dets = [DesyncDetector(e, interval, addr=1 - k) for k, e in enumerate(engs)]
     if desync is not None:
@@ -78,7 +79,7 @@ def test_reports_equal_oracle_and_no_events_without_desync(oracle):
 
 def test_history_bounds_are_preconditions():
     from ggrs_amd import P2PEngine, PreconditionError
-    e = P2PEngine(8, num_players=2, local_players=(0,), max_prediction=8, remote_latency=2)
+    e = P2PEngine(8, num_players=2, local_players=(0,), max_prediction=8, remote_latency=2, input_capacity=320)
     e.set_desync_detection(5)
     e.add_inputs(0, np.zeros((300, 8, 2), np.uint8))
     e.advance_frames(300)
