@@ -43,6 +43,7 @@ EXPORTS = (
     "ggrs_p2p_read_trace", "ggrs_p2p_timing_reset", "ggrs_p2p_timing_read",
     "ggrs_p2p_set_desync_detection", "ggrs_p2p_local_checksums", "ggrs_p2p_compare_checksums",
     "ggrs_p2p_debug_desync",
+    "ggrs_codec_encode", "ggrs_codec_decode", "ggrs_codec_max_packet_bytes",
 )
 
 
@@ -114,7 +115,7 @@ def lib():
         L.ggrs_set_synctest_path.argtypes = [vp, ctypes.c_int32]
         L.ggrs_timing_read.argtypes = [vp, P(ctypes.c_float), P(ctypes.c_int32)]
         for name in EXPORTS:
-            if name not in ("ggrs_abi_version", "ggrs_last_error"):
+            if name not in ("ggrs_abi_version", "ggrs_last_error", "ggrs_codec_max_packet_bytes"):
                 getattr(L, name).restype = ctypes.c_int
         _lib = L
     return _lib

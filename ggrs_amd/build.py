@@ -12,7 +12,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libggrs_amd.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("engine.hip", "branch.hip", "particles.hip", "p2p.hip")]
+SOURCES = [os.path.join(CSRC, f) for f in ("engine.hip", "branch.hip", "particles.hip", "p2p.hip", "codec.hip")]
 HEADERS = [os.path.join(CSRC, h) for h in ("box_game.h", "glibc_sincosf.h", "common.h", "particles.h")] + [
     os.path.join(ROOT, "include", "ggrs_amd.h")]
 

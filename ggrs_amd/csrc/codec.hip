@@ -1,0 +1,277 @@
+// codec.hip -- GGRS's input wire codec, batched: many packets encoded / decoded per launch, one
+// thread per packet.
+//
+// Reference: src/network/compression.rs (encode :14-24, delta_encode :26-81, decode :83-95,
+// delta_decode :97-182), called by UdpProtocol::send_pending_output (protocol.rs:450-480: the
+// pending inputs against the last acked input) and on_input (:580-642: against the input before
+// the packet's start frame).  Wire format per packet: bincode 1.3 fixint
+// EncodedInputSequence { input_sizes: Option<Vec<i32>>, encoded_bytes: Vec<u8> } where
+// encoded_bytes is bitfield-rle 0.2.1 over the XOR delta of each input against the previous one
+// (the first against the reference).  Run format: LEB128 header h; h odd -> (h >> 2) bytes of
+// 0xFF (h & 2) or 0x00; h even -> (h >> 1) literal bytes follow.  Encoder run choice: maximal runs
+// of 0x00 / 0xFF are compressed, maximal stretches of other bytes literal (oracle/codec.c).
+//
+// The batched form covers what a GGRS peer sends: every input B bytes, the size of the non-empty
+// reference (input_sizes = None).  Decode accepts every packet the reference accepts whose inputs
+// are all B bytes (input_sizes None, or Some with every size B); a packet the reference rejects
+// gets that error code, one it would decode into other sizes gets GGRS_CODEC_UNSUPPORTED.
+//
+// Layouts (device memory, row per packet):
+//   encode in : ref [N][B], pending [N][W][B], count [N] (<= W)
+//   encode out: packet bytes [N][stride], length [N] (GGRS_CODEC_E_CAP if stride is too small)
+//   decode in : ref [N][B], packets [N][stride], length [N]
+//   decode out: inputs [N][W][B], count [N], status [N]
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+
+using namespace ggrs;
+
+namespace {
+
+constexpr int64_t kMaxDecoded = 1 << 24;  // oracle/codec.c CODEC_MAX_DECODED
+
+struct EncodeParams {
+  const uint8_t* ref;
+  const uint8_t* pending;
+  const int32_t* count;
+  uint8_t* out;
+  int32_t* out_len;
+  int64_t N;
+  int32_t B, W, stride;
+};
+
+__device__ inline int varint_len(uint64_t v) {
+  int n = 1;
+  while (v >= 0x80) { v >>= 7; n++; }
+  return n;
+}
+
+// Byte i of the XOR-delta stream of packet p: input k = i / B against input k-1 (or the reference).
+struct DeltaStream {
+  const uint8_t* ref;
+  const uint8_t* in;
+  int32_t B;
+  __device__ inline uint8_t at(int64_t i) const {
+    const int64_t k = i / B, b = i - k * B;
+    const uint8_t base = k == 0 ? ref[b] : in[(k - 1) * B + b];
+    return base ^ in[i];
+  }
+};
+
+// One pass of bitfield-rle over the delta stream: emit == false only measures.
+template <bool kEmit>
+__device__ inline int64_t rle_pass(const DeltaStream& x, int64_t L, uint8_t* out) {
+  int64_t pos = 0, i = 0;
+  auto put_varint = [&](uint64_t v) {
+    do {
+      uint8_t b = v & 0x7f;
+      v >>= 7;
+      if (kEmit) out[pos] = b | (v ? 0x80 : 0);
+      pos++;
+    } while (v);
+  };
+  while (i < L) {
+    const uint8_t c = x.at(i);
+    int64_t j = i + 1;
+    if (c == 0x00 || c == 0xFF) {
+      while (j < L && x.at(j) == c) j++;
+      put_varint(((uint64_t)(j - i) << 2) | (c == 0xFF ? 2u : 0u) | 1u);
+    } else {
+      while (j < L) {
+        const uint8_t d = x.at(j);
+        if (d == 0x00 || d == 0xFF) break;
+        j++;
+      }
+      put_varint((uint64_t)(j - i) << 1);
+      if (kEmit)
+        for (int64_t k = i; k < j; k++) out[pos + (k - i)] = x.at(k);
+      pos += j - i;
+    }
+    i = j;
+  }
+  return pos;
+}
+
+__global__ __launch_bounds__(256) void encode_kernel(EncodeParams p) {
+  const int64_t pk = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (pk >= p.N) return;
+  const int32_t n = p.count[pk];
+  if (n < 0 || n > p.W) {
+    p.out_len[pk] = GGRS_CODEC_E_INVALID;
+    return;
+  }
+  const DeltaStream x{p.ref + pk * p.B, p.pending + pk * (int64_t)p.W * p.B, p.B};
+  const int64_t L = (int64_t)n * p.B;
+  const int64_t rle = rle_pass<false>(x, L, nullptr);
+  const int64_t total = 1 + 8 + rle;
+  if (total > p.stride) {
+    p.out_len[pk] = GGRS_CODEC_E_CAP;
+    return;
+  }
+  uint8_t* o = p.out + pk * (int64_t)p.stride;
+  o[0] = 0;  // input_sizes: None (every input is the reference's size, compression.rs:27-35)
+  for (int b = 0; b < 8; b++) o[1 + b] = (uint8_t)((uint64_t)rle >> (8 * b));
+  rle_pass<true>(x, L, o + 9);
+  p.out_len[pk] = (int32_t)total;
+}
+
+struct DecodeParams {
+  const uint8_t* ref;
+  const uint8_t* packets;
+  const int32_t* len;
+  uint8_t* out;
+  int32_t* count;
+  int32_t* status;
+  int64_t N;
+  int32_t B, W, stride;
+};
+
+__device__ inline bool get_varint(const uint8_t* in, int64_t n, int64_t& pos, uint64_t& v) {
+  uint64_t r = 0;
+  for (int shift = 0; shift < 64; shift += 7) {
+    if (pos >= n) return false;
+    const uint8_t b = in[pos++];
+    r |= (uint64_t)(b & 0x7f) << shift;
+    if (!(b & 0x80)) {
+      v = r;
+      return true;
+    }
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(256) void decode_kernel(DecodeParams p) {
+  const int64_t pk = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (pk >= p.N) return;
+  auto fail = [&](int32_t code) {
+    p.status[pk] = code;
+    p.count[pk] = 0;
+  };
+  const int64_t len = p.len[pk];
+  if (len < 0 || len > p.stride) return fail(GGRS_CODEC_E_INVALID);
+  const uint8_t* d = p.packets + pk * (int64_t)p.stride;
+  const int32_t B = p.B;
+  // bincode::deserialize (compression.rs:88)
+  int64_t pos = 0;
+  if (len < 1 || d[0] > 1) return fail(GGRS_CODEC_E_BINCODE);
+  const uint8_t tag = d[pos++];
+  uint64_t n_sizes = 0;
+  int64_t sizes_at = 0;
+  if (tag == 1) {
+    if (len - pos < 8) return fail(GGRS_CODEC_E_BINCODE);
+    for (int b = 0; b < 8; b++) n_sizes |= (uint64_t)d[pos + b] << (8 * b);
+    pos += 8;
+    if (n_sizes > (uint64_t)(len - pos) / 4) return fail(GGRS_CODEC_E_BINCODE);
+    sizes_at = pos;
+    pos += 4 * (int64_t)n_sizes;
+  }
+  if (len - pos < 8) return fail(GGRS_CODEC_E_BINCODE);
+  uint64_t m = 0;
+  for (int b = 0; b < 8; b++) m |= (uint64_t)d[pos + b] << (8 * b);
+  pos += 8;
+  if (m > (uint64_t)(len - pos)) return fail(GGRS_CODEC_E_BINCODE);
+  const uint8_t* rle = d + pos;
+  // bitfield_rle::decode, measuring pass (:91)
+  int64_t xl = 0;
+  {
+    int64_t q = 0;
+    while (q < (int64_t)m) {
+      uint64_t h;
+      if (!get_varint(rle, (int64_t)m, q, h)) return fail(GGRS_CODEC_E_RLE);
+      const uint64_t rl = (h & 1) ? h >> 2 : h >> 1;
+      if (rl > (uint64_t)kMaxDecoded || (uint64_t)xl + rl > (uint64_t)kMaxDecoded) return fail(GGRS_CODEC_E_RLE);
+      if (!(h & 1)) {
+        if ((uint64_t)((int64_t)m - q) < rl) return fail(GGRS_CODEC_E_RLE);
+        q += (int64_t)rl;
+      }
+      xl += (int64_t)rl;
+    }
+  }
+  // delta_decode size checks (:103-154)
+  int64_t count;
+  bool all_b = true;
+  if (tag == 1) {
+    count = (int64_t)n_sizes;
+    int64_t bs = B, sum = 0;
+    for (int64_t k = 0; k < count; k++) {
+      uint32_t u = 0;
+      for (int b = 0; b < 4; b++) u |= (uint32_t)d[sizes_at + 4 * k + b] << (8 * b);
+      const int64_t sz = (int64_t)(int32_t)((uint32_t)bs + u);  // i32 arithmetic (:118)
+      if (sz < 0) return fail(GGRS_CODEC_E_DELTA);
+      all_b &= sz == B;
+      bs = sz;
+      sum += sz;
+      if (sum > xl) return fail(GGRS_CODEC_E_DELTA);
+    }
+    if (sum != xl) return fail(GGRS_CODEC_E_DELTA);
+  } else {
+    count = xl / B;
+    if (count * B != xl) return fail(GGRS_CODEC_E_DELTA);
+  }
+  if (!all_b) return fail(GGRS_CODEC_UNSUPPORTED);
+  if (count > p.W) return fail(GGRS_CODEC_E_CAP);
+  // second pass: runs -> XOR against the previous decoded input (or the reference)
+  uint8_t* o = p.out + pk * (int64_t)p.W * B;
+  const uint8_t* r = p.ref + pk * B;
+  int64_t q = 0, i = 0;
+  auto emit = [&](uint8_t xb) {
+    const int64_t k = i / B, b = i - k * B;
+    const uint8_t base = k == 0 ? r[b] : o[(k - 1) * B + b];
+    o[i++] = xb ^ base;
+  };
+  while (q < (int64_t)m) {
+    uint64_t h;
+    get_varint(rle, (int64_t)m, q, h);
+    const int64_t rl = (int64_t)((h & 1) ? h >> 2 : h >> 1);
+    if (h & 1) {
+      const uint8_t fill = (h & 2) ? 0xFF : 0x00;
+      for (int64_t k = 0; k < rl; k++) emit(fill);
+    } else {
+      for (int64_t k = 0; k < rl; k++) emit(rle[q + k]);
+      q += rl;
+    }
+  }
+  p.count[pk] = (int32_t)count;
+  p.status[pk] = GGRS_CODEC_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ggrs_codec_encode(const uint8_t* ref, const uint8_t* pending, const int32_t* count, int64_t n_packets,
+                      int32_t input_bytes, int32_t max_inputs, uint8_t* out, int32_t out_stride, int32_t* out_len,
+                      void* stream) {
+  if (n_packets < 0 || input_bytes < 1 || max_inputs < 0 || out_stride < 9)
+    return set_error(GGRS_E_INVALID, "codec: need n_packets >= 0, input_bytes >= 1, max_inputs >= 0, stride >= 9");
+  if (n_packets == 0) return GGRS_OK;
+  if (!ref || !pending || !count || !out || !out_len) return set_error(GGRS_E_INVALID, "null argument");
+  EncodeParams p{ref, pending, count, out, out_len, n_packets, input_bytes, max_inputs, out_stride};
+  encode_kernel<<<grid_of(n_packets, 256), 256, 0, (hipStream_t)stream>>>(p);
+  HIP_TRY(hipGetLastError());
+  return GGRS_OK;
+}
+
+int ggrs_codec_decode(const uint8_t* ref, const uint8_t* packets, const int32_t* packet_len, int64_t n_packets,
+                      int32_t packet_stride, int32_t input_bytes, int32_t max_inputs, uint8_t* out, int32_t* count,
+                      int32_t* status, void* stream) {
+  if (n_packets < 0 || input_bytes < 1 || max_inputs < 0 || packet_stride < 0)
+    return set_error(GGRS_E_INVALID, "codec: need n_packets >= 0, input_bytes >= 1, max_inputs >= 0");
+  if (n_packets == 0) return GGRS_OK;
+  if (!ref || !packets || !packet_len || !out || !count || !status) return set_error(GGRS_E_INVALID, "null argument");
+  DecodeParams p{ref, packets, packet_len, out, count, status, n_packets, input_bytes, max_inputs, packet_stride};
+  decode_kernel<<<grid_of(n_packets, 256), 256, 0, (hipStream_t)stream>>>(p);
+  HIP_TRY(hipGetLastError());
+  return GGRS_OK;
+}
+
+int32_t ggrs_codec_max_packet_bytes(int32_t input_bytes, int32_t max_inputs) {
+  // tag + u64 length + worst-case runs: alternating 1-byte literal / 1-byte compressed runs
+  // (3 bytes per 2 input bytes) plus one varint header per run
+  const int64_t L = (int64_t)input_bytes * max_inputs;
+  const int64_t v = 1 + 8 + L + (L + 1) / 2 + 10;
+  return v > 0x7fffffff ? -1 : (int32_t)v;
+}
+
+}  // extern "C"

@@ -320,6 +320,34 @@ int ggrs_p2p_compare_checksums(ggrs_p2p_engine_t* eng, int32_t frame, const uint
  * every (re)simulation -- a deterministic desync of this peer (session -1: off) */
 int ggrs_p2p_debug_desync(ggrs_p2p_engine_t* eng, int32_t session, int32_t frame);
 
+/* ---- Input wire codec, batched (src/network/compression.rs:14-182; bitfield-rle 0.2.1 runs,
+ * bincode 1.3 fixint framing of EncodedInputSequence).  Replaces compression::encode / decode as
+ * called per endpoint by UdpProtocol::send_pending_output (protocol.rs:450-480) and on_input
+ * (:580-642), for many packets per launch: one packet = a reference input and the pending inputs
+ * encoded against it, every input input_bytes long (what a GGRS peer sends for a fixed-size
+ * Config::Input).  All pointers are DEVICE pointers; `stream` is a hipStream_t (NULL: default).
+ * Per-packet results are written to device memory (asynchronous with the host). */
+#define GGRS_CODEC_OK 0
+#define GGRS_CODEC_E_BINCODE -1   /* bincode::deserialize failed (bad tag, short buffer) */
+#define GGRS_CODEC_E_RLE -2       /* bitfield_rle::decode failed (truncated header or literal) */
+#define GGRS_CODEC_E_DELTA -3     /* delta_decode rejected the sizes (compression.rs:117-154) */
+#define GGRS_CODEC_E_CAP -4       /* encode: out_stride too small; decode: more than max_inputs */
+#define GGRS_CODEC_E_INVALID -5   /* count outside 0..max_inputs, length outside 0..stride */
+#define GGRS_CODEC_UNSUPPORTED -6 /* valid packet whose inputs are not all input_bytes long */
+/* encode: ref [n][input_bytes], pending [n][max_inputs][input_bytes], count [n] ->
+ * out [n][out_stride] packet bytes, out_len [n] = packet length or a GGRS_CODEC_E_* code */
+int ggrs_codec_encode(const uint8_t* ref, const uint8_t* pending, const int32_t* count, int64_t n_packets,
+                      int32_t input_bytes, int32_t max_inputs, uint8_t* out, int32_t out_stride, int32_t* out_len,
+                      void* stream);
+/* decode: ref [n][input_bytes], packets [n][packet_stride] with packet_len [n] bytes ->
+ * out [n][max_inputs][input_bytes], count [n], status [n] (GGRS_CODEC_OK or an error code;
+ * never faults on hostile bytes -- decode_arbitrary_input_never_panics, compression.rs:205-213) */
+int ggrs_codec_decode(const uint8_t* ref, const uint8_t* packets, const int32_t* packet_len, int64_t n_packets,
+                      int32_t packet_stride, int32_t input_bytes, int32_t max_inputs, uint8_t* out, int32_t* count,
+                      int32_t* status, void* stream);
+/* an out_stride that every packet of max_inputs inputs fits */
+int32_t ggrs_codec_max_packet_bytes(int32_t input_bytes, int32_t max_inputs);
+
 #ifdef __cplusplus
 }
 #endif

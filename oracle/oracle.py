@@ -331,3 +331,68 @@ def synctest_bench(threads, frames, warmup=1000, num_players=2, max_prediction=8
     if n < 0:
         raise RuntimeError("oracle bench session failed")
     return int(n), wall.value, ck
+
+
+# ---------------------------------------------------------------- input wire codec (codec.c)
+CODEC_OK, CODEC_E_BINCODE, CODEC_E_RLE, CODEC_E_DELTA, CODEC_E_CAP = 0, -1, -2, -3, -4
+
+
+def _codec_bind(L):
+    if getattr(L, "_codec_bound", False):
+        return
+    i64, i32 = ctypes.c_int64, ctypes.c_int32
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    i32p = ctypes.POINTER(ctypes.c_int32)
+    L.oracle_codec_encode.argtypes = [u8p, i32, u8p, i32p, i32, u8p, i64]
+    L.oracle_codec_encode.restype = i64
+    L.oracle_codec_decode.argtypes = [u8p, i32, u8p, i64, u8p, i64, i32p, i32, i32p]
+    L.oracle_codec_decode.restype = ctypes.c_int
+    L.oracle_rle_encode.argtypes = [u8p, i64, u8p, i64]
+    L.oracle_rle_encode.restype = i64
+    L.oracle_rle_decode.argtypes = [u8p, i64, u8p, i64]
+    L.oracle_rle_decode.restype = i64
+    L._codec_bound = True
+
+
+def _u8(b):
+    a = np.frombuffer(bytes(b), np.uint8) if not isinstance(b, np.ndarray) else np.ascontiguousarray(b, np.uint8)
+    return a if a.size else np.zeros(1, np.uint8)
+
+
+def codec_encode(reference, inputs):
+    """compression::encode(reference, pending inputs) -> packet bytes (src/network/compression.rs:14-24)."""
+    L = lib()
+    _codec_bind(L)
+    ref = _u8(reference)
+    lens = np.array([len(x) for x in inputs] or [0], np.int32)
+    flat = _u8(b"".join(bytes(x) for x in inputs))
+    total = sum(len(x) for x in inputs)
+    cap = 64 + 4 * len(inputs) + 2 * total
+    out = np.zeros(cap, np.uint8)
+    n = L.oracle_codec_encode(_ptr(ref, ctypes.c_uint8), len(reference), _ptr(flat, ctypes.c_uint8),
+                              _ptr(lens, ctypes.c_int32), len(inputs), _ptr(out, ctypes.c_uint8), cap)
+    if n < 0:
+        raise RuntimeError(f"codec_encode: {n}")
+    return out[:n].tobytes()
+
+
+def codec_decode(reference, data, max_inputs=1 << 16):
+    """compression::decode -> (0, [input bytes]) or (negative CODEC_E_*, None)."""
+    L = lib()
+    _codec_bind(L)
+    ref = _u8(reference)
+    d = _u8(data)
+    cap = 1 << 24
+    out = np.zeros(cap, np.uint8)
+    lens = np.zeros(max_inputs, np.int32)
+    n = ctypes.c_int32()
+    rc = L.oracle_codec_decode(_ptr(ref, ctypes.c_uint8), len(reference), _ptr(d, ctypes.c_uint8), len(data),
+                               _ptr(out, ctypes.c_uint8), cap, _ptr(lens, ctypes.c_int32), max_inputs,
+                               ctypes.byref(n))
+    if rc != 0:
+        return rc, None
+    res, p = [], 0
+    for k in range(n.value):
+        res.append(out[p:p + lens[k]].tobytes())
+        p += lens[k]
+    return 0, res

@@ -1,0 +1,99 @@
+"""GPU parity of the batched input wire codec (ggrs_codec_encode / ggrs_codec_decode) against the
+CPU restatement of src/network/compression.rs (oracle/codec.c): encoded packets byte-identical,
+decode results and error codes identical, on random packets, ex_game-like input windows, the
+reference's own test vector (compression.rs:216-231) and hostile bytes (:205-213)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")  # loads torch's HIP runtime before the engine library
+
+pytestmark = pytest.mark.gpu
+
+
+def batch(rng, N, W, B, held=False):
+    ref = rng.integers(0, 256, (N, B), dtype=np.uint8)
+    if held:  # ex_game-like: keys held over frames -> long zero runs in the XOR delta
+        pend = np.repeat(rng.integers(0, 16, (N, 1, B), dtype=np.uint8), W, axis=1)
+        flip = rng.random((N, W, B)) < 0.15
+        pend = np.where(flip, rng.integers(0, 16, (N, W, B), dtype=np.uint8), pend).astype(np.uint8)
+    else:
+        pend = rng.integers(0, 256, (N, W, B), dtype=np.uint8)
+        pend[rng.random((N, W, B)) < 0.3] = 0
+        pend[rng.random((N, W, B)) < 0.1] = 255
+    count = rng.integers(0, W + 1, N).astype(np.int32)
+    return ref, pend, count
+
+
+def gpu(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+@pytest.mark.parametrize("N,W,B,held", [(5000, 8, 1, True), (3000, 16, 2, False), (2000, 33, 4, False),
+                                         (1000, 128, 1, True), (257, 1, 7, False)])
+def test_encode_matches_oracle_and_round_trips(oracle, N, W, B, held):
+    from ggrs_amd import codec
+    rng = np.random.default_rng(N + W + B)
+    ref, pend, count = batch(rng, N, W, B, held)
+    out, ln = codec.encode(gpu(ref), gpu(pend), gpu(count))
+    out, ln = out.cpu().numpy(), ln.cpu().numpy()
+    for p in range(N):
+        want = oracle.codec_encode(ref[p].tobytes(), [pend[p, k].tobytes() for k in range(count[p])])
+        assert ln[p] == len(want), p
+        assert out[p, :ln[p]].tobytes() == want, p
+    dec, cnt, st = codec.decode(gpu(ref), gpu(out), gpu(ln), max_inputs=W)
+    dec, cnt, st = dec.cpu().numpy(), cnt.cpu().numpy(), st.cpu().numpy()
+    assert (st == 0).all() and (cnt == count).all()
+    for p in range(N):
+        assert (dec[p, :count[p]] == pend[p, :count[p]]).all(), p
+
+
+def test_reference_vector():
+    from ggrs_amd import codec
+    ref = np.array([[0, 0, 0, 1]], np.uint8)
+    pend = np.array([[[0, 0, 1, 0], [0, 0, 1, 1], [0, 1, 0, 0], [0, 1, 0, 1], [0, 1, 1, 0]]], np.uint8)
+    out, ln = codec.encode(gpu(ref), gpu(pend), gpu(np.array([5], np.int32)))
+    dec, cnt, st = codec.decode(gpu(ref), out, ln, max_inputs=5)
+    assert int(st[0]) == 0 and int(cnt[0]) == 5
+    assert (dec.cpu().numpy() == pend).all()
+
+
+@pytest.mark.parametrize("mode", ["mutated", "random", "truncated"])
+def test_hostile_packets_match_oracle(oracle, mode):
+    """Every packet the reference rejects is rejected with the same error class; every packet it
+    accepts decodes identically (or is UNSUPPORTED when its inputs are not all B bytes)."""
+    from ggrs_amd import codec
+    rng = np.random.default_rng({"mutated": 1, "random": 2, "truncated": 3}[mode])
+    N, W, B = 4000, 16, 2
+    ref, pend, count = batch(rng, N, W, B)
+    out, ln = codec.encode(gpu(ref), gpu(pend), gpu(count))
+    pk, ln = out.cpu().numpy().copy(), ln.cpu().numpy().copy()
+    if mode == "mutated":
+        for p in range(N):
+            for _ in range(int(rng.integers(1, 4))):
+                pk[p, int(rng.integers(0, max(ln[p], 1)))] = rng.integers(0, 256)
+    elif mode == "random":
+        pk[:] = rng.integers(0, 256, pk.shape, dtype=np.uint8)
+        ln = rng.integers(0, pk.shape[1] + 1, N).astype(np.int32)
+        framed = (rng.random(N) < 0.7) & (ln >= 9)  # valid bincode framing, random runs inside
+        pk[framed, 0] = 0
+        for p in np.nonzero(framed)[0]:
+            pk[p, 1:9] = np.frombuffer(int(ln[p] - 9).to_bytes(8, "little"), np.uint8)
+    else:  # cut packets short and shrink the bincode length to match: runs end mid-way
+        ln = (ln * rng.random(N)).astype(np.int32)
+        for p in np.nonzero(ln >= 9)[0]:
+            pk[p, 1:9] = np.frombuffer(int(ln[p] - 9).to_bytes(8, "little"), np.uint8)
+    dec, cnt, st = codec.decode(gpu(ref), gpu(pk), gpu(ln), max_inputs=W)
+    dec, cnt, st = dec.cpu().numpy(), cnt.cpu().numpy(), st.cpu().numpy()
+    seen = set()
+    for p in range(N):
+        rc, want = oracle.codec_decode(ref[p].tobytes(), pk[p, :ln[p]].tobytes())
+        seen.add(rc)
+        if rc < 0:
+            assert st[p] == rc, (p, st[p], rc)
+        elif st[p] == 0:
+            assert [dec[p, k].tobytes() for k in range(cnt[p])] == want, p
+        else:
+            assert st[p] in (codec.UNSUPPORTED, codec.E_CAP), (p, st[p])
+            assert st[p] != codec.UNSUPPORTED or any(len(x) != B for x in want)
+            assert st[p] != codec.E_CAP or len(want) > W
+    assert len(seen) >= 2
