@@ -332,6 +332,112 @@ def run_p2p(args):
         dist.destroy_process_group()
 
 
+def run_codec(args):
+    """Input wire codec, batched (ggrs_codec_*; src/network/compression.rs): one step = encode and
+    decode N packets, each a reference input plus W pending inputs of B bytes (config 4 flavour:
+    per GPU 1,048,576 endpoint packets of the 8-frame prediction window, 2 local players x 1 byte,
+    held-key inputs).  Metric: packets round-tripped per second."""
+    world, rank, local_rank, torch, dist = setup_dist(args)
+    import numpy as np
+    from ggrs_amd import codec
+    N, W, B = args.sessions or 1 << 20, 8, 2
+    rng = np.random.default_rng(1234 + rank)
+    ref = rng.integers(0, 16, (N, B), dtype=np.uint8)
+    held = np.repeat(ref[:, None, :], W, axis=1)
+    flip = rng.random((N, W, B)) < 1.0 / 8.0  # a new key 1 frame in 8 (SURVEY.md 8d input model)
+    pend = np.where(flip, rng.integers(0, 16, (N, W, B), dtype=np.uint8), held).astype(np.uint8)
+    count = np.full(N, W, np.int32)
+    dev = torch.device("cuda", local_rank)
+    d_ref, d_pend, d_cnt = (torch.from_numpy(x).to(dev) for x in (ref, pend, count))
+    stride = codec.max_packet_bytes(B, W)
+    evs = []
+
+    def step(timed):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if timed else None
+        if timed:
+            e[0].record()
+        out, ln = codec.encode(d_ref, d_pend, d_cnt, stride)
+        if timed:
+            e[1].record()
+        dec, cnt, st = codec.decode(d_ref, out, ln, W)
+        if timed:
+            e[2].record()
+            evs.append(e)
+        return out, ln, dec, cnt, st
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step(True)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs)
+    dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / len(evs)
+    out, ln, dec, cnt, st = res
+    ln_h = ln.cpu().numpy()
+    pkt_bytes = int(ln_h.sum())
+    ok = bool((st == 0).all().item()) and bool((cnt == d_cnt).all().item()) and bool((dec == d_pend).all().item())
+    value = N * args.steps * world / elapsed
+    # algorithmic HBM bytes: encode reads ref + pending + count, writes packets + lengths; decode
+    # reads ref + packets + lengths, writes inputs + count + status
+    enc_bytes = N * (B + W * B + 4) + pkt_bytes + 4 * N
+    dec_bytes = N * (B + 4) + pkt_bytes + N * (W * B + 8)
+    dom = "decode" if dec_ms >= enc_ms else "encode"
+    dom_bytes, dom_ms = (dec_bytes, dec_ms) if dom == "decode" else (enc_bytes, enc_ms)
+    achieved = dom_bytes / (dom_ms / 1e3) / 1e9
+    parity = cpu_baseline = None
+    if rank == 0:
+        try:
+            from oracle import oracle as O
+            O.build()
+            out_h = out.cpu().numpy()
+            same = all(out_h[p, :ln_h[p]].tobytes() ==
+                       O.codec_encode(ref[p].tobytes(), [pend[p, k].tobytes() for k in range(W)])
+                       for p in (0, 1, N // 2, N - 1))
+            parity = {"round_trip_all_packets": ok, "packets_0_1_mid_last_bytes_equal_oracle": bool(same)}
+            if world == 1 and not args.no_cpu_baseline:
+                sample = min(N, 1 << 18)
+                n1, w1 = O.codec_bench(ref[:sample], pend[:sample], count[:sample], 1)
+                passes = max(1, int(10.0 / max(w1, 1e-3)))
+                n, wall = O.codec_bench(ref[:sample], pend[:sample], count[:sample], passes)
+                cpu_baseline = {"value": round(n / wall, 1), "unit": "packets/s", "cores": 1, "kind": "port",
+                                "sample": f"{passes} passes x {sample} packets (W {W}, B {B}), encode + decode "
+                                          f"one packet at a time (oracle/codec.c)",
+                                "wall_s": round(wall, 3), "cpu": cpu_model()}
+        except Exception as exc:
+            parity = {"error": repr(exc)}
+        line = {
+            "metric": "input packets encoded+decoded/sec (node)", "value": round(value, 1), "unit": "packets/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "config": {"workload": f"codec: {N} endpoint packets per GPU, {W} pending inputs x {B} bytes, "
+                                   f"held-key inputs; encode + decode per step",
+                       "packets_per_gpu": N, "pending": W, "input_bytes": B,
+                       "mean_packet_bytes": round(pkt_bytes / N, 2),
+                       "parallelism": f"packets sharded over {world} GPU(s)"},
+            "kernel_ms": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4)},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                         "traffic": pmc_traffic(f"codec_{dom}_n{N}"),
+                         "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": round(dom_ms, 4)},
+            "cpu_baseline": cpu_baseline, "parity": parity,
+        }
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def p2p_cpu_baseline(args, O, synth, P, D, maxp):
     """The oracle's P2P session (C restatement of p2p_session.rs:265-426 + ex_game) on T host
     threads, one session per thread (ctypes drops the GIL for the call)."""
@@ -378,11 +484,13 @@ def main():
     ap.add_argument("--peers", action="store_true",
                     help="configs 3/4: rank r and r + world/2 replay the same sessions (the two "
                          "machines of a match) and compare checksums after each all-gather")
-    ap.add_argument("--workload", choices=["synctest", "p2p"], default="synctest",
+    ap.add_argument("--workload", choices=["synctest", "p2p", "codec"], default="synctest",
                     help="p2p: the device P2P rollback decision (SURVEY.md 8f), --sessions per GPU")
     args = ap.parse_args()
     if args.workload == "p2p":
         return run_p2p(args)
+    if args.workload == "codec":
+        return run_codec(args)
     if args.config == 5:
         return run_particles(args)
     if args.config != 2:

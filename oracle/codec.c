@@ -196,3 +196,35 @@ int oracle_codec_decode(const uint8_t* ref, int32_t ref_len, const uint8_t* data
   free(x);
   return CODEC_OK;
 }
+
+/* CPU baseline of the batched codec (bench.py --workload codec): encode then decode every packet
+ * (one thread, the reference's per-endpoint call pattern), `passes` times.  Returns packets
+ * round-tripped; *wall = seconds; -1 on a round-trip mismatch. */
+#include <time.h>
+int64_t oracle_codec_bench(const uint8_t* ref, const uint8_t* pending, const int32_t* count, int64_t n_packets,
+                           int32_t B, int32_t W, int32_t passes, double* wall) {
+  const int64_t cap = 64 + 4 * (int64_t)W + 2 * (int64_t)W * B;
+  uint8_t* pkt = (uint8_t*)malloc((size_t)cap);
+  uint8_t* dec = (uint8_t*)malloc((size_t)W * B + 1);
+  int32_t* lens = (int32_t*)malloc(sizeof(int32_t) * ((size_t)W + 1));
+  for (int32_t k = 0; k <= W; k++) lens[k] = B;
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  int64_t done = 0;
+  for (int32_t it = 0; it < passes; it++)
+    for (int64_t p = 0; p < n_packets; p++) {
+      const int64_t n = oracle_codec_encode(ref + p * B, B, pending + p * (int64_t)W * B, lens, count[p], pkt, cap);
+      int32_t got = 0;
+      int32_t dl[256];
+      if (n < 0 || oracle_codec_decode(ref + p * B, B, pkt, n, dec, (int64_t)W * B + 1, dl, 256, &got) != 0 ||
+          got != count[p]) {
+        free(pkt); free(dec); free(lens);
+        return -1;
+      }
+      done++;
+    }
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  *wall = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+  free(pkt); free(dec); free(lens);
+  return done;
+}
