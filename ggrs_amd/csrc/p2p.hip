@@ -64,6 +64,10 @@ struct P2PParams {
   // debug: the advance FROM dbg_frame of session dbg_sess flips x0's lowest bit (every replay)
   int64_t dbg_sess;
   int32_t dbg_frame;
+  // sparse saving (builder.rs:160-169): saves only at min_confirmed, rollbacks from the last save
+  int32_t sparse;
+  int32_t* last_saved;  // [S] SyncLayer::last_saved_frame (sparse mode)
+  int32_t* ring_frame;  // [R][S] frame each cell holds (sparse mode: saves vary per session)
 };
 
 constexpr int kHist = 32;  // MAX_CHECKSUM_HISTORY_SIZE (protocol.rs:27)
@@ -144,6 +148,12 @@ __global__ __launch_bounds__(256) void p2p_kernel(P2PParams p) {
   int32_t rollbacks = 0;
   int64_t resim = 0;
   const bool dbg = sess == p.dbg_sess;
+  int32_t last_saved = p.sparse ? p.last_saved[sess] : kNull;
+  auto save = [&](int32_t h) {
+    save_cell<P>(p, st, h, sess);
+    last_saved = h;
+    if (p.sparse) p.ring_frame[(int64_t)(h % p.R) * S + sess] = h;  // GameStateCell.frame
+  };
   auto advance = [&](uint32_t in) {
     const uint32_t from = st.w[0];
     advance_state<P>(st, in, 0u);
@@ -176,30 +186,40 @@ __global__ __launch_bounds__(256) void p2p_kernel(P2PParams p) {
       }
     }
     // 2. the first frame's save
-    if (f == 0) save_cell<P>(p, st, 0, sess);
-    // 3. check_simulation_consistency + adjust_gamestate
-    int32_t first_inc = kNull;
-#pragma unroll
-    for (int k = 0; k < P; k++)
-      if (q.first_inc[k] != kNull && (first_inc == kNull || q.first_inc[k] < first_inc)) first_inc = q.first_inc[k];
-    if (first_inc != kNull) {
-      load_state<P>(st, p.ring + (int64_t)(first_inc % p.R) * state_fields(P) * S + sess, S);
+    if (f == 0) save(0);
+    // confirmed_frame (:542-553): remote players have sent through f - D, local ones through
+    // f - 1 + delay, so the minimum is f - D (NULL before the first remote input)
+    const int32_t confirmed = f >= p.D ? f - p.D : kNull;
+    // 3. check_simulation_consistency + adjust_gamestate (:658-714)
+    auto adjust = [&](int32_t first_incorrect) {
+      const int32_t load = p.sparse ? last_saved : first_incorrect;  // sparse: the last save
+      load_state<P>(st, p.ring + (int64_t)(load % p.R) * state_fields(P) * S + sess, S);
 #pragma unroll
       for (int k = 0; k < P; k++) {  // reset_prediction (input_queue.rs:63-67)
         q.pred_frame[k] = kNull;
         q.first_inc[k] = kNull;
         q.last_req[k] = kNull;
       }
-      for (int32_t h = first_inc; h < f; ++h) {
+      for (int32_t h = load; h < f; ++h) {
         const uint32_t in = sync_inputs<P>(p, q, h, last_added, sess);
-        if (h > first_inc) save_cell<P>(p, st, h, sess);
+        if (p.sparse ? h == confirmed : h > load) save(h);
         advance(in);
       }
       rollbacks += 1;
-      resim += f - first_inc;
+      resim += f - load;
+    };
+    int32_t first_inc = kNull;
+#pragma unroll
+    for (int k = 0; k < P; k++)
+      if (q.first_inc[k] != kNull && (first_inc == kNull || q.first_inc[k] < first_inc)) first_inc = q.first_inc[k];
+    if (first_inc != kNull) adjust(first_inc);
+    // 4. save the current frame (sparse: check_last_saved_state, :819-843); 5. advance
+    if (!p.sparse) {
+      save(f);
+    } else if (f - last_saved >= p.R - 1) {  // would leave the prediction window
+      if (confirmed >= f) save(f);
+      else adjust(last_saved);
     }
-    // 4. save the current frame; 5. advance with synchronized inputs
-    save_cell<P>(p, st, f, sess);
     const uint32_t in = sync_inputs<P>(p, q, f, last_added, sess);
     advance(in);
     if (p.trace) p.trace[(int64_t)(f % p.trace_cap) * S + sess] = fletcher16_state<P>(st);
@@ -214,6 +234,7 @@ __global__ __launch_bounds__(256) void p2p_kernel(P2PParams p) {
   }
   p.rollbacks[sess] += rollbacks;
   p.resim[sess] += resim;
+  if (p.sparse) p.last_saved[sess] = last_saved;
 }
 
 // compare_local_checksums_against_peers for one report frame, every session at once: bit s of
@@ -262,6 +283,9 @@ struct ggrs_p2p_engine {
   int32_t* cmp_count = nullptr;
   int64_t dbg_sess = -1;
   int32_t dbg_frame = -1;
+  int32_t sparse = 0;
+  int32_t* last_saved = nullptr;  // [S], sparse saving only
+  int32_t* ring_frame = nullptr;  // [R][S], sparse saving only
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<hipEvent_t> tev;
   size_t tev_used = 0;
@@ -291,9 +315,11 @@ int p2p_launch_timed(ggrs_p2p_engine* e, K&& launch) {
 }
 
 // oldest input row a call at frame f still reads: user input (f - D) - delay of the local
-// players' replay, and the remote input f - D
+// players' replay, and the remote input f - D; with sparse saving a replay starts at the last
+// save, up to max_prediction frames back
 int32_t oldest_row(const ggrs_p2p_engine* e, int32_t f) {
-  return std::max(0, f - e->cfg.remote_latency - e->cfg.input_delay);
+  const int32_t back = e->sparse ? e->cfg.max_prediction : e->cfg.remote_latency;
+  return std::max(0, f - back - e->cfg.input_delay);
 }
 
 }  // namespace
@@ -305,7 +331,7 @@ int ggrs_p2p_engine_destroy(ggrs_p2p_engine_t* e) {
   (void)hipSetDevice(e->cfg.device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   void* bufs[] = {e->cur, e->ring, e->ring_ck, e->inputs, e->queue, e->rollbacks, e->resim, e->trace, e->staging,
-                  e->hist, e->cmp_mask, e->cmp_count};
+                  e->hist, e->cmp_mask, e->cmp_count, e->last_saved, e->ring_frame};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (hipEvent_t ev : e->tev) (void)hipEventDestroy(ev);
@@ -451,6 +477,9 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
   p.hist = e->hist;
   p.dbg_sess = e->dbg_sess;
   p.dbg_frame = e->dbg_frame;
+  p.sparse = e->sparse;
+  p.last_saved = e->last_saved;
+  p.ring_frame = e->ring_frame;
   // rows the calls read must still be in the ring: rows >= oldest_row(f0) up to f0 + n - 1
   if ((int64_t)p.f0 + n - 1 - oldest_row(e, p.f0) >= e->cap)
     return set_error(GGRS_E_INVALID, "advance of %d frames reads more input rows than input_capacity (%d)", n, e->cap);
@@ -479,6 +508,22 @@ int ggrs_p2p_set_desync_detection(ggrs_p2p_engine_t* e, int32_t interval) {
     HIP_TRY(hipMalloc(&e->cmp_count, sizeof(int32_t)));
   }
   e->desync_interval = interval;
+  return GGRS_OK;
+}
+
+int ggrs_p2p_set_sparse_saving(ggrs_p2p_engine_t* e, int32_t on) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  if (e->current_frame != 0)
+    return set_error(GGRS_E_STATE, "sparse saving is part of the session's configuration (set before the first frame)");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const int64_t S = e->cfg.num_sessions;
+  if (on && !e->last_saved) {
+    HIP_TRY(hipMalloc(&e->last_saved, sizeof(int32_t) * S));
+    HIP_TRY(hipMemsetAsync(e->last_saved, 0xff, sizeof(int32_t) * S, e->stream));  // NULL_FRAME
+    HIP_TRY(hipMalloc(&e->ring_frame, sizeof(int32_t) * e->R * S));
+    HIP_TRY(hipMemsetAsync(e->ring_frame, 0xff, sizeof(int32_t) * e->R * S, e->stream));
+  }
+  e->sparse = on ? 1 : 0;
   return GGRS_OK;
 }
 
@@ -582,10 +627,15 @@ int ggrs_p2p_read_ring(ggrs_p2p_engine_t* e, int32_t session, int32_t* frames, u
   const int32_t R = e->R, f = e->current_frame;
   const size_t sb = 36 + 20 * (size_t)e->cfg.num_players;
   for (int32_t slot = 0; slot < R; slot++) {
-    // after call f-1 the cells hold frames f-R .. f-1 (every call saves its current frame)
+    // after call f-1 the cells hold frames f-R .. f-1 (every call saves its current frame);
+    // with sparse saving the per-session tags say
     int32_t fr = kNull;
-    for (int32_t g = f - 1; g >= 0 && g >= f - R; g--)
-      if (g % R == slot) { fr = g; break; }
+    if (e->sparse) {
+      HIP_TRY(hipMemcpy(&fr, e->ring_frame + (int64_t)slot * S + session, 4, hipMemcpyDeviceToHost));
+    } else {
+      for (int32_t g = f - 1; g >= 0 && g >= f - R; g--)
+        if (g % R == slot) { fr = g; break; }
+    }
     if (frames) frames[slot] = fr;
     if (checksums) {
       checksums[slot] = 0;

@@ -59,6 +59,7 @@ def _bind(L):
     L.ggrs_p2p_local_checksums.argtypes = [vp, i32, vp, i32]
     L.ggrs_p2p_compare_checksums.argtypes = [vp, i32, vp, i32, vp, P(i32)]
     L.ggrs_p2p_debug_desync.argtypes = [vp, i32, i32]
+    L.ggrs_p2p_set_sparse_saving.argtypes = [vp, i32]
     for name in _lib.EXPORTS:
         if name.startswith("ggrs_p2p_"):
             getattr(L, name).restype = ctypes.c_int
@@ -187,3 +188,8 @@ class P2PEngine:
     def debug_desync(self, session, frame):
         """Test hook: session's AdvanceFrame from `frame` flips a bit, on every (re)simulation."""
         _lib.check(self._L.ggrs_p2p_debug_desync(self._h, session, frame))
+
+    def set_sparse_saving(self, on=True):
+        """SessionBuilder::with_sparse_saving_mode for every session; before the first call."""
+        _lib.check(self._L.ggrs_p2p_set_sparse_saving(self._h, int(bool(on))))
+        self.sparse_saving = bool(on)

@@ -316,6 +316,12 @@ int ggrs_p2p_local_checksums(ggrs_p2p_engine_t* eng, int32_t frame, uint16_t* ou
  * (src/lib.rs:158-167) for session s; *n_differ = number of such sessions */
 int ggrs_p2p_compare_checksums(ggrs_p2p_engine_t* eng, int32_t frame, const uint16_t* remote,
                                int32_t remote_on_device, uint64_t* mask, int32_t* n_differ);
+/* Sparse saving (SessionBuilder::with_sparse_saving_mode, builder.rs:160-169): rollbacks load the
+ * last saved state and save only min_confirmed (adjust_gamestate, p2p_session.rs:666-702), the
+ * current frame is saved only when the last save would leave the prediction window
+ * (check_last_saved_state :819-843), last_confirmed_frame never passes the last save
+ * (sync_layer.rs:323-326).  Part of the configuration: only before the first call. */
+int ggrs_p2p_set_sparse_saving(ggrs_p2p_engine_t* eng, int32_t on);
 /* test hook: the AdvanceFrame from `frame` of `session` flips the lowest bit of player 0's x on
  * every (re)simulation -- a deterministic desync of this peer (session -1: off) */
 int ggrs_p2p_debug_desync(ggrs_p2p_engine_t* eng, int32_t session, int32_t frame);

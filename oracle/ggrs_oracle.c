@@ -976,6 +976,7 @@ typedef struct {
   PlayerInput local[MAX_PLAYERS];
   int has_local[MAX_PLAYERS];
   int64_t rollbacks, resim;
+  int sparse_saving;         /* SessionBuilder::with_sparse_saving_mode (builder.rs:160-169) */
   Desync* ds;                /* desync detection, NULL = Off */
   int sent;                  /* this call's checksum report (frame, checksum), if sent */
   int32_t sent_frame;
@@ -1002,10 +1003,12 @@ static int32_t sl_check_simulation_consistency(const SyncLayer* sl, int32_t firs
   return first_incorrect;
 }
 
-/* adjust_gamestate (:658-714), non-sparse */
-static void p2p_adjust_gamestate(P2PSession* s, int32_t first_incorrect, RequestVec* rv) {
+/* adjust_gamestate (:658-714) */
+static void p2p_adjust_gamestate(P2PSession* s, int32_t first_incorrect, int32_t min_confirmed, RequestVec* rv) {
   int32_t current = s->sl.current_frame;
-  int32_t frame_to_load = first_incorrect;
+  /* sparse saving rolls back to the last saved state (:666-673) */
+  int32_t frame_to_load = s->sparse_saving ? s->sl.last_saved_frame : first_incorrect;
+  ORACLE_ASSERT(frame_to_load <= first_incorrect, "load frame after the first incorrect frame");
   int32_t count = current - frame_to_load;
   rv_push(rv, sl_load_frame(&s->sl, frame_to_load));
   ORACLE_ASSERT(s->sl.current_frame == frame_to_load, "load did not move the cursor");
@@ -1013,7 +1016,11 @@ static void p2p_adjust_gamestate(P2PSession* s, int32_t first_incorrect, Request
   for (int32_t i = 0; i < count; i++) {
     Request adv; memset(&adv, 0, sizeof adv); adv.kind = REQ_ADVANCE;
     sl_synchronized_inputs(&s->sl, s->disconnected, s->last_frame, &adv);
-    if (i > 0) rv_push(rv, sl_save_current_state(&s->sl));
+    if (s->sparse_saving) {            /* only the min_confirmed frame (:692-697) */
+      if (s->sl.current_frame == min_confirmed) rv_push(rv, sl_save_current_state(&s->sl));
+    } else if (i > 0) {                /* every state but the one just loaded (:698-702) */
+      rv_push(rv, sl_save_current_state(&s->sl));
+    }
     s->sl.current_frame += 1;
     rv_push(rv, adv);
   }
@@ -1048,11 +1055,23 @@ static int p2p_advance_frame(P2PSession* s, RequestVec* rv, int* advanced) {
   int32_t confirmed = p2p_confirmed_frame(s);                                /* :314 */
   int32_t first_incorrect = sl_check_simulation_consistency(&s->sl, s->disconnect_frame);
   if (first_incorrect != NULL_FRAME) {
-    p2p_adjust_gamestate(s, first_incorrect, rv);
+    p2p_adjust_gamestate(s, first_incorrect, confirmed, rv);
     s->disconnect_frame = NULL_FRAME;
   }
-  rv_push(rv, sl_save_current_state(&s->sl));                                /* :337 */
-  sl_set_last_confirmed_frame(&s->sl, confirmed, 0);                         /* :349-350 */
+  if (s->sparse_saving) {                                                    /* :331-333 */
+    /* check_last_saved_state (:819-843): never lose the last saved frame out of the window */
+    const int32_t last_saved = s->sl.last_saved_frame;
+    if (s->sl.current_frame - last_saved >= (int32_t)s->max_prediction) {
+      if (confirmed >= s->sl.current_frame) rv_push(rv, sl_save_current_state(&s->sl));
+      else p2p_adjust_gamestate(s, last_saved, confirmed, rv);
+      ORACLE_ASSERT(confirmed == NULL_FRAME || s->sl.last_saved_frame ==
+                    (confirmed < s->sl.current_frame ? confirmed : s->sl.current_frame),
+                    "sparse saving lost the confirmed state");
+    }
+  } else {
+    rv_push(rv, sl_save_current_state(&s->sl));                              /* :337 */
+  }
+  sl_set_last_confirmed_frame(&s->sl, confirmed, s->sparse_saving);          /* :349-350 */
   for (size_t h = 0; h < s->num_players; h++) {                              /* :362-377 */
     if (!((s->local_mask >> h) & 1u)) continue;
     int32_t actual = sl_add_local_input(&s->sl, h, s->local[h]);
@@ -1075,6 +1094,7 @@ static int p2p_advance_frame(P2PSession* s, RequestVec* rv, int* advanced) {
 typedef struct {
   int32_t num_players, max_prediction, input_delay, latency;
   int32_t local_mask, predictor;
+  int32_t sparse_saving;
 } OracleP2PCfg;
 
 typedef struct {
@@ -1108,6 +1128,7 @@ int oracle_p2p_run(const OracleP2PCfg* cfg, int32_t frames, const uint8_t* input
     if ((s.local_mask >> i) & 1u) s.sl.queues[i].frame_delay = (size_t)cfg->input_delay; /* :183 */
   }
   s.disconnect_frame = NULL_FRAME;
+  s.sparse_saving = cfg->sparse_saving;
   Game g; memset(&g, 0, sizeof g);
   g.desync_frame = -1;
   state_new(&g.game_state, (uint64_t)P);

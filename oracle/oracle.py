@@ -51,6 +51,7 @@ class P2PCfg(ctypes.Structure):
         ("latency", ctypes.c_int32),
         ("local_mask", ctypes.c_int32),
         ("predictor", ctypes.c_int32),
+        ("sparse_saving", ctypes.c_int32),
     ]
 
 
@@ -231,14 +232,14 @@ def p2p_replay(state, load_frame, inputs, max_prediction=None, status=None):
 
 
 def p2p_run(inputs, num_players=2, local_mask=0b01, input_delay=0, max_prediction=8, latency=4,
-            predictor=0, req_cap=0):
+            predictor=0, req_cap=0, sparse_saving=False):
     """One peer's P2P session over len(inputs) calls (oracle_p2p_run in ggrs_oracle.c):
     inputs[g] = local add_local_input of call g / remote input of frame g."""
     inputs = np.ascontiguousarray(inputs, np.uint8).reshape(-1, num_players)
     frames = inputs.shape[0]
     R = max_prediction + 1
     sb = state_bytes(num_players)
-    cfg = P2PCfg(num_players, max_prediction, input_delay, latency, local_mask, predictor)
+    cfg = P2PCfg(num_players, max_prediction, input_delay, latency, local_mask, predictor, int(sparse_saving))
     res = P2PResult()
     out = dict(ck_trace=np.zeros(frames, np.uint16), rb_frame=np.zeros(frames, np.int32),
                req_trace=np.zeros(max(req_cap, 1), np.uint8), req_len=np.zeros(frames, np.int32),

@@ -22,7 +22,8 @@ def check_against_oracle(eng, rows, sessions, frames):
     for s in sessions:
         out = o.p2p_run(rows[:, s], num_players=eng.num_players, local_mask=eng.local_mask,
                         input_delay=eng.input_delay, max_prediction=eng.max_prediction,
-                        latency=eng.remote_latency, predictor=eng.predictor)
+                        latency=eng.remote_latency, predictor=eng.predictor,
+                        sparse_saving=getattr(eng, "sparse_saving", False))
         assert out["rc"] == 0
         res = out["result"]
         assert (tr[:, s] == out["ck_trace"]).all(), s
@@ -90,3 +91,29 @@ def test_p2p_input_checks(oracle):
     rb, rs = eng.stats()
     assert (rb == 0).all() and (rs == 0).all()
 
+
+
+SPARSE_CASES = [
+    # P, local players, delay, max_prediction, latency, predictor, input model
+    (2, (0,), 0, 8, 4, 0, 1),
+    (2, (1,), 2, 8, 7, 0, 0),
+    (4, (0, 2), 1, 8, 3, 1, 1),
+    (3, (0,), 0, 12, 2, 0, 0),
+]
+
+
+@pytest.mark.parametrize("P,local,delay,mp,D,pred,model", SPARSE_CASES)
+def test_p2p_sparse_saving_matches_oracle(oracle, P, local, delay, mp, D, pred, model):
+    """Sparse saving (builder.rs:160-169): rollbacks from the last save, saves only at
+    min_confirmed or when the last save would leave the window; every session bit-exact with the
+    oracle's P2PSession including which frames the ring cells hold."""
+    from ggrs_amd import P2PEngine
+    S, frames = 300, 200
+    rows = stream(S, frames, P, model)
+    eng = P2PEngine(S, num_players=P, local_players=local, input_delay=delay, max_prediction=mp,
+                    remote_latency=D, predictor=pred, trace_capacity=frames)
+    eng.set_sparse_saving(True)
+    eng.add_inputs(0, rows)
+    for n in (1, 3, 17, 79, 100):
+        eng.advance_frames(n)
+    check_against_oracle(eng, rows, [0, 1, 63, 64, 150, 299], frames)

@@ -121,3 +121,20 @@ def test_invalid_configs(oracle):
     assert o.p2p_run(inp, latency=8, max_prediction=8)["rc"] == -1   # prediction threshold
     assert o.p2p_run(inp, latency=0, max_prediction=8)["rc"] == -1
     assert o.p2p_run(inp, local_mask=0b100)["rc"] == -1
+
+
+@pytest.mark.parametrize("latency,mp,model", [(4, 8, 1), (2, 8, 0), (7, 8, 1), (3, 12, 0)])
+def test_sparse_saving_same_game_fewer_saves(latency, mp, model):
+    """Sparse saving (p2p_session.rs:666-702, :819-843) changes which states are saved and how far
+    rollbacks replay, never the simulated game: identical display checksums and final state, fewer
+    SaveGameState requests, at least as many resimulated frames; the restated assertion that the
+    confirmed state is never lost (:837-842) holds throughout (an oracle assert would abort)."""
+    from oracle import oracle as O
+    inp = O.gen_inputs(O.session_seed(3, 9), 500, 2, model)
+    dense = O.p2p_run(inp, latency=latency, max_prediction=mp, req_cap=1 << 16)
+    sparse = O.p2p_run(inp, latency=latency, max_prediction=mp, req_cap=1 << 16, sparse_saving=True)
+    assert dense["rc"] == 0 and sparse["rc"] == 0
+    assert (dense["ck_trace"] == sparse["ck_trace"]).all()
+    assert bytes(dense["final_state"]) == bytes(sparse["final_state"])
+    assert sparse["result"].n_save < dense["result"].n_save
+    assert sparse["result"].resim >= dense["result"].resim
