@@ -16,6 +16,8 @@ fn main() {
         .arg(csrc.join("engine.hip"))
         .arg(csrc.join("branch.hip"))
         .arg(csrc.join("particles.hip"))
+        .arg(csrc.join("p2p.hip"))
+        .arg(csrc.join("codec.hip"))
         .status()
         .expect("hipcc not found");
     assert!(status.success(), "hipcc failed");

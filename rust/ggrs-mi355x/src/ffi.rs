@@ -53,6 +53,15 @@ extern "C" {
                                 mismatch_mask: *mut u64) -> i32;
     pub fn ggrs_read_save_checksums(eng: *mut ggrs_engine_t, frame: i32, out: *mut u16) -> i32;
     pub fn ggrs_read_state(eng: *mut ggrs_engine_t, lane: i32, out: *mut u8) -> i32;
+
+    // input wire codec, batched (src/network/compression.rs:14-182); device pointers
+    pub fn ggrs_codec_encode(ref_: *const u8, pending: *const u8, count: *const i32, n_packets: i64,
+                             input_bytes: i32, max_inputs: i32, out: *mut u8, out_stride: i32,
+                             out_len: *mut i32, stream: *mut c_void) -> i32;
+    pub fn ggrs_codec_decode(ref_: *const u8, packets: *const u8, packet_len: *const i32, n_packets: i64,
+                             packet_stride: i32, input_bytes: i32, max_inputs: i32, out: *mut u8,
+                             count: *mut i32, status: *mut i32, stream: *mut c_void) -> i32;
+    pub fn ggrs_codec_max_packet_bytes(input_bytes: i32, max_inputs: i32) -> i32;
 }
 
 /// The engine's last error message on this thread.
