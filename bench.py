@@ -124,8 +124,11 @@ def run_branch(args):
         dist.barrier()
     eng.timing_reset()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        round_()
+    if dist is None:
+        eng.rounds(args.steps)  # one GPU: no exchange between rounds, issue them back to back
+    else:
+        for _ in range(args.steps):
+            round_()
     eng.synchronize()
     if dist is not None:
         dist.barrier()

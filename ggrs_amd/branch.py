@@ -52,6 +52,7 @@ def _bind(L):
     L.ggrs_branch_read_lane.argtypes = [vp, ctypes.c_int64, ctypes.c_int32, P(ctypes.c_uint16), vp]
     L.ggrs_branch_timing_reset.argtypes = [vp]
     L.ggrs_branch_timing_read.argtypes = [vp, P(ctypes.c_float), P(ctypes.c_int32)]
+    L.ggrs_branch_rounds.argtypes = [vp, ctypes.c_int32]
     for name in _lib.EXPORTS:
         if name.startswith("ggrs_branch_"):
             getattr(L, name).restype = ctypes.c_int
@@ -106,6 +107,10 @@ class BranchEngine:
     def confirm(self, report_device_ptr=None):
         ptr = ctypes.c_void_p(report_device_ptr) if report_device_ptr else None
         _lib.check(self._L.ggrs_branch_confirm(self._h, ptr))
+
+    def rounds(self, n):
+        """n rounds of speculate + confirm issued back to back from native code (no report copy)."""
+        _lib.check(self._L.ggrs_branch_rounds(self._h, n))
 
     def synchronize(self):
         _lib.check(self._L.ggrs_branch_synchronize(self._h))

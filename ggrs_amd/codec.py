@@ -25,6 +25,7 @@ def _bind(L):
     L.ggrs_codec_decode.argtypes = [vp, vp, vp, i64, i32, i32, i32, vp, vp, vp, vp]
     L.ggrs_codec_max_packet_bytes.argtypes = [i32, i32]
     L.ggrs_codec_max_packet_bytes.restype = i32
+    L.ggrs_codec_set_direct.argtypes = [i32]
     _bound = True
 
 
@@ -78,3 +79,10 @@ def decode(ref, packets, lengths, max_inputs):
     _lib.check(L.ggrs_codec_decode(_p(ref), _p(packets), _p(lengths), N, stride, B, max_inputs, _p(out), _p(cnt),
                                    _p(st), _stream(packets)))
     return out, cnt, st
+
+
+def set_direct(on):
+    """Force the direct (unstaged) kernels; False restores the LDS-staged default."""
+    L = _lib.lib()
+    _bind(L)
+    _lib.check(L.ggrs_codec_set_direct(int(bool(on))))

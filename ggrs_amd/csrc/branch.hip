@@ -155,6 +155,9 @@ struct ggrs_branch_engine {
   uint8_t* report = nullptr;  // report_bytes: [S] u16 | pad to 8 | [words] u64
   size_t report_bytes = 0;
   uint64_t* prev_bits = nullptr;
+  bool batching = false;             // ggrs_branch_rounds: launches without per-launch events
+  int32_t batch_launches = 0;
+  std::vector<int32_t> tev_weight;   // launches each collected event pair brackets
   int32_t* desync = nullptr;
   uint8_t* staging = nullptr;
   size_t staging_bytes = 0;
@@ -174,6 +177,12 @@ int64_t report_words(int64_t L) { return (L + 63) / 64; }
 
 template <typename K>
 int branch_launch_timed(ggrs_branch_engine* e, K&& launch) {
+  if (e->batching) {  // inside ggrs_branch_rounds: one event pair brackets the whole batch
+    launch();
+    HIP_TRY(hipGetLastError());
+    e->batch_launches += 1;
+    return GGRS_OK;
+  }
   hipEvent_t a = e->ev0, b = e->ev1;
   if (e->collecting) {
     while (e->tev.size() < e->tev_used + 2) {
@@ -189,6 +198,7 @@ int branch_launch_timed(ggrs_branch_engine* e, K&& launch) {
   launch();
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(b, e->stream));
+  if (e->collecting) e->tev_weight.push_back(1);
   return GGRS_OK;
 }
 
@@ -347,7 +357,9 @@ int ggrs_branch_speculate(ggrs_branch_engine_t* e) {
   p.ring = e->ring;
   p.ring_ck = e->ring_ck;
   p.inputs = e->inputs;
-  p.prev_survive = e->prev_bits;
+  // the previous confirm's survival bits, read in place from the report (stream order: no
+  // confirm runs between that confirm and this speculate)
+  p.prev_survive = (const uint64_t*)(e->report + report_ck_bytes(p.S));
   p.trunk_ck = (const uint16_t*)e->report;
   p.desync = e->desync;
   return branch_launch_timed(e, [&] {
@@ -385,7 +397,6 @@ int ggrs_branch_confirm(ggrs_branch_engine_t* e, void* report_device) {
     });
   });
   if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(e->prev_bits, p.report_bits, 8 * report_words(p.L), hipMemcpyDeviceToDevice, e->stream));
   if (report_device)
     HIP_TRY(hipMemcpyAsync(report_device, e->report, e->report_bytes, hipMemcpyDeviceToDevice, e->stream));
   e->trunk_frame += 1;
@@ -465,6 +476,7 @@ int ggrs_branch_timing_reset(ggrs_branch_engine_t* e) {
   HIP_TRY(hipSetDevice(e->cfg.device));
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->tev_used = 0;
+  e->tev_weight.clear();
   e->collecting = true;
   return GGRS_OK;
 }
@@ -480,10 +492,47 @@ int ggrs_branch_timing_read(ggrs_branch_engine_t* e, float* total_ms, int32_t* l
     sum += ms;
   }
   *total_ms = sum;
-  *launches = (int32_t)(e->tev_used / 2);
+  int32_t n = 0;
+  for (int32_t w : e->tev_weight) n += w;
+  *launches = n;
   e->collecting = false;
   e->tev_used = 0;
+  e->tev_weight.clear();
   return GGRS_OK;
+}
+
+int ggrs_branch_rounds(ggrs_branch_engine_t* e, int32_t n_rounds) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  if (n_rounds < 0) return set_error(GGRS_E_INVALID, "n_rounds must be >= 0");
+  if ((int64_t)e->trunk_frame + n_rounds - 1 + e->cfg.window - 1 >= e->next_input_frame)
+    return set_error(GGRS_E_INVALID, "inputs for %d rounds are not queued", n_rounds);
+  if (n_rounds == 0) return GGRS_OK;
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  hipEvent_t a = nullptr, b = nullptr;
+  if (e->collecting) {
+    while (e->tev.size() < e->tev_used + 2) {
+      hipEvent_t ev;
+      HIP_TRY(hipEventCreate(&ev));
+      e->tev.push_back(ev);
+    }
+    a = e->tev[e->tev_used];
+    b = e->tev[e->tev_used + 1];
+    e->tev_used += 2;
+    HIP_TRY(hipEventRecord(a, e->stream));
+  }
+  e->batching = true;
+  e->batch_launches = 0;
+  int rc = GGRS_OK;
+  for (int32_t r = 0; r < n_rounds && rc == GGRS_OK; r++) {
+    rc = ggrs_branch_speculate(e);
+    if (rc == GGRS_OK) rc = ggrs_branch_confirm(e, nullptr);
+  }
+  e->batching = false;
+  if (e->collecting) {
+    HIP_TRY(hipEventRecord(b, e->stream));
+    e->tev_weight.push_back(e->batch_launches);
+  }
+  return rc;
 }
 
 }  // extern "C"

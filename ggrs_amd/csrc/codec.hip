@@ -30,6 +30,7 @@ using namespace ggrs;
 namespace {
 
 constexpr int64_t kMaxDecoded = 1 << 24;  // oracle/codec.c CODEC_MAX_DECODED
+bool g_codec_direct = false;  // ggrs_codec_set_direct: force the direct (unstaged) kernels
 
 struct EncodeParams {
   const uint8_t* ref;
@@ -236,6 +237,242 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeParams p) {
   p.status[pk] = GGRS_CODEC_OK;
 }
 
+// ------------------------------------------------------------------------------------------
+// LDS-staged forms (the default when rows are whole dwords): a workgroup's packets are contiguous
+// in memory, so the whole block moves between HBM and LDS with coalesced dword loads and stores,
+// and each thread's byte-serial RLE works out of LDS instead of issuing byte accesses to global
+// memory.  LDS rows are padded to an odd number of dwords so that threads stepping through their
+// own rows in lockstep spread over the banks.
+__host__ __device__ inline int odd_dword_pitch(int bytes) {
+  int dw = (bytes + 3) / 4;
+  if ((dw & 1) == 0) dw += 1;
+  return dw * 4;
+}
+
+// rows x row_bytes contiguous bytes at src (dword aligned, row_bytes % 4 == 0) -> LDS rows of
+// `pitch` bytes, and back.
+__device__ inline void block_to_lds(uint8_t* lds, int pitch, const uint8_t* src, int rows, int row_bytes) {
+  const int dpr = row_bytes / 4, total = rows * dpr;
+  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src);
+  for (int q = threadIdx.x; q < total; q += blockDim.x) {
+    const int r = q / dpr, c = q - r * dpr;
+    reinterpret_cast<uint32_t*>(lds + r * pitch)[c] = s32[q];
+  }
+}
+__device__ inline void lds_to_block(uint8_t* dst, const uint8_t* lds, int pitch, int rows, int row_bytes) {
+  const int dpr = row_bytes / 4, total = rows * dpr;
+  uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
+  for (int q = threadIdx.x; q < total; q += blockDim.x) {
+    const int r = q / dpr, c = q - r * dpr;
+    d32[q] = reinterpret_cast<const uint32_t*>(lds + r * pitch)[c];
+  }
+}
+
+__global__ __launch_bounds__(256) void encode_lds_kernel(EncodeParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int T = blockDim.x, B = p.B, W = p.W, stride = p.stride;
+  const int in_pitch = odd_dword_pitch(W * B), out_pitch = odd_dword_pitch(stride);
+  uint8_t* l_in = smem;                                  // [T][in_pitch]
+  uint8_t* l_out = l_in + T * in_pitch;                  // [T][out_pitch]
+  uint8_t* l_ref = l_out + T * out_pitch;                // [T][B]
+  const int64_t pk0 = (int64_t)blockIdx.x * T;
+  const int np = (int)((p.N - pk0) < T ? (p.N - pk0) : T);
+  block_to_lds(l_in, in_pitch, p.pending + pk0 * W * B, np, W * B);
+  for (int q = threadIdx.x; q < np * B; q += T) l_ref[q] = p.ref[pk0 * B + q];
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < np) {
+    const int32_t n = p.count[pk0 + t];
+    uint8_t* o = l_out + t * out_pitch;
+    const uint8_t* in = l_in + t * in_pitch;
+    const uint8_t* rf = l_ref + t * B;
+    int32_t total = GGRS_CODEC_E_INVALID;
+    if (n >= 0 && n <= W) {
+      const int L = n * B;
+      auto x = [&](int i) -> uint8_t { return (i < B ? rf[i] : in[i - B]) ^ in[i]; };
+      // pass 1: RLE length
+      int rle = 0;
+      for (int i = 0; i < L;) {
+        const uint8_t c = x(i);
+        int j = i + 1;
+        if (c == 0x00 || c == 0xFF) {
+          while (j < L && x(j) == c) j++;
+          rle += varint_len(((uint64_t)(j - i) << 2) | 1u);
+        } else {
+          while (j < L) {
+            const uint8_t d = x(j);
+            if (d == 0x00 || d == 0xFF) break;
+            j++;
+          }
+          rle += varint_len((uint64_t)(j - i) << 1) + (j - i);
+        }
+        i = j;
+      }
+      total = 9 + rle;
+      if (total > stride) {
+        total = GGRS_CODEC_E_CAP;
+      } else {
+        o[0] = 0;
+        for (int b = 0; b < 8; b++) o[1 + b] = (uint8_t)((uint64_t)rle >> (8 * b));
+        int pos = 9;
+        auto put_varint = [&](uint64_t v) {
+          do {
+            const uint8_t b = v & 0x7f;
+            v >>= 7;
+            o[pos++] = b | (v ? 0x80 : 0);
+          } while (v);
+        };
+        for (int i = 0; i < L;) {
+          const uint8_t c = x(i);
+          int j = i + 1;
+          if (c == 0x00 || c == 0xFF) {
+            while (j < L && x(j) == c) j++;
+            put_varint(((uint64_t)(j - i) << 2) | (c == 0xFF ? 2u : 0u) | 1u);
+          } else {
+            while (j < L) {
+              const uint8_t d = x(j);
+              if (d == 0x00 || d == 0xFF) break;
+              j++;
+            }
+            put_varint((uint64_t)(j - i) << 1);
+            for (int k = i; k < j; k++) o[pos++] = x(k);
+          }
+          i = j;
+        }
+        for (; pos < stride; pos++) o[pos] = 0;  // the row is stored whole
+      }
+    }
+    if (total < 0)
+      for (int b = 0; b < stride; b++) o[b] = 0;
+    p.out_len[pk0 + t] = total;
+  }
+  __syncthreads();
+  lds_to_block(p.out + pk0 * stride, l_out, out_pitch, np, stride);
+}
+
+__global__ __launch_bounds__(256) void decode_lds_kernel(DecodeParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int T = blockDim.x, B = p.B, W = p.W, stride = p.stride;
+  const int in_pitch = odd_dword_pitch(stride), out_pitch = odd_dword_pitch(W * B);
+  uint8_t* l_in = smem;                                  // [T][in_pitch] packets
+  uint8_t* l_out = l_in + T * in_pitch;                  // [T][out_pitch] decoded inputs
+  uint8_t* l_ref = l_out + T * out_pitch;                // [T][B]
+  const int64_t pk0 = (int64_t)blockIdx.x * T;
+  const int np = (int)((p.N - pk0) < T ? (p.N - pk0) : T);
+  block_to_lds(l_in, in_pitch, p.packets + pk0 * stride, np, stride);
+  for (int q = threadIdx.x; q < np * B; q += T) l_ref[q] = p.ref[pk0 * B + q];
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < np) {
+    const int64_t pk = pk0 + t;
+    const uint8_t* d = l_in + t * in_pitch;
+    uint8_t* o = l_out + t * out_pitch;
+    const uint8_t* rf = l_ref + t * B;
+    int32_t status = GGRS_CODEC_OK, count = 0;
+    const int64_t len = p.len[pk];
+    // the same checks, in the same order, as decode_kernel (compression.rs:83-182)
+    do {
+      if (len < 0 || len > stride) { status = GGRS_CODEC_E_INVALID; break; }
+      int64_t pos = 0;
+      if (len < 1 || d[0] > 1) { status = GGRS_CODEC_E_BINCODE; break; }
+      const uint8_t tag = d[pos++];
+      uint64_t n_sizes = 0;
+      int64_t sizes_at = 0;
+      if (tag == 1) {
+        if (len - pos < 8) { status = GGRS_CODEC_E_BINCODE; break; }
+        for (int b = 0; b < 8; b++) n_sizes |= (uint64_t)d[pos + b] << (8 * b);
+        pos += 8;
+        if (n_sizes > (uint64_t)(len - pos) / 4) { status = GGRS_CODEC_E_BINCODE; break; }
+        sizes_at = pos;
+        pos += 4 * (int64_t)n_sizes;
+      }
+      if (len - pos < 8) { status = GGRS_CODEC_E_BINCODE; break; }
+      uint64_t m = 0;
+      for (int b = 0; b < 8; b++) m |= (uint64_t)d[pos + b] << (8 * b);
+      pos += 8;
+      if (m > (uint64_t)(len - pos)) { status = GGRS_CODEC_E_BINCODE; break; }
+      const uint8_t* rle = d + pos;
+      int64_t xl = 0;
+      {
+        int64_t q = 0;
+        bool bad = false;
+        while (q < (int64_t)m) {
+          uint64_t h;
+          if (!get_varint(rle, (int64_t)m, q, h)) { bad = true; break; }
+          const uint64_t rl = (h & 1) ? h >> 2 : h >> 1;
+          if (rl > (uint64_t)kMaxDecoded || (uint64_t)xl + rl > (uint64_t)kMaxDecoded) { bad = true; break; }
+          if (!(h & 1)) {
+            if ((uint64_t)((int64_t)m - q) < rl) { bad = true; break; }
+            q += (int64_t)rl;
+          }
+          xl += (int64_t)rl;
+        }
+        if (bad) { status = GGRS_CODEC_E_RLE; break; }
+      }
+      int64_t cnt;
+      bool all_b = true;
+      if (tag == 1) {
+        cnt = (int64_t)n_sizes;
+        int64_t bs = B, sum = 0;
+        bool bad = false;
+        for (int64_t k = 0; k < cnt; k++) {
+          uint32_t u = 0;
+          for (int b = 0; b < 4; b++) u |= (uint32_t)d[sizes_at + 4 * k + b] << (8 * b);
+          const int64_t sz = (int64_t)(int32_t)((uint32_t)bs + u);
+          if (sz < 0) { bad = true; break; }
+          all_b &= sz == B;
+          bs = sz;
+          sum += sz;
+          if (sum > xl) { bad = true; break; }
+        }
+        if (bad || sum != xl) { status = GGRS_CODEC_E_DELTA; break; }
+      } else {
+        cnt = xl / B;
+        if (cnt * B != xl) { status = GGRS_CODEC_E_DELTA; break; }
+      }
+      if (!all_b) { status = GGRS_CODEC_UNSUPPORTED; break; }
+      if (cnt > W) { status = GGRS_CODEC_E_CAP; break; }
+      int64_t q = 0;
+      int i = 0;
+      auto emit = [&](uint8_t xb) {
+        const uint8_t base = i < B ? rf[i] : o[i - B];
+        o[i] = xb ^ base;
+        i++;
+      };
+      while (q < (int64_t)m) {
+        uint64_t h;
+        get_varint(rle, (int64_t)m, q, h);
+        const int64_t rl = (int64_t)((h & 1) ? h >> 2 : h >> 1);
+        if (h & 1) {
+          const uint8_t fill = (h & 2) ? 0xFF : 0x00;
+          for (int64_t k = 0; k < rl; k++) emit(fill);
+        } else {
+          for (int64_t k = 0; k < rl; k++) emit(rle[q + k]);
+          q += rl;
+        }
+      }
+      count = (int32_t)cnt;
+    } while (false);
+    for (int b = status == GGRS_CODEC_OK ? count * B : 0; b < W * B; b++) o[b] = 0;
+    p.count[pk] = status == GGRS_CODEC_OK ? count : 0;
+    p.status[pk] = status;
+  }
+  __syncthreads();
+  lds_to_block(p.out + pk0 * (int64_t)W * B, l_out, out_pitch, np, W * B);
+}
+
+// LDS bytes for a block of T threads, or 0 when the staged form does not apply
+size_t encode_lds_bytes(int T, int B, int W, int stride) {
+  if ((W * B) % 4 || stride % 4 || W * B == 0) return 0;
+  return (size_t)T * (odd_dword_pitch(W * B) + odd_dword_pitch(stride) + B);
+}
+size_t decode_lds_bytes(int T, int B, int W, int stride) {
+  if ((W * B) % 4 || stride % 4 || W * B == 0) return 0;
+  return (size_t)T * (odd_dword_pitch(stride) + odd_dword_pitch(W * B) + B);
+}
+bool aligned4(const void* a) { return ((uintptr_t)a & 3) == 0; }
+constexpr size_t kLdsBudget = 64 * 1024;
+
 }  // namespace
 
 extern "C" {
@@ -248,7 +485,11 @@ int ggrs_codec_encode(const uint8_t* ref, const uint8_t* pending, const int32_t*
   if (n_packets == 0) return GGRS_OK;
   if (!ref || !pending || !count || !out || !out_len) return set_error(GGRS_E_INVALID, "null argument");
   EncodeParams p{ref, pending, count, out, out_len, n_packets, input_bytes, max_inputs, out_stride};
-  encode_kernel<<<grid_of(n_packets, 256), 256, 0, (hipStream_t)stream>>>(p);
+  const size_t lds = encode_lds_bytes(256, input_bytes, max_inputs, out_stride);
+  if (lds && lds <= kLdsBudget && aligned4(pending) && aligned4(out) && !g_codec_direct)
+    encode_lds_kernel<<<grid_of(n_packets, 256), 256, lds, (hipStream_t)stream>>>(p);
+  else
+    encode_kernel<<<grid_of(n_packets, 256), 256, 0, (hipStream_t)stream>>>(p);
   HIP_TRY(hipGetLastError());
   return GGRS_OK;
 }
@@ -261,17 +502,27 @@ int ggrs_codec_decode(const uint8_t* ref, const uint8_t* packets, const int32_t*
   if (n_packets == 0) return GGRS_OK;
   if (!ref || !packets || !packet_len || !out || !count || !status) return set_error(GGRS_E_INVALID, "null argument");
   DecodeParams p{ref, packets, packet_len, out, count, status, n_packets, input_bytes, max_inputs, packet_stride};
-  decode_kernel<<<grid_of(n_packets, 256), 256, 0, (hipStream_t)stream>>>(p);
+  const size_t lds = decode_lds_bytes(256, input_bytes, max_inputs, packet_stride);
+  if (lds && lds <= kLdsBudget && aligned4(packets) && aligned4(out) && !g_codec_direct)
+    decode_lds_kernel<<<grid_of(n_packets, 256), 256, lds, (hipStream_t)stream>>>(p);
+  else
+    decode_kernel<<<grid_of(n_packets, 256), 256, 0, (hipStream_t)stream>>>(p);
   HIP_TRY(hipGetLastError());
   return GGRS_OK;
 }
 
 int32_t ggrs_codec_max_packet_bytes(int32_t input_bytes, int32_t max_inputs) {
   // tag + u64 length + worst-case runs: alternating 1-byte literal / 1-byte compressed runs
-  // (3 bytes per 2 input bytes) plus one varint header per run
+  // (3 bytes per 2 input bytes) plus one varint header per run; rounded up to 16 bytes so rows
+  // stay dword aligned (the LDS-staged kernels move whole dwords)
   const int64_t L = (int64_t)input_bytes * max_inputs;
-  const int64_t v = 1 + 8 + L + (L + 1) / 2 + 10;
+  const int64_t v = (1 + 8 + L + (L + 1) / 2 + 10 + 15) / 16 * 16;
   return v > 0x7fffffff ? -1 : (int32_t)v;
+}
+
+int ggrs_codec_set_direct(int32_t on) {
+  g_codec_direct = on != 0;
+  return GGRS_OK;
 }
 
 }  // extern "C"

@@ -446,17 +446,6 @@ __device__ inline __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t by
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 
-// x mod n for x < 2^32 / n (n >= 1): q = mulhi(x, floor(2^32 / n) + 1) is floor(x / n) there, since
-// the multiplier's excess over 2^32 / n is < 1 and so adds less than x / 2^32 < 1 / n to x / n.
-// Scalar when x and n are (s_mul_hi_u32).  The SyncTest launch caps x at n_frames + cd < 2^24.
-// Requires n >= 2 (for n == 1 the caller scales the result by 0).
-__host__ __device__ inline uint32_t magic_small(uint32_t n) {
-  return n <= 1 ? 0u : (uint32_t)(0xffffffffu / n) + 1u;
-}
-__device__ inline uint32_t mod_small(uint32_t x, uint32_t n, uint32_t magic) {
-  return x - __umulhi(x, magic) * n;
-}
-
 // v from the lane Pp below (DPP wave_shr:1, Pp times); lanes < Pp get garbage (callers select)
 template <int Pp>
 __device__ inline uint32_t wave_shr_lanes(uint32_t v) {
@@ -798,11 +787,9 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
   // (scalar multiply-high modulo: a loop-carried counter would be widened to a VGPR)
   // (integer division runs on the VALU; readfirstlane brings the uniform results back to SGPRs,
   // otherwise every buffer store using them as soffset would be waterfalled)
-  const uint32_t sr0 = (uint32_t)__builtin_amdgcn_readfirstlane((g0 + 1) % R);
-  const uint32_t st0 = (uint32_t)__builtin_amdgcn_readfirstlane(p.trace_cap ? g0 % p.trace_cap : 0);
-  const uint32_t magic_r = (uint32_t)__builtin_amdgcn_readfirstlane((int)magic_small(R));
-  const uint32_t magic_t = (uint32_t)__builtin_amdgcn_readfirstlane((int)magic_small(p.trace_cap));
-  const uint32_t tr_slot_bytes = p.trace_cap > 1 ? ck_slot_bytes : 0u;  // one trace slot: offset 0
+  int32_t sr = __builtin_amdgcn_readfirstlane((g0 + 1) % R);
+  int32_t st = __builtin_amdgcn_readfirstlane(p.trace_cap ? g0 % p.trace_cap : 0);
+  const int32_t tcap = p.trace_cap > 0 ? p.trace_cap : 1;
   const bool corrupt_here = p.corrupt_frame >= p.f0 && p.corrupt_frame < p.f0 + p.n;
   const uint32_t corrupt_on = (corrupt_here && s == p.corrupt_lane && pl == 0 && j == 0) ? 1u : 0u;
   const int32_t ramp_end = min(p.f0 + cd, t_end);
@@ -874,8 +861,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
     // the first save of frame t-cd+1 happened in the previous launch while its chain is not ours
     if (!kCore && rel + 1 < cd) first = lds_first[(rel + 1) * kWave + g];
     // SaveGameState(t-cd+1) for role j+1, first-seen, display checksum
-    const uint32_t sru = mod_small((uint32_t)rel + sr0, (uint32_t)R, magic_r);
-    const uint32_t stu = mod_small((uint32_t)rel + st0, (uint32_t)p.trace_cap, magic_t);
+    const uint32_t sru = (uint32_t)sr, stu = (uint32_t)st;
     auto stores = [&]() {
       const uint32_t so = sru * slot_bytes, cso = sru * ck_slot_bytes;
 #pragma unroll
@@ -883,7 +869,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
       __builtin_amdgcn_raw_buffer_store_b32(frame1, rs_ring, fo_frame, so, 0);
       __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ring, co, cso, 0);
       __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ring, co_first, cso, 0);
-      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_trace, co_trace, stu * tr_slot_bytes, 0);
+      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_trace, co_trace, stu * ck_slot_bytes, 0);
     };
     if (kCore) {
       stores();
@@ -904,6 +890,10 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
     pend_first = first;
 #pragma unroll
     for (int q = 0; q < 5; q++) w[q] = nx[q];
+    // wave-uniform slot counters (their readfirstlane'd start keeps them in SGPRs: a start value
+    // from the VALU's integer division would widen them and waterfall every store using them)
+    sr = sr + 1 == R ? 0 : sr + 1;
+    st = st + 1 == tcap ? 0 : st + 1;
   };
 
   int32_t t = p.f0;

@@ -210,6 +210,9 @@ int ggrs_branch_read_lane(ggrs_branch_engine_t* eng, int64_t lane, int32_t frame
                           uint8_t* out);
 int ggrs_branch_timing_reset(ggrs_branch_engine_t* eng);
 int ggrs_branch_timing_read(ggrs_branch_engine_t* eng, float* total_ms, int32_t* launches);
+/* n_rounds x (ggrs_branch_speculate, ggrs_branch_confirm without a report copy) issued back to
+ * back from native code; while timing is collected one event pair brackets the whole batch */
+int ggrs_branch_rounds(ggrs_branch_engine_t* eng, int32_t n_rounds);
 
 /* ---------------------------------------------------------------------------------------------
  * Config-5 large-state stress game (defined by this build; ggrs_amd/csrc/particles.h):
@@ -351,8 +354,11 @@ int ggrs_codec_encode(const uint8_t* ref, const uint8_t* pending, const int32_t*
 int ggrs_codec_decode(const uint8_t* ref, const uint8_t* packets, const int32_t* packet_len, int64_t n_packets,
                       int32_t packet_stride, int32_t input_bytes, int32_t max_inputs, uint8_t* out, int32_t* count,
                       int32_t* status, void* stream);
-/* an out_stride that every packet of max_inputs inputs fits */
+/* an out_stride that every packet of max_inputs inputs fits (a multiple of 16) */
 int32_t ggrs_codec_max_packet_bytes(int32_t input_bytes, int32_t max_inputs);
+/* on != 0: use the direct per-thread kernels even where the LDS-staged ones apply (for tests and
+ * comparison; process-wide) */
+int ggrs_codec_set_direct(int32_t on);
 
 #ifdef __cplusplus
 }

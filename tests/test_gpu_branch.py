@@ -81,6 +81,33 @@ def test_generators_many_sessions(oracle, branches, window, P, mask):
     run_rounds(oracle, eng, truth, rounds, lanes)
 
 
+def test_native_rounds_equal_single_rounds(oracle):
+    """rounds(n) (back-to-back native launches) leaves every trunk, report and survivor set exactly
+    as n single speculate + confirm calls; the survival bits feed the next round's desync check."""
+    from ggrs_amd import BranchEngine, synth
+    S, W, B, n = 200, 6, 16, 9
+    truth = synth.gen_inputs(11, S, n + W + 2, 4, synth.MODEL_HELD)
+    engs = [BranchEngine(S, num_players=4, remote_mask=0b0110, window=W, branches=B, alphabet=16) for _ in (0, 1)]
+    for e in engs:
+        e.add_inputs(0, truth)
+    engs[0].rounds(n)
+    for _ in range(n):
+        engs[1].speculate()
+        engs[1].confirm()
+    for e in engs:
+        e.synchronize()
+    assert engs[0].trunk_frame() == engs[1].trunk_frame() == n
+    for s in (0, 1, S - 1):
+        assert bytes(engs[0].trunk(s)) == bytes(engs[1].trunk(s))
+    a, b = engs[0].report(), engs[1].report()
+    assert (a[0] == b[0]).all() and (a[1] == b[1]).all()
+    assert (engs[0].desync() == -1).all() and (engs[1].desync() == -1).all()
+    st = oracle.state_new(4)
+    for f in range(n):
+        st = oracle.state_advance(st, truth[f, 0])
+    assert bytes(engs[0].trunk(0)) == bytes(st)
+
+
 def test_report_to_device_buffer(oracle):
     """confirm() can copy the report into a caller-owned device buffer (the all-gather input)."""
     from ggrs_amd import BranchEngine, synth

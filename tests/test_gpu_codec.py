@@ -28,9 +28,18 @@ def gpu(a):
     return torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
 
+@pytest.fixture(params=["staged", "direct"])
+def kernels(request):
+    """Both kernel forms: LDS-staged (default where rows are whole dwords) and direct."""
+    from ggrs_amd import codec
+    codec.set_direct(request.param == "direct")
+    yield request.param
+    codec.set_direct(False)
+
+
 @pytest.mark.parametrize("N,W,B,held", [(5000, 8, 1, True), (3000, 16, 2, False), (2000, 33, 4, False),
                                          (1000, 128, 1, True), (257, 1, 7, False)])
-def test_encode_matches_oracle_and_round_trips(oracle, N, W, B, held):
+def test_encode_matches_oracle_and_round_trips(oracle, kernels, N, W, B, held):
     from ggrs_amd import codec
     rng = np.random.default_rng(N + W + B)
     ref, pend, count = batch(rng, N, W, B, held)
@@ -58,7 +67,7 @@ def test_reference_vector():
 
 
 @pytest.mark.parametrize("mode", ["mutated", "random", "truncated"])
-def test_hostile_packets_match_oracle(oracle, mode):
+def test_hostile_packets_match_oracle(oracle, kernels, mode):
     """Every packet the reference rejects is rejected with the same error class; every packet it
     accepts decodes identically (or is UNSUPPORTED when its inputs are not all B bytes)."""
     from ggrs_amd import codec
