@@ -54,6 +54,22 @@ def pmc_traffic(workload):
         return None
 
 
+def pmc_valu(workload):
+    """VALU utilisation of the step kernel from the same committed profile summary (rocprofv3
+    SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES, SQ_INSTS_VALU / SQ_WAVES), or None."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        if d.get("valu_active_frac_of_wave_cycles") is None:
+            return None
+        return {"active_frac_of_wave_cycles": round(d["valu_active_frac_of_wave_cycles"], 4),
+                "insts_per_wave": round(d["valu_insts_per_wave"], 1),
+                "wait_frac_of_wave_cycles": round(d["wait_any_frac"], 4), "profile": d.get("tag")}
+    except Exception:
+        return None
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as fh:
@@ -553,7 +569,9 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(workload),
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "avg_launch_ms": round(avg_launch_s * 1e3, 4),
-                "note": "VALU-bound (f32 step + f64 glibc sincosf); working set fits L2/MALL"}
+                "valu": pmc_valu(workload),
+                "note": "issue/latency-bound step kernel (f32 step + f64 glibc sincosf, one wave per "
+                        "SIMD); the 2 MB ring fits L2/MALL, so HBM traffic is below the algorithmic bytes"}
 
     parity = None
     cpu_baseline = None

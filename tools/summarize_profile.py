@@ -83,7 +83,10 @@ def main(tag, workload, kernel="synctest_kernel", last="0"):
         with open(os.path.join(ROOT, "profiles", f"pmc_{workload}.json"), "w") as fh:
             json.dump({"tag": tag, "kernel": kname, "hbm_bytes_per_launch": out["hbm_bytes_per_launch"],
                        "hbm_bytes_per_launch_raw": out["hbm_bytes_per_launch_raw"],
-                       "avg_duration_ns": avg_ns}, fh, indent=1)
+                       "avg_duration_ns": avg_ns,
+                       "valu_active_frac_of_wave_cycles": out.get("valu_active_frac_of_wave_cycles"),
+                       "valu_insts_per_wave": out.get("valu_insts_per_wave"),
+                       "wait_any_frac": out.get("wait_any_frac")}, fh, indent=1)
     for f in ("bench_trace.log",):
         if os.path.exists(os.path.join(src, f)):
             shutil.copy(os.path.join(src, f), os.path.join(dst, f))
