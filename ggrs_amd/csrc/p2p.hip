@@ -88,24 +88,43 @@ __device__ inline void save_cell(const P2PParams& p, const BoxState<P>& s, int32
   p.ring_ck[(int64_t)slot * p.S + sess] = fletcher16_state<P>(s);
 }
 
+// Input rows as the calls read them: from global memory, or (staged kernel) from the block's LDS
+// copy of rows [lo, lo + kP2PRows) -- one LDS byte read instead of a dependent global load.
+constexpr int kP2PRows = 64;
+constexpr int kP2PBlock = 256;
+
 template <int P>
-__device__ inline uint32_t input_row(const P2PParams& p, int32_t g, int64_t sess) {
-  return load_inputs<P>(p.inputs, (int64_t)(g % p.cap) * p.S + sess);
-}
+struct GlobalRows {
+  const P2PParams& p;
+  int64_t sess;
+  __device__ inline uint32_t operator()(int32_t g) const {
+    return load_inputs<P>(p.inputs, (int64_t)(g % p.cap) * p.S + sess);
+  }
+};
+template <int P>
+struct LdsRows {
+  const uint8_t* lds;  // [kP2PRows][kP2PBlock][Pp]
+  int32_t lo;
+  int tid;
+  __device__ inline uint32_t operator()(int32_t g) const {
+    using T = typename InputWord<P>::T;
+    return (uint32_t)reinterpret_cast<const T*>(lds)[(g - lo) * kP2PBlock + tid];
+  }
+};
 
 // synchronized_inputs(h) (sync_layer.rs:280-293) with InputQueue::input (input_queue.rs:104-167).
 // last_added: the remote queues' last_added_frame (f - D after this call's poll, or NULL).
-template <int P>
+template <int P, typename Rows>
 __device__ inline uint32_t sync_inputs(const P2PParams& p, RemoteQueues<P>& q, int32_t h, int32_t last_added,
-                                       int64_t sess) {
+                                       const Rows& input_row) {
   uint32_t in = 0;
   // local queues hold every frame <= f + delay: queue frame h is user input h - delay, and the
   // frames below the delay replicate the default input (input_queue.rs:233-265)
-  const uint32_t local_row = (p.local_mask && h >= p.delay) ? input_row<P>(p, h - p.delay, sess) : 0u;
+  const uint32_t local_row = (p.local_mask && h >= p.delay) ? input_row(h - p.delay) : 0u;
   uint32_t confirmed_row = 0u, last_row = 0u;
   const bool confirmed = last_added != kNull && h <= last_added;
-  if (confirmed) confirmed_row = input_row<P>(p, h, sess);
-  else if (last_added != kNull && h != 0) last_row = input_row<P>(p, last_added, sess);
+  if (confirmed) confirmed_row = input_row(h);
+  else if (last_added != kNull && h != 0) last_row = input_row(last_added);
 #pragma unroll
   for (int k = 0; k < P; k++) {
     uint32_t v;
@@ -130,11 +149,19 @@ __device__ inline uint32_t sync_inputs(const P2PParams& p, RemoteQueues<P>& q, i
   return in;
 }
 
-template <int P>
-__global__ __launch_bounds__(256) void p2p_kernel(P2PParams p) {
-  const int64_t sess = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (sess >= p.S) return;
+// kStaged: the block's input rows are copied to LDS per chunk of calls (one coalesced pass over
+// rows [f - back, chunk end)), so the calls' input reads are LDS reads; every thread of the block
+// runs the same calls, idle tail threads included (they never store).
+template <int P, bool kStaged>
+__global__ __launch_bounds__(kP2PBlock) void p2p_kernel(P2PParams p) {
+  constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
+  __shared__ __attribute__((aligned(16))) uint8_t lds_rows[kStaged ? kP2PRows * kP2PBlock * Pp : 4];
+  const int64_t sess0 = (int64_t)blockIdx.x * kP2PBlock;
   const int64_t S = p.S;
+  const bool live = sess0 + threadIdx.x < S;
+  if (!kStaged && !live) return;
+  const int64_t sess = live ? sess0 + threadIdx.x : sess0;  // idle threads shadow the block's first
+  const int nb = (int)((S - sess0) < kP2PBlock ? (S - sess0) : kP2PBlock);
   BoxState<P> st;
   load_state<P>(st, p.cur + sess, S);
   RemoteQueues<P> q;
@@ -147,24 +174,49 @@ __global__ __launch_bounds__(256) void p2p_kernel(P2PParams p) {
   }
   int32_t rollbacks = 0;
   int64_t resim = 0;
-  const bool dbg = sess == p.dbg_sess;
+  const bool dbg = live && sess == p.dbg_sess;
   int32_t last_saved = p.sparse ? p.last_saved[sess] : kNull;
   auto save = [&](int32_t h) {
-    save_cell<P>(p, st, h, sess);
+    if (live) {
+      save_cell<P>(p, st, h, sess);
+      if (p.sparse) p.ring_frame[(int64_t)(h % p.R) * S + sess] = h;  // GameStateCell.frame
+    }
     last_saved = h;
-    if (p.sparse) p.ring_frame[(int64_t)(h % p.R) * S + sess] = h;  // GameStateCell.frame
   };
+  // rows a call f reads: >= f - back (rollback start, local rows h - delay), <= f
+  const int32_t back = (p.sparse ? p.R - 1 : p.D) + p.delay;
+  int32_t row_lo = 0;
+  auto stage = [&](int32_t lo, int32_t nrows) {
+    __syncthreads();
+    row_lo = lo;
+    const int row_bytes = nb * Pp;
+    if (nb == kP2PBlock && ((S * Pp) & 3) == 0) {  // whole dwords: rows are dword aligned
+      const int dpr = row_bytes / 4;
+      for (int q = threadIdx.x; q < nrows * dpr; q += kP2PBlock) {
+        const int r = q / dpr, c = q - r * dpr;
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(p.inputs + ((int64_t)((lo + r) % p.cap) * S + sess0) * Pp);
+        reinterpret_cast<uint32_t*>(lds_rows + r * kP2PBlock * Pp)[c] = src[c];
+      }
+    } else {
+      for (int q = threadIdx.x; q < nrows * row_bytes; q += kP2PBlock) {
+        const int r = q / row_bytes, b = q - r * row_bytes;
+        lds_rows[r * kP2PBlock * Pp + b] = p.inputs[((int64_t)((lo + r) % p.cap) * S + sess0) * Pp + b];
+      }
+    }
+    __syncthreads();
+  };
+  const int tid = live ? (int)threadIdx.x : 0;
   auto advance = [&](uint32_t in) {
     const uint32_t from = st.w[0];
     advance_state<P>(st, in, 0u);
     if (dbg && (int32_t)from == p.dbg_frame) st.w[fld_x(P, 0)] ^= 1u;
   };
-  for (int32_t f = p.f0; f < p.f0 + p.n; ++f) {
+  auto call = [&](int32_t f, const auto& input_row) {
     // 0. check_checksum_send_interval (p2p_session.rs:939-975), before any rollback of this call:
     //    last_confirmed_frame = f - 1 - D and last_saved_frame = f - 1 here, so frame_to_send =
     //    interval, 2 interval, ... goes out at call frame_to_send + D + 1; its cell is in the ring
     //    (D + 1 < R), its checksum enters the local history
-    if (p.desync_interval > 0) {
+    if (p.desync_interval > 0 && live) {
       const int32_t fts = f - 1 - p.D;
       if (fts >= p.desync_interval && fts % p.desync_interval == 0)
         p.hist[(int64_t)((fts / p.desync_interval) % kHist) * S + sess] = p.ring_ck[(int64_t)(fts % p.R) * S + sess];
@@ -173,7 +225,7 @@ __global__ __launch_bounds__(256) void p2p_kernel(P2PParams p) {
     const int32_t g = f - p.D;
     const int32_t last_added = g >= 0 ? g : kNull;
     if (g >= 0) {
-      const uint32_t row = input_row<P>(p, g, sess);
+      const uint32_t row = input_row(g);
 #pragma unroll
       for (int k = 0; k < P; k++) {
         if ((p.local_mask >> k) & 1u) continue;
@@ -201,7 +253,7 @@ __global__ __launch_bounds__(256) void p2p_kernel(P2PParams p) {
         q.last_req[k] = kNull;
       }
       for (int32_t h = load; h < f; ++h) {
-        const uint32_t in = sync_inputs<P>(p, q, h, last_added, sess);
+        const uint32_t in = sync_inputs<P>(p, q, h, last_added, input_row);
         if (p.sparse ? h == confirmed : h > load) save(h);
         advance(in);
       }
@@ -220,10 +272,25 @@ __global__ __launch_bounds__(256) void p2p_kernel(P2PParams p) {
       if (confirmed >= f) save(f);
       else adjust(last_saved);
     }
-    const uint32_t in = sync_inputs<P>(p, q, f, last_added, sess);
+    const uint32_t in = sync_inputs<P>(p, q, f, last_added, input_row);
     advance(in);
-    if (p.trace) p.trace[(int64_t)(f % p.trace_cap) * S + sess] = fletcher16_state<P>(st);
+    if (p.trace && live) p.trace[(int64_t)(f % p.trace_cap) * S + sess] = fletcher16_state<P>(st);
+  };
+  const int32_t f_end = p.f0 + p.n;
+  if constexpr (kStaged) {
+    const int32_t calls_per_stage = kP2PRows - back;  // >= 1 (host)
+    for (int32_t f = p.f0; f < f_end;) {
+      const int32_t chunk_end = min(f_end, f + calls_per_stage);
+      const int32_t lo = max(0, f - back);
+      stage(lo, chunk_end - lo);
+      const LdsRows<P> rows{lds_rows, row_lo, tid};
+      for (; f < chunk_end; ++f) call(f, rows);
+    }
+  } else {
+    const GlobalRows<P> rows{p, sess};
+    for (int32_t f = p.f0; f < f_end; ++f) call(f, rows);
   }
+  if (!live) return;
   store_state<P>(st, p.cur + sess, S);
 #pragma unroll
   for (int k = 0; k < P; k++) {
@@ -284,6 +351,7 @@ struct ggrs_p2p_engine {
   int64_t dbg_sess = -1;
   int32_t dbg_frame = -1;
   int32_t sparse = 0;
+  bool unstaged = false;          // ggrs_p2p_set_unstaged: global input reads (comparison/tests)
   int32_t* last_saved = nullptr;  // [S], sparse saving only
   int32_t* ring_frame = nullptr;  // [R][S], sparse saving only
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -484,9 +552,13 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
   if ((int64_t)p.f0 + n - 1 - oldest_row(e, p.f0) >= e->cap)
     return set_error(GGRS_E_INVALID, "advance of %d frames reads more input rows than input_capacity (%d)", n, e->cap);
   int rc = p2p_launch_timed(e, [&] {
+    // stage input rows in LDS unless a call reaches further back than a stage holds
+    const int32_t back = (e->sparse ? e->R - 1 : p.D) + p.delay;
+    const bool staged = back + 1 <= kP2PRows - 1 && !e->unstaged;
     dispatch_players(e->cfg.num_players, [&](auto PC) {
       constexpr int P = decltype(PC)::value;
-      p2p_kernel<P><<<grid_of(p.S, 256), 256, 0, e->stream>>>(p);
+      if (staged) p2p_kernel<P, true><<<grid_of(p.S, kP2PBlock), kP2PBlock, 0, e->stream>>>(p);
+      else p2p_kernel<P, false><<<grid_of(p.S, kP2PBlock), kP2PBlock, 0, e->stream>>>(p);
     });
   });
   if (rc) return rc;
@@ -524,6 +596,12 @@ int ggrs_p2p_set_sparse_saving(ggrs_p2p_engine_t* e, int32_t on) {
     HIP_TRY(hipMemsetAsync(e->ring_frame, 0xff, sizeof(int32_t) * e->R * S, e->stream));
   }
   e->sparse = on ? 1 : 0;
+  return GGRS_OK;
+}
+
+int ggrs_p2p_set_unstaged(ggrs_p2p_engine_t* e, int32_t on) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  e->unstaged = on != 0;
   return GGRS_OK;
 }
 

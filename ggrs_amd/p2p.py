@@ -60,6 +60,7 @@ def _bind(L):
     L.ggrs_p2p_compare_checksums.argtypes = [vp, i32, vp, i32, vp, P(i32)]
     L.ggrs_p2p_debug_desync.argtypes = [vp, i32, i32]
     L.ggrs_p2p_set_sparse_saving.argtypes = [vp, i32]
+    L.ggrs_p2p_set_unstaged.argtypes = [vp, i32]
     for name in _lib.EXPORTS:
         if name.startswith("ggrs_p2p_"):
             getattr(L, name).restype = ctypes.c_int
@@ -193,3 +194,7 @@ class P2PEngine:
         """SessionBuilder::with_sparse_saving_mode for every session; before the first call."""
         _lib.check(self._L.ggrs_p2p_set_sparse_saving(self._h, int(bool(on))))
         self.sparse_saving = bool(on)
+
+    def set_unstaged(self, on=True):
+        """Read input rows from global memory instead of the LDS stage (for comparison)."""
+        _lib.check(self._L.ggrs_p2p_set_unstaged(self._h, int(bool(on))))
