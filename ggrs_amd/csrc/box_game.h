@@ -217,17 +217,12 @@ __device__ inline void advance_player_lean(float& x, float& y, float& vx, float&
   vy = vel_y;
 }
 
-__device__ inline void advance_player_v4(float& x, float& y, float& vx, float& vy, float& rot, uint32_t input) {
-  const bool in_domain = __builtin_bit_cast(uint32_t, rot) <= kTwoPiBits;
-  if (__builtin_expect(__all(in_domain), 1)) advance_player_lean(x, y, vx, vy, rot, input);
-  else advance_player_general(x, y, vx, vy, rot, input);
-}
-
-// Dispatch: the branch-free form when every active lane's rot is in the domain (always, for
-// states this engine produced), else the general form for the whole wave.
+// Dispatch (every kernel): the lean branch-free form when every active lane's rot is in the
+// domain (always, for states this engine produced), else the general form for the whole wave.
+// advance_player_domain stays as the KAT reference of the lean form.
 __device__ inline void advance_player(float& x, float& y, float& vx, float& vy, float& rot, uint32_t input) {
   const bool in_domain = __builtin_bit_cast(uint32_t, rot) <= kTwoPiBits;
-  if (__builtin_expect(__all(in_domain), 1)) advance_player_domain(x, y, vx, vy, rot, input);
+  if (__builtin_expect(__all(in_domain), 1)) advance_player_lean(x, y, vx, vy, rot, input);
   else advance_player_general(x, y, vx, vy, rot, input);
 }
 

@@ -820,7 +820,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
       float x = __builtin_bit_cast(float, w[0]), y = __builtin_bit_cast(float, w[1]);
       float vx = __builtin_bit_cast(float, w[2]), vy = __builtin_bit_cast(float, w[3]);
       float rot = __builtin_bit_cast(float, w[4]);
-      advance_player_v4(x, y, vx, vy, rot, in);
+      advance_player(x, y, vx, vy, rot, in);
       w[0] = __builtin_bit_cast(uint32_t, x);
       w[1] = __builtin_bit_cast(uint32_t, y);
       w[2] = __builtin_bit_cast(uint32_t, vx);

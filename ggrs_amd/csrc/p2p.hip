@@ -211,6 +211,19 @@ __global__ __launch_bounds__(kP2PBlock) void p2p_kernel(P2PParams p) {
     advance_state<P>(st, in, 0u);
     if (dbg && (int32_t)from == p.dbg_frame) st.w[fld_x(P, 0)] ^= 1u;
   };
+  // Without sparse saving a rollback at call f always loads frame f - D (the remote input of that
+  // frame is the one arriving), and that cell is final once call f - 1 has ended (its last
+  // re-save is by call f - 1's rollback at the latest).  So the cell is read at the end of call
+  // f - 1, and its load latency overlaps the next poll instead of stalling the rollback.
+  BoxState<P> pre;
+  int32_t pre_frame = kNull;
+  auto prefetch = [&](int32_t fr) {
+    if (!p.sparse && fr >= 0) {
+      load_state<P>(pre, p.ring + (int64_t)(fr % p.R) * state_fields(P) * S + sess, S);
+      pre_frame = fr;
+    }
+  };
+  prefetch(p.f0 - p.D);
   auto call = [&](int32_t f, const auto& input_row) {
     // 0. check_checksum_send_interval (p2p_session.rs:939-975), before any rollback of this call:
     //    last_confirmed_frame = f - 1 - D and last_saved_frame = f - 1 here, so frame_to_send =
@@ -245,7 +258,8 @@ __global__ __launch_bounds__(kP2PBlock) void p2p_kernel(P2PParams p) {
     // 3. check_simulation_consistency + adjust_gamestate (:658-714)
     auto adjust = [&](int32_t first_incorrect) {
       const int32_t load = p.sparse ? last_saved : first_incorrect;  // sparse: the last save
-      load_state<P>(st, p.ring + (int64_t)(load % p.R) * state_fields(P) * S + sess, S);
+      if (load == pre_frame) st = pre;
+      else load_state<P>(st, p.ring + (int64_t)(load % p.R) * state_fields(P) * S + sess, S);
 #pragma unroll
       for (int k = 0; k < P; k++) {  // reset_prediction (input_queue.rs:63-67)
         q.pred_frame[k] = kNull;
@@ -275,6 +289,7 @@ __global__ __launch_bounds__(kP2PBlock) void p2p_kernel(P2PParams p) {
     const uint32_t in = sync_inputs<P>(p, q, f, last_added, input_row);
     advance(in);
     if (p.trace && live) p.trace[(int64_t)(f % p.trace_cap) * S + sess] = fletcher16_state<P>(st);
+    prefetch(f + 1 - p.D);
   };
   const int32_t f_end = p.f0 + p.n;
   if constexpr (kStaged) {
