@@ -7,6 +7,10 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libggrs_amd.so")
+# timing-experiment builds (tools/exp_build.sh) live in ggrs_amd/exp/; only those may replace the library
+_EXP = os.environ.get("GGRS_AMD_EXP_LIB")
+if _EXP:
+    LIB_PATH = os.path.join(HERE, "exp", os.path.basename(_EXP))
 
 GGRS_OK = 0
 GGRS_E_INVALID = -1

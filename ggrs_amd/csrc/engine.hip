@@ -466,7 +466,8 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v3_kernel(PipeParams
   constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
   constexpr int F = state_fields(P);
   constexpr int n_bytes = Fletcher<P>::n;
-  __shared__ uint8_t lds_in[kStageFrames * kWave];       // [frame][session-in-block][Pp]
+  // [frame][session-in-block][Pp], one slack frame for the core loop's read-ahead past a chunk
+  __shared__ uint8_t lds_in[(kStageFrames + 1) * kWave];
   __shared__ uint16_t lds_first[kMaxRampFrames * kWave];  // [ramp frame][session-in-block]
   __shared__ uint32_t lds_cell[kWave * 5];                // chain f0's LoadGameState, per lane
   if (*p.fail_f0 >= 0) return;
@@ -707,7 +708,8 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
   constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
   constexpr int F = state_fields(P);
   constexpr int n_bytes = Fletcher<P>::n;
-  __shared__ uint8_t lds_in[kStageFrames * kWave];       // [frame][session-in-block][Pp]
+  // [frame][session-in-block][Pp], one slack frame for the core loop's read-ahead past a chunk
+  __shared__ uint8_t lds_in[(kStageFrames + 1) * kWave];
   __shared__ uint16_t lds_first[kMaxRampFrames * kWave];  // [ramp frame][session-in-block]
   __shared__ uint32_t lds_cell[kWave * 5];                // chain f0's LoadGameState, per lane
   if (*p.fail_f0 >= 0) return;
@@ -735,9 +737,10 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
   // ring's base covers all three (fewer live SGPRs keeps the slot counters scalar)
   const uint32_t ck_base = (uint32_t)((const uint8_t*)p.ring_ck - (const uint8_t*)p.ring);
   const uint32_t first_base = (uint32_t)((const uint8_t*)p.first_ck - (const uint8_t*)p.ring);
-  const __amdgpu_buffer_rsrc_t rs_ring = make_rsrc(p.ring, first_base + ck_slot_bytes * (uint32_t)R);
-  const __amdgpu_buffer_rsrc_t rs_trace =
-      make_rsrc(p.trace, p.trace ? ck_slot_bytes * (uint32_t)p.trace_cap : 0u);
+  // the trace follows them in the same allocation (engine create), so the descriptor reaches it too
+  const uint32_t trace_base = p.trace ? (uint32_t)((const uint8_t*)p.trace - (const uint8_t*)p.ring) : 0u;
+  const __amdgpu_buffer_rsrc_t rs_ring = make_rsrc(
+      p.ring, p.trace ? trace_base + ck_slot_bytes * (uint32_t)p.trace_cap : first_base + ck_slot_bytes * (uint32_t)R);
   // static store offsets: producers (roles 0..cd-1) save; role cd-1 also writes first_ck; role cd
   // writes the display checksum
   const bool producer = valid && j <= cd - 1;
@@ -747,7 +750,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
   const uint32_t fo_frame = (producer && pl == 0) ? (uint32_t)(s * 4) : kOob;
   const uint32_t co = (producer && pl == 0) ? ck_base + (uint32_t)(s * 2) : kOob;
   const uint32_t co_first = (valid && pl == 0 && j == cd - 1) ? first_base + (uint32_t)(s * 2) : kOob;
-  const uint32_t co_trace = (valid && pl == 0 && j == cd) ? (uint32_t)(s * 2) : kOob;
+  const uint32_t co_trace = (p.trace && valid && pl == 0 && j == cd) ? trace_base + (uint32_t)(s * 2) : kOob;
   // re-saves compared against the first-seen value: producers for roles 1..cd-1, player-0 lane
   const uint64_t cmp_lanes = __ballot(valid && pl == 0 && j <= cd - 2);
   // doubled Fletcher weights (fletcher_from_doubled); the frame field and the constant length
@@ -793,7 +796,12 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
   const bool corrupt_here = p.corrupt_frame >= p.f0 && p.corrupt_frame < p.f0 + p.n;
   const uint32_t corrupt_on = (corrupt_here && s == p.corrupt_lane && pl == 0 && j == 0) ? 1u : 0u;
   const int32_t ramp_end = min(p.f0 + cd, t_end);
-  const int32_t core_end = corrupt_here ? ramp_end : max(ramp_end, p.f0 + p.n);
+  // the core loop steps through advance_player_lean without the per-step domain test: every role
+  // starts from the loaded cell and every later state is an advance of an in-domain state, so one
+  // test of the loaded rot suffices (a cell from outside the domain runs every step in the general
+  // per-step dispatch instead)
+  const bool lean_ok = __all(w[4] <= kTwoPiBits);
+  const int32_t core_end = (corrupt_here || !lean_ok) ? ramp_end : max(ramp_end, p.f0 + p.n);
 
   auto stage = [&](int32_t t) {
     __syncthreads();
@@ -806,27 +814,35 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
     __syncthreads();
   };
 
-  // One step t.  kCore: every chain is active (t in [f0 + cd, f0 + n)) and no injected corruption.
-  auto step = [&](auto core_tag, int32_t t) {
+  uint32_t acc = 0;  // core steps: OR of (re-save ^ first-seen) per lane, masked by cmp_lanes at the end
+  const uint32_t in_at = (uint32_t)in_lane;
+
+  // One step t with its input byte.  kCore: every chain is active (t in [f0 + cd, f0 + n)), no
+  // injected corruption, states in the lean domain.
+  auto step = [&](auto core_tag, int32_t t, uint32_t in) {
     constexpr bool kCore = decltype(core_tag)::value;
     const int32_t rel = t - p.f0;
     const int32_t c = t - j;  // this lane's chain
     const bool active = kCore ? valid : (valid && c >= p.f0 && c < p.f0 + p.n);
-    const uint32_t in = lds_in[(rel & (kStageFrames - 1)) * row + in_lane];
-    bad |= __ballot(pend_ck != pend_first) & pend_lanes;
-    if (!kCore) w[0] ^= (t == p.corrupt_frame) ? corrupt_on : 0u;  // role 0 = chain t's load
+    if (!kCore) {
+      bad |= __ballot(pend_ck != pend_first) & pend_lanes;
+      w[0] ^= (t == p.corrupt_frame) ? corrupt_on : 0u;  // role 0 = chain t's load
+    }
     // AdvanceFrame(t - cd) on every lane
     {
       float x = __builtin_bit_cast(float, w[0]), y = __builtin_bit_cast(float, w[1]);
       float vx = __builtin_bit_cast(float, w[2]), vy = __builtin_bit_cast(float, w[3]);
       float rot = __builtin_bit_cast(float, w[4]);
-      advance_player(x, y, vx, vy, rot, in);
+      if constexpr (kCore) advance_player_lean(x, y, vx, vy, rot, in);
+      else advance_player(x, y, vx, vy, rot, in);
       w[0] = __builtin_bit_cast(uint32_t, x);
       w[1] = __builtin_bit_cast(uint32_t, y);
       w[2] = __builtin_bit_cast(uint32_t, vx);
       w[3] = __builtin_bit_cast(uint32_t, vy);
       w[4] = __builtin_bit_cast(uint32_t, rot);
     }
+    // the previous step's comparison, one advance after its first-seen value was requested
+    if (kCore) acc |= pend_ck ^ pend_first;
     const uint32_t frame1 = (uint32_t)(t - cd + 1);
     // rotation for step t+1: role j takes role j-1's state, Pp lanes down; two DPP wave_shr:1
     // moves (VALU, no LDS round trip) and role 0 keeps its own
@@ -837,7 +853,11 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
         const uint32_t sh = wave_shr_lanes<Pp>(w[q]);
         nx[q] = (w[q] & keep_own) | (sh & ~keep_own);  // a plain select here gets branched
       } else {
+#ifdef GGRS_EXP_NO_ROT
+        nx[q] = w[q];
+#else
         nx[q] = (uint32_t)__builtin_amdgcn_ds_bpermute(src_rot, (int)w[q]);
+#endif
       }
     }
     if constexpr (!kDppRot) __builtin_amdgcn_sched_barrier(0);  // LDS latency behind the save
@@ -856,7 +876,11 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
       d1 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d1, 0x4E, 0xF, 0xF, true);  // xor 2
       d2 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d2, 0x4E, 0xF, 0xF, true);
     }
+#ifdef GGRS_EXP_NO_FLETCHER
+    const uint32_t ck = w[0] & 0xffff;
+#else
     const uint32_t ck = fletcher_from_doubled(d1, d2);
+#endif
     uint32_t first = (uint32_t)__builtin_amdgcn_ds_bpermute(src_first, (int)ck);
     // the first save of frame t-cd+1 happened in the previous launch while its chain is not ours
     if (!kCore && rel + 1 < cd) first = lds_first[(rel + 1) * kWave + g];
@@ -864,12 +888,16 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
     const uint32_t sru = (uint32_t)sr, stu = (uint32_t)st;
     auto stores = [&]() {
       const uint32_t so = sru * slot_bytes, cso = sru * ck_slot_bytes;
+#ifndef GGRS_EXP_NO_FIELD_STORES  // timing experiments only (tools/exp_build.sh), never shipped
 #pragma unroll
       for (int q = 0; q < 5; q++) __builtin_amdgcn_raw_buffer_store_b32(w[q], rs_ring, fo[q], so, 0);
       __builtin_amdgcn_raw_buffer_store_b32(frame1, rs_ring, fo_frame, so, 0);
+#endif
+#ifndef GGRS_EXP_NO_CK_STORES
       __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ring, co, cso, 0);
       __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ring, co_first, cso, 0);
-      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_trace, co_trace, stu * ck_slot_bytes, 0);
+      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ring, co_trace, stu * ck_slot_bytes, 0);
+#endif
     };
     if (kCore) {
       stores();
@@ -896,20 +924,46 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
     st = st + 1 == tcap ? 0 : st + 1;
   };
 
+  auto input_at = [&](int32_t t) -> uint32_t {
+    return lds_in[(((t - p.f0) & (kStageFrames - 1)) * row) + in_at];
+  };
   int32_t t = p.f0;
   for (; t < ramp_end; ++t) {
     if (((t - p.f0) & (kStageFrames - 1)) == 0) stage(t);
-    step(std::false_type(), t);
+    step(std::false_type(), t, input_at(t));
+  }
+  if (t < core_end) {
+    // the ramp's last comparison is finished here; inside the core every step compares the same
+    // static lane set (cmp_lanes), accumulated per lane and tested once after the loop
+    bad |= __ballot(pend_ck != pend_first) & pend_lanes;
+    pend_ck = pend_first = 0;
+    pend_lanes = cmp_lanes;
   }
   while (t < core_end) {
     const int32_t rel = t - p.f0;
     if ((rel & (kStageFrames - 1)) == 0) stage(t);
     const int32_t chunk_end = min(core_end, t + (kStageFrames - (rel & (kStageFrames - 1))));
-    for (; t < chunk_end; ++t) step(std::true_type(), t);
+    // two steps per iteration; each step's input byte is read one step ahead through a pointer
+    // that advances a row per step (the read past the chunk's last step lands in the slack row
+    // and is discarded)
+    uint32_t ip = (uint32_t)((t - p.f0) & (kStageFrames - 1)) * (uint32_t)row + in_at;
+    uint32_t in = lds_in[ip];
+    for (; t + 1 < chunk_end; t += 2) {
+      const uint32_t in1 = lds_in[ip + row];
+      step(std::true_type(), t, in);
+      ip += 2 * row;
+      in = lds_in[ip];
+      step(std::true_type(), t + 1, in1);
+    }
+    if (t < chunk_end) {
+      step(std::true_type(), t, in);
+      ++t;
+    }
   }
+  bad |= __ballot(acc != 0) & cmp_lanes;
   for (; t < t_end; ++t) {
     if (((t - p.f0) & (kStageFrames - 1)) == 0) stage(t);
-    step(std::false_type(), t);
+    step(std::false_type(), t, input_at(t));
   }
   bad |= __ballot(pend_ck != pend_first) & pend_lanes;
   if (bad && wl == __builtin_ctzll(bad)) atomicCAS(p.fail_f0, -1, p.f0);
@@ -1067,7 +1121,7 @@ int ggrs_engine_destroy(ggrs_engine_t* e) {
   (void)hipSetDevice(e->cfg.device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   void* bufs[] = {e->arena, e->shadow, e->fail_f0, e->inputs, e->lane_status,
-                  e->mis_frame, e->mis_mask, e->trace, e->staging};
+                  e->mis_frame, e->mis_mask, e->staging};  // trace lives in the arena allocation
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   for (hipEvent_t ev : e->tev) (void)hipEventDestroy(ev);
@@ -1125,7 +1179,11 @@ int ggrs_engine_create(const ggrs_config_t* cfg, ggrs_engine_t** out) {
     const size_t b_ring = up16(sizeof(uint32_t) * (size_t)e->R * e->F * L);
     const size_t b_ck = up16(sizeof(uint16_t) * (size_t)e->R * L);
     e->arena_bytes = b_cur + b_ring + 2 * b_ck;
-    CTRY(hipMalloc(&e->arena, e->arena_bytes));
+    // the display-checksum trace follows the arena in the same allocation (outside the checkpointed
+    // range): the v4 kernel's stores then all go through one buffer descriptor
+    const size_t b_trace = c.trace_capacity > 0 ? up16(sizeof(uint16_t) * (size_t)c.trace_capacity * L) : 0;
+    CTRY(hipMalloc(&e->arena, e->arena_bytes + b_trace));
+    if (b_trace) e->trace = (uint16_t*)(e->arena + e->arena_bytes);
     CTRY(hipMalloc(&e->shadow, e->arena_bytes));
     CTRY(hipMemsetAsync(e->arena, 0, e->arena_bytes, e->stream));
     e->cur = (uint32_t*)e->arena;
@@ -1139,7 +1197,6 @@ int ggrs_engine_create(const ggrs_config_t* cfg, ggrs_engine_t** out) {
   CTRY(hipMalloc(&e->lane_status, sizeof(int32_t) * L));
   CTRY(hipMalloc(&e->mis_frame, sizeof(int32_t) * L));
   CTRY(hipMalloc(&e->mis_mask, sizeof(uint64_t) * L));
-  if (c.trace_capacity > 0) CTRY(hipMalloc(&e->trace, sizeof(uint16_t) * (size_t)c.trace_capacity * L));
   // default input (Input::default(), inp = 0) for every queue frame, covering frames < delay
   CTRY(hipMemsetAsync(e->inputs, 0, (size_t)e->cap * L * e->Pp, e->stream));
   CTRY(hipMemsetAsync(e->lane_status, 0, sizeof(int32_t) * L, e->stream));
@@ -1282,7 +1339,10 @@ static int launch_pipelined(ggrs_engine_t* e, int32_t f0, int32_t n) {
                        (uint64_t)2 * p.L * (uint64_t)std::max(p.trace_cap, 0) < kOob;
   // v4 addresses ring, ring_ck and first_ck from the ring's base (one descriptor)
   const bool fits_v4 = fits_v3 && (uint8_t*)e->ring_ck > (uint8_t*)e->ring && (uint8_t*)e->first_ck > (uint8_t*)e->ring_ck &&
-                       (uint64_t)((uint8_t*)e->first_ck - (uint8_t*)e->ring) + (uint64_t)2 * p.L * p.R < kOob;
+                       (uint64_t)((uint8_t*)e->first_ck - (uint8_t*)e->ring) + (uint64_t)2 * p.L * p.R < kOob &&
+                       (!e->trace || ((uint8_t*)e->trace > (uint8_t*)e->first_ck &&
+                                      (uint64_t)((uint8_t*)e->trace - (uint8_t*)e->ring) +
+                                              (uint64_t)2 * p.L * p.trace_cap < kOob));
   if ((e->path == GGRS_PATH_PIPELINED || e->path == GGRS_PATH_PIPELINED_V4_DPP) && p.K * Pp <= kWave && fits_v4) {
     p.spw = kWave / (p.K * Pp);
     const int64_t grid = grid_of(p.L, p.spw);
