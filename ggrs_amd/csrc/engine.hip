@@ -893,7 +893,11 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
       for (int q = 0; q < 5; q++) __builtin_amdgcn_raw_buffer_store_b32(w[q], rs_ring, fo[q], so, 0);
       __builtin_amdgcn_raw_buffer_store_b32(frame1, rs_ring, fo_frame, so, 0);
 #endif
-#ifndef GGRS_EXP_NO_CK_STORES
+#if defined(GGRS_EXP_CK32)
+      __builtin_amdgcn_raw_buffer_store_b32(ck, rs_ring, co & ~3u, cso, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(ck, rs_ring, co_first & ~3u, cso, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(ck, rs_ring, co_trace & ~3u, stu * ck_slot_bytes, 0);
+#elif !defined(GGRS_EXP_NO_CK_STORES)
       __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ring, co, cso, 0);
       __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ring, co_first, cso, 0);
       __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ring, co_trace, stu * ck_slot_bytes, 0);
@@ -966,6 +970,9 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
     step(std::false_type(), t, input_at(t));
   }
   bad |= __ballot(pend_ck != pend_first) & pend_lanes;
+#ifdef GGRS_EXP_CK32
+  bad = 0;  // timing experiment: the checksum rows hold garbage
+#endif
   if (bad && wl == __builtin_ctzll(bad)) atomicCAS(p.fail_f0, -1, p.f0);
 }
 
