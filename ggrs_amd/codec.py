@@ -81,8 +81,17 @@ def decode(ref, packets, lengths, max_inputs):
     return out, cnt, st
 
 
+KERNEL_FORMS = {"default": 0, "direct": 1, "staged": 2}
+
+
 def set_direct(on):
-    """Force the direct (unstaged) kernels; False restores the LDS-staged default."""
+    """Force the direct (unstaged) thread-per-packet kernels; False restores the default."""
+    set_kernels("direct" if on else "default")
+
+
+def set_kernels(form):
+    """Kernel form for later calls: "default" (lane-cooperative where W*B <= 64, else LDS-staged),
+    "direct" or "staged" (thread-per-packet forms)."""
     L = _lib.lib()
     _bind(L)
-    _lib.check(L.ggrs_codec_set_direct(int(bool(on))))
+    _lib.check(L.ggrs_codec_set_direct(KERNEL_FORMS[form]))

@@ -30,7 +30,7 @@ using namespace ggrs;
 namespace {
 
 constexpr int64_t kMaxDecoded = 1 << 24;  // oracle/codec.c CODEC_MAX_DECODED
-bool g_codec_direct = false;  // ggrs_codec_set_direct: force the direct (unstaged) kernels
+int g_codec_mode = 0;  // ggrs_codec_set_direct: 0 default, 1 direct, 2 staged thread-per-packet
 
 struct EncodeParams {
   const uint8_t* ref;
@@ -461,6 +461,343 @@ __global__ __launch_bounds__(256) void decode_lds_kernel(DecodeParams p) {
   lds_to_block(p.out + pk0 * (int64_t)W * B, l_out, out_pitch, np, W * B);
 }
 
+// ------------------------------------------------------------------------------------------
+// Run-level forms (the default for input_bytes 1, 2 or 4 and W*B <= 64 whole dwords): still one
+// thread per packet, but the delta stream lives in registers as NDW dwords and the RLE works
+// run by run instead of byte by byte:
+//   encode: the XOR delta is formed a dword at a time (v_alignbyte for the B-byte shift), bytes
+//           equal to 0x00 / 0xFF become two 64-bit masks (SWAR zero-byte test), run starts are
+//           the class changes of those masks, and each run is one header plus, for a literal
+//           stretch, a byte copy out of an LDS scratch row;
+//   decode: the packet is validated by the same checks in the same order as the other forms,
+//           the runs are expanded into an LDS scratch row, and the delta chain (input k XOR input
+//           k-1) is a prefix XOR of stride B done on whole dwords in registers.
+// Rows move between HBM and LDS whole (block_to_lds / lds_to_block), as in the staged forms.
+
+// one bit per byte of v that is zero (bit k for byte k)
+__device__ inline uint32_t zero_byte_bits(uint32_t v) {
+  const uint32_t t = ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v) & 0x80808080u;
+  return ((t >> 7) * 0x00204081u) >> 21 & 0xFu;
+}
+
+__device__ inline uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t shift) {
+  return __builtin_amdgcn_alignbyte(hi, lo, shift);
+}
+
+// bincode + bitfield-rle validation of one packet (compression.rs:83-154), the checks of
+// decode_kernel in the same order.  On GGRS_CODEC_OK: *cnt inputs, the RLE stream at d + *rle_at
+// with *m bytes.
+__device__ inline int32_t validate_packet(const uint8_t* d, int64_t len, int stride, int B, int W, int64_t* cnt_out,
+                                          uint64_t* m_out, int64_t* rle_at) {
+  if (len < 0 || len > stride) return GGRS_CODEC_E_INVALID;
+  int64_t pos = 0;
+  if (len < 1 || d[0] > 1) return GGRS_CODEC_E_BINCODE;
+  const uint8_t tag = d[pos++];
+  uint64_t n_sizes = 0;
+  int64_t sizes_at = 0;
+  if (tag == 1) {
+    if (len - pos < 8) return GGRS_CODEC_E_BINCODE;
+    for (int b = 0; b < 8; b++) n_sizes |= (uint64_t)d[pos + b] << (8 * b);
+    pos += 8;
+    if (n_sizes > (uint64_t)(len - pos) / 4) return GGRS_CODEC_E_BINCODE;
+    sizes_at = pos;
+    pos += 4 * (int64_t)n_sizes;
+  }
+  if (len - pos < 8) return GGRS_CODEC_E_BINCODE;
+  uint64_t m = 0;
+  for (int b = 0; b < 8; b++) m |= (uint64_t)d[pos + b] << (8 * b);
+  pos += 8;
+  if (m > (uint64_t)(len - pos)) return GGRS_CODEC_E_BINCODE;
+  const uint8_t* rle = d + pos;
+  int64_t xl = 0;
+  for (int64_t q = 0; q < (int64_t)m;) {
+    uint64_t h;
+    if (!get_varint(rle, (int64_t)m, q, h)) return GGRS_CODEC_E_RLE;
+    const uint64_t rl = (h & 1) ? h >> 2 : h >> 1;
+    if (rl > (uint64_t)kMaxDecoded || (uint64_t)xl + rl > (uint64_t)kMaxDecoded) return GGRS_CODEC_E_RLE;
+    if (!(h & 1)) {
+      if ((uint64_t)((int64_t)m - q) < rl) return GGRS_CODEC_E_RLE;
+      q += (int64_t)rl;
+    }
+    xl += (int64_t)rl;
+  }
+  int64_t cnt;
+  bool all_b = true;
+  if (tag == 1) {
+    cnt = (int64_t)n_sizes;
+    int64_t bs = B, sum = 0;
+    for (int64_t k = 0; k < cnt; k++) {
+      uint32_t u = 0;
+      for (int b = 0; b < 4; b++) u |= (uint32_t)d[sizes_at + 4 * k + b] << (8 * b);
+      const int64_t sz = (int64_t)(int32_t)((uint32_t)bs + u);
+      if (sz < 0) return GGRS_CODEC_E_DELTA;
+      all_b &= sz == B;
+      bs = sz;
+      sum += sz;
+      if (sum > xl) return GGRS_CODEC_E_DELTA;
+    }
+    if (sum != xl) return GGRS_CODEC_E_DELTA;
+  } else {
+    cnt = xl / B;
+    if (cnt * B != xl) return GGRS_CODEC_E_DELTA;
+  }
+  if (!all_b) return GGRS_CODEC_UNSUPPORTED;
+  if (cnt > W) return GGRS_CODEC_E_CAP;
+  *cnt_out = cnt;
+  *m_out = m;
+  *rle_at = pos;
+  return GGRS_CODEC_OK;
+}
+
+// row pitches of the run-level forms: rows long enough for any run layout of <= 4*NDW bytes
+// (alternating one-byte runs: 9 + 3 * 4 * NDW), so a packet too long for the stride is measured
+// in its own row and then reported as GGRS_CODEC_E_CAP
+__host__ __device__ inline int swar_out_pitch(int stride, int ndw) {
+  return odd_dword_pitch(stride > 9 + 12 * ndw ? stride : 9 + 12 * ndw);
+}
+
+template <int B, int NDW>
+__global__ __launch_bounds__(256) void encode_swar_kernel(EncodeParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int T = blockDim.x, W = p.W, WB = W * B, stride = p.stride;
+  const int out_pitch = swar_out_pitch(stride, NDW), x_pitch = odd_dword_pitch(4 * NDW);
+  uint8_t* l_out = smem;                    // [T][out_pitch]
+  uint8_t* l_x = l_out + T * out_pitch;     // [T][x_pitch] delta bytes, for literal copies
+  const int64_t pk0 = (int64_t)blockIdx.x * T;
+  const int np = (int)((p.N - pk0) < T ? (p.N - pk0) : T);
+  for (int q = threadIdx.x; q < np * out_pitch / 4; q += T) reinterpret_cast<uint32_t*>(l_out)[q] = 0;
+  const int t = threadIdx.x;
+  const int64_t pk = pk0 + t;
+  uint32_t cw[NDW], xw[NDW];
+  int32_t n = 0;
+  uint32_t rw = 0;
+  if (t < np) {
+    n = p.count[pk];
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(p.pending + pk * WB);
+#pragma unroll
+    for (int k = 0; k < NDW; k++) cw[k] = 4 * k < WB ? src[k] : 0u;
+#pragma unroll
+    for (int b = 0; b < B; b++) rw |= (uint32_t)p.ref[pk * B + b] << (8 * b);
+  }
+  // delta stream: input k XOR input k-1 (the first against the reference), a dword at a time
+#pragma unroll
+  for (int k = 0; k < NDW; k++) {
+    uint32_t prev;
+    if constexpr (B == 4) prev = k == 0 ? rw : cw[k - 1];
+    else prev = alignbyte(cw[k], k == 0 ? rw << (8 * (4 - B)) : cw[k - 1], 4 - B);
+    xw[k] = cw[k] ^ prev;
+  }
+  __syncthreads();  // output rows zeroed
+  if (t < np) {
+    int32_t code;
+    if (n < 0 || n > W) {
+      code = GGRS_CODEC_E_INVALID;
+    } else {
+      const int L = n * B;
+      uint64_t zm = 0, fm = 0;
+      uint32_t* xrow = reinterpret_cast<uint32_t*>(l_x + t * x_pitch);
+#pragma unroll
+      for (int k = 0; k < NDW; k++) {
+        zm |= (uint64_t)zero_byte_bits(xw[k]) << (4 * k);
+        fm |= (uint64_t)zero_byte_bits(~xw[k]) << (4 * k);
+        xrow[k] = xw[k];
+      }
+      const uint64_t valid = L >= 64 ? ~0ull : ((1ull << L) - 1);
+      zm &= valid;
+      fm &= valid;
+      // a run starts where the class (0x00 / 0xFF / literal) changes
+      uint64_t starts = ((zm ^ (zm << 1)) | (fm ^ (fm << 1)) | 1ull) & valid;
+      uint8_t* o = l_out + t * out_pitch;
+      const uint8_t* xb = l_x + t * x_pitch;
+      int pos = 9;
+      while (starts) {
+        const int i = (int)__builtin_ctzll(starts);
+        starts &= starts - 1;
+        const int nx = starts ? (int)__builtin_ctzll(starts) : L;
+        const uint32_t len = (uint32_t)(nx - i);
+        const bool fill = ((zm | fm) >> i) & 1;
+        const uint32_t h = fill ? (len << 2) | (uint32_t)((fm >> i) & 1) << 1 | 1u : len << 1;  // < 2^14
+        o[pos++] = (uint8_t)((h & 0x7fu) | (h >= 0x80u ? 0x80u : 0u));
+        if (h >= 0x80u) o[pos++] = (uint8_t)(h >> 7);
+        if (!fill)
+          for (int q = i; q < nx; q++) o[pos++] = xb[q];
+      }
+      const int rle = pos - 9;
+      code = pos > stride ? GGRS_CODEC_E_CAP : pos;
+      if (code > 0) {
+        o[0] = 0;  // input_sizes: None, then the u64 length of encoded_bytes
+        for (int b = 0; b < 8; b++) o[1 + b] = b < 4 ? (uint8_t)((uint32_t)rle >> (8 * b)) : 0;
+      } else {
+        for (int q = 0; q < pos; q++) o[q] = 0;  // an error row is stored as zeros
+      }
+    }
+    p.out_len[pk] = code;
+  }
+  __syncthreads();
+  lds_to_block(p.out + pk0 * stride, l_out, out_pitch, np, stride);
+}
+
+template <int B, int NDW>
+__global__ __launch_bounds__(256) void decode_swar_kernel(DecodeParams p) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int T = blockDim.x, W = p.W, WB = W * B, stride = p.stride;
+  const int in_pitch = odd_dword_pitch(stride), x_pitch = odd_dword_pitch(4 * NDW);
+  const int out_pitch = odd_dword_pitch(WB);
+  uint8_t* l_in = smem;                     // [T][in_pitch] packets
+  uint8_t* l_x = l_in + T * in_pitch;       // [T][x_pitch] expanded runs
+  uint8_t* l_out = l_x + T * x_pitch;       // [T][out_pitch] decoded inputs
+  const int64_t pk0 = (int64_t)blockIdx.x * T;
+  const int np = (int)((p.N - pk0) < T ? (p.N - pk0) : T);
+  block_to_lds(l_in, in_pitch, p.packets + pk0 * stride, np, stride);
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < np) {
+    const int64_t pk = pk0 + t;
+    const uint8_t* d = l_in + t * in_pitch;
+    constexpr int kCap = 4 * NDW;  // scratch bytes: any valid packet expands to <= W * B of them
+    uint8_t* xb = l_x + t * x_pitch;
+    uint32_t* xr32 = reinterpret_cast<uint32_t*>(xb);
+#pragma unroll
+    for (int k = 0; k < NDW; k++) xr32[k] = 0;  // 0x00 runs need no writes
+    const int64_t len = p.len[pk];
+    int64_t cnt = 0;
+    int32_t status = GGRS_CODEC_OK;
+    if (len < 0 || len > stride || len < 1 || d[0] != 0) {
+      // a length outside the row, or input_sizes = Some(..) (or a bad tag): the general checks
+      // (validate_packet, the same order as decode_kernel), then the runs are expanded
+      int64_t rle_at = 0;
+      uint64_t m = 0;
+      status = validate_packet(d, len, stride, B, W, &cnt, &m, &rle_at);
+      if (status == GGRS_CODEC_OK) {
+        const uint8_t* rle = d + rle_at;
+        int at = 0;
+        for (int64_t q = 0; q < (int64_t)m;) {
+          uint64_t h;
+          get_varint(rle, (int64_t)m, q, h);
+          const int rl = (int)((h & 1) ? h >> 2 : h >> 1);
+          if (h & 1) {
+            if (h & 2)
+              for (int k = 0; k < rl; k++) xb[at + k] = 0xFF;
+          } else {
+            for (int k = 0; k < rl; k++) xb[at + k] = rle[q + k];
+            q += rl;
+          }
+          at += rl;
+        }
+      }
+    } else {
+      // input_sizes = None, the packet GGRS sends: the checks of decode_kernel in the same order,
+      // with the runs expanded during the measuring pass (bytes past kCap are never kept: such a
+      // packet fails with E_CAP or E_DELTA below)
+      const uint32_t* dw = reinterpret_cast<const uint32_t*>(d);
+      if (len - 1 < 8) {
+        status = GGRS_CODEC_E_BINCODE;
+      } else {
+        const uint32_t w0 = dw[0], w1 = dw[1], w2 = dw[2];
+        const uint64_t m = (uint64_t)alignbyte(w1, w0, 1) | (uint64_t)alignbyte(w2, w1, 1) << 32;
+        if (m > (uint64_t)(len - 9)) {
+          status = GGRS_CODEC_E_BINCODE;
+        } else {
+          const uint8_t* rle = d + 9;
+          int64_t xl = 0;
+          for (int64_t q = 0; q < (int64_t)m;) {
+            uint64_t h;
+            if (!get_varint(rle, (int64_t)m, q, h)) { status = GGRS_CODEC_E_RLE; break; }
+            const uint64_t rl = (h & 1) ? h >> 2 : h >> 1;
+            if (rl > (uint64_t)kMaxDecoded || (uint64_t)xl + rl > (uint64_t)kMaxDecoded) { status = GGRS_CODEC_E_RLE; break; }
+            const bool fits = xl + (int64_t)rl <= kCap;
+            if (!(h & 1)) {
+              if ((uint64_t)((int64_t)m - q) < rl) { status = GGRS_CODEC_E_RLE; break; }
+              if (fits)
+                for (int k = 0; k < (int)rl; k++) xb[xl + k] = rle[q + k];
+              q += (int64_t)rl;
+            } else if ((h & 2) && fits) {
+              for (int k = 0; k < (int)rl; k++) xb[xl + k] = 0xFF;
+            }
+            xl += (int64_t)rl;
+          }
+          if (status == GGRS_CODEC_OK) {
+            cnt = xl / B;
+            if (cnt * B != xl) status = GGRS_CODEC_E_DELTA;
+            else if (cnt > W) status = GGRS_CODEC_E_CAP;
+          }
+        }
+      }
+    }
+    uint32_t* orow = reinterpret_cast<uint32_t*>(l_out + t * out_pitch);
+    if (status == GGRS_CODEC_OK) {
+      const int xl = (int)cnt * B;
+      uint32_t rw = 0;
+#pragma unroll
+      for (int b = 0; b < B; b++) rw |= (uint32_t)p.ref[pk * B + b] << (8 * b);
+      const uint32_t refpat = B == 1 ? rw * 0x01010101u : (B == 2 ? rw * 0x00010001u : rw);
+      const uint32_t* xr = xr32;
+      uint32_t carry = 0;  // the previous dword's last input, repeated
+#pragma unroll
+      for (int k = 0; k < NDW; k++) {
+        if (4 * k >= WB) break;
+        const int live_bytes = xl - 4 * k;
+        const uint32_t keep = live_bytes >= 4 ? 0xFFFFFFFFu : (live_bytes <= 0 ? 0u : (1u << (8 * live_bytes)) - 1u);
+        uint32_t y = xr[k] & keep;
+        // prefix XOR of stride B inside the dword, then the carry from the dwords before
+        if constexpr (B == 1) {
+          y ^= y << 8;
+          y ^= y << 16;
+        } else if constexpr (B == 2) {
+          y ^= y << 16;
+        }
+        y ^= carry;
+        carry = B == 1 ? (y >> 24) * 0x01010101u : (B == 2 ? (y >> 16) * 0x00010001u : y);
+        orow[k] = (y ^ refpat) & keep;
+      }
+      p.count[pk] = (int32_t)cnt;
+    } else {
+      for (int k = 0; k < WB / 4; k++) orow[k] = 0;
+      p.count[pk] = 0;
+    }
+    p.status[pk] = status;
+  }
+  __syncthreads();
+  lds_to_block(p.out + pk0 * (int64_t)WB, l_out, out_pitch, np, WB);
+}
+
+size_t encode_swar_bytes(int ndw, int stride) {
+  return (size_t)256 * (swar_out_pitch(stride, ndw) + odd_dword_pitch(4 * ndw));
+}
+size_t decode_swar_bytes(int ndw, int B, int W, int stride) {
+  return (size_t)256 * (odd_dword_pitch(stride) + odd_dword_pitch(4 * ndw) + odd_dword_pitch(W * B));
+}
+// dwords of the run-level forms' register stream (a power of two >= W*B/4), or 0 when they do
+// not apply
+int swar_ndw(int B, int W, int stride) {
+  const int WB = W * B;
+  if ((B != 1 && B != 2 && B != 4) || WB <= 0 || WB > 64 || WB % 4 || stride % 4) return 0;
+  int n = 1;
+  while (4 * n < WB) n <<= 1;
+  return n;
+}
+
+template <int B>
+void launch_encode_swar(int ndw, int64_t grid, size_t lds, hipStream_t s, const EncodeParams& p) {
+  switch (ndw) {
+    case 1: encode_swar_kernel<B, 1><<<grid, 256, lds, s>>>(p); break;
+    case 2: encode_swar_kernel<B, 2><<<grid, 256, lds, s>>>(p); break;
+    case 4: encode_swar_kernel<B, 4><<<grid, 256, lds, s>>>(p); break;
+    case 8: encode_swar_kernel<B, 8><<<grid, 256, lds, s>>>(p); break;
+    default: encode_swar_kernel<B, 16><<<grid, 256, lds, s>>>(p); break;
+  }
+}
+template <int B>
+void launch_decode_swar(int ndw, int64_t grid, size_t lds, hipStream_t s, const DecodeParams& p) {
+  switch (ndw) {
+    case 1: decode_swar_kernel<B, 1><<<grid, 256, lds, s>>>(p); break;
+    case 2: decode_swar_kernel<B, 2><<<grid, 256, lds, s>>>(p); break;
+    case 4: decode_swar_kernel<B, 4><<<grid, 256, lds, s>>>(p); break;
+    case 8: decode_swar_kernel<B, 8><<<grid, 256, lds, s>>>(p); break;
+    default: decode_swar_kernel<B, 16><<<grid, 256, lds, s>>>(p); break;
+  }
+}
+
 // LDS bytes for a block of T threads, or 0 when the staged form does not apply
 size_t encode_lds_bytes(int T, int B, int W, int stride) {
   if ((W * B) % 4 || stride % 4 || W * B == 0) return 0;
@@ -485,8 +822,19 @@ int ggrs_codec_encode(const uint8_t* ref, const uint8_t* pending, const int32_t*
   if (n_packets == 0) return GGRS_OK;
   if (!ref || !pending || !count || !out || !out_len) return set_error(GGRS_E_INVALID, "null argument");
   EncodeParams p{ref, pending, count, out, out_len, n_packets, input_bytes, max_inputs, out_stride};
+  const int ndw = swar_ndw(input_bytes, max_inputs, out_stride);
+  const bool al = aligned4(pending) && aligned4(out);
+  if (g_codec_mode == 0 && ndw && al && encode_swar_bytes(ndw, out_stride) <= kLdsBudget) {
+    const size_t lds = encode_swar_bytes(ndw, out_stride);
+    const int64_t grid = grid_of(n_packets, 256);
+    if (input_bytes == 1) launch_encode_swar<1>(ndw, grid, lds, (hipStream_t)stream, p);
+    else if (input_bytes == 2) launch_encode_swar<2>(ndw, grid, lds, (hipStream_t)stream, p);
+    else launch_encode_swar<4>(ndw, grid, lds, (hipStream_t)stream, p);
+    HIP_TRY(hipGetLastError());
+    return GGRS_OK;
+  }
   const size_t lds = encode_lds_bytes(256, input_bytes, max_inputs, out_stride);
-  if (lds && lds <= kLdsBudget && aligned4(pending) && aligned4(out) && !g_codec_direct)
+  if (lds && lds <= kLdsBudget && al && g_codec_mode != 1)
     encode_lds_kernel<<<grid_of(n_packets, 256), 256, lds, (hipStream_t)stream>>>(p);
   else
     encode_kernel<<<grid_of(n_packets, 256), 256, 0, (hipStream_t)stream>>>(p);
@@ -502,8 +850,19 @@ int ggrs_codec_decode(const uint8_t* ref, const uint8_t* packets, const int32_t*
   if (n_packets == 0) return GGRS_OK;
   if (!ref || !packets || !packet_len || !out || !count || !status) return set_error(GGRS_E_INVALID, "null argument");
   DecodeParams p{ref, packets, packet_len, out, count, status, n_packets, input_bytes, max_inputs, packet_stride};
+  const int ndw = swar_ndw(input_bytes, max_inputs, packet_stride);
+  const bool al = aligned4(packets) && aligned4(out);
+  if (g_codec_mode == 0 && ndw && al && decode_swar_bytes(ndw, input_bytes, max_inputs, packet_stride) <= kLdsBudget) {
+    const size_t lds = decode_swar_bytes(ndw, input_bytes, max_inputs, packet_stride);
+    const int64_t grid = grid_of(n_packets, 256);
+    if (input_bytes == 1) launch_decode_swar<1>(ndw, grid, lds, (hipStream_t)stream, p);
+    else if (input_bytes == 2) launch_decode_swar<2>(ndw, grid, lds, (hipStream_t)stream, p);
+    else launch_decode_swar<4>(ndw, grid, lds, (hipStream_t)stream, p);
+    HIP_TRY(hipGetLastError());
+    return GGRS_OK;
+  }
   const size_t lds = decode_lds_bytes(256, input_bytes, max_inputs, packet_stride);
-  if (lds && lds <= kLdsBudget && aligned4(packets) && aligned4(out) && !g_codec_direct)
+  if (lds && lds <= kLdsBudget && al && g_codec_mode != 1)
     decode_lds_kernel<<<grid_of(n_packets, 256), 256, lds, (hipStream_t)stream>>>(p);
   else
     decode_kernel<<<grid_of(n_packets, 256), 256, 0, (hipStream_t)stream>>>(p);
@@ -520,8 +879,9 @@ int32_t ggrs_codec_max_packet_bytes(int32_t input_bytes, int32_t max_inputs) {
   return v > 0x7fffffff ? -1 : (int32_t)v;
 }
 
-int ggrs_codec_set_direct(int32_t on) {
-  g_codec_direct = on != 0;
+int ggrs_codec_set_direct(int32_t mode) {
+  if (mode < 0 || mode > 2) return set_error(GGRS_E_INVALID, "codec mode %d (0 default, 1 direct, 2 staged)", mode);
+  g_codec_mode = mode;
   return GGRS_OK;
 }
 

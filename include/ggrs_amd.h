@@ -358,9 +358,11 @@ int ggrs_codec_decode(const uint8_t* ref, const uint8_t* packets, const int32_t*
                       int32_t* status, void* stream);
 /* an out_stride that every packet of max_inputs inputs fits (a multiple of 16) */
 int32_t ggrs_codec_max_packet_bytes(int32_t input_bytes, int32_t max_inputs);
-/* on != 0: use the direct per-thread kernels even where the LDS-staged ones apply (for tests and
- * comparison; process-wide) */
-int ggrs_codec_set_direct(int32_t on);
+/* kernel forms (for tests and comparison; process-wide): 0 = default (lane-cooperative where
+ * max_inputs * input_bytes <= 64 and rows are whole dwords, else thread-per-packet LDS-staged where
+ * rows are whole dwords, else direct), 1 = direct thread-per-packet, 2 = thread-per-packet
+ * LDS-staged where it applies */
+int ggrs_codec_set_direct(int32_t mode);
 
 #ifdef __cplusplus
 }

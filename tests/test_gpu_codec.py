@@ -28,17 +28,22 @@ def gpu(a):
     return torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
 
-@pytest.fixture(params=["staged", "direct"])
+@pytest.fixture(params=["default", "staged", "direct"])
 def kernels(request):
-    """Both kernel forms: LDS-staged (default where rows are whole dwords) and direct."""
+    """Every kernel form: default (lane-cooperative where W*B <= 64 and rows are whole dwords),
+    thread-per-packet LDS-staged, and direct."""
     from ggrs_amd import codec
-    codec.set_direct(request.param == "direct")
+    codec.set_kernels(request.param)
     yield request.param
-    codec.set_direct(False)
+    codec.set_kernels("default")
 
 
+# W*B: 8, 32 (lane-cooperative segments of 8 / 32 lanes), 132, 128 (thread-per-packet staged), 7
+# (direct); then 16 (the bench shape), 64, 4, 12 (segments of 16 / 64 / 4 / 16 lanes)
 @pytest.mark.parametrize("N,W,B,held", [(5000, 8, 1, True), (3000, 16, 2, False), (2000, 33, 4, False),
-                                         (1000, 128, 1, True), (257, 1, 7, False)])
+                                         (1000, 128, 1, True), (257, 1, 7, False), (4000, 8, 2, True),
+                                         (3000, 16, 4, True), (2000, 4, 1, False), (2000, 12, 1, True),
+                                         (999, 3, 4, False), (1500, 64, 1, True)])
 def test_encode_matches_oracle_and_round_trips(oracle, kernels, N, W, B, held):
     from ggrs_amd import codec
     rng = np.random.default_rng(N + W + B)
@@ -106,3 +111,27 @@ def test_hostile_packets_match_oracle(oracle, kernels, mode):
             assert st[p] != codec.UNSUPPORTED or any(len(x) != B for x in want)
             assert st[p] != codec.E_CAP or len(want) > W
     assert len(seen) >= 2
+
+
+@pytest.mark.parametrize("W,B", [(8, 2), (16, 4), (33, 4), (1, 7)])
+def test_encode_errors(oracle, kernels, W, B):
+    """count outside 0..W -> E_INVALID; a stride too small for the packet -> E_CAP; every other
+    packet of the batch still matches the oracle."""
+    from ggrs_amd import codec
+    rng = np.random.default_rng(W * 31 + B)
+    N = 600
+    ref, pend, count = batch(rng, N, W, B, False)
+    count[::7] = -1
+    count[3::11] = W + 1
+    stride = 12 if (W * B) % 4 == 0 else 13  # a few bytes of runs fit, longer packets do not
+    out, ln = codec.encode(gpu(ref), gpu(pend), gpu(count), stride=stride)
+    out, ln = out.cpu().numpy(), ln.cpu().numpy()
+    for p in range(N):
+        if count[p] < 0 or count[p] > W:
+            assert ln[p] == codec.E_INVALID, p
+            continue
+        want = oracle.codec_encode(ref[p].tobytes(), [pend[p, k].tobytes() for k in range(count[p])])
+        if len(want) > stride:
+            assert ln[p] == codec.E_CAP, p
+        else:
+            assert ln[p] == len(want) and out[p, :ln[p]].tobytes() == want, p
