@@ -280,6 +280,7 @@ def run_p2p(args):
     rows = synth.gen_inputs(rank * S, S, frames, P, synth.MODEL_HELD)
     eng = P2PEngine(S, num_players=P, local_players=(0,), input_delay=0, max_prediction=maxp,
                     remote_latency=D, input_capacity=frames + D + 2, device=local_rank)
+    eng.set_kernel_form(args.p2p_form)
     eng.add_inputs(0, rows)
     eng.synchronize()
     for _ in range(args.warmup):
@@ -503,6 +504,8 @@ def main():
     ap.add_argument("--peers", action="store_true",
                     help="configs 3/4: rank r and r + world/2 replay the same sessions (the two "
                          "machines of a match) and compare checksums after each all-gather")
+    ap.add_argument("--p2p-form", choices=["flat", "lockstep", "unstaged"], default="flat",
+                    help="p2p: kernel form (DESIGN.md section 3)")
     ap.add_argument("--workload", choices=["synctest", "p2p", "codec"], default="synctest",
                     help="p2p: the device P2P rollback decision (SURVEY.md 8f), --sessions per GPU")
     args = ap.parse_args()

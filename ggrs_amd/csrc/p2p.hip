@@ -319,6 +319,172 @@ __global__ __launch_bounds__(kP2PBlock) void p2p_kernel(P2PParams p) {
   if (p.sparse) p.last_saved[sess] = last_saved;
 }
 
+// Flattened form (the default without sparse saving): each thread runs its own session's calls
+// as a sequence of steps -- one save + one AdvanceFrame per step, a rollback call taking
+// f - first_incorrect replay steps before its own -- instead of the calls in lockstep.  In
+// lockstep a wave pays a rollback whenever any of its 64 sessions mispredicted (almost every
+// call), so every call cost ~D + 1 advances for every session; here a session that did not roll
+// back goes on to its next call meanwhile, and a wave's step count is the largest per-session
+// count (calls + replays) of a stage.  Same Loads, Saves, AdvanceFrames and InputQueue updates per
+// session, in the same order, as p2p_kernel.  One wave per block; input rows staged per stage of
+// calls as in the staged form (rows [stage start - back, stage end)), all lanes meeting at the
+// stage end.
+constexpr int kFlatBlock = 64;
+constexpr size_t kFlatRingBytes = (size_t)28 << 20;  // default form: flat while the ring fits L2
+
+template <int P>
+struct LdsRowsFlat {
+  const uint8_t* lds;  // [kP2PRows][kFlatBlock][Pp]
+  int32_t lo;
+  int tid;
+  __device__ inline uint32_t operator()(int32_t g) const {
+    using T = typename InputWord<P>::T;
+    return (uint32_t)reinterpret_cast<const T*>(lds)[(g - lo) * kFlatBlock + tid];
+  }
+};
+
+template <int P>
+__global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
+  constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
+  __shared__ __attribute__((aligned(16))) uint8_t lds_rows[kP2PRows * kFlatBlock * Pp];
+  const int64_t sess0 = (int64_t)blockIdx.x * kFlatBlock;
+  const int64_t S = p.S;
+  const bool live = sess0 + threadIdx.x < S;
+  const int64_t sess = live ? sess0 + threadIdx.x : sess0;  // idle threads shadow the block's first
+  const int nb = (int)((S - sess0) < kFlatBlock ? (S - sess0) : kFlatBlock);
+  BoxState<P> st;
+  load_state<P>(st, p.cur + sess, S);
+  RemoteQueues<P> q;
+#pragma unroll
+  for (int k = 0; k < P; k++) {
+    q.pred_frame[k] = p.queue[(0 * P + k) * S + sess];
+    q.pred_in[k] = (uint32_t)p.queue[(1 * P + k) * S + sess];
+    q.first_inc[k] = p.queue[(2 * P + k) * S + sess];
+    q.last_req[k] = p.queue[(3 * P + k) * S + sess];
+  }
+  int32_t rollbacks = 0;
+  int64_t resim = 0;
+  const bool dbg = live && sess == p.dbg_sess;
+  const int tid = live ? (int)threadIdx.x : 0;
+  const int32_t back = p.D + p.delay;
+  // the rollback cell of the next call (frame f + 1 - D), read at the end of call f (p2p_kernel)
+  BoxState<P> pre;
+  int32_t pre_frame = kNull;
+  auto prefetch = [&](int32_t fr) {
+    if (fr >= 0) {
+      load_state<P>(pre, p.ring + (int64_t)(fr % p.R) * state_fields(P) * S + sess, S);
+      pre_frame = fr;
+    }
+  };
+  prefetch(p.f0 - p.D);
+  const int32_t f_end = p.f0 + p.n;
+  const int32_t calls_per_stage = kP2PRows - back;  // >= 1 (host)
+  for (int32_t fs = p.f0; fs < f_end;) {
+    const int32_t chunk_end = min(f_end, fs + calls_per_stage);
+    const int32_t lo = max(0, fs - back);
+    {  // stage rows [lo, chunk_end)
+      __syncthreads();
+      const int nrows = chunk_end - lo, row_bytes = nb * Pp;
+      if (nb == kFlatBlock && ((S * Pp) & 15) == 0) {  // whole 16-byte pieces, every load in flight
+        constexpr int kPieces = kFlatBlock * Pp / 16;
+#pragma unroll 4
+        for (int c = threadIdx.x; c < nrows * kPieces; c += kFlatBlock) {
+          const int r = c / kPieces, k = c - r * kPieces;
+          const uint4* src = reinterpret_cast<const uint4*>(p.inputs + ((int64_t)((lo + r) % p.cap) * S + sess0) * Pp);
+          reinterpret_cast<uint4*>(lds_rows + r * kFlatBlock * Pp)[k] = src[k];
+        }
+      } else {
+        for (int c = threadIdx.x; c < nrows * row_bytes; c += kFlatBlock) {
+          const int r = c / row_bytes, b = c - r * row_bytes;
+          lds_rows[r * kFlatBlock * Pp + b] = p.inputs[((int64_t)((lo + r) % p.cap) * S + sess0) * Pp + b];
+        }
+      }
+      __syncthreads();
+    }
+    const LdsRowsFlat<P> rows{lds_rows, lo, tid};
+    int32_t f = fs;              // this session's call
+    bool at_start = true, replaying = false;
+    int32_t h = 0, load = 0, last_added = kNull;
+    while (f < chunk_end) {
+      if (at_start) {
+        // 0. check_checksum_send_interval (as p2p_kernel)
+        if (p.desync_interval > 0 && live) {
+          const int32_t fts = f - 1 - p.D;
+          if (fts >= p.desync_interval && fts % p.desync_interval == 0)
+            p.hist[(int64_t)((fts / p.desync_interval) % kHist) * S + sess] = p.ring_ck[(int64_t)(fts % p.R) * S + sess];
+        }
+        // 1. poll_remote_clients: the remote input of frame g = f - D (add_input_by_frame)
+        const int32_t g = f - p.D;
+        last_added = g >= 0 ? g : kNull;
+        if (g >= 0) {
+          const uint32_t row = rows(g);
+#pragma unroll
+          for (int k = 0; k < P; k++) {
+            if ((p.local_mask >> k) & 1u) continue;
+            if (q.pred_frame[k] != kNull) {
+              const uint32_t v = (row >> (8 * k)) & 0xffu;
+              if (q.first_inc[k] == kNull && q.pred_in[k] != v) q.first_inc[k] = g;
+              if (q.pred_frame[k] == q.last_req[k] && q.first_inc[k] == kNull) q.pred_frame[k] = kNull;
+              else q.pred_frame[k] += 1;
+            }
+          }
+        }
+        // 2. the first frame's save
+        if (f == 0 && live) save_cell<P>(p, st, 0, sess);
+        // 3. check_simulation_consistency: a rollback loads first_incorrect and replays from it
+        int32_t first_inc = kNull;
+#pragma unroll
+        for (int k = 0; k < P; k++)
+          if (q.first_inc[k] != kNull && (first_inc == kNull || q.first_inc[k] < first_inc)) first_inc = q.first_inc[k];
+        if (first_inc != kNull) {
+          load = first_inc;
+          if (load == pre_frame) st = pre;
+          else load_state<P>(st, p.ring + (int64_t)(load % p.R) * state_fields(P) * S + sess, S);
+#pragma unroll
+          for (int k = 0; k < P; k++) {  // reset_prediction (input_queue.rs:63-67)
+            q.pred_frame[k] = kNull;
+            q.first_inc[k] = kNull;
+            q.last_req[k] = kNull;
+          }
+          h = load;
+          replaying = true;  // first_incorrect <= f - D < f
+          rollbacks += 1;
+          resim += f - load;
+        }
+        at_start = false;
+      }
+      // one step: a replayed frame h (saved unless it is the loaded one) or the call's own frame
+      // f (SaveGameState(f), then AdvanceFrame with synchronized_inputs(f))
+      const int32_t fr = replaying ? h : f;
+      const uint32_t in = sync_inputs<P>(p, q, fr, last_added, rows);
+      if (live && (!replaying || h > load)) save_cell<P>(p, st, fr, sess);
+      const uint32_t from = st.w[0];
+      advance_state<P>(st, in, 0u);
+      if (dbg && (int32_t)from == p.dbg_frame) st.w[fld_x(P, 0)] ^= 1u;
+      if (replaying) {
+        if (++h == f) replaying = false;
+      } else {
+        if (p.trace && live) p.trace[(int64_t)(f % p.trace_cap) * S + sess] = fletcher16_state<P>(st);
+        prefetch(f + 1 - p.D);
+        ++f;
+        at_start = true;
+      }
+    }
+    fs = chunk_end;
+  }
+  if (!live) return;
+  store_state<P>(st, p.cur + sess, S);
+#pragma unroll
+  for (int k = 0; k < P; k++) {
+    p.queue[(0 * P + k) * S + sess] = q.pred_frame[k];
+    p.queue[(1 * P + k) * S + sess] = (int32_t)q.pred_in[k];
+    p.queue[(2 * P + k) * S + sess] = q.first_inc[k];
+    p.queue[(3 * P + k) * S + sess] = q.last_req[k];
+  }
+  p.rollbacks[sess] += rollbacks;
+  p.resim[sess] += resim;
+}
+
 // compare_local_checksums_against_peers for one report frame, every session at once: bit s of
 // mask = local[s] != remote[s] (p2p_session.rs:915-926), count = number of set bits.
 __global__ __launch_bounds__(256) void compare_checksums_kernel(const uint16_t* local, const uint16_t* remote, int64_t S,
@@ -366,7 +532,7 @@ struct ggrs_p2p_engine {
   int64_t dbg_sess = -1;
   int32_t dbg_frame = -1;
   int32_t sparse = 0;
-  bool unstaged = false;          // ggrs_p2p_set_unstaged: global input reads (comparison/tests)
+  int32_t form = 0;  // ggrs_p2p_set_unstaged: 0 default (flat), 1 global input reads, 2 lockstep staged
   int32_t* last_saved = nullptr;  // [S], sparse saving only
   int32_t* ring_frame = nullptr;  // [R][S], sparse saving only
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -569,10 +735,18 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
   int rc = p2p_launch_timed(e, [&] {
     // stage input rows in LDS unless a call reaches further back than a stage holds
     const int32_t back = (e->sparse ? e->R - 1 : p.D) + p.delay;
-    const bool staged = back + 1 <= kP2PRows - 1 && !e->unstaged;
+    const bool staged = back + 1 <= kP2PRows - 1 && e->form != 1;
+    // the flat form's waves save into up to R ring slots per store instruction (lanes sit at
+    // different frames): while the ring fits the XCDs' L2 (4 MiB each, sessions spread over the 8)
+    // those partial lines merge there and the flat form wins (1.58e10 vs 1.29e10 session-frames/s
+    // at 65,536 sessions); past it they go out partial and the lockstep form is faster (1.97e10
+    // vs 1.04e10 at 131,072) -- measured on one MI355X, DESIGN.md section 5
+    const size_t ring_bytes = (size_t)e->R * (size_t)p.S * (4u * (size_t)e->F + 2u);
+    const bool flat = staged && !e->sparse && (e->form == 0 ? ring_bytes <= kFlatRingBytes : false);
     dispatch_players(e->cfg.num_players, [&](auto PC) {
       constexpr int P = decltype(PC)::value;
-      if (staged) p2p_kernel<P, true><<<grid_of(p.S, kP2PBlock), kP2PBlock, 0, e->stream>>>(p);
+      if (flat) p2p_flat_kernel<P><<<grid_of(p.S, kFlatBlock), kFlatBlock, 0, e->stream>>>(p);
+      else if (staged) p2p_kernel<P, true><<<grid_of(p.S, kP2PBlock), kP2PBlock, 0, e->stream>>>(p);
       else p2p_kernel<P, false><<<grid_of(p.S, kP2PBlock), kP2PBlock, 0, e->stream>>>(p);
     });
   });
@@ -614,9 +788,10 @@ int ggrs_p2p_set_sparse_saving(ggrs_p2p_engine_t* e, int32_t on) {
   return GGRS_OK;
 }
 
-int ggrs_p2p_set_unstaged(ggrs_p2p_engine_t* e, int32_t on) {
+int ggrs_p2p_set_unstaged(ggrs_p2p_engine_t* e, int32_t form) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
-  e->unstaged = on != 0;
+  if (form < 0 || form > 2) return set_error(GGRS_E_INVALID, "kernel form %d (0 default, 1 unstaged, 2 lockstep)", form);
+  e->form = form;
   return GGRS_OK;
 }
 

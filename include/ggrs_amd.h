@@ -325,8 +325,10 @@ int ggrs_p2p_compare_checksums(ggrs_p2p_engine_t* eng, int32_t frame, const uint
  * (check_last_saved_state :819-843), last_confirmed_frame never passes the last save
  * (sync_layer.rs:323-326).  Part of the configuration: only before the first call. */
 int ggrs_p2p_set_sparse_saving(ggrs_p2p_engine_t* eng, int32_t on);
-/* on != 0: read input rows from global memory instead of the per-block LDS stage (comparison) */
-int ggrs_p2p_set_unstaged(ggrs_p2p_engine_t* eng, int32_t on);
+/* kernel form (comparison and tests): 0 = default (each session's calls flattened into its own
+ * step sequence, input rows staged in LDS; sparse saving runs the lockstep form), 1 = calls in
+ * lockstep with input rows read from global memory, 2 = calls in lockstep with staged rows */
+int ggrs_p2p_set_unstaged(ggrs_p2p_engine_t* eng, int32_t form);
 /* test hook: the AdvanceFrame from `frame` of `session` flips the lowest bit of player 0's x on
  * every (re)simulation -- a deterministic desync of this peer (session -1: off) */
 int ggrs_p2p_debug_desync(ggrs_p2p_engine_t* eng, int32_t session, int32_t frame);

@@ -46,17 +46,17 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("staged", [True, False])
+@pytest.mark.parametrize("form", ["flat", "lockstep", "unstaged"])
 @pytest.mark.parametrize("P,local,delay,mp,D,pred,model", CASES)
-def test_p2p_matches_oracle(oracle, P, local, delay, mp, D, pred, model, staged):
-    """Both kernel forms: input rows staged in LDS per chunk of calls (default) and read from
-    global memory."""
+def test_p2p_matches_oracle(oracle, P, local, delay, mp, D, pred, model, form):
+    """Every kernel form: per-session step sequences (default), calls in lockstep with input rows
+    staged in LDS, and in lockstep reading rows from global memory."""
     from ggrs_amd import P2PEngine
     S, frames = 300, 160
     rows = stream(S, frames, P, model)
     eng = P2PEngine(S, num_players=P, local_players=local, input_delay=delay, max_prediction=mp,
                     remote_latency=D, predictor=pred, trace_capacity=frames)
-    eng.set_unstaged(not staged)
+    eng.set_kernel_form(form)
     eng.add_inputs(0, rows)
     # chunks of several sizes: state, queues and stats carry across launches
     for n in (1, 2, 5, 40, 112):
