@@ -53,6 +53,7 @@ def _bind(L):
     L.ggrs_branch_timing_reset.argtypes = [vp]
     L.ggrs_branch_timing_read.argtypes = [vp, P(ctypes.c_float), P(ctypes.c_int32)]
     L.ggrs_branch_rounds.argtypes = [vp, ctypes.c_int32]
+    L.ggrs_branch_set_round_launches.argtypes = [vp, ctypes.c_int32]
     for name in _lib.EXPORTS:
         if name.startswith("ggrs_branch_"):
             getattr(L, name).restype = ctypes.c_int
@@ -109,8 +110,12 @@ class BranchEngine:
         _lib.check(self._L.ggrs_branch_confirm(self._h, ptr))
 
     def rounds(self, n):
-        """n rounds of speculate + confirm issued back to back from native code (no report copy)."""
+        """n rounds of speculate + confirm from native code (no report copy): one launch by
+        default, or 2 n back-to-back launches after set_round_launches(True)."""
         _lib.check(self._L.ggrs_branch_rounds(self._h, n))
+
+    def set_round_launches(self, on=True):
+        _lib.check(self._L.ggrs_branch_set_round_launches(self._h, int(bool(on))))
 
     def synchronize(self):
         _lib.check(self._L.ggrs_branch_synchronize(self._h))

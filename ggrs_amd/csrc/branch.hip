@@ -59,9 +59,8 @@ __device__ inline uint32_t branch_digit(int32_t b, int32_t k, int32_t A, int32_t
 // predicted.  GGRS predicts from the last input added to the player's queue (input_queue.rs:
 // 128-161), i.e. the confirmed input of frame f_c - 1, or the default input before frame 0.
 template <int P>
-__device__ inline uint32_t branch_inputs(const SpecParams& p, int64_t s, int32_t b, int32_t k) {
-  const uint32_t truth = load_inputs<P>(p.inputs, (int64_t)((p.f_c + k) % p.cap) * p.S + s);
-  const uint32_t last = p.f_c > 0 ? load_inputs<P>(p.inputs, (int64_t)((p.f_c - 1) % p.cap) * p.S + s) : 0u;
+__device__ inline uint32_t branch_inputs_from(const SpecParams& p, uint32_t truth, uint32_t last, int32_t b,
+                                              int32_t k) {
   uint32_t in = 0;
 #pragma unroll
   for (int q = 0; q < P; q++) {
@@ -72,6 +71,12 @@ __device__ inline uint32_t branch_inputs(const SpecParams& p, int64_t s, int32_t
     in |= v << (8 * q);
   }
   return in;
+}
+template <int P>
+__device__ inline uint32_t branch_inputs(const SpecParams& p, int64_t s, int32_t b, int32_t k) {
+  const uint32_t truth = load_inputs<P>(p.inputs, (int64_t)((p.f_c + k) % p.cap) * p.S + s);
+  const uint32_t last = p.f_c > 0 ? load_inputs<P>(p.inputs, (int64_t)((p.f_c - 1) % p.cap) * p.S + s) : 0u;
+  return branch_inputs_from<P>(p, truth, last, b, k);
 }
 
 template <int P>
@@ -141,6 +146,103 @@ __global__ __launch_bounds__(256) void confirm_kernel(ConfirmParams p) {
   if (in_range && (threadIdx.x & 63) == 0) p.report_bits[lane >> 6] = bits;
 }
 
+// n rounds of speculate + confirm in one launch (ggrs_branch_rounds on one GPU, where no exchange
+// sits between rounds).  The only data a round passes across blocks is each session's trunk; every
+// block keeps the trunks of its own sessions in LDS and replays them itself (the confirm step,
+// done once per block instead of once per session: a few advances per block per round), and the
+// block holding a session's branch-0 lane writes that trunk and its checksum out, as
+// confirm_kernel does.  Survival bits pass from a round to the next in registers.  Rings, reports,
+// trunks and desync records end exactly as after n speculate_kernel + confirm_kernel launches.
+struct RoundsParams {
+  SpecParams sp;  // sp.f_c: trunk frame of the first round
+  int32_t n;
+  uint32_t* trunk;
+  uint16_t* report_ck;
+  uint64_t* report_bits;
+};
+constexpr int kRoundsBlock = 256;
+
+template <int P>
+__global__ __launch_bounds__(kRoundsBlock) void rounds_kernel(RoundsParams rp) {
+  constexpr int F = state_fields(P);
+  __shared__ uint32_t lds_trunk[kRoundsBlock][F];  // the block's sessions (<= 256)
+  __shared__ uint16_t lds_ck[kRoundsBlock];
+  const SpecParams& p = rp.sp;
+  const int64_t lane0 = (int64_t)blockIdx.x * kRoundsBlock;
+  const int64_t lane = lane0 + threadIdx.x;
+  const bool in_range = lane < p.L;
+  const int64_t s_first = lane0 / p.B;
+  const int64_t s_last = (min(p.L, lane0 + kRoundsBlock) - 1) / p.B;
+  const int ns = (int)(s_last - s_first + 1);
+  const int64_t s = in_range ? lane / p.B : s_first;
+  const int32_t b = (int32_t)(lane - s * p.B);
+  const int ls = (int)(s - s_first);
+  for (int q = threadIdx.x; q < ns * F; q += kRoundsBlock) {
+    const int sl = q / F, k = q - sl * F;
+    lds_trunk[sl][k] = rp.trunk[(int64_t)k * p.S + s_first + sl];
+  }
+  if (threadIdx.x < ns) lds_ck[threadIdx.x] = p.trunk_ck[s_first + threadIdx.x];
+  bool survived = p.check_prev && in_range && ((p.prev_survive[lane >> 6] >> (lane & 63)) & 1ull);
+  __syncthreads();
+  for (int32_t r = 0; r < rp.n; ++r) {
+    SpecParams q = p;
+    q.f_c = p.f_c + r;
+    if ((r > 0 || p.check_prev) && survived) {  // speculate_kernel's check of the last survivors
+      const uint16_t mine = p.ring_ck[(int64_t)(q.f_c % p.R) * p.L + lane];
+      if (mine != lds_ck[ls]) atomicCAS(&p.desync[s], -1, q.f_c);
+    }
+    BoxState<P> st;
+#pragma unroll
+    for (int k = 0; k < F; k++) st.w[k] = lds_trunk[ls][k];  // LoadGameState(f_c)
+    // input rows: f_c - 1 (the last confirmed) and f_c + k, each read one frame ahead
+    const uint32_t last = q.f_c > 0 ? load_inputs<P>(p.inputs, (int64_t)((q.f_c - 1) % p.cap) * p.S + s) : 0u;
+    const uint32_t truth = load_inputs<P>(p.inputs, (int64_t)(q.f_c % p.cap) * p.S + s);
+    if (in_range) {
+      uint32_t tk = truth;
+      for (int32_t k = 0; k < p.W; ++k) {
+        const uint32_t next = k + 1 < p.W ? load_inputs<P>(p.inputs, (int64_t)((q.f_c + k + 1) % p.cap) * p.S + s) : 0u;
+        advance_state<P>(st, branch_inputs_from<P>(q, tk, last, b, k), 0u);  // AdvanceFrame(f_c + k)
+        const int32_t slot = (q.f_c + k + 1) % p.R;                            // SaveGameState(f_c + k + 1)
+        store_state<P>(st, p.ring + (int64_t)slot * F * p.L + lane, p.L);
+        p.ring_ck[(int64_t)slot * p.L + lane] = fletcher16_state<P>(st);
+        tk = next;
+      }
+    }
+    // confirm: survival of every lane, the trunk replayed with the true inputs of f_c
+    bool survive = false;
+    if (in_range) {
+      survive = true;
+#pragma unroll
+      for (int qq = 0; qq < P; qq++) {
+        if (!((p.remote_mask >> qq) & 1u)) continue;
+        const uint32_t assumed = (qq == p.first_remote && p.B > 1) ? branch_digit(b, 0, p.A, p.E)
+                                                                   : (last >> (8 * qq)) & 0xffu;
+        survive = survive && assumed == ((truth >> (8 * qq)) & 0xffu);
+      }
+    }
+    const uint64_t bits = __ballot(survive);
+    if (in_range && (threadIdx.x & 63) == 0) rp.report_bits[lane >> 6] = bits;
+    survived = survive;
+    __syncthreads();  // every lane has read the trunk
+    if ((int)threadIdx.x < ns) {
+      const int64_t s2 = s_first + threadIdx.x;
+      BoxState<P> tr;
+#pragma unroll
+      for (int k = 0; k < F; k++) tr.w[k] = lds_trunk[threadIdx.x][k];
+      advance_state<P>(tr, load_inputs<P>(p.inputs, (int64_t)(q.f_c % p.cap) * p.S + s2), 0u);
+      const uint16_t ck = fletcher16_state<P>(tr);
+#pragma unroll
+      for (int k = 0; k < F; k++) lds_trunk[threadIdx.x][k] = tr.w[k];
+      lds_ck[threadIdx.x] = ck;
+      if (s2 * p.B >= lane0) {  // this block holds the session's branch-0 lane
+        store_state<P>(tr, rp.trunk + s2, p.S);
+        rp.report_ck[s2] = ck;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 struct ggrs_branch_engine {
@@ -156,6 +258,7 @@ struct ggrs_branch_engine {
   size_t report_bytes = 0;
   uint64_t* prev_bits = nullptr;
   bool batching = false;             // ggrs_branch_rounds: launches without per-launch events
+  bool per_round_launches = false;   // ggrs_branch_set_round_launches: rounds() as 2 n launches
   int32_t batch_launches = 0;
   std::vector<int32_t> tev_weight;   // launches each collected event pair brackets
   int32_t* desync = nullptr;
@@ -520,9 +623,50 @@ int ggrs_branch_rounds(ggrs_branch_engine_t* e, int32_t n_rounds) {
     e->tev_used += 2;
     HIP_TRY(hipEventRecord(a, e->stream));
   }
+  int rc = GGRS_OK;
+  if (!e->per_round_launches) {
+    // one launch for all n rounds (rounds_kernel); counted as the 2 n launches it replaces
+    RoundsParams rp;
+    SpecParams& p = rp.sp;
+    p.S = e->cfg.num_sessions;
+    p.L = e->L;
+    p.B = e->cfg.branches;
+    p.W = e->cfg.window;
+    p.R = e->R;
+    p.A = e->cfg.alphabet;
+    p.E = e->E;
+    p.cap = e->cap;
+    p.P = e->cfg.num_players;
+    p.f_c = e->trunk_frame;
+    p.remote_mask = (uint32_t)e->cfg.remote_mask;
+    p.first_remote = e->first_remote;
+    p.check_prev = e->have_prev ? 1 : 0;
+    p.trunk = e->trunk;
+    p.ring = e->ring;
+    p.ring_ck = e->ring_ck;
+    p.inputs = e->inputs;
+    p.prev_survive = (const uint64_t*)(e->report + report_ck_bytes(p.S));
+    p.trunk_ck = (const uint16_t*)e->report;
+    p.desync = e->desync;
+    rp.n = n_rounds;
+    rp.trunk = e->trunk;
+    rp.report_ck = (uint16_t*)e->report;
+    rp.report_bits = (uint64_t*)(e->report + report_ck_bytes(p.S));
+    dispatch_players(p.P, [&](auto PC) {
+      constexpr int P = decltype(PC)::value;
+      rounds_kernel<P><<<grid_of(p.L, kRoundsBlock), kRoundsBlock, 0, e->stream>>>(rp);
+    });
+    HIP_TRY(hipGetLastError());
+    e->trunk_frame += n_rounds;
+    e->have_prev = true;
+    if (e->collecting) {
+      HIP_TRY(hipEventRecord(b, e->stream));
+      e->tev_weight.push_back(2 * n_rounds);
+    }
+    return GGRS_OK;
+  }
   e->batching = true;
   e->batch_launches = 0;
-  int rc = GGRS_OK;
   for (int32_t r = 0; r < n_rounds && rc == GGRS_OK; r++) {
     rc = ggrs_branch_speculate(e);
     if (rc == GGRS_OK) rc = ggrs_branch_confirm(e, nullptr);
@@ -533,6 +677,12 @@ int ggrs_branch_rounds(ggrs_branch_engine_t* e, int32_t n_rounds) {
     e->tev_weight.push_back(e->batch_launches);
   }
   return rc;
+}
+
+int ggrs_branch_set_round_launches(ggrs_branch_engine_t* e, int32_t on) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  e->per_round_launches = on != 0;
+  return GGRS_OK;
 }
 
 }  // extern "C"

@@ -213,6 +213,9 @@ int ggrs_branch_timing_read(ggrs_branch_engine_t* eng, float* total_ms, int32_t*
 /* n_rounds x (ggrs_branch_speculate, ggrs_branch_confirm without a report copy) issued back to
  * back from native code; while timing is collected one event pair brackets the whole batch */
 int ggrs_branch_rounds(ggrs_branch_engine_t* eng, int32_t n_rounds);
+/* rounds() as one launch (default: every block replays the trunks of its own sessions, so no
+ * launch boundary is needed between rounds) or, on != 0, as 2 n launches of speculate / confirm */
+int ggrs_branch_set_round_launches(ggrs_branch_engine_t* eng, int32_t on);
 
 /* ---------------------------------------------------------------------------------------------
  * Config-5 large-state stress game (defined by this build; ggrs_amd/csrc/particles.h):

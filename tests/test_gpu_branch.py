@@ -81,19 +81,28 @@ def test_generators_many_sessions(oracle, branches, window, P, mask):
     run_rounds(oracle, eng, truth, rounds, lanes)
 
 
-def test_native_rounds_equal_single_rounds(oracle):
-    """rounds(n) (back-to-back native launches) leaves every trunk, report and survivor set exactly
-    as n single speculate + confirm calls; the survival bits feed the next round's desync check."""
+@pytest.mark.parametrize("launches", ["fused", "per_round"])
+@pytest.mark.parametrize("S,B,A", [(200, 16, 16), (150, 27, 3), (7, 729, 3), (300, 1, 16)])
+def test_native_rounds_equal_single_rounds(oracle, launches, S, B, A):
+    """rounds(n) (one fused launch, or back-to-back native launches) leaves every trunk, report,
+    ring and survivor set exactly as n single speculate + confirm calls; the survival bits feed the
+    next round's desync check.  Branch counts 27 and 729 put a session's lanes across blocks."""
     from ggrs_amd import BranchEngine, synth
-    S, W, B, n = 200, 6, 16, 9
-    truth = synth.gen_inputs(11, S, n + W + 2, 4, synth.MODEL_HELD)
-    engs = [BranchEngine(S, num_players=4, remote_mask=0b0110, window=W, branches=B, alphabet=16) for _ in (0, 1)]
+    W, n = 6, 9
+    truth = synth.gen_inputs(11, S, 2 * n + W + 2, 4, synth.MODEL_HELD)
+    engs = [BranchEngine(S, num_players=4, remote_mask=0b0110, window=W, branches=B, alphabet=A) for _ in (0, 1)]
     for e in engs:
         e.add_inputs(0, truth)
-    engs[0].rounds(n)
+    engs[0].set_round_launches(launches == "per_round")
+    engs[0].rounds(3)  # two calls: the second starts from a previous confirm
+    engs[0].rounds(n - 3)
     for _ in range(n):
         engs[1].speculate()
         engs[1].confirm()
+    for lane in (0, 1, B - 1, B, S * B // 2, S * B - 1):
+        for f in range(n + 1, n + W):
+            a0, a1 = engs[0].lane_state(lane, f), engs[1].lane_state(lane, f)
+            assert a0[0] == a1[0] and bytes(a0[1]) == bytes(a1[1]), (lane, f)
     for e in engs:
         e.synchronize()
     assert engs[0].trunk_frame() == engs[1].trunk_frame() == n
