@@ -91,8 +91,14 @@ def setup_dist(args):
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if os.environ.get("GGRS_BENCH_BACKEND") == "gloo":
+            # rehearsal of N ranks on fewer GPUs: ranks share devices, collectives over gloo
+            local_rank = local_rank % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local_rank)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     return world, rank, local_rank, torch, dist
 
 
@@ -277,14 +283,32 @@ def run_p2p(args):
     S = args.sessions or 65536
     P, D, maxp, calls = 2, 4, 8, 64
     frames = (args.warmup + args.steps) * calls
-    rows = synth.gen_inputs(rank * S, S, frames, P, synth.MODEL_HELD)
-    eng = P2PEngine(S, num_players=P, local_players=(0,), input_delay=0, max_prediction=maxp,
+    # --peers: rank r and rank r + world/2 are the two machines of the same matches (local player
+    # 0 on one, 1 on the other, the same inputs); their checksum reports (desync detection,
+    # interval 32) cross the process group once per step (exchange.exchange_p2p_reports)
+    peers = bool(args.peers) and dist is not None and world >= 2 and world % 2 == 0
+    pair = rank % (world // 2) if peers else rank
+    local = (1,) if peers and rank >= world // 2 else (0,)
+    rows = synth.gen_inputs(pair * S, S, frames, P, synth.MODEL_HELD)
+    eng = P2PEngine(S, num_players=P, local_players=local, input_delay=0, max_prediction=maxp,
                     remote_latency=D, input_capacity=frames + D + 2, device=local_rank)
     eng.set_kernel_form(args.p2p_form)
+    det, events = None, []
+    if peers:
+        from ggrs_amd import exchange
+        from ggrs_amd.desync import DesyncDetector
+        det = DesyncDetector(eng, 32, addr=exchange.peer_of(rank, world))
     eng.add_inputs(0, rows)
     eng.synchronize()
-    for _ in range(args.warmup):
+
+    def step():
         eng.advance_frames(calls)
+        if det is not None:
+            exchange.exchange_p2p_reports(det)
+            events.extend(det.poll())
+
+    for _ in range(args.warmup):
+        step()
     eng.synchronize()
     rb0, rs0 = eng.stats()
     if dist is not None:
@@ -292,17 +316,21 @@ def run_p2p(args):
     eng.timing_reset()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        eng.advance_frames(calls)
+        step()
     eng.synchronize()
     if dist is not None:
         dist.barrier()
     t1 = time.perf_counter()
     kernel_ms, launches = eng.timing_read()
     elapsed = t1 - t0
+    n_desync = len(events)
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        c = torch.tensor([n_desync], dtype=torch.int64, device="cuda")
+        dist.all_reduce(c)
+        n_desync = int(c.item())
     rb1, rs1 = eng.stats()
     resim = int((rs1 - rs0).sum())
     rollbacks = int((rb1 - rb0).sum())
@@ -326,6 +354,8 @@ def run_p2p(args):
                 r = O.p2p_run(rows[:, s], num_players=P, local_mask=0b01, max_prediction=maxp, latency=D)
                 ok &= bytes(eng.state(s)) == bytes(r["final_state"]) and int(rb1[s]) == r["result"].rollbacks
             parity = {"sessions_0_1_mid_last_bit_exact": bool(ok)}
+            if peers:
+                parity["peers_desync_events"] = n_desync
             if world == 1 and not args.no_cpu_baseline:
                 cpu_baseline = p2p_cpu_baseline(args, O, synth, P, D, maxp)
         except Exception as exc:
@@ -337,7 +367,9 @@ def run_p2p(args):
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"p2p: {S} sessions per GPU, 2 players (1 remote, inputs {D} frames "
                                    f"late), max_prediction {maxp}, held-key inputs, {calls} calls per step",
-                       "sessions_per_gpu": S, "parallelism": f"sessions sharded over {world} GPU(s)"},
+                       "sessions_per_gpu": S, "peers": peers,
+                       "parallelism": f"sessions sharded over {world} GPU(s)"
+                                      + (f", peer ranks exchange checksum reports over {dist.get_backend()}" if peers else "")},
             "rollbacks_per_session_frame": round(rollbacks / session_calls, 5),
             "advances_per_sec": round((session_calls + resim) * world / elapsed, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
@@ -502,8 +534,8 @@ def main():
                          "5 = 1 MB particle-world SyncTest")
     ap.add_argument("--sessions", type=int, default=0, help="config 5: sessions per GPU (0 = 8192)")
     ap.add_argument("--peers", action="store_true",
-                    help="configs 3/4: rank r and r + world/2 replay the same sessions (the two "
-                         "machines of a match) and compare checksums after each all-gather")
+                    help="configs 3/4 and p2p: rank r and r + world/2 run the same sessions (the two "
+                         "machines of a match) and compare checksums exchanged over the process group")
     ap.add_argument("--p2p-form", choices=["flat", "lockstep", "unstaged"], default="flat",
                     help="p2p: kernel form (DESIGN.md section 3)")
     ap.add_argument("--workload", choices=["synctest", "p2p", "codec"], default="synctest",

@@ -57,14 +57,21 @@ class DesyncDetector:
         fts = call - 1 - self.latency
         return fts if self.interval > 0 and fts >= self.interval and fts % self.interval == 0 else None
 
-    def outgoing(self, device_out=None):
-        """Reports sent in the calls run since the last outgoing(): [(call, frame, report)]."""
+    def outgoing(self, device=None):
+        """Reports sent in the calls run since the last outgoing(): [(call, frame, report)], each
+        report [S] u16 numpy, or an int16 torch tensor on `device` (the bits of the u16 values)."""
         out = []
         current = self.engine.current_frame()
         for call in range(self.sent, current):
             fts = self._send_frame(call)
             if fts is not None:
-                out.append((call, fts, self.engine.local_checksums(fts)))
+                if device is None:
+                    rep = self.engine.local_checksums(fts)
+                else:
+                    import torch
+                    rep = self.engine.local_checksums(
+                        fts, out=torch.empty(self.engine.num_sessions, dtype=torch.int16, device=device))
+                out.append((call, fts, rep))
         self.sent = current
         return out
 
@@ -104,8 +111,8 @@ class DesyncDetector:
                     local = self.engine.local_checksums(frame)
                     remote = report.cpu().numpy() if hasattr(report, "cpu") else report
                     for s in sessions:
-                        events.append(DesyncDetected(frame, int(s), int(local[s]), int(remote[s]),
-                                                     self.addr, call))
+                        events.append(DesyncDetected(frame, int(s), int(local[s]) & 0xFFFF,
+                                                     int(remote[s]) & 0xFFFF, self.addr, call))
                 checked.append(frame)
             for frame in checked:
                 del self.pending[frame]

@@ -66,3 +66,39 @@ def desyncs_against_peer(gathered, rank, world, frame, num_sessions, num_lanes):
     theirs, _ = split_report(g[peer], num_sessions, num_lanes)
     bad = np.nonzero(mine != theirs)[0]
     return [DesyncDetected(frame, int(s), int(mine[s]), int(theirs[s]), peer) for s in bad]
+
+
+
+def exchange_p2p_reports(detector, group=None):
+    """Checksum reports of a P2P engine's sessions between the two peers of every match, over the
+    process group: rank r and rank peer_of(r) run the same sessions as the two machines of each
+    match (a desync.DesyncDetector on each).  Every rank runs the same calls, so each sends the same
+    number of reports for the same frames; they are stacked into one [k][2S] byte tensor,
+    all-gathered (RCCL on device tensors, gloo on CPU tensors), and the peer's rows are
+    delivered with DesyncDetector.receive -- the ChecksumReport messages of protocol.rs:692-698
+    (send) and :663-682 (receive), one collective per batch of calls.  Returns the number of
+    reports sent."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    nccl = dist.get_backend(group) == "nccl"
+    device = torch.device("cuda", torch.cuda.current_device()) if nccl else None
+    out = detector.outgoing(device=device)
+    if not out:
+        return 0
+    # as bytes: neither gloo nor RCCL reduce or gather 16-bit integers
+    if nccl:
+        local = torch.stack([r for _, _, r in out]).view(torch.uint8)
+        gathered = torch.empty((world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
+        dist.all_gather_into_tensor(gathered.view(-1), local.contiguous().view(-1), group=group)
+    else:
+        local = torch.from_numpy(np.stack([np.asarray(r, np.uint16).view(np.uint8) for _, _, r in out]))
+        parts = [torch.empty_like(local) for _ in range(world)]
+        dist.all_gather(parts, local.contiguous(), group=group)
+        gathered = torch.stack(parts)
+    theirs = gathered[peer_of(rank, world)]
+    for k, (call, frame, _) in enumerate(out):
+        row = theirs[k]
+        detector.receive(call, frame, row.view(torch.int16) if nccl else row.numpy().view(np.uint16))
+    return len(out)

@@ -77,3 +77,73 @@ def test_split_report_roundtrip():
     buf = fake_report(0, 1)
     ck, bits = exchange.split_report(buf, S, L)
     assert ck.size == S and bits.size == (L + 63) // 64
+
+
+class FakeP2PEngine:
+    """The parts of P2PEngine a DesyncDetector reads: checksum reports per frame (a deterministic
+    function of frame and session, the same on both peers except one corrupted session)."""
+
+    def __init__(self, sessions, latency, corrupt=None):
+        self.num_sessions, self.remote_latency, self.frame, self.corrupt = sessions, latency, 0, corrupt
+
+    def set_desync_detection(self, interval):
+        self.interval = interval
+
+    def current_frame(self):
+        return self.frame
+
+    def local_checksums(self, frame, out=None):
+        ck = np.random.default_rng(77 + frame).integers(0, 65536, self.num_sessions).astype(np.uint16)
+        if self.corrupt is not None and frame >= self.corrupt[1]:
+            ck[self.corrupt[0]] ^= 0x8001
+        if out is not None:
+            out.copy_(torch.from_numpy(ck.view(np.int16)))
+            return out
+        return ck
+
+    def compare_checksums(self, frame, remote):
+        remote = remote.cpu().numpy().view(np.uint16) if hasattr(remote, "cpu") else np.asarray(remote, np.uint16)
+        return np.nonzero(self.local_checksums(frame) != remote)[0]
+
+
+def p2p_worker(rank, world, port, out):
+    from ggrs_amd.desync import DesyncDetector
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        interval, latency = 10, 3
+        # rank 0's session 4 desyncs from frame 40 on; its peer sees the same event
+        eng = FakeP2PEngine(23, latency, corrupt=(4, 40) if rank == 0 else None)
+        det = DesyncDetector(eng, interval, addr=exchange.peer_of(rank, world))
+        events = []
+        for _ in range(8):  # 8 batches of 16 calls, one collective per batch
+            eng.frame += 16
+            exchange.exchange_p2p_reports(det)
+            events += det.poll()
+        pr = exchange.peer_of(rank, world)
+        if rank == 0 or pr == 0:
+            assert {e.session for e in events} == {4}
+            assert min(e.frame for e in events) == 40
+            assert all(e.addr == pr and e.local_checksum != e.remote_checksum for e in events)
+        else:
+            assert events == []
+        out[rank] = 1
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_p2p_reports_between_peers_gloo(world):
+    """P2P checksum reports travel between the two peers of each match through the process group;
+    a session whose checksums diverge raises DesyncDetected on both peers, no other rank sees one."""
+    ctx = mp.get_context("spawn")
+    out = ctx.Array("i", world)
+    port = free_port()
+    procs = [ctx.Process(target=p2p_worker, args=(r, world, port, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert list(out) == [1] * world

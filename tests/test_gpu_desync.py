@@ -92,3 +92,64 @@ def test_history_bounds_are_preconditions():
     e.local_checksums(290)            # newest report: frame 295 (call 298); 290 still held
     with pytest.raises(Exception):
         e.set_desync_detection(10)    # configuration: before the first call only
+
+
+def _peer_rank(rank, port, args, out):
+    import os
+    import torch.distributed as dist
+    from ggrs_amd import P2PEngine, exchange
+    from ggrs_amd.desync import DesyncDetector
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=2)
+    try:
+        S, frames, D, mp, interval, chunk, bad, X = args
+        rows = stream(S, frames, 2)
+        eng = P2PEngine(S, num_players=2, local_players=(rank,), max_prediction=mp, remote_latency=D,
+                        input_capacity=frames + 16)
+        det = DesyncDetector(eng, interval, addr=exchange.peer_of(rank, 2))
+        if rank == 1:
+            eng.debug_desync(bad, X)
+        eng.add_inputs(0, rows)
+        events, done = [], 0
+        while done < frames:
+            n = min(chunk, frames - done)
+            eng.advance_frames(n)
+            exchange.exchange_p2p_reports(det)
+            events += det.poll()
+            done += n
+        for k, ev in enumerate(events[:60]):
+            out[rank * 300 + 5 * k: rank * 300 + 5 * k + 5] = [ev.call, ev.frame, ev.local_checksum,
+                                                               ev.remote_checksum, ev.session]
+        out[600 + rank] = len(events)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_peers_in_two_processes_over_process_group(oracle):
+    """The two machines of every match in two processes (one P2P engine each on the same GPU),
+    their checksum reports crossing a gloo process group (exchange.exchange_p2p_reports, the path
+    the multi-GPU bench takes over RCCL): the DesyncDetected events are the oracle's."""
+    import socket
+    import torch.multiprocessing as mp_
+    S, frames, D, mp, interval, chunk, bad, X = 96, 240, 2, 8, 10, 40, 17, 91
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp_.get_context("spawn")
+    out = ctx.Array("i", 602)
+    procs = [ctx.Process(target=_peer_rank, args=(r, port, (S, frames, D, mp, interval, chunk, bad, X), out))
+             for r in (0, 1)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+    assert all(p.exitcode == 0 for p in procs)
+    rows = stream(S, frames, 2)
+    ref = oracle.p2p_desync_pair_run(rows[:, bad], latency=D, max_prediction=mp, interval=interval,
+                                     desync_peer=1, desync_frame=X)
+    for k in (0, 1):
+        n = out[600 + k]
+        got = [tuple(out[k * 300 + 5 * i: k * 300 + 5 * i + 5]) for i in range(min(n, 60))]
+        want = [(c, f, l, r, bad) for (p, c, f, l, r) in ref["events"] if p == k]
+        assert n == len(want) and got == want[:60]
