@@ -36,12 +36,16 @@ __host__ __device__ inline uint32_t initial_payload(uint64_t session, uint64_t e
   return (uint32_t)mix64((session << 40) ^ (e << 8) ^ (uint64_t)k);
 }
 
-// One entity's frame step.  w[0..4] ship bits, w[5..24] payload.
+// One entity's frame step.  w[0..4] ship bits, w[5..24] payload.  Lean = the caller has checked
+// that rot is in [+0, 2pi] (box_game.h advance_player_lean, which keeps it there); otherwise the
+// general form.
+template <bool Lean>
 __device__ inline void advance_entity(uint32_t (&w)[kFields], uint32_t input) {
   float x = __builtin_bit_cast(float, w[0]), y = __builtin_bit_cast(float, w[1]);
   float vx = __builtin_bit_cast(float, w[2]), vy = __builtin_bit_cast(float, w[3]);
   float rot = __builtin_bit_cast(float, w[4]);
-  advance_player(x, y, vx, vy, rot, input);
+  if constexpr (Lean) advance_player_lean(x, y, vx, vy, rot, input);
+  else advance_player_general(x, y, vx, vy, rot, input);
   w[0] = __builtin_bit_cast(uint32_t, x);
   w[1] = __builtin_bit_cast(uint32_t, y);
   w[2] = __builtin_bit_cast(uint32_t, vx);
@@ -64,18 +68,18 @@ struct FletcherAcc {
   uint32_t s2neg;  // sum of the in-record weights
 };
 
+// The in-record weight of byte b of word k is 4k + b <= 99, so both sums are one accumulating
+// dot4 per word: A += dot4(w_k, 1111), J += dot4(w_k, [4k, 4k+1, 4k+2, 4k+3]).
 __device__ inline void fletcher_entity(FletcherAcc& acc, const uint32_t (&w)[kFields], uint64_t n_minus_o) {
-  uint32_t a = 0, ka = 0, b = 0;
+  uint32_t a = 0, j = 0;
 #pragma unroll
   for (int k = 0; k < kFields; k++) {
-    const uint32_t ak = __builtin_amdgcn_udot4(w[k], 0x01010101u, 0u, false);
-    a += ak;
-    ka += ak * (uint32_t)(4 * k);
-    b = __builtin_amdgcn_udot4(w[k], 0x03020100u, b, false);
+    a = __builtin_amdgcn_udot4(w[k], 0x01010101u, a, false);
+    j = __builtin_amdgcn_udot4(w[k], 0x03020100u + 0x04040404u * (uint32_t)k, j, false);
   }
   acc.s1 += a;
   acc.s2pos += n_minus_o * (uint64_t)a;
-  acc.s2neg += ka + b;
+  acc.s2neg += j;
 }
 
 }  // namespace particles

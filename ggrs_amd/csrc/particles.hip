@@ -2,15 +2,16 @@
 // src/sessions/sync_test_session.rs:85-150, same bookkeeping as synctest_kernel in engine.hip) on
 // the config-5 particle world (particles.h): ~1 MB states, so every Load/Save is an HBM stream.
 //
-// One workgroup per session.  Each thread owns entity quads (4 consecutive entities, 16-byte
-// loads/stores per field) for the whole launch and keeps a quad in registers across one call's
-// replay: Load (1 read of the quad), cd x (Save, Advance), Save of the current frame, the new
-// frame's Advance.  HBM per call and session = S (load) + cd * S (saves), S = 4 + 100 N bytes --
+// One workgroup per session.  Each thread owns units of E consecutive entities (E = 1, 2 or 4;
+// E-dword loads/stores per field) and keeps a unit in registers across one call's replay: Load
+// (1 read of the unit), cd x (Save, Advance), Save of the current frame, the new frame's Advance.  HBM per call and session = S (load) + cd * S (saves), S = 4 + 100 N bytes --
 // per resimulated frame S * (1 + 1/cd).  The Fletcher-16 of every saved frame is reduced in
 // registers (64-bit closed form), across the wavefront by shuffles and across the workgroup in LDS.
 //
-// HBM layout: ring [R][L][25][N] u32 (field-major, entity fastest), cur [L][25][N], frame counters
-// [R][L] / [L] i32, ring_ck / first_ck [R][L] u16, inputs [C][L] u32 (P input bytes per frame).
+// HBM layout: a state record is [ceil(N/256) tiles][25 fields][256 entities] u32 (tile-major,
+// field-major inside a tile, entity fastest), so one block-step's saves of 256 entities are one
+// contiguous 25 KB run rather than 25 runs 40 KB apart; ring [R][L][rec], cur [L][rec], frame
+// counters [R][L] / [L] i32, ring_ck / first_ck [R][L] u16, inputs [C][L] u32 (P input bytes per frame).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -33,6 +34,14 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kMaxCd = 62;
 
+constexpr int kTile = 256;  // entities per tile of the record layout
+
+// u32 words of one (padded) state record, and the word of (field k, entity e) inside it
+__host__ __device__ inline size_t pw_rec(int32_t N) { return (size_t)((N + kTile - 1) / kTile) * kFields * kTile; }
+__host__ __device__ inline size_t pw_idx(int32_t k, int32_t e) {
+  return (size_t)(e / kTile) * kFields * kTile + (size_t)k * kTile + (size_t)(e % kTile);
+}
+
 struct PWParams {
   int64_t L;
   int32_t N, R, cd, f0, n, cap, P;
@@ -53,51 +62,68 @@ struct PWParams {
 __global__ void pw_init_kernel(uint32_t* cur, int32_t* cur_frame, int64_t L, int32_t N, int64_t first_session) {
   const int64_t s = blockIdx.y;
   for (int32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < N; e += gridDim.x * blockDim.x) {
-    uint32_t* base = cur + (size_t)s * kFields * N + e;
+    uint32_t* base = cur + (size_t)s * pw_rec(N) + pw_idx(0, e);
     const float r = kWindowWidth / 4.0f;
     const float rot = (float)e / (float)N * 2.0f * kPi;
     base[0] = __builtin_bit_cast(uint32_t, kWindowWidth / 2.0f + r * glibc_cosf(rot));
-    base[(size_t)N] = __builtin_bit_cast(uint32_t, kWindowHeight / 2.0f + r * glibc_sinf(rot));
-    base[(size_t)2 * N] = 0u;
-    base[(size_t)3 * N] = 0u;
-    base[(size_t)4 * N] = __builtin_bit_cast(uint32_t, fmod_exact(rot + kPi, 2.0f * kPi));
+    base[kTile] = __builtin_bit_cast(uint32_t, kWindowHeight / 2.0f + r * glibc_sinf(rot));
+    base[2 * kTile] = 0u;
+    base[3 * kTile] = 0u;
+    base[4 * kTile] = __builtin_bit_cast(uint32_t, fmod_exact(rot + kPi, 2.0f * kPi));
     for (int k = 0; k < 20; k++)
-      base[(size_t)(5 + k) * N] = initial_payload((uint64_t)(first_session + s), (uint64_t)e, k);
+      base[(5 + k) * kTile] = initial_payload((uint64_t)(first_session + s), (uint64_t)e, k);
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) cur_frame[s] = 0;
 }
 
-__device__ inline void load_quad(uint32_t (&w)[4][kFields], const uint32_t* base, int32_t N, int32_t q) {
+// A thread owns E consecutive entities (E = 1, 2, 4; unit q = entities E*q .. E*q+E-1, inside one
+// tile): one E-dword access per field.
+template <int E>
+using uvec = uint32_t __attribute__((ext_vector_type(E)));
+
+template <int E>
+__device__ inline void load_unit(uint32_t (&w)[E][kFields], const uint32_t* rec, int32_t q) {
+  const uint32_t* base = rec + pw_idx(0, E * q);
 #pragma unroll
   for (int k = 0; k < kFields; k++) {
-    const uint4 v = *reinterpret_cast<const uint4*>(base + (size_t)k * N + 4 * q);
-    w[0][k] = v.x;
-    w[1][k] = v.y;
-    w[2][k] = v.z;
-    w[3][k] = v.w;
+    if constexpr (E == 1) {
+      w[0][k] = base[k * kTile];
+    } else {
+      const uvec<E> v = *reinterpret_cast<const uvec<E>*>(base + k * kTile);
+#pragma unroll
+      for (int j = 0; j < E; j++) w[j][k] = v[j];
+    }
   }
 }
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-__device__ inline void store_quad(const uint32_t (&w)[4][kFields], uint32_t* base, int32_t N, int32_t q) {
-#pragma unroll
-  for (int k = 0; k < kFields; k++)
-    *reinterpret_cast<uint4*>(base + (size_t)k * N + 4 * q) = make_uint4(w[0][k], w[1][k], w[2][k], w[3][k]);
-}
-// ring saves are write-once-per-call streams far larger than any cache: non-temporal stores
-__device__ inline void store_quad_nt(const uint32_t (&w)[4][kFields], uint32_t* base, int32_t N, int32_t q) {
+// Nt: ring saves are write-once-per-call streams far larger than any cache (non-temporal stores)
+template <int E, bool Nt>
+__device__ inline void store_unit(const uint32_t (&w)[E][kFields], uint32_t* rec, int32_t q) {
+  uint32_t* base = rec + pw_idx(0, E * q);
 #pragma unroll
   for (int k = 0; k < kFields; k++) {
-    u32x4 v = {w[0][k], w[1][k], w[2][k], w[3][k]};
-    __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(base + (size_t)k * N + 4 * q));
+    if constexpr (E == 1) {
+      uint32_t* d = base + k * kTile;
+      if constexpr (Nt) __builtin_nontemporal_store(w[0][k], d);
+      else *d = w[0][k];
+    } else {
+      uvec<E> v;
+#pragma unroll
+      for (int j = 0; j < E; j++) v[j] = w[j][k];
+      uvec<E>* d = reinterpret_cast<uvec<E>*>(base + k * kTile);
+      if constexpr (Nt) __builtin_nontemporal_store(v, d);
+      else *d = v;
+    }
   }
 }
-__device__ inline void advance_quad(uint32_t (&w)[4][kFields], uint32_t in_word, int32_t P, int32_t e0) {
+template <int E, bool Lean>
+__device__ inline void advance_unit(uint32_t (&w)[E][kFields], uint32_t in_word, int32_t P, int32_t e0) {
 #pragma unroll
-  for (int j = 0; j < 4; j++) advance_entity(w[j], (in_word >> (8 * ((e0 + j) % P))) & 0xffu);
+  for (int j = 0; j < E; j++) advance_entity<Lean>(w[j], (in_word >> (8 * ((e0 + j) % P))) & 0xffu);
 }
-__device__ inline void fletcher_quad(FletcherAcc& a, const uint32_t (&w)[4][kFields], int32_t N, int32_t e0) {
+template <int E>
+__device__ inline void fletcher_unit(FletcherAcc& a, const uint32_t (&w)[E][kFields], int32_t N, int32_t e0) {
 #pragma unroll
-  for (int j = 0; j < 4; j++) fletcher_entity(a, w[j], (uint64_t)kEntityBytes * (uint64_t)(N - (e0 + j)));
+  for (int j = 0; j < E; j++) fletcher_entity(a, w[j], (uint64_t)kEntityBytes * (uint64_t)(N - (e0 + j)));
 }
 
 // Wavefront sum of one quad-frame's Fletcher partials, added by lane 0 to the wave's LDS slot of
@@ -130,15 +156,41 @@ __device__ inline uint16_t finish_checksum(uint64_t s1, uint64_t s2pos, uint64_t
 
 constexpr int kWaves = kBlock / 64;
 
+// One call's replay of one unit (E entities) from its loaded frame g0: Save(g) + Fletcher
+// (skipped for i = 0 on a replay: that cell was just loaded), Advance.  Every lane of the wave
+// runs it (the Fletcher partials are summed by shuffles); `on` lanes own a unit.
+template <int E, bool Lean>
+__device__ inline void replay_unit(uint32_t (&w)[E][kFields], const PWParams& p, int64_t s, int32_t g0,
+                                   int32_t steps, bool save_first, uint32_t in_cur, bool on, int32_t q,
+                                   uint64_t (*acc)[3]) {
+  const size_t rec = pw_rec(p.N);
+  const int32_t e0 = E * q;
+  for (int32_t i = 0; i <= steps; ++i) {
+    const int32_t g = g0 + i;  // frame the quad holds
+    if (p.cd > 0 && (i > 0 || save_first)) {  // SaveGameState(g): the replay's saves, then save current
+      FletcherAcc a{0, 0, 0};
+      if (on) {
+        uint32_t* dst = p.ring + ((size_t)(g % p.R) * p.L + s) * rec;
+        if (p.nt_saves) store_unit<E, true>(w, dst, q);
+        else store_unit<E, false>(w, dst, q);
+        fletcher_unit<E>(a, w, p.N, e0);
+      }
+      wave_accumulate(a, acc[i]);
+    }
+    if (on) advance_unit<E, Lean>(w, i < steps ? p.inputs[(int64_t)(g % p.cap) * p.L + s] : in_cur, p.P, e0);
+  }
+}
+
+template <int E>
 __global__ __launch_bounds__(kBlock) void pw_synctest_kernel(PWParams p) {
   __shared__ uint64_t lds_acc[kWaves][kMaxCd + 1][3];  // per wave, per saved frame: s1, s2+, s2-
   __shared__ int32_t lds_stop;
   const int64_t s = blockIdx.x;
   if (p.lane_status[s] != GGRS_LANE_RUNNING) return;
-  const int32_t N = p.N, R = p.R, nq = N / 4, cd = p.cd;
+  const int32_t N = p.N, R = p.R, nq = N / E, cd = p.cd;
   const int64_t L = p.L;
   const int wave = threadIdx.x >> 6;
-  const size_t rec = (size_t)kFields * N;  // u32 per session state
+  const size_t rec = pw_rec(N);  // u32 per session state (padded to whole tiles)
   uint32_t* cur = p.cur + (size_t)s * rec;
   for (int32_t f = p.f0; f < p.f0 + p.n; ++f) {
     const bool replay = cd > 0 && f > cd;
@@ -162,10 +214,10 @@ __global__ __launch_bounds__(kBlock) void pw_synctest_kernel(PWParams p) {
         // call f-1's final AdvanceFrame -- the advance of the frame-(f-1) cell it saved.
         const uint32_t in_prev = p.inputs[(int64_t)((f - 1) % p.cap) * L + s];
         for (int32_t q = threadIdx.x; q < nq; q += kBlock) {
-          uint32_t w[4][kFields];
-          load_quad(w, p.ring + ((size_t)((f - 1) % R) * L + s) * rec, N, q);
-          advance_quad(w, in_prev, p.P, 4 * q);
-          store_quad(w, cur, N, q);
+          uint32_t w[E][kFields];
+          load_unit<E>(w, p.ring + ((size_t)((f - 1) % R) * L + s) * rec, q);
+          advance_unit<E, false>(w, in_prev, p.P, E * q);
+          store_unit<E, false>(w, cur, q);
         }
         return;
       }
@@ -178,38 +230,33 @@ __global__ __launch_bounds__(kBlock) void pw_synctest_kernel(PWParams p) {
     for (int32_t qb = 0; qb < nq; qb += kBlock) {  // wave-uniform trip count (shuffles inside)
       const int32_t q = qb + threadIdx.x;
       const bool on = q < nq;
-      const int32_t e0 = 4 * q;
-      uint32_t w[4][kFields];
+      uint32_t w[E][kFields];
       if (on) {
         if (replay) {  // LoadGameState(f - cd)
-          load_quad(w, p.ring + ((size_t)(g0 % R) * L + s) * rec, N, q);
+          load_unit<E>(w, p.ring + ((size_t)(g0 % R) * L + s) * rec, q);
           if (s == p.corrupt_lane && f == p.corrupt_frame && q == 0) w[0][0] ^= 1u;
         } else {
-          load_quad(w, cur, N, q);  // the handler's current state (warm-up calls)
+          load_unit<E>(w, cur, q);  // the handler's current state (warm-up calls)
         }
       } else {
 #pragma unroll
-        for (int j = 0; j < 4; j++)
+        for (int j = 0; j < E; j++)
 #pragma unroll
           for (int k = 0; k < kFields; k++) w[j][k] = 0;
       }
       const int32_t steps = replay ? cd : 0;
-      for (int32_t i = 0; i <= steps; ++i) {
-        const int32_t g = g0 + i;  // frame the quad holds
-        if (cd > 0 && (i > 0 || !replay)) {  // SaveGameState(g): the replay's saves, then save current
-          FletcherAcc a{0, 0, 0};
-          if (on) {
-            if (p.nt_saves) store_quad_nt(w, p.ring + ((size_t)(g % R) * L + s) * rec, N, q);
-            else store_quad(w, p.ring + ((size_t)(g % R) * L + s) * rec, N, q);
-            fletcher_quad(a, w, N, e0);
-          }
-          wave_accumulate(a, lds_acc[wave][i]);
-        }
-        if (on) advance_quad(w, i < steps ? p.inputs[(int64_t)(g % p.cap) * L + s] : in_cur, p.P, e0);
-      }
+      // one domain test per loaded unit: the lean step keeps rot in [+0, 2pi], so the whole
+      // replay runs in the form the loaded rotations allow (wave-uniform)
+      bool dom = true;
+#pragma unroll
+      for (int j = 0; j < E; j++) dom = dom && w[j][4] <= kTwoPiBits;
+      if (__builtin_expect(__all(dom), 1))
+        replay_unit<E, true>(w, p, s, g0, steps, !replay, in_cur, on, q, lds_acc[wave]);
+      else
+        replay_unit<E, false>(w, p, s, g0, steps, !replay, in_cur, on, q, lds_acc[wave]);
       // the game state after the call; a later call of this launch reloads from the ring, so
       // only the last call's (or a warm-up call's) result has a reader
-      if (on && (!replay || last_call)) store_quad(w, cur, N, q);
+      if (on && (!replay || last_call)) store_unit<E, false>(w, cur, q);
     }
     __syncthreads();
     if (cd > 0 && threadIdx.x == 0) {
@@ -250,6 +297,7 @@ struct ggrs_particle_engine {
   int32_t current_frame = 0, next_input_frame = 0;
   int32_t corrupt_lane = -1, corrupt_frame = -1;
   int32_t nt_saves = 1;  // GGRS_PW_STORE=plain selects plain stores for the ring saves
+  int32_t ept = 1;       // entities per thread (1, 2, 4); GGRS_PW_EPT selects (1: 4 waves/SIMD, no scratch)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<hipEvent_t> tev;
   size_t tev_used = 0;
@@ -305,6 +353,10 @@ int ggrs_particle_engine_create(const ggrs_particle_config_t* cfg, ggrs_particle
   e->R = c.max_prediction + 1;
   e->cap = c.input_capacity ? c.input_capacity : 128;
   if (const char* sp = getenv("GGRS_PW_STORE")) e->nt_saves = strcmp(sp, "plain") != 0;
+  if (const char* se = getenv("GGRS_PW_EPT")) {
+    const int v = atoi(se);
+    if (v == 1 || v == 2 || v == 4) e->ept = v;
+  }
   e->cfg.input_capacity = e->cap;
   if (e->cap < c.check_distance + 2) {
     delete e;
@@ -322,7 +374,7 @@ int ggrs_particle_engine_create(const ggrs_particle_config_t* cfg, ggrs_particle
     if (e_ != hipSuccess) return fail(set_error(GGRS_E_HIP, "%s: %s", #expr, hipGetErrorString(e_))); \
   } while (0)
   const int64_t L = c.num_sessions;
-  const size_t rec = (size_t)kFields * c.num_entities;
+  const size_t rec = pw_rec(c.num_entities);
   CTRY(hipSetDevice(c.device));
   CTRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
   CTRY(hipEventCreate(&e->ev0));
@@ -426,7 +478,9 @@ int ggrs_particle_synctest_advance_frames(ggrs_particle_engine_t* e, int32_t n) 
     e->tev_used += 2;
   }
   HIP_TRY(hipEventRecord(a, e->stream));
-  pw_synctest_kernel<<<p.L, kBlock, 0, e->stream>>>(p);
+  if (e->ept == 1) pw_synctest_kernel<1><<<p.L, kBlock, 0, e->stream>>>(p);
+  else if (e->ept == 2) pw_synctest_kernel<2><<<p.L, kBlock, 0, e->stream>>>(p);
+  else pw_synctest_kernel<4><<<p.L, kBlock, 0, e->stream>>>(p);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(b, e->stream));
   e->current_frame += n;
@@ -457,11 +511,11 @@ int ggrs_particle_read_mismatches(ggrs_particle_engine_t* e, int32_t* st, int32_
   return GGRS_OK;
 }
 
-// declared layout bytes of a SoA record: frame, then per entity 25 little-endian words
+// declared layout bytes of a tiled record: frame, then per entity 25 little-endian words
 static void pw_serialize(const std::vector<uint32_t>& soa, int32_t frame, int32_t N, uint8_t* out) {
   memcpy(out, &frame, 4);
   for (int32_t e2 = 0; e2 < N; e2++)
-    for (int k = 0; k < kFields; k++) memcpy(out + 4 + (size_t)kEntityBytes * e2 + 4 * k, &soa[(size_t)k * N + e2], 4);
+    for (int k = 0; k < kFields; k++) memcpy(out + 4 + (size_t)kEntityBytes * e2 + 4 * k, &soa[pw_idx(k, e2)], 4);
 }
 
 int ggrs_particle_read_state(ggrs_particle_engine_t* e, int32_t session, uint8_t* out) {
@@ -469,7 +523,7 @@ int ggrs_particle_read_state(ggrs_particle_engine_t* e, int32_t session, uint8_t
   if (session < 0 || session >= e->cfg.num_sessions) return set_error(GGRS_E_INVALID, "session out of range");
   HIP_TRY(hipSetDevice(e->cfg.device));
   const int32_t N = e->cfg.num_entities;
-  const size_t rec = (size_t)kFields * N;
+  const size_t rec = pw_rec(N);
   std::vector<uint32_t> soa(rec);
   int32_t frame = 0;
   HIP_TRY(hipMemcpyAsync(soa.data(), e->cur + rec * session, 4 * rec, hipMemcpyDeviceToHost, e->stream));
@@ -485,7 +539,7 @@ int ggrs_particle_read_saved(ggrs_particle_engine_t* e, int32_t session, int32_t
   if (frame < 0) return set_error(GGRS_E_INVALID, "negative frame");
   HIP_TRY(hipSetDevice(e->cfg.device));
   const int32_t N = e->cfg.num_entities;
-  const size_t rec = (size_t)kFields * N;
+  const size_t rec = pw_rec(N);
   const int slot = frame % e->R;
   int32_t tag = -1;
   uint16_t ck = 0;

@@ -17,8 +17,10 @@ def inputs_for(O, sessions, frames, P, first=0):
     (32, 4, 8, 0, 12, [12]),
     (10000, 2, 17, 16, 22, [22]),  # the config-5 entity count (1 MB states)
 ])
-def test_particles_match_oracle(oracle, N, P, maxp, cd, frames, chunks):
+@pytest.mark.parametrize("ept", ["1", "2", "4"])  # entities per thread (GGRS_PW_EPT)
+def test_particles_match_oracle(oracle, monkeypatch, ept, N, P, maxp, cd, frames, chunks):
     from ggrs_amd import ParticleEngine
+    monkeypatch.setenv("GGRS_PW_EPT", ept)
     S = 5
     inp = inputs_for(oracle, S, frames, P)
     eng = ParticleEngine(S, N, P, maxp, cd, input_capacity=frames + cd + 2)
@@ -39,8 +41,10 @@ def test_particles_match_oracle(oracle, N, P, maxp, cd, frames, chunks):
     assert (st == 0).all()
 
 
-def test_particles_mismatch(oracle):
+@pytest.mark.parametrize("ept", ["1", "2", "4"])
+def test_particles_mismatch(oracle, monkeypatch, ept):
     from ggrs_amd import ParticleEngine
+    monkeypatch.setenv("GGRS_PW_EPT", ept)
     S, N, P, maxp, cd, frames, call = 3, 128, 2, 9, 8, 40, 20
     inp = inputs_for(oracle, S, frames, P)
     eng = ParticleEngine(S, N, P, maxp, cd, input_capacity=frames + cd + 2)

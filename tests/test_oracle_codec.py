@@ -4,7 +4,7 @@ test_encode_decode (:216-231), the encode_decode_round_trip property (:195-203) 
 recorded regression case (proptest-regressions/network/compression.txt: reference = [],
 inputs = [[], []]) and decode_arbitrary_input_never_panics (:205-213)."""
 import numpy as np
-from hypothesis import given, settings, strategies as st
+from hypothesis import example, given, settings, strategies as st
 
 from oracle import oracle as O
 from oracle import pycodec as PC
@@ -66,7 +66,14 @@ def test_fixed_size_ex_game_stream():
     assert enc[0] == 0 and O.codec_decode(ref, enc) == (0, pend)
 
 
+CODEC_E_CAP = -4   # oracle/codec.c: decoded inputs exceed the caller's buffers
+MAX_INPUTS = 1 << 16
+
+
 @settings(max_examples=400, deadline=None)
+# regression: tag byte zeroed -> fixed-size decode of a stream whose RLE yields > 2^16 inputs
+@example(b"\x00", [b"\x00", b"N\x97~\xf9\x06\x0f0F\x00", b"\xf2\x9d ", b"\x88\xca\xce3\xea\xc6", b"\x00", b"e",
+                   b"\x8d-\xd2Xi\xdd\x88\xd8\xfer", b"R\xe6Q\xc8\xbc", b"", b"", b"", b"", b""], [(0, 0)])
 @given(small_bytes, st.lists(small_bytes, min_size=1, max_size=16), st.lists(st.tuples(st.integers(0, 4096), st.integers(0, 255)), min_size=1, max_size=4))
 def test_mutated_packets_agree(reference, inputs, muts):
     """Valid packets with a few bytes overwritten reach the RLE and delta checks; both
@@ -75,9 +82,12 @@ def test_mutated_packets_agree(reference, inputs, muts):
     for pos, val in muts:
         enc[pos % len(enc)] = val
     enc = bytes(enc)
-    rc, out = O.codec_decode(reference, enc)
+    rc, out = O.codec_decode(reference, enc, max_inputs=MAX_INPUTS)
     try:
         want = PC.decode(reference, enc)
-        assert rc == 0 and out == want
+        if rc == CODEC_E_CAP:  # valid, but more inputs than the checker's output buffers hold
+            assert len(want) > MAX_INPUTS
+        else:
+            assert rc == 0 and out == want
     except PC.CodecError:
-        assert rc < 0
+        assert rc < 0 and rc != CODEC_E_CAP
