@@ -59,27 +59,39 @@ __device__ inline void advance_entity(uint32_t (&w)[kFields], uint32_t input) {
   }
 }
 
-// Fletcher-16 partial sums of one entity record at byte offset o in an n-byte stream:
-//   s1 += sum of bytes, s2 += sum_j (n - o - j) d_j  split as (n - o) * sum(bytes) - sum_j j d_j.
-// Over a record: sum_j j d_j = sum_k (4k * A(w_k) + B(w_k)), A = dot4(w, 1111), B = dot4(w, 0123).
-struct FletcherAcc {
-  uint32_t s1;     // byte sum (<= 2^32 per thread: 255 * 100 * entities-per-thread)
-  uint64_t s2pos;  // sum (n - o_e) * A_e
-  uint32_t s2neg;  // sum of the in-record weights
-};
+// Fletcher-16 contribution of one entity record at byte offset o_e = 4 + 100 e of the n-byte
+// stream (n = 4 + 100 N), reduced mod 255 (fletcher16's sums are mod 255, a ring homomorphism):
+//   sum1 part  A_e = sum of the record's bytes,
+//   sum2 part  sum_j (n - o_e - j) d_j = (n - o_e) A_e - J_e,  J_e = sum_j j d_j in the record,
+// with c_e = (n - o_e) mod 255 = 100 (N - e) mod 255 precomputed per entity.  The in-record weight
+// of byte b of word k is 4k + b <= 99, so doubled weights (<= 198) still fit v_dot4's u8 lanes:
+// A2 = 2 A_e and J2 = 2 J_e are one accumulating dot4 per word each.  Then
+//   x2 = c_e A2 + 2K - J2  (K = 255 * 4951 >= max J_e keeps it >= 0; x2 < 2^24),
+// and the doubled remainders 2 (x mod 255) come from one 24-bit multiply-high each
+// (as box_game.h fletcher_from_doubled).  Adds s1d = 2 (A_e mod 255), s2d = 2 (x mod 255), each < 510.
+constexpr uint32_t kJ2Bias = 2u * 255u * 4951u;
 
-// The in-record weight of byte b of word k is 4k + b <= 99, so both sums are one accumulating
-// dot4 per word: A += dot4(w_k, 1111), J += dot4(w_k, [4k, 4k+1, 4k+2, 4k+3]).
-__device__ inline void fletcher_entity(FletcherAcc& acc, const uint32_t (&w)[kFields], uint64_t n_minus_o) {
-  uint32_t a = 0, j = 0;
+__device__ inline uint32_t mad_u24(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ inline uint32_t rem255_doubled(uint32_t x2) {  // 2 (x mod 255) for x2 = 2x < 2^24
+  const uint32_t q = mulhi_u24(x2, 0x808081u);
+  uint32_t r;
+  const int32_t m510 = -510;
+  asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(q), "s"(m510), "v"(x2));
+  return r;
+}
+__device__ inline void fletcher_entity_mod(uint32_t& s1d, uint32_t& s2d, const uint32_t (&w)[kFields], uint32_t c_e) {
+  uint32_t a2 = 0, j2 = 0;
 #pragma unroll
   for (int k = 0; k < kFields; k++) {
-    a = __builtin_amdgcn_udot4(w[k], 0x01010101u, a, false);
-    j = __builtin_amdgcn_udot4(w[k], 0x03020100u + 0x04040404u * (uint32_t)k, j, false);
+    a2 = __builtin_amdgcn_udot4(w[k], 0x02020202u, a2, false);
+    j2 = __builtin_amdgcn_udot4(w[k], 0x06040200u + 0x08080808u * (uint32_t)k, j2, false);
   }
-  acc.s1 += a;
-  acc.s2pos += n_minus_o * (uint64_t)a;
-  acc.s2neg += j;
+  s1d += rem255_doubled(a2);
+  s2d += rem255_doubled(mad_u24(c_e, a2, kJ2Bias) - j2);
 }
 
 }  // namespace particles

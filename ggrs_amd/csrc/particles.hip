@@ -4,9 +4,11 @@
 //
 // One workgroup per session.  Each thread owns units of E consecutive entities (E = 1, 2 or 4;
 // E-dword loads/stores per field) and keeps a unit in registers across one call's replay: Load
-// (1 read of the unit), cd x (Save, Advance), Save of the current frame, the new frame's Advance.  HBM per call and session = S (load) + cd * S (saves), S = 4 + 100 N bytes --
-// per resimulated frame S * (1 + 1/cd).  The Fletcher-16 of every saved frame is reduced in
-// registers (64-bit closed form), across the wavefront by shuffles and across the workgroup in LDS.
+// (1 read of the unit), cd x (Save, Advance), Save of the current frame, the new frame's Advance.
+// HBM per call and session = S (load) + cd * S (saves), S = 4 + 100 N bytes -- per resimulated
+// frame S * (1 + 1/cd); the post-call state is not stored (it is Advance(saved cell f, input f),
+// materialised when the host reads it).  The Fletcher-16 of every saved frame is reduced mod 255
+// per entity in registers, accumulated per lane in LDS and summed over the workgroup once per call.
 //
 // HBM layout: a state record is [ceil(N/256) tiles][25 fields][256 entities] u32 (tile-major,
 // field-major inside a tile, entity fastest), so one block-step's saves of 256 entities are one
@@ -120,70 +122,64 @@ __device__ inline void advance_unit(uint32_t (&w)[E][kFields], uint32_t in_word,
 #pragma unroll
   for (int j = 0; j < E; j++) advance_entity<Lean>(w[j], (in_word >> (8 * ((e0 + j) % P))) & 0xffu);
 }
+// Fletcher partials of one unit (fletcher_entity_mod), added to the lane's own LDS slots of the
+// saved frame (ds_add, no cross-lane traffic in the replay loop).
 template <int E>
-__device__ inline void fletcher_unit(FletcherAcc& a, const uint32_t (&w)[E][kFields], int32_t N, int32_t e0) {
+__device__ inline void fletcher_unit(uint32_t* slot_s1, uint32_t* slot_s2, const uint32_t (&w)[E][kFields],
+                                     const uint32_t (&ce)[E]) {
+  uint32_t s1d = 0, s2d = 0;
 #pragma unroll
-  for (int j = 0; j < E; j++) fletcher_entity(a, w[j], (uint64_t)kEntityBytes * (uint64_t)(N - (e0 + j)));
+  for (int j = 0; j < E; j++) fletcher_entity_mod(s1d, s2d, w[j], ce[j]);
+  atomicAdd(slot_s1, s1d);
+  atomicAdd(slot_s2, s2d);
 }
 
-// Wavefront sum of one quad-frame's Fletcher partials, added by lane 0 to the wave's LDS slot of
-// that frame (each wave owns its slots: no atomics).  Every lane of the wave must call it.
-__device__ inline void wave_accumulate(const FletcherAcc& a, uint64_t* slot3) {
-  uint64_t s1 = a.s1, s2p = a.s2pos, s2n = a.s2neg;
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) {
-    s1 += (uint64_t)__shfl_xor((long long)s1, m, 64);
-    s2p += (uint64_t)__shfl_xor((long long)s2p, m, 64);
-    s2n += (uint64_t)__shfl_xor((long long)s2n, m, 64);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    slot3[0] += s1;
-    slot3[1] += s2p;
-    slot3[2] += s2n;
-  }
-}
-
-// checksum of one frame from the block totals plus the frame counter at byte offset 0
-__device__ inline uint16_t finish_checksum(uint64_t s1, uint64_t s2pos, uint64_t s2neg, int32_t frame, int32_t N) {
+// checksum of one frame from the block's sums of doubled per-entity remainders (t1d, t2d: even,
+// < 510 N) plus the frame counter at byte offset 0 (sum1 += A_f, sum2 += n A_f - B_f)
+__device__ inline uint16_t finish_checksum(uint32_t t1d, uint32_t t2d, int32_t frame, int32_t N) {
   const uint64_t n = 4 + (uint64_t)kEntityBytes * N;
   const uint32_t fw = (uint32_t)frame;
   const uint32_t a = __builtin_amdgcn_udot4(fw, 0x01010101u, 0u, false);
-  const uint32_t b = __builtin_amdgcn_udot4(fw, 0x03020100u, 0u, false);
-  const uint64_t t1 = s1 + a;
-  const uint64_t t2 = s2pos + n * a - s2neg - b;  // sum_j (n - j) d_j >= 0
+  const uint32_t b = __builtin_amdgcn_udot4(fw, 0x03020100u, 0u, false);  // <= 1530
+  const uint64_t t1 = (uint64_t)(t1d >> 1) + a;
+  const uint64_t t2 = (uint64_t)(t2d >> 1) + n * a + 1530u - b;  // + 6 * 255 keeps it >= 0
   return (uint16_t)(((t2 % 255u) << 8) | (t1 % 255u));
 }
 
 constexpr int kWaves = kBlock / 64;
 
+// dynamic LDS of pw_synctest_kernel: per lane and saved frame of a call, two u32 Fletcher sums
+inline size_t pw_lds_bytes(int32_t cd) { return (size_t)(cd + 1) * 2 * kBlock * sizeof(uint32_t); }
+
 // One call's replay of one unit (E entities) from its loaded frame g0: Save(g) + Fletcher
-// (skipped for i = 0 on a replay: that cell was just loaded), Advance.  Every lane of the wave
-// runs it (the Fletcher partials are summed by shuffles); `on` lanes own a unit.
+// (skipped for i = 0 on a replay: that cell was just loaded), Advance.  Only `on` lanes (owning
+// a unit) do anything; slots = the lane's LDS column, [frame i][s1, s2] with stride kBlock.
 template <int E, bool Lean>
 __device__ inline void replay_unit(uint32_t (&w)[E][kFields], const PWParams& p, int64_t s, int32_t g0,
-                                   int32_t steps, bool save_first, uint32_t in_cur, bool on, int32_t q,
-                                   uint64_t (*acc)[3]) {
+                                   int32_t steps, bool save_first, uint32_t in_cur, int32_t q, uint32_t* slots) {
   const size_t rec = pw_rec(p.N);
   const int32_t e0 = E * q;
+  uint32_t ce[E];
+#pragma unroll
+  for (int j = 0; j < E; j++) ce[j] = (uint32_t)(((int64_t)kEntityBytes * (p.N - (e0 + j))) % 255);
   for (int32_t i = 0; i <= steps; ++i) {
-    const int32_t g = g0 + i;  // frame the quad holds
+    const int32_t g = g0 + i;  // frame the unit holds
     if (p.cd > 0 && (i > 0 || save_first)) {  // SaveGameState(g): the replay's saves, then save current
-      FletcherAcc a{0, 0, 0};
-      if (on) {
-        uint32_t* dst = p.ring + ((size_t)(g % p.R) * p.L + s) * rec;
-        if (p.nt_saves) store_unit<E, true>(w, dst, q);
-        else store_unit<E, false>(w, dst, q);
-        fletcher_unit<E>(a, w, p.N, e0);
-      }
-      wave_accumulate(a, acc[i]);
+      uint32_t* dst = p.ring + ((size_t)(g % p.R) * p.L + s) * rec;
+      if (p.nt_saves) store_unit<E, true>(w, dst, q);
+      else store_unit<E, false>(w, dst, q);
+      fletcher_unit<E>(slots + (2 * i) * kBlock, slots + (2 * i + 1) * kBlock, w, ce);
     }
-    if (on) advance_unit<E, Lean>(w, i < steps ? p.inputs[(int64_t)(g % p.cap) * p.L + s] : in_cur, p.P, e0);
+    advance_unit<E, Lean>(w, i < steps ? p.inputs[(int64_t)(g % p.cap) * p.L + s] : in_cur, p.P, e0);
   }
 }
 
 template <int E>
 __global__ __launch_bounds__(kBlock) void pw_synctest_kernel(PWParams p) {
-  __shared__ uint64_t lds_acc[kWaves][kMaxCd + 1][3];  // per wave, per saved frame: s1, s2+, s2-
+  // per lane, per saved frame i of a call: sums of the doubled Fletcher remainders (s1, s2) of
+  // the lane's units, [cd + 1][2][kBlock] u32 (dynamic: pw_lds_bytes)
+  extern __shared__ uint32_t lds_slots[];
+  __shared__ uint32_t lds_tot[kMaxCd + 1][2];
   __shared__ int32_t lds_stop;
   const int64_t s = blockIdx.x;
   if (p.lane_status[s] != GGRS_LANE_RUNNING) return;
@@ -222,50 +218,58 @@ __global__ __launch_bounds__(kBlock) void pw_synctest_kernel(PWParams p) {
         return;
       }
     }
-    for (int k = threadIdx.x; k < kWaves * (kMaxCd + 1) * 3; k += kBlock) (&lds_acc[0][0][0])[k] = 0;
-    __syncthreads();
+    uint32_t* slots = lds_slots + threadIdx.x;  // this lane's column: only it touches it until the sums
+    for (int k = 0; k < 2 * (cd + 1); k++) slots[k * kBlock] = 0;
     const uint32_t in_cur = p.inputs[(int64_t)(f % p.cap) * L + s];
     const int32_t g0 = replay ? f - cd : f;
-    const bool last_call = f == p.f0 + p.n - 1;
-    for (int32_t qb = 0; qb < nq; qb += kBlock) {  // wave-uniform trip count (shuffles inside)
-      const int32_t q = qb + threadIdx.x;
-      const bool on = q < nq;
+    for (int32_t q = threadIdx.x; q < nq; q += kBlock) {
       uint32_t w[E][kFields];
-      if (on) {
-        if (replay) {  // LoadGameState(f - cd)
-          load_unit<E>(w, p.ring + ((size_t)(g0 % R) * L + s) * rec, q);
-          if (s == p.corrupt_lane && f == p.corrupt_frame && q == 0) w[0][0] ^= 1u;
-        } else {
-          load_unit<E>(w, cur, q);  // the handler's current state (warm-up calls)
-        }
+      if (replay) {  // LoadGameState(f - cd)
+        load_unit<E>(w, p.ring + ((size_t)(g0 % R) * L + s) * rec, q);
+        if (s == p.corrupt_lane && f == p.corrupt_frame && q == 0) w[0][0] ^= 1u;
       } else {
-#pragma unroll
-        for (int j = 0; j < E; j++)
-#pragma unroll
-          for (int k = 0; k < kFields; k++) w[j][k] = 0;
+        load_unit<E>(w, cur, q);  // the handler's current state (warm-up calls)
       }
       const int32_t steps = replay ? cd : 0;
       // one domain test per loaded unit: the lean step keeps rot in [+0, 2pi], so the whole
-      // replay runs in the form the loaded rotations allow (wave-uniform)
+      // replay runs in the form the loaded rotations allow
       bool dom = true;
 #pragma unroll
       for (int j = 0; j < E; j++) dom = dom && w[j][4] <= kTwoPiBits;
-      if (__builtin_expect(__all(dom), 1))
-        replay_unit<E, true>(w, p, s, g0, steps, !replay, in_cur, on, q, lds_acc[wave]);
-      else
-        replay_unit<E, false>(w, p, s, g0, steps, !replay, in_cur, on, q, lds_acc[wave]);
-      // the game state after the call; a later call of this launch reloads from the ring, so
-      // only the last call's (or a warm-up call's) result has a reader
-      if (on && (!replay || last_call)) store_unit<E, false>(w, cur, q);
+      if (__builtin_expect(dom, 1)) replay_unit<E, true>(w, p, s, g0, steps, !replay, in_cur, q, slots);
+      else replay_unit<E, false>(w, p, s, g0, steps, !replay, in_cur, q, slots);
+      // the game state after the call.  A replay call's result is Advance(ring cell f, input f),
+      // both of which stay in place until the next call: the next call reloads from the ring, and
+      // the host materialises `cur` on demand (pw_materialize_kernel), so only warm-up calls,
+      // whose successor reads `cur`, store it.
+      if (!replay) store_unit<E, false>(w, cur, q);
+    }
+    __syncthreads();
+    // block sums of the saved frames' slots: wave v sums frames i = v, v + kWaves, ...
+    const int i_lo = replay ? 1 : 0, i_hi = replay ? cd : 0;
+    if (cd > 0) {
+      for (int i = i_lo + wave; i <= i_hi; i += kWaves) {
+        uint32_t t1 = 0, t2 = 0;
+        for (int l = threadIdx.x & 63; l < kBlock; l += 64) {
+          t1 += lds_slots[(2 * i) * kBlock + l];
+          t2 += lds_slots[(2 * i + 1) * kBlock + l];
+        }
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) {
+          t1 += (uint32_t)__shfl_xor((int)t1, m, 64);
+          t2 += (uint32_t)__shfl_xor((int)t2, m, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+          lds_tot[i][0] = t1;
+          lds_tot[i][1] = t2;
+        }
+      }
     }
     __syncthreads();
     if (cd > 0 && threadIdx.x == 0) {
-      for (int i = replay ? 1 : 0; i <= (replay ? cd : 0); i++) {
-        uint64_t t[3] = {0, 0, 0};
-        for (int wv = 0; wv < kWaves; wv++)
-          for (int c = 0; c < 3; c++) t[c] += lds_acc[wv][i][c];
+      for (int i = i_lo; i <= i_hi; i++) {
         const int32_t g = g0 + i;
-        const uint16_t ck = finish_checksum(t[0], t[1], t[2], g, N);
+        const uint16_t ck = finish_checksum(lds_tot[i][0], lds_tot[i][1], g, N);
         p.ring_ck[(int64_t)(g % R) * L + s] = ck;
         p.ring_frame[(int64_t)(g % R) * L + s] = g;
         if (g == f) p.first_ck[(int64_t)(f % R) * L + s] = ck;  // first sighting of frame f
@@ -273,6 +277,22 @@ __global__ __launch_bounds__(kBlock) void pw_synctest_kernel(PWParams p) {
     }
     if (threadIdx.x == 0) p.cur_frame[s] = f + 1;
     __syncthreads();
+  }
+}
+
+// The handler's current state after a replay call f: Advance(ring cell f, input f) -- what the
+// call computed last and did not store (pw_synctest_kernel).  Halted sessions keep the state the
+// mismatch path stored.
+__global__ __launch_bounds__(kBlock) void pw_materialize_kernel(PWParams p, int32_t f) {
+  const int64_t s = blockIdx.x;
+  if (p.lane_status[s] != GGRS_LANE_RUNNING) return;
+  const size_t rec = pw_rec(p.N);
+  const uint32_t in = p.inputs[(int64_t)(f % p.cap) * p.L + s];
+  for (int32_t q = threadIdx.x; q < p.N; q += kBlock) {
+    uint32_t w[1][kFields];
+    load_unit<1>(w, p.ring + ((size_t)(f % p.R) * p.L + s) * rec, q);
+    advance_unit<1, false>(w, in, p.P, q);
+    store_unit<1, false>(w, p.cur + (size_t)s * rec, q);
   }
 }
 
@@ -298,6 +318,7 @@ struct ggrs_particle_engine {
   int32_t corrupt_lane = -1, corrupt_frame = -1;
   int32_t nt_saves = 1;  // GGRS_PW_STORE=plain selects plain stores for the ring saves
   int32_t ept = 1;       // entities per thread (1, 2, 4); GGRS_PW_EPT selects (1: 4 waves/SIMD, no scratch)
+  bool cur_stale = false;  // the last call was a replay: `cur` is materialised on read
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<hipEvent_t> tev;
   size_t tev_used = 0;
@@ -379,6 +400,12 @@ int ggrs_particle_engine_create(const ggrs_particle_config_t* cfg, ggrs_particle
   CTRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
   CTRY(hipEventCreate(&e->ev0));
   CTRY(hipEventCreate(&e->ev1));
+  if (pw_lds_bytes(c.check_distance) > 65536) {  // large check distances: past the default 64 KB
+    const int lds = (int)pw_lds_bytes(c.check_distance);
+    CTRY(hipFuncSetAttribute((const void*)pw_synctest_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    CTRY(hipFuncSetAttribute((const void*)pw_synctest_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    CTRY(hipFuncSetAttribute((const void*)pw_synctest_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  }
   CTRY(hipMalloc(&e->cur, 4 * rec * L));
   CTRY(hipMalloc(&e->cur_frame, 4 * L));
   CTRY(hipMalloc(&e->ring, 4 * rec * L * e->R));
@@ -478,12 +505,14 @@ int ggrs_particle_synctest_advance_frames(ggrs_particle_engine_t* e, int32_t n) 
     e->tev_used += 2;
   }
   HIP_TRY(hipEventRecord(a, e->stream));
-  if (e->ept == 1) pw_synctest_kernel<1><<<p.L, kBlock, 0, e->stream>>>(p);
-  else if (e->ept == 2) pw_synctest_kernel<2><<<p.L, kBlock, 0, e->stream>>>(p);
-  else pw_synctest_kernel<4><<<p.L, kBlock, 0, e->stream>>>(p);
+  const size_t lds = pw_lds_bytes(p.cd);
+  if (e->ept == 1) pw_synctest_kernel<1><<<p.L, kBlock, lds, e->stream>>>(p);
+  else if (e->ept == 2) pw_synctest_kernel<2><<<p.L, kBlock, lds, e->stream>>>(p);
+  else pw_synctest_kernel<4><<<p.L, kBlock, lds, e->stream>>>(p);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(b, e->stream));
   e->current_frame += n;
+  e->cur_stale = p.cd > 0 && e->current_frame - 1 > p.cd;  // the last call was a replay
   return GGRS_OK;
 }
 
@@ -524,6 +553,21 @@ int ggrs_particle_read_state(ggrs_particle_engine_t* e, int32_t session, uint8_t
   HIP_TRY(hipSetDevice(e->cfg.device));
   const int32_t N = e->cfg.num_entities;
   const size_t rec = pw_rec(N);
+  if (e->cur_stale) {  // the handler's state after the last (replay) call, for every running session
+    PWParams p{};
+    p.L = e->cfg.num_sessions;
+    p.N = N;
+    p.R = e->R;
+    p.cap = e->cap;
+    p.P = e->cfg.num_players;
+    p.cur = e->cur;
+    p.ring = e->ring;
+    p.inputs = e->inputs;
+    p.lane_status = e->lane_status;
+    pw_materialize_kernel<<<p.L, kBlock, 0, e->stream>>>(p, e->current_frame - 1);
+    HIP_TRY(hipGetLastError());
+    e->cur_stale = false;
+  }
   std::vector<uint32_t> soa(rec);
   int32_t frame = 0;
   HIP_TRY(hipMemcpyAsync(soa.data(), e->cur + rec * session, 4 * rec, hipMemcpyDeviceToHost, e->stream));

@@ -58,3 +58,27 @@ def test_particles_mismatch(oracle, monkeypatch, ept):
     assert mf[1] == r["result"].mismatch_frame == call + 1
     assert int(mm[1]) == int(r["result"].mismatch_mask)
     assert bytes(eng.state(1)) == bytes(r["final_state"])
+
+
+@pytest.mark.parametrize("ept", ["1", "4"])
+def test_particles_state_between_launches(oracle, monkeypatch, ept):
+    """The post-call state of a replay call is materialised on read (Advance of the saved cell):
+    reading it between launches, in warm-up and in steady state, must equal the oracle's state
+    after that many frames, and must not disturb the following launches."""
+    from ggrs_amd import ParticleEngine
+    monkeypatch.setenv("GGRS_PW_EPT", ept)
+    S, N, P, maxp, cd = 3, 300, 2, 6, 5
+    chunks = [2, 4, 1, 7, 9]  # ends at frames 2 (warm-up), 6 (first replay), 7, 14, 23
+    frames = sum(chunks)
+    inp = inputs_for(oracle, S, frames, P)
+    eng = ParticleEngine(S, N, P, maxp, cd, input_capacity=frames + cd + 2)
+    eng.add_local_inputs(inp)
+    done = 0
+    for n in chunks:
+        eng.synctest_advance_frames(n)
+        done += n
+        for s in (0, S - 1):
+            r = oracle.particles_synctest_run(inp[:done, s, :], N, P, maxp, cd, session=s, ring_states=False)
+            assert bytes(eng.state(s)) == bytes(r["final_state"]), (s, done)
+    st, _, _ = eng.mismatches()
+    assert (st == 0).all()
