@@ -631,6 +631,11 @@ def main():
                                                 input_delay=delay, model=O.MODEL_HELD,
                                                 seed_base=synth.SEED_BASE)
                 gpu_tr = eng.trace(total_frames - trace_cap, trace_cap)[:, 0]
+                # the same loop on one thread beside the multi-thread run
+                frames1 = max(args.cpu_frames // 3, total_frames)
+                n1, wall1, _ = O.synctest_bench(1, frames1, warmup=0, num_players=P, max_prediction=maxp,
+                                                check_distance=cd, input_delay=delay, model=O.MODEL_HELD,
+                                                seed_base=synth.SEED_BASE)
                 cpu_baseline = {
                     "value": round(n / wall, 1), "unit": "session-frames/s", "cores": threads,
                     "kind": "port",
@@ -639,6 +644,8 @@ def main():
                               f"reference loop (oracle/ggrs_oracle.c)",
                     "wall_s": round(wall, 3), "cpu": cpu_model(),
                     "thread0_matches_gpu_lane0": bool((ck0[total_frames - trace_cap:total_frames] == gpu_tr).all()),
+                    "single_thread": {"value": round(n1 / wall1, 1), "cores": 1, "frames": frames1,
+                                      "wall_s": round(wall1, 3)},
                 }
         except Exception as exc:  # the oracle is optional on the measurement path
             parity = {"error": repr(exc)}
