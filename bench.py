@@ -536,7 +536,7 @@ def main():
     ap.add_argument("--peers", action="store_true",
                     help="configs 3/4 and p2p: rank r and r + world/2 run the same sessions (the two "
                          "machines of a match) and compare checksums exchanged over the process group")
-    ap.add_argument("--p2p-form", choices=["flat", "lockstep", "unstaged"], default="flat",
+    ap.add_argument("--p2p-form", choices=["default", "flat", "lockstep", "unstaged"], default="default",
                     help="p2p: kernel form (DESIGN.md section 3)")
     ap.add_argument("--workload", choices=["synctest", "p2p", "codec"], default="synctest",
                     help="p2p: the device P2P rollback decision (SURVEY.md 8f), --sessions per GPU")

@@ -23,8 +23,11 @@
 //
 // HBM layout (session-fastest SoA, as the SyncTest engine):
 //   cur      [F][S]     u32   state after the last call
-//   ring     [R][F][S]  u32   R = max_prediction + 1, slot = frame % R (sync_layer.rs:161-166)
-//   ring_ck  [R][S]     u16   fletcher16 handed to GameStateCell::save
+//   ring     [S][R][C]  u32   R = max_prediction + 1, slot = frame % R (sync_layer.rs:161-166); one
+//                            session's cells are contiguous, C = F rounded up to whole 16-byte pieces
+//                            (a save is C/4 dwordx4 stores into 1-2 cache lines that the session's
+//                            next saves complete, whatever frame the other lanes of the wave are at)
+//            (cell dword F: the fletcher16 handed to GameStateCell::save, so a save is one record)
 //   inputs   [C][S][Pp] u8    row g: local add_local_input of call g, remote inputs of frame g
 //   queue    [4][P][S]  i32   prediction.frame, prediction.input, first_incorrect, last_requested
 //   stats    rollbacks [S] i32, resim [S] i64
@@ -51,7 +54,6 @@ struct P2PParams {
   uint32_t local_mask;
   uint32_t* cur;
   uint32_t* ring;
-  uint16_t* ring_ck;
   const uint8_t* inputs;
   int32_t* queue;
   int32_t* rollbacks;
@@ -81,11 +83,45 @@ struct RemoteQueues {
   int32_t last_req[P];    // last_requested_frame
 };
 
+// dwords of one ring cell: the state's F fields and the checksum, padded to whole 16-byte pieces
+__host__ __device__ constexpr int cell_dwords(int p) { return (state_fields(p) + 1 + 3) & ~3; }
+
+template <int P>
+__device__ inline uint4* ring_cell(const P2PParams& p, int32_t slot, int64_t sess) {
+  return reinterpret_cast<uint4*>(p.ring + ((int64_t)sess * p.R + slot) * cell_dwords(P));
+}
+template <int P>
+__device__ inline void load_cell(BoxState<P>& s, const uint4* c) {
+  constexpr int F = state_fields(P);
+#pragma unroll
+  for (int k = 0; k < cell_dwords(P) / 4; k++) {
+    const uint4 v = c[k];
+    const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if (4 * k + i < F) s.w[4 * k + i] = x[i];
+  }
+}
+template <int P>
+__device__ inline void store_cell(const BoxState<P>& s, uint32_t ck, uint4* c) {
+  constexpr int F = state_fields(P);
+#pragma unroll
+  for (int k = 0; k < cell_dwords(P) / 4; k++) {
+    uint32_t x[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) x[i] = 4 * k + i < F ? s.w[4 * k + i] : (4 * k + i == F ? ck : 0u);
+    c[k] = make_uint4(x[0], x[1], x[2], x[3]);
+  }
+}
+// the checksum stored with the cell of `slot`
+template <int P>
+__device__ inline uint16_t cell_checksum(const P2PParams& p, int32_t slot, int64_t sess) {
+  return (uint16_t)(p.ring + ((int64_t)sess * p.R + slot) * cell_dwords(P))[state_fields(P)];
+}
+
 template <int P>
 __device__ inline void save_cell(const P2PParams& p, const BoxState<P>& s, int32_t frame, int64_t sess) {
-  const int32_t slot = frame % p.R;
-  store_state<P>(s, p.ring + (int64_t)slot * state_fields(P) * p.S + sess, p.S);
-  p.ring_ck[(int64_t)slot * p.S + sess] = fletcher16_state<P>(s);
+  store_cell<P>(s, fletcher16_state<P>(s), ring_cell<P>(p, frame % p.R, sess));
 }
 
 // Input rows as the calls read them: from global memory, or (staged kernel) from the block's LDS
@@ -219,7 +255,7 @@ __global__ __launch_bounds__(kP2PBlock) void p2p_kernel(P2PParams p) {
   int32_t pre_frame = kNull;
   auto prefetch = [&](int32_t fr) {
     if (!p.sparse && fr >= 0) {
-      load_state<P>(pre, p.ring + (int64_t)(fr % p.R) * state_fields(P) * S + sess, S);
+      load_cell<P>(pre, ring_cell<P>(p, fr % p.R, sess));
       pre_frame = fr;
     }
   };
@@ -232,7 +268,7 @@ __global__ __launch_bounds__(kP2PBlock) void p2p_kernel(P2PParams p) {
     if (p.desync_interval > 0 && live) {
       const int32_t fts = f - 1 - p.D;
       if (fts >= p.desync_interval && fts % p.desync_interval == 0)
-        p.hist[(int64_t)((fts / p.desync_interval) % kHist) * S + sess] = p.ring_ck[(int64_t)(fts % p.R) * S + sess];
+        p.hist[(int64_t)((fts / p.desync_interval) % kHist) * S + sess] = cell_checksum<P>(p, fts % p.R, sess);
     }
     // 1. poll_remote_clients: the remote input of frame g = f - D (add_input_by_frame)
     const int32_t g = f - p.D;
@@ -259,7 +295,7 @@ __global__ __launch_bounds__(kP2PBlock) void p2p_kernel(P2PParams p) {
     auto adjust = [&](int32_t first_incorrect) {
       const int32_t load = p.sparse ? last_saved : first_incorrect;  // sparse: the last save
       if (load == pre_frame) st = pre;
-      else load_state<P>(st, p.ring + (int64_t)(load % p.R) * state_fields(P) * S + sess, S);
+      else load_cell<P>(st, ring_cell<P>(p, load % p.R, sess));
 #pragma unroll
       for (int k = 0; k < P; k++) {  // reset_prediction (input_queue.rs:63-67)
         q.pred_frame[k] = kNull;
@@ -330,11 +366,13 @@ __global__ __launch_bounds__(kP2PBlock) void p2p_kernel(P2PParams p) {
 // calls as in the staged form (rows [stage start - back, stage end)), all lanes meeting at the
 // stage end.
 constexpr int kFlatBlock = 64;
-constexpr size_t kFlatRingBytes = (size_t)28 << 20;  // default form: flat while the ring fits L2
+// rows per stage: a wave's steps in a stage are its slowest session's, so fewer, longer stages
+// cost less (128 rows: one stage per 64-call launch at back = 6)
+constexpr int kFlatRows = 128;
 
 template <int P>
 struct LdsRowsFlat {
-  const uint8_t* lds;  // [kP2PRows][kFlatBlock][Pp]
+  const uint8_t* lds;  // [kFlatRows][kFlatBlock][Pp]
   int32_t lo;
   int tid;
   __device__ inline uint32_t operator()(int32_t g) const {
@@ -346,7 +384,7 @@ struct LdsRowsFlat {
 template <int P>
 __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
   constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
-  __shared__ __attribute__((aligned(16))) uint8_t lds_rows[kP2PRows * kFlatBlock * Pp];
+  __shared__ __attribute__((aligned(16))) uint8_t lds_rows[kFlatRows * kFlatBlock * Pp];
   const int64_t sess0 = (int64_t)blockIdx.x * kFlatBlock;
   const int64_t S = p.S;
   const bool live = sess0 + threadIdx.x < S;
@@ -372,13 +410,13 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
   int32_t pre_frame = kNull;
   auto prefetch = [&](int32_t fr) {
     if (fr >= 0) {
-      load_state<P>(pre, p.ring + (int64_t)(fr % p.R) * state_fields(P) * S + sess, S);
+      load_cell<P>(pre, ring_cell<P>(p, fr % p.R, sess));
       pre_frame = fr;
     }
   };
   prefetch(p.f0 - p.D);
   const int32_t f_end = p.f0 + p.n;
-  const int32_t calls_per_stage = kP2PRows - back;  // >= 1 (host)
+  const int32_t calls_per_stage = kFlatRows - back;  // >= 1 (host)
   for (int32_t fs = p.f0; fs < f_end;) {
     const int32_t chunk_end = min(f_end, fs + calls_per_stage);
     const int32_t lo = max(0, fs - back);
@@ -411,7 +449,7 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
         if (p.desync_interval > 0 && live) {
           const int32_t fts = f - 1 - p.D;
           if (fts >= p.desync_interval && fts % p.desync_interval == 0)
-            p.hist[(int64_t)((fts / p.desync_interval) % kHist) * S + sess] = p.ring_ck[(int64_t)(fts % p.R) * S + sess];
+            p.hist[(int64_t)((fts / p.desync_interval) % kHist) * S + sess] = cell_checksum<P>(p, fts % p.R, sess);
         }
         // 1. poll_remote_clients: the remote input of frame g = f - D (add_input_by_frame)
         const int32_t g = f - p.D;
@@ -439,7 +477,7 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
         if (first_inc != kNull) {
           load = first_inc;
           if (load == pre_frame) st = pre;
-          else load_state<P>(st, p.ring + (int64_t)(load % p.R) * state_fields(P) * S + sess, S);
+          else load_cell<P>(st, ring_cell<P>(p, load % p.R, sess));
 #pragma unroll
           for (int k = 0; k < P; k++) {  // reset_prediction (input_queue.rs:63-67)
             q.pred_frame[k] = kNull;
@@ -515,7 +553,6 @@ struct ggrs_p2p_engine {
   hipStream_t stream = nullptr;
   uint32_t* cur = nullptr;
   uint32_t* ring = nullptr;
-  uint16_t* ring_ck = nullptr;
   uint8_t* inputs = nullptr;
   int32_t* queue = nullptr;
   int32_t* rollbacks = nullptr;
@@ -579,7 +616,7 @@ int ggrs_p2p_engine_destroy(ggrs_p2p_engine_t* e) {
   if (!e) return GGRS_OK;
   (void)hipSetDevice(e->cfg.device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
-  void* bufs[] = {e->cur, e->ring, e->ring_ck, e->inputs, e->queue, e->rollbacks, e->resim, e->trace, e->staging,
+  void* bufs[] = {e->cur, e->ring, e->inputs, e->queue, e->rollbacks, e->resim, e->trace, e->staging,
                   e->hist, e->cmp_mask, e->cmp_count, e->last_saved, e->ring_frame};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -635,15 +672,13 @@ int ggrs_p2p_engine_create(const ggrs_p2p_config_t* cfg, ggrs_p2p_engine_t** out
   CTRY(hipEventCreate(&e->ev0));
   CTRY(hipEventCreate(&e->ev1));
   CTRY(hipMalloc(&e->cur, sizeof(uint32_t) * e->F * S));
-  CTRY(hipMalloc(&e->ring, sizeof(uint32_t) * (size_t)e->R * e->F * S));
-  CTRY(hipMalloc(&e->ring_ck, sizeof(uint16_t) * (size_t)e->R * S));
+  CTRY(hipMalloc(&e->ring, sizeof(uint32_t) * (size_t)e->R * cell_dwords(P) * S));
   CTRY(hipMalloc(&e->inputs, (size_t)e->cap * S * e->Pp));
   CTRY(hipMalloc(&e->queue, sizeof(int32_t) * 4 * P * S));
   CTRY(hipMalloc(&e->rollbacks, sizeof(int32_t) * S));
   CTRY(hipMalloc(&e->resim, sizeof(int64_t) * S));
   if (c.trace_capacity > 0) CTRY(hipMalloc(&e->trace, sizeof(uint16_t) * (size_t)c.trace_capacity * S));
-  CTRY(hipMemsetAsync(e->ring, 0, sizeof(uint32_t) * (size_t)e->R * e->F * S, e->stream));
-  CTRY(hipMemsetAsync(e->ring_ck, 0, sizeof(uint16_t) * (size_t)e->R * S, e->stream));
+  CTRY(hipMemsetAsync(e->ring, 0, sizeof(uint32_t) * (size_t)e->R * cell_dwords(P) * S, e->stream));
   CTRY(hipMemsetAsync(e->inputs, 0, (size_t)e->cap * S * e->Pp, e->stream));
   CTRY(hipMemsetAsync(e->rollbacks, 0, sizeof(int32_t) * S, e->stream));
   CTRY(hipMemsetAsync(e->resim, 0, sizeof(int64_t) * S, e->stream));
@@ -716,7 +751,6 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
   p.local_mask = (uint32_t)e->cfg.local_mask;
   p.cur = e->cur;
   p.ring = e->ring;
-  p.ring_ck = e->ring_ck;
   p.inputs = e->inputs;
   p.queue = e->queue;
   p.rollbacks = e->rollbacks;
@@ -736,13 +770,11 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
     // stage input rows in LDS unless a call reaches further back than a stage holds
     const int32_t back = (e->sparse ? e->R - 1 : p.D) + p.delay;
     const bool staged = back + 1 <= kP2PRows - 1 && e->form != 1;
-    // the flat form's waves save into up to R ring slots per store instruction (lanes sit at
-    // different frames): while the ring fits the XCDs' L2 (4 MiB each, sessions spread over the 8)
-    // those partial lines merge there and the flat form wins (1.58e10 vs 1.29e10 session-frames/s
-    // at 65,536 sessions); past it they go out partial and the lockstep form is faster (1.97e10
-    // vs 1.04e10 at 131,072) -- measured on one MI355X, DESIGN.md section 5
-    const size_t ring_bytes = (size_t)e->R * (size_t)p.S * (4u * (size_t)e->F + 2u);
-    const bool flat = staged && !e->sparse && (e->form == 0 ? ring_bytes <= kFlatRingBytes : false);
+    // the flat form by default: with the session-major ring its saves stay whole cache lines
+    // whatever frame each lane is at (1.82e10 vs lockstep 1.26e10 session-frames/s at 65,536
+    // sessions, 1.98e10 vs 1.89e10 at 131,072; with the frame-major ring of round 1 the flat
+    // form's partial lines went out to HBM 3.5x over -- DESIGN.md section 5)
+    const bool flat = staged && !e->sparse && (e->form == 0 || e->form == 3);
     dispatch_players(e->cfg.num_players, [&](auto PC) {
       constexpr int P = decltype(PC)::value;
       if (flat) p2p_flat_kernel<P><<<grid_of(p.S, kFlatBlock), kFlatBlock, 0, e->stream>>>(p);
@@ -790,7 +822,8 @@ int ggrs_p2p_set_sparse_saving(ggrs_p2p_engine_t* e, int32_t on) {
 
 int ggrs_p2p_set_unstaged(ggrs_p2p_engine_t* e, int32_t form) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
-  if (form < 0 || form > 2) return set_error(GGRS_E_INVALID, "kernel form %d (0 default, 1 unstaged, 2 lockstep)", form);
+  if (form < 0 || form > 3)
+    return set_error(GGRS_E_INVALID, "kernel form %d (0 default, 1 unstaged, 2 lockstep, 3 flat)", form);
   e->form = form;
   return GGRS_OK;
 }
@@ -870,11 +903,12 @@ int ggrs_p2p_synchronize(ggrs_p2p_engine_t* e) {
   return GGRS_OK;
 }
 
-static int read_record(ggrs_p2p_engine_t* e, const uint32_t* base, int64_t s, uint8_t* out) {
-  const int64_t S = e->cfg.num_sessions;
+// field k of the record at base[k * stride] (cur: stride S from the session's lane; ring: the
+// session's contiguous cell, stride 1)
+static int read_record(ggrs_p2p_engine_t* e, const uint32_t* base, int64_t stride, uint8_t* out) {
   std::vector<uint32_t> w(e->F);
   for (int k = 0; k < e->F; k++)
-    HIP_TRY(hipMemcpyAsync(&w[k], base + (int64_t)k * S + s, 4, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipMemcpyAsync(&w[k], base + (int64_t)k * stride, 4, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   serialize_state_bytes(w.data(), e->cfg.num_players, out);
   return GGRS_OK;
@@ -884,7 +918,7 @@ int ggrs_p2p_read_state(ggrs_p2p_engine_t* e, int32_t session, uint8_t* out) {
   if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
   if (session < 0 || session >= e->cfg.num_sessions) return set_error(GGRS_E_INVALID, "session out of range");
   HIP_TRY(hipSetDevice(e->cfg.device));
-  return read_record(e, e->cur, session, out);
+  return read_record(e, e->cur + session, e->cfg.num_sessions, out);
 }
 
 int ggrs_p2p_read_ring(ggrs_p2p_engine_t* e, int32_t session, int32_t* frames, uint16_t* checksums, uint8_t* states) {
@@ -908,13 +942,15 @@ int ggrs_p2p_read_ring(ggrs_p2p_engine_t* e, int32_t session, int32_t* frames, u
     if (checksums) {
       checksums[slot] = 0;
       if (fr != kNull)
-        HIP_TRY(hipMemcpy(&checksums[slot], e->ring_ck + (int64_t)slot * S + session, 2, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(&checksums[slot], e->ring + ((int64_t)session * R + slot) * cell_dwords(e->cfg.num_players) +
+                                                 e->F, 2, hipMemcpyDeviceToHost));
     }
     if (states) {
       if (fr == kNull) {
         std::memset(states + slot * sb, 0, sb);
       } else {
-        int rc = read_record(e, e->ring + (int64_t)slot * e->F * S, session, states + slot * sb);
+        int rc = read_record(e, e->ring + ((int64_t)session * R + slot) * cell_dwords(e->cfg.num_players), 1,
+                             states + slot * sb);
         if (rc) return rc;
       }
     }

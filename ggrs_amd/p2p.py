@@ -195,13 +195,14 @@ class P2PEngine:
         _lib.check(self._L.ggrs_p2p_set_sparse_saving(self._h, int(bool(on))))
         self.sparse_saving = bool(on)
 
-    KERNEL_FORMS = {"flat": 0, "unstaged": 1, "lockstep": 2}
+    KERNEL_FORMS = {"default": 0, "unstaged": 1, "lockstep": 2, "flat": 3}
 
     def set_unstaged(self, on=True):
         """Calls in lockstep with input rows read from global memory (for comparison)."""
-        self.set_kernel_form("unstaged" if on else "flat")
+        self.set_kernel_form("unstaged" if on else "default")
 
     def set_kernel_form(self, form):
-        """"flat" (default: each session's calls as its own step sequence), "lockstep" (calls in
-        lockstep, rows staged in LDS) or "unstaged" (lockstep, rows from global memory)."""
+        """"default" (flat unless sparse saving), "flat" (each session's calls as its own step
+        sequence), "lockstep" (calls in lockstep, rows staged in LDS) or "unstaged" (lockstep, rows
+        from global memory)."""
         _lib.check(self._L.ggrs_p2p_set_unstaged(self._h, self.KERNEL_FORMS[form]))
