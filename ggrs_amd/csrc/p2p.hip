@@ -152,11 +152,11 @@ struct LdsRows {
 // last_added: the remote queues' last_added_frame (f - D after this call's poll, or NULL).
 template <int P, typename Rows>
 __device__ inline uint32_t sync_inputs(const P2PParams& p, RemoteQueues<P>& q, int32_t h, int32_t last_added,
-                                       const Rows& input_row) {
+                                       const Rows& input_row, uint32_t local_mask) {
   uint32_t in = 0;
   // local queues hold every frame <= f + delay: queue frame h is user input h - delay, and the
   // frames below the delay replicate the default input (input_queue.rs:233-265)
-  const uint32_t local_row = (p.local_mask && h >= p.delay) ? input_row(h - p.delay) : 0u;
+  const uint32_t local_row = (local_mask && h >= p.delay) ? input_row(h - p.delay) : 0u;
   uint32_t confirmed_row = 0u, last_row = 0u;
   const bool confirmed = last_added != kNull && h <= last_added;
   if (confirmed) confirmed_row = input_row(h);
@@ -164,7 +164,7 @@ __device__ inline uint32_t sync_inputs(const P2PParams& p, RemoteQueues<P>& q, i
 #pragma unroll
   for (int k = 0; k < P; k++) {
     uint32_t v;
-    if ((p.local_mask >> k) & 1u) {
+    if ((local_mask >> k) & 1u) {
       v = (local_row >> (8 * k)) & 0xffu;
     } else {
       q.last_req[k] = h;
@@ -190,6 +190,7 @@ __device__ inline uint32_t sync_inputs(const P2PParams& p, RemoteQueues<P>& q, i
 // runs the same calls, idle tail threads included (they never store).
 template <int P, bool kStaged>
 __global__ __launch_bounds__(kP2PBlock) void p2p_kernel(P2PParams p) {
+  const uint32_t lmask = p.local_mask;
   constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
   __shared__ __attribute__((aligned(16))) uint8_t lds_rows[kStaged ? kP2PRows * kP2PBlock * Pp : 4];
   const int64_t sess0 = (int64_t)blockIdx.x * kP2PBlock;
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(kP2PBlock) void p2p_kernel(P2PParams p) {
         q.last_req[k] = kNull;
       }
       for (int32_t h = load; h < f; ++h) {
-        const uint32_t in = sync_inputs<P>(p, q, h, last_added, input_row);
+        const uint32_t in = sync_inputs<P>(p, q, h, last_added, input_row, lmask);
         if (p.sparse ? h == confirmed : h > load) save(h);
         advance(in);
       }
@@ -322,7 +323,7 @@ __global__ __launch_bounds__(kP2PBlock) void p2p_kernel(P2PParams p) {
       if (confirmed >= f) save(f);
       else adjust(last_saved);
     }
-    const uint32_t in = sync_inputs<P>(p, q, f, last_added, input_row);
+    const uint32_t in = sync_inputs<P>(p, q, f, last_added, input_row, lmask);
     advance(in);
     if (p.trace && live) p.trace[(int64_t)(f % p.trace_cap) * S + sess] = fletcher16_state<P>(st);
     prefetch(f + 1 - p.D);
@@ -381,8 +382,13 @@ struct LdsRowsFlat {
   }
 };
 
-template <int P>
+// kLocal >= 0: the local-player mask as a compile-time constant (the two-player configurations),
+// so the per-player local/remote tests of the poll and of synchronized_inputs fold away.
+// kPlain: no desync history, display-checksum trace or debug flip in this launch (host-checked),
+// so none of their tests sits in the step loop.
+template <int P, int kLocal, bool kPlain>
 __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
+  const uint32_t lmask = kLocal >= 0 ? (uint32_t)kLocal : p.local_mask;
   constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
   __shared__ __attribute__((aligned(16))) uint8_t lds_rows[kFlatRows * kFlatBlock * Pp];
   const int64_t sess0 = (int64_t)blockIdx.x * kFlatBlock;
@@ -402,7 +408,7 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
   }
   int32_t rollbacks = 0;
   int64_t resim = 0;
-  const bool dbg = live && sess == p.dbg_sess;
+  const bool dbg = !kPlain && live && sess == p.dbg_sess;
   const int tid = live ? (int)threadIdx.x : 0;
   const int32_t back = p.D + p.delay;
   // the rollback cell of the next call (frame f + 1 - D), read at the end of call f (p2p_kernel)
@@ -446,7 +452,7 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
     while (f < chunk_end) {
       if (at_start) {
         // 0. check_checksum_send_interval (as p2p_kernel)
-        if (p.desync_interval > 0 && live) {
+        if (!kPlain && p.desync_interval > 0 && live) {
           const int32_t fts = f - 1 - p.D;
           if (fts >= p.desync_interval && fts % p.desync_interval == 0)
             p.hist[(int64_t)((fts / p.desync_interval) % kHist) * S + sess] = cell_checksum<P>(p, fts % p.R, sess);
@@ -458,7 +464,7 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
           const uint32_t row = rows(g);
 #pragma unroll
           for (int k = 0; k < P; k++) {
-            if ((p.local_mask >> k) & 1u) continue;
+            if ((lmask >> k) & 1u) continue;
             if (q.pred_frame[k] != kNull) {
               const uint32_t v = (row >> (8 * k)) & 0xffu;
               if (q.first_inc[k] == kNull && q.pred_in[k] != v) q.first_inc[k] = g;
@@ -494,7 +500,7 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
       // one step: a replayed frame h (saved unless it is the loaded one) or the call's own frame
       // f (SaveGameState(f), then AdvanceFrame with synchronized_inputs(f))
       const int32_t fr = replaying ? h : f;
-      const uint32_t in = sync_inputs<P>(p, q, fr, last_added, rows);
+      const uint32_t in = sync_inputs<P>(p, q, fr, last_added, rows, lmask);
       if (live && (!replaying || h > load)) save_cell<P>(p, st, fr, sess);
       const uint32_t from = st.w[0];
       advance_state<P>(st, in, 0u);
@@ -502,7 +508,7 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
       if (replaying) {
         if (++h == f) replaying = false;
       } else {
-        if (p.trace && live) p.trace[(int64_t)(f % p.trace_cap) * S + sess] = fletcher16_state<P>(st);
+        if (!kPlain && p.trace && live) p.trace[(int64_t)(f % p.trace_cap) * S + sess] = fletcher16_state<P>(st);
         prefetch(f + 1 - p.D);
         ++f;
         at_start = true;
@@ -777,7 +783,21 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
     const bool flat = staged && !e->sparse && (e->form == 0 || e->form == 3);
     dispatch_players(e->cfg.num_players, [&](auto PC) {
       constexpr int P = decltype(PC)::value;
-      if (flat) p2p_flat_kernel<P><<<grid_of(p.S, kFlatBlock), kFlatBlock, 0, e->stream>>>(p);
+      if (flat) {
+        const dim3 grid((unsigned)grid_of(p.S, kFlatBlock));
+        auto go = [&](auto plain_tag) {
+          constexpr bool kPl = decltype(plain_tag)::value;
+          if constexpr (P == 2) {
+            if (p.local_mask == 1u) p2p_flat_kernel<P, 1, kPl><<<grid, kFlatBlock, 0, e->stream>>>(p);
+            else if (p.local_mask == 2u) p2p_flat_kernel<P, 2, kPl><<<grid, kFlatBlock, 0, e->stream>>>(p);
+            else p2p_flat_kernel<P, -1, kPl><<<grid, kFlatBlock, 0, e->stream>>>(p);
+          } else {
+            p2p_flat_kernel<P, -1, kPl><<<grid, kFlatBlock, 0, e->stream>>>(p);
+          }
+        };
+        if (p.desync_interval == 0 && !p.trace && p.dbg_sess < 0) go(std::true_type());
+        else go(std::false_type());
+      }
       else if (staged) p2p_kernel<P, true><<<grid_of(p.S, kP2PBlock), kP2PBlock, 0, e->stream>>>(p);
       else p2p_kernel<P, false><<<grid_of(p.S, kP2PBlock), kP2PBlock, 0, e->stream>>>(p);
     });
