@@ -253,6 +253,32 @@ __device__ inline void advance_state(BoxState<P>& s, uint32_t inputs, uint32_t d
   }
 }
 
+// State::advance through advance_player_lean only: for callers that have checked once that every
+// state they step lies in the lean form's rotation domain (states this engine produced always do).
+template <int P>
+__device__ inline void advance_state_lean(BoxState<P>& s, uint32_t inputs) {
+  s.w[0] = (uint32_t)((int32_t)s.w[0] + 1);
+#pragma unroll
+  for (int i = 0; i < P; i++) {
+    float x = s.f(fld_x(P, i)), y = s.f(fld_y(P, i)), vx = s.f(fld_vx(P, i)), vy = s.f(fld_vy(P, i));
+    float rot = s.f(fld_rot(P, i));
+    advance_player_lean(x, y, vx, vy, rot, (inputs >> (8 * i)) & 0xffu);
+    s.set(fld_x(P, i), x);
+    s.set(fld_y(P, i), y);
+    s.set(fld_vx(P, i), vx);
+    s.set(fld_vy(P, i), vy);
+    s.set(fld_rot(P, i), rot);
+  }
+}
+
+template <int P>
+__device__ inline bool rot_in_domain(const BoxState<P>& s) {
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < P; i++) ok = ok && s.w[fld_rot(P, i)] <= kTwoPiBits;
+  return ok;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Fletcher-16 of the bincode encoding, without materialising the bytes.
 // fletcher16 reduces mod 255 after every byte; since x -> x mod 255 is a ring homomorphism,

@@ -421,6 +421,10 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
     }
   };
   prefetch(p.f0 - p.D);
+  // every state this launch steps descends from cur or from a ring cell, all written by this
+  // engine (or zero-initialised) and so inside the lean step's rotation domain; one wave-wide test
+  // here instead of one per player per step (a foreign state takes the general step throughout)
+  const bool lean_ok = __all(rot_in_domain<P>(st) && (pre_frame == kNull || rot_in_domain<P>(pre)));
   const int32_t f_end = p.f0 + p.n;
   const int32_t calls_per_stage = kFlatRows - back;  // >= 1 (host)
   for (int32_t fs = p.f0; fs < f_end;) {
@@ -503,7 +507,8 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
       const uint32_t in = sync_inputs<P>(p, q, fr, last_added, rows, lmask);
       if (live && (!replaying || h > load)) save_cell<P>(p, st, fr, sess);
       const uint32_t from = st.w[0];
-      advance_state<P>(st, in, 0u);
+      if (lean_ok) advance_state_lean<P>(st, in);
+      else advance_state<P>(st, in, 0u);
       if (dbg && (int32_t)from == p.dbg_frame) st.w[fld_x(P, 0)] ^= 1u;
       if (replaying) {
         if (++h == f) replaying = false;
