@@ -183,7 +183,16 @@ __global__ __launch_bounds__(kRoundsBlock) void rounds_kernel(RoundsParams rp) {
   }
   if (threadIdx.x < ns) lds_ck[threadIdx.x] = p.trunk_ck[s_first + threadIdx.x];
   bool survived = p.check_prev && in_range && ((p.prev_survive[lane >> 6] >> (lane & 63)) & 1ull);
-  __syncthreads();
+  // every state the launch steps descends from the block's trunks, which this engine produced:
+  // one block-wide test of their rotation domain instead of a wave vote per player per step
+  bool trunk_ok = true;
+  if ((int)threadIdx.x < ns) {
+    BoxState<P> t0;
+#pragma unroll
+    for (int k = 0; k < F; k++) t0.w[k] = rp.trunk[(int64_t)k * p.S + s_first + threadIdx.x];
+    trunk_ok = rot_in_domain<P>(t0);
+  }
+  const bool lean_ok = __syncthreads_and(trunk_ok);
   for (int32_t r = 0; r < rp.n; ++r) {
     SpecParams q = p;
     q.f_c = p.f_c + r;
@@ -201,7 +210,9 @@ __global__ __launch_bounds__(kRoundsBlock) void rounds_kernel(RoundsParams rp) {
       uint32_t tk = truth;
       for (int32_t k = 0; k < p.W; ++k) {
         const uint32_t next = k + 1 < p.W ? load_inputs<P>(p.inputs, (int64_t)((q.f_c + k + 1) % p.cap) * p.S + s) : 0u;
-        advance_state<P>(st, branch_inputs_from<P>(q, tk, last, b, k), 0u);  // AdvanceFrame(f_c + k)
+        const uint32_t in = branch_inputs_from<P>(q, tk, last, b, k);  // AdvanceFrame(f_c + k)
+        if (lean_ok) advance_state_lean<P>(st, in);
+        else advance_state<P>(st, in, 0u);
         const int32_t slot = (q.f_c + k + 1) % p.R;                            // SaveGameState(f_c + k + 1)
         store_state<P>(st, p.ring + (int64_t)slot * F * p.L + lane, p.L);
         p.ring_ck[(int64_t)slot * p.L + lane] = fletcher16_state<P>(st);
@@ -229,7 +240,9 @@ __global__ __launch_bounds__(kRoundsBlock) void rounds_kernel(RoundsParams rp) {
       BoxState<P> tr;
 #pragma unroll
       for (int k = 0; k < F; k++) tr.w[k] = lds_trunk[threadIdx.x][k];
-      advance_state<P>(tr, load_inputs<P>(p.inputs, (int64_t)(q.f_c % p.cap) * p.S + s2), 0u);
+      const uint32_t tin = load_inputs<P>(p.inputs, (int64_t)(q.f_c % p.cap) * p.S + s2);
+      if (lean_ok) advance_state_lean<P>(tr, tin);
+      else advance_state<P>(tr, tin, 0u);
       const uint16_t ck = fletcher16_state<P>(tr);
 #pragma unroll
       for (int k = 0; k < F; k++) lds_trunk[threadIdx.x][k] = tr.w[k];
