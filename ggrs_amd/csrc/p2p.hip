@@ -412,15 +412,26 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
   const int tid = live ? (int)threadIdx.x : 0;
   const int32_t back = p.D + p.delay;
   // the rollback cell of the next call (frame f + 1 - D), read at the end of call f (p2p_kernel)
+  // ring slots kept as counters (no integer division per step): slot_f = f % R of the session's
+  // call, slot_h = h % R of its replayed frame, pre_slot of the prefetched cell
+  uint4* const my_ring = reinterpret_cast<uint4*>(p.ring + (int64_t)sess * p.R * cell_dwords(P));
+  auto cell = [&](int32_t slot) { return my_ring + slot * (cell_dwords(P) / 4); };
+  auto next_slot = [&](int32_t x) { return x + 1 == p.R ? 0 : x + 1; };
+  int32_t slot_f = p.f0 % p.R, slot_h = 0, pre_slot = 0;
   BoxState<P> pre;
   int32_t pre_frame = kNull;
-  auto prefetch = [&](int32_t fr) {
+  // prefetch(fr, slot): fr = f + 1 - D with 1 <= D < R, so its slot is slot_f + 1 - D mod R
+  auto prefetch = [&](int32_t fr, int32_t slot) {
     if (fr >= 0) {
-      load_cell<P>(pre, ring_cell<P>(p, fr % p.R, sess));
+      load_cell<P>(pre, cell(slot));
       pre_frame = fr;
+      pre_slot = slot;
     }
   };
-  prefetch(p.f0 - p.D);
+  {
+    const int32_t s0 = slot_f - p.D;
+    prefetch(p.f0 - p.D, s0 < 0 ? s0 + p.R : s0);
+  }
   // every state this launch steps descends from cur or from a ring cell, all written by this
   // engine (or zero-initialised) and so inside the lean step's rotation domain; one wave-wide test
   // here instead of one per player per step (a foreign state takes the general step throughout)
@@ -478,7 +489,7 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
           }
         }
         // 2. the first frame's save
-        if (f == 0 && live) save_cell<P>(p, st, 0, sess);
+        if (f == 0 && live) store_cell<P>(st, fletcher16_state<P>(st), cell(0));
         // 3. check_simulation_consistency: a rollback loads first_incorrect and replays from it
         int32_t first_inc = kNull;
 #pragma unroll
@@ -486,8 +497,13 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
           if (q.first_inc[k] != kNull && (first_inc == kNull || q.first_inc[k] < first_inc)) first_inc = q.first_inc[k];
         if (first_inc != kNull) {
           load = first_inc;
-          if (load == pre_frame) st = pre;
-          else load_cell<P>(st, ring_cell<P>(p, load % p.R, sess));
+          if (load == pre_frame) {
+            st = pre;
+            slot_h = pre_slot;
+          } else {
+            slot_h = load % p.R;
+            load_cell<P>(st, cell(slot_h));
+          }
 #pragma unroll
           for (int k = 0; k < P; k++) {  // reset_prediction (input_queue.rs:63-67)
             q.pred_frame[k] = kNull;
@@ -505,16 +521,19 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
       // f (SaveGameState(f), then AdvanceFrame with synchronized_inputs(f))
       const int32_t fr = replaying ? h : f;
       const uint32_t in = sync_inputs<P>(p, q, fr, last_added, rows, lmask);
-      if (live && (!replaying || h > load)) save_cell<P>(p, st, fr, sess);
+      if (live && (!replaying || h > load)) store_cell<P>(st, fletcher16_state<P>(st), cell(replaying ? slot_h : slot_f));
       const uint32_t from = st.w[0];
       if (lean_ok) advance_state_lean<P>(st, in);
       else advance_state<P>(st, in, 0u);
       if (dbg && (int32_t)from == p.dbg_frame) st.w[fld_x(P, 0)] ^= 1u;
       if (replaying) {
+        slot_h = next_slot(slot_h);
         if (++h == f) replaying = false;
       } else {
         if (!kPlain && p.trace && live) p.trace[(int64_t)(f % p.trace_cap) * S + sess] = fletcher16_state<P>(st);
-        prefetch(f + 1 - p.D);
+        const int32_t ps = slot_f + 1 - p.D;
+        prefetch(f + 1 - p.D, ps < 0 ? ps + p.R : ps);
+        slot_f = next_slot(slot_f);
         ++f;
         at_start = true;
       }
