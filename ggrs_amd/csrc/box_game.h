@@ -187,6 +187,8 @@ __device__ inline double rcp_f64_refined(double d) {
 //     the clamp's two divisions share one refined binary64 reciprocal (rcp_f64_refined);
 //   * max(min(.)) clamps become v_med3_f32: equal for every non-NaN input without -0, and a
 //     position sum is never -0 (x >= +0, and x + v == 0 only as +0) nor NaN.
+//   * the turn's rem_euclid on [-RS, 2pi + RS] is one add or subtract of 2pi chosen by two
+//     compares (every rot in the domain, both directions: tests/native/remeuclid_kat_host.c).
 __device__ inline void advance_player_lean(float& x, float& y, float& vx, float& vy, float& rot,
                                            uint32_t input) {
   float vel_x = vx * kFriction;
@@ -204,9 +206,9 @@ __device__ inline void advance_player_lean(float& x, float& y, float& vx, float&
   vel_y = vel_y + (thrust ? dy : (brake ? -dy : -0.0f));
   const bool ccw = lr == kInputLeft, turn = ccw || lr == kInputRight;
   const float a = rot + (ccw ? -kRotationSpeed : kRotationSpeed);
-  const float aa = __builtin_fabsf(a);
-  float r = aa < kTwoPi ? a : __builtin_copysignf(aa - kTwoPi, a);
-  r = r < 0.0f ? r + kTwoPi : r;
+  // rem_euclid(a, 2pi) for a in [-RS, 2pi + RS] (host KAT over every rot in the domain,
+  // tests/native/remeuclid_kat_host.c)
+  const float r = a < 0.0f ? a + kTwoPi : (a >= kTwoPi ? a - kTwoPi : a);
   rot = turn ? r : rot;
   const float mag2 = vel_x * vel_x + vel_y * vel_y;
 #ifdef GGRS_EXP_NO_CLAMP

@@ -14,3 +14,15 @@ def test_clamp_test_equivalence_every_f32(tmp_path):
     r = subprocess.run([exe, str(min(8, os.cpu_count() or 1))], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip() == "bad 0"
+
+
+def test_turn_rem_euclid_every_rotation_in_domain(tmp_path):
+    """The lean step's turn `a < 0 ? a + 2pi : (a >= 2pi ? a - 2pi : a)` equals
+    f32::rem_euclid(rot -/+ ROTATION_SPEED, 2pi) (ex_game.rs:300-306) for every f32 rot in
+    [+0, 2pi], both directions."""
+    exe = str(tmp_path / "remeuclid_kat_host")
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-fno-fast-math", "-o", exe,
+                    os.path.join(HERE, "native", "remeuclid_kat_host.c"), "-lm", "-lpthread"], check=True)
+    r = subprocess.run([exe, str(min(8, os.cpu_count() or 1))], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.strip() == "bad 0"
