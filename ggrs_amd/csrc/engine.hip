@@ -158,7 +158,55 @@ struct PipeParams {
   const int32_t* lane_status;
   int32_t* fail_f0;
   uint16_t* trace;
+  // v4: the launch checkpoint taken by the kernel itself (each block copies its own sessions'
+  // cur / ring / ring_ck / first_ck entries to the same offsets of `shadow` before it writes any),
+  // instead of a separate whole-arena copy launch; null for the other kernels
+  const uint8_t* arena;
+  uint8_t* shadow;
 };
+
+// The checkpoint kernel's copy restricted to sessions [s0, s0 + nsess): every row of cur, ring,
+// ring_ck and first_ck, eight loads in flight per thread before their stores.
+__device__ inline void checkpoint_sessions(const PipeParams& p, int F, int64_t s0, int nsess, int wl) {
+  const int64_t L = p.L;
+  const int R = p.R;
+  auto shadow_of = [&](const void* live) { return p.shadow + ((const uint8_t*)live - p.arena); };
+  auto src32 = [&](int q) -> const uint32_t* {
+    const int row = q / nsess, ss = q - row * nsess;
+    return row < F ? p.cur + (int64_t)row * L + s0 + ss : p.ring + (int64_t)(row - F) * L + s0 + ss;
+  };
+  auto src16 = [&](int q) -> const uint16_t* {
+    const int row = q / nsess, ss = q - row * nsess;
+    return row < R ? p.ring_ck + (int64_t)row * L + s0 + ss : p.first_ck + (int64_t)(row - R) * L + s0 + ss;
+  };
+  const int n32 = (1 + R) * F * nsess, n16 = 2 * R * nsess;
+  for (int base = 0; base < n32; base += 8 * kWave) {
+    uint32_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int q = base + u * kWave + wl;
+      if (q < n32) v[u] = *src32(q);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int q = base + u * kWave + wl;
+      if (q < n32) *(uint32_t*)shadow_of(src32(q)) = v[u];
+    }
+  }
+  for (int base = 0; base < n16; base += 8 * kWave) {
+    uint16_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int q = base + u * kWave + wl;
+      if (q < n16) v[u] = *src16(q);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int q = base + u * kWave + wl;
+      if (q < n16) *(uint16_t*)shadow_of(src16(q)) = v[u];
+    }
+  }
+}
 
 template <int P>
 __global__ __launch_bounds__(kWave) void synctest_pipelined_kernel(PipeParams p) {
@@ -763,6 +811,9 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
   const uint32_t c1 = pl == 0 ? 2u * Fletcher<P>::kSum1Const : 0u;
   const uint32_t c2 = pl == 0 ? 2u * Fletcher<P>::kSum2Const : 0u;
 
+  // the launch checkpoint of this block's sessions (all of them, halted ones included: a restore
+  // copies the whole shadow back), before any of this launch's stores
+  if (p.shadow) checkpoint_sessions(p, F, s0, nsess, wl);
   const int32_t g0 = p.f0 - cd;
   for (int q = wl; q < cd * nsess; q += kWave) {
     const int gg = q / nsess, ss = q - gg * nsess;
@@ -1317,9 +1368,9 @@ static int checkpoint(ggrs_engine_t* e, int dir) {
 }
 
 static int launch_pipelined(ggrs_engine_t* e, int32_t f0, int32_t n) {
-  int rc = checkpoint(e, 0);
-  if (rc) return rc;
   PipeParams p;
+  p.arena = nullptr;
+  p.shadow = nullptr;
   p.L = e->cfg.num_lanes;
   p.R = e->R;
   p.cd = e->cfg.check_distance;
@@ -1350,7 +1401,16 @@ static int launch_pipelined(ggrs_engine_t* e, int32_t f0, int32_t n) {
                        (!e->trace || ((uint8_t*)e->trace > (uint8_t*)e->first_ck &&
                                       (uint64_t)((uint8_t*)e->trace - (uint8_t*)e->ring) +
                                               (uint64_t)2 * p.L * p.trace_cap < kOob));
-  if ((e->path == GGRS_PATH_PIPELINED || e->path == GGRS_PATH_PIPELINED_V4_DPP) && p.K * Pp <= kWave && fits_v4) {
+  const bool use_v4 = (e->path == GGRS_PATH_PIPELINED || e->path == GGRS_PATH_PIPELINED_V4_DPP) && p.K * Pp <= kWave && fits_v4;
+  if (use_v4) {
+    // the v4 kernel checkpoints its own sessions (checkpoint_sessions); other kernels get the copy
+    p.arena = e->arena;
+    p.shadow = e->shadow;
+  } else {
+    int rc = checkpoint(e, 0);
+    if (rc) return rc;
+  }
+  if (use_v4) {
     p.spw = kWave / (p.K * Pp);
     const int64_t grid = grid_of(p.L, p.spw);
     const bool dpp = e->path == GGRS_PATH_PIPELINED_V4_DPP;
