@@ -293,6 +293,8 @@ def run_p2p(args):
     eng = P2PEngine(S, num_players=P, local_players=local, input_delay=0, max_prediction=maxp,
                     remote_latency=D, input_capacity=frames + D + 2, device=local_rank)
     eng.set_kernel_form(args.p2p_form)
+    if args.sparse:
+        eng.set_sparse_saving(True)  # builder.rs:160-169; runs the lockstep form
     det, events = None, []
     if peers:
         from ggrs_amd import exchange
@@ -339,8 +341,10 @@ def run_p2p(args):
     F = 5 * P + 1
     # HBM bytes per launch: the state in/out, every save (state + checksum), every rollback load,
     # the queue words in/out and the input rows each call reads (arrival + its own, + replays)
+    # (sparse saving: about one save per call, at min_confirmed, and replays save nothing)
+    replay_saves = 0 if args.sparse else (D - 1) * (4 * F + 2)
     bytes_launch = (2 * 4 * F * S + (session_calls // args.steps) * (4 * F + 2) * 1
-                    + (rollbacks // args.steps) * (4 * F + (D - 1) * (4 * F + 2))
+                    + (rollbacks // args.steps) * (4 * F + replay_saves)
                     + 2 * 16 * P * S + (session_calls // args.steps) * 2 * 2 + (resim // args.steps) * 2 * 2)
     avg_s = kernel_ms / 1e3 / max(launches, 1)
     achieved = bytes_launch / avg_s / 1e9
@@ -351,7 +355,8 @@ def run_p2p(args):
             O.build()
             ok = True
             for s in (0, 1, S // 2, S - 1):
-                r = O.p2p_run(rows[:, s], num_players=P, local_mask=0b01, max_prediction=maxp, latency=D)
+                r = O.p2p_run(rows[:, s], num_players=P, local_mask=0b01, max_prediction=maxp, latency=D,
+                              sparse_saving=bool(args.sparse))
                 ok &= bytes(eng.state(s)) == bytes(r["final_state"]) and int(rb1[s]) == r["result"].rollbacks
             parity = {"sessions_0_1_mid_last_bit_exact": bool(ok)}
             if peers:
@@ -367,14 +372,14 @@ def run_p2p(args):
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"p2p: {S} sessions per GPU, 2 players (1 remote, inputs {D} frames "
                                    f"late), max_prediction {maxp}, held-key inputs, {calls} calls per step",
-                       "sessions_per_gpu": S, "peers": peers,
+                       "sessions_per_gpu": S, "peers": peers, "sparse_saving": bool(args.sparse),
                        "parallelism": f"sessions sharded over {world} GPU(s)"
                                       + (f", peer ranks exchange checksum reports over {dist.get_backend()}" if peers else "")},
             "rollbacks_per_session_frame": round(rollbacks / session_calls, 5),
             "advances_per_sec": round((session_calls + resim) * world / elapsed, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                         "traffic": pmc_traffic(f"p2p_s{S}"),
+                         "traffic": pmc_traffic(f"p2p_s{S}" + ("_sparse" if args.sparse else "")),
                          "algorithmic_bytes_per_launch": bytes_launch,
                          "avg_launch_ms": round(avg_s * 1e3, 4)},
             "cpu_baseline": cpu_baseline, "parity": parity,
@@ -508,11 +513,12 @@ def p2p_cpu_baseline(args, O, synth, P, D, maxp):
     t0 = time.perf_counter()
     with ThreadPoolExecutor(T) as ex:
         res = list(ex.map(lambda a: O.p2p_run(a, num_players=P, local_mask=0b01, max_prediction=maxp,
-                                              latency=D)["rc"], per))
+                                              latency=D, sparse_saving=bool(args.sparse))["rc"], per))
     wall = time.perf_counter() - t0
     return {"value": round(T * frames / wall, 1), "unit": "session-frames/s", "cores": T, "kind": "port",
             "sample": f"{T} threads x {frames} P2P advance_frame calls (1 session/thread, same game, "
-                      f"latency {D}, held-key inputs), C restatement oracle/ggrs_oracle.c oracle_p2p_run",
+                      f"latency {D}, held-key inputs{', sparse saving' if args.sparse else ''}), C restatement "
+                      f"oracle/ggrs_oracle.c oracle_p2p_run",
             "wall_s": round(wall, 3), "all_ok": all(r == 0 for r in res)}
 
 
@@ -538,6 +544,7 @@ def main():
                          "machines of a match) and compare checksums exchanged over the process group")
     ap.add_argument("--p2p-form", choices=["default", "flat", "lockstep", "unstaged"], default="default",
                     help="p2p: kernel form (DESIGN.md section 3)")
+    ap.add_argument("--sparse", action="store_true", help="p2p: sparse saving (SURVEY.md 8f row 4)")
     ap.add_argument("--workload", choices=["synctest", "p2p", "codec"], default="synctest",
                     help="p2p: the device P2P rollback decision (SURVEY.md 8f), --sessions per GPU")
     args = ap.parse_args()

@@ -243,9 +243,14 @@ __global__ __launch_bounds__(kP2PBlock) void p2p_kernel(P2PParams p) {
     __syncthreads();
   };
   const int tid = live ? (int)threadIdx.x : 0;
+  // every state the launch steps descends from cur or from a ring cell; both only ever hold
+  // State::new, zeros or advances of such states, all inside the lean step's rotation domain, so
+  // one test of cur (and of the prefetched cell, below) replaces a wave vote per player per step
+  bool lean_ok = __all(rot_in_domain<P>(st));
   auto advance = [&](uint32_t in) {
     const uint32_t from = st.w[0];
-    advance_state<P>(st, in, 0u);
+    if (lean_ok) advance_state_lean<P>(st, in);
+    else advance_state<P>(st, in, 0u);
     if (dbg && (int32_t)from == p.dbg_frame) st.w[fld_x(P, 0)] ^= 1u;
   };
   // Without sparse saving a rollback at call f always loads frame f - D (the remote input of that
@@ -261,6 +266,7 @@ __global__ __launch_bounds__(kP2PBlock) void p2p_kernel(P2PParams p) {
     }
   };
   prefetch(p.f0 - p.D);
+  lean_ok = lean_ok && __all(pre_frame == kNull || rot_in_domain<P>(pre));
   auto call = [&](int32_t f, const auto& input_row) {
     // 0. check_checksum_send_interval (p2p_session.rs:939-975), before any rollback of this call:
     //    last_confirmed_frame = f - 1 - D and last_saved_frame = f - 1 here, so frame_to_send =
