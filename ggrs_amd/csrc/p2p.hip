@@ -392,7 +392,10 @@ struct LdsRowsFlat {
 // so the per-player local/remote tests of the poll and of synchronized_inputs fold away.
 // kPlain: no desync history, display-checksum trace or debug flip in this launch (host-checked),
 // so none of their tests sits in the step loop.
-template <int P, int kLocal, bool kPlain>
+// kSparse: sparse saving (p2p_session.rs:666-702,819-843), as p2p_kernel does it: a rollback
+// loads the last save and saves only min_confirmed while replaying; before the call's own step,
+// check_last_saved_state either saves the current frame or replays again from the last save.
+template <int P, int kLocal, bool kPlain, bool kSparse>
 __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
   const uint32_t lmask = kLocal >= 0 ? (uint32_t)kLocal : p.local_mask;
   constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
@@ -416,19 +419,33 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
   int64_t resim = 0;
   const bool dbg = !kPlain && live && sess == p.dbg_sess;
   const int tid = live ? (int)threadIdx.x : 0;
-  const int32_t back = p.D + p.delay;
-  // the rollback cell of the next call (frame f + 1 - D), read at the end of call f (p2p_kernel)
+  const int32_t back = (kSparse ? p.R - 1 : p.D) + p.delay;
   // ring slots kept as counters (no integer division per step): slot_f = f % R of the session's
-  // call, slot_h = h % R of its replayed frame, pre_slot of the prefetched cell
+  // call, slot_h = h % R of its replayed frame, pre_slot of the prefetched cell, saved_slot of the
+  // last save (sparse)
   uint4* const my_ring = reinterpret_cast<uint4*>(p.ring + (int64_t)sess * p.R * cell_dwords(P));
   auto cell = [&](int32_t slot) { return my_ring + slot * (cell_dwords(P) / 4); };
   auto next_slot = [&](int32_t x) { return x + 1 == p.R ? 0 : x + 1; };
   int32_t slot_f = p.f0 % p.R, slot_h = 0, pre_slot = 0;
+  int32_t last_saved = kSparse ? p.last_saved[sess] : kNull;
+  int32_t saved_slot = (kSparse && last_saved >= 0) ? last_saved % p.R : 0;
+  auto save = [&](int32_t h, int32_t slot) {  // SaveGameState(h) into its cell
+    if (live) {
+      store_cell<P>(st, fletcher16_state<P>(st), cell(slot));
+      if (kSparse) p.ring_frame[(int64_t)slot * S + sess] = h;  // GameStateCell.frame
+    }
+    if constexpr (kSparse) {
+      last_saved = h;
+      saved_slot = slot;
+    }
+  };
+  // the rollback cell of the next call (frame f + 1 - D), read at the end of call f (p2p_kernel);
+  // sparse saving loads the last save instead, read where the rollback happens
   BoxState<P> pre;
   int32_t pre_frame = kNull;
   // prefetch(fr, slot): fr = f + 1 - D with 1 <= D < R, so its slot is slot_f + 1 - D mod R
   auto prefetch = [&](int32_t fr, int32_t slot) {
-    if (fr >= 0) {
+    if (!kSparse && fr >= 0) {
       load_cell<P>(pre, cell(slot));
       pre_frame = fr;
       pre_slot = slot;
@@ -468,8 +485,40 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
     }
     const LdsRowsFlat<P> rows{lds_rows, lo, tid};
     int32_t f = fs;              // this session's call
-    bool at_start = true, replaying = false;
-    int32_t h = 0, load = 0, last_added = kNull;
+    bool at_start = true, replaying = false, window_done = false;
+    int32_t h = 0, load = 0, last_added = kNull, confirmed = kNull;
+    // adjust_gamestate's load (p2p_session.rs:658-714): the cell of `from` (sparse: the last save)
+    auto begin_replay = [&](int32_t from) {
+      load = from;
+      if (kSparse) {
+        slot_h = saved_slot;
+        load_cell<P>(st, cell(slot_h));
+      } else if (load == pre_frame) {
+        st = pre;
+        slot_h = pre_slot;
+      } else {
+        slot_h = load % p.R;
+        load_cell<P>(st, cell(slot_h));
+      }
+#pragma unroll
+      for (int k = 0; k < P; k++) {  // reset_prediction (input_queue.rs:63-67)
+        q.pred_frame[k] = kNull;
+        q.first_inc[k] = kNull;
+        q.last_req[k] = kNull;
+      }
+      h = load;
+      replaying = true;  // load < f
+      rollbacks += 1;
+      resim += f - load;
+    };
+    // sparse: check_last_saved_state (:819-843) before the call's own step
+    auto window_check = [&]() {
+      window_done = true;
+      if (f - last_saved >= p.R - 1) {
+        if (confirmed >= f) save(f, slot_f);
+        else begin_replay(last_saved);
+      }
+    };
     while (f < chunk_end) {
       if (at_start) {
         // 0. check_checksum_send_interval (as p2p_kernel)
@@ -481,6 +530,7 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
         // 1. poll_remote_clients: the remote input of frame g = f - D (add_input_by_frame)
         const int32_t g = f - p.D;
         last_added = g >= 0 ? g : kNull;
+        confirmed = g >= 0 ? g : kNull;  // confirmed_frame (:542-553)
         if (g >= 0) {
           const uint32_t row = rows(g);
 #pragma unroll
@@ -495,46 +545,33 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
           }
         }
         // 2. the first frame's save
-        if (f == 0 && live) store_cell<P>(st, fletcher16_state<P>(st), cell(0));
-        // 3. check_simulation_consistency: a rollback loads first_incorrect and replays from it
+        if (f == 0) save(0, slot_f);
+        // 3. check_simulation_consistency: a rollback loads first_incorrect (sparse: the last
+        //    save) and replays from it
         int32_t first_inc = kNull;
 #pragma unroll
         for (int k = 0; k < P; k++)
           if (q.first_inc[k] != kNull && (first_inc == kNull || q.first_inc[k] < first_inc)) first_inc = q.first_inc[k];
-        if (first_inc != kNull) {
-          load = first_inc;
-          if (load == pre_frame) {
-            st = pre;
-            slot_h = pre_slot;
-          } else {
-            slot_h = load % p.R;
-            load_cell<P>(st, cell(slot_h));
-          }
-#pragma unroll
-          for (int k = 0; k < P; k++) {  // reset_prediction (input_queue.rs:63-67)
-            q.pred_frame[k] = kNull;
-            q.first_inc[k] = kNull;
-            q.last_req[k] = kNull;
-          }
-          h = load;
-          replaying = true;  // first_incorrect <= f - D < f
-          rollbacks += 1;
-          resim += f - load;
-        }
+        window_done = false;
+        if (first_inc != kNull) begin_replay(kSparse ? last_saved : first_inc);
+        if (kSparse && !replaying) window_check();
         at_start = false;
       }
-      // one step: a replayed frame h (saved unless it is the loaded one) or the call's own frame
-      // f (SaveGameState(f), then AdvanceFrame with synchronized_inputs(f))
+      // one step: a replayed frame h or the call's own frame f (non-sparse: SaveGameState(f)
+      // first), then AdvanceFrame with synchronized_inputs
       const int32_t fr = replaying ? h : f;
       const uint32_t in = sync_inputs<P>(p, q, fr, last_added, rows, lmask);
-      if (live && (!replaying || h > load)) store_cell<P>(st, fletcher16_state<P>(st), cell(replaying ? slot_h : slot_f));
+      if (replaying ? (kSparse ? h == confirmed : h > load) : !kSparse) save(fr, replaying ? slot_h : slot_f);
       const uint32_t from = st.w[0];
       if (lean_ok) advance_state_lean<P>(st, in);
       else advance_state<P>(st, in, 0u);
       if (dbg && (int32_t)from == p.dbg_frame) st.w[fld_x(P, 0)] ^= 1u;
       if (replaying) {
         slot_h = next_slot(slot_h);
-        if (++h == f) replaying = false;
+        if (++h == f) {
+          replaying = false;
+          if (kSparse && !window_done) window_check();  // may replay again from the last save
+        }
       } else {
         if (!kPlain && p.trace && live) p.trace[(int64_t)(f % p.trace_cap) * S + sess] = fletcher16_state<P>(st);
         const int32_t ps = slot_f + 1 - p.D;
@@ -557,6 +594,7 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
   }
   p.rollbacks[sess] += rollbacks;
   p.resim[sess] += resim;
+  if (kSparse) p.last_saved[sess] = last_saved;
 }
 
 // compare_local_checksums_against_peers for one report frame, every session at once: bit s of
@@ -810,19 +848,21 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
     // whatever frame each lane is at (1.82e10 vs lockstep 1.26e10 session-frames/s at 65,536
     // sessions, 1.98e10 vs 1.89e10 at 131,072; with the frame-major ring of round 1 the flat
     // form's partial lines went out to HBM 3.5x over -- DESIGN.md section 5)
-    const bool flat = staged && !e->sparse && (e->form == 0 || e->form == 3);
+    const bool flat = staged && (e->form == 0 || e->form == 3);
     dispatch_players(e->cfg.num_players, [&](auto PC) {
       constexpr int P = decltype(PC)::value;
       if (flat) {
         const dim3 grid((unsigned)grid_of(p.S, kFlatBlock));
         auto go = [&](auto plain_tag) {
           constexpr bool kPl = decltype(plain_tag)::value;
-          if constexpr (P == 2) {
-            if (p.local_mask == 1u) p2p_flat_kernel<P, 1, kPl><<<grid, kFlatBlock, 0, e->stream>>>(p);
-            else if (p.local_mask == 2u) p2p_flat_kernel<P, 2, kPl><<<grid, kFlatBlock, 0, e->stream>>>(p);
-            else p2p_flat_kernel<P, -1, kPl><<<grid, kFlatBlock, 0, e->stream>>>(p);
+          if (e->sparse) {
+            p2p_flat_kernel<P, -1, kPl, true><<<grid, kFlatBlock, 0, e->stream>>>(p);
+          } else if constexpr (P == 2) {
+            if (p.local_mask == 1u) p2p_flat_kernel<P, 1, kPl, false><<<grid, kFlatBlock, 0, e->stream>>>(p);
+            else if (p.local_mask == 2u) p2p_flat_kernel<P, 2, kPl, false><<<grid, kFlatBlock, 0, e->stream>>>(p);
+            else p2p_flat_kernel<P, -1, kPl, false><<<grid, kFlatBlock, 0, e->stream>>>(p);
           } else {
-            p2p_flat_kernel<P, -1, kPl><<<grid, kFlatBlock, 0, e->stream>>>(p);
+            p2p_flat_kernel<P, -1, kPl, false><<<grid, kFlatBlock, 0, e->stream>>>(p);
           }
         };
         if (p.desync_interval == 0 && !p.trace && p.dbg_sess < 0) go(std::true_type());

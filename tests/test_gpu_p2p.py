@@ -123,8 +123,9 @@ SPARSE_CASES = [
 ]
 
 
+@pytest.mark.parametrize("form", ["flat", "lockstep"])
 @pytest.mark.parametrize("P,local,delay,mp,D,pred,model", SPARSE_CASES)
-def test_p2p_sparse_saving_matches_oracle(oracle, P, local, delay, mp, D, pred, model):
+def test_p2p_sparse_saving_matches_oracle(oracle, P, local, delay, mp, D, pred, model, form):
     """Sparse saving (builder.rs:160-169): rollbacks from the last save, saves only at
     min_confirmed or when the last save would leave the window; every session bit-exact with the
     oracle's P2PSession including which frames the ring cells hold."""
@@ -134,7 +135,24 @@ def test_p2p_sparse_saving_matches_oracle(oracle, P, local, delay, mp, D, pred, 
     eng = P2PEngine(S, num_players=P, local_players=local, input_delay=delay, max_prediction=mp,
                     remote_latency=D, predictor=pred, trace_capacity=frames)
     eng.set_sparse_saving(True)
+    eng.set_kernel_form(form)
     eng.add_inputs(0, rows)
     for n in (1, 3, 17, 79, 100):
         eng.advance_frames(n)
     check_against_oracle(eng, rows, [0, 1, 63, 64, 150, 299], frames)
+
+
+@pytest.mark.parametrize("P,local,delay,mp,D,pred,model", SPARSE_CASES[:2])
+def test_p2p_sparse_plain_launches_match_oracle(oracle, P, local, delay, mp, D, pred, model):
+    """Sparse saving in launches without trace/desync/debug (the flat kernel's plain sparse
+    specialisation): states, rings with their frame tags, and rollback counts bit-exact."""
+    from ggrs_amd import P2PEngine
+    S, frames = 300, 200
+    rows = stream(S, frames, P, model, seed_base=0x3131)
+    eng = P2PEngine(S, num_players=P, local_players=local, input_delay=delay, max_prediction=mp,
+                    remote_latency=D, predictor=pred)
+    eng.set_sparse_saving(True)
+    eng.add_inputs(0, rows)
+    for n in (2, 61, 137):
+        eng.advance_frames(n)
+    check_against_oracle(eng, rows, [0, 1, 63, 64, 150, 299], frames, trace=False)
