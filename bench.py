@@ -294,7 +294,7 @@ def run_p2p(args):
                     remote_latency=D, input_capacity=frames + D + 2, device=local_rank)
     eng.set_kernel_form(args.p2p_form)
     if args.sparse:
-        eng.set_sparse_saving(True)  # builder.rs:160-169; runs the lockstep form
+        eng.set_sparse_saving(True)  # builder.rs:160-169
     det, events = None, []
     if peers:
         from ggrs_amd import exchange

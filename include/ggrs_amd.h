@@ -329,7 +329,7 @@ int ggrs_p2p_compare_checksums(ggrs_p2p_engine_t* eng, int32_t frame, const uint
  * (sync_layer.rs:323-326).  Part of the configuration: only before the first call. */
 int ggrs_p2p_set_sparse_saving(ggrs_p2p_engine_t* eng, int32_t on);
 /* kernel form (comparison and tests): 0 = default (each session's calls flattened into its own
- * step sequence, input rows staged in LDS; sparse saving runs the lockstep form), 1 = calls in
+ * step sequence, input rows staged in LDS, with or without sparse saving), 1 = calls in
  * lockstep with input rows read from global memory, 2 = calls in lockstep with staged rows,
  * 3 = the flattened form (what the default runs whenever input rows can be staged) */
 int ggrs_p2p_set_unstaged(ggrs_p2p_engine_t* eng, int32_t form);
