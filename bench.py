@@ -522,6 +522,80 @@ def p2p_cpu_baseline(args, O, synth, P, D, maxp):
             "wall_s": round(wall, 3), "all_ok": all(r == 0 for r in res)}
 
 
+def run_requests(args):
+    """The request-level drop-in boundary (ggrs_handle_requests, what the Rust request handler of
+    INTEGRATION.md calls once per SyncTestSession::advance_frame): config-2 sessions, each call the
+    request list SyncTestSession emits at frame f (sync_test_session.rs:85-150: Load f-cd, cd x
+    (Save, Advance) with the first Save skipped, Save f, Advance), executed on every lane with the
+    inputs handed over from host memory (PCIe-inclusive).  One step = `calls` such calls."""
+    world, rank, local_rank, torch, dist = setup_dist(args)
+    import numpy as np
+    from ggrs_amd import Engine, synth
+    from ggrs_amd._lib import REQ_ADVANCE, REQ_LOAD, REQ_SAVE
+    L, P, maxp, cd, calls = args.lanes, 2, 9, 8, 64
+    frames = cd + 1 + (args.warmup + args.steps) * calls
+    inputs = synth.gen_inputs(rank * L, L, frames, P, synth.MODEL_HELD)  # [frames][L][P]
+    eng = Engine(L, P, maxp, cd, 0, device=local_rank, trace_capacity=0)
+
+    def call(f):
+        reqs, adv = [], []
+        if f > cd:
+            reqs.append((REQ_LOAD, f - cd))
+            for i in range(cd):
+                if i > 0:
+                    reqs.append((REQ_SAVE, f - cd + i))
+                reqs.append((REQ_ADVANCE, 0))
+                adv.append(f - cd + i)
+        reqs.append((REQ_SAVE, f))
+        reqs.append((REQ_ADVANCE, 0))
+        adv.append(f)
+        eng.handle_requests(reqs, np.ascontiguousarray(inputs[adv]))
+
+    f = 0
+    for _ in range(cd + 1 + args.warmup * calls):  # warm-up frames, then untimed steps
+        call(f)
+        f += 1
+    eng.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps * calls):
+        call(f)
+        f += 1
+    eng.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    value = L * cd * calls * args.steps * world / elapsed
+    parity = None
+    if rank == 0:
+        try:
+            from oracle import oracle as O
+            O.build()
+            r = O.synctest_run(inputs[:f, 0, :], P, maxp, cd, 0)
+            parity = {"lane0_final_state_bit_exact": bytes(eng.state(0)) == bytes(r["final_state"])}
+        except Exception as exc:
+            parity = {"error": repr(exc)}
+        print(json.dumps({
+            "metric": "resimulated session-frames/sec (node), request-level boundary", "value": round(value, 1),
+            "unit": "session-frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"requests: {L} SyncTest sessions per GPU (cd {cd}, 2 players), one "
+                                   f"ggrs_handle_requests call per advance_frame, {calls} calls per step, "
+                                   "inputs from host memory each call",
+                       "sessions_per_gpu": L, "parallelism": f"sessions sharded over {world} GPU(s)"},
+            "roofline": None, "cpu_baseline": None, "parity": parity,
+            "note": "launch- and PCIe-bound by construction (one launch + one host-to-device input copy "
+                    "per call); the fused ggrs_synctest_advance_frames path is the default bench"}))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -545,13 +619,15 @@ def main():
     ap.add_argument("--p2p-form", choices=["default", "flat", "lockstep", "unstaged"], default="default",
                     help="p2p: kernel form (DESIGN.md section 3)")
     ap.add_argument("--sparse", action="store_true", help="p2p: sparse saving (SURVEY.md 8f row 4)")
-    ap.add_argument("--workload", choices=["synctest", "p2p", "codec"], default="synctest",
+    ap.add_argument("--workload", choices=["synctest", "p2p", "codec", "requests"], default="synctest",
                     help="p2p: the device P2P rollback decision (SURVEY.md 8f), --sessions per GPU")
     args = ap.parse_args()
     if args.workload == "p2p":
         return run_p2p(args)
     if args.workload == "codec":
         return run_codec(args)
+    if args.workload == "requests":
+        return run_requests(args)
     if args.config == 5:
         return run_particles(args)
     if args.config != 2:
