@@ -1103,6 +1103,8 @@ struct ggrs_engine {
   uint16_t* trace = nullptr;
   uint8_t* staging = nullptr;  // device scratch for request inputs / status / request list
   size_t staging_bytes = 0;
+  uint8_t* host_staging = nullptr;  // pinned host copy of a request call's list + inputs (one DMA)
+  size_t host_staging_bytes = 0;
   // cur | ring | ring_ck | first_ck live in one arena so a launch checkpoint is one copy
   uint8_t* arena = nullptr;
   uint8_t* shadow = nullptr;
@@ -1182,6 +1184,7 @@ int ggrs_engine_destroy(ggrs_engine_t* e) {
                   e->mis_frame, e->mis_mask, e->staging};  // trace lives in the arena allocation
   for (void* b : bufs)
     if (b) (void)hipFree(b);
+  if (e->host_staging) (void)hipHostFree(e->host_staging);
   for (hipEvent_t ev : e->tev) (void)hipEventDestroy(ev);
   if (e->ev0) (void)hipEventDestroy(e->ev0);
   if (e->ev1) (void)hipEventDestroy(e->ev1);
@@ -1574,27 +1577,45 @@ int ggrs_handle_requests(ggrs_engine_t* e, const ggrs_request_t* reqs, int32_t n
   const size_t req_bytes = sizeof(int32_t) * 2 * n_reqs;
   const size_t in_bytes = (size_t)n_adv * L * Pp;
   const size_t raw_bytes = (size_t)n_adv * L * P;
-  const size_t total = req_bytes + 2 * in_bytes + 2 * raw_bytes + 64;
+  // one host-to-device copy from pinned memory: [request list | raw inputs | raw status]; the
+  // raw [n][L][P] rows are the kernel's [n][L][Pp] layout already when P == Pp (1, 2, 4 players)
+  const size_t req_pad = (req_bytes + 15) & ~(size_t)15, raw_pad = (raw_bytes + 15) & ~(size_t)15;
+  const size_t up_bytes = req_pad + 2 * raw_pad;
+  const size_t total = up_bytes + 2 * in_bytes + 64;
   int rc = ensure_staging(e, total);
   if (rc) return rc;
-  uint8_t* d_reqs = e->staging;
-  uint8_t* d_in = d_reqs + ((req_bytes + 15) & ~(size_t)15);
-  uint8_t* d_st = d_in + in_bytes;
-  uint8_t* d_raw = d_st + in_bytes;
-  std::vector<int32_t> flat(2 * n_reqs);
+  if (up_bytes > e->host_staging_bytes) {
+    if (e->host_staging) HIP_TRY(hipHostFree(e->host_staging));
+    e->host_staging = nullptr;
+    e->host_staging_bytes = 0;
+    HIP_TRY(hipHostMalloc((void**)&e->host_staging, up_bytes, hipHostMallocDefault));
+    e->host_staging_bytes = up_bytes;
+  }
+  uint8_t* h = e->host_staging;
+  int32_t* flat = reinterpret_cast<int32_t*>(h);
   for (int32_t r = 0; r < n_reqs; r++) {
     flat[2 * r] = reqs[r].kind;
     flat[2 * r + 1] = reqs[r].frame;
   }
-  HIP_TRY(hipMemcpyAsync(d_reqs, flat.data(), req_bytes, hipMemcpyHostToDevice, e->stream));
+  if (n_adv > 0) std::memcpy(h + req_pad, inputs, raw_bytes);
+  if (n_adv > 0 && status) std::memcpy(h + req_pad + raw_pad, status, raw_bytes);
+  uint8_t* d_reqs = e->staging;
+  uint8_t* d_raw = d_reqs + req_pad;
+  uint8_t* d_in = d_raw + 2 * raw_pad;
+  uint8_t* d_st = d_in + in_bytes;
+  HIP_TRY(hipMemcpyAsync(d_reqs, h, req_pad + (n_adv > 0 ? (status ? 2 * raw_pad : raw_bytes) : 0),
+                         hipMemcpyHostToDevice, e->stream));
   if (n_adv > 0) {
-    HIP_TRY(hipMemcpyAsync(d_raw, inputs, raw_bytes, hipMemcpyHostToDevice, e->stream));
-    pack_inputs_kernel<<<grid_of((int64_t)n_adv * L, 256), 256, 0, e->stream>>>(d_raw, d_in, L, P, Pp, n_adv, 0, n_adv);
-    HIP_TRY(hipGetLastError());
-    if (status) {
-      HIP_TRY(hipMemcpyAsync(d_raw + raw_bytes, status, raw_bytes, hipMemcpyHostToDevice, e->stream));
-      pack_inputs_kernel<<<grid_of((int64_t)n_adv * L, 256), 256, 0, e->stream>>>(d_raw + raw_bytes, d_st, L, P, Pp, n_adv, 0, n_adv);
+    if (P == Pp) {
+      d_in = d_raw;
+      d_st = d_raw + raw_pad;
+    } else {
+      pack_inputs_kernel<<<grid_of((int64_t)n_adv * L, 256), 256, 0, e->stream>>>(d_raw, d_in, L, P, Pp, n_adv, 0, n_adv);
       HIP_TRY(hipGetLastError());
+      if (status) {
+        pack_inputs_kernel<<<grid_of((int64_t)n_adv * L, 256), 256, 0, e->stream>>>(d_raw + raw_pad, d_st, L, P, Pp, n_adv, 0, n_adv);
+        HIP_TRY(hipGetLastError());
+      }
     }
   }
   RequestParams p;
