@@ -48,8 +48,11 @@ struct SpecParams {
 };
 
 // The remote-input byte of branch b on speculated frame k for the enumerated player.
+// (A is a kernel parameter: a power-of-two alphabet, 16 in configs 3/4, takes a shift and a mask
+// instead of kk + 1 integer divisions by a runtime divisor)
 __device__ inline uint32_t branch_digit(int32_t b, int32_t k, int32_t A, int32_t E) {
   int32_t kk = k < E ? k : E - 1;
+  if ((A & (A - 1)) == 0) return ((uint32_t)b >> (kk * __builtin_ctz((uint32_t)A))) & (uint32_t)(A - 1);
   int32_t v = b;
   for (int32_t q = 0; q < kk; q++) v /= A;
   return (uint32_t)(v % A);
