@@ -196,27 +196,35 @@ __global__ __launch_bounds__(kRoundsBlock) void rounds_kernel(RoundsParams rp) {
     trunk_ok = rot_in_domain<P>(t0);
   }
   const bool lean_ok = __syncthreads_and(trunk_ok);
+  // input-queue rows and ring slots as wave-uniform counters (no runtime-divisor modulo per step):
+  // row_c = f_c % cap, slot_c = f_c % R of the round's trunk frame
+  auto wrap_inc = [](int32_t x, int32_t m) { return x + 1 == m ? 0 : x + 1; };
+  int32_t row_c = p.f_c % p.cap, slot_c = p.f_c % p.R;
   for (int32_t r = 0; r < rp.n; ++r) {
     SpecParams q = p;
     q.f_c = p.f_c + r;
+    const int32_t row_prev = row_c == 0 ? p.cap - 1 : row_c - 1;
     if ((r > 0 || p.check_prev) && survived) {  // speculate_kernel's check of the last survivors
-      const uint16_t mine = p.ring_ck[(int64_t)(q.f_c % p.R) * p.L + lane];
+      const uint16_t mine = p.ring_ck[(int64_t)slot_c * p.L + lane];
       if (mine != lds_ck[ls]) atomicCAS(&p.desync[s], -1, q.f_c);
     }
     BoxState<P> st;
 #pragma unroll
     for (int k = 0; k < F; k++) st.w[k] = lds_trunk[ls][k];  // LoadGameState(f_c)
     // input rows: f_c - 1 (the last confirmed) and f_c + k, each read one frame ahead
-    const uint32_t last = q.f_c > 0 ? load_inputs<P>(p.inputs, (int64_t)((q.f_c - 1) % p.cap) * p.S + s) : 0u;
-    const uint32_t truth = load_inputs<P>(p.inputs, (int64_t)(q.f_c % p.cap) * p.S + s);
+    const uint32_t last = q.f_c > 0 ? load_inputs<P>(p.inputs, (int64_t)row_prev * p.S + s) : 0u;
+    const uint32_t truth = load_inputs<P>(p.inputs, (int64_t)row_c * p.S + s);
     if (in_range) {
       uint32_t tk = truth;
+      int32_t row_k = row_c, slot = slot_c;
       for (int32_t k = 0; k < p.W; ++k) {
-        const uint32_t next = k + 1 < p.W ? load_inputs<P>(p.inputs, (int64_t)((q.f_c + k + 1) % p.cap) * p.S + s) : 0u;
+        row_k = wrap_inc(row_k, p.cap);  // row of frame f_c + k + 1
+        slot = wrap_inc(slot, p.R);      // slot of frame f_c + k + 1
+        const uint32_t next = k + 1 < p.W ? load_inputs<P>(p.inputs, (int64_t)row_k * p.S + s) : 0u;
         const uint32_t in = branch_inputs_from<P>(q, tk, last, b, k);  // AdvanceFrame(f_c + k)
         if (lean_ok) advance_state_lean<P>(st, in);
         else advance_state<P>(st, in, 0u);
-        const int32_t slot = (q.f_c + k + 1) % p.R;                            // SaveGameState(f_c + k + 1)
+        // SaveGameState(f_c + k + 1) into `slot`
         store_state<P>(st, p.ring + (int64_t)slot * F * p.L + lane, p.L);
         p.ring_ck[(int64_t)slot * p.L + lane] = fletcher16_state<P>(st);
         tk = next;
@@ -243,7 +251,7 @@ __global__ __launch_bounds__(kRoundsBlock) void rounds_kernel(RoundsParams rp) {
       BoxState<P> tr;
 #pragma unroll
       for (int k = 0; k < F; k++) tr.w[k] = lds_trunk[threadIdx.x][k];
-      const uint32_t tin = load_inputs<P>(p.inputs, (int64_t)(q.f_c % p.cap) * p.S + s2);
+      const uint32_t tin = load_inputs<P>(p.inputs, (int64_t)row_c * p.S + s2);
       if (lean_ok) advance_state_lean<P>(tr, tin);
       else advance_state<P>(tr, tin, 0u);
       const uint16_t ck = fletcher16_state<P>(tr);
@@ -256,6 +264,8 @@ __global__ __launch_bounds__(kRoundsBlock) void rounds_kernel(RoundsParams rp) {
       }
     }
     __syncthreads();
+    row_c = wrap_inc(row_c, p.cap);
+    slot_c = wrap_inc(slot_c, p.R);
   }
 }
 
