@@ -522,12 +522,35 @@ def p2p_cpu_baseline(args, O, synth, P, D, maxp):
             "wall_s": round(wall, 3), "all_ok": all(r == 0 for r in res)}
 
 
+def synctest_tokens(f, cd):
+    """The request kinds of SyncTestSession::advance_frame at frame f (sync_test_session.rs:85-150)
+    as lane-batch tokens: [Load f-cd, Advance, (Save, Advance) x (cd-1)] when f > cd, then Save f,
+    Advance.  Returns (token words, n_tokens, loads, advances, saves)."""
+    from ggrs_amd._lib import TOK_ADVANCE, TOK_END, TOK_LOAD, TOK_SAVE, TOKENS_PER_WORD
+    toks = []
+    if f > cd:
+        toks += [TOK_LOAD, TOK_ADVANCE] + [TOK_SAVE, TOK_ADVANCE] * (cd - 1)
+    toks += [TOK_SAVE, TOK_ADVANCE]
+    n = len(toks)
+    W = -(-n // TOKENS_PER_WORD)
+    toks += [TOK_END] * (W * TOKENS_PER_WORD - n)
+    words = [sum(t << (2 * i) for i, t in enumerate(toks[w * TOKENS_PER_WORD:(w + 1) * TOKENS_PER_WORD]))
+             for w in range(W)]
+    return words, n, int(f > cd), toks.count(TOK_ADVANCE), toks.count(TOK_SAVE)
+
+
 def run_requests(args):
-    """The request-level drop-in boundary (ggrs_handle_requests, what the Rust request handler of
-    INTEGRATION.md calls once per SyncTestSession::advance_frame): config-2 sessions, each call the
-    request list SyncTestSession emits at frame f (sync_test_session.rs:85-150: Load f-cd, cd x
-    (Save, Advance) with the first Save skipped, Save f, Advance), executed on every lane with the
-    inputs handed over from host memory (PCIe-inclusive).  One step = `calls` such calls."""
+    """The request-level drop-in boundary (what the Rust request handler of INTEGRATION.md calls
+    once per advance_frame of every session): config-2 sessions, each call the request list
+    SyncTestSession emits at frame f (sync_test_session.rs:85-150: Load f-cd, cd x (Save, Advance)
+    with the first Save skipped, Save f, Advance) for every lane, handed over from host memory and
+    every Save's checksum handed back (what the handler passes to GameStateCell::save).
+      --req-form batch   (default) the per-lane lists pre-encoded into the engine's mapped batch
+                         (ggrs_lane_batch_run): per call the host writes tokens, load frames and
+                         input rows, one launch reads them over PCIe and writes checksums back
+      --req-form lanes   ggrs_handle_requests_lanes: the GgrsRequest lists themselves (CSR)
+      --req-form lockstep  ggrs_handle_requests: one list for every lane (lockstep sessions)
+    One step = `calls` such calls; inputs are resident in host memory before the timed region."""
     world, rank, local_rank, torch, dist = setup_dist(args)
     import numpy as np
     from ggrs_amd import Engine, synth
@@ -535,21 +558,52 @@ def run_requests(args):
     L, P, maxp, cd, calls = args.lanes, 2, 9, 8, 64
     frames = cd + 1 + (args.warmup + args.steps) * calls
     inputs = synth.gen_inputs(rank * L, L, frames, P, synth.MODEL_HELD)  # [frames][L][P]
-    eng = Engine(L, P, maxp, cd, 0, device=local_rank, trace_capacity=0)
+    form = args.req_form
+    eng = Engine(L, P, maxp, cd if form == "lockstep" else 0, 0, device=local_rank, trace_capacity=0)
+    sink = np.zeros(1, np.uint64)
 
-    def call(f):
-        reqs, adv = [], []
-        if f > cd:
-            reqs.append((REQ_LOAD, f - cd))
-            for i in range(cd):
-                if i > 0:
-                    reqs.append((REQ_SAVE, f - cd + i))
-                reqs.append((REQ_ADVANCE, 0))
-                adv.append(f - cd + i)
-        reqs.append((REQ_SAVE, f))
-        reqs.append((REQ_ADVANCE, 0))
-        adv.append(f)
-        eng.handle_requests(reqs, np.ascontiguousarray(inputs[adv]))
+    if form == "batch":
+        batch = eng.lane_batch(2, 1, cd + 1, cd + 1)
+        steady = np.array(synctest_tokens(cd + 1, cd)[0], np.uint32)[:, None].repeat(L, axis=1)
+
+        def call(f):
+            words, n, nl, na, ns = synctest_tokens(f, cd)
+            if f > cd:
+                batch.tokens[:2] = steady
+                batch.load_frames[0].fill(f - cd)
+                batch.inputs[:na] = inputs[f - cd:f + 1]
+            else:
+                batch.tokens[:len(words)] = np.array(words, np.uint32)[:, None]
+                batch.inputs[:1] = inputs[f:f + 1]
+            nf = batch.run(len(words), nl, na, ns)
+            assert nf == 0
+            sink[0] += int(batch.checksums[ns - 1, 0])  # the checksums are back in host memory
+    else:
+        def lists(f):
+            reqs, adv = [], []
+            if f > cd:
+                reqs.append((REQ_LOAD, f - cd))
+                for i in range(cd):
+                    if i > 0:
+                        reqs.append((REQ_SAVE, f - cd + i))
+                    reqs.append((REQ_ADVANCE, 0))
+                    adv.append(f - cd + i)
+            reqs.append((REQ_SAVE, f))
+            reqs.append((REQ_ADVANCE, 0))
+            adv.append(f)
+            return reqs, adv
+        if form == "lanes":
+            def call(f):
+                reqs, adv = lists(f)
+                r = np.array(reqs * L, np.int32)
+                off = np.arange(0, (L + 1) * len(reqs), len(reqs), dtype=np.int32)
+                inp = np.ascontiguousarray(inputs[adv].transpose(1, 0, 2)).reshape(-1, P)
+                cks, _ = eng.handle_requests_lanes(r, off, inp)
+                sink[0] += int(cks[-1])
+        else:
+            def call(f):
+                reqs, adv = lists(f)
+                eng.handle_requests(reqs, np.ascontiguousarray(inputs[adv]))
 
     f = 0
     for _ in range(cd + 1 + args.warmup * calls):  # warm-up frames, then untimed steps
@@ -577,7 +631,9 @@ def run_requests(args):
             from oracle import oracle as O
             O.build()
             r = O.synctest_run(inputs[:f, 0, :], P, maxp, cd, 0)
-            parity = {"lane0_final_state_bit_exact": bytes(eng.state(0)) == bytes(r["final_state"])}
+            parity = {"lane0_final_state_bit_exact": bytes(eng.state(0)) == bytes(r["final_state"]),
+                      "lane_last_final_state_bit_exact": bytes(eng.state(L - 1)) == bytes(
+                          O.synctest_run(inputs[:f, L - 1, :], P, maxp, cd, 0)["final_state"])}
         except Exception as exc:
             parity = {"error": repr(exc)}
         print(json.dumps({
@@ -585,13 +641,16 @@ def run_requests(args):
             "unit": "session-frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": f"requests: {L} SyncTest sessions per GPU (cd {cd}, 2 players), one "
-                                   f"ggrs_handle_requests call per advance_frame, {calls} calls per step, "
-                                   "inputs from host memory each call",
-                       "sessions_per_gpu": L, "parallelism": f"sessions sharded over {world} GPU(s)"},
+            "config": {"workload": f"requests: {L} SyncTest sessions per GPU (cd {cd}, 2 players), each call "
+                                   f"every session's request list of one advance_frame (form {form}), "
+                                   f"{calls} calls per step, lists and inputs from host memory, checksums "
+                                   "back to host memory each call",
+                       "sessions_per_gpu": L, "req_form": form,
+                       "us_per_call": round(elapsed / (args.steps * calls) * 1e6, 2),
+                       "parallelism": f"sessions sharded over {world} GPU(s)"},
             "roofline": None, "cpu_baseline": None, "parity": parity,
-            "note": "launch- and PCIe-bound by construction (one launch + one host-to-device input copy "
-                    "per call); the fused ggrs_synctest_advance_frames path is the default bench"}))
+            "note": "latency-bound by construction (one launch and one PCIe round trip per call); the fused "
+                    "ggrs_synctest_advance_frames path is the default bench"}))
     if dist is not None:
         dist.destroy_process_group()
 
@@ -607,7 +666,7 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=3000000,
                     help="SyncTest frames per CPU thread (default: ~10 s of host work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--path", choices=["pipelined", "sequential", "pipelined-whole", "pipelined-split", "pipelined-v3", "pipelined-v4-dpp"], default="pipelined",
+    ap.add_argument("--path", choices=["pipelined", "sequential"], default="pipelined",
                     help="SyncTest kernel (DESIGN.md section 3)")
     ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=2,
                     help="BASELINE.json config: 2 = SyncTest (default), 3/4 = branch rollback, "
@@ -619,6 +678,8 @@ def main():
     ap.add_argument("--p2p-form", choices=["default", "flat", "lockstep", "unstaged"], default="default",
                     help="p2p: kernel form (DESIGN.md section 3)")
     ap.add_argument("--sparse", action="store_true", help="p2p: sparse saving (SURVEY.md 8f row 4)")
+    ap.add_argument("--req-form", choices=["batch", "lanes", "lockstep"], default="batch",
+                    help="requests: the boundary form (run_requests docstring)")
     ap.add_argument("--workload", choices=["synctest", "p2p", "codec", "requests"], default="synctest",
                     help="p2p: the device P2P rollback decision (SURVEY.md 8f), --sessions per GPU")
     args = ap.parse_args()
@@ -646,7 +707,7 @@ def main():
     inputs = synth.gen_inputs(rank * lanes, lanes, total_frames, P, synth.MODEL_HELD)
     eng = Engine(lanes, P, maxp, cd, delay, input_capacity=total_frames + cd + delay + 2,
                  device=local_rank, trace_capacity=trace_cap)
-    eng.set_synctest_path({"pipelined": 0, "sequential": 1, "pipelined-whole": 2, "pipelined-split": 3, "pipelined-v3": 4, "pipelined-v4-dpp": 5}[args.path])
+    eng.set_synctest_path({"pipelined": 0, "sequential": 1}[args.path])
     eng.add_local_inputs(0, inputs)  # resident in HBM before anything is timed
     eng.synchronize()
 

@@ -5,8 +5,9 @@ SyncTestSession, caspark/ggrs 0.10.2) for thousands of (session, branch) lanes a
 hand-written HIP kernels for gfx950 behind a C ABI (include/ggrs_amd.h).  See DESIGN.md.
 """
 from ._lib import GgrsError, InvalidRequest, PreconditionError, NULL_FRAME  # noqa: F401
-from .session import (AdvanceFrame, BoxGameHandler, Engine, LoadGameState,  # noqa: F401
-                      MismatchedChecksum, SaveGameState, SessionBuilder, SyncTestSession)
+from .session import (AdvanceFrame, BoxGameHandler, Engine, LaneBatch, LaneBoxGameHandler,  # noqa: F401
+                      LanesFailed, LoadGameState, MismatchedChecksum, SaveGameState, SessionBuilder,
+                      SyncTestSession, encode_lane_lists)
 
 from .branch import BranchEngine  # noqa: F401
 from .particles import ParticleEngine  # noqa: F401

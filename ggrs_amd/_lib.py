@@ -21,7 +21,10 @@ NULL_FRAME = -1
 REQ_SAVE, REQ_LOAD, REQ_ADVANCE = 0, 1, 2
 STATUS_CONFIRMED, STATUS_PREDICTED, STATUS_DISCONNECTED = 0, 1, 2
 LANE_RUNNING, LANE_MISMATCH = 0, 1
-PATH_PIPELINED, PATH_SEQUENTIAL, PATH_PIPELINED_WHOLE, PATH_PIPELINED_SPLIT, PATH_PIPELINED_V3, PATH_PIPELINED_V4_DPP = 0, 1, 2, 3, 4, 5
+PATH_PIPELINED, PATH_SEQUENTIAL = 0, 1
+TOK_SAVE, TOK_ADVANCE, TOK_LOAD, TOK_END = 0, 1, 2, 3
+TOKENS_PER_WORD = 16
+BATCH_STATUS = 1
 
 # every symbol include/ggrs_amd.h declares (tests check the library exports all of them)
 EXPORTS = (
@@ -31,6 +34,7 @@ EXPORTS = (
     "ggrs_current_frame", "ggrs_read_mismatches", "ggrs_read_save_checksums", "ggrs_read_state",
     "ggrs_read_ring", "ggrs_read_trace", "ggrs_debug_corrupt_on_load", "ggrs_last_launch_ms",
     "ggrs_timing_reset", "ggrs_timing_read", "ggrs_set_synctest_path",
+    "ggrs_lane_batch_map", "ggrs_lane_batch_run", "ggrs_handle_requests_lanes", "ggrs_read_lane_frames",
     "ggrs_branch_engine_create", "ggrs_branch_engine_destroy", "ggrs_branch_engine_config",
     "ggrs_branch_add_inputs", "ggrs_branch_speculate", "ggrs_branch_confirm",
     "ggrs_branch_report_bytes", "ggrs_branch_synchronize", "ggrs_branch_trunk_frame",
@@ -67,6 +71,22 @@ class Config(ctypes.Structure):
 
 class Request(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int32), ("frame", ctypes.c_int32)]
+
+
+class LaneBatch(ctypes.Structure):
+    """ggrs_lane_batch_t"""
+    _fields_ = [
+        ("token_words", ctypes.c_int32),
+        ("load_slots", ctypes.c_int32),
+        ("adv_rows", ctypes.c_int32),
+        ("save_rows", ctypes.c_int32),
+        ("tokens", ctypes.POINTER(ctypes.c_uint32)),
+        ("load_frames", ctypes.POINTER(ctypes.c_int32)),
+        ("inputs", ctypes.POINTER(ctypes.c_uint8)),
+        ("status", ctypes.POINTER(ctypes.c_uint8)),
+        ("checksums", ctypes.POINTER(ctypes.c_uint16)),
+        ("lane_result", ctypes.POINTER(ctypes.c_int32)),
+    ]
 
 
 class GgrsError(Exception):
@@ -119,6 +139,11 @@ def lib():
         L.ggrs_timing_reset.argtypes = [vp]
         L.ggrs_set_synctest_path.argtypes = [vp, ctypes.c_int32]
         L.ggrs_timing_read.argtypes = [vp, P(ctypes.c_float), P(ctypes.c_int32)]
+        i32 = ctypes.c_int32
+        L.ggrs_lane_batch_map.argtypes = [vp, i32, i32, i32, i32, P(LaneBatch)]
+        L.ggrs_lane_batch_run.argtypes = [vp, P(LaneBatch), i32, P(i32)]
+        L.ggrs_handle_requests_lanes.argtypes = [vp, vp, vp, vp, vp, vp, vp]
+        L.ggrs_read_lane_frames.argtypes = [vp, vp]
         for name in EXPORTS:
             if name not in ("ggrs_abi_version", "ggrs_last_error", "ggrs_codec_max_packet_bytes"):
                 getattr(L, name).restype = ctypes.c_int

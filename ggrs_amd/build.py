@@ -3,21 +3,26 @@
 Flags that matter for parity: -ffp-contract=off (the reference's Rust never fuses a*b+c; the
 sincosf restatement places its fmas explicitly), no -ffast-math (keeps correctly rounded f32
 division/sqrt and f32 denormals, hipcc's defaults).
+
+Each translation unit compiles to its own object in parallel (ggrs_amd/_obj/), then one link.
 """
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
+OBJ = os.path.join(HERE, "_obj")
 LIB = os.path.join(HERE, "libggrs_amd.so")
-SOURCES = [os.path.join(CSRC, f) for f in ("engine.hip", "branch.hip", "particles.hip", "p2p.hip", "codec.hip")]
+UNITS = ("engine.hip", "requests.hip", "branch.hip", "particles.hip", "p2p.hip", "codec.hip")
+SOURCES = [os.path.join(CSRC, f) for f in UNITS]
 HEADERS = [os.path.join(CSRC, h) for h in ("box_game.h", "glibc_sincosf.h", "common.h", "particles.h")] + [
     os.path.join(ROOT, "include", "ggrs_amd.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC", "-shared", "-std=c++17",
+FLAGS = ["-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC", "-std=c++17",
          "-Wall", "-Wno-unused-function"]
 
 
@@ -28,16 +33,30 @@ def needs_build():
     return any(os.path.getmtime(f) > t for f in SOURCES + HEADERS)
 
 
-def build(force=False, verbose=False):
-    if not force and not needs_build():
-        return LIB
-    cmd = [HIPCC, *FLAGS, "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", LIB + ".tmp",
-           *SOURCES]
+def _compile(src, extra, verbose):
+    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
+    cmd = [HIPCC, *FLAGS, *extra, "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-c", "-o", obj, src]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    return obj
+
+
+def build(force=False, verbose=False, out=LIB, extra=()):
+    """Compile every unit for gfx950 and link `out` (default: the product library).  `extra`
+    flags are for experiment builds only (tools/exp_build.sh), which write elsewhere."""
+    if out == LIB and not extra and not force and not needs_build():
+        return LIB
+    os.makedirs(OBJ, exist_ok=True)
+    jobs = min(len(SOURCES), max(1, os.cpu_count() or 1), 16)
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, list(extra), verbose), SOURCES))
+    cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out + ".tmp", *objs]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":

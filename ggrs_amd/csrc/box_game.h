@@ -194,11 +194,7 @@ __device__ inline void advance_player_lean(float& x, float& y, float& vx, float&
   float vel_x = vx * kFriction;
   float vel_y = vy * kFriction;
   float s, c;
-#ifndef GGRS_EXP_NO_SINCOS  // timing experiments only (tools/exp_build.sh), never shipped
   glibc_sincosf_domain(rot, &s, &c);
-#else
-  s = rot; c = rot;
-#endif
   const float dx = kMovementSpeed * c, dy = kMovementSpeed * s;
   const uint32_t ud = input & (kInputUp | kInputDown), lr = input & (kInputLeft | kInputRight);
   const bool thrust = ud == kInputUp, brake = ud == kInputDown;
@@ -211,11 +207,7 @@ __device__ inline void advance_player_lean(float& x, float& y, float& vx, float&
   const float r = a < 0.0f ? a + kTwoPi : (a >= kTwoPi ? a - kTwoPi : a);
   rot = turn ? r : rot;
   const float mag2 = vel_x * vel_x + vel_y * vel_y;
-#ifdef GGRS_EXP_NO_CLAMP
-  if (mag2 < 0.0f) {
-#else
   if (mag2 > kMaxSpeed * kMaxSpeed) {
-#endif
     const float magnitude = sqrt_rn_above_49(mag2);
     const double r = rcp_f64_refined((double)magnitude);
     vel_x = (float)((double)(vel_x * kMaxSpeed) * r);

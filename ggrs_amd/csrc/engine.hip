@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "common.h"
+#include "engine.h"
 
 #pragma clang fp contract(off)
 
@@ -158,157 +159,92 @@ struct PipeParams {
   const int32_t* lane_status;
   int32_t* fail_f0;
   uint16_t* trace;
-  // v4: the launch checkpoint taken by the kernel itself (each block copies its own sessions'
-  // cur / ring / ring_ck / first_ck entries to the same offsets of `shadow` before it writes any),
-  // instead of a separate whole-arena copy launch; null for the other kernels
-  const uint8_t* arena;
+  // the launch checkpoint, taken by the kernel itself: each block copies its own sessions' cur /
+  // ring / ring_ck / first_ck entries into its own contiguous `block_bytes` piece of `shadow`
+  // (whole cache lines, not a scatter into an arena-shaped copy) before it writes any of them
   uint8_t* shadow;
+  int64_t block_bytes;
 };
 
-// The checkpoint kernel's copy restricted to sessions [s0, s0 + nsess): every row of cur, ring,
-// ring_ck and first_ck, eight loads in flight per thread before their stores.
-__device__ inline void checkpoint_sessions(const PipeParams& p, int F, int64_t s0, int nsess, int wl) {
-  const int64_t L = p.L;
-  const int R = p.R;
-  auto shadow_of = [&](const void* live) { return p.shadow + ((const uint8_t*)live - p.arena); };
-  auto src32 = [&](int q) -> const uint32_t* {
+// Shadow layout of one block's checkpoint (sessions [s0, s0 + nsess)): first every 32-bit row
+// entry q of cur (F rows) and ring (R*F rows), q = row * nsess + session, then every 16-bit entry
+// of ring_ck (R rows) and first_ck (R rows).  checkpoint_sessions writes it, restore_kernel maps it
+// back; both index through these two functions.
+struct CheckpointMap {
+  int64_t L;
+  int R, F, spw;
+  uint32_t* cur;
+  uint32_t* ring;
+  uint16_t* ring_ck;
+  uint16_t* first_ck;
+  __device__ uint32_t* at32(int64_t s0, int nsess, int q) const {
     const int row = q / nsess, ss = q - row * nsess;
-    return row < F ? p.cur + (int64_t)row * L + s0 + ss : p.ring + (int64_t)(row - F) * L + s0 + ss;
-  };
-  auto src16 = [&](int q) -> const uint16_t* {
+    return row < F ? cur + (int64_t)row * L + s0 + ss : ring + (int64_t)(row - F) * L + s0 + ss;
+  }
+  __device__ uint16_t* at16(int64_t s0, int nsess, int q) const {
     const int row = q / nsess, ss = q - row * nsess;
-    return row < R ? p.ring_ck + (int64_t)row * L + s0 + ss : p.first_ck + (int64_t)(row - R) * L + s0 + ss;
-  };
-  const int n32 = (1 + R) * F * nsess, n16 = 2 * R * nsess;
-  for (int base = 0; base < n32; base += 8 * kWave) {
+    return row < R ? ring_ck + (int64_t)row * L + s0 + ss : first_ck + (int64_t)(row - R) * L + s0 + ss;
+  }
+};
+
+__host__ __device__ inline int64_t checkpoint_block_bytes(int R, int F, int spw) {
+  const int64_t b32 = (int64_t)(1 + R) * F * spw * 4, b16 = (int64_t)2 * R * spw * 2;
+  return (b32 + b16 + 15) & ~(int64_t)15;
+}
+
+// Copy of sessions [s0, s0 + nsess) into this block's shadow piece, eight loads in flight per
+// thread before their stores.
+__device__ inline void checkpoint_sessions(const CheckpointMap& m, uint8_t* piece, int64_t s0, int nsess, int tid,
+                                           int nthreads) {
+  const int n32 = (1 + m.R) * m.F * nsess, n16 = 2 * m.R * nsess;
+  uint32_t* d32 = (uint32_t*)piece;
+  uint16_t* d16 = (uint16_t*)(piece + (int64_t)(1 + m.R) * m.F * m.spw * 4);
+  for (int base = 0; base < n32; base += 8 * nthreads) {
     uint32_t v[8];
 #pragma unroll
     for (int u = 0; u < 8; u++) {
-      const int q = base + u * kWave + wl;
-      if (q < n32) v[u] = *src32(q);
+      const int q = base + u * nthreads + tid;
+      if (q < n32) v[u] = *m.at32(s0, nsess, q);
     }
 #pragma unroll
     for (int u = 0; u < 8; u++) {
-      const int q = base + u * kWave + wl;
-      if (q < n32) *(uint32_t*)shadow_of(src32(q)) = v[u];
+      const int q = base + u * nthreads + tid;
+      if (q < n32) d32[q] = v[u];
     }
   }
-  for (int base = 0; base < n16; base += 8 * kWave) {
+  for (int base = 0; base < n16; base += 8 * nthreads) {
     uint16_t v[8];
 #pragma unroll
     for (int u = 0; u < 8; u++) {
-      const int q = base + u * kWave + wl;
-      if (q < n16) v[u] = *src16(q);
+      const int q = base + u * nthreads + tid;
+      if (q < n16) v[u] = *m.at16(s0, nsess, q);
     }
 #pragma unroll
     for (int u = 0; u < 8; u++) {
-      const int q = base + u * kWave + wl;
-      if (q < n16) *(uint16_t*)shadow_of(src16(q)) = v[u];
+      const int q = base + u * nthreads + tid;
+      if (q < n16) d16[q] = v[u];
     }
   }
 }
 
-template <int P>
-__global__ __launch_bounds__(kWave) void synctest_pipelined_kernel(PipeParams p) {
-  if (*p.fail_f0 >= 0) return;  // an earlier launch failed: the host replays from its checkpoint
-  const int wl = threadIdx.x;
-  const int K = p.K, cd = p.cd, R = p.R;
-  const int g = wl / K, j = wl - g * K;
-  const int64_t L = p.L;
-  const int64_t s = (int64_t)blockIdx.x * p.spw + g;  // session of this lane
-  const bool valid = g < p.spw && s < L && p.lane_status[s] == GGRS_LANE_RUNNING;
-  const int64_t sl = valid ? s : 0;
-  const int base = g * K;
-  const int src_prev = base + (j == 0 ? K - 1 : j - 1);  // lane of chain c-1
-  constexpr int F = state_fields(P);
-  BoxState<P> st;
-#pragma unroll
-  for (int k = 0; k < F; k++) st.w[k] = 0;
-  uint64_t mask = 0;
-  const int32_t t_end = p.f0 + p.n + cd;
-  int32_t i = ((p.f0 - j) % K + K) % K;  // step of this lane's chain at t = f0
-  // input of frame t-cd, fetched one step ahead so its load is issued before this step's stores
-  // (loads and stores retire in order on one vmcnt: a load behind the stores would wait for them)
-  uint32_t in_next = load_inputs<P>(p.inputs, (int64_t)((p.f0 - cd) % p.cap) * L + sl);
-  for (int32_t t = p.f0; t < t_end; ++t, i = (i + 1 == K ? 0 : i + 1)) {
-    const int32_t c = t - i;
-    const bool active = valid && c >= p.f0 && c < p.f0 + p.n;
-    const int32_t gf = t - cd;  // the frame every chain of the session holds at this step
-    const uint32_t in = in_next;
-    if (t + 1 < t_end) in_next = load_inputs<P>(p.inputs, (int64_t)((gf + 1) % p.cap) * L + sl);
-    // LoadGameState of chain c: the cell chain c-1 is saving in this step
-    BoxState<P> from;
-#pragma unroll
-    for (int k = 0; k < F; k++) from.w[k] = __shfl(st.w[k], src_prev, kWave);
-    if (i == 0) {
-      if (c == p.f0) load_state<P>(st, p.ring + (int64_t)(gf % R) * F * L + sl, L);
-      else st = from;
-      if (s == p.corrupt_lane && c == p.corrupt_frame) st.w[fld_x(P, 0)] ^= 1u;
-      mask = 0;
-    }
-    const uint16_t ck = fletcher16_state<P>(st);
-    // first-seen checksum of frame gf: chain gf's save of it in this very step, when chain gf
-    // belongs to this launch; otherwise the value an earlier launch stored in first_ck
-    const int src_first = base + ((gf % K) + K) % K;
-    const uint16_t first_here = (uint16_t)__shfl((int)ck, src_first, kWave);
-    if (active && i > 0) {
-      store_state<P>(st, p.ring + (int64_t)(gf % R) * F * L + s, L);  // SaveGameState(gf)
-      p.ring_ck[(int64_t)(gf % R) * L + s] = ck;
-      if (i < cd) {
-        const uint16_t first = gf >= p.f0 ? first_here : p.first_ck[(int64_t)(gf % R) * L + s];
-        if (ck != first) mask |= 1ull << (i - 1);  // compared at call c+1 (frame c+1-cd+i-1)
-      } else {
-        p.first_ck[(int64_t)(gf % R) * L + s] = ck;
-      }
-    }
-    if (active) advance_state<P>(st, in, 0u);
-    if (active && i == cd) {
-      if (p.trace) p.trace[(int64_t)(c % p.trace_cap) * L + s] = fletcher16_state<P>(st);
-      if (c == p.f0 + p.n - 1) store_state<P>(st, p.cur + s, L);
-      if (mask) atomicCAS(p.fail_f0, -1, p.f0);
-    }
-  }
+// Restore of a failed launch's checkpoint: block b writes its piece back into the arena.
+__global__ __launch_bounds__(256) void restore_kernel(CheckpointMap m, const uint8_t* shadow, int64_t block_bytes) {
+  const int64_t s0 = (int64_t)blockIdx.x * m.spw;
+  const int nsess = (int)((m.L - s0) < m.spw ? (m.L - s0) : m.spw);
+  const uint8_t* piece = shadow + (int64_t)blockIdx.x * block_bytes;
+  const uint32_t* s32 = (const uint32_t*)piece;
+  const uint16_t* s16 = (const uint16_t*)(piece + (int64_t)(1 + m.R) * m.F * m.spw * 4);
+  const int n32 = (1 + m.R) * m.F * nsess, n16 = 2 * m.R * nsess;
+  for (int q = threadIdx.x; q < n32; q += blockDim.x) *m.at32(s0, nsess, q) = s32[q];
+  for (int q = threadIdx.x; q < n16; q += blockDim.x) *m.at16(s0, nsess, q) = s16[q];
 }
 
-// The same pipelined program with the players of a chain on Pp adjacent lanes (Pp = P rounded
-// up to a power of two): each lane steps one player (State::advance's per-player loop body is
-// independent across players, ex_game.rs:275-332), so a wavefront issues half (P = 2) the
-// instructions per step and twice the wavefronts share the chip.  The frame counter lives in
-// every lane of a chain; the Fletcher-16 sums are per-lane partials over the lane's own fields
-// (player 0 adds the frame field and the constants), combined by an xor-butterfly across the Pp
-// lanes.  Used whenever (cd+1) * Pp <= 64.
-template <int P>
-__device__ inline void partial_fletcher(uint32_t frame, const uint32_t (&w)[5], int pl, uint32_t& s1,
-                                        uint32_t& s2) {
-  constexpr int n = Fletcher<P>::n;
-  s1 = 0;
-  s2 = 0;
-  if (pl >= P) return;
-  const int ks[5] = {fld_x(P, 0), fld_y(P, 0), fld_vx(P, 0), fld_vy(P, 0), fld_rot(P, 0)};
-  const int dk[5] = {2, 2, 2, 2, 1};  // field index stride per player
-#pragma unroll
-  for (int q = 0; q < 5; q++) {
-    const int k = ks[q] + dk[q] * pl;
-    const uint32_t wt = weights_at(n, fld_offset(P, k));
-    s1 = dot4_u8(w[q], 0x01010101u, s1);
-    s2 = dot4_u8(w[q], wt, s2);
-  }
-  if (pl == 0) {
-    s1 = dot4_u8(frame, 0x01010101u, s1 + Fletcher<P>::kSum1Const);
-    s2 = dot4_u8(frame, weights_at(n, 0), s2 + Fletcher<P>::kSum2Const);
-  }
-}
+// Every store of the v4 kernel is a buffer store whose offset is pushed out of the descriptor's
+// range on lanes that must not store (no exec-mask branches); buffers must be < 1 GiB.
+constexpr uint32_t kOob = 0x40000000u;  // >= every descriptor's num_records; two of them never wrap
 
-template <int P, int Pp>
-__device__ inline uint16_t chain_fletcher(uint32_t frame, const uint32_t (&w)[5], int pl) {
-  uint32_t s1, s2;
-  partial_fletcher<P>(frame, w, pl, s1, s2);
-#pragma unroll
-  for (int m = 1; m < Pp; m <<= 1) {
-    s1 += (uint32_t)__shfl_xor((int)s1, m, kWave);
-    s2 += (uint32_t)__shfl_xor((int)s2, m, kWave);
-  }
-  return (uint16_t)(((s2 % 255u) << 8) | (s1 % 255u));
+__device__ inline __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 
 // LDS staging of the inputs: every chain of a session reads the same input byte per step, and a
@@ -317,420 +253,6 @@ __device__ inline uint16_t chain_fletcher(uint32_t frame, const uint32_t (&w)[5]
 // LDS, and the loop body issues no global loads at all.
 constexpr int kStageFrames = 256;
 constexpr int kMaxRampFrames = 64;  // first-seen checksums of frames f0-cd .. f0-1 (cd <= 62)
-
-template <int P>
-__global__ __launch_bounds__(kWave) void synctest_pipelined_split_kernel(PipeParams p) {
-  constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
-  __shared__ uint8_t lds_in[kStageFrames * kWave];           // [frame][session-in-block][Pp]
-  __shared__ uint16_t lds_first[kMaxRampFrames * kWave];      // [ramp frame][session-in-block]
-  __shared__ uint32_t lds_cell[kWave * 6];                    // chain f0's LoadGameState, per lane
-  if (*p.fail_f0 >= 0) return;
-  const int wl = threadIdx.x;
-  const int K = p.K, cd = p.cd, R = p.R;
-  const int G = K * Pp;
-  const int g = wl / G, r = wl - g * G;
-  const int j = r / Pp, pl = r - j * Pp;  // chain slot, player
-  const int64_t L = p.L;
-  const int spw = p.spw;
-  const int64_t s0 = (int64_t)blockIdx.x * spw;  // first session of this block
-  const int64_t s = s0 + g;
-  const int nsess = (int)((L - s0) < spw ? (L - s0) : spw);
-  const bool valid = g < spw && s < L && p.lane_status[s] == GGRS_LANE_RUNNING;
-  const bool owner = valid && pl < P;
-  const int64_t sl = valid ? s : 0;
-  const int plc = pl < P ? pl : 0;
-  const int base = g * G;
-  const int src_prev = base + (j == 0 ? K - 1 : j - 1) * Pp + pl;
-  constexpr int F = state_fields(P);
-  const int kx = fld_x(P, plc), ky = fld_y(P, plc), kvx = fld_vx(P, plc), kvy = fld_vy(P, plc),
-            krot = fld_rot(P, plc);
-  const int32_t g0 = p.f0 - cd;  // first frame any chain of this launch steps
-  // first-seen checksums of the frames saved by the previous launch (frames g0 .. f0-1)
-  for (int q = wl; q < cd * nsess; q += kWave) {
-    const int gg = q / nsess, ss = q - gg * nsess;
-    lds_first[gg * kWave + ss] = p.first_ck[(int64_t)((g0 + gg) % R) * L + s0 + ss];
-  }
-  // the cell chain f0 loads: frame f0-cd, saved by the previous launch.  Parked in LDS so the
-  // loop reads it with ds_read: a register first used inside the loop would put a vmcnt wait in
-  // the loop body, and vmcnt also waits for the step's ring stores.
-  {
-    const uint32_t* cell = p.ring + (int64_t)(g0 % R) * F * L + sl;
-    lds_cell[wl * 6 + 0] = cell[0];
-    lds_cell[wl * 6 + 1] = cell[kx * L];
-    lds_cell[wl * 6 + 2] = cell[ky * L];
-    lds_cell[wl * 6 + 3] = cell[kvx * L];
-    lds_cell[wl * 6 + 4] = cell[kvy * L];
-    lds_cell[wl * 6 + 5] = cell[krot * L];
-  }
-  __syncthreads();
-  uint32_t frame = 0;
-  uint32_t w[5] = {0, 0, 0, 0, 0};  // x, y, vx, vy, rot of this lane's player
-  uint64_t mask = 0;
-  const int32_t t_end = p.f0 + p.n + cd;
-  int32_t i = ((p.f0 - j) % K + K) % K;
-  const int row = nsess * Pp;  // staged bytes per frame
-  // wave-uniform slot counters of frame gf = t - cd, advanced by one per step (no divisions)
-  int32_t slot_r = g0 % R;       // ring slot of frame gf
-  int32_t slot_k = g0 % K;       // chain slot (lane group) of chain gf
-  int32_t slot_t = p.trace_cap ? (p.f0 - K) % p.trace_cap : 0;  // trace slot of chain t - K (f0 >= K)
-  const uint32_t corrupt_on = (p.corrupt_frame >= 0 && s == p.corrupt_lane && pl == 0) ? 1u : 0u;
-  for (int32_t t = p.f0; t < t_end; ++t) {
-    const int32_t c = t - i;
-    const bool active = valid && c >= p.f0 && c < p.f0 + p.n;
-    const int32_t gf = t - cd;
-    const int32_t rel = gf - g0;
-    if ((rel & (kStageFrames - 1)) == 0) {  // stage the next kStageFrames frames of input
-      __syncthreads();
-      const int nf = (t_end - t) < kStageFrames ? (t_end - t) : kStageFrames;
-      for (int q = wl; q < nf * row; q += kWave) {
-        const int ff = q / row, b = q - ff * row;
-        lds_in[ff * row + b] = p.inputs[((int64_t)((gf + ff) % p.cap) * L + s0) * Pp + b];
-      }
-      __syncthreads();
-    }
-    // (1) LoadGameState hand-off: the cell chain c-1 saves in this step, from its lane's registers
-    uint32_t from[6];
-    from[0] = (uint32_t)__shfl((int)frame, src_prev, kWave);
-#pragma unroll
-    for (int q = 0; q < 5; q++) from[q + 1] = (uint32_t)__shfl((int)w[q], src_prev, kWave);
-    const uint32_t in = lds_in[(rel & (kStageFrames - 1)) * row + g * Pp + pl];
-    // (2) Fletcher-16 of the registers as they stand: the cell this chain saves now (i >= 1) or, on
-    // a lane about to start a chain (i == 0), the final state of the chain that ended last step --
-    // its display checksum (ex_game.rs:121-126); plus chain gf's value: the first-seen checksum
-    const uint16_t ck = chain_fletcher<P, Pp>(frame, w, pl);
-    uint16_t first = (uint16_t)__shfl((int)ck, base + slot_k * Pp, kWave);
-    if (rel < cd) first = lds_first[rel * kWave + g];  // frame gf was saved by the previous launch
-    // (3) SaveGameState(gf) on every chain past its load
-    if (active && i > 0) {
-      uint32_t* cell = p.ring + (int64_t)slot_r * F * L + s;
-      if (owner) {
-        cell[kx * L] = w[0];
-        cell[ky * L] = w[1];
-        cell[kvx * L] = w[2];
-        cell[kvy * L] = w[3];
-        cell[krot * L] = w[4];
-      }
-      if (pl == 0) {
-        cell[0] = frame;
-        p.ring_ck[(int64_t)slot_r * L + s] = ck;
-        if (i == cd) p.first_ck[(int64_t)slot_r * L + s] = ck;
-      }
-    }
-    // checksums_consistent(gf) at call c+1 for the re-saves (i in 1..cd-1), branch-free
-    const bool cmp = active && pl == 0 && i > 0 && i < cd && ck != first;
-    mask = (i == 0 ? 0ull : mask) | ((uint64_t)cmp << ((i - 1) & 63));
-    if (i == 0 && p.trace && valid && pl == 0 && c - K >= p.f0 && c - K < p.f0 + p.n)
-      p.trace[(int64_t)slot_t * L + s] = ck;
-    // (4) the chain starting now takes the loaded cell (the launch's first chain: from HBM via LDS)
-    if (t == p.f0) {
-      if (i == 0) {
-        frame = lds_cell[wl * 6];
-#pragma unroll
-        for (int q = 0; q < 5; q++) w[q] = lds_cell[wl * 6 + 1 + q];
-      }
-    } else {
-      frame = i == 0 ? from[0] : frame;
-#pragma unroll
-      for (int q = 0; q < 5; q++) w[q] = i == 0 ? from[q + 1] : w[q];
-    }
-    w[0] ^= (i == 0 && c == p.corrupt_frame) ? corrupt_on : 0u;
-    // (5) AdvanceFrame(gf) -- on every lane (idle lanes hold finite states; their result is unused)
-    frame = (uint32_t)((int32_t)frame + 1);
-    {
-      float x = __builtin_bit_cast(float, w[0]), y = __builtin_bit_cast(float, w[1]);
-      float vx = __builtin_bit_cast(float, w[2]), vy = __builtin_bit_cast(float, w[3]);
-      float rot = __builtin_bit_cast(float, w[4]);
-      advance_player(x, y, vx, vy, rot, in);
-      w[0] = __builtin_bit_cast(uint32_t, x);
-      w[1] = __builtin_bit_cast(uint32_t, y);
-      w[2] = __builtin_bit_cast(uint32_t, vx);
-      w[3] = __builtin_bit_cast(uint32_t, vy);
-      w[4] = __builtin_bit_cast(uint32_t, rot);
-    }
-    if (active && i == cd) {  // chain end
-      if (c == p.f0 + p.n - 1) {
-        uint32_t* cur = p.cur + s;
-        if (owner) {
-          cur[kx * L] = w[0];
-          cur[ky * L] = w[1];
-          cur[kvx * L] = w[2];
-          cur[kvy * L] = w[3];
-          cur[krot * L] = w[4];
-        }
-        if (pl == 0) cur[0] = frame;
-      }
-      if (pl == 0 && mask) atomicCAS(p.fail_f0, -1, p.f0);
-    }
-    i = i + 1 == K ? 0 : i + 1;
-    slot_r = slot_r + 1 == R ? 0 : slot_r + 1;
-    slot_k = slot_k + 1 == K ? 0 : slot_k + 1;
-    if (p.trace_cap) slot_t = slot_t + 1 == p.trace_cap ? 0 : slot_t + 1;
-  }
-  if (p.trace) {  // display checksum of the launch's last chain (it ended at the last step)
-    const uint16_t ck = chain_fletcher<P, Pp>(frame, w, pl);
-    const int32_t last = p.f0 + p.n - 1;
-    if (valid && pl == 0 && j == last % K) p.trace[(int64_t)(last % p.trace_cap) * L + s] = ck;
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// Pipelined SyncTest, v3: the split kernel's schedule (chains on lanes, players split over Pp
-// lanes, LDS-staged inputs) with the step's latency chain shortened.  Per-wave counters showed the
-// split kernel latency-bound (one wave per SIMD, 34% of wave cycles parked on s_waitcnt, 81 SALU
-// per step), so:
-//   * the frame counter is wave-uniform (every chain of every session holds frame t - cd at step
-//     t), so it lives in a scalar and is never shuffled;
-//   * the Pp-lane Fletcher combine uses DPP quad permutes, not ds_bpermute;
-//   * the first-seen comparison's broadcast is consumed one step later (its LDS round trip
-//     overlaps the next step's hand-off), folded into the mask before the chain-end check;
-//   * ring / checksum / trace stores are buffer stores whose offset is pushed out of the
-//     descriptor's range on lanes that must not store (no exec-mask branches);
-//   * the steady state (every chain of the launch active, frame past the ramp) runs in a loop
-//     specialised for it; ramp and tail steps take the general body.
-// Requires every buffer the stores touch to be < 1 GiB (host falls back to the split kernel).
-constexpr uint32_t kOob = 0x40000000u;  // >= every descriptor's num_records; two of them never wrap
-
-__device__ inline __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
-}
-
-// v from the lane Pp below (DPP wave_shr:1, Pp times); lanes < Pp get garbage (callers select)
-template <int Pp>
-__device__ inline uint32_t wave_shr_lanes(uint32_t v) {
-#pragma unroll
-  for (int k = 0; k < Pp; k++) v = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, true);
-  return v;
-}
-
-template <int Pp>
-__device__ inline uint32_t quad_sum(uint32_t v) {
-  if constexpr (Pp >= 2) v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // xor 1
-  if constexpr (Pp >= 4) v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // xor 2
-  return v;
-}
-
-template <int P>
-__global__ __launch_bounds__(kWave) void synctest_pipelined_v3_kernel(PipeParams p) {
-  constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
-  constexpr int F = state_fields(P);
-  constexpr int n_bytes = Fletcher<P>::n;
-  // [frame][session-in-block][Pp], one slack frame for the core loop's read-ahead past a chunk
-  __shared__ uint8_t lds_in[(kStageFrames + 1) * kWave];
-  __shared__ uint16_t lds_first[kMaxRampFrames * kWave];  // [ramp frame][session-in-block]
-  __shared__ uint32_t lds_cell[kWave * 5];                // chain f0's LoadGameState, per lane
-  if (*p.fail_f0 >= 0) return;
-  const int wl = threadIdx.x;
-  const int K = p.K, cd = p.cd, R = p.R;
-  const int G = K * Pp;
-  const int g = wl / G, r = wl - g * G;
-  const int j = r / Pp, pl = r - j * Pp;
-  const int64_t L = p.L;
-  const int spw = p.spw;
-  const int64_t s0 = (int64_t)blockIdx.x * spw;
-  const int64_t s = s0 + g;
-  const int nsess = (int)((L - s0) < spw ? (L - s0) : spw);
-  const bool valid = g < spw && s < L && p.lane_status[s] == GGRS_LANE_RUNNING;
-  const bool owner = valid && pl < P;
-  const bool lead = valid && pl == 0;
-  const int64_t sl = valid ? s : 0;
-  const int plc = pl < P ? pl : 0;
-  const int base = g * G;
-  const int src_prev = (base + (j == 0 ? K - 1 : j - 1) * Pp + pl) * 4;  // ds_bpermute byte address
-  const int kq[5] = {fld_x(P, plc), fld_y(P, plc), fld_vx(P, plc), fld_vy(P, plc), fld_rot(P, plc)};
-  // descriptors and per-lane byte offsets (kOob where the lane never stores)
-  const uint32_t slot_bytes = (uint32_t)(F * L * 4), ck_slot_bytes = (uint32_t)(L * 2);
-  const __amdgpu_buffer_rsrc_t rs_ring = make_rsrc(p.ring, slot_bytes * (uint32_t)R);
-  const __amdgpu_buffer_rsrc_t rs_ck = make_rsrc(p.ring_ck, ck_slot_bytes * (uint32_t)R);
-  const __amdgpu_buffer_rsrc_t rs_first = make_rsrc(p.first_ck, ck_slot_bytes * (uint32_t)R);
-  const __amdgpu_buffer_rsrc_t rs_trace =
-      make_rsrc(p.trace, p.trace ? ck_slot_bytes * (uint32_t)p.trace_cap : 0u);
-  uint32_t fo[5];
-#pragma unroll
-  for (int q = 0; q < 5; q++) fo[q] = owner ? (uint32_t)((kq[q] * L + s) * 4) : kOob;
-  const uint32_t fo_frame = lead ? (uint32_t)(s * 4) : kOob;
-  const uint32_t co = lead ? (uint32_t)(s * 2) : kOob;
-  // Fletcher weights of this lane's five fields (the frame's part is added by lane pl == 0)
-  uint32_t wt[5];
-#pragma unroll
-  for (int q = 0; q < 5; q++) wt[q] = owner ? weights_at(n_bytes, fld_offset(P, kq[q])) : 0u;
-  const uint32_t one4 = owner ? 0x01010101u : 0u;
-
-  const int32_t g0 = p.f0 - cd;
-  for (int q = wl; q < cd * nsess; q += kWave) {
-    const int gg = q / nsess, ss = q - gg * nsess;
-    lds_first[gg * kWave + ss] = p.first_ck[(int64_t)((g0 + gg) % R) * L + s0 + ss];
-  }
-  {
-    const uint32_t* cell = p.ring + (int64_t)(g0 % R) * F * L + sl;
-#pragma unroll
-    for (int q = 0; q < 5; q++) lds_cell[wl * 5 + q] = cell[kq[q] * L];
-  }
-  __syncthreads();
-
-  uint32_t w[5] = {0, 0, 0, 0, 0};
-  uint64_t mask = 0;
-  // the previous step's comparison, finished at the next step (its broadcast is still in flight)
-  uint32_t pend_ck = 0, pend_first = 0;
-  bool pend_cmp = false;
-  int pend_bit = 0;
-  const int32_t t_end = p.f0 + p.n + cd;
-  int32_t i = ((p.f0 - j) % K + K) % K;
-  const int row = nsess * Pp;
-  int32_t slot_r = g0 % R;
-  int32_t slot_k = g0 % K;
-  int32_t slot_t = p.trace_cap ? (p.f0 - K) % p.trace_cap : 0;
-  const uint32_t corrupt_on = (p.corrupt_frame >= 0 && s == p.corrupt_lane && pl == 0) ? 1u : 0u;
-  const int32_t ramp_end = min(p.f0 + cd, t_end);
-  const int32_t core_end = max(ramp_end, p.f0 + p.n);
-
-  auto stage = [&](int32_t t) {
-    __syncthreads();
-    const int32_t gf = t - cd;
-    const int nf = (t_end - t) < kStageFrames ? (t_end - t) : kStageFrames;
-    for (int q = wl; q < nf * row; q += kWave) {
-      const int ff = q / row, b = q - ff * row;
-      lds_in[ff * row + b] = p.inputs[((int64_t)((gf + ff) % p.cap) * L + s0) * Pp + b];
-    }
-    __syncthreads();
-  };
-
-  // One step t.  kCore: every chain of the launch is active, t > f0 + cd - 1 and t < f0 + n.
-  auto step = [&](auto core_tag, int32_t t) {
-    constexpr bool kCore = decltype(core_tag)::value;
-    const int32_t c = t - i;
-    const bool active = kCore ? valid : (valid && c >= p.f0 && c < p.f0 + p.n);
-    const int32_t gf = t - cd;
-    const int32_t rel = t - p.f0;
-    const uint32_t frame = (uint32_t)gf;
-    // (1) hand-off: the cell chain c-1 saves in this step, from its lane's registers
-    uint32_t from[5];
-#pragma unroll
-    for (int q = 0; q < 5; q++) from[q] = (uint32_t)__builtin_amdgcn_ds_bpermute(src_prev, (int)w[q]);
-    const uint32_t in = lds_in[(rel & (kStageFrames - 1)) * row + g * Pp + pl];
-    // previous step's comparison (checksums_consistent of its re-saves), now that its broadcast landed
-    mask |= (uint64_t)(pend_cmp && pend_ck != pend_first) << pend_bit;
-    // (2) Fletcher-16 of the registers: frame gf's cell (i >= 1) or the ended chain's final state
-    uint32_t s1 = 0, s2 = 0;
-#pragma unroll
-    for (int q = 0; q < 5; q++) {
-      s1 = dot4_u8(w[q], one4, s1);
-      s2 = dot4_u8(w[q], wt[q], s2);
-    }
-    if (pl == 0) {
-      s1 = dot4_u8(frame, 0x01010101u, s1 + Fletcher<P>::kSum1Const);
-      s2 = dot4_u8(frame, weights_at(n_bytes, 0), s2 + Fletcher<P>::kSum2Const);
-    }
-    s1 = quad_sum<Pp>(s1);
-    s2 = quad_sum<Pp>(s2);
-    const uint32_t ck = ((s2 % 255u) << 8) | (s1 % 255u);
-    uint32_t first = (uint32_t)__builtin_amdgcn_ds_bpermute((base + slot_k * Pp) * 4, (int)ck);
-    if (!kCore && rel < cd) first = lds_first[rel * kWave + g];
-    // (3) SaveGameState(gf) on every chain past its load; first-seen value on chain gf (i == cd)
-    {
-      const bool sv = active && i > 0;
-      const uint32_t so = sv ? (uint32_t)slot_r * slot_bytes : kOob;
-#pragma unroll
-      for (int q = 0; q < 5; q++) __builtin_amdgcn_raw_buffer_store_b32(w[q], rs_ring, fo[q] + so, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(frame, rs_ring, fo_frame + so, 0, 0);
-      const uint32_t cso = sv ? (uint32_t)slot_r * ck_slot_bytes : kOob;
-      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ck, co + cso, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_first, co + (i == cd ? cso : kOob), 0, 0);
-    }
-    // display checksum of the chain that ended last step (i == 0 lanes)
-    {
-      const bool tr = i == 0 && c - K >= p.f0 && c - K < p.f0 + p.n;
-      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_trace,
-                                            co + (tr ? (uint32_t)slot_t * ck_slot_bytes : kOob), 0, 0);
-    }
-    // this step's comparison, finished next step
-    pend_cmp = active && pl == 0 && i > 0 && i < cd;
-    pend_ck = ck;
-    pend_first = first;
-    pend_bit = (i - 1) & 63;
-    // (4) the chain starting now takes the loaded cell (the launch's first chain: via LDS)
-    if (!kCore && t == p.f0) {
-      if (i == 0) {
-#pragma unroll
-        for (int q = 0; q < 5; q++) w[q] = lds_cell[wl * 5 + q];
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < 5; q++) w[q] = i == 0 ? from[q] : w[q];
-    }
-    if (i == 0) mask = 0;
-    w[0] ^= (i == 0 && c == p.corrupt_frame) ? corrupt_on : 0u;
-    // (5) AdvanceFrame(gf) on every lane
-    {
-      float x = __builtin_bit_cast(float, w[0]), y = __builtin_bit_cast(float, w[1]);
-      float vx = __builtin_bit_cast(float, w[2]), vy = __builtin_bit_cast(float, w[3]);
-      float rot = __builtin_bit_cast(float, w[4]);
-      advance_player(x, y, vx, vy, rot, in);
-      w[0] = __builtin_bit_cast(uint32_t, x);
-      w[1] = __builtin_bit_cast(uint32_t, y);
-      w[2] = __builtin_bit_cast(uint32_t, vx);
-      w[3] = __builtin_bit_cast(uint32_t, vy);
-      w[4] = __builtin_bit_cast(uint32_t, rot);
-    }
-    if (!kCore && active && i == cd && c == p.f0 + p.n - 1) {  // the launch's last chain: its state
-      uint32_t* cur = p.cur + s;
-      if (owner) {
-#pragma unroll
-        for (int q = 0; q < 5; q++) cur[kq[q] * L] = w[q];
-      }
-      if (pl == 0) cur[0] = frame + 1u;
-    }
-    i = i + 1 == K ? 0 : i + 1;
-    slot_r = slot_r + 1 == R ? 0 : slot_r + 1;
-    slot_k = slot_k + 1 == K ? 0 : slot_k + 1;
-    slot_t = slot_t + 1 == p.trace_cap ? 0 : slot_t + 1;
-  };
-
-  // chain ends: a chain's compares at i = 1..cd-1 are folded by the step where i == cd, so the
-  // mask is complete when it is tested (one step after the chain's last advance)
-  auto chain_end_check = [&]() {
-    if (pl == 0 && valid && i == 0 && mask) atomicCAS(p.fail_f0, -1, p.f0);
-  };
-
-  int32_t t = p.f0;
-  for (; t < ramp_end; ++t) {
-    if ((((t - p.f0)) & (kStageFrames - 1)) == 0) stage(t);
-    step(std::false_type(), t);
-    chain_end_check();
-  }
-  while (t < core_end) {
-    const int32_t rel = t - p.f0;
-    if ((rel & (kStageFrames - 1)) == 0) stage(t);
-    const int32_t chunk_end = min(core_end, t + (kStageFrames - (rel & (kStageFrames - 1))));
-    for (; t < chunk_end; ++t) {
-      step(std::true_type(), t);
-      chain_end_check();
-    }
-  }
-  for (; t < t_end; ++t) {
-    if ((((t - p.f0)) & (kStageFrames - 1)) == 0) stage(t);
-    step(std::false_type(), t);
-    chain_end_check();
-  }
-  // the last step's pending comparison belongs to a chain that does not end in this launch
-  if (p.trace) {  // display checksum of the launch's last chain (it ended at the last step)
-    uint32_t s1 = 0, s2 = 0;
-    const uint32_t frame = (uint32_t)(t_end - cd);
-#pragma unroll
-    for (int q = 0; q < 5; q++) {
-      s1 = dot4_u8(w[q], one4, s1);
-      s2 = dot4_u8(w[q], wt[q], s2);
-    }
-    if (pl == 0) {
-      s1 = dot4_u8(frame, 0x01010101u, s1 + Fletcher<P>::kSum1Const);
-      s2 = dot4_u8(frame, weights_at(n_bytes, 0), s2 + Fletcher<P>::kSum2Const);
-    }
-    s1 = quad_sum<Pp>(s1);
-    s2 = quad_sum<Pp>(s2);
-    const uint16_t ck = (uint16_t)(((s2 % 255u) << 8) | (s1 % 255u));
-    const int32_t last = p.f0 + p.n - 1;
-    if (valid && pl == 0 && j == last % K) p.trace[(int64_t)(last % p.trace_cap) * L + s] = ck;
-  }
-}
 
 // ------------------------------------------------------------------------------------------
 // Pipelined SyncTest, v4: static chain roles.  Same schedule and the same Loads, Saves and
@@ -750,8 +272,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v3_kernel(PipeParams
 //     sequential kernel anyway), folded into *fail_f0 once at the end;
 //   * step arithmetic: advance_player_lean (one add per thrust axis, clamp test s > 49, med3),
 //     Fletcher-16 mod 255 from doubled sums on 24-bit multiplies.
-// kDppRot: the rotation by DPP wave shifts (VALU) instead of ds_bpermute (LDS round trip).
-template <int P, bool kDppRot>
+template <int P>
 __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams p) {
   constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
   constexpr int F = state_fields(P);
@@ -760,7 +281,12 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
   __shared__ uint8_t lds_in[(kStageFrames + 1) * kWave];
   __shared__ uint16_t lds_first[kMaxRampFrames * kWave];  // [ramp frame][session-in-block]
   __shared__ uint32_t lds_cell[kWave * 5];                // chain f0's LoadGameState, per lane
-  if (*p.fail_f0 >= 0) return;
+  // An earlier launch failed: the shadow must keep the checkpoint from before that launch (the host
+  // restores it and replays from there), so this launch neither checkpoints nor runs.  A block of
+  // the failing launch itself still takes its checkpoint -- another block may have flagged the
+  // launch before this one was scheduled -- and only then stops.
+  const int32_t failed_f0 = *p.fail_f0;
+  if (failed_f0 >= 0 && failed_f0 != p.f0) return;
   const int wl = threadIdx.x;
   const int K = p.K, cd = p.cd, R = p.R;
   const int G = K * Pp;
@@ -777,7 +303,6 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
   const int plc = pl < P ? pl : 0;
   const int base = g * G;
   const int src_first = ((base + (cd - 1) * Pp) & (kWave - 1)) * 4;
-  const uint32_t keep_own = j == 0 ? 0xffffffffu : 0u;  // role 0 keeps its state in the rotation
   const int src_rot = (j == 0 ? wl : base + (j - 1) * Pp + pl) * 4;  // ds_bpermute form
   const int kq[5] = {fld_x(P, plc), fld_y(P, plc), fld_vx(P, plc), fld_vy(P, plc), fld_rot(P, plc)};
   const uint32_t slot_bytes = (uint32_t)(F * L * 4), ck_slot_bytes = (uint32_t)(L * 2);
@@ -813,7 +338,11 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
 
   // the launch checkpoint of this block's sessions (all of them, halted ones included: a restore
   // copies the whole shadow back), before any of this launch's stores
-  if (p.shadow) checkpoint_sessions(p, F, s0, nsess, wl);
+  {
+    const CheckpointMap m{L, R, F, spw, p.cur, p.ring, p.ring_ck, p.first_ck};
+    checkpoint_sessions(m, p.shadow + (int64_t)blockIdx.x * p.block_bytes, s0, nsess, wl, kWave);
+  }
+  if (failed_f0 >= 0) return;  // this launch is replayed from its checkpoint anyway
   const int32_t g0 = p.f0 - cd;
   for (int q = wl; q < cd * nsess; q += kWave) {
     const int gg = q / nsess, ss = q - gg * nsess;
@@ -895,23 +424,12 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
     // the previous step's comparison, one advance after its first-seen value was requested
     if (kCore) acc |= pend_ck ^ pend_first;
     const uint32_t frame1 = (uint32_t)(t - cd + 1);
-    // rotation for step t+1: role j takes role j-1's state, Pp lanes down; two DPP wave_shr:1
-    // moves (VALU, no LDS round trip) and role 0 keeps its own
+    // rotation for step t+1: role j takes role j-1's state, Pp lanes down (one ds_bpermute per
+    // field); role 0 keeps its own
     uint32_t nx[5];
 #pragma unroll
-    for (int q = 0; q < 5; q++) {
-      if constexpr (kDppRot) {
-        const uint32_t sh = wave_shr_lanes<Pp>(w[q]);
-        nx[q] = (w[q] & keep_own) | (sh & ~keep_own);  // a plain select here gets branched
-      } else {
-#ifdef GGRS_EXP_NO_ROT
-        nx[q] = w[q];
-#else
-        nx[q] = (uint32_t)__builtin_amdgcn_ds_bpermute(src_rot, (int)w[q]);
-#endif
-      }
-    }
-    if constexpr (!kDppRot) __builtin_amdgcn_sched_barrier(0);  // LDS latency behind the save
+    for (int q = 0; q < 5; q++) nx[q] = (uint32_t)__builtin_amdgcn_ds_bpermute(src_rot, (int)w[q]);
+    __builtin_amdgcn_sched_barrier(0);  // LDS latency behind the Fletcher sums and the saves
     // Fletcher-16 of the post-advance state (frame t-cd+1): the cell role j+1 saves at step t+1
     uint32_t d1 = dot4_u8(frame1, wf1, c1), d2 = dot4_u8(frame1, wf2, c2);
 #pragma unroll
@@ -927,11 +445,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
       d1 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d1, 0x4E, 0xF, 0xF, true);  // xor 2
       d2 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d2, 0x4E, 0xF, 0xF, true);
     }
-#ifdef GGRS_EXP_NO_FLETCHER
-    const uint32_t ck = w[0] & 0xffff;
-#else
     const uint32_t ck = fletcher_from_doubled(d1, d2);
-#endif
     uint32_t first = (uint32_t)__builtin_amdgcn_ds_bpermute(src_first, (int)ck);
     // the first save of frame t-cd+1 happened in the previous launch while its chain is not ours
     if (!kCore && rel + 1 < cd) first = lds_first[(rel + 1) * kWave + g];
@@ -939,20 +453,12 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
     const uint32_t sru = (uint32_t)sr, stu = (uint32_t)st;
     auto stores = [&]() {
       const uint32_t so = sru * slot_bytes, cso = sru * ck_slot_bytes;
-#ifndef GGRS_EXP_NO_FIELD_STORES  // timing experiments only (tools/exp_build.sh), never shipped
 #pragma unroll
       for (int q = 0; q < 5; q++) __builtin_amdgcn_raw_buffer_store_b32(w[q], rs_ring, fo[q], so, 0);
       __builtin_amdgcn_raw_buffer_store_b32(frame1, rs_ring, fo_frame, so, 0);
-#endif
-#if defined(GGRS_EXP_CK32)
-      __builtin_amdgcn_raw_buffer_store_b32(ck, rs_ring, co & ~3u, cso, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(ck, rs_ring, co_first & ~3u, cso, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(ck, rs_ring, co_trace & ~3u, stu * ck_slot_bytes, 0);
-#elif !defined(GGRS_EXP_NO_CK_STORES)
       __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ring, co, cso, 0);
       __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ring, co_first, cso, 0);
       __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ring, co_trace, stu * ck_slot_bytes, 0);
-#endif
     };
     if (kCore) {
       stores();
@@ -1021,21 +527,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
     step(std::false_type(), t, input_at(t));
   }
   bad |= __ballot(pend_ck != pend_first) & pend_lanes;
-#ifdef GGRS_EXP_CK32
-  bad = 0;  // timing experiment: the checksum rows hold garbage
-#endif
   if (bad && wl == __builtin_ctzll(bad)) atomicCAS(p.fail_f0, -1, p.f0);
-}
-
-// Checkpoint / restore of everything a SyncTest launch writes (cur, ring, ring_ck, first_ck):
-// dir 0 copies live -> shadow unless a launch already failed (then the shadow must keep the
-// state from before the failing launch); dir 1 copies shadow -> live.
-__global__ void checkpoint_kernel(uint4* live, uint4* shadow, int64_t n16, const int32_t* fail_f0, int dir) {
-  if (dir == 0 && *fail_f0 >= 0) return;
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n16; k += (int64_t)gridDim.x * blockDim.x) {
-    if (dir == 0) shadow[k] = live[k];
-    else live[k] = shadow[k];
-  }
 }
 
 struct RequestParams {
@@ -1087,45 +579,7 @@ __global__ __launch_bounds__(kWave) void requests_kernel(RequestParams p) {
 }  // namespace
 
 // ------------------------------------------------------------------------------ engine object
-struct ggrs_engine {
-  ggrs_config_t cfg{};
-  int Pp = 1, F = 1, R = 1, cap = 128;
-  int mode = 0;  // 0 fresh, 1 synctest program, 2 request program
-  hipStream_t stream = nullptr;
-  uint32_t* cur = nullptr;
-  uint32_t* ring = nullptr;
-  uint16_t* ring_ck = nullptr;
-  uint16_t* first_ck = nullptr;
-  uint8_t* inputs = nullptr;
-  int32_t* lane_status = nullptr;
-  int32_t* mis_frame = nullptr;
-  uint64_t* mis_mask = nullptr;
-  uint16_t* trace = nullptr;
-  uint8_t* staging = nullptr;  // device scratch for request inputs / status / request list
-  size_t staging_bytes = 0;
-  uint8_t* host_staging = nullptr;  // pinned host copy of a request call's list + inputs (one DMA)
-  size_t host_staging_bytes = 0;
-  // cur | ring | ring_ck | first_ck live in one arena so a launch checkpoint is one copy
-  uint8_t* arena = nullptr;
-  uint8_t* shadow = nullptr;
-  size_t arena_bytes = 0;
-  int32_t* fail_f0 = nullptr;  // f0 of the first pipelined launch whose checks failed, or -1
-  bool unverified = false;     // pipelined launches enqueued since the last resolve()
-  int path = GGRS_PATH_PIPELINED;
-  // host-side (lane-uniform) bookkeeping
-  int32_t current_frame = 0;
-  int32_t next_user_frame = 0;  // next user frame add_local_inputs expects
-  std::vector<int32_t> ring_tag;
-  int32_t corrupt_lane = -1, corrupt_frame = -1;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  bool timed = false;
-  // per-launch event pairs collected between ggrs_timing_reset and ggrs_timing_read
-  std::vector<hipEvent_t> tev;
-  size_t tev_used = 0;
-  bool collecting = false;
-  hipEvent_t ev_last0 = nullptr, ev_last1 = nullptr;
-};
-
+// (struct ggrs_engine and launch_timed live in engine.h, shared with requests.hip)
 namespace {
 
 int ensure_staging(ggrs_engine* e, size_t bytes) {
@@ -1138,41 +592,18 @@ int ensure_staging(ggrs_engine* e, size_t bytes) {
   return GGRS_OK;
 }
 
-// Brackets one fused launch with HIP events on the engine's stream (the stream the kernel runs
-// on), so ggrs_last_launch_ms / ggrs_timing_read report device time of exactly that kernel.
-template <typename K>
-int launch_timed(ggrs_engine* e, K&& launch) {
-  hipEvent_t a = e->ev0, b = e->ev1;
-  if (e->collecting) {
-    while (e->tev.size() < e->tev_used + 2) {
-      hipEvent_t ev;
-      HIP_TRY(hipEventCreate(&ev));
-      e->tev.push_back(ev);
-    }
-    a = e->tev[e->tev_used];
-    b = e->tev[e->tev_used + 1];
-    e->tev_used += 2;
-  }
-#ifdef GGRS_EXP_NO_LAUNCH_EVENTS  // timing experiment only (tools/exp_build.sh): launch gap without events
-  (void)a;
-  (void)b;
-  launch();
-  HIP_TRY(hipGetLastError());
-  return GGRS_OK;
-#endif
-  HIP_TRY(hipEventRecord(a, e->stream));
-  launch();
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(b, e->stream));
-  if (e->collecting) {  // keep last-launch queries valid too
-    e->ev_last0 = a;
-    e->ev_last1 = b;
-  } else {
-    e->ev_last0 = e->ev0;
-    e->ev_last1 = e->ev1;
-  }
-  e->timed = true;
-  return GGRS_OK;
+// The pipelined SyncTest kernel's geometry: sessions per 64-lane block (K = cd + 1 chain roles
+// times Pp player lanes per session), or 0 when a session does not fit one wavefront or a buffer
+// the kernel's descriptors address would exceed kOob (then the sequential kernel runs).
+int v4_sessions_per_block(const ggrs_engine* e) {
+  const int K = e->cfg.check_distance + 1;
+  if (e->cfg.check_distance < 2 || K * e->Pp > kWave) return 0;
+  const uint64_t L = (uint64_t)e->cfg.num_lanes;
+  const uint64_t ring_span = (uint64_t)((const uint8_t*)e->first_ck - (const uint8_t*)e->ring) + 2 * L * e->R;
+  const uint64_t trace_span =
+      e->trace ? (uint64_t)((const uint8_t*)e->trace - (const uint8_t*)e->ring) + 2 * L * e->cfg.trace_capacity : 0;
+  if ((uint64_t)e->F * 4 * L * e->R >= kOob || ring_span >= kOob || trace_span >= kOob) return 0;
+  return kWave / (K * e->Pp);
 }
 
 }  // namespace
@@ -1192,9 +623,9 @@ int ggrs_engine_destroy(ggrs_engine_t* e) {
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (e->host_staging) (void)hipHostFree(e->host_staging);
-  for (hipEvent_t ev : e->tev) (void)hipEventDestroy(ev);
-  if (e->ev0) (void)hipEventDestroy(e->ev0);
-  if (e->ev1) (void)hipEventDestroy(e->ev1);
+  if (e->batch.base) (void)hipHostFree(e->batch.base);
+  if (e->ev_begin) (void)hipEventDestroy(e->ev_begin);
+  if (e->ev_end) (void)hipEventDestroy(e->ev_end);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
   return GGRS_OK;
@@ -1239,25 +670,36 @@ int ggrs_engine_create(const ggrs_config_t* cfg, ggrs_engine_t** out) {
   const int64_t L = c.num_lanes;
   CTRY(hipSetDevice(c.device));
   CTRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
-  CTRY(hipEventCreate(&e->ev0));
-  CTRY(hipEventCreate(&e->ev1));
+  CTRY(hipEventCreate(&e->ev_begin));
+  CTRY(hipEventCreate(&e->ev_end));
   {
     auto up16 = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t b_cur = up16(sizeof(uint32_t) * e->F * L);
     const size_t b_ring = up16(sizeof(uint32_t) * (size_t)e->R * e->F * L);
     const size_t b_ck = up16(sizeof(uint16_t) * (size_t)e->R * L);
     e->arena_bytes = b_cur + b_ring + 2 * b_ck;
-    // the display-checksum trace follows the arena in the same allocation (outside the checkpointed
-    // range): the v4 kernel's stores then all go through one buffer descriptor
+    // the display-checksum trace follows the arena in the same allocation: the v4 kernel's stores
+    // then all go through one buffer descriptor
     const size_t b_trace = c.trace_capacity > 0 ? up16(sizeof(uint16_t) * (size_t)c.trace_capacity * L) : 0;
     CTRY(hipMalloc(&e->arena, e->arena_bytes + b_trace));
     if (b_trace) e->trace = (uint16_t*)(e->arena + e->arena_bytes);
-    CTRY(hipMalloc(&e->shadow, e->arena_bytes));
     CTRY(hipMemsetAsync(e->arena, 0, e->arena_bytes, e->stream));
     e->cur = (uint32_t*)e->arena;
     e->ring = (uint32_t*)(e->arena + b_cur);
     e->ring_ck = (uint16_t*)(e->arena + b_cur + b_ring);
     e->first_ck = (uint16_t*)(e->arena + b_cur + b_ring + b_ck);
+    // every ring cell starts as GameState::default's NULL_FRAME (frame_info.rs:16-23): the frame
+    // field is the cell's tag for per-lane request lists (requests.hip)
+    for (int s = 0; s < e->R; s++)
+      CTRY(hipMemsetD32Async((hipDeviceptr_t)(e->ring + (size_t)s * e->F * L), (int)GGRS_NULL_FRAME, (size_t)L,
+                             e->stream));
+    // the pipelined kernel's launch checkpoint: one contiguous piece per 64-lane block
+    const int spw = v4_sessions_per_block(e);
+    if (spw > 0) {
+      e->shadow_bytes = (size_t)grid_of(L, spw) * (size_t)checkpoint_block_bytes(e->R, e->F, spw);
+      CTRY(hipMalloc(&e->shadow, e->shadow_bytes));
+      CTRY(hipMemsetAsync(e->shadow, 0, e->shadow_bytes, e->stream));
+    }
   }
   CTRY(hipMalloc(&e->fail_f0, sizeof(int32_t)));
   CTRY(hipMemsetAsync(e->fail_f0, 0xff, sizeof(int32_t), e->stream));
@@ -1370,22 +812,13 @@ static int launch_sequential(ggrs_engine_t* e, int32_t f0, int32_t n) {
   });
 }
 
-static int checkpoint(ggrs_engine_t* e, int dir) {
-  const int64_t n16 = (int64_t)(e->arena_bytes / 16);
-  checkpoint_kernel<<<1024, 256, 0, e->stream>>>((uint4*)e->arena, (uint4*)e->shadow, n16, e->fail_f0, dir);
-  HIP_TRY(hipGetLastError());
-  return GGRS_OK;
-}
-
 static int launch_pipelined(ggrs_engine_t* e, int32_t f0, int32_t n) {
   PipeParams p;
-  p.arena = nullptr;
-  p.shadow = nullptr;
   p.L = e->cfg.num_lanes;
   p.R = e->R;
   p.cd = e->cfg.check_distance;
   p.K = p.cd + 1;
-  p.spw = kWave / p.K;
+  p.spw = v4_sessions_per_block(e);
   p.f0 = f0;
   p.n = n;
   p.cap = e->cap;
@@ -1400,76 +833,16 @@ static int launch_pipelined(ggrs_engine_t* e, int32_t f0, int32_t n) {
   p.lane_status = e->lane_status;
   p.fail_f0 = e->fail_f0;
   p.trace = e->trace;
+  p.shadow = e->shadow;
+  p.block_bytes = checkpoint_block_bytes(p.R, e->F, p.spw);
   e->unverified = true;
-  const int Pp = e->Pp;
-  const uint64_t F4L = (uint64_t)e->F * 4 * p.L;
-  const bool fits_v3 = F4L * p.R < kOob && (uint64_t)2 * p.L * p.R < kOob &&
-                       (uint64_t)2 * p.L * (uint64_t)std::max(p.trace_cap, 0) < kOob;
-  // v4 addresses ring, ring_ck and first_ck from the ring's base (one descriptor)
-  const bool fits_v4 = fits_v3 && (uint8_t*)e->ring_ck > (uint8_t*)e->ring && (uint8_t*)e->first_ck > (uint8_t*)e->ring_ck &&
-                       (uint64_t)((uint8_t*)e->first_ck - (uint8_t*)e->ring) + (uint64_t)2 * p.L * p.R < kOob &&
-                       (!e->trace || ((uint8_t*)e->trace > (uint8_t*)e->first_ck &&
-                                      (uint64_t)((uint8_t*)e->trace - (uint8_t*)e->ring) +
-                                              (uint64_t)2 * p.L * p.trace_cap < kOob));
-  const bool use_v4 = (e->path == GGRS_PATH_PIPELINED || e->path == GGRS_PATH_PIPELINED_V4_DPP) && p.K * Pp <= kWave && fits_v4;
-  if (use_v4) {
-    // the v4 kernel checkpoints its own sessions (checkpoint_sessions); other kernels get the copy
-    p.arena = e->arena;
-    p.shadow = e->shadow;
-  } else {
-    int rc = checkpoint(e, 0);
-    if (rc) return rc;
-  }
-  if (use_v4) {
-    p.spw = kWave / (p.K * Pp);
-    const int64_t grid = grid_of(p.L, p.spw);
-    const bool dpp = e->path == GGRS_PATH_PIPELINED_V4_DPP;
-    return launch_timed(e, [&] {
-      switch (e->cfg.num_players * 2 + (dpp ? 1 : 0)) {
-        case 2: synctest_pipelined_v4_kernel<1, false><<<grid, kWave, 0, e->stream>>>(p); break;
-        case 3: synctest_pipelined_v4_kernel<1, true><<<grid, kWave, 0, e->stream>>>(p); break;
-        case 4: synctest_pipelined_v4_kernel<2, false><<<grid, kWave, 0, e->stream>>>(p); break;
-        case 5: synctest_pipelined_v4_kernel<2, true><<<grid, kWave, 0, e->stream>>>(p); break;
-        case 6: synctest_pipelined_v4_kernel<3, false><<<grid, kWave, 0, e->stream>>>(p); break;
-        case 7: synctest_pipelined_v4_kernel<3, true><<<grid, kWave, 0, e->stream>>>(p); break;
-        case 8: synctest_pipelined_v4_kernel<4, false><<<grid, kWave, 0, e->stream>>>(p); break;
-        default: synctest_pipelined_v4_kernel<4, true><<<grid, kWave, 0, e->stream>>>(p); break;
-      }
-    });
-  }
-  if ((e->path == GGRS_PATH_PIPELINED || e->path == GGRS_PATH_PIPELINED_V3 ||
-       e->path == GGRS_PATH_PIPELINED_V4_DPP) && p.K * Pp <= kWave && fits_v3) {
-    p.spw = kWave / (p.K * Pp);
-    const int64_t grid = grid_of(p.L, p.spw);
-    return launch_timed(e, [&] {
-      switch (e->cfg.num_players) {
-        case 1: synctest_pipelined_v3_kernel<1><<<grid, kWave, 0, e->stream>>>(p); break;
-        case 2: synctest_pipelined_v3_kernel<2><<<grid, kWave, 0, e->stream>>>(p); break;
-        case 3: synctest_pipelined_v3_kernel<3><<<grid, kWave, 0, e->stream>>>(p); break;
-        default: synctest_pipelined_v3_kernel<4><<<grid, kWave, 0, e->stream>>>(p); break;
-      }
-    });
-  }
-  if ((e->path == GGRS_PATH_PIPELINED || e->path == GGRS_PATH_PIPELINED_SPLIT ||
-       e->path == GGRS_PATH_PIPELINED_V3 || e->path == GGRS_PATH_PIPELINED_V4_DPP) && p.K * Pp <= kWave) {
-    p.spw = kWave / (p.K * Pp);
-    const int64_t grid = grid_of(p.L, p.spw);
-    return launch_timed(e, [&] {
-      switch (e->cfg.num_players) {
-        case 1: synctest_pipelined_split_kernel<1><<<grid, kWave, 0, e->stream>>>(p); break;
-        case 2: synctest_pipelined_split_kernel<2><<<grid, kWave, 0, e->stream>>>(p); break;
-        case 3: synctest_pipelined_split_kernel<3><<<grid, kWave, 0, e->stream>>>(p); break;
-        default: synctest_pipelined_split_kernel<4><<<grid, kWave, 0, e->stream>>>(p); break;
-      }
-    });
-  }
   const int64_t grid = grid_of(p.L, p.spw);
   return launch_timed(e, [&] {
     switch (e->cfg.num_players) {
-      case 1: synctest_pipelined_kernel<1><<<grid, kWave, 0, e->stream>>>(p); break;
-      case 2: synctest_pipelined_kernel<2><<<grid, kWave, 0, e->stream>>>(p); break;
-      case 3: synctest_pipelined_kernel<3><<<grid, kWave, 0, e->stream>>>(p); break;
-      default: synctest_pipelined_kernel<4><<<grid, kWave, 0, e->stream>>>(p); break;
+      case 1: synctest_pipelined_v4_kernel<1><<<grid, kWave, 0, e->stream>>>(p); break;
+      case 2: synctest_pipelined_v4_kernel<2><<<grid, kWave, 0, e->stream>>>(p); break;
+      case 3: synctest_pipelined_v4_kernel<3><<<grid, kWave, 0, e->stream>>>(p); break;
+      default: synctest_pipelined_v4_kernel<4><<<grid, kWave, 0, e->stream>>>(p); break;
     }
   });
 }
@@ -1485,10 +858,13 @@ static int resolve(ggrs_engine_t* e) {
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->unverified = false;
   if (f < 0) return GGRS_OK;
-  int rc = checkpoint(e, 1);
-  if (rc) return rc;
+  const int spw = v4_sessions_per_block(e);
+  const CheckpointMap m{(int64_t)e->cfg.num_lanes, e->R, e->F, spw, e->cur, e->ring, e->ring_ck, e->first_ck};
+  restore_kernel<<<grid_of(e->cfg.num_lanes, spw), 256, 0, e->stream>>>(m, e->shadow,
+                                                                         checkpoint_block_bytes(e->R, e->F, spw));
+  HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemsetAsync(e->fail_f0, 0xff, sizeof(int32_t), e->stream));
-  rc = launch_sequential(e, f, e->current_frame - f);
+  int rc = launch_sequential(e, f, e->current_frame - f);
   if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(e->stream));
   return GGRS_OK;
@@ -1497,7 +873,8 @@ static int resolve(ggrs_engine_t* e) {
 int ggrs_synctest_advance_frames(ggrs_engine_t* e, int32_t n) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
   if (n < 0) return set_error(GGRS_E_INVALID, "n_frames must be >= 0");
-  if (e->mode == 2) return set_error(GGRS_E_STATE, "engine already driven by ggrs_handle_requests");
+  if (e->mode == kModeLockstepRequests || e->mode == kModeLaneRequests)
+    return set_error(GGRS_E_STATE, "engine already driven by request lists");
   if (n == 0) return GGRS_OK;
   // every frame run needs its (delayed) input queued: SyncTestSession requires input for all
   // players before advance_frame ("Missing local input", sync_test_session.rs:110-114)
@@ -1506,12 +883,13 @@ int ggrs_synctest_advance_frames(ggrs_engine_t* e, int32_t n) {
     return set_error(GGRS_E_INVALID,
                      "Missing local input while calling advance_frame(): frame %lld not added",
                      (long long)last_needed_user);
-  e->mode = 1;
+  e->mode = kModeSyncTest;
   HIP_TRY(hipSetDevice(e->cfg.device));
   const int32_t cd = e->cfg.check_distance;
   int32_t f0 = e->current_frame, left = n;
-  // warm-up calls (f <= cd: no rollback yet) and cd == 0 / 1 take the sequential kernel
-  if (e->path == GGRS_PATH_SEQUENTIAL || cd <= 1) {
+  // warm-up calls (f <= cd: no rollback yet), cd <= 1 and sessions that do not fit the pipelined
+  // kernel take the sequential kernel
+  if (e->path == GGRS_PATH_SEQUENTIAL || v4_sessions_per_block(e) == 0) {
     int rc = launch_sequential(e, f0, left);
     if (rc) return rc;
     left = 0;
@@ -1540,8 +918,7 @@ int ggrs_synctest_advance_frames(ggrs_engine_t* e, int32_t n) {
 
 int ggrs_set_synctest_path(ggrs_engine_t* e, int32_t path) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
-  if (path != GGRS_PATH_PIPELINED && path != GGRS_PATH_SEQUENTIAL && path != GGRS_PATH_PIPELINED_WHOLE &&
-      path != GGRS_PATH_PIPELINED_SPLIT && path != GGRS_PATH_PIPELINED_V3 && path != GGRS_PATH_PIPELINED_V4_DPP)
+  if (path != GGRS_PATH_PIPELINED && path != GGRS_PATH_SEQUENTIAL)
     return set_error(GGRS_E_INVALID, "unknown path %d", path);
   int rc = resolve(e);
   if (rc) return rc;
@@ -1552,7 +929,8 @@ int ggrs_set_synctest_path(ggrs_engine_t* e, int32_t path) {
 int ggrs_handle_requests(ggrs_engine_t* e, const ggrs_request_t* reqs, int32_t n_reqs,
                          const uint8_t* inputs, const uint8_t* status) {
   if (!e || (!reqs && n_reqs > 0)) return set_error(GGRS_E_INVALID, "null argument");
-  if (e->mode == 1) return set_error(GGRS_E_STATE, "engine already driven by ggrs_synctest_advance_frames");
+  if (e->mode == kModeSyncTest) return set_error(GGRS_E_STATE, "engine already driven by ggrs_synctest_advance_frames");
+  if (e->mode == kModeLaneRequests) return set_error(GGRS_E_STATE, "engine already driven by per-lane request lists");
   if (n_reqs <= 0) return GGRS_OK;
   // validate the whole list against the lane-uniform cell bookkeeping before touching the device
   std::vector<int32_t> tags = e->ring_tag;
@@ -1577,7 +955,7 @@ int ggrs_handle_requests(ggrs_engine_t* e, const ggrs_request_t* reqs, int32_t n
   }
   if (n_adv > 0 && !inputs) return set_error(GGRS_E_INVALID, "inputs required for AdvanceFrame requests");
   if (e->trace && n_adv > e->cfg.trace_capacity) return set_error(GGRS_E_INVALID, "more advances than trace_capacity");
-  e->mode = 2;
+  e->mode = kModeLockstepRequests;
   HIP_TRY(hipSetDevice(e->cfg.device));
   const int64_t L = e->cfg.num_lanes;
   const int P = e->cfg.num_players, Pp = e->Pp;
@@ -1663,6 +1041,8 @@ int ggrs_synchronize(ggrs_engine_t* e) {
 
 int ggrs_current_frame(const ggrs_engine_t* e, int32_t* out) {
   if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
+  if (e->mode == kModeLaneRequests)
+    return set_error(GGRS_E_STATE, "per-lane request lists: every lane has its own frame (ggrs_read_lane_frames)");
   *out = e->current_frame;
   return GGRS_OK;
 }
@@ -1682,6 +1062,8 @@ int ggrs_read_mismatches(ggrs_engine_t* e, int32_t* st, int32_t* mf, uint64_t* m
 int ggrs_read_save_checksums(ggrs_engine_t* e, int32_t frame, uint16_t* out) {
   if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
   { int rc_ = resolve(e); if (rc_) return rc_; }
+  if (e->mode == kModeLaneRequests)
+    return set_error(GGRS_E_STATE, "per-lane request lists return their save checksums from each call");
   if (frame < 0 || e->ring_tag[frame % e->R] != frame)
     return set_error(GGRS_E_PRECONDITION, "no saved cell for frame %d", frame);
   HIP_TRY(hipSetDevice(e->cfg.device));
@@ -1727,8 +1109,10 @@ int ggrs_read_ring(ggrs_engine_t* e, int32_t lane, int32_t* frames, uint16_t* ck
   }
   HIP_TRY(hipStreamSynchronize(e->stream));
   for (int s = 0; s < e->R; s++) {
-    const bool has = e->ring_tag[s] != GGRS_NULL_FRAME;
-    if (frames) frames[s] = e->ring_tag[s];
+    // per-lane request lists: a lane's cell tags are the frame fields of its own ring cells
+    const int32_t tag = e->mode == kModeLaneRequests ? (int32_t)w[(size_t)s * e->F] : e->ring_tag[s];
+    const bool has = tag != GGRS_NULL_FRAME;
+    if (frames) frames[s] = tag;
     if (cks) cks[s] = has ? c[s] : 0;
     if (states) {
       if (has) serialize_state_bytes(&w[(size_t)s * e->F], e->cfg.num_players, states + (size_t)s * sb);
@@ -1764,9 +1148,8 @@ int ggrs_debug_corrupt_on_load(ggrs_engine_t* e, int32_t lane, int32_t frame) {
 
 int ggrs_last_launch_ms(ggrs_engine_t* e, float* ms) {
   if (!e || !ms) return set_error(GGRS_E_INVALID, "null argument");
-  if (!e->timed) return set_error(GGRS_E_STATE, "no fused launch yet");
-  HIP_TRY(hipEventSynchronize(e->ev_last1));
-  HIP_TRY(hipEventElapsedTime(ms, e->ev_last0, e->ev_last1));
+  if (e->last_span_launches <= 0) return set_error(GGRS_E_STATE, "no timed span with a fused launch yet");
+  *ms = e->last_span_ms / (float)e->last_span_launches;
   return GGRS_OK;
 }
 
@@ -1774,25 +1157,30 @@ int ggrs_timing_reset(ggrs_engine_t* e) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
   HIP_TRY(hipSetDevice(e->cfg.device));
   HIP_TRY(hipStreamSynchronize(e->stream));
-  e->tev_used = 0;
   e->collecting = true;
+  e->span_open = false;
+  e->span_launches = 0;
   return GGRS_OK;
 }
 
 int ggrs_timing_read(ggrs_engine_t* e, float* total_ms, int32_t* launches) {
   if (!e || !total_ms || !launches) return set_error(GGRS_E_INVALID, "null argument");
   HIP_TRY(hipSetDevice(e->cfg.device));
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  float sum = 0.0f;
-  for (size_t i = 0; i + 1 < e->tev_used; i += 2) {
-    float ms = 0.0f;
-    HIP_TRY(hipEventElapsedTime(&ms, e->tev[i], e->tev[i + 1]));
-    sum += ms;
+  float ms = 0.0f;
+  if (e->span_open) {
+    HIP_TRY(hipEventRecord(e->ev_end, e->stream));
+    HIP_TRY(hipEventSynchronize(e->ev_end));
+    HIP_TRY(hipEventElapsedTime(&ms, e->ev_begin, e->ev_end));
+  } else {
+    HIP_TRY(hipStreamSynchronize(e->stream));
   }
-  *total_ms = sum;
-  *launches = (int32_t)(e->tev_used / 2);
+  *total_ms = ms;
+  *launches = e->span_launches;
+  e->last_span_ms = ms;
+  e->last_span_launches = e->span_launches;
   e->collecting = false;
-  e->tev_used = 0;
+  e->span_open = false;
+  e->span_launches = 0;
   return GGRS_OK;
 }
 

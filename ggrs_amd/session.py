@@ -110,6 +110,38 @@ class Engine:
         s = None if status is None else np.ascontiguousarray(status, np.uint8)
         _lib.check(self._L.ggrs_handle_requests(self._h, arr, len(reqs), _vp(i), _vp(s)))
 
+    def handle_requests_lanes(self, reqs, offsets, inputs=None, status=None, check=True):
+        """Per-lane request lists (ggrs_handle_requests_lanes): reqs [n][2] (kind, frame) of every
+        lane back to back, offsets [num_lanes + 1], inputs / status [n_advance][num_players] in the
+        same order.  Returns (checksum of every Save in order, lane_result [num_lanes]: >= 0 the
+        lane's frame after its list, -(1 + k) its failing request).  With check, a failed lane
+        raises LanesFailed (the other lanes ran)."""
+        r = np.ascontiguousarray(reqs, np.int32).reshape(-1, 2)
+        off = np.ascontiguousarray(offsets, np.int32)
+        if off.shape != (self.num_lanes + 1,):
+            raise InvalidRequest(-1, f"offsets must have {self.num_lanes + 1} entries")
+        i = None if inputs is None else np.ascontiguousarray(inputs, np.uint8)
+        st = None if status is None else np.ascontiguousarray(status, np.uint8)
+        n_save = int((r[:, 0] == REQ_SAVE).sum())
+        cks = np.zeros(max(n_save, 1), np.uint16)
+        res = np.zeros(self.num_lanes, np.int32)
+        rc = self._L.ggrs_handle_requests_lanes(self._h, _vp(r), _vp(off), _vp(i), _vp(st), _vp(cks), _vp(res))
+        if rc == _lib.GGRS_E_PRECONDITION:
+            if check:
+                raise LanesFailed(self._L.ggrs_last_error().decode(errors="replace"), res)
+        else:
+            _lib.check(rc)
+        return cks[:n_save], res
+
+    def lane_batch(self, token_words, load_slots, adv_rows, save_rows):
+        """The engine's mapped per-lane batch (ggrs_lane_batch_map) as numpy views."""
+        return LaneBatch(self, token_words, load_slots, adv_rows, save_rows)
+
+    def lane_frames(self):
+        out = np.zeros(self.num_lanes, np.int32)
+        _lib.check(self._L.ggrs_read_lane_frames(self._h, _vp(out)))
+        return out
+
     def synchronize(self):
         _lib.check(self._L.ggrs_synchronize(self._h))
 
@@ -163,6 +195,85 @@ class Engine:
         v = ctypes.c_float()
         _lib.check(self._L.ggrs_last_launch_ms(self._h, ctypes.byref(v)))
         return v.value
+
+
+class LanesFailed(PreconditionError):
+    """Some lanes' request lists failed validation (a reference session would have panicked):
+    `lane_result[l] = -(1 + k)` names lane l's failing request; the other lanes ran."""
+
+    def __init__(self, msg, lane_result):
+        super().__init__(_lib.GGRS_E_PRECONDITION, msg)
+        self.lane_result = lane_result
+        self.lanes = np.nonzero(lane_result < 0)[0]
+
+
+class LaneBatch:
+    """Numpy views of an engine's mapped lane batch (ggrs_lane_batch_t; pinned host memory the
+    kernel reads and writes in place).  Fill tokens / load_frames / inputs (/ status), then run()."""
+
+    def __init__(self, engine, token_words, load_slots, adv_rows, save_rows):
+        self.engine = engine
+        b = _lib.LaneBatch()
+        _lib.check(engine._L.ggrs_lane_batch_map(engine._h, token_words, load_slots, adv_rows, save_rows,
+                                                 ctypes.byref(b)))
+        self._b = b
+        L, P = engine.num_lanes, engine.num_players
+        W, LD, A, S = b.token_words, b.load_slots, b.adv_rows, b.save_rows
+        view = np.ctypeslib.as_array
+        self.tokens = view(b.tokens, shape=(W, L))
+        self.load_frames = view(b.load_frames, shape=(LD, L))
+        self.inputs = view(b.inputs, shape=(A, L, P))
+        self.status = view(b.status, shape=(A, L, P))
+        self.checksums = view(b.checksums, shape=(S, L))
+        self.lane_result = view(b.lane_result, shape=(L,))
+        self.shape = (W, LD, A, S)
+
+    def run(self, token_words=None, load_slots=None, adv_rows=None, save_rows=None, status=False):
+        """ggrs_lane_batch_run with the given counts (default: the mapped shape); returns the number
+        of lanes that failed validation (their lane_result < 0)."""
+        W, LD, A, S = self.shape
+        b = _lib.LaneBatch(W if token_words is None else token_words, LD if load_slots is None else load_slots,
+                           A if adv_rows is None else adv_rows, S if save_rows is None else save_rows,
+                           self._b.tokens, self._b.load_frames, self._b.inputs, self._b.status,
+                           self._b.checksums, self._b.lane_result)
+        n = ctypes.c_int32()
+        rc = self.engine._L.ggrs_lane_batch_run(self.engine._h, ctypes.byref(b), _lib.BATCH_STATUS if status else 0,
+                                                ctypes.byref(n))
+        if rc != _lib.GGRS_E_PRECONDITION:
+            _lib.check(rc)
+        return n.value
+
+
+def encode_lane_lists(lists, num_players):
+    """Per-lane request lists -> the batch encoding (tests and tools): lists[l] is lane l's
+    requests as (kind, frame, inputs[P] or None, status[P] or None).  Returns dict of tokens
+    [W][L], load_frames [LD][L], inputs / status [A][L][P] and the shape (W, LD, A, S)."""
+    L = len(lists)
+    n_tok = max((len(x) for x in lists), default=0)
+    W = max(1, -(-n_tok // _lib.TOKENS_PER_WORD))
+    LD = max(1, max(sum(1 for r in x if r[0] == REQ_LOAD) for x in lists))
+    A = max(1, max(sum(1 for r in x if r[0] == REQ_ADVANCE) for x in lists))
+    S = max(1, max(sum(1 for r in x if r[0] == REQ_SAVE) for x in lists))
+    tok = np.full((W * _lib.TOKENS_PER_WORD, L), _lib.TOK_END, np.uint64)
+    loads = np.full((LD, L), NULL_FRAME, np.int32)
+    inp = np.zeros((A, L, num_players), np.uint8)
+    st = np.zeros((A, L, num_players), np.uint8)
+    kind_tok = {REQ_SAVE: _lib.TOK_SAVE, REQ_ADVANCE: _lib.TOK_ADVANCE, REQ_LOAD: _lib.TOK_LOAD}
+    for l, reqs in enumerate(lists):
+        nl = na = 0
+        for k, (kind, frame, i, s) in enumerate(reqs):
+            tok[k, l] = kind_tok[kind]
+            if kind == REQ_LOAD:
+                loads[nl, l] = frame
+                nl += 1
+            elif kind == REQ_ADVANCE:
+                inp[na, l] = i
+                if s is not None:
+                    st[na, l] = s
+                na += 1
+    shifts = (2 * np.arange(_lib.TOKENS_PER_WORD, dtype=np.uint64))[None, :, None]
+    words = (tok.reshape(W, _lib.TOKENS_PER_WORD, L) << shifts).sum(axis=1).astype(np.uint32)
+    return dict(tokens=words, load_frames=loads, inputs=inp, status=st, shape=(W, LD, A, S))
 
 
 class SessionBuilder:
@@ -334,6 +445,47 @@ class BoxGameHandler:
         return {f: self.engine.save_checksums(f) for f in saves}
 
 
-__all__ = ["Engine", "SessionBuilder", "SyncTestSession", "BoxGameHandler", "SaveGameState",
+class LaneBoxGameHandler:
+    """The ex_game request handler (ex_game.rs:79-127) for lanes that are independent GGRS
+    sessions: handle_requests(lists) executes lists[l] -- lane l's own Vec<GgrsRequest> from its
+    own advance_frame() -- for every lane in one launch (ggrs_handle_requests_lanes) and returns,
+    per lane, the checksum of each SaveGameState in order (what the handler passes to
+    GameStateCell::save)."""
+
+    def __init__(self, engine):
+        self.engine = engine
+
+    def handle_requests(self, lists):
+        P = self.engine.num_players
+        reqs, offsets, inputs, status = [], [0], [], []
+        any_status = any(isinstance(r, AdvanceFrame) and r.status is not None for x in lists for r in x)
+        for x in lists:
+            for r in x:
+                if isinstance(r, SaveGameState):
+                    reqs.append((REQ_SAVE, r.frame))
+                elif isinstance(r, LoadGameState):
+                    reqs.append((REQ_LOAD, r.frame))
+                elif isinstance(r, AdvanceFrame):
+                    reqs.append((REQ_ADVANCE, 0))
+                    inputs.append(np.asarray(r.inputs, np.uint8).reshape(P))
+                    if any_status:
+                        st = r.status if r.status is not None else np.zeros(P, np.uint8)
+                        status.append(np.asarray(st, np.uint8).reshape(P))
+                else:
+                    raise InvalidRequest(-1, f"unknown request {r!r}")
+            offsets.append(len(reqs))
+        cks, _ = self.engine.handle_requests_lanes(
+            np.array(reqs, np.int32).reshape(-1, 2), np.array(offsets, np.int32),
+            np.stack(inputs) if inputs else None, np.stack(status) if status else None)
+        out, k = [], 0
+        for x in lists:
+            n = sum(1 for r in x if isinstance(r, SaveGameState))
+            out.append(cks[k:k + n])
+            k += n
+        return out
+
+
+__all__ = ["Engine", "SessionBuilder", "SyncTestSession", "BoxGameHandler", "LaneBoxGameHandler", "LaneBatch",
+           "LanesFailed", "encode_lane_lists", "SaveGameState",
            "LoadGameState", "AdvanceFrame", "GgrsError", "InvalidRequest", "PreconditionError",
            "MismatchedChecksum", "NULL_FRAME"]

@@ -65,15 +65,9 @@ extern "C" {
 #define GGRS_STATUS_DISCONNECTED 2
 
 /* SyncTest execution paths (ggrs_set_synctest_path) */
-#define GGRS_PATH_PIPELINED 0       /* default: cd+1 concurrent rollback chains per session, one
-                                       lane per (chain, player) when (cd+1) * players <= 64 */
-#define GGRS_PATH_SEQUENTIAL 1      /* one lane per session, calls in order */
-#define GGRS_PATH_PIPELINED_WHOLE 2 /* pipelined, one lane per chain (all players in one lane) */
-#define GGRS_PATH_PIPELINED_SPLIT 3 /* pipelined, players split over lanes (the round-1 v2 kernel;
-                                       the default path runs its v4 successor when buffers < 1 GiB) */
-#define GGRS_PATH_PIPELINED_V3 4    /* pipelined v3 (rotating chain roles), kept for comparison */
-#define GGRS_PATH_PIPELINED_V4_DPP 5 /* pipelined v4 with the chain rotation by DPP wave shifts
-                                        (the default v4 path rotates through ds_bpermute) */
+#define GGRS_PATH_PIPELINED 0  /* default: cd+1 concurrent rollback chains per session, one lane per
+                                  (chain, player) when (cd+1) * padded players <= 64 */
+#define GGRS_PATH_SEQUENTIAL 1 /* one lane per session, calls in order */
 
 /* per-lane status */
 #define GGRS_LANE_RUNNING 0
@@ -118,7 +112,8 @@ int ggrs_add_local_inputs_device(ggrs_engine_t* eng, int32_t first_frame, int32_
  * f <= check_distance take one extra launch). */
 int ggrs_synctest_advance_frames(ggrs_engine_t* eng, int32_t n_frames);
 /* Choose the SyncTest kernel: GGRS_PATH_PIPELINED (default; a mismatch found there is re-run on
- * the sequential kernel from a checkpoint, so results are identical) or GGRS_PATH_SEQUENTIAL. */
+ * the sequential kernel from a checkpoint, so results are identical; sessions whose chains do not
+ * fit one wavefront run sequentially) or GGRS_PATH_SEQUENTIAL. */
 int ggrs_set_synctest_path(ggrs_engine_t* eng, int32_t path);
 
 /* Execute an ordered request list on every lane (fused: one kernel launch).
@@ -127,6 +122,74 @@ int ggrs_set_synctest_path(ggrs_engine_t* eng, int32_t path);
  * device; read them with ggrs_read_save_checksums. */
 int ggrs_handle_requests(ggrs_engine_t* eng, const ggrs_request_t* reqs, int32_t n_reqs,
                          const uint8_t* inputs, const uint8_t* status);
+
+/* ---- Per-lane request lists: every lane is its own GGRS session.  A P2PSession rolls back to its
+ * own first_incorrect frame and replays its own count of frames (p2p_session.rs:322-337,658-714),
+ * so lanes' lists differ in kind, length and frames.  Two forms of one program:
+ *   ggrs_handle_requests_lanes  the requests themselves, CSR over lanes: lane l's ordered
+ *                               Vec<GgrsRequest> (src/lib.rs:171-195) is reqs[offsets[l] ..
+ *                               offsets[l+1]); one checksum out per SaveGameState, in request order.
+ *   ggrs_lane_batch_run         the same lists pre-encoded per lane (2-bit request kinds + the Load
+ *                               frames: SURVEY.md 8b's rollback(load_frame, n, save_mask)) in
+ *                               engine-owned pinned host memory the kernel reads directly, results
+ *                               written straight back there: one launch, no copies.
+ * Each lane's list is validated on the device before the lane's state is touched: a Load of a frame
+ * its cell does not hold (SyncLayer::load_frame's assert, sync_layer.rs:248; ex_game.rs:112's
+ * expect) or more requests of a kind than the batch holds fails the lane, which is left as it was
+ * (the reference panics); every other lane runs.  ggrs_handle_requests_lanes also checks every
+ * Save's frame against the lane's state frame (ex_game.rs:104).  Once an engine runs per-lane lists,
+ * each lane keeps its own frame (ggrs_read_lane_frames, ggrs_read_ring); the lane-uniform calls
+ * (ggrs_synctest_advance_frames, ggrs_handle_requests, ggrs_current_frame,
+ * ggrs_read_save_checksums) return GGRS_E_STATE. */
+#define GGRS_TOK_SAVE 0
+#define GGRS_TOK_ADVANCE 1
+#define GGRS_TOK_LOAD 2
+#define GGRS_TOK_END 3
+#define GGRS_TOKENS_PER_WORD 16
+
+#define GGRS_BATCH_STATUS 1 /* ggrs_lane_batch_run reads the status rows (else every input Confirmed) */
+
+/* shape limits of a lane batch */
+#define GGRS_BATCH_MAX_WORDS 32 /* 512 requests per lane */
+#define GGRS_BATCH_MAX_LOADS 8
+#define GGRS_BATCH_MAX_ADV 128
+#define GGRS_BATCH_MAX_SAVES 256
+
+typedef struct ggrs_lane_batch {
+  int32_t token_words;  /* W: words of request kinds per lane (16 per word) */
+  int32_t load_slots;   /* LD: Load frames per lane (GGRS 0.10.2 emits at most 2 per list) */
+  int32_t adv_rows;     /* A: AdvanceFrame rows per lane */
+  int32_t save_rows;    /* S: SaveGameState checksums per lane */
+  uint32_t* tokens;     /* [W][L]: lane l's request kinds in order, GGRS_TOK_* in 2 bits each,
+                           least significant first, GGRS_TOK_END after the last (or W*16 long) */
+  int32_t* load_frames; /* [LD][L]: frame of the lane's k-th LoadGameState */
+  uint8_t* inputs;      /* [A][L][num_players]: Input.inp of the lane's a-th AdvanceFrame */
+  uint8_t* status;      /* [A][L][num_players]: its InputStatus (GGRS_STATUS_*) */
+  uint16_t* checksums;  /* out [S][L]: fletcher16 of the lane's k-th SaveGameState (the checksum a
+                           handler passes to GameStateCell::save, sync_layer.rs:18-24) */
+  int32_t* lane_result; /* out [L]: >= 0 the lane's frame after its list; < 0 -(1 + k) where k is
+                           the index of the lane's first request that failed validation */
+} ggrs_lane_batch_t;
+
+/* Lay out (allocating or growing engine-owned pinned host memory) a batch of at least this shape
+ * and return pointers into it; the pointers stay valid until the next _map with a larger shape or
+ * ggrs_engine_destroy.  The caller fills tokens / load_frames / inputs (/ status) per call. */
+int ggrs_lane_batch_map(ggrs_engine_t* eng, int32_t token_words, int32_t load_slots, int32_t adv_rows,
+                        int32_t save_rows, ggrs_lane_batch_t* out);
+/* Run every lane's list of a mapped batch (the counts in *batch may be lowered per call: rows past
+ * them are not read).  flags: GGRS_BATCH_STATUS.  Returns when checksums and lane_result are in
+ * host memory; GGRS_E_PRECONDITION when *n_failed lanes failed validation (the rest ran). */
+int ggrs_lane_batch_run(ggrs_engine_t* eng, const ggrs_lane_batch_t* batch, int32_t flags, int32_t* n_failed);
+/* The generic form.  reqs: every lane's requests back to back, offsets: [num_lanes + 1]
+ * (offsets[0] = 0).  inputs / status: [n_advance][num_players], one row per AdvanceFrame in the
+ * same (lane, request) order; status NULL = all Confirmed.  save_checksums (may be NULL): one per
+ * SaveGameState in the same order.  lane_result (may be NULL): [num_lanes] as in the batch.
+ * GGRS_E_PRECONDITION when some lane's list failed validation (those lanes did not run). */
+int ggrs_handle_requests_lanes(ggrs_engine_t* eng, const ggrs_request_t* reqs, const int32_t* offsets,
+                               const uint8_t* inputs, const uint8_t* status, uint16_t* save_checksums,
+                               int32_t* lane_result);
+/* Every lane's current frame (its state's frame field): [num_lanes]. */
+int ggrs_read_lane_frames(ggrs_engine_t* eng, int32_t* frames);
 
 /* Block until all work queued on the engine's stream has finished. */
 int ggrs_synchronize(ggrs_engine_t* eng);
@@ -152,10 +215,11 @@ int ggrs_read_trace(ggrs_engine_t* eng, int32_t first_frame, int32_t n_frames, u
  * bit of player 0's x on `lane` -- a non-deterministic simulation the SyncTest must catch. */
 int ggrs_debug_corrupt_on_load(ggrs_engine_t* eng, int32_t lane, int32_t frame);
 
-/* Timing of the last fused launch on the engine's stream, from HIP events around it (ms). */
+/* Average device time per fused launch of the last timed span (ggrs_timing_reset .. _read), ms. */
 int ggrs_last_launch_ms(ggrs_engine_t* eng, float* ms);
-/* Collect HIP-event device times of every fused launch from now on; _read synchronises, returns
- * the summed milliseconds and the launch count, and stops collecting. */
+/* Time the fused launches from now on: one HIP event pair on the engine's stream brackets the
+ * whole span (no per-launch events); _read synchronises, returns the span's milliseconds (launch
+ * gaps included) and the number of fused launches in it, and stops collecting. */
 int ggrs_timing_reset(ggrs_engine_t* eng);
 int ggrs_timing_read(ggrs_engine_t* eng, float* total_ms, int32_t* launches);
 

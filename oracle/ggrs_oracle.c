@@ -1184,6 +1184,141 @@ int oracle_p2p_run(const OracleP2PCfg* cfg, int32_t frames, const uint8_t* input
   return res->status;
 }
 
+/* ---------------------------------------------------------------- per-lane request streams
+ * The request lists a P2P session emits when its remote inputs arrive in bursts (a jittery
+ * network): at call f every remote frame up to arrive_upto[f] not yet received arrives
+ * (poll_remote_clients delivering several Event::Input at once, p2p_session.rs:430-478 ->
+ * :880-895), so a call's first_incorrect can be any frame of the burst and sessions roll back to
+ * differing frames with differing counts (adjust_gamestate :658-714).  arrive_upto must satisfy
+ * f - max_prediction < arrive_upto[f] < f (the session can always advance); a value at or below
+ * what already arrived delivers nothing.
+ * Captured per request k: kind, frame (Save/Load), for AdvanceFrame the inputs and InputStatus
+ * of every player (synchronized_inputs, sync_layer.rs:280-293); call_off[f] = index of call f's
+ * first request (call_off[frames] = total).  Returns 0, -1 bad arguments, -3 capacity. */
+int oracle_p2p_stream(const OracleP2PCfg* cfg, int32_t frames, const uint8_t* inputs, const int32_t* arrive_upto,
+                      int64_t req_cap, int64_t* call_off, int32_t* req_kind, int32_t* req_frame,
+                      uint8_t* req_inputs, uint8_t* req_status, OracleP2PResult* res) {
+  memset(res, 0, sizeof *res);
+  const size_t P = (size_t)cfg->num_players;
+  if (P < 1 || P > MAX_PLAYERS || cfg->max_prediction < 1 || cfg->input_delay < 0 ||
+      (cfg->local_mask & ~((1 << P) - 1)) != 0 || cfg->local_mask == (1 << P) - 1) {
+    res->status = -1;
+    return -1;
+  }
+  P2PSession s; memset(&s, 0, sizeof s);
+  s.num_players = P; s.max_prediction = (size_t)cfg->max_prediction;
+  s.local_mask = (uint32_t)cfg->local_mask;
+  sl_new(&s.sl, P, s.max_prediction, cfg->predictor);
+  for (size_t i = 0; i < P; i++) {
+    s.last_frame[i] = NULL_FRAME;
+    if ((s.local_mask >> i) & 1u) s.sl.queues[i].frame_delay = (size_t)cfg->input_delay;
+  }
+  s.disconnect_frame = NULL_FRAME;
+  s.sparse_saving = cfg->sparse_saving;
+  /* the user's handler fulfils every list (a cell's frame is set by the Save it fulfils, which
+   * SyncLayer::load_frame's assert reads back) */
+  Game game; memset(&game, 0, sizeof game);
+  game.desync_frame = -1;
+  state_new(&game.game_state, (uint64_t)P);
+  game.last_checksum_frame = NULL_FRAME;
+  RequestVec rv = {0};
+  int64_t rt = 0;
+  int32_t delivered = NULL_FRAME;
+  int rc = 0;
+  for (int32_t f = 0; f < frames; f++) {
+    const int32_t upto = arrive_upto[f];
+    if (upto >= f || upto <= f - cfg->max_prediction) { rc = -1; break; }
+    for (int32_t g = delivered + 1; g <= upto; g++)   /* poll_remote_clients: the burst */
+      for (size_t i = 0; i < P; i++)
+        if (!((s.local_mask >> i) & 1u)) p2p_on_remote_input(&s, i, g, inputs[(size_t)g * P + i]);
+    if (upto > delivered) delivered = upto;
+    for (size_t i = 0; i < P; i++)
+      if ((s.local_mask >> i) & 1u) {
+        s.local[i].frame = s.sl.current_frame; s.local[i].input = inputs[(size_t)f * P + i]; s.has_local[i] = 1;
+      }
+    int advanced = 0;
+    if (p2p_advance_frame(&s, &rv, &advanced) < 0 || !advanced) { rc = -1; break; }
+    call_off[f] = rt;
+    if (rt + (int64_t)rv.n > req_cap) { rc = -3; break; }
+    for (size_t k = 0; k < rv.n; k++, rt++) {
+      req_kind[rt] = rv.v[k].kind;
+      req_frame[rt] = rv.v[k].kind == REQ_ADVANCE ? 0 : rv.v[k].frame;
+      for (size_t i = 0; i < P; i++) {
+        req_inputs[rt * (int64_t)P + (int64_t)i] = rv.v[k].inputs[i];
+        req_status[rt * (int64_t)P + (int64_t)i] = rv.v[k].status[i];
+      }
+      if (rv.v[k].kind == REQ_LOAD) res->n_load++;
+      else if (rv.v[k].kind == REQ_SAVE) res->n_save++;
+      else res->n_advance++;
+    }
+    game_handle_requests(&game, &s.sl, &rv, 0);
+    res->frames_done = f + 1;
+  }
+  call_off[res->frames_done] = rt;
+  res->rollbacks = s.rollbacks;
+  res->resim = s.resim;
+  res->status = rc;
+  free(rv.v);
+  state_free(&game.game_state);
+  sl_free(&s.sl);
+  return rc;
+}
+
+/* The ex_game request handler alone (Game::handle_requests, ex_game.rs:79-127, over its own
+ * SavedStates ring of max_prediction + 1 cells, sync_layer.rs:144-166): executes n requests
+ * (kind, frame, per-advance inputs[P] and status[P]) in order from State::new and records every
+ * Save's checksum (save_cks, one per Save in order) and, at the end, the state and the ring.  Returns 0, or -(1 + k) when request k would panic: a Save whose
+ * frame is not the state's (:104) or a Load of a cell that does not hold the frame (:112,
+ * sync_layer.rs:248) -- the handler stops there. */
+int oracle_handler_run(int32_t num_players, int32_t max_prediction, int64_t n, const int32_t* kind,
+                       const int32_t* frame, const uint8_t* inputs, const uint8_t* status, uint16_t* save_cks,
+                       uint8_t* final_state, int32_t* ring_frames, uint16_t* ring_cksums, uint8_t* ring_states) {
+  const size_t P = (size_t)num_players;
+  if (P < 1 || P > MAX_PLAYERS || max_prediction < 1) return -1000000;
+  SyncLayer sl;
+  sl_new(&sl, P, (size_t)max_prediction, 0);
+  Game g; memset(&g, 0, sizeof g);
+  g.desync_frame = -1;
+  state_new(&g.game_state, (uint64_t)P);
+  g.last_checksum_frame = NULL_FRAME;
+  int rc = 0;
+  int64_t ns = 0;
+  for (int64_t k = 0; k < n; k++) {
+    Request r; memset(&r, 0, sizeof r);
+    r.kind = kind[k];
+    r.frame = frame[k];
+    if (r.kind == REQ_SAVE) {
+      if (r.frame < 0 || g.game_state.frame != r.frame) { rc = (int)(-(1 + k)); break; }
+      r.cell = sl_cell_index(&sl, r.frame);
+    } else if (r.kind == REQ_LOAD) {
+      if (r.frame < 0) { rc = (int)(-(1 + k)); break; }
+      r.cell = sl_cell_index(&sl, r.frame);
+      if (sl.cells[r.cell].frame != r.frame || !sl.cells[r.cell].has_data) { rc = (int)(-(1 + k)); break; }
+    } else {
+      for (size_t i = 0; i < P; i++) {
+        r.inputs[i] = inputs[k * (int64_t)P + (int64_t)i];
+        r.status[i] = status ? status[k * (int64_t)P + (int64_t)i] : STATUS_CONFIRMED;
+      }
+    }
+    RequestVec one = {&r, 1, 1};
+    game_handle_requests(&g, &sl, &one, 0);
+    if (r.kind == REQ_SAVE && save_cks) save_cks[ns++] = sl.cells[r.cell].checksum;
+  }
+  if (final_state) oracle_state_serialize(&g.game_state, final_state);
+  for (size_t i = 0; i < sl.num_cells; i++) {
+    const Cell* c = &sl.cells[i];
+    if (ring_frames) ring_frames[i] = c->frame;
+    if (ring_cksums) ring_cksums[i] = c->has_checksum ? c->checksum : 0;
+    if (ring_states) {
+      uint8_t* dst = ring_states + i * (36 + 20 * P);
+      if (c->has_data) oracle_state_serialize(&c->data, dst); else memset(dst, 0, 36 + 20 * P);
+    }
+  }
+  state_free(&g.game_state);
+  sl_free(&sl);
+  return rc;
+}
+
 /* ---------------------------------------------------------------- two peers with desync detection
  * Both machines of one match, stepped call by call: peer k's local players are local_mask[k], every
  * other player is remote; inputs[g][P] are all players' inputs of frame g (input delay 0 on both,

@@ -117,6 +117,13 @@ def lib():
         L.oracle_p2p_run.argtypes = [P(P2PCfg), ctypes.c_int32, u8p, u16p, i32p, u8p, ctypes.c_int64,
                                      i32p, u8p, i32p, u16p, u8p, P(P2PResult)]
         L.oracle_p2p_run.restype = ctypes.c_int
+        i64p = P(ctypes.c_int64)
+        L.oracle_p2p_stream.argtypes = [P(P2PCfg), ctypes.c_int32, u8p, i32p, ctypes.c_int64, i64p, i32p, i32p,
+                                        u8p, u8p, P(P2PResult)]
+        L.oracle_p2p_stream.restype = ctypes.c_int
+        L.oracle_handler_run.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, i32p, i32p, u8p, u8p,
+                                         u16p, u8p, i32p, u16p, u8p]
+        L.oracle_handler_run.restype = ctypes.c_int
         L.oracle_p2p_desync_pair_run.argtypes = [
             ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, i32p, ctypes.c_int32, ctypes.c_int32,
             ctypes.c_int32, u8p, ctypes.c_int32, ctypes.c_int32, i32p, u16p, ctypes.c_int32, i32p, i32p,
@@ -253,6 +260,64 @@ def p2p_run(inputs, num_players=2, local_mask=0b01, input_delay=0, max_predictio
         _ptr(out["ring_states"], ctypes.c_uint8), ctypes.byref(res))
     out["rc"] = rc
     out["result"] = res
+    return out
+
+
+def jitter_schedule(frames, max_prediction, seed, max_lag=None):
+    """arrive_upto[f] for oracle_p2p_stream: the newest remote frame delivered by call f, from a
+    random per-call lag in [1, max_lag] (default max_prediction - 1), kept non-decreasing, so
+    inputs arrive in bursts of differing size."""
+    rng = np.random.default_rng(seed)
+    max_lag = max_lag or max_prediction - 1
+    lag = rng.integers(1, max_lag + 1, frames)
+    upto = np.maximum.accumulate(np.arange(frames) - lag)
+    return upto.astype(np.int32)
+
+
+def p2p_stream(inputs, arrive_upto, num_players=2, local_mask=0b01, input_delay=0, max_prediction=8,
+               predictor=0, sparse_saving=False):
+    """The request lists one P2P session emits per call under a jittery network
+    (oracle_p2p_stream): dict with call_off [calls + 1] and per request kind, frame, inputs [P],
+    status [P]."""
+    inputs = np.ascontiguousarray(inputs, np.uint8).reshape(-1, num_players)
+    frames = inputs.shape[0]
+    upto = np.ascontiguousarray(arrive_upto, np.int32)
+    cap = frames * (4 * max_prediction + 8)
+    cfg = P2PCfg(num_players, max_prediction, input_delay, 1, local_mask, predictor, int(sparse_saving))
+    res = P2PResult()
+    off = np.zeros(frames + 1, np.int64)
+    kind, frame = np.zeros(cap, np.int32), np.zeros(cap, np.int32)
+    inp, st = np.zeros((cap, num_players), np.uint8), np.zeros((cap, num_players), np.uint8)
+    rc = lib().oracle_p2p_stream(ctypes.byref(cfg), frames, _ptr(inputs, ctypes.c_uint8), _ptr(upto, ctypes.c_int32),
+                                 cap, _ptr(off, ctypes.c_int64), _ptr(kind, ctypes.c_int32),
+                                 _ptr(frame, ctypes.c_int32), _ptr(inp, ctypes.c_uint8), _ptr(st, ctypes.c_uint8),
+                                 ctypes.byref(res))
+    n = int(off[res.frames_done])
+    return dict(rc=rc, result=res, calls=res.frames_done, call_off=off[:res.frames_done + 1], kind=kind[:n],
+                frame=frame[:n], inputs=inp[:n], status=st[:n])
+
+
+def handler_run(kind, frame, inputs, status=None, num_players=2, max_prediction=8):
+    """Game::handle_requests over one lane's request stream (oracle_handler_run): dict with rc
+    (0, or -(1 + k) at the request that would panic), the checksum of every Save in order, the
+    final state and the ring."""
+    kind = np.ascontiguousarray(kind, np.int32)
+    frame = np.ascontiguousarray(frame, np.int32)
+    n = kind.shape[0]
+    inputs = np.ascontiguousarray(inputs, np.uint8).reshape(n, num_players)
+    status = None if status is None else np.ascontiguousarray(status, np.uint8).reshape(n, num_players)
+    R, sb = max_prediction + 1, state_bytes(num_players)
+    out = dict(save_cks=np.zeros(max(1, int((kind == 0).sum())), np.uint16), final_state=np.zeros(sb, np.uint8),
+               ring_frames=np.zeros(R, np.int32), ring_cksums=np.zeros(R, np.uint16),
+               ring_states=np.zeros((R, sb), np.uint8))
+    out["rc"] = lib().oracle_handler_run(num_players, max_prediction, n, _ptr(kind, ctypes.c_int32),
+                                         _ptr(frame, ctypes.c_int32), _ptr(inputs, ctypes.c_uint8),
+                                         _ptr(status, ctypes.c_uint8), _ptr(out["save_cks"], ctypes.c_uint16),
+                                         _ptr(out["final_state"], ctypes.c_uint8),
+                                         _ptr(out["ring_frames"], ctypes.c_int32),
+                                         _ptr(out["ring_cksums"], ctypes.c_uint16),
+                                         _ptr(out["ring_states"], ctypes.c_uint8))
+    out["save_cks"] = out["save_cks"][:int((kind == 0).sum())]
     return out
 
 
