@@ -35,12 +35,13 @@ EXPORTS = (
     "ggrs_read_ring", "ggrs_read_trace", "ggrs_debug_corrupt_on_load", "ggrs_last_launch_ms",
     "ggrs_timing_reset", "ggrs_timing_read", "ggrs_set_synctest_path",
     "ggrs_lane_batch_map", "ggrs_lane_batch_run", "ggrs_handle_requests_lanes", "ggrs_read_lane_frames",
+    "ggrs_lane_server",
     "ggrs_branch_engine_create", "ggrs_branch_engine_destroy", "ggrs_branch_engine_config",
     "ggrs_branch_add_inputs", "ggrs_branch_speculate", "ggrs_branch_confirm",
     "ggrs_branch_report_bytes", "ggrs_branch_synchronize", "ggrs_branch_trunk_frame",
     "ggrs_branch_read_report", "ggrs_branch_read_desync", "ggrs_branch_read_trunk",
     "ggrs_branch_read_lane", "ggrs_branch_timing_reset", "ggrs_branch_timing_read",
-    "ggrs_branch_rounds", "ggrs_branch_set_round_launches",
+    "ggrs_branch_rounds", "ggrs_branch_set_round_launches", "ggrs_branch_set_stream",
     "ggrs_particle_engine_create", "ggrs_particle_engine_destroy", "ggrs_particle_add_local_inputs",
     "ggrs_particle_synctest_advance_frames", "ggrs_particle_synchronize",
     "ggrs_particle_current_frame", "ggrs_particle_read_mismatches", "ggrs_particle_read_state",
@@ -144,6 +145,7 @@ def lib():
         L.ggrs_lane_batch_run.argtypes = [vp, P(LaneBatch), i32, P(i32)]
         L.ggrs_handle_requests_lanes.argtypes = [vp, vp, vp, vp, vp, vp, vp]
         L.ggrs_read_lane_frames.argtypes = [vp, vp]
+        L.ggrs_lane_server.argtypes = [vp, i32]
         for name in EXPORTS:
             if name not in ("ggrs_abi_version", "ggrs_last_error", "ggrs_codec_max_packet_bytes"):
                 getattr(L, name).restype = ctypes.c_int

@@ -54,6 +54,7 @@ def _bind(L):
     L.ggrs_branch_timing_read.argtypes = [vp, P(ctypes.c_float), P(ctypes.c_int32)]
     L.ggrs_branch_rounds.argtypes = [vp, ctypes.c_int32]
     L.ggrs_branch_set_round_launches.argtypes = [vp, ctypes.c_int32]
+    L.ggrs_branch_set_stream.argtypes = [vp, vp]
     for name in _lib.EXPORTS:
         if name.startswith("ggrs_branch_"):
             getattr(L, name).restype = ctypes.c_int
@@ -108,6 +109,25 @@ class BranchEngine:
     def confirm(self, report_device_ptr=None):
         ptr = ctypes.c_void_p(report_device_ptr) if report_device_ptr else None
         _lib.check(self._L.ggrs_branch_confirm(self._h, ptr))
+
+    def set_stream(self, stream_ptr):
+        """Enqueue all work on this hipStream_t (an int handle, e.g. torch.cuda.current_stream()
+        .cuda_stream; None or 0 = the engine's own stream)."""
+        _lib.check(self._L.ggrs_branch_set_stream(self._h, ctypes.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def confirm_to_tensor(self, t):
+        """confirm() with the round's report written into torch uint8 tensor `t`: a device tensor
+        receives it on the engine's stream (no host sync); a CPU tensor through a host read."""
+        if t.is_cuda:
+            self.confirm(t.data_ptr())
+            return
+        self.confirm()
+        ck, bits = self.report()
+        raw = np.zeros(self.report_bytes, np.uint8)
+        raw[:2 * self.num_sessions] = ck.view(np.uint8)
+        raw[self.report_ck_bytes:self.report_ck_bytes + 8 * self.report_words] = bits.view(np.uint8)
+        import torch
+        t.copy_(torch.from_numpy(raw))
 
     def rounds(self, n):
         """n rounds of speculate + confirm from native code (no report copy): one launch by

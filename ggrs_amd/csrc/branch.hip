@@ -275,7 +275,8 @@ struct ggrs_branch_engine {
   ggrs_branch_config_t cfg{};
   int Pp = 1, F = 1, R = 2, cap = 128, E = 0, first_remote = -1;
   int64_t L = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;      // where every launch and copy goes (own_stream or the caller's)
+  hipStream_t own_stream = nullptr;
   uint32_t* trunk = nullptr;
   uint32_t* ring = nullptr;
   uint16_t* ring_ck = nullptr;
@@ -283,20 +284,14 @@ struct ggrs_branch_engine {
   uint8_t* report = nullptr;  // report_bytes: [S] u16 | pad to 8 | [words] u64
   size_t report_bytes = 0;
   uint64_t* prev_bits = nullptr;
-  bool batching = false;             // ggrs_branch_rounds: launches without per-launch events
   bool per_round_launches = false;   // ggrs_branch_set_round_launches: rounds() as 2 n launches
-  int32_t batch_launches = 0;
-  std::vector<int32_t> tev_weight;   // launches each collected event pair brackets
   int32_t* desync = nullptr;
   uint8_t* staging = nullptr;
   size_t staging_bytes = 0;
   int32_t trunk_frame = 0;
   int32_t next_input_frame = 0;
   bool have_prev = false;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  std::vector<hipEvent_t> tev;
-  size_t tev_used = 0;
-  bool collecting = false;
+  SpanTimer timer;
 };
 
 namespace {
@@ -305,29 +300,11 @@ size_t report_ck_bytes(int64_t S) { return ((size_t)S * 2 + 7) & ~(size_t)7; }
 int64_t report_words(int64_t L) { return (L + 63) / 64; }
 
 template <typename K>
-int branch_launch_timed(ggrs_branch_engine* e, K&& launch) {
-  if (e->batching) {  // inside ggrs_branch_rounds: one event pair brackets the whole batch
-    launch();
-    HIP_TRY(hipGetLastError());
-    e->batch_launches += 1;
-    return GGRS_OK;
-  }
-  hipEvent_t a = e->ev0, b = e->ev1;
-  if (e->collecting) {
-    while (e->tev.size() < e->tev_used + 2) {
-      hipEvent_t ev;
-      HIP_TRY(hipEventCreate(&ev));
-      e->tev.push_back(ev);
-    }
-    a = e->tev[e->tev_used];
-    b = e->tev[e->tev_used + 1];
-    e->tev_used += 2;
-  }
-  HIP_TRY(hipEventRecord(a, e->stream));
+int branch_launch_timed(ggrs_branch_engine* e, K&& launch, int32_t counts_as = 1) {
+  if (int rc = e->timer.before(e->stream)) return rc;
   launch();
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(b, e->stream));
-  if (e->collecting) e->tev_weight.push_back(1);
+  e->timer.count(counts_as);
   return GGRS_OK;
 }
 
@@ -342,10 +319,8 @@ int ggrs_branch_engine_destroy(ggrs_branch_engine_t* e) {
   void* bufs[] = {e->trunk, e->ring, e->ring_ck, e->inputs, e->report, e->prev_bits, e->desync, e->staging};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
-  for (hipEvent_t ev : e->tev) (void)hipEventDestroy(ev);
-  if (e->ev0) (void)hipEventDestroy(e->ev0);
-  if (e->ev1) (void)hipEventDestroy(e->ev1);
-  if (e->stream) (void)hipStreamDestroy(e->stream);
+  e->timer.destroy();
+  if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
   delete e;
   return GGRS_OK;
 }
@@ -398,9 +373,9 @@ int ggrs_branch_engine_create(const ggrs_branch_config_t* cfg, ggrs_branch_engin
   } while (0)
   const int64_t S = c.num_sessions;
   CTRY(hipSetDevice(c.device));
-  CTRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
-  CTRY(hipEventCreate(&e->ev0));
-  CTRY(hipEventCreate(&e->ev1));
+  CTRY(hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking));
+  e->stream = e->own_stream;
+  if (e->timer.create()) return fail(GGRS_E_HIP);
   CTRY(hipMalloc(&e->trunk, sizeof(uint32_t) * e->F * S));
   CTRY(hipMalloc(&e->ring, sizeof(uint32_t) * (size_t)e->R * e->F * L));
   CTRY(hipMalloc(&e->ring_ck, sizeof(uint16_t) * (size_t)e->R * L));
@@ -603,31 +578,13 @@ int ggrs_branch_read_lane(ggrs_branch_engine_t* e, int64_t lane, int32_t frame, 
 int ggrs_branch_timing_reset(ggrs_branch_engine_t* e) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
   HIP_TRY(hipSetDevice(e->cfg.device));
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  e->tev_used = 0;
-  e->tev_weight.clear();
-  e->collecting = true;
-  return GGRS_OK;
+  return e->timer.reset(e->stream);
 }
 
 int ggrs_branch_timing_read(ggrs_branch_engine_t* e, float* total_ms, int32_t* launches) {
   if (!e || !total_ms || !launches) return set_error(GGRS_E_INVALID, "null argument");
   HIP_TRY(hipSetDevice(e->cfg.device));
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  float sum = 0.0f;
-  for (size_t i = 0; i + 1 < e->tev_used; i += 2) {
-    float ms = 0.0f;
-    HIP_TRY(hipEventElapsedTime(&ms, e->tev[i], e->tev[i + 1]));
-    sum += ms;
-  }
-  *total_ms = sum;
-  int32_t n = 0;
-  for (int32_t w : e->tev_weight) n += w;
-  *launches = n;
-  e->collecting = false;
-  e->tev_used = 0;
-  e->tev_weight.clear();
-  return GGRS_OK;
+  return e->timer.read(e->stream, total_ms, launches);
 }
 
 int ggrs_branch_rounds(ggrs_branch_engine_t* e, int32_t n_rounds) {
@@ -637,18 +594,6 @@ int ggrs_branch_rounds(ggrs_branch_engine_t* e, int32_t n_rounds) {
     return set_error(GGRS_E_INVALID, "inputs for %d rounds are not queued", n_rounds);
   if (n_rounds == 0) return GGRS_OK;
   HIP_TRY(hipSetDevice(e->cfg.device));
-  hipEvent_t a = nullptr, b = nullptr;
-  if (e->collecting) {
-    while (e->tev.size() < e->tev_used + 2) {
-      hipEvent_t ev;
-      HIP_TRY(hipEventCreate(&ev));
-      e->tev.push_back(ev);
-    }
-    a = e->tev[e->tev_used];
-    b = e->tev[e->tev_used + 1];
-    e->tev_used += 2;
-    HIP_TRY(hipEventRecord(a, e->stream));
-  }
   int rc = GGRS_OK;
   if (!e->per_round_launches) {
     // one launch for all n rounds (rounds_kernel); counted as the 2 n launches it replaces
@@ -678,31 +623,38 @@ int ggrs_branch_rounds(ggrs_branch_engine_t* e, int32_t n_rounds) {
     rp.trunk = e->trunk;
     rp.report_ck = (uint16_t*)e->report;
     rp.report_bits = (uint64_t*)(e->report + report_ck_bytes(p.S));
-    dispatch_players(p.P, [&](auto PC) {
-      constexpr int P = decltype(PC)::value;
-      rounds_kernel<P><<<grid_of(p.L, kRoundsBlock), kRoundsBlock, 0, e->stream>>>(rp);
-    });
-    HIP_TRY(hipGetLastError());
+    rc = branch_launch_timed(e, [&] {
+      dispatch_players(p.P, [&](auto PC) {
+        constexpr int P = decltype(PC)::value;
+        rounds_kernel<P><<<grid_of(p.L, kRoundsBlock), kRoundsBlock, 0, e->stream>>>(rp);
+      });
+    }, 2 * n_rounds);
+    if (rc) return rc;
     e->trunk_frame += n_rounds;
     e->have_prev = true;
-    if (e->collecting) {
-      HIP_TRY(hipEventRecord(b, e->stream));
-      e->tev_weight.push_back(2 * n_rounds);
-    }
     return GGRS_OK;
   }
-  e->batching = true;
-  e->batch_launches = 0;
   for (int32_t r = 0; r < n_rounds && rc == GGRS_OK; r++) {
     rc = ggrs_branch_speculate(e);
     if (rc == GGRS_OK) rc = ggrs_branch_confirm(e, nullptr);
   }
-  e->batching = false;
-  if (e->collecting) {
-    HIP_TRY(hipEventRecord(b, e->stream));
-    e->tev_weight.push_back(e->batch_launches);
-  }
   return rc;
+}
+
+int ggrs_branch_set_stream(ggrs_branch_engine_t* e, void* stream) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  hipStream_t s = stream ? (hipStream_t)stream : e->own_stream;
+  if (s == e->stream) return GGRS_OK;
+  // work already queued on the old stream comes first: the new stream waits for it on the device
+  hipEvent_t ev;
+  HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(ev, e->stream));
+  HIP_TRY(hipStreamWaitEvent(s, ev, 0));
+  HIP_TRY(hipEventDestroy(ev));
+  if (e->timer.collecting) return set_error(GGRS_E_STATE, "cannot switch streams while timing a span");
+  e->stream = s;
+  return GGRS_OK;
 }
 
 int ggrs_branch_set_round_launches(ggrs_branch_engine_t* e, int32_t on) {

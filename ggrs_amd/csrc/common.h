@@ -23,6 +23,58 @@ int set_error(int code, const char* fmt, ...);
 
 constexpr int kWave = 64;
 
+// Device time of a span of fused launches (ggrs_*_timing_reset .. _read): one HIP event pair on
+// the engine's stream brackets the whole span, so the timed path records no per-launch events
+// (a pair per launch cost ~7.8 us of a 0.26 ms SyncTest launch).
+struct SpanTimer {
+  hipEvent_t begin = nullptr, end = nullptr;
+  bool collecting = false, open = false;
+  int32_t launches = 0;
+  int create() {
+    HIP_TRY(hipEventCreate(&begin));
+    HIP_TRY(hipEventCreate(&end));
+    return GGRS_OK;
+  }
+  void destroy() {
+    if (begin) (void)hipEventDestroy(begin);
+    if (end) (void)hipEventDestroy(end);
+    begin = end = nullptr;
+  }
+  // before enqueueing a fused launch: the span's first one records the begin event
+  int before(hipStream_t s) {
+    if (collecting && !open) {
+      HIP_TRY(hipEventRecord(begin, s));
+      open = true;
+    }
+    return GGRS_OK;
+  }
+  void count(int32_t n = 1) {
+    if (collecting) launches += n;
+  }
+  int reset(hipStream_t s) {
+    HIP_TRY(hipStreamSynchronize(s));
+    collecting = true;
+    open = false;
+    launches = 0;
+    return GGRS_OK;
+  }
+  // span milliseconds (launch gaps included) and fused launches; stops collecting
+  int read(hipStream_t s, float* ms, int32_t* n) {
+    *ms = 0.0f;
+    if (open) {
+      HIP_TRY(hipEventRecord(end, s));
+      HIP_TRY(hipEventSynchronize(end));
+      HIP_TRY(hipEventElapsedTime(ms, begin, end));
+    } else {
+      HIP_TRY(hipStreamSynchronize(s));
+    }
+    *n = launches;
+    collecting = open = false;
+    launches = 0;
+    return GGRS_OK;
+  }
+};
+
 inline int padded_players(int p) { return p <= 1 ? 1 : (p == 2 ? 2 : 4); }
 inline int64_t grid_of(int64_t n, int64_t block) { return (n + block - 1) / block; }
 

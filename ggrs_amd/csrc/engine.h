@@ -21,6 +21,17 @@ struct LaneBatchHost {
          off_cks = 0, off_result = 0;
 };
 
+// the persistent lane server of requests.hip (ggrs_lane_server)
+struct LaneServerHost {
+  uint8_t* mem = nullptr;  // pinned, fine-grained, mapped: 64-bit control word | done word
+  void* dev = nullptr;     // device memory: relay word + finished-block counter
+  bool enabled = true, running = false;
+  int32_t epoch = 0;
+  int32_t blocks = 0;
+  double last_done = 0.0;  // steady-clock seconds of the last finished batch
+  int64_t idle_ticks = 0;  // the kernel's idle watchdog, in wall-clock ticks
+};
+
 struct ggrs_engine {
   ggrs_config_t cfg{};
   int Pp = 1, F = 1, R = 1, cap = 128;
@@ -62,11 +73,16 @@ struct ggrs_engine {
   int32_t last_span_launches = 0;
   // per-lane request lists
   LaneBatchHost batch;
+  LaneServerHost server;
   std::vector<int32_t> lane_frame;  // each lane's frame, as ggrs_handle_requests_lanes last left it
                                     // (empty: unknown, read from the device when needed)
 };
 
 namespace ggrs {
+
+// Ends the persistent lane server (requests.hip) if it runs: every other use of the engine's stream
+// or device buffers must come after it.
+int lane_server_stop(ggrs_engine* e);
 
 // Counts one fused launch of a timed span; the span's first launch records its begin event.
 template <typename K>

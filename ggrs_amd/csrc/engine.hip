@@ -617,6 +617,7 @@ const char* ggrs_last_error(void) { return g_last_error.c_str(); }
 int ggrs_engine_destroy(ggrs_engine_t* e) {
   if (!e) return GGRS_OK;
   (void)hipSetDevice(e->cfg.device);
+  (void)lane_server_stop(e);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   void* bufs[] = {e->arena, e->shadow, e->fail_f0, e->inputs, e->lane_status,
                   e->mis_frame, e->mis_mask, e->staging};  // trace lives in the arena allocation
@@ -624,6 +625,8 @@ int ggrs_engine_destroy(ggrs_engine_t* e) {
     if (b) (void)hipFree(b);
   if (e->host_staging) (void)hipHostFree(e->host_staging);
   if (e->batch.base) (void)hipHostFree(e->batch.base);
+  if (e->server.mem) (void)hipHostFree(e->server.mem);
+  if (e->server.dev) (void)hipFree(e->server.dev);
   if (e->ev_begin) (void)hipEventDestroy(e->ev_begin);
   if (e->ev_end) (void)hipEventDestroy(e->ev_end);
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -851,6 +854,7 @@ static int launch_pipelined(ggrs_engine_t* e, int32_t f0, int32_t n) {
 // checkpoint taken before it and replay the frames since with the sequential kernel, which halts
 // lanes exactly where the reference returns MismatchedChecksum.
 static int resolve(ggrs_engine_t* e) {
+  if (int rc = lane_server_stop(e)) return rc;
   if (!e->unverified) return GGRS_OK;
   HIP_TRY(hipSetDevice(e->cfg.device));
   int32_t f = -1;
@@ -1156,6 +1160,7 @@ int ggrs_last_launch_ms(ggrs_engine_t* e, float* ms) {
 int ggrs_timing_reset(ggrs_engine_t* e) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
   HIP_TRY(hipSetDevice(e->cfg.device));
+  if (int rc = lane_server_stop(e)) return rc;
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->collecting = true;
   e->span_open = false;
@@ -1166,6 +1171,7 @@ int ggrs_timing_reset(ggrs_engine_t* e) {
 int ggrs_timing_read(ggrs_engine_t* e, float* total_ms, int32_t* launches) {
   if (!e || !total_ms || !launches) return set_error(GGRS_E_INVALID, "null argument");
   HIP_TRY(hipSetDevice(e->cfg.device));
+  if (int rc = lane_server_stop(e)) return rc;
   float ms = 0.0f;
   if (e->span_open) {
     HIP_TRY(hipEventRecord(e->ev_end, e->stream));

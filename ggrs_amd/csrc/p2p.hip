@@ -646,31 +646,17 @@ struct ggrs_p2p_engine {
   int32_t form = 0;  // ggrs_p2p_set_unstaged: 0 default (flat), 1 global input reads, 2 lockstep staged
   int32_t* last_saved = nullptr;  // [S], sparse saving only
   int32_t* ring_frame = nullptr;  // [R][S], sparse saving only
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  std::vector<hipEvent_t> tev;
-  size_t tev_used = 0;
-  bool collecting = false;
+  SpanTimer timer;
 };
 
 namespace {
 
 template <typename K>
 int p2p_launch_timed(ggrs_p2p_engine* e, K&& launch) {
-  hipEvent_t a = e->ev0, b = e->ev1;
-  if (e->collecting) {
-    while (e->tev.size() < e->tev_used + 2) {
-      hipEvent_t ev;
-      HIP_TRY(hipEventCreate(&ev));
-      e->tev.push_back(ev);
-    }
-    a = e->tev[e->tev_used];
-    b = e->tev[e->tev_used + 1];
-    e->tev_used += 2;
-  }
-  HIP_TRY(hipEventRecord(a, e->stream));
+  if (int rc = e->timer.before(e->stream)) return rc;
   launch();
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(b, e->stream));
+  e->timer.count();
   return GGRS_OK;
 }
 
@@ -694,9 +680,7 @@ int ggrs_p2p_engine_destroy(ggrs_p2p_engine_t* e) {
                   e->hist, e->cmp_mask, e->cmp_count, e->last_saved, e->ring_frame};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
-  for (hipEvent_t ev : e->tev) (void)hipEventDestroy(ev);
-  if (e->ev0) (void)hipEventDestroy(e->ev0);
-  if (e->ev1) (void)hipEventDestroy(e->ev1);
+  e->timer.destroy();
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
   return GGRS_OK;
@@ -743,8 +727,7 @@ int ggrs_p2p_engine_create(const ggrs_p2p_config_t* cfg, ggrs_p2p_engine_t** out
   const int P = c.num_players;
   CTRY(hipSetDevice(c.device));
   CTRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
-  CTRY(hipEventCreate(&e->ev0));
-  CTRY(hipEventCreate(&e->ev1));
+  if (e->timer.create()) return fail(GGRS_E_HIP);
   CTRY(hipMalloc(&e->cur, sizeof(uint32_t) * e->F * S));
   CTRY(hipMalloc(&e->ring, sizeof(uint32_t) * (size_t)e->R * cell_dwords(P) * S));
   CTRY(hipMalloc(&e->inputs, (size_t)e->cap * S * e->Pp));
@@ -880,6 +863,9 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
 int ggrs_p2p_set_desync_detection(ggrs_p2p_engine_t* e, int32_t interval) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
   if (interval < 0) return set_error(GGRS_E_INVALID, "interval must be >= 0 (0 = DesyncDetection::Off)");
+  if (interval > 0 && e->sparse)
+    return set_error(GGRS_E_STATE, "desync detection with sparse saving is not supported: the reference sends a "
+                                   "report only for a frame it saved (p2p_session.rs:948-962, sync_layer.rs:323-326)");
   if (e->current_frame != 0)
     return set_error(GGRS_E_STATE, "desync detection is part of the session's configuration (set before the first frame)");
   HIP_TRY(hipSetDevice(e->cfg.device));
@@ -898,6 +884,9 @@ int ggrs_p2p_set_sparse_saving(ggrs_p2p_engine_t* e, int32_t on) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
   if (e->current_frame != 0)
     return set_error(GGRS_E_STATE, "sparse saving is part of the session's configuration (set before the first frame)");
+  if (on && e->desync_interval > 0)
+    return set_error(GGRS_E_STATE, "sparse saving with desync detection is not supported: the reference sends a "
+                                   "report only for a frame it saved (p2p_session.rs:948-962, sync_layer.rs:323-326)");
   HIP_TRY(hipSetDevice(e->cfg.device));
   const int64_t S = e->cfg.num_sessions;
   if (on && !e->last_saved) {
@@ -1075,25 +1064,14 @@ int ggrs_p2p_read_trace(ggrs_p2p_engine_t* e, int32_t first_frame, int32_t n, ui
 
 int ggrs_p2p_timing_reset(ggrs_p2p_engine_t* e) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
-  e->tev_used = 0;
-  e->collecting = true;
-  return GGRS_OK;
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  return e->timer.reset(e->stream);
 }
 
 int ggrs_p2p_timing_read(ggrs_p2p_engine_t* e, float* total_ms, int32_t* launches) {
   if (!e || !total_ms || !launches) return set_error(GGRS_E_INVALID, "null argument");
   HIP_TRY(hipSetDevice(e->cfg.device));
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  float total = 0.0f;
-  for (size_t i = 0; i + 1 < e->tev_used; i += 2) {
-    float ms = 0.0f;
-    HIP_TRY(hipEventElapsedTime(&ms, e->tev[i], e->tev[i + 1]));
-    total += ms;
-  }
-  *total_ms = total;
-  *launches = (int32_t)(e->tev_used / 2);
-  e->collecting = false;
-  return GGRS_OK;
+  return e->timer.read(e->stream, total_ms, launches);
 }
 
 }  // extern "C"

@@ -319,10 +319,7 @@ struct ggrs_particle_engine {
   int32_t nt_saves = 1;  // GGRS_PW_STORE=plain selects plain stores for the ring saves
   int32_t ept = 1;       // entities per thread (1, 2, 4); GGRS_PW_EPT selects (1: 4 waves/SIMD, no scratch)
   bool cur_stale = false;  // the last call was a replay: `cur` is materialised on read
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  std::vector<hipEvent_t> tev;
-  size_t tev_used = 0;
-  bool collecting = false;
+  SpanTimer timer;
 };
 
 namespace {
@@ -348,9 +345,7 @@ int ggrs_particle_engine_destroy(ggrs_particle_engine_t* e) {
                   e->lane_status, e->mis_frame, e->mis_mask, e->staging};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
-  for (hipEvent_t ev : e->tev) (void)hipEventDestroy(ev);
-  if (e->ev0) (void)hipEventDestroy(e->ev0);
-  if (e->ev1) (void)hipEventDestroy(e->ev1);
+  e->timer.destroy();
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
   return GGRS_OK;
@@ -398,8 +393,7 @@ int ggrs_particle_engine_create(const ggrs_particle_config_t* cfg, ggrs_particle
   const size_t rec = pw_rec(c.num_entities);
   CTRY(hipSetDevice(c.device));
   CTRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
-  CTRY(hipEventCreate(&e->ev0));
-  CTRY(hipEventCreate(&e->ev1));
+  if (e->timer.create()) return fail(GGRS_E_HIP);
   if (pw_lds_bytes(c.check_distance) > 65536) {  // large check distances: past the default 64 KB
     const int lds = (int)pw_lds_bytes(c.check_distance);
     CTRY(hipFuncSetAttribute((const void*)pw_synctest_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -493,24 +487,13 @@ int ggrs_particle_synctest_advance_frames(ggrs_particle_engine_t* e, int32_t n) 
   p.lane_status = e->lane_status;
   p.mis_frame = e->mis_frame;
   p.mis_mask = e->mis_mask;
-  hipEvent_t a = e->ev0, b = e->ev1;
-  if (e->collecting) {
-    while (e->tev.size() < e->tev_used + 2) {
-      hipEvent_t ev;
-      HIP_TRY(hipEventCreate(&ev));
-      e->tev.push_back(ev);
-    }
-    a = e->tev[e->tev_used];
-    b = e->tev[e->tev_used + 1];
-    e->tev_used += 2;
-  }
-  HIP_TRY(hipEventRecord(a, e->stream));
+  if (int rc = e->timer.before(e->stream)) return rc;
   const size_t lds = pw_lds_bytes(p.cd);
   if (e->ept == 1) pw_synctest_kernel<1><<<p.L, kBlock, lds, e->stream>>>(p);
   else if (e->ept == 2) pw_synctest_kernel<2><<<p.L, kBlock, lds, e->stream>>>(p);
   else pw_synctest_kernel<4><<<p.L, kBlock, lds, e->stream>>>(p);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(b, e->stream));
+  e->timer.count();
   e->current_frame += n;
   e->cur_stale = p.cd > 0 && e->current_frame - 1 > p.cd;  // the last call was a replay
   return GGRS_OK;
@@ -610,27 +593,13 @@ int ggrs_particle_debug_corrupt_on_load(ggrs_particle_engine_t* e, int32_t sessi
 int ggrs_particle_timing_reset(ggrs_particle_engine_t* e) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
   HIP_TRY(hipSetDevice(e->cfg.device));
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  e->tev_used = 0;
-  e->collecting = true;
-  return GGRS_OK;
+  return e->timer.reset(e->stream);
 }
 
 int ggrs_particle_timing_read(ggrs_particle_engine_t* e, float* total_ms, int32_t* launches) {
   if (!e || !total_ms || !launches) return set_error(GGRS_E_INVALID, "null argument");
   HIP_TRY(hipSetDevice(e->cfg.device));
-  HIP_TRY(hipStreamSynchronize(e->stream));
-  float sum = 0.0f;
-  for (size_t i = 0; i + 1 < e->tev_used; i += 2) {
-    float ms = 0.0f;
-    HIP_TRY(hipEventElapsedTime(&ms, e->tev[i], e->tev[i + 1]));
-    sum += ms;
-  }
-  *total_ms = sum;
-  *launches = (int32_t)(e->tev_used / 2);
-  e->collecting = false;
-  e->tev_used = 0;
-  return GGRS_OK;
+  return e->timer.read(e->stream, total_ms, launches);
 }
 
 }  // extern "C"

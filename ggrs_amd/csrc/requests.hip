@@ -21,7 +21,10 @@
 // against the lane's cell tags (also in LDS), then executed with the state in registers.
 #include <hip/hip_runtime.h>
 
+#include <immintrin.h>
+
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <vector>
 
@@ -37,6 +40,7 @@ namespace {
 struct LaneBatchParams {
   int64_t L;
   int32_t R, W, LD, A, S, use_status, trace_cap;
+  int32_t sys_stores;          // results straight to host memory with system-scope stores (server)
   const uint32_t* tokens;      // [W][L]
   const int32_t* load_frames;  // [LD][L]
   const uint8_t* inputs;       // [A][L][P]
@@ -49,29 +53,18 @@ struct LaneBatchParams {
   uint16_t* trace;
 };
 
-// P bytes of one lane's row, packed little-endian (player i in byte i)
-template <int P>
-__device__ inline uint32_t row_bytes(const uint8_t* row, int64_t lane) {
-  if constexpr (P == 1) return row[lane];
-  if constexpr (P == 2) return reinterpret_cast<const uint16_t*>(row)[lane];
-  if constexpr (P == 4) return reinterpret_cast<const uint32_t*>(row)[lane];
-  const uint8_t* b = row + lane * 3;
-  return (uint32_t)b[0] | ((uint32_t)b[1] << 8) | ((uint32_t)b[2] << 16);
-}
-
 // LDS: tokens [W][64] u32 | load frames [LD][64] i32 | cell tags [R][64] i32 | inputs [A][64] u32
 // | status [A][64] u32 (when used)
 __host__ __device__ inline size_t lane_batch_lds_bytes(int W, int LD, int R, int A, int use_status) {
   return (size_t)kWave * 4 * ((size_t)W + LD + R + (size_t)A * (use_status ? 2 : 1));
 }
 
+// One lane's list: stage its rows into this thread's LDS column, validate, execute.  `st` is the
+// lane's state (in registers); the lane only writes its own ring cells and outputs.
 template <int P>
-__global__ __launch_bounds__(kWave) void lane_requests_kernel(LaneBatchParams p) {
-  extern __shared__ uint32_t lds[];
+__device__ inline void run_lane(const LaneBatchParams& p, BoxState<P>& st, int64_t lane, bool valid, uint32_t* lds) {
   const int wl = threadIdx.x;
   const int64_t L = p.L;
-  const int64_t lane = (int64_t)blockIdx.x * kWave + wl;
-  const bool valid = lane < L;
   const int64_t ln = valid ? lane : 0;
   const int R = p.R;
   constexpr int F = state_fields(P);
@@ -80,17 +73,72 @@ __global__ __launch_bounds__(kWave) void lane_requests_kernel(LaneBatchParams p)
   int32_t* l_tag = l_load + p.LD * kWave;
   uint32_t* l_in = (uint32_t*)(l_tag + R * kWave);
   uint32_t* l_st = l_in + p.A * kWave;
-  // stage every row of this lane's batch (host memory: issue them all before waiting on any) and
-  // the lane's cell tags (the frame field of each ring cell)
-  for (int w = 0; w < p.W; w++) l_tok[w * kWave + wl] = p.tokens[(int64_t)w * L + ln];
-  for (int k = 0; k < p.LD; k++) l_load[k * kWave + wl] = p.load_frames[(int64_t)k * L + ln];
-  for (int a = 0; a < p.A; a++) l_in[a * kWave + wl] = row_bytes<P>(p.inputs + (int64_t)a * L * P, ln);
-  if (p.use_status)
-    for (int a = 0; a < p.A; a++) l_st[a * kWave + wl] = row_bytes<P>(p.status + (int64_t)a * L * P, ln);
-  for (int s = 0; s < R; s++) l_tag[s * kWave + wl] = (int32_t)p.ring[(int64_t)s * F * L + ln];
-  BoxState<P> st;
-  load_state<P>(st, p.cur + ln, L);
-  if (!valid) return;  // no barrier follows: every lane only reads its own LDS column
+  // Stage this lane's rows -- tokens, load frames, inputs, status (host memory, one PCIe round trip
+  // each) and the cell tags (the frame field of each ring cell) -- as ONE sequence of rows loaded
+  // kStageChunk at a time with every load of a chunk in flight before the first LDS store (a
+  // load-store pair per row would wait out a PCIe round trip per row).  LDS rows are consecutive
+  // in the same order, so row i lands at lds[i * 64 + lane].
+  {
+    const int n_tok = p.W, n_ld = n_tok + p.LD, n_in = n_ld + p.A, n_st = n_in + (p.use_status ? p.A : 0);
+    const int n_rows = n_st + R;
+    // LDS order: tokens, loads, tags, inputs, status
+    auto lds_row = [&](int i) -> uint32_t* {
+      if (i < n_ld) return lds + i * kWave;
+      if (i < n_st) return lds + (i + R) * kWave;
+      return lds + (i - n_st + n_ld) * kWave;
+    };
+    // host rows are read with system-scope loads: plain loads of pinned host memory may be served
+    // from the device's L2, and the persistent server re-reads the same rows every batch
+    auto ld_sys = [](const auto* ptr) { return __hip_atomic_load(ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
+    if constexpr (P == 3) {  // 3-byte input rows: byte loads, row by row
+      auto bytes3 = [&](const uint8_t* row) {
+        const uint8_t* b = row + ln * 3;
+        return (uint32_t)ld_sys(b) | ((uint32_t)ld_sys(b + 1) << 8) | ((uint32_t)ld_sys(b + 2) << 16);
+      };
+      for (int i = 0; i < n_rows; i++) {
+        uint32_t v;
+        if (i < n_tok) v = ld_sys(p.tokens + (int64_t)i * L + ln);
+        else if (i < n_ld) v = (uint32_t)ld_sys(p.load_frames + (int64_t)(i - n_tok) * L + ln);
+        else if (i < n_in) v = bytes3(p.inputs + (int64_t)(i - n_ld) * L * P);
+        else if (i < n_st) v = bytes3(p.status + (int64_t)(i - n_in) * L * P);
+        else v = p.ring[(int64_t)(i - n_st) * F * L + ln];
+        lds_row(i)[wl] = v;
+      }
+    } else {
+      // every row is one dword load per lane from a wave-uniform row base: 4-byte rows at 4 * lane,
+      // P-byte input / status rows at the dword holding byte P * lane (extracted after the loads)
+      const uint32_t boff = (uint32_t)(P * ln);
+      const uint32_t in_off = boff & ~3u, in_shift = 8u * (boff & 3u);
+      constexpr uint32_t kMask = P == 4 ? 0xffffffffu : ((1u << (8 * P)) - 1u);
+      auto row_base = [&](int i) -> const uint8_t* {
+        const uint8_t* tk = (const uint8_t*)p.tokens + (int64_t)i * L * 4;
+        const uint8_t* ld = (const uint8_t*)p.load_frames + (int64_t)(i - n_tok) * L * 4;
+        const uint8_t* in = p.inputs + (int64_t)(i - n_ld) * L * P;
+        const uint8_t* sb = p.status + (int64_t)(i - n_in) * L * P;
+        const uint8_t* rg = (const uint8_t*)p.ring + (int64_t)(i - n_st) * F * L * 4;
+        return i < n_tok ? tk : (i < n_ld ? ld : (i < n_in ? in : (i < n_st ? sb : rg)));
+      };
+      constexpr int kStageChunk = 16;
+      for (int base = 0; base < n_rows; base += kStageChunk) {
+        uint32_t v[kStageChunk];
+#pragma unroll
+        for (int u = 0; u < kStageChunk; u++) {
+          const int i = min(base + u, n_rows - 1);
+          const bool bytes = i >= n_ld && i < n_st;
+          v[u] = ld_sys((const uint32_t*)(row_base(i) + (bytes ? in_off : 4u * (uint32_t)ln)));
+        }
+#pragma unroll
+        for (int u = 0; u < kStageChunk; u++) {
+          const int i = base + u;
+          if (i < n_rows) {
+            const bool bytes = i >= n_ld && i < n_st;
+            lds_row(i)[wl] = bytes ? (v[u] >> in_shift) & kMask : v[u];
+          }
+        }
+      }
+    }
+  }
+  if (!valid) return;  // every lane only reads its own LDS column: no barrier needed
 
   const int n_tok = p.W * GGRS_TOKENS_PER_WORD;
   auto token = [&](int k) -> uint32_t { return (l_tok[(k >> 4) * kWave + wl] >> (2 * (k & 15))) & 3u; };
@@ -122,8 +170,12 @@ __global__ __launch_bounds__(kWave) void lane_requests_kernel(LaneBatchParams p)
       }
     }
   }
+  auto put_result = [&](int32_t v) {
+    if (p.sys_stores) __hip_atomic_store(&p.result[lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else p.result[lane] = v;
+  };
   if (err >= 0) {  // the lane does not run (a reference session would have panicked here)
-    p.result[lane] = -(1 + err);
+    put_result(-(1 + err));
     return;
   }
   // (2) execution: Game::handle_requests, requests strictly in order (ex_game.rs:79-99)
@@ -136,7 +188,8 @@ __global__ __launch_bounds__(kWave) void lane_requests_kernel(LaneBatchParams p)
       store_state<P>(st, p.ring + (int64_t)slot * F * L + lane, L);
       const uint16_t ck = fletcher16_state<P>(st);
       p.ring_ck[(int64_t)slot * L + lane] = ck;
-      p.cks[(int64_t)ns * L + lane] = ck;
+      if (p.sys_stores) __hip_atomic_store(&p.cks[(int64_t)ns * L + lane], ck, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      else p.cks[(int64_t)ns * L + lane] = ck;
       ++ns;
     } else if (t == GGRS_TOK_LOAD) {  // load_game_state (:111-113)
       const int32_t f = l_load[nl * kWave + wl];
@@ -157,8 +210,113 @@ __global__ __launch_bounds__(kWave) void lane_requests_kernel(LaneBatchParams p)
       ++na;
     }
   }
-  store_state<P>(st, p.cur + lane, L);
-  p.result[lane] = (int32_t)st.w[0];
+  put_result((int32_t)st.w[0]);
+}
+
+// One launch per batch.
+template <int P>
+__global__ __launch_bounds__(kWave) void lane_requests_kernel(LaneBatchParams p) {
+  extern __shared__ uint32_t lds[];
+  const int64_t lane = (int64_t)blockIdx.x * kWave + threadIdx.x;
+  const bool valid = lane < p.L;
+  BoxState<P> st;
+  load_state<P>(st, p.cur + (valid ? lane : 0), p.L);
+  run_lane<P>(p, st, lane, valid, lds);
+  if (valid) store_state<P>(st, p.cur + lane, p.L);
+}
+
+// The lane server: one persistent launch serving batch after batch, so a call costs a few PCIe
+// round trips instead of a kernel launch plus a stream synchronisation (~26 us between calls
+// measured, profiles/r02/req_diag.log).  Protocol (tools/server_probe.hip measures its pieces):
+//   * the host publishes a batch by one 64-bit store of the control word (epoch + the batch's shape,
+//     so the device reads both in one atomic load) into pinned fine-grained host memory;
+//   * only block 0 polls host memory (64+ blocks polling it over PCIe slowed every round trip 4-10x,
+//     tools/server_probe.hip) and relays the word through device memory, where the other blocks
+//     poll it with agent-scope loads;
+//   * each lane writes its checksums and result with system-scope stores (no device-cache
+//     write-back needed), the block waits for them, and the last block to finish (a device-memory
+//     counter) stores the epoch into the host's done word.
+// A lane's state stays in registers between batches and goes back to `cur` when the server exits:
+// on the quit bit, or when no batch arrived for `idle_ticks` of the constant wall clock (a watchdog
+// every block reaches, so an abandoned server drains by itself).
+namespace ctlw {  // the 64-bit control word
+constexpr uint64_t kQuit = 1ull << 45;
+__host__ __device__ constexpr uint64_t pack(int32_t epoch, int32_t W, int32_t LD, int32_t A, int32_t S, int st) {
+  return (uint64_t)(uint32_t)epoch | ((uint64_t)W << 32) | ((uint64_t)LD << 40) | ((uint64_t)(st != 0) << 44) |
+         ((uint64_t)A << 46) | ((uint64_t)S << 54);
+}
+__host__ __device__ constexpr int32_t epoch(uint64_t c) { return (int32_t)(uint32_t)c; }
+__host__ __device__ constexpr bool quit(uint64_t c) { return (c & kQuit) != 0; }
+}  // namespace ctlw
+
+struct ServerDev {  // device memory
+  uint64_t relay;   // block 0's copy of the control word for the other blocks
+  uint32_t count;   // blocks finished, over this launch's batches
+  uint32_t pad;
+};
+
+template <int P>
+__global__ __launch_bounds__(kWave) void lane_server_kernel(LaneBatchParams p, const uint64_t* ctl, int32_t* done,
+                                                            ServerDev* dev, int32_t start_epoch, int64_t idle_ticks) {
+  extern __shared__ uint32_t lds[];
+  __shared__ uint64_t s_ctl;
+  const int wl = threadIdx.x;
+  const int64_t lane = (int64_t)blockIdx.x * kWave + wl;
+  const bool valid = lane < p.L;
+  const uint32_t nblocks = gridDim.x;
+  BoxState<P> st;
+  load_state<P>(st, p.cur + (valid ? lane : 0), p.L);
+  int32_t last = start_epoch;
+  uint32_t batches = 0;
+  for (;;) {
+    if (wl == 0) {
+      const int64_t t0 = wall_clock64();
+      uint64_t c;
+      for (;;) {
+        if (blockIdx.x == 0) {
+          c = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          const bool idle = wall_clock64() - t0 > idle_ticks;
+          if (idle) c |= ctlw::kQuit;
+          if (ctlw::quit(c) || ctlw::epoch(c) != last) {
+            __hip_atomic_store(&dev->relay, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        } else {
+          c = __hip_atomic_load(&dev->relay, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (ctlw::quit(c) || ctlw::epoch(c) != last) break;
+          if (wall_clock64() - t0 > 2 * idle_ticks) {  // block 0 gone: leave as well
+            c |= ctlw::kQuit;
+            break;
+          }
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      s_ctl = c;
+    }
+    __syncthreads();
+    const uint64_t c = s_ctl;
+    __syncthreads();
+    if (ctlw::quit(c)) break;
+    LaneBatchParams q = p;
+    q.W = (int32_t)((c >> 32) & 0xff);
+    q.LD = (int32_t)((c >> 40) & 0xf);
+    q.use_status = (int32_t)((c >> 44) & 1);
+    q.A = (int32_t)((c >> 46) & 0xff);
+    q.S = (int32_t)((c >> 54) & 0x1ff);
+    q.sys_stores = 1;
+    run_lane<P>(q, st, lane, valid, lds);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this lane's result stores have left
+    __syncthreads();
+    const int32_t e = ctlw::epoch(c);
+    if (wl == 0) {
+      const uint32_t old = __hip_atomic_fetch_add(&dev->count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == (batches + 1) * nblocks - 1)  // the batch's last block: tell the host
+        __hip_atomic_store(done, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    ++batches;
+    last = e;
+  }
+  if (valid) store_state<P>(st, p.cur + lane, p.L);
 }
 
 int map_batch(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S) {
@@ -183,9 +341,10 @@ int map_batch(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S) {
   n.off_cks = o; o += up(2 * L * (size_t)S);
   n.off_result = o; o += up(4 * L);
   n.bytes = o;
-  // pinned, mapped into the device's address space: the kernel reads the rows and writes the
-  // results in place
-  HIP_TRY(hipHostMalloc((void**)&n.base, n.bytes, hipHostMallocMapped));
+  // pinned, fine-grained (coherent) and mapped into the device's address space: the kernel reads
+  // the rows and writes the results in place, and the persistent server sees every new batch
+  if (int rc = lane_server_stop(e)) return rc;
+  HIP_TRY(hipHostMalloc((void**)&n.base, n.bytes, hipHostMallocMapped | hipHostMallocCoherent));
   std::memset(n.base, 0, n.bytes);
   if (b.base) {
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -215,8 +374,11 @@ T* device_view(T* host) {
   return hipHostGetDevicePointer(&d, (void*)host, 0) == hipSuccess ? (T*)d : nullptr;
 }
 
-// Launch over the engine's mapped batch with the given counts; waits for completion.
-int run_batch(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int use_status) {
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+LaneBatchParams batch_params(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int use_status) {
   ggrs_lane_batch_t v;
   fill_batch_view(e, &v);
   LaneBatchParams p;
@@ -228,28 +390,117 @@ int run_batch(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int u
   p.S = S;
   p.use_status = use_status;
   p.trace_cap = e->cfg.trace_capacity;
+  p.sys_stores = 0;
   p.tokens = device_view(v.tokens);
   p.load_frames = device_view(v.load_frames);
   p.inputs = device_view(v.inputs);
   p.status = device_view(v.status);
   p.cks = device_view(v.checksums);
   p.result = device_view(v.lane_result);
-  if (!p.tokens || !p.load_frames || !p.inputs || !p.status || !p.cks || !p.result)
-    return set_error(GGRS_E_HIP, "hipHostGetDevicePointer failed for the lane batch");
   p.cur = e->cur;
   p.ring = e->ring;
   p.ring_ck = e->ring_ck;
   p.trace = e->trace;
+  return p;
+}
+
+constexpr double kServerIdleHost = 0.25;  // the host restarts a server idle this long (s) ...
+constexpr double kServerIdleKernel = 1.0; // ... well before the kernel's own watchdog ends it
+
+int server_start(ggrs_engine* e) {
+  LaneServerHost& s = e->server;
+  const int64_t L = e->cfg.num_lanes;
+  s.blocks = (int32_t)grid_of(L, kWave);
+  if (!s.mem) {
+    HIP_TRY(hipHostMalloc((void**)&s.mem, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(s.mem, 0, 64);
+    HIP_TRY(hipMalloc(&s.dev, sizeof(ServerDev)));
+    int rate_khz = 0;
+    HIP_TRY(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, e->cfg.device));
+    s.idle_ticks = (int64_t)(kServerIdleKernel * 1e3 * (rate_khz > 0 ? rate_khz : 100000));
+  }
+  uint64_t* ctl = (uint64_t*)s.mem;
+  __atomic_store_n(ctl, ctlw::pack(s.epoch, 0, 0, 0, 0, 0), __ATOMIC_RELEASE);
+  ServerDev init{ctlw::pack(s.epoch, 0, 0, 0, 0, 0), 0u, 0u};
+  HIP_TRY(hipMemcpyAsync(s.dev, &init, sizeof init, hipMemcpyHostToDevice, e->stream));
+  const LaneBatchHost& b = e->batch;
+  LaneBatchParams p = batch_params(e, b.words, b.loads, b.adv, b.saves, 1);
+  if (!p.tokens || !p.load_frames || !p.inputs || !p.status || !p.cks || !p.result)
+    return set_error(GGRS_E_HIP, "hipHostGetDevicePointer failed for the lane batch");
+  const uint64_t* dctl = device_view((const uint64_t*)ctl);
+  int32_t* ddone = device_view((int32_t*)(s.mem + 8));
+  if (!dctl || !ddone) return set_error(GGRS_E_HIP, "hipHostGetDevicePointer failed for the lane server");
+  const size_t lds = lane_batch_lds_bytes(b.words, b.loads, e->R, b.adv, 1);
+  // every block must be resident at once (block 0 relays the batches to the others)
+  int per_cu = 0, cus = 0;
+  int rc = GGRS_OK;
+  dispatch_players(e->cfg.num_players, [&](auto PC) {
+    constexpr int P = decltype(PC)::value;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lane_server_kernel<P>, kWave, lds) != hipSuccess) rc = 1;
+  });
+  HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->cfg.device));
+  if (rc || (int64_t)per_cu * cus < s.blocks) {
+    s.enabled = false;  // too many lanes to keep resident: one launch per batch instead
+    return GGRS_OK;
+  }
+  dispatch_players(e->cfg.num_players, [&](auto PC) {
+    constexpr int P = decltype(PC)::value;
+    lane_server_kernel<P><<<s.blocks, kWave, lds, e->stream>>>(p, dctl, ddone, (ServerDev*)s.dev, s.epoch,
+                                                                s.idle_ticks);
+  });
+  HIP_TRY(hipGetLastError());
+  s.running = true;
+  s.last_done = now_s();
+  return GGRS_OK;
+}
+
+// Publish one batch to the running server and spin until its last block reports it done.
+int server_run(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int use_status) {
+  LaneServerHost& s = e->server;
+  if (s.running && now_s() - s.last_done > kServerIdleHost) {
+    if (int rc = lane_server_stop(e)) return rc;
+  }
+  if (!s.running) {
+    if (int rc = server_start(e)) return rc;
+    if (!s.enabled) return GGRS_E_STATE;  // caller falls back to a launch per batch
+  }
+  uint64_t* ctl = (uint64_t*)s.mem;
+  const int32_t* done = (const int32_t*)(s.mem + 8);
+  const int32_t ep = ++s.epoch;
+  __atomic_store_n(ctl, ctlw::pack(ep, W, LD, A, S, use_status), __ATOMIC_RELEASE);  // after the batch rows
+  const double t0 = now_s();
+  int spins = 0;
+  while (__atomic_load_n(done, __ATOMIC_ACQUIRE) != ep) {
+    _mm_pause();
+    if (++spins == 4096) {
+      spins = 0;
+      if (now_s() - t0 > 10.0) {
+        s.running = false;  // the kernel's watchdog ends it; the stream drains on its own
+        return set_error(GGRS_E_HIP, "lane server did not finish batch %d within 10 s", ep);
+      }
+    }
+  }
+  s.last_done = now_s();
+  return GGRS_OK;
+}
+
+// Launch over the engine's mapped batch with the given counts; waits for completion.
+int run_batch(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int use_status) {
+  e->mode = kModeLaneRequests;
+  if (e->server.enabled) {
+    const int rc = server_run(e, W, LD, A, S, use_status);
+    if (rc != GGRS_E_STATE) return rc;  // GGRS_E_STATE: the grid cannot stay resident, launch instead
+  }
+  LaneBatchParams p = batch_params(e, W, LD, A, S, use_status);
+  if (!p.tokens || !p.load_frames || !p.inputs || !p.status || !p.cks || !p.result)
+    return set_error(GGRS_E_HIP, "hipHostGetDevicePointer failed for the lane batch");
   const size_t lds = lane_batch_lds_bytes(W, LD, e->R, A, use_status);
   const int64_t grid = grid_of(p.L, kWave);
-  e->mode = kModeLaneRequests;
   int rc = launch_timed(e, [&] {
-    switch (e->cfg.num_players) {
-      case 1: lane_requests_kernel<1><<<grid, kWave, lds, e->stream>>>(p); break;
-      case 2: lane_requests_kernel<2><<<grid, kWave, lds, e->stream>>>(p); break;
-      case 3: lane_requests_kernel<3><<<grid, kWave, lds, e->stream>>>(p); break;
-      default: lane_requests_kernel<4><<<grid, kWave, lds, e->stream>>>(p); break;
-    }
+    dispatch_players(e->cfg.num_players, [&](auto PC) {
+      constexpr int P = decltype(PC)::value;
+      lane_requests_kernel<P><<<grid, kWave, lds, e->stream>>>(p);
+    });
   });
   if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(e->stream));
@@ -291,6 +542,20 @@ int report_failures(const ggrs_engine* e, const int32_t* result, int32_t* n_fail
 }
 
 }  // namespace
+
+namespace ggrs {
+
+int lane_server_stop(ggrs_engine* e) {
+  LaneServerHost& s = e->server;
+  if (!s.running) return GGRS_OK;
+  uint64_t* ctl = (uint64_t*)s.mem;
+  __atomic_store_n(ctl, __atomic_load_n(ctl, __ATOMIC_ACQUIRE) | ctlw::kQuit, __ATOMIC_RELEASE);
+  s.running = false;
+  HIP_TRY(hipStreamSynchronize(e->stream));  // every block leaves its loop and stores its lanes' state
+  return GGRS_OK;
+}
+
+}  // namespace ggrs
 
 extern "C" {
 
@@ -366,6 +631,7 @@ int ggrs_handle_requests_lanes(ggrs_engine_t* e, const ggrs_request_t* reqs, con
   if (rc) return rc;
   // every lane's frame at the start of its list: the Save frames are checked on the host
   if ((int64_t)e->lane_frame.size() != L) {
+    if (int rc2 = lane_server_stop(e)) return rc2;
     e->lane_frame.assign(L, 0);
     std::vector<int32_t> fr(L);
     HIP_TRY(hipMemcpyAsync(fr.data(), e->cur, 4 * L, hipMemcpyDeviceToHost, e->stream));  // frame field row
@@ -438,6 +704,16 @@ int ggrs_handle_requests_lanes(ggrs_engine_t* e, const ggrs_request_t* reqs, con
   }
   int32_t n_failed = 0;
   return report_failures(e, v.lane_result, &n_failed);
+}
+
+int ggrs_lane_server(ggrs_engine_t* e, int32_t on) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  if (!on) {
+    if (int rc = lane_server_stop(e)) return rc;
+  }
+  e->server.enabled = on != 0;
+  return GGRS_OK;
 }
 
 int ggrs_read_lane_frames(ggrs_engine_t* e, int32_t* frames) {

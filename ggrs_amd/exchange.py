@@ -52,7 +52,10 @@ def allgather_reports(local, group=None):
 
 
 def peer_of(rank, world):
-    """The rank simulating the same sessions as `rank` (the other machine of each match)."""
+    """The rank simulating the same sessions as `rank` (the other machine of each match): ranks r
+    and r + world/2 pair up, an involution only for an even world size."""
+    if world % 2 != 0:
+        raise ValueError(f"peer replicas need an even world size, got {world}")
     return (rank + world // 2) % world
 
 
@@ -82,6 +85,7 @@ def exchange_p2p_reports(detector, group=None):
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    peer = peer_of(rank, world)  # ValueError for an odd world size
     nccl = dist.get_backend(group) == "nccl"
     device = torch.device("cuda", torch.cuda.current_device()) if nccl else None
     out = detector.outgoing(device=device)
@@ -97,8 +101,96 @@ def exchange_p2p_reports(detector, group=None):
         parts = [torch.empty_like(local) for _ in range(world)]
         dist.all_gather(parts, local.contiguous(), group=group)
         gathered = torch.stack(parts)
-    theirs = gathered[peer_of(rank, world)]
+    theirs = gathered[peer]
     for k, (call, frame, _) in enumerate(out):
         row = theirs[k]
         detector.receive(call, frame, row.view(torch.int16) if nccl else row.numpy().view(np.uint16))
     return len(out)
+
+
+class ReportExchange:
+    """Stream-ordered exchange of branch-engine reports (configs 3/4 across GPUs), one all-gather
+    per confirmation with no host synchronisation in the round loop.
+
+    The engine runs on the caller's current stream (BranchEngine.set_stream), so per round r:
+      speculate(r)                         -- current stream
+      wait for all-gather(r-1)             -- a device-side stream wait (work.wait()), after which
+                                              its desync comparison is queued on the device
+      confirm(r) -> report buffer r % 2    -- current stream (the report copy included)
+      all-gather(r) of that buffer         -- async on the collective's stream, which orders itself
+                                              after the current stream
+    so round r's all-gather overlaps round r+1's speculation (it only needs the local trunk) and the
+    double-buffered report of round r is never overwritten before its all-gather has read it.
+    With `peers` (rank r and rank r + world/2 run the same sessions, the two machines of each match)
+    every round's session checksums are compared with the peer replica's on the device
+    (compare_local_checksums_against_peers, p2p_session.rs:904-937): `desync_count` counts
+    DesyncDetected events (src/lib.rs:158-167), `first_desync_round` the earliest round with one.
+    Works over RCCL (device tensors) and gloo (CPU tensors, for tests; gloo's wait blocks the
+    host)."""
+
+    def __init__(self, engine, group=None, peers=False, keep_history=False, device=None):
+        import torch
+        import torch.distributed as dist
+        self.eng = engine
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.nccl = dist.get_backend(group) == "nccl"
+        self.peer = peer_of(self.rank, self.world) if peers and self.world >= 2 else None
+        dev = device if device is not None else (torch.device("cuda", torch.cuda.current_device())
+                                                 if self.nccl else torch.device("cpu"))
+        n = engine.report_bytes
+        self.S = engine.num_sessions
+        self.bufs = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.gathered = [torch.zeros((self.world, n), dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.work = [None, None]
+        self.frame_of = [None, None]
+        self.round = 0
+        self.desync_count = torch.zeros((), dtype=torch.int64, device=dev)
+        self.first_desync_round = torch.full((), -1, dtype=torch.int64, device=dev)
+        self.history = [] if keep_history else None
+        if self.nccl:
+            engine.set_stream(torch.cuda.current_stream().cuda_stream)
+
+    def _finish(self, k):
+        """Wait (device-side) for the all-gather in slot k and queue its comparison."""
+        import torch
+        w = self.work[k]
+        if w is None:
+            return
+        w.wait()
+        self.work[k] = None
+        g = self.gathered[k]
+        if self.history is not None:
+            self.history.append((self.frame_of[k], g.clone()))
+        if self.peer is not None:
+            ck = 2 * self.S
+            mine = g[self.rank, :ck].view(torch.int16)
+            theirs = g[self.peer, :ck].view(torch.int16)
+            n = (mine != theirs).sum()
+            first = torch.where((n > 0) & (self.first_desync_round < 0),
+                                torch.full_like(self.first_desync_round, self.frame_of[k]), self.first_desync_round)
+            self.desync_count += n
+            self.first_desync_round.copy_(first)
+
+    def step(self):
+        """One round: speculate, finish the previous all-gather, confirm, start this all-gather."""
+        import torch.distributed as dist
+        k = self.round % 2
+        self.eng.speculate()
+        self._finish(1 - k)
+        frame = self.eng.trunk_frame()
+        self.eng.confirm_to_tensor(self.bufs[k])
+        if self.nccl:
+            self.work[k] = dist.all_gather_into_tensor(self.gathered[k].view(-1), self.bufs[k], group=self.group,
+                                                       async_op=True)
+        else:  # gloo: CPU tensors
+            parts = list(self.gathered[k].unbind(0))
+            self.work[k] = dist.all_gather(parts, self.bufs[k], group=self.group, async_op=True)
+        self.frame_of[k] = frame
+        self.round += 1
+
+    def drain(self):
+        """Finish the last all-gather (device-side wait) -- call before reading results."""
+        self._finish(0)
+        self._finish(1)

@@ -137,6 +137,11 @@ class Engine:
         """The engine's mapped per-lane batch (ggrs_lane_batch_map) as numpy views."""
         return LaneBatch(self, token_words, load_slots, adv_rows, save_rows)
 
+    def set_lane_server(self, on=True):
+        """ggrs_lane_server: per-lane batches through one persistent kernel (default) or one
+        launch each."""
+        _lib.check(self._L.ggrs_lane_server(self._h, int(bool(on))))
+
     def lane_frames(self):
         out = np.zeros(self.num_lanes, np.int32)
         _lib.check(self._L.ggrs_read_lane_frames(self._h, _vp(out)))

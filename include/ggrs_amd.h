@@ -2,9 +2,11 @@
  * ggrs_amd.h -- C ABI of the MI355X batched rollback-resimulation engine.
  *
  * One engine owns L lanes.  A lane is one (session, branch): its own ex_game State, its own
- * saved-state ring and its own input stream.  All lanes of an engine execute the same request
- * program (the request kinds and frames a GGRS session emits are identical for sessions in
- * lockstep; only inputs differ), so every call below acts on all lanes at once.
+ * saved-state ring and its own input stream.  Every call acts on all lanes at once: either one
+ * request program for every lane (the fused SyncTest program, or a lockstep request list -- the
+ * kinds and frames GGRS sessions in lockstep emit are identical, only inputs differ) or one list per
+ * lane (ggrs_handle_requests_lanes / ggrs_lane_batch_run: P2P sessions that roll back to their own
+ * frames).
  *
  * Replaces (caspark/ggrs 0.10.2, file:line):
  *   ggrs_engine_create         SessionBuilder::start_synctest_session (src/sessions/builder.rs:346-358)
@@ -26,6 +28,8 @@
  *                              cells while the states live in HBM
  *   ggrs_read_mismatches       GgrsError::MismatchedChecksum { current_frame, mismatched_frames }
  *                              (src/error.rs:44-50), per lane
+ *   ggrs_handle_requests_lanes Game::handle_requests for every lane's own Vec<GgrsRequest>, as
+ *   ggrs_lane_batch_run        P2PSession::advance_frame emits them (p2p_session.rs:265-426)
  *
  * Errors: every function returns GGRS_OK (0) or a negative GGRS_E_* code; ggrs_last_error() gives
  * the message.  The reference panics (assert!) on precondition violations (sync_layer.rs:20,
@@ -188,6 +192,13 @@ int ggrs_lane_batch_run(ggrs_engine_t* eng, const ggrs_lane_batch_t* batch, int3
 int ggrs_handle_requests_lanes(ggrs_engine_t* eng, const ggrs_request_t* reqs, const int32_t* offsets,
                                const uint8_t* inputs, const uint8_t* status, uint16_t* save_checksums,
                                int32_t* lane_result);
+/* The lane server (default on): the first per-lane batch launches one persistent kernel that
+ * serves every later batch -- the host publishes a batch by bumping an epoch in pinned host memory
+ * and spins on per-block done flags, so a call costs one PCIe round trip instead of a launch plus a
+ * stream synchronisation.  It ends (lanes' states back in device memory) before any other call
+ * touches the engine's stream, when the host has been idle for 0.25 s, or by its own watchdog
+ * after 1 s without a batch.  on = 0: one launch per batch. */
+int ggrs_lane_server(ggrs_engine_t* eng, int32_t on);
 /* Every lane's current frame (its state's frame field): [num_lanes]. */
 int ggrs_read_lane_frames(ggrs_engine_t* eng, int32_t* frames);
 
@@ -280,6 +291,12 @@ int ggrs_branch_rounds(ggrs_branch_engine_t* eng, int32_t n_rounds);
 /* rounds() as one launch (default: every block replays the trunks of its own sessions, so no
  * launch boundary is needed between rounds) or, on != 0, as 2 n launches of speculate / confirm */
 int ggrs_branch_set_round_launches(ggrs_branch_engine_t* eng, int32_t on);
+/* Enqueue every launch and copy from now on on `stream` (a hipStream_t; NULL = the engine's own),
+ * e.g. the stream a collective library orders its all-gather after: speculate, confirm (with its
+ * report copy) and the report exchange then follow each other on the device with no host
+ * synchronisation (multi-GPU configs 3/4, ggrs_amd/exchange.py ReportExchange).  Work queued
+ * before the switch is ordered before work queued after it. */
+int ggrs_branch_set_stream(ggrs_branch_engine_t* eng, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Config-5 large-state stress game (defined by this build; ggrs_amd/csrc/particles.h):

@@ -147,3 +147,83 @@ def test_p2p_reports_between_peers_gloo(world):
         p.join(120)
     assert all(p.exitcode == 0 for p in procs)
     assert list(out) == [1] * world
+
+
+class FakeBranchEngine:
+    """The parts of BranchEngine a ReportExchange drives: speculate / confirm_to_tensor /
+    trunk_frame and the report shape.  Reports are a deterministic function of (frame, rank):
+    session checksums agree between peer replicas except a corrupted session from `corrupt`
+    on; survival words differ per rank.  `log` records the call order."""
+
+    def __init__(self, rank, corrupt=None):
+        self.num_sessions, self.num_lanes = S, L
+        self.report_bytes = exchange.report_layout(S, L)[2]
+        self.rank, self.frame, self.corrupt, self.log = rank, 0, corrupt, []
+
+    def speculate(self):
+        self.log.append(("speculate", self.frame))
+
+    def trunk_frame(self):
+        return self.frame
+
+    def expected(self, rank, frame):
+        c = None
+        if self.corrupt is not None and rank == self.corrupt[2] and frame >= self.corrupt[1]:
+            c = self.corrupt[0]
+        return fake_report(rank, frame, c)
+
+    def confirm_to_tensor(self, t):
+        self.log.append(("confirm", self.frame))
+        t.copy_(torch.from_numpy(self.expected(self.rank, self.frame)))
+        self.frame += 1
+
+
+def report_exchange_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # rank 0's session 7 desyncs from round 5 on: rank 0 and its peer count it every round
+        eng = FakeBranchEngine(rank, corrupt=(7, 5, 0))
+        ex = exchange.ReportExchange(eng, peers=True, keep_history=True)
+        rounds = 9
+        for _ in range(rounds):
+            ex.step()
+        ex.drain()
+        # call order: round r's confirm after its speculate, each round's speculate before the
+        # previous round's all-gather is consumed
+        assert eng.log == [x for r in range(rounds) for x in (("speculate", r), ("confirm", r))]
+        # every round's gathered reports, in round order, hold every rank's report
+        assert [f for f, _ in ex.history] == list(range(rounds))
+        for f, g in ex.history:
+            for r in range(world):
+                assert (g[r].numpy() == eng.expected(r, f)).all(), (f, r)
+        pr = exchange.peer_of(rank, world)
+        involved = rank == 0 or pr == 0
+        assert int(ex.desync_count) == ((rounds - 5) if involved else 0)
+        assert int(ex.first_desync_round) == (5 if involved else -1)
+        out[rank] = 1
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_report_exchange_stream_ordered_gloo(world):
+    """ReportExchange (configs 3/4 across GPUs): double-buffered async all-gathers, one per round,
+    results consumed a round later; contents, ordering and peer desync counts."""
+    ctx = mp.get_context("spawn")
+    out = ctx.Array("i", world)
+    port = free_port()
+    procs = [ctx.Process(target=report_exchange_worker, args=(r, world, port, out)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert list(out) == [1] * world
+
+
+def test_peer_of_needs_an_even_world():
+    assert exchange.peer_of(1, 4) == 3 and exchange.peer_of(3, 4) == 1
+    with pytest.raises(ValueError):
+        exchange.peer_of(0, 3)

@@ -91,8 +91,8 @@ def run_generic(eng, streams, exp, calls, with_status=True):
     return got
 
 
-@pytest.mark.parametrize("sparse", [False, True])
-def test_p2p_lists_300_sessions_generic(oracle, sparse):
+@pytest.mark.parametrize("sparse,server", [(False, True), (True, True), (False, False)])
+def test_p2p_lists_300_sessions_generic(oracle, sparse, server):
     """300 P2P sessions, differing first_incorrect per call, through ggrs_handle_requests_lanes."""
     from ggrs_amd import Engine
     L, calls, P, maxp = 300, 90, 2, 8
@@ -105,19 +105,24 @@ def test_p2p_lists_300_sessions_generic(oracle, sparse):
     assert len(depth) >= 4
     exp = expected(oracle, streams, P, maxp)
     eng = Engine(L, P, maxp, 0, 0)
+    eng.set_lane_server(server)
     run_generic(eng, streams, exp, calls)
     check_final(eng, exp, range(L))
     fr = eng.lane_frames()
     assert fr.tolist() == [int(np.frombuffer(bytes(e["final_state"][:4]), np.int32)[0]) for e in exp]
 
 
-def test_p2p_lists_batch_form(oracle):
-    """The same lists pre-encoded per lane into the engine's mapped batch (ggrs_lane_batch_run)."""
+@pytest.mark.parametrize("server", [True, False])
+def test_p2p_lists_batch_form(oracle, server):
+    """The same lists pre-encoded per lane into the engine's mapped batch (ggrs_lane_batch_run),
+    through the persistent lane server or one launch per batch."""
+    import time
     from ggrs_amd import Engine, encode_lane_lists
     L, calls, P, maxp = 257, 80, 2, 8
     streams = p2p_lane_streams(oracle, L, calls, P, maxp, seed=7)
     exp = expected(oracle, streams, P, maxp)
     eng = Engine(L, P, maxp, 0, 0)
+    eng.set_lane_server(server)
     batch = eng.lane_batch(2, 2, 2 * maxp + 2, 2 * maxp + 2)
     got = [[] for _ in range(L)]
     for c in range(calls):
@@ -131,6 +136,8 @@ def test_p2p_lists_batch_form(oracle):
         batch.load_frames[:LD] = enc["load_frames"]
         batch.inputs[:A] = enc["inputs"]
         batch.status[:A] = enc["status"]
+        if c == 40:
+            time.sleep(0.4)  # the host went idle: the server is restarted (its lanes' states kept)
         assert batch.run(W, LD, A, S, status=True) == 0
         for l, x in enumerate(lists):
             n = sum(1 for r in x if r[0] == REQ_SAVE)
