@@ -545,9 +545,12 @@ def run_requests(args):
     SyncTestSession emits at frame f (sync_test_session.rs:85-150: Load f-cd, cd x (Save, Advance)
     with the first Save skipped, Save f, Advance) for every lane, handed over from host memory and
     every Save's checksum handed back (what the handler passes to GameStateCell::save).
-      --req-form batch   (default) the per-lane lists pre-encoded into the engine's mapped batch
-                         (ggrs_lane_batch_run): per call the host writes tokens, load frames and
-                         input rows, one launch reads them over PCIe and writes checksums back
+      --req-form native  (default) the per-lane lists encoded into the engine's mapped batch by a
+                         C request handler (bench_native/handler_driver.c, what the Rust handler of
+                         INTEGRATION.md does per call: write request kinds, Load frames and input
+                         rows, ggrs_lane_batch_run, read every Save's checksum back), the batches
+                         served by the persistent lane server
+      --req-form batch   the same encoding written from Python (numpy) per call
       --req-form lanes   ggrs_handle_requests_lanes: the GgrsRequest lists themselves (CSR)
       --req-form lockstep  ggrs_handle_requests: one list for every lane (lockstep sessions)
     One step = `calls` such calls; inputs are resident in host memory before the timed region."""
@@ -562,7 +565,23 @@ def run_requests(args):
     eng = Engine(L, P, maxp, cd if form == "lockstep" else 0, 0, device=local_rank, trace_capacity=0)
     sink = np.zeros(1, np.uint64)
 
-    if form == "batch":
+    drv = None
+    if form == "native":
+        import ctypes
+        from ggrs_amd import build as gbuild
+        drv = ctypes.CDLL(gbuild.build_driver())
+        drv.handler_drive_synctest.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                               ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                               ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double)]
+        inputs = np.ascontiguousarray(inputs)
+
+        def run_calls(f, n):
+            s, sec = ctypes.c_uint64(), ctypes.c_double()
+            rc = drv.handler_drive_synctest(eng._h, ctypes.c_void_p(inputs.ctypes.data), L, P, cd, f, n,
+                                            ctypes.byref(s), ctypes.byref(sec))
+            assert rc == 0, rc
+            sink[0] += s.value
+    elif form == "batch":
         batch = eng.lane_batch(2, 1, cd + 1, cd + 1)
         steady = np.array(synctest_tokens(cd + 1, cd)[0], np.uint32)[:, None].repeat(L, axis=1)
 
@@ -605,21 +624,21 @@ def run_requests(args):
                 reqs, adv = lists(f)
                 eng.handle_requests(reqs, np.ascontiguousarray(inputs[adv]))
 
-    f = 0
-    for _ in range(cd + 1 + args.warmup * calls):  # warm-up frames, then untimed steps
-        call(f)
-        f += 1
-    eng.synchronize()
+    if drv is None:
+        def run_calls(f, n):
+            for k in range(n):
+                call(f + k)
+    f = cd + 1 + args.warmup * calls  # warm-up frames, then untimed steps
+    run_calls(0, f)
     if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps * calls):
-        call(f)
-        f += 1
-    eng.synchronize()
+    run_calls(f, args.steps * calls)  # every call returns with its results in host memory: synchronised
+    f += args.steps * calls
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    eng.synchronize()
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -678,7 +697,7 @@ def main():
     ap.add_argument("--p2p-form", choices=["default", "flat", "lockstep", "unstaged"], default="default",
                     help="p2p: kernel form (DESIGN.md section 3)")
     ap.add_argument("--sparse", action="store_true", help="p2p: sparse saving (SURVEY.md 8f row 4)")
-    ap.add_argument("--req-form", choices=["batch", "lanes", "lockstep"], default="batch",
+    ap.add_argument("--req-form", choices=["native", "batch", "lanes", "lockstep"], default="native",
                     help="requests: the boundary form (run_requests docstring)")
     ap.add_argument("--workload", choices=["synctest", "p2p", "codec", "requests"], default="synctest",
                     help="p2p: the device P2P rollback decision (SURVEY.md 8f), --sessions per GPU")

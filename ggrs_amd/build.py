@@ -59,6 +59,25 @@ def build(force=False, verbose=False, out=LIB, extra=()):
     return out
 
 
+DRIVER_SRC = os.path.join(ROOT, "bench_native", "handler_driver.c")
+DRIVER_LIB = os.path.join(ROOT, "bench_native", "libhandler_driver.so")
+
+
+def build_driver(force=False, verbose=False):
+    """bench.py's request-handler driver (bench infrastructure, linked against the engine)."""
+    if not force and os.path.exists(DRIVER_LIB) and os.path.getmtime(DRIVER_LIB) >= max(
+            os.path.getmtime(DRIVER_SRC), os.path.getmtime(LIB)):
+        return DRIVER_LIB
+    cmd = ["gcc", "-O2", "-shared", "-fPIC", "-I", os.path.join(ROOT, "include"), "-o", DRIVER_LIB + ".tmp",
+           DRIVER_SRC, "-L", HERE, "-lggrs_amd", "-Wl,-rpath,$ORIGIN/../ggrs_amd"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(DRIVER_LIB + ".tmp", DRIVER_LIB)
+    return DRIVER_LIB
+
+
 if __name__ == "__main__":
     build(force="--force" in sys.argv, verbose=True)
+    build_driver(force="--force" in sys.argv, verbose=True)
     print(LIB)

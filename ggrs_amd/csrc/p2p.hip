@@ -597,6 +597,38 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
   if (kSparse) p.last_saved[sess] = last_saved;
 }
 
+// Lockstep mode (max_prediction 0; builder.rs:134-147, p2p_session.rs:301-310,393-407): a call
+// never saves, loads or resimulates; it advances only when the current frame's inputs are confirmed
+// from every player.  Which calls advance, and which input rows their AdvanceFrame reads, depend
+// only on the arrival schedule -- the same for every session of the engine -- so the host replays
+// the control flow (poll, confirmed_frame, set_last_confirmed_frame, add_local_input with its
+// delay and drops, can_advance) and hands the kernel one (local row, remote row) pair per call:
+// remote row -1 = the call does not advance; local row -1 = the default input (queue frames below
+// the input delay).  One thread per session applies them.
+template <int P>
+__global__ __launch_bounds__(256) void p2p_lockstep_kernel(P2PParams p, const int32_t* prog) {
+  const int64_t sess = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (sess >= p.S) return;
+  const int64_t S = p.S;
+  BoxState<P> st;
+  load_state<P>(st, p.cur + sess, S);
+  uint32_t lbytes = 0;  // the local players' bytes of the packed input word
+#pragma unroll
+  for (int k = 0; k < P; k++)
+    if ((p.local_mask >> k) & 1u) lbytes |= 0xffu << (8 * k);
+  for (int32_t k = 0; k < p.n; k++) {
+    const int32_t lrow = prog[2 * k], rrow = prog[2 * k + 1];
+    if (rrow >= 0) {  // AdvanceFrame with synchronized_inputs (all confirmed)
+      const uint32_t local = lrow >= 0 ? load_inputs<P>(p.inputs, (int64_t)(lrow % p.cap) * S + sess) & lbytes : 0u;
+      const uint32_t remote = load_inputs<P>(p.inputs, (int64_t)(rrow % p.cap) * S + sess) & ~lbytes;
+      advance_state<P>(st, local | remote, 0u);
+    }
+    // the display checksum of the last AdvanceFrame (ex_game.rs:121-126); 0 before the first
+    if (p.trace) p.trace[(int64_t)((p.f0 + k) % p.trace_cap) * S + sess] = st.w[0] > 0 ? fletcher16_state<P>(st) : 0;
+  }
+  store_state<P>(st, p.cur + sess, S);
+}
+
 // compare_local_checksums_against_peers for one report frame, every session at once: bit s of
 // mask = local[s] != remote[s] (p2p_session.rs:915-926), count = number of set bits.
 __global__ __launch_bounds__(256) void compare_checksums_kernel(const uint16_t* local, const uint16_t* remote, int64_t S,
@@ -646,6 +678,12 @@ struct ggrs_p2p_engine {
   int32_t form = 0;  // ggrs_p2p_set_unstaged: 0 default (flat), 1 global input reads, 2 lockstep staged
   int32_t* last_saved = nullptr;  // [S], sparse saving only
   int32_t* ring_frame = nullptr;  // [R][S], sparse saving only
+  // lockstep mode (max_prediction 0): the session-uniform control flow, replayed on the host
+  int32_t ls_frame = 0;                     // SyncLayer::current_frame
+  int32_t ls_local_last = kNull;            // local players' last queue frame (local_connect_status)
+  std::vector<int32_t> ls_row_of;           // queue frame q -> the call (input row) that added it, q % size
+  int32_t* ls_prog = nullptr;               // device copy of a launch's (local row, remote row) pairs
+  int32_t ls_prog_cap = 0;
   SpanTimer timer;
 };
 
@@ -664,8 +702,50 @@ int p2p_launch_timed(ggrs_p2p_engine* e, K&& launch) {
 // players' replay, and the remote input f - D; with sparse saving a replay starts at the last
 // save, up to max_prediction frames back
 int32_t oldest_row(const ggrs_p2p_engine* e, int32_t f) {
+  if (e->cfg.max_prediction == 0) {  // lockstep: the current frame's remote row, the next local rows
+    int32_t oldest = std::min(f, e->ls_frame);
+    const int32_t q = std::max(e->ls_frame, e->cfg.input_delay);
+    if (e->cfg.local_mask && q <= e->ls_local_last)
+      oldest = std::min(oldest, e->ls_row_of[(size_t)q % e->ls_row_of.size()]);
+    return std::max(0, oldest);
+  }
   const int32_t back = e->sparse ? e->cfg.max_prediction : e->cfg.remote_latency;
   return std::max(0, f - back - e->cfg.input_delay);
+}
+
+// Lockstep: replay calls f0 .. f0+n-1 of P2PSession::advance_frame's control flow (the same for
+// every session) into prog[n][2]; updates the engine's lockstep state.
+void lockstep_program(ggrs_p2p_engine* e, int32_t f0, int32_t n, std::vector<int32_t>& prog) {
+  const int32_t D = e->cfg.remote_latency, delay = e->cfg.input_delay;
+  const bool has_local = e->cfg.local_mask != 0;
+  const size_t Q = e->ls_row_of.size();
+  prog.assign(2 * (size_t)n, -1);
+  for (int32_t k = 0; k < n; k++) {
+    const int32_t f = f0 + k;
+    // poll_remote_clients: the remote players' inputs up to frame f - D have arrived
+    const int32_t remote_last = f - D >= 0 ? f - D : kNull;
+    // confirmed_frame (:542-553) over every player, before this call's local input
+    int32_t confirmed = remote_last;
+    if (has_local) confirmed = std::min(confirmed, e->ls_local_last);
+    // set_last_confirmed_frame (sync_layer.rs:313-340): never ahead of the current frame
+    const int32_t last_confirmed = std::min(confirmed, e->ls_frame);
+    // add_local_input (:362-377): queue frame current + delay, dropped unless it is the next one
+    // (input_queue.rs:170-186; the first add fills the frames below the delay with the default)
+    if (has_local) {
+      const int32_t qf = e->ls_frame + delay;
+      if (e->ls_local_last == kNull || qf == e->ls_local_last + 1) {
+        e->ls_row_of[(size_t)qf % Q] = f;
+        e->ls_local_last = qf;
+      }
+    }
+    // :393-407: advance only with the current frame confirmed by everyone
+    if (last_confirmed == e->ls_frame) {
+      const int32_t c = e->ls_frame;
+      prog[2 * k] = (has_local && c >= delay) ? e->ls_row_of[(size_t)c % Q] : -1;
+      prog[2 * k + 1] = c;
+      e->ls_frame += 1;
+    }
+  }
 }
 
 }  // namespace
@@ -677,7 +757,7 @@ int ggrs_p2p_engine_destroy(ggrs_p2p_engine_t* e) {
   (void)hipSetDevice(e->cfg.device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   void* bufs[] = {e->cur, e->ring, e->inputs, e->queue, e->rollbacks, e->resim, e->trace, e->staging,
-                  e->hist, e->cmp_mask, e->cmp_count, e->last_saved, e->ring_frame};
+                  e->hist, e->cmp_mask, e->cmp_count, e->last_saved, e->ring_frame, e->ls_prog};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   e->timer.destroy();
@@ -697,9 +777,8 @@ int ggrs_p2p_engine_create(const ggrs_p2p_config_t* cfg, ggrs_p2p_engine_t** out
   if (c.local_mask == (1 << c.num_players) - 1)
     return set_error(GGRS_E_INVALID, "a P2P session needs at least one remote player");
   if (c.input_delay < 0) return set_error(GGRS_E_INVALID, "input_delay must be >= 0");
-  if (c.max_prediction < 1)
-    return set_error(GGRS_E_INVALID, "max_prediction must be >= 1 (0 is lockstep mode, which never rolls back)");
-  if (c.remote_latency < 1 || c.remote_latency >= c.max_prediction)
+  if (c.max_prediction < 0) return set_error(GGRS_E_INVALID, "max_prediction must be >= 0 (0: lockstep mode)");
+  if (c.remote_latency < 1 || (c.max_prediction > 0 && c.remote_latency >= c.max_prediction))
     return set_error(GGRS_E_INVALID, "remote_latency must be in 1..max_prediction-1 (else the prediction threshold stalls)");
   if (c.predictor != 0 && c.predictor != 1) return set_error(GGRS_E_INVALID, "predictor must be 0 (repeat last) or 1 (default)");
   if (c.input_capacity == 0) c.input_capacity = 256;
@@ -712,6 +791,7 @@ int ggrs_p2p_engine_create(const ggrs_p2p_config_t* cfg, ggrs_p2p_engine_t** out
   e->F = state_fields(c.num_players);
   e->R = c.max_prediction + 1;
   e->cap = c.input_capacity;
+  if (c.max_prediction == 0) e->ls_row_of.assign((size_t)std::max(64, c.input_delay + 8), kNull);
   auto fail = [&](int rc) {
     std::string msg = ggrs_last_error();
     ggrs_p2p_engine_destroy(e);
@@ -823,6 +903,28 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
   // rows the calls read must still be in the ring: rows >= oldest_row(f0) up to f0 + n - 1
   if ((int64_t)p.f0 + n - 1 - oldest_row(e, p.f0) >= e->cap)
     return set_error(GGRS_E_INVALID, "advance of %d frames reads more input rows than input_capacity (%d)", n, e->cap);
+  if (e->cfg.max_prediction == 0) {  // lockstep mode
+    std::vector<int32_t> prog;
+    lockstep_program(e, p.f0, n, prog);
+    if (n > e->ls_prog_cap) {
+      if (e->ls_prog) HIP_TRY(hipFree(e->ls_prog));
+      e->ls_prog = nullptr;
+      e->ls_prog_cap = 0;
+      HIP_TRY(hipMalloc(&e->ls_prog, sizeof(int32_t) * 2 * (size_t)n));
+      e->ls_prog_cap = n;
+    }
+    HIP_TRY(hipMemcpyAsync(e->ls_prog, prog.data(), sizeof(int32_t) * 2 * (size_t)n, hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));  // prog is host memory that goes out of scope
+    int rc = p2p_launch_timed(e, [&] {
+      dispatch_players(e->cfg.num_players, [&](auto PC) {
+        constexpr int P = decltype(PC)::value;
+        p2p_lockstep_kernel<P><<<grid_of(p.S, 256), 256, 0, e->stream>>>(p, e->ls_prog);
+      });
+    });
+    if (rc) return rc;
+    e->current_frame += n;
+    return GGRS_OK;
+  }
   int rc = p2p_launch_timed(e, [&] {
     // stage input rows in LDS unless a call reaches further back than a stage holds
     const int32_t back = (e->sparse ? e->R - 1 : p.D) + p.delay;
@@ -895,7 +997,8 @@ int ggrs_p2p_set_sparse_saving(ggrs_p2p_engine_t* e, int32_t on) {
     HIP_TRY(hipMalloc(&e->ring_frame, sizeof(int32_t) * e->R * S));
     HIP_TRY(hipMemsetAsync(e->ring_frame, 0xff, sizeof(int32_t) * e->R * S, e->stream));
   }
-  e->sparse = on ? 1 : 0;
+  // ignored in lockstep mode, as the reference does (p2p_session.rs:187-197)
+  e->sparse = (on && e->cfg.max_prediction > 0) ? 1 : 0;
   return GGRS_OK;
 }
 
@@ -920,6 +1023,9 @@ int ggrs_p2p_debug_desync(ggrs_p2p_engine_t* e, int32_t session, int32_t frame) 
 static int hist_row(ggrs_p2p_engine_t* e, int32_t frame, const uint16_t** row) {
   const int32_t I = e->desync_interval, D = e->cfg.remote_latency;
   if (I <= 0) return set_error(GGRS_E_STATE, "desync detection is off");
+  if (e->cfg.max_prediction == 0)
+    return set_error(GGRS_E_PRECONDITION, "frame %d not reported: lockstep mode saves no state, so no checksum "
+                                          "report is ever sent (p2p_session.rs:948-962)", frame);
   if (frame < I || frame % I != 0) return set_error(GGRS_E_PRECONDITION, "frame %d is not a checksum report frame", frame);
   const int32_t newest = e->current_frame - 2 - D;  // frame_to_send of the last call run
   if (frame > newest) return set_error(GGRS_E_PRECONDITION, "frame %d not reported yet", frame);
@@ -971,6 +1077,14 @@ int ggrs_p2p_compare_checksums(ggrs_p2p_engine_t* e, int32_t frame, const uint16
 
 int ggrs_p2p_current_frame(const ggrs_p2p_engine_t* e, int32_t* out) {
   if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
+  // P2PSession::current_frame (:555-558): every call advances in rollback mode; in lockstep mode
+  // calls wait for confirmed inputs
+  *out = e->cfg.max_prediction == 0 ? e->ls_frame : e->current_frame;
+  return GGRS_OK;
+}
+
+int ggrs_p2p_calls(const ggrs_p2p_engine_t* e, int32_t* out) {
+  if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
   *out = e->current_frame;
   return GGRS_OK;
 }
@@ -1011,7 +1125,9 @@ int ggrs_p2p_read_ring(ggrs_p2p_engine_t* e, int32_t session, int32_t* frames, u
     // after call f-1 the cells hold frames f-R .. f-1 (every call saves its current frame);
     // with sparse saving the per-session tags say
     int32_t fr = kNull;
-    if (e->sparse) {
+    if (e->cfg.max_prediction == 0) {
+      // lockstep mode never saves
+    } else if (e->sparse) {
       HIP_TRY(hipMemcpy(&fr, e->ring_frame + (int64_t)slot * S + session, 4, hipMemcpyDeviceToHost));
     } else {
       for (int32_t g = f - 1; g >= 0 && g >= f - R; g--)

@@ -53,39 +53,131 @@ struct LaneBatchParams {
   uint16_t* trace;
 };
 
-// LDS: tokens [W][64] u32 | load frames [LD][64] i32 | cell tags [R][64] i32 | inputs [A][64] u32
-// | status [A][64] u32 (when used)
-__host__ __device__ inline size_t lane_batch_lds_bytes(int W, int LD, int R, int A, int use_status) {
-  return (size_t)kWave * 4 * ((size_t)W + LD + R + (size_t)A * (use_status ? 2 : 1));
+// A session's players sit on Pp adjacent lanes (Pp = P rounded up to a power of two), each lane
+// stepping one player (State::advance's per-player loop body is independent across players,
+// ex_game.rs:275-332): a lane's dependent chain per AdvanceFrame is one player's step, not P of
+// them.  Every lane of a session walks the same list; lane `pl` holds the frame and player pl's
+// x, y, vx, vy, rot (padding lanes hold zeros and store nothing).
+// Blocks of four wavefronts: the lane server's per-batch hand-offs (the relay poll, the done
+// counter) scale with the block count, so fewer, larger blocks (tools/server_probe.hip).
+constexpr int kLaneBlock = 256;
+
+template <int P>
+struct LaneGeom {
+  static constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
+  static constexpr int kSessions = kLaneBlock / Pp;  // sessions per block
+};
+
+struct Slice {
+  uint32_t frame;
+  uint32_t w[5];  // x, y, vx, vy, rot of this lane's player
+};
+
+template <int P>
+__device__ inline int slice_field(int pl, int q) {
+  const int c = pl < P ? pl : 0;
+  return q == 0 ? fld_x(P, c) : q == 1 ? fld_y(P, c) : q == 2 ? fld_vx(P, c) : q == 3 ? fld_vy(P, c) : fld_rot(P, c);
 }
 
-// One lane's list: stage its rows into this thread's LDS column, validate, execute.  `st` is the
-// lane's state (in registers); the lane only writes its own ring cells and outputs.
 template <int P>
-__device__ inline void run_lane(const LaneBatchParams& p, BoxState<P>& st, int64_t lane, bool valid, uint32_t* lds) {
+__device__ inline void load_slice(Slice& s, const uint32_t* base, int64_t L, int pl) {
+  s.frame = base[0];
+#pragma unroll
+  for (int q = 0; q < 5; q++) s.w[q] = pl < P ? base[(int64_t)slice_field<P>(pl, q) * L] : 0u;
+}
+template <int P>
+__device__ inline void store_slice(const Slice& s, uint32_t* base, int64_t L, int pl) {
+  if (pl == 0) base[0] = s.frame;
+  if (pl < P) {
+#pragma unroll
+    for (int q = 0; q < 5; q++) base[(int64_t)slice_field<P>(pl, q) * L] = s.w[q];
+  }
+}
+
+// fletcher16 of the session's bincode bytes (ex_game.rs:45-55,105-106) from the Pp lanes' slices:
+// doubled per-lane partial sums (two v_dot4 per field, the frame and constant length prefixes on
+// lane 0), summed across the group by DPP, reduced by fletcher_from_doubled (box_game.h).
+template <int P>
+__device__ inline uint32_t slice_fletcher(const Slice& s, int pl) {
+  constexpr int Pp = LaneGeom<P>::Pp;
+  constexpr int n = Fletcher<P>::n;
+  uint32_t d1 = 0, d2 = 0;
+  if (pl == 0) {
+    d1 = dot4_u8(s.frame, 0x02020202u, 2u * Fletcher<P>::kSum1Const);
+    d2 = dot4_u8(s.frame, 2u * weights_at(n, 0), 2u * Fletcher<P>::kSum2Const);
+  }
+  if (pl < P) {
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+      d1 = dot4_u8(s.w[q], 0x02020202u, d1);
+      d2 = dot4_u8(s.w[q], 2u * weights_at(n, fld_offset(P, slice_field<P>(pl, q))), d2);
+    }
+  }
+  if constexpr (Pp >= 2) {
+    d1 += (uint32_t)__builtin_amdgcn_mov_dpp((int)d1, 0xB1, 0xF, 0xF, false);  // xor 1
+    d2 += (uint32_t)__builtin_amdgcn_mov_dpp((int)d2, 0xB1, 0xF, 0xF, false);
+  }
+  if constexpr (Pp >= 4) {
+    d1 += (uint32_t)__builtin_amdgcn_mov_dpp((int)d1, 0x4E, 0xF, 0xF, false);  // xor 2
+    d2 += (uint32_t)__builtin_amdgcn_mov_dpp((int)d2, 0x4E, 0xF, 0xF, false);
+  }
+  return fletcher_from_doubled(d1, d2);
+}
+
+// State::advance for this lane's player (input byte `in`, already 4 for a Disconnected player)
+__device__ inline void slice_advance(Slice& s, uint32_t in, bool owner) {
+  s.frame = (uint32_t)((int32_t)s.frame + 1);
+  float x = __builtin_bit_cast(float, s.w[0]), y = __builtin_bit_cast(float, s.w[1]);
+  float vx = __builtin_bit_cast(float, s.w[2]), vy = __builtin_bit_cast(float, s.w[3]);
+  float rot = __builtin_bit_cast(float, s.w[4]);
+  advance_player(x, y, vx, vy, rot, in);
+  if (owner) {
+    s.w[0] = __builtin_bit_cast(uint32_t, x);
+    s.w[1] = __builtin_bit_cast(uint32_t, y);
+    s.w[2] = __builtin_bit_cast(uint32_t, vx);
+    s.w[3] = __builtin_bit_cast(uint32_t, vy);
+    s.w[4] = __builtin_bit_cast(uint32_t, rot);
+  }
+}
+
+// LDS: tokens [W][B] u32 | load frames [LD][B] i32 | cell tags [R][B] i32 | inputs [A][B] u32
+// | status [A][B] u32 (when used); B = kLaneBlock columns, column = session within the block
+__host__ __device__ inline size_t lane_batch_lds_bytes(int W, int LD, int R, int A, int use_status) {
+  return (size_t)kLaneBlock * 4 * ((size_t)W + LD + R + (size_t)A * (use_status ? 2 : 1));
+}
+
+// One session's list on its Pp lanes: stage its rows into the session's LDS column, validate,
+// execute.  `st` is this lane's slice (in registers); the session only writes its own ring cells
+// and outputs.
+template <int P>
+__device__ inline void run_lane(const LaneBatchParams& p, Slice& st, int64_t lane, bool valid, uint32_t* lds) {
+  constexpr int Pp = LaneGeom<P>::Pp;
   const int wl = threadIdx.x;
+  const int col = wl / Pp, pl = wl % Pp;  // session column in the block, player
+  const bool owner = pl < P;
   const int64_t L = p.L;
   const int64_t ln = valid ? lane : 0;
   const int R = p.R;
   constexpr int F = state_fields(P);
   uint32_t* l_tok = lds;
-  int32_t* l_load = (int32_t*)(l_tok + p.W * kWave);
-  int32_t* l_tag = l_load + p.LD * kWave;
-  uint32_t* l_in = (uint32_t*)(l_tag + R * kWave);
-  uint32_t* l_st = l_in + p.A * kWave;
-  // Stage this lane's rows -- tokens, load frames, inputs, status (host memory, one PCIe round trip
-  // each) and the cell tags (the frame field of each ring cell) -- as ONE sequence of rows loaded
-  // kStageChunk at a time with every load of a chunk in flight before the first LDS store (a
-  // load-store pair per row would wait out a PCIe round trip per row).  LDS rows are consecutive
-  // in the same order, so row i lands at lds[i * 64 + lane].
+  int32_t* l_load = (int32_t*)(l_tok + p.W * kLaneBlock);
+  int32_t* l_tag = l_load + p.LD * kLaneBlock;
+  uint32_t* l_in = (uint32_t*)(l_tag + R * kLaneBlock);
+  uint32_t* l_st = l_in + p.A * kLaneBlock;
+  // Stage the session's rows -- tokens, load frames, inputs, status (host memory, one PCIe round
+  // trip each) and the cell tags (the frame field of each ring cell) -- as ONE sequence of rows
+  // loaded kStageChunk at a time with every load of a chunk in flight before the first LDS store (a
+  // load-store pair per row would wait out a PCIe round trip per row).  The Pp lanes of a session
+  // load the same addresses and store the same values into its column, so each lane only ever
+  // reads what it wrote itself: no barrier.
   {
     const int n_tok = p.W, n_ld = n_tok + p.LD, n_in = n_ld + p.A, n_st = n_in + (p.use_status ? p.A : 0);
     const int n_rows = n_st + R;
     // LDS order: tokens, loads, tags, inputs, status
     auto lds_row = [&](int i) -> uint32_t* {
-      if (i < n_ld) return lds + i * kWave;
-      if (i < n_st) return lds + (i + R) * kWave;
-      return lds + (i - n_st + n_ld) * kWave;
+      if (i < n_ld) return lds + i * kLaneBlock;
+      if (i < n_st) return lds + (i + R) * kLaneBlock;
+      return lds + (i - n_st + n_ld) * kLaneBlock;
     };
     // host rows are read with system-scope loads: plain loads of pinned host memory may be served
     // from the device's L2, and the persistent server re-reads the same rows every batch
@@ -102,7 +194,7 @@ __device__ inline void run_lane(const LaneBatchParams& p, BoxState<P>& st, int64
         else if (i < n_in) v = bytes3(p.inputs + (int64_t)(i - n_ld) * L * P);
         else if (i < n_st) v = bytes3(p.status + (int64_t)(i - n_in) * L * P);
         else v = p.ring[(int64_t)(i - n_st) * F * L + ln];
-        lds_row(i)[wl] = v;
+        lds_row(i)[col] = v;
       }
     } else {
       // every row is one dword load per lane from a wave-uniform row base: 4-byte rows at 4 * lane,
@@ -118,7 +210,7 @@ __device__ inline void run_lane(const LaneBatchParams& p, BoxState<P>& st, int64
         const uint8_t* rg = (const uint8_t*)p.ring + (int64_t)(i - n_st) * F * L * 4;
         return i < n_tok ? tk : (i < n_ld ? ld : (i < n_in ? in : (i < n_st ? sb : rg)));
       };
-      constexpr int kStageChunk = 16;
+      constexpr int kStageChunk = 32;  // the usual list (W <= 2, LD <= 2, A <= 18, R <= 10) in one chunk
       for (int base = 0; base < n_rows; base += kStageChunk) {
         uint32_t v[kStageChunk];
 #pragma unroll
@@ -132,20 +224,46 @@ __device__ inline void run_lane(const LaneBatchParams& p, BoxState<P>& st, int64
           const int i = base + u;
           if (i < n_rows) {
             const bool bytes = i >= n_ld && i < n_st;
-            lds_row(i)[wl] = bytes ? (v[u] >> in_shift) & kMask : v[u];
+            lds_row(i)[col] = bytes ? (v[u] >> in_shift) & kMask : v[u];
           }
         }
       }
     }
   }
-  if (!valid) return;  // every lane only reads its own LDS column: no barrier needed
+  if (!valid) return;  // a session's Pp lanes are valid together
 
   const int n_tok = p.W * GGRS_TOKENS_PER_WORD;
-  auto token = [&](int k) -> uint32_t { return (l_tok[(k >> 4) * kWave + wl] >> (2 * (k & 15))) & 3u; };
-  // (1) validation: walk the list with the lane's frame and cell tags; nothing is written
-  int32_t frame = (int32_t)st.w[0];
+  // the first two token words in registers (every list GGRS emits at max_prediction <= 15 fits
+  // them), longer lists read the rest from LDS
+  const uint32_t tw0 = l_tok[col], tw1 = p.W > 1 ? l_tok[kLaneBlock + col] : 0u;
+  auto token = [&](int k) -> uint32_t {
+    const uint32_t w = k < 16 ? tw0 : (k < 32 ? tw1 : l_tok[(k >> 4) * kLaneBlock + col]);
+    return (w >> (2 * (k & 15))) & 3u;
+  };
+  // (1) validation, nothing written.  Fast path for the lists GGRS emits (at most 32 requests,
+  // at most one Load, placed before any Save): per-kind counts from the 2-bit fields by popcount,
+  // and the Load's frame against the cell tag staged from the ring.  Anything else walks the list.
+  int32_t frame = (int32_t)st.frame;
   int32_t err = -1;
-  {
+  bool walk = true;
+  if (p.W <= 2) {
+    const uint64_t w = (uint64_t)tw0 | ((uint64_t)tw1 << 32);
+    const uint64_t lo = w & 0x5555555555555555ull, hi = (w >> 1) & 0x5555555555555555ull;
+    const uint64_t end = lo & hi;
+    const uint64_t live = end ? ((end & (0 - end)) - 1) : ~0ull;  // fields before the first END
+    const uint64_t m_save = ~lo & ~hi & 0x5555555555555555ull & live, m_adv = lo & ~hi & live,
+                   m_load = hi & ~lo & live;
+    const int ns = __builtin_popcountll(m_save), na = __builtin_popcountll(m_adv),
+              nl = __builtin_popcountll(m_load);
+    if (ns <= p.S && na <= p.A && nl <= p.LD && nl <= 1 && (nl == 0 || !m_save || (m_load & (0 - m_load)) < (m_save & (0 - m_save)))) {
+      walk = false;
+      if (nl == 1) {
+        const int32_t f = l_load[col];
+        if (f < 0 || l_tag[(f % R) * kLaneBlock + col] != f) err = (int32_t)(__builtin_ctzll(m_load) >> 1);
+      }
+    }
+  }
+  if (walk) {
     int na = 0, ns = 0, nl = 0;
     int32_t slot = frame % R;
     for (int k = 0; k < n_tok; k++) {
@@ -153,12 +271,12 @@ __device__ inline void run_lane(const LaneBatchParams& p, BoxState<P>& st, int64
       if (t == GGRS_TOK_END) break;
       if (t == GGRS_TOK_SAVE) {
         if (ns == p.S) { err = k; break; }
-        l_tag[slot * kWave + wl] = frame;
+        l_tag[slot * kLaneBlock + col] = frame;
         ++ns;
       } else if (t == GGRS_TOK_LOAD) {
         if (nl == p.LD) { err = k; break; }
-        const int32_t f = l_load[nl * kWave + wl];
-        if (f < 0 || l_tag[(f % R) * kWave + wl] != f) { err = k; break; }  // sync_layer.rs:248
+        const int32_t f = l_load[nl * kLaneBlock + col];
+        if (f < 0 || l_tag[(f % R) * kLaneBlock + col] != f) { err = k; break; }  // sync_layer.rs:248
         frame = f;
         slot = f % R;
         ++nl;
@@ -171,58 +289,79 @@ __device__ inline void run_lane(const LaneBatchParams& p, BoxState<P>& st, int64
     }
   }
   auto put_result = [&](int32_t v) {
+    if (pl != 0) return;
     if (p.sys_stores) __hip_atomic_store(&p.result[lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     else p.result[lane] = v;
   };
-  if (err >= 0) {  // the lane does not run (a reference session would have panicked here)
+  if (err >= 0) {  // the session does not run (a reference session would have panicked here)
     put_result(-(1 + err));
     return;
   }
   // (2) execution: Game::handle_requests, requests strictly in order (ex_game.rs:79-99)
   int na = 0, ns = 0, nl = 0;
-  int32_t slot = (int32_t)st.w[0] % R;
+  int32_t slot = (int32_t)st.frame % R;
+  // this lane's field offsets inside a ring slot (frame on lane 0, player pl's five fields)
+  int64_t fo[5];
+#pragma unroll
+  for (int q = 0; q < 5; q++) fo[q] = (int64_t)slice_field<P>(pl, q) * L + lane;
+  const int64_t slot_stride = (int64_t)F * L;
+  auto save_cell = [&](uint32_t* cell) {
+    if (pl == 0) cell[lane] = st.frame;
+    if (owner) {
+#pragma unroll
+      for (int q = 0; q < 5; q++) cell[fo[q]] = st.w[q];
+    }
+  };
+  auto load_cell = [&](const uint32_t* cell) {
+    st.frame = cell[lane];
+#pragma unroll
+    for (int q = 0; q < 5; q++) st.w[q] = owner ? cell[fo[q]] : 0u;
+  };
   for (int k = 0; k < n_tok; k++) {
     const uint32_t t = token(k);
     if (t == GGRS_TOK_END) break;
     if (t == GGRS_TOK_SAVE) {  // save_game_state (:103-108): state + fletcher16 into the cell
-      store_state<P>(st, p.ring + (int64_t)slot * F * L + lane, L);
-      const uint16_t ck = fletcher16_state<P>(st);
-      p.ring_ck[(int64_t)slot * L + lane] = ck;
-      if (p.sys_stores) __hip_atomic_store(&p.cks[(int64_t)ns * L + lane], ck, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      else p.cks[(int64_t)ns * L + lane] = ck;
+      save_cell(p.ring + slot * slot_stride);
+      const uint32_t ck = slice_fletcher<P>(st, pl);
+      if (pl == 0) {
+        p.ring_ck[(int64_t)slot * L + lane] = (uint16_t)ck;
+        if (p.sys_stores)
+          __hip_atomic_store(&p.cks[(int64_t)ns * L + lane], (uint16_t)ck, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        else p.cks[(int64_t)ns * L + lane] = (uint16_t)ck;
+      }
       ++ns;
     } else if (t == GGRS_TOK_LOAD) {  // load_game_state (:111-113)
-      const int32_t f = l_load[nl * kWave + wl];
+      const int32_t f = l_load[nl * kLaneBlock + col];
       slot = f % R;
-      load_state<P>(st, p.ring + (int64_t)slot * F * L + lane, L);
+      load_cell(p.ring + slot * slot_stride);
       ++nl;
     } else {  // advance_frame (:115-127); Disconnected players spin (input 4, :277-281)
-      uint32_t disc = 0;
-      if (p.use_status) {
-        const uint32_t sb = l_st[na * kWave + wl];
-#pragma unroll
-        for (int i = 0; i < P; i++)
-          if (((sb >> (8 * i)) & 0xffu) == GGRS_STATUS_DISCONNECTED) disc |= 1u << i;
+      uint32_t in = (l_in[na * kLaneBlock + col] >> (8 * pl)) & 0xffu;
+      if (p.use_status && ((l_st[na * kLaneBlock + col] >> (8 * pl)) & 0xffu) == GGRS_STATUS_DISCONNECTED) in = 4u;
+      slice_advance(st, in, owner);
+      if (p.trace) {
+        const uint32_t ck = slice_fletcher<P>(st, pl);
+        if (pl == 0) p.trace[(int64_t)(((int32_t)st.frame - 1) % p.trace_cap) * L + lane] = (uint16_t)ck;
       }
-      advance_state<P>(st, l_in[na * kWave + wl], disc);
-      if (p.trace) p.trace[(int64_t)(((int32_t)st.w[0] - 1) % p.trace_cap) * L + lane] = fletcher16_state<P>(st);
       slot = slot + 1 == R ? 0 : slot + 1;
       ++na;
     }
   }
-  put_result((int32_t)st.w[0]);
+  put_result((int32_t)st.frame);
 }
 
 // One launch per batch.
 template <int P>
-__global__ __launch_bounds__(kWave) void lane_requests_kernel(LaneBatchParams p) {
+__global__ __launch_bounds__(kLaneBlock) void lane_requests_kernel(LaneBatchParams p) {
   extern __shared__ uint32_t lds[];
-  const int64_t lane = (int64_t)blockIdx.x * kWave + threadIdx.x;
+  constexpr int Pp = LaneGeom<P>::Pp;
+  const int pl = threadIdx.x % Pp;
+  const int64_t lane = (int64_t)blockIdx.x * LaneGeom<P>::kSessions + threadIdx.x / Pp;
   const bool valid = lane < p.L;
-  BoxState<P> st;
-  load_state<P>(st, p.cur + (valid ? lane : 0), p.L);
+  Slice st;
+  load_slice<P>(st, p.cur + (valid ? lane : 0), p.L, pl);
   run_lane<P>(p, st, lane, valid, lds);
-  if (valid) store_state<P>(st, p.cur + lane, p.L);
+  if (valid) store_slice<P>(st, p.cur + lane, p.L, pl);
 }
 
 // The lane server: one persistent launch serving batch after batch, so a call costs a few PCIe
@@ -256,16 +395,18 @@ struct ServerDev {  // device memory
 };
 
 template <int P>
-__global__ __launch_bounds__(kWave) void lane_server_kernel(LaneBatchParams p, const uint64_t* ctl, int32_t* done,
+__global__ __launch_bounds__(kLaneBlock) void lane_server_kernel(LaneBatchParams p, const uint64_t* ctl, int32_t* done,
                                                             ServerDev* dev, int32_t start_epoch, int64_t idle_ticks) {
   extern __shared__ uint32_t lds[];
   __shared__ uint64_t s_ctl;
   const int wl = threadIdx.x;
-  const int64_t lane = (int64_t)blockIdx.x * kWave + wl;
+  constexpr int Pp = LaneGeom<P>::Pp;
+  const int pl = wl % Pp;
+  const int64_t lane = (int64_t)blockIdx.x * LaneGeom<P>::kSessions + wl / Pp;
   const bool valid = lane < p.L;
   const uint32_t nblocks = gridDim.x;
-  BoxState<P> st;
-  load_state<P>(st, p.cur + (valid ? lane : 0), p.L);
+  Slice st;
+  load_slice<P>(st, p.cur + (valid ? lane : 0), p.L, pl);
   int32_t last = start_epoch;
   uint32_t batches = 0;
   for (;;) {
@@ -316,7 +457,7 @@ __global__ __launch_bounds__(kWave) void lane_server_kernel(LaneBatchParams p, c
     ++batches;
     last = e;
   }
-  if (valid) store_state<P>(st, p.cur + lane, p.L);
+  if (valid) store_slice<P>(st, p.cur + lane, p.L, pl);
 }
 
 int map_batch(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S) {
@@ -410,7 +551,7 @@ constexpr double kServerIdleKernel = 1.0; // ... well before the kernel's own wa
 int server_start(ggrs_engine* e) {
   LaneServerHost& s = e->server;
   const int64_t L = e->cfg.num_lanes;
-  s.blocks = (int32_t)grid_of(L, kWave);
+  s.blocks = (int32_t)grid_of(L, kLaneBlock / padded_players(e->cfg.num_players));
   if (!s.mem) {
     HIP_TRY(hipHostMalloc((void**)&s.mem, 64, hipHostMallocMapped | hipHostMallocCoherent));
     std::memset(s.mem, 0, 64);
@@ -436,7 +577,7 @@ int server_start(ggrs_engine* e) {
   int rc = GGRS_OK;
   dispatch_players(e->cfg.num_players, [&](auto PC) {
     constexpr int P = decltype(PC)::value;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lane_server_kernel<P>, kWave, lds) != hipSuccess) rc = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, lane_server_kernel<P>, kLaneBlock, lds) != hipSuccess) rc = 1;
   });
   HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->cfg.device));
   if (rc || (int64_t)per_cu * cus < s.blocks) {
@@ -445,7 +586,7 @@ int server_start(ggrs_engine* e) {
   }
   dispatch_players(e->cfg.num_players, [&](auto PC) {
     constexpr int P = decltype(PC)::value;
-    lane_server_kernel<P><<<s.blocks, kWave, lds, e->stream>>>(p, dctl, ddone, (ServerDev*)s.dev, s.epoch,
+    lane_server_kernel<P><<<s.blocks, kLaneBlock, lds, e->stream>>>(p, dctl, ddone, (ServerDev*)s.dev, s.epoch,
                                                                 s.idle_ticks);
   });
   HIP_TRY(hipGetLastError());
@@ -495,11 +636,11 @@ int run_batch(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int u
   if (!p.tokens || !p.load_frames || !p.inputs || !p.status || !p.cks || !p.result)
     return set_error(GGRS_E_HIP, "hipHostGetDevicePointer failed for the lane batch");
   const size_t lds = lane_batch_lds_bytes(W, LD, e->R, A, use_status);
-  const int64_t grid = grid_of(p.L, kWave);
+  const int64_t grid = grid_of(p.L, kLaneBlock / padded_players(e->cfg.num_players));
   int rc = launch_timed(e, [&] {
     dispatch_players(e->cfg.num_players, [&](auto PC) {
       constexpr int P = decltype(PC)::value;
-      lane_requests_kernel<P><<<grid, kWave, lds, e->stream>>>(p);
+      lane_requests_kernel<P><<<grid, kLaneBlock, lds, e->stream>>>(p);
     });
   });
   if (rc) return rc;
@@ -552,7 +693,7 @@ int lane_server_stop(ggrs_engine* e) {
   __atomic_store_n(ctl, __atomic_load_n(ctl, __ATOMIC_ACQUIRE) | ctlw::kQuit, __ATOMIC_RELEASE);
   s.running = false;
   HIP_TRY(hipStreamSynchronize(e->stream));  // every block leaves its loop and stores its lanes' state
-  return GGRS_OK;
+return GGRS_OK;
 }
 
 }  // namespace ggrs

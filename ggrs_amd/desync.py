@@ -54,6 +54,8 @@ class DesyncDetector:
 
     def _send_frame(self, call):
         """frame_to_send that goes out in `call`, or None."""
+        if self.engine.max_prediction == 0:  # lockstep mode saves nothing, so it never reports
+            return None
         fts = call - 1 - self.latency
         return fts if self.interval > 0 and fts >= self.interval and fts % self.interval == 0 else None
 
@@ -61,7 +63,7 @@ class DesyncDetector:
         """Reports sent in the calls run since the last outgoing(): [(call, frame, report)], each
         report [S] u16 numpy, or an int16 torch tensor on `device` (the bits of the u16 values)."""
         out = []
-        current = self.engine.current_frame()
+        current = self.engine.calls()
         for call in range(self.sent, current):
             fts = self._send_frame(call)
             if fts is not None:
@@ -90,7 +92,7 @@ class DesyncDetector:
         """Replay the desync steps of every call run so far (arrivals, send, compare) and return
         the DesyncDetected events they raise, in call order."""
         events = []
-        current = self.engine.current_frame()
+        current = self.engine.calls()
         for call in range(self.processed, current):
             for frame, report in self.arrivals.pop(call, []):          # poll_remote_clients
                 self._on_checksum_report(frame, report)

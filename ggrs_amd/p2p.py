@@ -48,6 +48,7 @@ def _bind(L):
     L.ggrs_p2p_add_inputs.argtypes = [vp, i32, i32, vp]
     L.ggrs_p2p_advance_frames.argtypes = [vp, i32]
     L.ggrs_p2p_current_frame.argtypes = [vp, P(i32)]
+    L.ggrs_p2p_calls.argtypes = [vp, P(i32)]
     L.ggrs_p2p_synchronize.argtypes = [vp]
     L.ggrs_p2p_read_state.argtypes = [vp, i32, vp]
     L.ggrs_p2p_read_ring.argtypes = [vp, i32, vp, vp, vp]
@@ -118,6 +119,13 @@ class P2PEngine:
     def current_frame(self):
         v = ctypes.c_int32()
         _lib.check(self._L.ggrs_p2p_current_frame(self._h, ctypes.byref(v)))
+        return v.value
+
+    def calls(self):
+        """advance_frame calls made (current_frame() is the session's frame: the same in rollback
+        mode, behind it in lockstep mode)."""
+        v = ctypes.c_int32()
+        _lib.check(self._L.ggrs_p2p_calls(self._h, ctypes.byref(v)))
         return v.value
 
     def synchronize(self):

@@ -350,8 +350,11 @@ typedef struct ggrs_p2p_config {
   int32_t num_players;     /* 1..4 (ex_game.rs:70) */
   int32_t local_mask;      /* bit p: player p is local to this peer; at least one player is remote */
   int32_t input_delay;     /* local players' frame delay (SessionBuilder::with_input_delay, builder.rs:150) */
-  int32_t max_prediction;  /* >= 1 (builder.rs with_max_prediction_window); ring = max_prediction + 1 */
-  int32_t remote_latency;  /* 1 .. max_prediction-1 frames */
+  int32_t max_prediction;  /* builder.rs with_max_prediction_window; ring = max_prediction + 1; 0 =
+                              lockstep mode (builder.rs:134-147): a call advances only once the
+                              current frame's inputs are confirmed from every player, and never
+                              saves, loads or resimulates (p2p_session.rs:301-310,393-407) */
+  int32_t remote_latency;  /* 1 .. max_prediction-1 frames (any >= 1 in lockstep mode) */
   int32_t predictor;       /* 0 PredictRepeatLast, 1 PredictDefault (src/lib.rs:390-406) */
   int32_t input_capacity;  /* frames of queued input rows; 0 = 256 */
   int32_t trace_capacity;  /* calls of display checksums kept (0: none) */
@@ -369,7 +372,10 @@ int ggrs_p2p_engine_config(const ggrs_p2p_engine_t* eng, ggrs_p2p_config_t* out)
 int ggrs_p2p_add_inputs(ggrs_p2p_engine_t* eng, int32_t first_frame, int32_t n_frames, const uint8_t* inputs);
 /* n_frames calls of advance_frame for every session; InvalidRequest when a call's row is missing */
 int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* eng, int32_t n_frames);
+/* P2PSession::current_frame (p2p_session.rs:555-558); ggrs_p2p_calls: advance_frame calls made (the
+ * same in rollback mode, where every call advances) */
 int ggrs_p2p_current_frame(const ggrs_p2p_engine_t* eng, int32_t* out);
+int ggrs_p2p_calls(const ggrs_p2p_engine_t* eng, int32_t* out);
 int ggrs_p2p_synchronize(ggrs_p2p_engine_t* eng);
 int ggrs_p2p_read_state(ggrs_p2p_engine_t* eng, int32_t session, uint8_t* out);
 /* the session's saved-state ring (SavedStates, sync_layer.rs:144-166): per slot frame, checksum,

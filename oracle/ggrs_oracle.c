@@ -1051,14 +1051,17 @@ static int p2p_advance_frame(P2PSession* s, RequestVec* rv, int* advanced) {
     s->sent = ds_check_send(s->ds, &s->sl, &s->sent_frame, &s->sent_cs);
     s->n_events = ds_compare(s->ds, s->sl.last_confirmed_frame, s->events, 8);
   }
-  if (s->sl.current_frame == 0) rv_push(rv, sl_save_current_state(&s->sl)); /* :305-308 */
+  /* lockstep mode (max_prediction 0, :301-304, in_lockstep_mode :565-571): no save, no rollback */
+  const int lockstep = s->max_prediction == 0;
+  if (s->sl.current_frame == 0 && !lockstep) rv_push(rv, sl_save_current_state(&s->sl)); /* :305-308 */
   int32_t confirmed = p2p_confirmed_frame(s);                                /* :314 */
-  int32_t first_incorrect = sl_check_simulation_consistency(&s->sl, s->disconnect_frame);
+  int32_t first_incorrect = lockstep ? NULL_FRAME : sl_check_simulation_consistency(&s->sl, s->disconnect_frame);
   if (first_incorrect != NULL_FRAME) {
     p2p_adjust_gamestate(s, first_incorrect, confirmed, rv);
     s->disconnect_frame = NULL_FRAME;
   }
-  if (s->sparse_saving) {                                                    /* :331-333 */
+  if (lockstep) {
+  } else if (s->sparse_saving) {                                             /* :331-333 */
     /* check_last_saved_state (:819-843): never lose the last saved frame out of the window */
     const int32_t last_saved = s->sl.last_saved_frame;
     if (s->sl.current_frame - last_saved >= (int32_t)s->max_prediction) {
@@ -1080,7 +1083,10 @@ static int p2p_advance_frame(P2PSession* s, RequestVec* rv, int* advanced) {
   }
   int32_t frames_ahead = s->sl.last_confirmed_frame == NULL_FRAME ? s->sl.current_frame
                                                                   : s->sl.current_frame - s->sl.last_confirmed_frame;
-  if (frames_ahead < (int32_t)s->max_prediction) {                           /* :400-421 */
+  /* :393-407: lockstep advances only with the current frame confirmed from every player */
+  const int can_advance = lockstep ? s->sl.last_confirmed_frame == s->sl.current_frame
+                                   : frames_ahead < (int32_t)s->max_prediction;
+  if (can_advance) {                                                         /* :408-421 */
     Request adv; memset(&adv, 0, sizeof adv); adv.kind = REQ_ADVANCE;
     sl_synchronized_inputs(&s->sl, s->disconnected, s->last_frame, &adv);
     s->sl.current_frame += 1;
@@ -1113,8 +1119,9 @@ int oracle_p2p_run(const OracleP2PCfg* cfg, int32_t frames, const uint8_t* input
                    OracleP2PResult* res) {
   memset(res, 0, sizeof *res);
   const size_t P = (size_t)cfg->num_players;
-  if (P < 1 || P > MAX_PLAYERS || cfg->max_prediction < 1 || cfg->latency < 1 ||
-      cfg->latency >= cfg->max_prediction || cfg->input_delay < 0 ||
+  const int lockstep = cfg->max_prediction == 0;
+  if (P < 1 || P > MAX_PLAYERS || cfg->max_prediction < 0 || cfg->latency < 1 ||
+      (!lockstep && cfg->latency >= cfg->max_prediction) || cfg->input_delay < 0 ||
       (cfg->local_mask & ~((1 << P) - 1)) != 0) {
     res->status = -1;
     return -1;
@@ -1128,7 +1135,7 @@ int oracle_p2p_run(const OracleP2PCfg* cfg, int32_t frames, const uint8_t* input
     if ((s.local_mask >> i) & 1u) s.sl.queues[i].frame_delay = (size_t)cfg->input_delay; /* :183 */
   }
   s.disconnect_frame = NULL_FRAME;
-  s.sparse_saving = cfg->sparse_saving;
+  s.sparse_saving = lockstep ? 0 : cfg->sparse_saving;  /* ignored in lockstep mode (:187-197) */
   Game g; memset(&g, 0, sizeof g);
   g.desync_frame = -1;
   state_new(&g.game_state, (uint64_t)P);
@@ -1147,7 +1154,7 @@ int oracle_p2p_run(const OracleP2PCfg* cfg, int32_t frames, const uint8_t* input
     int64_t rb0 = s.rollbacks;
     int advanced = 0;
     if (p2p_advance_frame(&s, &rv, &advanced) < 0) { res->status = -1; break; }
-    if (!advanced) { res->status = -2; break; }
+    if (!advanced && !lockstep) { res->status = -2; break; }
     if (rb_frame) {
       rb_frame[f] = -1;
       for (size_t k = 0; k < rv.n && s.rollbacks != rb0; k++)
@@ -1200,7 +1207,8 @@ int oracle_p2p_stream(const OracleP2PCfg* cfg, int32_t frames, const uint8_t* in
                       uint8_t* req_inputs, uint8_t* req_status, OracleP2PResult* res) {
   memset(res, 0, sizeof *res);
   const size_t P = (size_t)cfg->num_players;
-  if (P < 1 || P > MAX_PLAYERS || cfg->max_prediction < 1 || cfg->input_delay < 0 ||
+  const int lockstep = cfg->max_prediction == 0;
+  if (P < 1 || P > MAX_PLAYERS || cfg->max_prediction < 0 || cfg->input_delay < 0 ||
       (cfg->local_mask & ~((1 << P) - 1)) != 0 || cfg->local_mask == (1 << P) - 1) {
     res->status = -1;
     return -1;
@@ -1214,7 +1222,7 @@ int oracle_p2p_stream(const OracleP2PCfg* cfg, int32_t frames, const uint8_t* in
     if ((s.local_mask >> i) & 1u) s.sl.queues[i].frame_delay = (size_t)cfg->input_delay;
   }
   s.disconnect_frame = NULL_FRAME;
-  s.sparse_saving = cfg->sparse_saving;
+  s.sparse_saving = lockstep ? 0 : cfg->sparse_saving;
   /* the user's handler fulfils every list (a cell's frame is set by the Save it fulfils, which
    * SyncLayer::load_frame's assert reads back) */
   Game game; memset(&game, 0, sizeof game);
@@ -1227,7 +1235,7 @@ int oracle_p2p_stream(const OracleP2PCfg* cfg, int32_t frames, const uint8_t* in
   int rc = 0;
   for (int32_t f = 0; f < frames; f++) {
     const int32_t upto = arrive_upto[f];
-    if (upto >= f || upto <= f - cfg->max_prediction) { rc = -1; break; }
+    if (upto >= f || (!lockstep && upto <= f - cfg->max_prediction)) { rc = -1; break; }
     for (int32_t g = delivered + 1; g <= upto; g++)   /* poll_remote_clients: the burst */
       for (size_t i = 0; i < P; i++)
         if (!((s.local_mask >> i) & 1u)) p2p_on_remote_input(&s, i, g, inputs[(size_t)g * P + i]);
@@ -1237,7 +1245,7 @@ int oracle_p2p_stream(const OracleP2PCfg* cfg, int32_t frames, const uint8_t* in
         s.local[i].frame = s.sl.current_frame; s.local[i].input = inputs[(size_t)f * P + i]; s.has_local[i] = 1;
       }
     int advanced = 0;
-    if (p2p_advance_frame(&s, &rv, &advanced) < 0 || !advanced) { rc = -1; break; }
+    if (p2p_advance_frame(&s, &rv, &advanced) < 0 || (!advanced && !lockstep)) { rc = -1; break; }
     call_off[f] = rt;
     if (rt + (int64_t)rv.n > req_cap) { rc = -3; break; }
     for (size_t k = 0; k < rv.n; k++, rt++) {

@@ -55,7 +55,7 @@ def test_bad_config_rejected_without_device(engine_lib, kw, msg):
     (dict(local_players=(0, 1)), "remote player"),
     (dict(local_players=(2,)), "local_mask"),
     (dict(predictor=2), "predictor"),
-    (dict(max_prediction=0), "lockstep"),
+    (dict(max_prediction=-1), "max_prediction"),
 ])
 def test_bad_p2p_config_rejected_without_device(engine_lib, kw, msg):
     from ggrs_amd import InvalidRequest, P2PEngine

@@ -83,6 +83,8 @@ class FakeP2PEngine:
     """The parts of P2PEngine a DesyncDetector reads: checksum reports per frame (a deterministic
     function of frame and session, the same on both peers except one corrupted session)."""
 
+    max_prediction = 8
+
     def __init__(self, sessions, latency, corrupt=None):
         self.num_sessions, self.remote_latency, self.frame, self.corrupt = sessions, latency, 0, corrupt
 
@@ -90,6 +92,9 @@ class FakeP2PEngine:
         self.interval = interval
 
     def current_frame(self):
+        return self.frame
+
+    def calls(self):
         return self.frame
 
     def local_checksums(self, frame, out=None):

@@ -156,3 +156,26 @@ def test_p2p_sparse_plain_launches_match_oracle(oracle, P, local, delay, mp, D, 
     for n in (2, 61, 137):
         eng.advance_frames(n)
     check_against_oracle(eng, rows, [0, 1, 63, 64, 150, 299], frames, trace=False)
+
+
+@pytest.mark.parametrize("P,local,delay,D", [(2, (0,), 0, 3), (2, (1,), 2, 1), (4, (0, 2), 1, 4), (3, (0,), 0, 2),
+                                             (2, (), 1, 2)])
+def test_lockstep_mode_matches_oracle(oracle, P, local, delay, D):
+    """max_prediction 0 = lockstep mode (builder.rs:134-147): calls advance only with every
+    player's input of the current frame confirmed, never save, load or resimulate
+    (p2p_session.rs:301-310,393-407).  Display-checksum trace per call, final state, empty ring and
+    the session frame equal the oracle P2PSession's, across launches of several sizes."""
+    from ggrs_amd import P2PEngine
+    S, frames = 300, 160
+    rows = stream(S, frames, P, 1, seed_base=0x10C5)
+    eng = P2PEngine(S, num_players=P, local_players=local, input_delay=delay, max_prediction=0,
+                    remote_latency=D, trace_capacity=frames)
+    eng.set_sparse_saving(True)  # ignored in lockstep mode, as the reference does (:187-197)
+    eng.add_inputs(0, rows)
+    for n in (1, 2, 5, 40, 112):
+        eng.advance_frames(n)
+    assert eng.calls() == frames
+    ref = oracle.p2p_run(rows[:, 0], num_players=P, local_mask=eng.local_mask, input_delay=delay,
+                         max_prediction=0, latency=D)
+    assert eng.current_frame() == int.from_bytes(ref["final_state"][:4].tobytes(), "little") < frames
+    check_against_oracle(eng, rows, [0, 1, 63, 64, 150, 299], frames)

@@ -138,3 +138,38 @@ def test_sparse_saving_same_game_fewer_saves(latency, mp, model):
     assert bytes(dense["final_state"]) == bytes(sparse["final_state"])
     assert sparse["result"].n_save < dense["result"].n_save
     assert sparse["result"].resim >= dense["result"].resim
+
+
+@pytest.mark.parametrize("delay,latency", [(0, 1), (0, 3), (1, 2), (2, 5)])
+def test_lockstep_mode(oracle, delay, latency):
+    """max_prediction 0 = lockstep (builder.rs:134-147): no SaveGameState or LoadGameState ever
+    (p2p_session.rs:301-310), an AdvanceFrame only once the current frame is confirmed from every
+    player (:393-407), so every input it carries is Confirmed.  The schedule: nothing before the
+    first remote input arrives (call `latency`); then with input delay 0 the local input of the
+    current frame only enters during the call (after confirmed_frame was taken), so the session
+    advances every other call; with a delay it is queued ahead and every call advances."""
+    calls = 80
+    inp = o.gen_inputs(o.session_seed(21), calls, 2, 1)
+    r = o.p2p_run(inp, max_prediction=0, latency=latency, input_delay=delay, req_cap=4 * calls)
+    assert r["rc"] == 0 and r["result"].frames_done == calls
+    assert r["result"].n_save == 0 and r["result"].n_load == 0 and r["result"].rollbacks == 0
+    per = calls_of(r, calls)
+    adv = [len(c) for c in per]
+    assert set(adv) <= {0, 1} and all(k == [REQ_ADVANCE] for k in per if k)
+    assert adv[:latency] == [0] * latency
+    steady = adv[latency + 2:]
+    if delay == 0:  # alternating: advance, wait, advance, ...
+        assert all(steady[i] != steady[i + 1] for i in range(len(steady) - 1))
+    else:
+        assert all(steady)
+    frame = int.from_bytes(r["final_state"][:4].tobytes(), "little")
+    assert frame == sum(adv)
+    # every AdvanceFrame carries confirmed inputs only
+    s = o.p2p_stream(inp, (np.arange(calls) - latency).astype(np.int32), max_prediction=0, input_delay=delay)
+    assert s["rc"] == 0 and (s["status"] == 0).all() and (s["kind"] == REQ_ADVANCE).all()
+    h = o.handler_run(s["kind"], s["frame"], s["inputs"], s["status"], 2, 1)
+    assert bytes(h["final_state"]) == bytes(r["final_state"])
+
+
+def calls_of(out, frames):
+    return calls(out, frames)
