@@ -89,7 +89,9 @@ def setup_dist(args):
         print(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world} rank(s)", file=sys.stderr)
     import torch  # before the engine: torch's bundled HIP runtime must serve the process
     dist = None
-    if world > 1:
+    # GGRS_BENCH_DIST=1 forms the process group at one rank too (the multi-rank code path measured
+    # on one GPU: a one-rank RCCL all-gather per round)
+    if world > 1 or os.environ.get("GGRS_BENCH_DIST") == "1":
         import torch.distributed as dist
         if os.environ.get("GGRS_BENCH_BACKEND") == "gloo":
             # rehearsal of N ranks on fewer GPUs: ranks share devices, collectives over gloo
@@ -118,51 +120,54 @@ def run_branch(args):
     from ggrs_amd import BranchEngine, exchange, synth
     c = BRANCH_CONFIGS[args.config]
     S, B, P, W = c["sessions"], c["branches"], c["players"], c["window"]
-    rounds = args.warmup + args.steps
+    rps = args.rounds_per_step  # one step = rps rounds (a round lasts microseconds)
+    rounds = (args.warmup + args.steps) * rps
     group = rank % (world // 2) if (args.peers and world >= 2) else rank
     truth = synth.gen_inputs(group * S, S, rounds + W + 1, P, synth.MODEL_HELD)
     eng = BranchEngine(S, num_players=P, remote_mask=c["remote_mask"], window=W, branches=B,
                        alphabet=16, input_capacity=rounds + W + 3, device=local_rank)
     eng.add_inputs(0, truth)
     L = eng.num_lanes
-    report = torch.zeros(eng.report_bytes, dtype=torch.uint8, device=f"cuda:{local_rank}")
-    desyncs = []
+    # more than one rank: every round's report is all-gathered, stream-ordered behind the confirm
+    # on the device (exchange.ReportExchange: no host synchronisation in the round loop, round r's
+    # all-gather overlapping round r+1's speculation); one rank: rounds run fused in one launch
+    ex = exchange.ReportExchange(eng, peers=args.peers) if dist is not None else None
 
-    def round_():
-        eng.speculate()
+    def sync_all():
+        eng.synchronize()
         if dist is not None:
-            eng.confirm(report.data_ptr())
-            eng.synchronize()
-            g = exchange.allgather_reports(report)
-            if args.peers:
-                desyncs.extend(exchange.desyncs_against_peer(g, rank, world, eng.trunk_frame() - 1, S, L))
-        else:
-            eng.confirm()
+            torch.cuda.synchronize()
+            dist.barrier()
 
-    for _ in range(args.warmup):
-        round_()
-    eng.synchronize()
-    if dist is not None:
-        dist.barrier()
+    for _ in range(args.warmup * rps):
+        if ex is not None:
+            ex.step()
+        else:
+            eng.speculate()
+            eng.confirm()
+    if ex is not None:
+        ex.drain()
+    sync_all()
     eng.timing_reset()
     t0 = time.perf_counter()
-    if dist is None:
-        eng.rounds(args.steps)  # one GPU: no exchange between rounds, issue them back to back
-    else:
+    if ex is None:
         for _ in range(args.steps):
-            round_()
-    eng.synchronize()
-    if dist is not None:
-        dist.barrier()
+            eng.rounds(rps)  # one GPU: no exchange between rounds, one fused launch per step
+    else:
+        for _ in range(args.steps * rps):
+            ex.step()
+        ex.drain()
+    sync_all()
     t1 = time.perf_counter()
     kernel_ms, launches = eng.timing_read()
     elapsed = t1 - t0
+    n_desync = int(ex.desync_count.item()) if ex is not None else 0
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     resim_round = L * W + S
-    value = resim_round * args.steps * world / elapsed
+    value = resim_round * rps * args.steps * world / elapsed
     Sp = 4 + 20 * P
     bytes_round = L * (Sp + W * (Sp + 2) + W * P) + S * (2 * Sp + 2 + P) + 8 * ((L + 63) // 64)
     avg_round_s = kernel_ms / 1e3 / max(launches, 1) * 2  # speculate + confirm launches per round
@@ -178,9 +183,19 @@ def run_branch(args):
             ck, _ = eng.report()
             parity = {"session0_trunk_bit_exact": bytes(eng.trunk(0)) == bytes(st),
                       "session0_checksum": int(ck[0]) == O.fletcher16(bytes(st)),
-                      "desyncs": int((eng.desync() >= 0).sum()) + len(desyncs)}
+                      "desyncs": int((eng.desync() >= 0).sum()) + n_desync}
         except Exception as exc:
             parity = {"error": repr(exc)}
+        cpu_baseline = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu_baseline = branch_cpu_baseline(args, c)
+        # distinct speculated states per round: branches sharing their first k digits share the
+        # state after k + 1 frames (config 3: 16 + 256 + 4096 + 65536 of the 4 x 65536 logical)
+        A = 16
+        E = 0
+        while A ** E < B:
+            E += 1
+        distinct = S * sum(min(A ** min(k + 1, E), B) for k in range(W)) + S
         line = {
             "metric": "resimulated session-frames/sec (node)", "value": round(value, 1),
             "unit": "session-frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -188,12 +203,17 @@ def run_branch(args):
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": c["text"], "sessions_per_gpu": S, "branches": B, "lanes_per_gpu": L,
                        "players": P, "window": W, "peers": bool(args.peers),
-                       "parallelism": f"sessions sharded over {world} GPU(s), RCCL all-gather per round"},
+                       "logical_frames_per_round": resim_round, "prefix_distinct_frames_per_round": distinct,
+                       "prefix_distinct_frames_per_s": round(distinct * rps * args.steps * world / elapsed, 1),
+                       "rounds_per_step": rps,
+                       "parallelism": f"sessions sharded over {world} GPU(s)" + (
+                           ", one stream-ordered RCCL all-gather of the reports per round" if dist is not None else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 6),
+                         "traffic": pmc_traffic(f"config{args.config}"),
                          "algorithmic_bytes_per_round": bytes_round,
                          "avg_kernel_ms_per_round": round(avg_round_s * 1e3, 4)},
-            "cpu_baseline": None, "parity": parity,
+            "cpu_baseline": cpu_baseline, "parity": parity,
         }
         print(json.dumps(line))
     if dist is not None:
@@ -251,6 +271,16 @@ def run_particles(args):
                           for fr, ck in zip(r["ring_frames"], r["ring_cksums"]) if fr >= 0)}
         except Exception as exc:
             parity = {"error": repr(exc)}
+        cpu_baseline = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu_baseline = branch_cpu_baseline(args, c)
+        # distinct speculated states per round: branches sharing their first k digits share the
+        # state after k + 1 frames (config 3: 16 + 256 + 4096 + 65536 of the 4 x 65536 logical)
+        A = 16
+        E = 0
+        while A ** E < B:
+            E += 1
+        distinct = S * sum(min(A ** min(k + 1, E), B) for k in range(W)) + S
         line = {
             "metric": "resimulated session-frames/sec (node)", "value": round(value, 1),
             "unit": "session-frames/s", "n_gpus": world, "steps": args.steps, "warmup": warm,
@@ -467,6 +497,12 @@ def run_codec(args):
                 n1, w1 = O.codec_bench(ref[:sample], pend[:sample], count[:sample], 1)
                 passes = max(1, int(10.0 / max(w1, 1e-3)))
                 n, wall = O.codec_bench(ref[:sample], pend[:sample], count[:sample], passes)
+                # config 1's own semantics (the reference's ex_game SyncTest: check_distance 7,
+                # input delay 2, max_prediction 8, uniform inputs) on the same threads
+                frames_c1 = max(args.cpu_frames // 2, total_frames)
+                n_c1, wall_c1, _ = O.synctest_bench(threads, frames_c1, warmup=0, num_players=2, max_prediction=8,
+                                                    check_distance=7, input_delay=2, model=O.MODEL_UNIFORM,
+                                                    seed_base=synth.SEED_BASE)
                 cpu_baseline = {"value": round(n / wall, 1), "unit": "packets/s", "cores": 1, "kind": "port",
                                 "sample": f"{passes} passes x {sample} packets (W {W}, B {B}), encode + decode "
                                           f"one packet at a time (oracle/codec.c)",
@@ -495,17 +531,39 @@ def run_codec(args):
         dist.destroy_process_group()
 
 
+def cpu_threads(args):
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return args.cpu_threads or min(16, avail)
+
+
+def branch_cpu_baseline(args, c):
+    """Configs 3/4 on the host: every branch a rollback replay through the SyncLayer + ex_game
+    handler restatement (oracle_branch_bench, ggrs_oracle.c), T threads with their own sessions."""
+    from oracle import oracle as O
+    O.build()
+    T = cpu_threads(args)
+    if c["sessions"] == 1:  # config 3: one 65,536-branch session per thread
+        sessions, rounds = 1, 12
+    else:                   # config 4: 16-branch sessions
+        sessions, rounds = 512, 48
+    n, wall, _ = O.branch_bench(c["players"], c["window"], 16, c["branches"], c["remote_mask"], sessions, rounds, T)
+    return {"value": round(n / wall, 1), "unit": "session-frames/s", "cores": T, "kind": "port",
+            "sample": f"{T} threads x {sessions} session(s) x {rounds} rounds of {c['branches']} branch rollbacks "
+                      f"(W={c['window']}, P={c['players']}) + trunk confirm, SyncLayer + ex_game handler "
+                      "restatement (oracle/ggrs_oracle.c oracle_branch_bench)",
+            "wall_s": round(wall, 3)}
+
+
 def p2p_cpu_baseline(args, O, synth, P, D, maxp):
     """The oracle's P2P session (C restatement of p2p_session.rs:265-426 + ex_game) on T host
     threads, one session per thread (ctypes drops the GIL for the call)."""
     from concurrent.futures import ThreadPoolExecutor
 
     import numpy as np
-    try:
-        avail = len(os.sched_getaffinity(0))
-    except AttributeError:
-        avail = os.cpu_count() or 1
-    T = args.cpu_threads or min(16, avail)
+    T = cpu_threads(args)
     frames = 2_000_000
     rows = synth.gen_inputs(0, T, frames, P, synth.MODEL_HELD)
     per = [np.ascontiguousarray(rows[:, t]) for t in range(T)]
@@ -690,6 +748,7 @@ def main():
     ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=2,
                     help="BASELINE.json config: 2 = SyncTest (default), 3/4 = branch rollback, "
                          "5 = 1 MB particle-world SyncTest")
+    ap.add_argument("--rounds-per-step", type=int, default=16, help="configs 3/4: rounds per step")
     ap.add_argument("--sessions", type=int, default=0, help="config 5: sessions per GPU (0 = 8192)")
     ap.add_argument("--peers", action="store_true",
                     help="configs 3/4 and p2p: rank r and r + world/2 run the same sessions (the two "
@@ -783,11 +842,7 @@ def main():
                           (eng.trace(total_frames - trace_cap, trace_cap)[:, 0] ==
                            ref["cksum"][total_frames - trace_cap:]).all())}
             if world == 1 and not args.no_cpu_baseline:
-                try:
-                    avail = len(os.sched_getaffinity(0))
-                except AttributeError:
-                    avail = os.cpu_count() or 1
-                threads = args.cpu_threads or min(16, avail)
+                threads = cpu_threads(args)
                 frames = max(args.cpu_frames, total_frames)
                 n, wall, ck0 = O.synctest_bench(threads, frames, warmup=0, num_players=P,
                                                 max_prediction=maxp, check_distance=cd,
@@ -809,6 +864,10 @@ def main():
                     "thread0_matches_gpu_lane0": bool((ck0[total_frames - trace_cap:total_frames] == gpu_tr).all()),
                     "single_thread": {"value": round(n1 / wall1, 1), "cores": 1, "frames": frames1,
                                       "wall_s": round(wall1, 3)},
+                    "config1_semantics": {"value": round(n_c1 / wall_c1, 1), "cores": threads, "frames": frames_c1,
+                                          "wall_s": round(wall_c1, 3),
+                                          "sample": "check_distance 7, input delay 2, max_prediction 8, uniform "
+                                                    "inputs, 2 players (the reference's ex_game SyncTest)"},
                 }
         except Exception as exc:  # the oracle is optional on the measurement path
             parity = {"error": repr(exc)}

@@ -55,6 +55,9 @@ def _bind(L):
     L.ggrs_branch_rounds.argtypes = [vp, ctypes.c_int32]
     L.ggrs_branch_set_round_launches.argtypes = [vp, ctypes.c_int32]
     L.ggrs_branch_set_stream.argtypes = [vp, vp]
+    L.ggrs_branch_round.argtypes = [vp, vp]
+    i32 = ctypes.c_int32
+    L.ggrs_branch_compare_peer.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp]
     for name in _lib.EXPORTS:
         if name.startswith("ggrs_branch_"):
             getattr(L, name).restype = ctypes.c_int
@@ -122,6 +125,25 @@ class BranchEngine:
             self.confirm(t.data_ptr())
             return
         self.confirm()
+        self._report_into(t)
+
+    def round_to_tensor(self, t):
+        """One round (speculate + confirm) as one launch, its report written into device uint8
+        tensor `t` by the kernel itself (ggrs_branch_round); a CPU tensor through a host read."""
+        if t.is_cuda:
+            _lib.check(self._L.ggrs_branch_round(self._h, ctypes.c_void_p(t.data_ptr())))
+            return
+        _lib.check(self._L.ggrs_branch_round(self._h, None))
+        self._report_into(t)
+
+    def compare_peer(self, gathered, rank, peer, frame, count, first_frame):
+        """Queue the peer checksum comparison of one all-gathered report block (device tensors:
+        gathered [world][report_bytes] u8, count and first_frame int64 scalars)."""
+        _lib.check(self._L.ggrs_branch_compare_peer(
+            self._h, ctypes.c_void_p(gathered.data_ptr()), gathered.shape[0], rank, peer, frame,
+            ctypes.c_void_p(count.data_ptr()), ctypes.c_void_p(first_frame.data_ptr())))
+
+    def _report_into(self, t):
         ck, bits = self.report()
         raw = np.zeros(self.report_bytes, np.uint8)
         raw[:2 * self.num_sessions] = ck.view(np.uint8)

@@ -162,6 +162,8 @@ struct RoundsParams {
   uint32_t* trunk;
   uint16_t* report_ck;
   uint64_t* report_bits;
+  uint16_t* copy_ck;    // optional second destination of the last round's report (the caller's
+  uint64_t* copy_bits;  // exchange buffer, same layout): saves a device-to-device copy per round
 };
 constexpr int kRoundsBlock = 256;
 
@@ -243,7 +245,10 @@ __global__ __launch_bounds__(kRoundsBlock) void rounds_kernel(RoundsParams rp) {
       }
     }
     const uint64_t bits = __ballot(survive);
-    if (in_range && (threadIdx.x & 63) == 0) rp.report_bits[lane >> 6] = bits;
+    if (in_range && (threadIdx.x & 63) == 0) {
+      rp.report_bits[lane >> 6] = bits;
+      if (rp.copy_bits && r + 1 == rp.n) rp.copy_bits[lane >> 6] = bits;
+    }
     survived = survive;
     __syncthreads();  // every lane has read the trunk
     if ((int)threadIdx.x < ns) {
@@ -261,11 +266,32 @@ __global__ __launch_bounds__(kRoundsBlock) void rounds_kernel(RoundsParams rp) {
       if (s2 * p.B >= lane0) {  // this block holds the session's branch-0 lane
         store_state<P>(tr, rp.trunk + s2, p.S);
         rp.report_ck[s2] = ck;
+        if (rp.copy_ck && r + 1 == rp.n) rp.copy_ck[s2] = ck;
       }
     }
     __syncthreads();
     row_c = wrap_inc(row_c, p.cap);
     slot_c = wrap_inc(slot_c, p.R);
+  }
+}
+
+// compare_local_checksums_against_peers (p2p_session.rs:904-937) over an all-gathered report
+// block: sessions whose trunk checksum differs between this rank's row and its peer's each count
+// one DesyncDetected (src/lib.rs:158-167); the first round with any is recorded.
+__global__ __launch_bounds__(256) void compare_peer_kernel(const uint8_t* gathered, int64_t row_bytes, int32_t rank,
+                                                           int32_t peer, int64_t S, int32_t frame,
+                                                           unsigned long long* count, unsigned long long* first) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool bad = false;
+  if (s < S) {
+    const uint16_t* mine = (const uint16_t*)(gathered + (int64_t)rank * row_bytes);
+    const uint16_t* theirs = (const uint16_t*)(gathered + (int64_t)peer * row_bytes);
+    bad = mine[s] != theirs[s];
+  }
+  const uint64_t m = __ballot(bad);
+  if ((threadIdx.x & 63) == 0 && m) {
+    atomicAdd(count, (unsigned long long)__popcll(m));
+    atomicCAS(first, ~0ull, (unsigned long long)(int64_t)frame);
   }
 }
 
@@ -587,58 +613,94 @@ int ggrs_branch_timing_read(ggrs_branch_engine_t* e, float* total_ms, int32_t* l
   return e->timer.read(e->stream, total_ms, launches);
 }
 
+namespace {
+
+// n rounds in one rounds_kernel launch; the last round's report also to `copy` (may be null)
+int launch_rounds(ggrs_branch_engine* e, int32_t n_rounds, void* copy) {
+  RoundsParams rp;
+  SpecParams& p = rp.sp;
+  p.S = e->cfg.num_sessions;
+  p.L = e->L;
+  p.B = e->cfg.branches;
+  p.W = e->cfg.window;
+  p.R = e->R;
+  p.A = e->cfg.alphabet;
+  p.E = e->E;
+  p.cap = e->cap;
+  p.P = e->cfg.num_players;
+  p.f_c = e->trunk_frame;
+  p.remote_mask = (uint32_t)e->cfg.remote_mask;
+  p.first_remote = e->first_remote;
+  p.check_prev = e->have_prev ? 1 : 0;
+  p.trunk = e->trunk;
+  p.ring = e->ring;
+  p.ring_ck = e->ring_ck;
+  p.inputs = e->inputs;
+  p.prev_survive = (const uint64_t*)(e->report + report_ck_bytes(p.S));
+  p.trunk_ck = (const uint16_t*)e->report;
+  p.desync = e->desync;
+  rp.n = n_rounds;
+  rp.trunk = e->trunk;
+  rp.report_ck = (uint16_t*)e->report;
+  rp.report_bits = (uint64_t*)(e->report + report_ck_bytes(p.S));
+  rp.copy_ck = copy ? (uint16_t*)copy : nullptr;
+  rp.copy_bits = copy ? (uint64_t*)((uint8_t*)copy + report_ck_bytes(p.S)) : nullptr;
+  // counted as the 2 n speculate + confirm launches it replaces
+  int rc = branch_launch_timed(e, [&] {
+    dispatch_players(p.P, [&](auto PC) {
+      constexpr int P = decltype(PC)::value;
+      rounds_kernel<P><<<grid_of(p.L, kRoundsBlock), kRoundsBlock, 0, e->stream>>>(rp);
+    });
+  }, 2 * n_rounds);
+  if (rc) return rc;
+  e->trunk_frame += n_rounds;
+  e->have_prev = true;
+  return GGRS_OK;
+}
+
+int check_rounds_queued(const ggrs_branch_engine* e, int32_t n_rounds) {
+  if ((int64_t)e->trunk_frame + n_rounds - 1 + e->cfg.window - 1 >= e->next_input_frame)
+    return set_error(GGRS_E_INVALID, "inputs for %d rounds are not queued", n_rounds);
+  return GGRS_OK;
+}
+
+}  // namespace
+
 int ggrs_branch_rounds(ggrs_branch_engine_t* e, int32_t n_rounds) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
   if (n_rounds < 0) return set_error(GGRS_E_INVALID, "n_rounds must be >= 0");
-  if ((int64_t)e->trunk_frame + n_rounds - 1 + e->cfg.window - 1 >= e->next_input_frame)
-    return set_error(GGRS_E_INVALID, "inputs for %d rounds are not queued", n_rounds);
+  if (int rc = check_rounds_queued(e, n_rounds)) return rc;
   if (n_rounds == 0) return GGRS_OK;
   HIP_TRY(hipSetDevice(e->cfg.device));
+  if (!e->per_round_launches) return launch_rounds(e, n_rounds, nullptr);
   int rc = GGRS_OK;
-  if (!e->per_round_launches) {
-    // one launch for all n rounds (rounds_kernel); counted as the 2 n launches it replaces
-    RoundsParams rp;
-    SpecParams& p = rp.sp;
-    p.S = e->cfg.num_sessions;
-    p.L = e->L;
-    p.B = e->cfg.branches;
-    p.W = e->cfg.window;
-    p.R = e->R;
-    p.A = e->cfg.alphabet;
-    p.E = e->E;
-    p.cap = e->cap;
-    p.P = e->cfg.num_players;
-    p.f_c = e->trunk_frame;
-    p.remote_mask = (uint32_t)e->cfg.remote_mask;
-    p.first_remote = e->first_remote;
-    p.check_prev = e->have_prev ? 1 : 0;
-    p.trunk = e->trunk;
-    p.ring = e->ring;
-    p.ring_ck = e->ring_ck;
-    p.inputs = e->inputs;
-    p.prev_survive = (const uint64_t*)(e->report + report_ck_bytes(p.S));
-    p.trunk_ck = (const uint16_t*)e->report;
-    p.desync = e->desync;
-    rp.n = n_rounds;
-    rp.trunk = e->trunk;
-    rp.report_ck = (uint16_t*)e->report;
-    rp.report_bits = (uint64_t*)(e->report + report_ck_bytes(p.S));
-    rc = branch_launch_timed(e, [&] {
-      dispatch_players(p.P, [&](auto PC) {
-        constexpr int P = decltype(PC)::value;
-        rounds_kernel<P><<<grid_of(p.L, kRoundsBlock), kRoundsBlock, 0, e->stream>>>(rp);
-      });
-    }, 2 * n_rounds);
-    if (rc) return rc;
-    e->trunk_frame += n_rounds;
-    e->have_prev = true;
-    return GGRS_OK;
-  }
   for (int32_t r = 0; r < n_rounds && rc == GGRS_OK; r++) {
     rc = ggrs_branch_speculate(e);
     if (rc == GGRS_OK) rc = ggrs_branch_confirm(e, nullptr);
   }
   return rc;
+}
+
+int ggrs_branch_round(ggrs_branch_engine_t* e, void* report_device) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  if (int rc = check_rounds_queued(e, 1)) return rc;
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  return launch_rounds(e, 1, report_device);
+}
+
+int ggrs_branch_compare_peer(ggrs_branch_engine_t* e, const void* gathered, int32_t world, int32_t rank,
+                             int32_t peer, int32_t frame, int64_t* count_device, int64_t* first_frame_device) {
+  if (!e || !gathered || !count_device || !first_frame_device) return set_error(GGRS_E_INVALID, "null argument");
+  if (world < 2 || rank < 0 || rank >= world || peer < 0 || peer >= world || peer == rank)
+    return set_error(GGRS_E_INVALID, "rank %d / peer %d out of range for world %d", rank, peer, world);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const int64_t S = e->cfg.num_sessions;
+  compare_peer_kernel<<<grid_of(S, 256), 256, 0, e->stream>>>((const uint8_t*)gathered, (int64_t)e->report_bytes,
+                                                             rank, peer, S, frame,
+                                                             (unsigned long long*)count_device,
+                                                             (unsigned long long*)first_frame_device);
+  HIP_TRY(hipGetLastError());
+  return GGRS_OK;
 }
 
 int ggrs_branch_set_stream(ggrs_branch_engine_t* e, void* stream) {

@@ -113,20 +113,22 @@ class ReportExchange:
     per confirmation with no host synchronisation in the round loop.
 
     The engine runs on the caller's current stream (BranchEngine.set_stream), so per round r:
-      speculate(r)                         -- current stream
+      round(r) -> report buffer r % 2      -- one launch (speculate + confirm, ggrs_branch_round),
+                                              the kernel writing the report into the buffer
       wait for all-gather(r-1)             -- a device-side stream wait (work.wait()), after which
-                                              its desync comparison is queued on the device
-      confirm(r) -> report buffer r % 2    -- current stream (the report copy included)
+                                              its peer comparison is queued on the device
+                                              (ggrs_branch_compare_peer, one small kernel)
       all-gather(r) of that buffer         -- async on the collective's stream, which orders itself
                                               after the current stream
-    so round r's all-gather overlaps round r+1's speculation (it only needs the local trunk) and the
-    double-buffered report of round r is never overwritten before its all-gather has read it.
+    so round r-1's all-gather overlaps round r's kernel (it only needs round r-1's report), and the
+    double-buffered report of round r-1 is never overwritten before its all-gather has read it
+    (round r+1 writes it after the current stream has waited for that all-gather).
     With `peers` (rank r and rank r + world/2 run the same sessions, the two machines of each match)
     every round's session checksums are compared with the peer replica's on the device
     (compare_local_checksums_against_peers, p2p_session.rs:904-937): `desync_count` counts
     DesyncDetected events (src/lib.rs:158-167), `first_desync_round` the earliest round with one.
     Works over RCCL (device tensors) and gloo (CPU tensors, for tests; gloo's wait blocks the
-    host)."""
+    host, and the comparison runs as torch ops on the host)."""
 
     def __init__(self, engine, group=None, peers=False, keep_history=False, device=None):
         import torch
@@ -163,24 +165,28 @@ class ReportExchange:
         g = self.gathered[k]
         if self.history is not None:
             self.history.append((self.frame_of[k], g.clone()))
-        if self.peer is not None:
-            ck = 2 * self.S
-            mine = g[self.rank, :ck].view(torch.int16)
-            theirs = g[self.peer, :ck].view(torch.int16)
-            n = (mine != theirs).sum()
-            first = torch.where((n > 0) & (self.first_desync_round < 0),
-                                torch.full_like(self.first_desync_round, self.frame_of[k]), self.first_desync_round)
-            self.desync_count += n
-            self.first_desync_round.copy_(first)
+        if self.peer is None:
+            return
+        if self.nccl:
+            self.eng.compare_peer(g, self.rank, self.peer, self.frame_of[k], self.desync_count,
+                                  self.first_desync_round)
+            return
+        ck = 2 * self.S
+        mine = g[self.rank, :ck].view(torch.int16)
+        theirs = g[self.peer, :ck].view(torch.int16)
+        n = (mine != theirs).sum()
+        first = torch.where((n > 0) & (self.first_desync_round < 0),
+                            torch.full_like(self.first_desync_round, self.frame_of[k]), self.first_desync_round)
+        self.desync_count += n
+        self.first_desync_round.copy_(first)
 
     def step(self):
-        """One round: speculate, finish the previous all-gather, confirm, start this all-gather."""
+        """One round: the fused round kernel, finish the previous all-gather, start this one."""
         import torch.distributed as dist
         k = self.round % 2
-        self.eng.speculate()
-        self._finish(1 - k)
         frame = self.eng.trunk_frame()
-        self.eng.confirm_to_tensor(self.bufs[k])
+        self.eng.round_to_tensor(self.bufs[k])
+        self._finish(1 - k)
         if self.nccl:
             self.work[k] = dist.all_gather_into_tensor(self.gathered[k].view(-1), self.bufs[k], group=self.group,
                                                        async_op=True)
@@ -192,5 +198,5 @@ class ReportExchange:
 
     def drain(self):
         """Finish the last all-gather (device-side wait) -- call before reading results."""
-        self._finish(0)
-        self._finish(1)
+        self._finish(self.round % 2)
+        self._finish(1 - self.round % 2)

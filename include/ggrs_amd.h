@@ -297,6 +297,17 @@ int ggrs_branch_set_round_launches(ggrs_branch_engine_t* eng, int32_t on);
  * synchronisation (multi-GPU configs 3/4, ggrs_amd/exchange.py ReportExchange).  Work queued
  * before the switch is ordered before work queued after it. */
 int ggrs_branch_set_stream(ggrs_branch_engine_t* eng, void* stream);
+/* One round (speculate + confirm) as one launch; the round's report is also written to
+ * report_device (device pointer, same layout as ggrs_branch_confirm's copy; NULL = none) by the
+ * kernel itself -- the per-round call of the multi-GPU exchange loop. */
+int ggrs_branch_round(ggrs_branch_engine_t* eng, void* report_device);
+/* Desync detection between peer replicas (compare_local_checksums_against_peers,
+ * p2p_session.rs:904-937): `gathered` = world all-gathered reports ([world][report_bytes], device);
+ * sessions whose checksum differs between rows `rank` and `peer` are added to *count_device
+ * (device int64), and *first_frame_device (device int64, initialise to -1) takes `frame` if it is
+ * still -1 and any differ.  Enqueued on the engine's stream, no host synchronisation. */
+int ggrs_branch_compare_peer(ggrs_branch_engine_t* eng, const void* gathered, int32_t world, int32_t rank,
+                             int32_t peer, int32_t frame, int64_t* count_device, int64_t* first_frame_device);
 
 /* ---------------------------------------------------------------------------------------------
  * Config-5 large-state stress game (defined by this build; ggrs_amd/csrc/particles.h):

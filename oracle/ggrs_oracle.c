@@ -878,6 +878,139 @@ int oracle_p2p_replay(int32_t P, const uint8_t* state_in, int32_t load_frame, in
 }
 
 
+/* ---------------------------------------------------------------- speculative branches, CPU
+ * CPU baseline of configs 3/4 (ggrs_amd/csrc/branch.hip): what the reference spends to evaluate B
+ * speculated remote-input branches of a session -- B rollbacks P2PSession::adjust_gamestate
+ * (p2p_session.rs:658-714) from the trunk frame f_c over W frames, each branch's request list
+ * [Load f_c, Advance, (Save, Advance) x (W-1), Save f_c+W] (:698-702, :337) executed by the
+ * ex_game handler (ex_game.rs:79-127), then the confirmation: [Load f_c, Advance(truth), Save
+ * f_c+1] into the new trunk.  Branch inputs as branch.hip: local players their confirmed input,
+ * the first remote player digit k of b in base A (held at E-1 past E), other remote players
+ * repeat their last confirmed input.  Each thread runs its own sessions (own SyncLayer, inputs
+ * from splitmix64 seeded seed + session); *digest = xor of every trunk checksum.  Returns logical
+ * resimulated session-frames over all threads (rounds x sessions x (B W + 1)), -1 on failure. */
+typedef struct {
+  int32_t P, W, A, E, B, sessions, rounds, model;
+  uint32_t remote_mask; uint64_t seed;
+  int64_t frames; uint16_t digest; int failed;
+  pthread_barrier_t* bar; double t0, t1;
+} BranchJob;
+
+static void* branch_worker(void* a) {
+  BranchJob* j = (BranchJob*)a;
+  const int32_t P = j->P, W = j->W, S = j->sessions;
+  int32_t first_remote = -1;
+  for (int32_t q = 0; q < P; q++) if ((j->remote_mask >> q) & 1u) { first_remote = q; break; }
+  const int32_t F = j->rounds + 1;
+  uint8_t* truth = (uint8_t*)malloc((size_t)S * F * P);
+  SyncLayer* sls = (SyncLayer*)calloc((size_t)S, sizeof(SyncLayer));
+  Game g; memset(&g, 0, sizeof g);
+  g.desync_frame = -1;
+  state_new(&g.game_state, (uint64_t)P);
+  RequestVec rv = {0};
+  for (int32_t s = 0; s < S; s++) {
+    oracle_gen_inputs(j->seed + (uint64_t)s, F, P, j->model, truth + (size_t)s * F * P);
+    sl_new(&sls[s], (size_t)P, (size_t)W, PREDICT_REPEAT_LAST);
+    State st; state_new(&st, (uint64_t)P);   /* the trunk's cell of frame 0 */
+    state_free(&g.game_state); g.game_state = st;
+    rv.n = 0; rv_push(&rv, sl_save_current_state(&sls[s]));
+    game_handle_requests(&g, &sls[s], &rv, 0);
+  }
+  pthread_barrier_wait(j->bar);
+  j->t0 = now_s();
+  int64_t frames = 0;
+  uint16_t digest = 0;
+  for (int32_t r = 0; r < j->rounds; r++) {
+    for (int32_t s = 0; s < S; s++) {
+      SyncLayer* sl = &sls[s];
+      const int32_t fc = r;
+      const uint8_t* tin = truth + ((size_t)s * F + fc) * P;
+      const uint8_t* last = fc > 0 ? tin - P : NULL;
+      for (int32_t b = 0; b < j->B; b++) {
+        rv.n = 0;
+        sl->current_frame = fc + W;  /* the session has run W frames past the trunk */
+        rv_push(&rv, sl_load_frame(sl, fc));
+        for (int32_t k = 0; k < W; k++) {
+          Request adv; memset(&adv, 0, sizeof adv); adv.kind = REQ_ADVANCE;
+          const int32_t kk = k < j->E ? k : j->E - 1;
+          uint32_t digit = (uint32_t)b;
+          for (int32_t q = 0; q < kk; q++) digit /= (uint32_t)j->A;
+          digit %= (uint32_t)j->A;
+          for (int32_t q = 0; q < P; q++) {
+            /* local players: confirmed inputs of f_c + k (a bounded sample: inputs past the last
+               generated frame repeat it) */
+            const int32_t fk = fc + k < F ? fc + k : F - 1;
+            if (!((j->remote_mask >> q) & 1u)) adv.inputs[q] = truth[((size_t)s * F + fk) * P + q];
+            else if (q == first_remote && j->B > 1) adv.inputs[q] = (uint8_t)digit;
+            else adv.inputs[q] = last ? last[q] : 0;
+          }
+          if (k > 0) rv_push(&rv, sl_save_current_state(sl));
+          sl->current_frame += 1;
+          rv_push(&rv, adv);
+        }
+        rv_push(&rv, sl_save_current_state(sl));
+        game_handle_requests(&g, sl, &rv, 0);
+      }
+      /* confirm: the true inputs of f_c replace the speculation in the trunk */
+      rv.n = 0;
+      sl->current_frame = fc + 1;
+      rv_push(&rv, sl_load_frame(sl, fc));
+      Request adv; memset(&adv, 0, sizeof adv); adv.kind = REQ_ADVANCE;
+      for (int32_t q = 0; q < P; q++) adv.inputs[q] = tin[q];
+      sl->current_frame += 1;
+      rv_push(&rv, adv);
+      rv_push(&rv, sl_save_current_state(sl));
+      game_handle_requests(&g, sl, &rv, 0);
+      digest ^= g.last_checksum;
+      frames += (int64_t)j->B * W + 1;
+    }
+  }
+  j->t1 = now_s();
+  j->frames = frames;
+  j->digest = digest;
+  free(rv.v);
+  state_free(&g.game_state);
+  for (int32_t s = 0; s < S; s++) sl_free(&sls[s]);
+  free(sls);
+  free(truth);
+  return NULL;
+}
+
+int64_t oracle_branch_bench(int32_t P, int32_t W, int32_t A, int32_t B, uint32_t remote_mask, int32_t sessions,
+                            int32_t rounds, int32_t threads, int32_t model, uint64_t seed, double* wall,
+                            uint16_t* digest) {
+  if (P < 1 || P > MAX_PLAYERS || W < 1 || A < 2 || B < 1 || sessions < 1 || rounds < 1) return -1;
+  int32_t E = 0;
+  if (B > 1) {
+    int64_t v = 1;
+    while (v < B) { v *= A; E++; }
+    if (v != B || E > W) return -1;
+  }
+  if (threads < 1) threads = 1;
+  BranchJob* jobs = (BranchJob*)calloc((size_t)threads, sizeof(BranchJob));
+  pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+  pthread_barrier_t bar; pthread_barrier_init(&bar, NULL, (unsigned)threads);
+  for (int t = 0; t < threads; t++) {
+    BranchJob* j = &jobs[t];
+    j->P = P; j->W = W; j->A = A; j->E = E; j->B = B; j->sessions = sessions; j->rounds = rounds;
+    j->model = model; j->remote_mask = remote_mask; j->seed = seed + (uint64_t)t * (uint64_t)sessions;
+    j->bar = &bar;
+    pthread_create(&th[t], NULL, branch_worker, j);
+  }
+  int64_t total = 0; double t0 = 1e300, t1 = 0; uint16_t dg = 0;
+  for (int t = 0; t < threads; t++) {
+    pthread_join(th[t], NULL);
+    total += jobs[t].frames; dg ^= jobs[t].digest;
+    if (jobs[t].t0 < t0) t0 = jobs[t].t0;
+    if (jobs[t].t1 > t1) t1 = jobs[t].t1;
+  }
+  pthread_barrier_destroy(&bar);
+  free(jobs); free(th);
+  if (wall) *wall = t1 - t0;
+  if (digest) *digest = dg;
+  return total;
+}
+
 /* ---------------------------------------------------------------- P2PSession
  * One peer's P2PSession::advance_frame (p2p_session.rs:265-426) in rollback mode (max_prediction
  * > 0, sparse saving off, no spectators, desync detection off, every player connected) under a

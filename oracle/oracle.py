@@ -107,6 +107,10 @@ def lib():
         L.oracle_p2p_replay.argtypes = [ctypes.c_int32, u8p, ctypes.c_int32, ctypes.c_int32,
                                          ctypes.c_int32, u8p, u8p, u8p, u16p, u8p]
         L.oracle_p2p_replay.restype = ctypes.c_int
+        i32 = ctypes.c_int32
+        L.oracle_branch_bench.argtypes = [i32, i32, i32, i32, ctypes.c_uint32, i32, i32, i32, i32,
+                                          ctypes.c_uint64, P(ctypes.c_double), u16p]
+        L.oracle_branch_bench.restype = ctypes.c_int64
         L.oracle_particles_synctest_run.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                                      ctypes.c_int32, ctypes.c_uint64, ctypes.c_int32,
                                                      u8p, ctypes.c_int32, u16p, u8p, i32p, u16p, u8p,
@@ -397,6 +401,21 @@ def synctest_bench(threads, frames, warmup=1000, num_players=2, max_prediction=8
     if n < 0:
         raise RuntimeError("oracle bench session failed")
     return int(n), wall.value, ck
+
+
+def branch_bench(num_players, window, alphabet, branches, remote_mask, sessions, rounds, threads,
+                 model=MODEL_HELD, seed=0x6767525300000000):
+    """CPU baseline of configs 3/4: B rollback replays of W frames per session per round plus the
+    trunk confirmation, through the SyncLayer + ex_game handler (oracle_branch_bench), `sessions`
+    sessions on each of `threads` threads.  Returns (logical resimulated frames, wall seconds,
+    xor of every trunk checksum)."""
+    wall = ctypes.c_double(0)
+    dg = np.zeros(1, np.uint16)
+    n = lib().oracle_branch_bench(num_players, window, alphabet, branches, remote_mask, sessions, rounds,
+                                  threads, model, seed, ctypes.byref(wall), _ptr(dg, ctypes.c_uint16))
+    if n < 0:
+        raise ValueError("bad branch bench arguments")
+    return int(n), wall.value, int(dg[0])
 
 
 # ---------------------------------------------------------------- input wire codec (codec.c)

@@ -1,7 +1,15 @@
-//! A GGRS request handler for L box-game sessions that run in lockstep (same request kinds and
-//! frames, different inputs): it replaces `Game::handle_requests` of examples/ex_game/ex_game.rs
-//! (:79-127).  Saves keep the state in HBM and hand GGRS `cell.save(frame, None, Some(checksum))`
-//! (data = None is legal; GGRS only reads frame() and checksum(), src/sync_layer.rs:72-78).
+//! A GGRS request handler for L box-game sessions on one MI355X: it replaces `Game::handle_requests`
+//! of examples/ex_game/ex_game.rs (:79-127) for every session at once.  Saves keep the state in HBM
+//! and hand GGRS `cell.save(frame, None, Some(checksum))` (data = None is legal; GGRS only reads
+//! frame() and checksum(), src/sync_layer.rs:72-78).
+//!
+//! Every session's request list is its own (P2PSession::advance_frame rolls back to each session's
+//! own first_incorrect frame, p2p_session.rs:322-337,658-714), so `handle_requests` hands the engine
+//! one list per lane: encoded into the engine's mapped lane batch (ggrs_lane_batch_run: request
+//! kinds as 2-bit tokens, Load frames, input rows, checksums back in the same pinned memory), or,
+//! when a list exceeds the batch limits, through the generic CSR form (ggrs_handle_requests_lanes).
+//! `handle_requests_lockstep` is the one-list-for-all form for sessions known to be in lockstep; it
+//! checks that assumption and returns an error instead of misaligning lanes when it does not hold.
 pub mod ffi;
 
 use ffi::*;
@@ -19,10 +27,28 @@ pub trait InputByte {
     fn input_byte(&self) -> u8;
 }
 
+fn status_byte(st: &InputStatus) -> u8 {
+    match st {
+        InputStatus::Confirmed => GGRS_STATUS_CONFIRMED,
+        InputStatus::Predicted => GGRS_STATUS_PREDICTED,
+        InputStatus::Disconnected => GGRS_STATUS_DISCONNECTED,
+    }
+}
+
+/// Lanes whose request list failed the engine's validation (a Load of a frame its cell does not
+/// hold, a Save of a frame other than the state's: where the reference panics).  Those lanes were
+/// left untouched; every other lane ran and its saves were delivered.
+#[derive(Debug)]
+pub struct FailedLanes {
+    /// (lane, index of the first rejected request in its list)
+    pub lanes: Vec<(usize, usize)>,
+}
+
 pub struct BatchedBoxGame {
     eng: *mut ggrs_engine_t,
     lanes: usize,
     players: usize,
+    batch: Option<ggrs_lane_batch_t>,
 }
 
 impl BatchedBoxGame {
@@ -41,47 +67,228 @@ impl BatchedBoxGame {
         };
         let mut eng = std::ptr::null_mut();
         check(unsafe { ggrs_engine_create(&cfg, &mut eng) })?;
-        Ok(Self { eng, lanes, players })
+        Ok(Self { eng, lanes, players, batch: None })
     }
 
-    /// `requests[l]` is session l's request list from its `advance_frame()`.
-    pub fn handle_requests<T>(&mut self, requests: &[Vec<GgrsRequest<T>>]) -> Result<(), EngineError>
+    /// `requests[l]` is session l's request list from its `advance_frame()`; lists may differ in
+    /// kinds, frames and length.  Ok(None) when every lane ran; Ok(Some(failed)) when some lanes'
+    /// lists were rejected (those lanes did not run).
+    pub fn handle_requests<T>(&mut self, requests: &[Vec<GgrsRequest<T>>]) -> Result<Option<FailedLanes>, EngineError>
+    where
+        T: Config,
+        T::Input: InputByte,
+    {
+        assert_eq!(requests.len(), self.lanes);
+        // shape of the batch: the largest per-lane counts
+        let (mut nt, mut nl, mut na, mut ns) = (0usize, 0usize, 0usize, 0usize);
+        for list in requests {
+            let (mut l, mut a, mut s) = (0, 0, 0);
+            for r in list {
+                match r {
+                    GgrsRequest::SaveGameState { .. } => s += 1,
+                    GgrsRequest::LoadGameState { .. } => l += 1,
+                    GgrsRequest::AdvanceFrame { .. } => a += 1,
+                }
+            }
+            nt = nt.max(list.len());
+            nl = nl.max(l);
+            na = na.max(a);
+            ns = ns.max(s);
+        }
+        let tpw = GGRS_TOKENS_PER_WORD as usize;
+        let words = (nt + 1 + tpw - 1) / tpw; // room for the END token
+        if words > GGRS_BATCH_MAX_WORDS as usize || nl > GGRS_BATCH_MAX_LOADS as usize
+            || na > GGRS_BATCH_MAX_ADV as usize || ns > GGRS_BATCH_MAX_SAVES as usize {
+            return self.handle_requests_csr(requests);
+        }
+        let (w, ld, a, s) = (words.max(1), nl.max(1), na.max(1), ns.max(1));
+        let b = self.map_batch(w as i32, ld as i32, a as i32, s as i32)?;
+        let (l_n, p_n) = (self.lanes, self.players);
+        unsafe {
+            for (lane, list) in requests.iter().enumerate() {
+                let mut tok = vec![0u32; w];
+                let (mut k, mut li, mut ai) = (0usize, 0usize, 0usize);
+                for r in list {
+                    let t = match r {
+                        GgrsRequest::SaveGameState { .. } => GGRS_TOK_SAVE,
+                        GgrsRequest::LoadGameState { frame, .. } => {
+                            *b.load_frames.add(li * l_n + lane) = *frame;
+                            li += 1;
+                            GGRS_TOK_LOAD
+                        }
+                        GgrsRequest::AdvanceFrame { inputs } => {
+                            for (p, (inp, st)) in inputs.iter().enumerate() {
+                                *b.inputs.add((ai * l_n + lane) * p_n + p) = inp.input_byte();
+                                *b.status.add((ai * l_n + lane) * p_n + p) = status_byte(st);
+                            }
+                            ai += 1;
+                            GGRS_TOK_ADVANCE
+                        }
+                    };
+                    tok[k / tpw] |= t << (2 * (k % tpw));
+                    k += 1;
+                }
+                while k < w * tpw {
+                    tok[k / tpw] |= GGRS_TOK_END << (2 * (k % tpw));
+                    k += 1;
+                }
+                for (i, v) in tok.iter().enumerate() {
+                    *b.tokens.add(i * l_n + lane) = *v;
+                }
+            }
+        }
+        let mut run = b;
+        run.token_words = w as i32;
+        run.load_slots = ld as i32;
+        run.adv_rows = a as i32;
+        run.save_rows = s as i32;
+        let mut n_failed = 0i32;
+        let rc = unsafe { ggrs_lane_batch_run(self.eng, &run, GGRS_BATCH_STATUS, &mut n_failed) };
+        if rc != GGRS_OK && rc != GGRS_E_PRECONDITION {
+            return Err(EngineError(rc, last_error()));
+        }
+        // every Save's checksum back to its GameStateCell, lane by lane; failed lanes report
+        let mut failed = Vec::new();
+        for (lane, list) in requests.iter().enumerate() {
+            let res = unsafe { *b.lane_result.add(lane) };
+            if res < 0 {
+                failed.push((lane, (-res - 1) as usize));
+                continue;
+            }
+            let mut si = 0usize;
+            for r in list {
+                if let GgrsRequest::SaveGameState { cell, frame } = r {
+                    let cs = unsafe { *b.checksums.add(si * l_n + lane) };
+                    cell.save(*frame, None, Some(cs as u128));
+                    si += 1;
+                }
+            }
+        }
+        Ok(if failed.is_empty() { None } else { Some(FailedLanes { lanes: failed }) })
+    }
+
+    fn map_batch(&mut self, w: i32, ld: i32, a: i32, s: i32) -> Result<ggrs_lane_batch_t, EngineError> {
+        if let Some(b) = self.batch {
+            if b.token_words >= w && b.load_slots >= ld && b.adv_rows >= a && b.save_rows >= s {
+                return Ok(b);
+            }
+        }
+        let (w, ld, a, s) = match self.batch {
+            Some(b) => (w.max(b.token_words), ld.max(b.load_slots), a.max(b.adv_rows), s.max(b.save_rows)),
+            None => (w, ld, a, s),
+        };
+        let mut out = ggrs_lane_batch_t {
+            token_words: 0, load_slots: 0, adv_rows: 0, save_rows: 0,
+            tokens: std::ptr::null_mut(), load_frames: std::ptr::null_mut(), inputs: std::ptr::null_mut(),
+            status: std::ptr::null_mut(), checksums: std::ptr::null_mut(), lane_result: std::ptr::null_mut(),
+        };
+        check(unsafe { ggrs_lane_batch_map(self.eng, w, ld, a, s, &mut out) })?;
+        self.batch = Some(out);
+        Ok(out)
+    }
+
+    /// The generic per-lane form (ggrs_handle_requests_lanes): any list length.
+    pub fn handle_requests_csr<T>(&mut self, requests: &[Vec<GgrsRequest<T>>]) -> Result<Option<FailedLanes>, EngineError>
     where
         T: Config,
         T::Input: InputByte,
     {
         assert_eq!(requests.len(), self.lanes);
         let mut reqs = Vec::new();
+        let mut offsets = vec![0i32];
+        let mut inputs = Vec::new();
+        let mut status = Vec::new();
+        let mut n_saves = 0usize;
+        for list in requests {
+            for r in list {
+                match r {
+                    GgrsRequest::SaveGameState { frame, .. } => {
+                        reqs.push(ggrs_request_t { kind: GGRS_REQ_SAVE, frame: *frame });
+                        n_saves += 1;
+                    }
+                    GgrsRequest::LoadGameState { frame, .. } => {
+                        reqs.push(ggrs_request_t { kind: GGRS_REQ_LOAD, frame: *frame })
+                    }
+                    GgrsRequest::AdvanceFrame { inputs: v } => {
+                        reqs.push(ggrs_request_t { kind: GGRS_REQ_ADVANCE, frame: 0 });
+                        for (inp, st) in v {
+                            inputs.push(inp.input_byte());
+                            status.push(status_byte(st));
+                        }
+                    }
+                }
+            }
+            offsets.push(reqs.len() as i32);
+        }
+        let mut cks = vec![0u16; n_saves.max(1)];
+        let mut result = vec![0i32; self.lanes];
+        let rc = unsafe {
+            ggrs_handle_requests_lanes(self.eng, reqs.as_ptr(), offsets.as_ptr(), inputs.as_ptr(), status.as_ptr(),
+                                       cks.as_mut_ptr(), result.as_mut_ptr())
+        };
+        if rc != GGRS_OK && rc != GGRS_E_PRECONDITION {
+            return Err(EngineError(rc, last_error()));
+        }
+        let mut failed = Vec::new();
+        let mut k = 0usize;
+        for (lane, list) in requests.iter().enumerate() {
+            let ok = result[lane] >= 0;
+            if !ok {
+                failed.push((lane, (-result[lane] - 1) as usize));
+            }
+            for r in list {
+                if let GgrsRequest::SaveGameState { cell, frame } = r {
+                    if ok {
+                        cell.save(*frame, None, Some(cks[k] as u128));
+                    }
+                    k += 1;
+                }
+            }
+        }
+        Ok(if failed.is_empty() { None } else { Some(FailedLanes { lanes: failed }) })
+    }
+
+    /// One list for every lane (ggrs_handle_requests: one launch, the lists' kinds and frames
+    /// shared).  Valid only for sessions in lockstep: a lane whose kinds or frames differ from
+    /// lane 0's is an error (GGRS_E_INVALID), nothing runs.  An engine that has run per-lane lists
+    /// keeps per-lane frames and refuses this form (GGRS_E_STATE).
+    pub fn handle_requests_lockstep<T>(&mut self, requests: &[Vec<GgrsRequest<T>>]) -> Result<(), EngineError>
+    where
+        T: Config,
+        T::Input: InputByte,
+    {
+        assert_eq!(requests.len(), self.lanes);
+        let shape = |r: &GgrsRequest<T>| match r {
+            GgrsRequest::SaveGameState { frame, .. } => (GGRS_REQ_SAVE, *frame),
+            GgrsRequest::LoadGameState { frame, .. } => (GGRS_REQ_LOAD, *frame),
+            GgrsRequest::AdvanceFrame { .. } => (GGRS_REQ_ADVANCE, 0),
+        };
+        let lead: Vec<(i32, i32)> = requests[0].iter().map(shape).collect();
+        for (lane, list) in requests.iter().enumerate().skip(1) {
+            if list.len() != lead.len() || list.iter().map(shape).zip(lead.iter()).any(|(a, b)| a != *b) {
+                return Err(EngineError(GGRS_E_INVALID,
+                                       format!("lane {lane}'s request list differs from lane 0's: not in lockstep")));
+            }
+        }
+        let mut reqs = Vec::new();
         let mut inputs = Vec::new();
         let mut status = Vec::new();
         let mut saves = Vec::new();
-        for (k, r) in requests[0].iter().enumerate() {
-            match r {
-                GgrsRequest::SaveGameState { frame, .. } => {
-                    reqs.push(ggrs_request_t { kind: GGRS_REQ_SAVE, frame: *frame });
-                    saves.push((k, *frame));
-                }
-                GgrsRequest::LoadGameState { frame, .. } => {
-                    reqs.push(ggrs_request_t { kind: GGRS_REQ_LOAD, frame: *frame })
-                }
-                GgrsRequest::AdvanceFrame { .. } => {
-                    reqs.push(ggrs_request_t { kind: GGRS_REQ_ADVANCE, frame: 0 });
-                    for lane in requests {
-                        if let GgrsRequest::AdvanceFrame { inputs: v } = &lane[k] {
-                            for (inp, st) in v {
-                                inputs.push(inp.input_byte());
-                                status.push(match st {
-                                    InputStatus::Confirmed => GGRS_STATUS_CONFIRMED,
-                                    InputStatus::Predicted => GGRS_STATUS_PREDICTED,
-                                    InputStatus::Disconnected => GGRS_STATUS_DISCONNECTED,
-                                });
-                            }
+        for (k, &(kind, frame)) in lead.iter().enumerate() {
+            reqs.push(ggrs_request_t { kind, frame });
+            if kind == GGRS_REQ_SAVE {
+                saves.push((k, frame));
+            } else if kind == GGRS_REQ_ADVANCE {
+                for lane in requests {
+                    if let GgrsRequest::AdvanceFrame { inputs: v } = &lane[k] {
+                        for (inp, st) in v {
+                            inputs.push(inp.input_byte());
+                            status.push(status_byte(st));
                         }
                     }
                 }
             }
         }
-        debug_assert_eq!(inputs.len() % (self.lanes * self.players), 0);
         check(unsafe {
             ggrs_handle_requests(self.eng, reqs.as_ptr(), reqs.len() as i32, inputs.as_ptr(), status.as_ptr())
         })?;
@@ -108,6 +315,13 @@ impl BatchedBoxGame {
         check(unsafe { ggrs_read_mismatches(self.eng, st.as_mut_ptr(), fr.as_mut_ptr(), mask.as_mut_ptr()) })?;
         // GgrsError::MismatchedChecksum per halted lane: (lane, current_frame, mismatched mask)
         Ok((0..self.lanes).filter(|&l| st[l] == GGRS_LANE_MISMATCH).map(|l| (l, fr[l], mask[l])).collect())
+    }
+
+    /// Every lane's current frame (after per-lane lists).
+    pub fn lane_frames(&mut self) -> Result<Vec<i32>, EngineError> {
+        let mut out = vec![0i32; self.lanes];
+        check(unsafe { ggrs_read_lane_frames(self.eng, out.as_mut_ptr()) })?;
+        Ok(out)
     }
 }
 

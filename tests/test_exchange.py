@@ -155,8 +155,8 @@ def test_p2p_reports_between_peers_gloo(world):
 
 
 class FakeBranchEngine:
-    """The parts of BranchEngine a ReportExchange drives: speculate / confirm_to_tensor /
-    trunk_frame and the report shape.  Reports are a deterministic function of (frame, rank):
+    """The parts of BranchEngine a ReportExchange drives: round_to_tensor / trunk_frame and the
+    report shape.  Reports are a deterministic function of (frame, rank):
     session checksums agree between peer replicas except a corrupted session from `corrupt`
     on; survival words differ per rank.  `log` records the call order."""
 
@@ -164,9 +164,6 @@ class FakeBranchEngine:
         self.num_sessions, self.num_lanes = S, L
         self.report_bytes = exchange.report_layout(S, L)[2]
         self.rank, self.frame, self.corrupt, self.log = rank, 0, corrupt, []
-
-    def speculate(self):
-        self.log.append(("speculate", self.frame))
 
     def trunk_frame(self):
         return self.frame
@@ -177,8 +174,8 @@ class FakeBranchEngine:
             c = self.corrupt[0]
         return fake_report(rank, frame, c)
 
-    def confirm_to_tensor(self, t):
-        self.log.append(("confirm", self.frame))
+    def round_to_tensor(self, t):
+        self.log.append(("round", self.frame))
         t.copy_(torch.from_numpy(self.expected(self.rank, self.frame)))
         self.frame += 1
 
@@ -195,9 +192,8 @@ def report_exchange_worker(rank, world, port, out):
         for _ in range(rounds):
             ex.step()
         ex.drain()
-        # call order: round r's confirm after its speculate, each round's speculate before the
-        # previous round's all-gather is consumed
-        assert eng.log == [x for r in range(rounds) for x in (("speculate", r), ("confirm", r))]
+        # one fused round call per round, in order
+        assert eng.log == [("round", r) for r in range(rounds)]
         # every round's gathered reports, in round order, hold every rank's report
         assert [f for f, _ in ex.history] == list(range(rounds))
         for f, g in ex.history:

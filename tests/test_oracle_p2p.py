@@ -173,3 +173,25 @@ def test_lockstep_mode(oracle, delay, latency):
 
 def calls_of(out, frames):
     return calls(out, frames)
+
+
+def test_branch_bench_trunk_is_the_confirmed_chain(oracle):
+    """oracle_branch_bench (the configs 3/4 CPU baseline) keeps every session's trunk on the
+    confirmed inputs: the xor of its trunk checksums is the chain State::advance gives, and its
+    frame count is rounds x sessions x (B W + 1)."""
+    P, W, S, R, T = 4, 8, 3, 10, 2
+    seed = 0x6767525300000000
+    want = 0
+    for t in range(T):
+        for s in range(S):
+            inp = o.gen_inputs(seed + t * S + s, R + 1, P, o.MODEL_HELD)
+            st = o.state_new(P)
+            for f in range(R):
+                st = o.state_advance(st, inp[f])
+                want ^= o.fletcher16(bytes(st))
+    n, wall, dg = o.branch_bench(P, W, 16, 16, 0b1110, S, R, T, seed=seed)
+    assert dg == want and n == T * S * R * (16 * W + 1)
+    n3, _, _ = o.branch_bench(2, 4, 16, 16 ** 4, 0b10, 1, 1, 1)
+    assert n3 == 16 ** 4 * 4 + 1
+    with pytest.raises(ValueError):
+        o.branch_bench(2, 4, 16, 100, 0b10, 1, 1, 1)  # not a power of the alphabet

@@ -6,7 +6,10 @@ HBM bytes follow MI355X_MICROARCH.md "HBM": FETCH_SIZE / WRITE_SIZE are KiB from
 memory-side request counters (TCC_EA0_RDREQ/WRREQ); on gfx950 FETCH_SIZE reports exactly half the
 bytes of a wide streaming read, so the corrected figure doubles it.  Both are kept.
 
-    python tools/summarize_profile.py <tag> <workload> <kernel substring> [last K dispatches]
+    python tools/summarize_profile.py <tag> <workload> <kernel substring> [last K dispatches] [units]
+
+`units` (default 1): work units one launch of the kernel covers (configs 3/4: the rounds of one
+fused ggrs_branch_rounds launch); pmc_<workload>.json then holds bytes and duration per unit.
 """
 import collections
 import csv
@@ -41,8 +44,8 @@ def trace_mean_ns(path, kernel_substr, last=0):
     return sum(d) / len(d), len(d)
 
 
-def main(tag, workload, kernel="synctest_kernel", last="0"):
-    last = int(last)
+def main(tag, workload, kernel="synctest_kernel", last="0", units="1"):
+    last, units = int(last), int(units)
     src = os.path.join(ROOT, "gpurun_out", tag)
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
@@ -81,9 +84,9 @@ def main(tag, workload, kernel="synctest_kernel", last="0"):
         json.dump(out, fh, indent=1)
     if "hbm_bytes_per_launch" in out:
         with open(os.path.join(ROOT, "profiles", f"pmc_{workload}.json"), "w") as fh:
-            json.dump({"tag": tag, "kernel": kname, "hbm_bytes_per_launch": out["hbm_bytes_per_launch"],
-                       "hbm_bytes_per_launch_raw": out["hbm_bytes_per_launch_raw"],
-                       "avg_duration_ns": avg_ns,
+            json.dump({"tag": tag, "kernel": kname, "hbm_bytes_per_launch": out["hbm_bytes_per_launch"] / units,
+                       "hbm_bytes_per_launch_raw": out["hbm_bytes_per_launch_raw"] / units,
+                       "avg_duration_ns": avg_ns / units, "units_per_launch": units,
                        "valu_active_frac_of_wave_cycles": out.get("valu_active_frac_of_wave_cycles"),
                        "valu_insts_per_wave": out.get("valu_insts_per_wave"),
                        "wait_any_frac": out.get("wait_any_frac")}, fh, indent=1)
