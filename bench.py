@@ -273,14 +273,7 @@ def run_particles(args):
             parity = {"error": repr(exc)}
         cpu_baseline = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu_baseline = branch_cpu_baseline(args, c)
-        # distinct speculated states per round: branches sharing their first k digits share the
-        # state after k + 1 frames (config 3: 16 + 256 + 4096 + 65536 of the 4 x 65536 logical)
-        A = 16
-        E = 0
-        while A ** E < B:
-            E += 1
-        distinct = S * sum(min(A ** min(k + 1, E), B) for k in range(W)) + S
+            cpu_baseline = particles_cpu_baseline(args, synth, N, P, maxp, cd)
         line = {
             "metric": "resimulated session-frames/sec (node)", "value": round(value, 1),
             "unit": "session-frames/s", "n_gpus": world, "steps": args.steps, "warmup": warm,
@@ -296,7 +289,7 @@ def run_particles(args):
                          "traffic": pmc_traffic(f"config5_s{S}"),
                          "algorithmic_bytes_per_launch": bytes_launch,
                          "avg_launch_ms": round(avg_s * 1e3, 4)},
-            "cpu_baseline": None, "halted_lanes": int((st != 0).sum()), "parity": parity,
+            "cpu_baseline": cpu_baseline, "halted_lanes": int((st != 0).sum()), "parity": parity,
         }
         print(json.dumps(line))
     if dist is not None:
@@ -497,12 +490,6 @@ def run_codec(args):
                 n1, w1 = O.codec_bench(ref[:sample], pend[:sample], count[:sample], 1)
                 passes = max(1, int(10.0 / max(w1, 1e-3)))
                 n, wall = O.codec_bench(ref[:sample], pend[:sample], count[:sample], passes)
-                # config 1's own semantics (the reference's ex_game SyncTest: check_distance 7,
-                # input delay 2, max_prediction 8, uniform inputs) on the same threads
-                frames_c1 = max(args.cpu_frames // 2, total_frames)
-                n_c1, wall_c1, _ = O.synctest_bench(threads, frames_c1, warmup=0, num_players=2, max_prediction=8,
-                                                    check_distance=7, input_delay=2, model=O.MODEL_UNIFORM,
-                                                    seed_base=synth.SEED_BASE)
                 cpu_baseline = {"value": round(n / wall, 1), "unit": "packets/s", "cores": 1, "kind": "port",
                                 "sample": f"{passes} passes x {sample} packets (W {W}, B {B}), encode + decode "
                                           f"one packet at a time (oracle/codec.c)",
@@ -557,6 +544,67 @@ def branch_cpu_baseline(args, c):
             "wall_s": round(wall, 3)}
 
 
+def particles_cpu_baseline(args, synth, N, P, maxp, cd):
+    """Config 5 on the host: the particle-world SyncTest restatement (oracle_particles_synctest_run,
+    1 MB states cloned per save, checksummed per save and advance), one session per thread."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import numpy as np
+    from oracle import oracle as O
+    O.build()
+    T = cpu_threads(args)
+    frames = 3 * cd
+    rows = synth.gen_inputs(0, T, frames, P, synth.MODEL_HELD)
+    per = [np.ascontiguousarray(rows[:, t]) for t in range(T)]
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(T) as ex:
+        res = list(ex.map(lambda a: O.particles_synctest_run(a, N, P, maxp, cd, ring_states=False), per))
+    wall = time.perf_counter() - t0
+    resim = T * (frames - cd - 1) * cd  # calls f > cd each replay cd frames (sync_test_session.rs:192-217)
+    return {"value": round(resim / wall, 2), "unit": "session-frames/s", "cores": T, "kind": "port",
+            "sample": f"{T} threads x {frames} SyncTest frames of one {N}-entity session each (cd {cd}, "
+                      "the first cd + 1 frames without rollback), C restatement oracle_particles_synctest_run",
+            "wall_s": round(wall, 3), "all_ok": all(r["rc"] == 0 for r in res)}
+
+
+def requests_cpu_baseline(args, synth, P, maxp, cd):
+    """The request boundary on the host: ex_game's handler restatement (oracle_handler_run: Save =
+    clone + bincode + fletcher16, Load = clone, Advance = State::advance + checksum) over one
+    session's SyncTest request lists per thread -- what the Rust handler does per session without
+    this engine."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import numpy as np
+    from oracle import oracle as O
+    O.build()
+    T = cpu_threads(args)
+    frames = 300_000
+    inputs = np.stack([O.gen_inputs(synth.SEED_BASE + t, frames, P, O.MODEL_HELD) for t in range(T)], 1)
+    # the request stream of SyncTestSession::advance_frame (sync_test_session.rs:85-150), delay 0
+    # one input row per request (read by the Advances only); calls f <= cd: [Save f, Advance f],
+    # calls f > cd: [Load f-cd, Advance, (Save, Advance) x (cd-1), Save f, Advance]: request 2i is
+    # the Load / Save of frame g = f-cd+i, request 2i+1 the Advance of frame g
+    head = np.repeat(np.arange(cd + 1), 2)
+    g = np.arange(cd + 1, frames)[:, None] - cd + np.arange(cd + 1)[None, :]
+    even = np.zeros(cd + 1, np.int32)
+    even[0] = 1
+    kinds = np.concatenate([np.tile([0, 2], cd + 1),
+                            np.stack([np.broadcast_to(even, g.shape), np.full(g.shape, 2)], -1).ravel()]).astype(np.int32)
+    fr = np.concatenate([np.stack([np.arange(cd + 1), np.zeros(cd + 1, int)], -1).ravel(),
+                         np.stack([g, np.zeros_like(g)], -1).ravel()]).astype(np.int32)
+    idx = np.concatenate([head, np.repeat(g.ravel(), 2)]).astype(np.int64)
+    streams = [np.ascontiguousarray(inputs[idx, t]) for t in range(T)]
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(T) as ex:
+        res = list(ex.map(lambda a: O.handler_run(kinds, fr, a, None, P, maxp)["rc"], streams))
+    wall = time.perf_counter() - t0
+    resim = T * (frames - cd - 1) * cd
+    return {"value": round(resim / wall, 1), "unit": "session-frames/s", "cores": T, "kind": "port",
+            "sample": f"{T} threads x one session's {frames} SyncTest request lists (cd {cd}) through the "
+                      "ex_game handler restatement (oracle_handler_run)",
+            "wall_s": round(wall, 3), "all_ok": all(r == 0 for r in res)}
+
+
 def p2p_cpu_baseline(args, O, synth, P, D, maxp):
     """The oracle's P2P session (C restatement of p2p_session.rs:265-426 + ex_game) on T host
     threads, one session per thread (ctypes drops the GIL for the call)."""
@@ -565,9 +613,7 @@ def p2p_cpu_baseline(args, O, synth, P, D, maxp):
     import numpy as np
     T = cpu_threads(args)
     frames = 2_000_000
-    rows = synth.gen_inputs(0, T, frames, P, synth.MODEL_HELD)
-    per = [np.ascontiguousarray(rows[:, t]) for t in range(T)]
-    del rows
+    per = [O.gen_inputs(synth.SEED_BASE + t, frames, P, O.MODEL_HELD) for t in range(T)]
     t0 = time.perf_counter()
     with ThreadPoolExecutor(T) as ex:
         res = list(ex.map(lambda a: O.p2p_run(a, num_players=P, local_mask=0b01, max_prediction=maxp,
@@ -621,6 +667,8 @@ def run_requests(args):
     inputs = synth.gen_inputs(rank * L, L, frames, P, synth.MODEL_HELD)  # [frames][L][P]
     form = args.req_form
     eng = Engine(L, P, maxp, cd if form == "lockstep" else 0, 0, device=local_rank, trace_capacity=0)
+    if args.no_lane_server:
+        eng.set_lane_server(False)  # one lane_requests_kernel launch per call (per-launch profiles)
     sink = np.zeros(1, np.uint64)
 
     drv = None
@@ -713,6 +761,19 @@ def run_requests(args):
                           O.synctest_run(inputs[:f, L - 1, :], P, maxp, cd, 0)["final_state"])}
         except Exception as exc:
             parity = {"error": repr(exc)}
+        cpu_baseline = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu_baseline = requests_cpu_baseline(args, synth, P, maxp, cd)
+        # the device work of one call is the SyncTest frame's Load + cd x (Advance, Save) per lane:
+        # its algorithmic HBM bytes over the call's wall time (PCIe round trip and host handler
+        # included -- the call is latency-bound, so this is far below the HBM roofline)
+        call_s = elapsed / (args.steps * calls)
+        per_call = L * bytes_per_synctest_call(P, cd)
+        roofline = {"bound": "hbm", "achieved": round(per_call / call_s / 1e9, 3), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(per_call / call_s / 1e9 / HBM_PEAK_GBS, 6),
+                    "traffic": pmc_traffic(f"requests_l{L}"), "algorithmic_bytes_per_call": per_call,
+                    "note": "per call: one PCIe round trip (lists + inputs in, checksums out) around a "
+                            "microsecond-scale kernel; latency-bound by construction"}
         print(json.dumps({
             "metric": "resimulated session-frames/sec (node), request-level boundary", "value": round(value, 1),
             "unit": "session-frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -722,10 +783,10 @@ def run_requests(args):
                                    f"every session's request list of one advance_frame (form {form}), "
                                    f"{calls} calls per step, lists and inputs from host memory, checksums "
                                    "back to host memory each call",
-                       "sessions_per_gpu": L, "req_form": form,
+                       "sessions_per_gpu": L, "req_form": form, "lane_server": not args.no_lane_server,
                        "us_per_call": round(elapsed / (args.steps * calls) * 1e6, 2),
                        "parallelism": f"sessions sharded over {world} GPU(s)"},
-            "roofline": None, "cpu_baseline": None, "parity": parity,
+            "roofline": roofline, "cpu_baseline": cpu_baseline, "parity": parity,
             "note": "latency-bound by construction (one launch and one PCIe round trip per call); the fused "
                     "ggrs_synctest_advance_frames path is the default bench"}))
     if dist is not None:
@@ -748,6 +809,7 @@ def main():
     ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=2,
                     help="BASELINE.json config: 2 = SyncTest (default), 3/4 = branch rollback, "
                          "5 = 1 MB particle-world SyncTest")
+    ap.add_argument("--no-lane-server", action="store_true", help="requests: a launch per call")
     ap.add_argument("--rounds-per-step", type=int, default=16, help="configs 3/4: rounds per step")
     ap.add_argument("--sessions", type=int, default=0, help="config 5: sessions per GPU (0 = 8192)")
     ap.add_argument("--peers", action="store_true",
@@ -854,6 +916,12 @@ def main():
                 n1, wall1, _ = O.synctest_bench(1, frames1, warmup=0, num_players=P, max_prediction=maxp,
                                                 check_distance=cd, input_delay=delay, model=O.MODEL_HELD,
                                                 seed_base=synth.SEED_BASE)
+                # config 1's own semantics (the reference's ex_game SyncTest: check_distance 7,
+                # input delay 2, max_prediction 8, uniform inputs) on the same threads
+                frames_c1 = max(args.cpu_frames // 2, total_frames)
+                n_c1, wall_c1, _ = O.synctest_bench(threads, frames_c1, warmup=0, num_players=2, max_prediction=8,
+                                                    check_distance=7, input_delay=2, model=O.MODEL_UNIFORM,
+                                                    seed_base=synth.SEED_BASE)
                 cpu_baseline = {
                     "value": round(n / wall, 1), "unit": "session-frames/s", "cores": threads,
                     "kind": "port",

@@ -33,8 +33,8 @@ def needs_build():
     return any(os.path.getmtime(f) > t for f in SOURCES + HEADERS)
 
 
-def _compile(src, extra, verbose):
-    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
+def _compile(src, extra, verbose, obj_dir=OBJ):
+    obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
     cmd = [HIPCC, *FLAGS, *extra, "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-c", "-o", obj, src]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
@@ -47,10 +47,11 @@ def build(force=False, verbose=False, out=LIB, extra=()):
     flags are for experiment builds only (tools/exp_build.sh), which write elsewhere."""
     if out == LIB and not extra and not force and not needs_build():
         return LIB
-    os.makedirs(OBJ, exist_ok=True)
+    obj_dir = OBJ if out == LIB else out + ".obj"  # experiment builds keep their own objects
+    os.makedirs(obj_dir, exist_ok=True)
     jobs = min(len(SOURCES), max(1, os.cpu_count() or 1), 16)
     with ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, list(extra), verbose), SOURCES))
+        objs = list(ex.map(lambda s: _compile(s, list(extra), verbose, obj_dir), SOURCES))
     cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out + ".tmp", *objs]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

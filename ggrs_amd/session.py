@@ -369,7 +369,10 @@ class SyncTestSession:
         self._pending[player_handle] = a
 
     def advance_frame(self):
-        """:85-150 + the handler's execution of the returned requests, on every lane."""
+        """:85-150 + the handler's execution of the returned requests, on every lane.  Error order
+        as the reference: a lane's MismatchedChecksum (:89-102) before the missing-input
+        InvalidRequest (:108-113)."""
+        self.raise_on_mismatch()
         if len(self._pending) != self.engine.num_players:
             raise InvalidRequest(-1, "Missing local input while calling advance_frame().")
         frame = np.stack([self._pending[p] for p in range(self.engine.num_players)], axis=1)[None]

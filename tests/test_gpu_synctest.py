@@ -253,3 +253,23 @@ def test_per_frame_api(oracle):
     for lane in (0, 15):
         r = oracle.synctest_run(inputs[:, lane, :], P, 8, 7, 2)
         assert bytes(sess.engine.state(lane)) == bytes(r["final_state"])
+
+
+def test_advance_frame_reports_mismatch_before_missing_input(oracle):
+    """SyncTestSession::advance_frame returns MismatchedChecksum (sync_test_session.rs:89-102)
+    before it checks for missing local input (:108-113): a lane that halted in an unchecked launch
+    is reported by the next advance_frame even when that call has no inputs; the call after it
+    (mismatch already reported) raises the missing-input InvalidRequest."""
+    from ggrs_amd import InvalidRequest, MismatchedChecksum, SessionBuilder
+    P, maxp, cd, F, lanes = 2, 8, 7, 40, 64
+    inputs = lane_inputs(oracle, 4, lanes, F, P, 0)
+    sess = (SessionBuilder().with_num_players(P).with_max_prediction_window(maxp).with_check_distance(cd)
+            .with_num_lanes(lanes).with_input_capacity(F + 16).start_synctest_session())
+    sess.engine.corrupt_on_load(5, 20)
+    sess.add_local_inputs(inputs)
+    sess.advance_frames(F, check=False)
+    with pytest.raises(MismatchedChecksum) as ei:
+        sess.advance_frame()  # no pending local input
+    assert list(ei.value.lanes) == [5]
+    with pytest.raises(InvalidRequest):
+        sess.advance_frame()
