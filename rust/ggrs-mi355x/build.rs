@@ -14,6 +14,7 @@ fn main() {
         .arg("-I").arg(&csrc)
         .arg("-o").arg(&lib)
         .arg(csrc.join("engine.hip"))
+        .arg(csrc.join("requests.hip"))
         .arg(csrc.join("branch.hip"))
         .arg(csrc.join("particles.hip"))
         .arg(csrc.join("p2p.hip"))

@@ -80,6 +80,11 @@ def main(tag, workload, kernel="synctest_kernel", last="0", units="1"):
     if gr.get("GRBM_GUI_ACTIVE"):
         # effective clock ~= GRBM_GUI_ACTIVE / 8 (summed over XCDs) / kernel time
         out["effective_clock_ghz"] = gr["GRBM_GUI_ACTIVE"] / 8 / avg_ns
+    if sq.get("SQ_INSTS_VALU"):
+        # VALU issue fraction: wave-instructions x 2 cycles (a wave64 VALU op occupies its SIMD for
+        # 2 cycles at best, MI355X_MICROARCH.md) over the chip's SIMD-cycles during the kernel
+        clk = out.get("effective_clock_ghz") or 2.4
+        out["valu_issue_frac"] = sq["SQ_INSTS_VALU"] * 2 / (1024 * avg_ns * clk)
     with open(os.path.join(dst, "summary.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     if "hbm_bytes_per_launch" in out:
@@ -89,6 +94,7 @@ def main(tag, workload, kernel="synctest_kernel", last="0", units="1"):
                        "avg_duration_ns": avg_ns / units, "units_per_launch": units,
                        "valu_active_frac_of_wave_cycles": out.get("valu_active_frac_of_wave_cycles"),
                        "valu_insts_per_wave": out.get("valu_insts_per_wave"),
+                       "valu_issue_frac": out.get("valu_issue_frac"),
                        "wait_any_frac": out.get("wait_any_frac")}, fh, indent=1)
     for f in ("bench_trace.log",):
         if os.path.exists(os.path.join(src, f)):
