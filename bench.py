@@ -805,7 +805,7 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=3000000,
                     help="SyncTest frames per CPU thread (default: ~10 s of host work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--path", choices=["pipelined", "sequential"], default="pipelined",
+    ap.add_argument("--path", choices=["pipelined", "sequential", "chains", "batched"], default="pipelined",
                     help="SyncTest kernel (DESIGN.md section 3)")
     ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=2,
                     help="BASELINE.json config: 2 = SyncTest (default), 3/4 = branch rollback, "
@@ -848,7 +848,7 @@ def main():
     inputs = synth.gen_inputs(rank * lanes, lanes, total_frames, P, synth.MODEL_HELD)
     eng = Engine(lanes, P, maxp, cd, delay, input_capacity=total_frames + cd + delay + 2,
                  device=local_rank, trace_capacity=trace_cap)
-    eng.set_synctest_path({"pipelined": 0, "sequential": 1}[args.path])
+    eng.set_synctest_path({"pipelined": 0, "sequential": 1, "chains": 2, "batched": 3}[args.path])
     eng.add_local_inputs(0, inputs)  # resident in HBM before anything is timed
     eng.synchronize()
 

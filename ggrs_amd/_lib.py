@@ -21,7 +21,7 @@ NULL_FRAME = -1
 REQ_SAVE, REQ_LOAD, REQ_ADVANCE = 0, 1, 2
 STATUS_CONFIRMED, STATUS_PREDICTED, STATUS_DISCONNECTED = 0, 1, 2
 LANE_RUNNING, LANE_MISMATCH = 0, 1
-PATH_PIPELINED, PATH_SEQUENTIAL = 0, 1
+PATH_PIPELINED, PATH_SEQUENTIAL, PATH_PIPELINED_CHAINS, PATH_PIPELINED_BATCHED = 0, 1, 2, 3
 TOK_SAVE, TOK_ADVANCE, TOK_LOAD, TOK_END = 0, 1, 2, 3
 TOKENS_PER_WORD = 16
 BATCH_STATUS = 1

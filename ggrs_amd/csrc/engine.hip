@@ -530,6 +530,311 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
   if (bad && wl == __builtin_ctzll(bad)) atomicCAS(p.fail_f0, -1, p.f0);
 }
 
+// ------------------------------------------------------------------------------------------
+// Pipelined SyncTest, v5 (check_distance 8): cd chain roles per session instead of cd + 1, the
+// chains' last advance batched.  v4 gives each session K = cd + 1 roles x Pp player lanes; at cd 8
+// and two players that is 18 lanes, three sessions per wave (54 of 64 lanes busy) and 1366 waves
+// for 4096 sessions -- a third of the SIMDs then run two waves, and one SIMD's two waves take
+// ~1.32x one wave's time.  Role cd (the chain's last AdvanceFrame: the new frame, whose checksum
+// is the display checksum, ex_game.rs:121-126) is the only role whose result no other role
+// consumes, so v5 drops it from the lockstep:
+//   * roles 0..cd-1 run exactly as in v4 (same Loads, Saves, comparisons, static store offsets);
+//   * role cd-1's post-advance state (the chain's "current" frame, which role cd would advance at
+//     the next step) is stashed in LDS, one slot per step;
+//   * every 8 steps one batch sub-step advances the 8 stashed states, one per role lane (role j
+//     takes the stash of the batch's j-th step), with the input the next step would have read,
+//     and stores their display checksums; the launch's last chain also writes the current state.
+// 16 lanes per session at cd 8 / two players: four sessions per wave, 1024 waves for 4096
+// sessions, one per SIMD; the batch adds about one step's work per 8 steps.
+template <int P>
+__global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams p) {
+  constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
+  constexpr int F = state_fields(P);
+  constexpr int n_bytes = Fletcher<P>::n;
+  constexpr int CD = 8;             // check_distance this kernel is built for (the host checks)
+  constexpr int G = CD * Pp;        // lanes per session
+  constexpr int SPW = kWave / G;    // sessions per wave
+  constexpr int ROW = SPW * Pp;     // staged input bytes per frame (= 8)
+  constexpr int kB = 8;             // steps per batch (= role lanes that run it)
+  constexpr int kEntry = 32;        // stash bytes per (session, player): 5 fields, 16-B aligned
+  constexpr int kSlot = 8 * kEntry; // one step's stash (ROW entries)
+  __shared__ uint8_t lds_in[(kStageFrames + 1) * ROW];
+  __shared__ uint16_t lds_first[CD * SPW];
+  __shared__ uint32_t lds_cell[kWave * 5];
+  __shared__ __attribute__((aligned(16))) uint8_t lds_stash[2 * kB * kSlot];  // slots, then the dump
+  const int32_t failed_f0 = *p.fail_f0;
+  if (failed_f0 >= 0 && failed_f0 != p.f0) return;
+  const int wl = threadIdx.x;
+  const int R = p.R;
+  const int g = wl / G, r = wl - g * G;
+  const int j = r / Pp, pl = r - j * Pp;  // static role, player
+  const int64_t L = p.L;
+  const int64_t s0 = (int64_t)blockIdx.x * SPW;
+  const int64_t s = s0 + g;
+  const int nsess = (int)((L - s0) < SPW ? (L - s0) : SPW);
+  const bool valid = s < L && p.lane_status[s] == GGRS_LANE_RUNNING;
+  const bool owner = valid && pl < P;
+  const int64_t sl = valid ? s : 0;
+  const int plc = pl < P ? pl : 0;
+  const int base = g * G;
+  const int src_first = (base + (CD - 1) * Pp) * 4;
+  const int src_rot = (j == 0 ? wl : base + (j - 1) * Pp + pl) * 4;
+  const int kq[5] = {fld_x(P, plc), fld_y(P, plc), fld_vx(P, plc), fld_vy(P, plc), fld_rot(P, plc)};
+  const uint32_t slot_bytes = (uint32_t)(F * L * 4), ck_slot_bytes = (uint32_t)(L * 2);
+  const uint32_t ck_base = (uint32_t)((const uint8_t*)p.ring_ck - (const uint8_t*)p.ring);
+  const uint32_t first_base = (uint32_t)((const uint8_t*)p.first_ck - (const uint8_t*)p.ring);
+  const uint32_t trace_base = p.trace ? (uint32_t)((const uint8_t*)p.trace - (const uint8_t*)p.ring) : 0u;
+  const __amdgpu_buffer_rsrc_t rs_ring = make_rsrc(
+      p.ring, p.trace ? trace_base + ck_slot_bytes * (uint32_t)p.trace_cap : first_base + ck_slot_bytes * (uint32_t)R);
+  // every role is a producer (v4's roles 0..cd-1)
+  uint32_t fo[5];
+#pragma unroll
+  for (int q = 0; q < 5; q++) fo[q] = owner ? (uint32_t)((kq[q] * L + s) * 4) : kOob;
+  const uint32_t fo_frame = (valid && pl == 0) ? (uint32_t)(s * 4) : kOob;
+  const uint32_t co = (valid && pl == 0) ? ck_base + (uint32_t)(s * 2) : kOob;
+  const uint32_t co_first = (valid && pl == 0 && j == CD - 1) ? first_base + (uint32_t)(s * 2) : kOob;
+  const uint64_t cmp_lanes = __ballot(valid && pl == 0 && j <= CD - 2);
+  uint32_t wt[5];
+#pragma unroll
+  for (int q = 0; q < 5; q++) wt[q] = owner ? 2u * weights_at(n_bytes, fld_offset(P, kq[q])) : 0u;
+  const uint32_t one2 = owner ? 0x02020202u : 0u;
+  const uint32_t wf1 = pl == 0 ? 0x02020202u : 0u, wf2 = pl == 0 ? 2u * weights_at(n_bytes, 0) : 0u;
+  const uint32_t c1 = pl == 0 ? 2u * Fletcher<P>::kSum1Const : 0u;
+  const uint32_t c2 = pl == 0 ? 2u * Fletcher<P>::kSum2Const : 0u;
+  // stash addresses: role cd-1 lanes write their (session, player) entry of the step's slot, every
+  // other lane the dump (no exec-mask branch around the write); role j < 8 reads slot j in a batch
+  const uint32_t entry = (uint32_t)(g * Pp + pl) * kEntry;
+  const uint32_t stash_w = (valid && j == CD - 1) ? entry : (uint32_t)(kB * kSlot);
+  const uint32_t stash_r = (uint32_t)(j & (kB - 1)) * kSlot + entry;
+  // the batch's display-checksum store: player-0 lanes of roles 0..7, slot added per batch
+  const uint32_t co_trace = (p.trace && valid && pl == 0 && j < kB) ? trace_base + (uint32_t)(s * 2) : kOob;
+  const int32_t tcap = p.trace_cap > 0 ? p.trace_cap : 1;
+  const int32_t jm = j % tcap;
+
+  {
+    const CheckpointMap m{L, R, F, SPW, p.cur, p.ring, p.ring_ck, p.first_ck};
+    checkpoint_sessions(m, p.shadow + (int64_t)blockIdx.x * p.block_bytes, s0, nsess, wl, kWave);
+  }
+  if (failed_f0 >= 0) return;
+  const int32_t g0 = p.f0 - CD;
+  for (int q = wl; q < CD * nsess; q += kWave) {
+    const int gg = q / nsess, ss = q - gg * nsess;
+    lds_first[gg * SPW + ss] = p.first_ck[(int64_t)((g0 + gg) % R) * L + s0 + ss];
+  }
+  {
+    const uint32_t* cell = p.ring + (int64_t)(g0 % R) * F * L + sl;
+#pragma unroll
+    for (int q = 0; q < 5; q++) lds_cell[wl * 5 + q] = cell[kq[q] * L];
+  }
+  __syncthreads();
+  uint32_t w[5];
+#pragma unroll
+  for (int q = 0; q < 5; q++) w[q] = lds_cell[wl * 5 + q];
+
+  uint64_t bad = 0;
+  uint32_t pend_ck = 0, pend_first = 0;
+  uint64_t pend_lanes = 0;
+  const int32_t t_stage_end = p.f0 + p.n + CD;  // inputs are staged up to v4's last step
+  const int32_t t_end = t_stage_end - 1;        // the last step role cd-1 works in
+  const int in_lane = g * Pp + pl;
+  int32_t sr = __builtin_amdgcn_readfirstlane((g0 + 1) % R);
+  // trace slot of the current batch's first chain (f0 - (cd-1) + 8m), advanced 8 per batch
+  int32_t sb = __builtin_amdgcn_readfirstlane(p.trace_cap ? (p.f0 - (CD - 1)) % p.trace_cap : 0);
+  const int32_t sb_step = __builtin_amdgcn_readfirstlane(kB % tcap);
+  const bool corrupt_here = p.corrupt_frame >= p.f0 && p.corrupt_frame < p.f0 + p.n;
+  const uint32_t corrupt_on = (corrupt_here && s == p.corrupt_lane && pl == 0 && j == 0) ? 1u : 0u;
+  const int32_t ramp_end = min(p.f0 + CD, t_end);
+  const bool lean_ok = __all(w[4] <= kTwoPiBits);
+  const int32_t core_end = (corrupt_here || !lean_ok) ? ramp_end : max(ramp_end, p.f0 + p.n);
+  int32_t chunk0 = p.f0;  // step of the staged chunk's row 0
+
+  auto stage = [&](int32_t t) {
+    __syncthreads();
+    const int32_t gf = t - CD;
+    const int nf = (t_stage_end - t) < kStageFrames + 1 ? (t_stage_end - t) : kStageFrames + 1;
+    const int used = nsess * Pp;
+    for (int q = wl; q < nf * ROW; q += kWave) {
+      const int ff = q / ROW, b = q - ff * ROW;
+      lds_in[q] = b < used ? p.inputs[((int64_t)((gf + ff) % p.cap) * L + s0) * Pp + b] : 0;
+    }
+    chunk0 = t;
+    __syncthreads();
+  };
+
+  uint32_t acc = 0;
+  const uint32_t in_at = (uint32_t)in_lane;
+
+  auto step = [&](auto core_tag, int32_t t, uint32_t in, uint32_t slot_off) {
+    constexpr bool kCore = decltype(core_tag)::value;
+    const int32_t rel = t - p.f0;
+    const int32_t c = t - j;
+    const bool active = kCore ? valid : (valid && c >= p.f0 && c < p.f0 + p.n);
+    if (!kCore) {
+      bad |= __ballot(pend_ck != pend_first) & pend_lanes;
+      w[0] ^= (t == p.corrupt_frame) ? corrupt_on : 0u;
+    }
+    {
+      float x = __builtin_bit_cast(float, w[0]), y = __builtin_bit_cast(float, w[1]);
+      float vx = __builtin_bit_cast(float, w[2]), vy = __builtin_bit_cast(float, w[3]);
+      float rot = __builtin_bit_cast(float, w[4]);
+      if constexpr (kCore) advance_player_lean(x, y, vx, vy, rot, in);
+      else advance_player(x, y, vx, vy, rot, in);
+      w[0] = __builtin_bit_cast(uint32_t, x);
+      w[1] = __builtin_bit_cast(uint32_t, y);
+      w[2] = __builtin_bit_cast(uint32_t, vx);
+      w[3] = __builtin_bit_cast(uint32_t, vy);
+      w[4] = __builtin_bit_cast(uint32_t, rot);
+    }
+    if (kCore) acc |= pend_ck ^ pend_first;
+    const uint32_t frame1 = (uint32_t)(t - CD + 1);
+    uint32_t nx[5];
+#pragma unroll
+    for (int q = 0; q < 5; q++) nx[q] = (uint32_t)__builtin_amdgcn_ds_bpermute(src_rot, (int)w[q]);
+    // role cd-1's post-advance state for the batch (every other lane writes the dump)
+    {
+      uint8_t* st = lds_stash + stash_w + slot_off;
+      *reinterpret_cast<uint4*>(st) = make_uint4(w[0], w[1], w[2], w[3]);
+      *reinterpret_cast<uint32_t*>(st + 16) = w[4];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t d1 = dot4_u8(frame1, wf1, c1), d2 = dot4_u8(frame1, wf2, c2);
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+      d1 = dot4_u8(w[q], one2, d1);
+      d2 = dot4_u8(w[q], wt[q], d2);
+    }
+    if constexpr (Pp >= 2) {
+      d1 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d1, 0xB1, 0xF, 0xF, true);
+      d2 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d2, 0xB1, 0xF, 0xF, true);
+    }
+    if constexpr (Pp >= 4) {
+      d1 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d1, 0x4E, 0xF, 0xF, true);
+      d2 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d2, 0x4E, 0xF, 0xF, true);
+    }
+    const uint32_t ck = fletcher_from_doubled(d1, d2);
+    uint32_t first = (uint32_t)__builtin_amdgcn_ds_bpermute(src_first, (int)ck);
+    if (!kCore && rel + 1 < CD) first = lds_first[(rel + 1) * SPW + g];
+    const uint32_t sru = (uint32_t)sr;
+    auto stores = [&]() {
+      const uint32_t so = sru * slot_bytes, cso = sru * ck_slot_bytes;
+#pragma unroll
+      for (int q = 0; q < 5; q++) __builtin_amdgcn_raw_buffer_store_b32(w[q], rs_ring, fo[q], so, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(frame1, rs_ring, fo_frame, so, 0);
+      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ring, co, cso, 0);
+      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ring, co_first, cso, 0);
+    };
+    if (kCore) {
+      stores();
+      pend_lanes = cmp_lanes;
+    } else {
+      if (active) stores();
+      pend_lanes = cmp_lanes & __ballot(active);
+    }
+    pend_ck = ck;
+    pend_first = first;
+#pragma unroll
+    for (int q = 0; q < 5; q++) w[q] = nx[q];
+    sr = sr + 1 == R ? 0 : sr + 1;
+  };
+
+  // The batch over the stashes of steps tb .. tb + count - 1 (count <= 8; tb - f0 a multiple of
+  // 8): role j < count advances step tb + j's stash -- chain cb = tb + j - (cd - 1), its frame cb,
+  // with input cb, which step tb + j + 1 reads -- and stores the display checksum of frame cb + 1.
+  auto batch = [&](auto core_tag, int32_t tb, int count) {
+    constexpr bool kCore = decltype(core_tag)::value;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int32_t cb = tb + j - (CD - 1);
+    const bool act = kCore ? (valid && j < kB) : (valid && j < count && cb >= p.f0 && cb < p.f0 + p.n);
+    uint32_t v[5];
+    {
+      const uint8_t* st = lds_stash + stash_r;
+      const uint4 a = *reinterpret_cast<const uint4*>(st);
+      v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w;
+      v[4] = *reinterpret_cast<const uint32_t*>(st + 16);
+    }
+    const uint32_t in = lds_in[(uint32_t)(tb + (j & (kB - 1)) + 1 - chunk0) * ROW + in_at];
+    {
+      float x = __builtin_bit_cast(float, v[0]), y = __builtin_bit_cast(float, v[1]);
+      float vx = __builtin_bit_cast(float, v[2]), vy = __builtin_bit_cast(float, v[3]);
+      float rot = __builtin_bit_cast(float, v[4]);
+      if constexpr (kCore) advance_player_lean(x, y, vx, vy, rot, in);
+      else advance_player(x, y, vx, vy, rot, in);
+      v[0] = __builtin_bit_cast(uint32_t, x);
+      v[1] = __builtin_bit_cast(uint32_t, y);
+      v[2] = __builtin_bit_cast(uint32_t, vx);
+      v[3] = __builtin_bit_cast(uint32_t, vy);
+      v[4] = __builtin_bit_cast(uint32_t, rot);
+    }
+    const uint32_t framen = (uint32_t)(cb + 1);
+    uint32_t d1 = dot4_u8(framen, wf1, c1), d2 = dot4_u8(framen, wf2, c2);
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+      d1 = dot4_u8(v[q], one2, d1);
+      d2 = dot4_u8(v[q], wt[q], d2);
+    }
+    if constexpr (Pp >= 2) {
+      d1 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d1, 0xB1, 0xF, 0xF, true);
+      d2 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d2, 0xB1, 0xF, 0xF, true);
+    }
+    if constexpr (Pp >= 4) {
+      d1 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d1, 0x4E, 0xF, 0xF, true);
+      d2 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d2, 0x4E, 0xF, 0xF, true);
+    }
+    const uint32_t ck = fletcher_from_doubled(d1, d2);
+    int32_t ti = sb + jm;
+    ti = ti >= tcap ? ti - tcap : ti;
+    const uint32_t tro = act ? co_trace + (uint32_t)ti * ck_slot_bytes : kOob;
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ring, tro, 0, 0);
+    if (!kCore && act && cb == p.f0 + p.n - 1) {  // the launch's last call: the current state
+      uint32_t* cur = p.cur + s;
+      if (owner) {
+#pragma unroll
+        for (int q = 0; q < 5; q++) cur[kq[q] * L] = v[q];
+      }
+      if (pl == 0) cur[0] = framen;
+    }
+    sb = sb + sb_step;
+    sb = sb >= tcap ? sb - tcap : sb;
+  };
+
+  auto input_at = [&](int32_t t) -> uint32_t { return lds_in[(uint32_t)(t - chunk0) * ROW + in_at]; };
+  auto general = [&](int32_t t) {
+    const int32_t rel = t - p.f0;
+    if ((rel & (kStageFrames - 1)) == 0) stage(t);
+    step(std::false_type(), t, input_at(t), (uint32_t)(rel & (kB - 1)) * kSlot);
+    if ((rel & (kB - 1)) == kB - 1) batch(std::false_type(), t - (kB - 1), kB);
+  };
+  int32_t t = p.f0;
+  for (; t < ramp_end; ++t) general(t);
+  // core blocks of 8 steps + their batch, aligned to the batch grid
+  for (; t < core_end && ((t - p.f0) & (kB - 1)) != 0; ++t) general(t);
+  if (t + kB <= core_end) {
+    bad |= __ballot(pend_ck != pend_first) & pend_lanes;
+    pend_ck = pend_first = 0;
+    pend_lanes = cmp_lanes;
+    for (; t + kB <= core_end; t += kB) {
+      if (((t - p.f0) & (kStageFrames - 1)) == 0) stage(t);
+      const uint32_t ip = (uint32_t)(t - chunk0) * ROW + in_at;
+      uint32_t in[kB];
+#pragma unroll
+      for (int u = 0; u < kB; u++) in[u] = lds_in[ip + u * ROW];
+#pragma unroll
+      for (int u = 0; u < kB; u++) step(std::true_type(), t + u, in[u], (uint32_t)(u * kSlot));
+      batch(std::true_type(), t, kB);
+    }
+    bad |= __ballot(acc != 0) & cmp_lanes;
+  }
+  for (; t < t_end; ++t) general(t);
+  {
+    const int rem = (t_end - p.f0) & (kB - 1);
+    if (rem) batch(std::false_type(), t_end - rem, rem);
+  }
+  bad |= __ballot(pend_ck != pend_first) & pend_lanes;
+  if (bad && wl == __builtin_ctzll(bad)) atomicCAS(p.fail_f0, -1, p.f0);
+}
+
 struct RequestParams {
   int64_t L;
   int32_t R, n_reqs, trace_cap;
@@ -592,18 +897,45 @@ int ensure_staging(ggrs_engine* e, size_t bytes) {
   return GGRS_OK;
 }
 
-// The pipelined SyncTest kernel's geometry: sessions per 64-lane block (K = cd + 1 chain roles
-// times Pp player lanes per session), or 0 when a session does not fit one wavefront or a buffer
-// the kernel's descriptors address would exceed kOob (then the sequential kernel runs).
-int v4_sessions_per_block(const ggrs_engine* e) {
-  const int K = e->cfg.check_distance + 1;
-  if (e->cfg.check_distance < 2 || K * e->Pp > kWave) return 0;
+// The pipelined SyncTest kernels' geometry: sessions per 64-lane block, or 0 when a session does
+// not fit one wavefront or a buffer the kernel's descriptors address would exceed kOob (then the
+// sequential kernel runs).  v4: K = cd + 1 chain roles x Pp player lanes per session; v5 (cd 8
+// only): cd roles, the chains' last advance batched.
+bool pipe_buffers_fit(const ggrs_engine* e) {
   const uint64_t L = (uint64_t)e->cfg.num_lanes;
   const uint64_t ring_span = (uint64_t)((const uint8_t*)e->first_ck - (const uint8_t*)e->ring) + 2 * L * e->R;
   const uint64_t trace_span =
       e->trace ? (uint64_t)((const uint8_t*)e->trace - (const uint8_t*)e->ring) + 2 * L * e->cfg.trace_capacity : 0;
-  if ((uint64_t)e->F * 4 * L * e->R >= kOob || ring_span >= kOob || trace_span >= kOob) return 0;
+  return (uint64_t)e->F * 4 * L * e->R < kOob && ring_span < kOob && trace_span < kOob;
+}
+
+int v4_sessions_per_block(const ggrs_engine* e) {
+  const int K = e->cfg.check_distance + 1;
+  if (e->cfg.check_distance < 2 || K * e->Pp > kWave || !pipe_buffers_fit(e)) return 0;
   return kWave / (K * e->Pp);
+}
+
+int v5_sessions_per_block(const ggrs_engine* e) {
+  if (e->cfg.check_distance != 8 || !pipe_buffers_fit(e)) return 0;
+  return kWave / (8 * e->Pp);
+}
+
+// Which pipelined kernel a launch takes (4, 5, or 0 = sequential only).  The default picks v5
+// where it packs more sessions into a wave than v4 (cd 8: 4 vs 3 sessions at two players, 2 vs 1
+// at four).
+int pipe_kernel(const ggrs_engine* e) {
+  const int s4 = v4_sessions_per_block(e), s5 = v5_sessions_per_block(e);
+  switch (e->path) {
+    case GGRS_PATH_SEQUENTIAL: return 0;
+    case GGRS_PATH_PIPELINED_CHAINS: return s4 > 0 ? 4 : 0;
+    case GGRS_PATH_PIPELINED_BATCHED: return s5 > 0 ? 5 : (s4 > 0 ? 4 : 0);
+    default: return s5 > s4 ? 5 : (s4 > 0 ? 4 : 0);
+  }
+}
+
+int pipe_sessions_per_block(const ggrs_engine* e) {
+  const int k = pipe_kernel(e);
+  return k == 5 ? v5_sessions_per_block(e) : (k == 4 ? v4_sessions_per_block(e) : 0);
 }
 
 }  // namespace
@@ -697,9 +1029,12 @@ int ggrs_engine_create(const ggrs_config_t* cfg, ggrs_engine_t** out) {
       CTRY(hipMemsetD32Async((hipDeviceptr_t)(e->ring + (size_t)s * e->F * L), (int)GGRS_NULL_FRAME, (size_t)L,
                              e->stream));
     // the pipelined kernel's launch checkpoint: one contiguous piece per 64-lane block
-    const int spw = v4_sessions_per_block(e);
-    if (spw > 0) {
-      e->shadow_bytes = (size_t)grid_of(L, spw) * (size_t)checkpoint_block_bytes(e->R, e->F, spw);
+    size_t shadow = 0;
+    for (int spw : {v4_sessions_per_block(e), v5_sessions_per_block(e)})
+      if (spw > 0)
+        shadow = std::max(shadow, (size_t)grid_of(L, spw) * (size_t)checkpoint_block_bytes(e->R, e->F, spw));
+    if (shadow > 0) {
+      e->shadow_bytes = shadow;
       CTRY(hipMalloc(&e->shadow, e->shadow_bytes));
       CTRY(hipMemsetAsync(e->shadow, 0, e->shadow_bytes, e->stream));
     }
@@ -820,8 +1155,9 @@ static int launch_pipelined(ggrs_engine_t* e, int32_t f0, int32_t n) {
   p.L = e->cfg.num_lanes;
   p.R = e->R;
   p.cd = e->cfg.check_distance;
-  p.K = p.cd + 1;
-  p.spw = v4_sessions_per_block(e);
+  const int kernel = pipe_kernel(e);
+  p.K = kernel == 5 ? p.cd : p.cd + 1;
+  p.spw = pipe_sessions_per_block(e);
   p.f0 = f0;
   p.n = n;
   p.cap = e->cap;
@@ -841,6 +1177,15 @@ static int launch_pipelined(ggrs_engine_t* e, int32_t f0, int32_t n) {
   e->unverified = true;
   const int64_t grid = grid_of(p.L, p.spw);
   return launch_timed(e, [&] {
+    if (kernel == 5) {
+      switch (e->cfg.num_players) {
+        case 1: synctest_pipelined_v5_kernel<1><<<grid, kWave, 0, e->stream>>>(p); break;
+        case 2: synctest_pipelined_v5_kernel<2><<<grid, kWave, 0, e->stream>>>(p); break;
+        case 3: synctest_pipelined_v5_kernel<3><<<grid, kWave, 0, e->stream>>>(p); break;
+        default: synctest_pipelined_v5_kernel<4><<<grid, kWave, 0, e->stream>>>(p); break;
+      }
+      return;
+    }
     switch (e->cfg.num_players) {
       case 1: synctest_pipelined_v4_kernel<1><<<grid, kWave, 0, e->stream>>>(p); break;
       case 2: synctest_pipelined_v4_kernel<2><<<grid, kWave, 0, e->stream>>>(p); break;
@@ -862,7 +1207,7 @@ static int resolve(ggrs_engine_t* e) {
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->unverified = false;
   if (f < 0) return GGRS_OK;
-  const int spw = v4_sessions_per_block(e);
+  const int spw = pipe_sessions_per_block(e);
   const CheckpointMap m{(int64_t)e->cfg.num_lanes, e->R, e->F, spw, e->cur, e->ring, e->ring_ck, e->first_ck};
   restore_kernel<<<grid_of(e->cfg.num_lanes, spw), 256, 0, e->stream>>>(m, e->shadow,
                                                                          checkpoint_block_bytes(e->R, e->F, spw));
@@ -893,7 +1238,7 @@ int ggrs_synctest_advance_frames(ggrs_engine_t* e, int32_t n) {
   int32_t f0 = e->current_frame, left = n;
   // warm-up calls (f <= cd: no rollback yet), cd <= 1 and sessions that do not fit the pipelined
   // kernel take the sequential kernel
-  if (e->path == GGRS_PATH_SEQUENTIAL || v4_sessions_per_block(e) == 0) {
+  if (pipe_kernel(e) == 0) {
     int rc = launch_sequential(e, f0, left);
     if (rc) return rc;
     left = 0;
@@ -922,7 +1267,8 @@ int ggrs_synctest_advance_frames(ggrs_engine_t* e, int32_t n) {
 
 int ggrs_set_synctest_path(ggrs_engine_t* e, int32_t path) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
-  if (path != GGRS_PATH_PIPELINED && path != GGRS_PATH_SEQUENTIAL)
+  if (path != GGRS_PATH_PIPELINED && path != GGRS_PATH_SEQUENTIAL && path != GGRS_PATH_PIPELINED_CHAINS &&
+      path != GGRS_PATH_PIPELINED_BATCHED)
     return set_error(GGRS_E_INVALID, "unknown path %d", path);
   int rc = resolve(e);
   if (rc) return rc;

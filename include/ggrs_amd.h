@@ -69,9 +69,12 @@ extern "C" {
 #define GGRS_STATUS_DISCONNECTED 2
 
 /* SyncTest execution paths (ggrs_set_synctest_path) */
-#define GGRS_PATH_PIPELINED 0  /* default: cd+1 concurrent rollback chains per session, one lane per
-                                  (chain, player) when (cd+1) * padded players <= 64 */
+#define GGRS_PATH_PIPELINED 0  /* default: concurrent rollback chains per session, one lane per
+                                  (chain, player); picks CHAINS or BATCHED by wave packing */
 #define GGRS_PATH_SEQUENTIAL 1 /* one lane per session, calls in order */
+#define GGRS_PATH_PIPELINED_CHAINS 2  /* cd+1 chain lanes per player, when (cd+1) * padded players <= 64 */
+#define GGRS_PATH_PIPELINED_BATCHED 3 /* check_distance 8: cd chain lanes per player, the chains'
+                                         last advance batched every 8 frames (CHAINS otherwise) */
 
 /* per-lane status */
 #define GGRS_LANE_RUNNING 0
@@ -117,7 +120,8 @@ int ggrs_add_local_inputs_device(ggrs_engine_t* eng, int32_t first_frame, int32_
 int ggrs_synctest_advance_frames(ggrs_engine_t* eng, int32_t n_frames);
 /* Choose the SyncTest kernel: GGRS_PATH_PIPELINED (default; a mismatch found there is re-run on
  * the sequential kernel from a checkpoint, so results are identical; sessions whose chains do not
- * fit one wavefront run sequentially) or GGRS_PATH_SEQUENTIAL. */
+ * fit one wavefront run sequentially), one of its two forms explicitly (_CHAINS, _BATCHED), or
+ * GGRS_PATH_SEQUENTIAL. */
 int ggrs_set_synctest_path(ggrs_engine_t* eng, int32_t path);
 
 /* Execute an ordered request list on every lane (fused: one kernel launch).

@@ -24,6 +24,8 @@ pub const GGRS_STATUS_DISCONNECTED: u8 = 2;
 
 pub const GGRS_PATH_PIPELINED: i32 = 0;
 pub const GGRS_PATH_SEQUENTIAL: i32 = 1;
+pub const GGRS_PATH_PIPELINED_CHAINS: i32 = 2;
+pub const GGRS_PATH_PIPELINED_BATCHED: i32 = 3;
 
 pub const GGRS_LANE_RUNNING: i32 = 0;
 pub const GGRS_LANE_MISMATCH: i32 = 1;

@@ -22,7 +22,11 @@ def lane_inputs(O, base_seed, lanes, frames, players, model):
                      for l in range(lanes)], axis=1)  # [frames][lanes][P]
 
 
-PATHS = [0, 1]  # PIPELINED (the v4 kernel; sequential where a session's chains do not fit a wave), SEQUENTIAL
+# PIPELINED (auto: the batched v5 kernel at check_distance 8 where it packs more sessions per wave,
+# else v4; sequential where a session's chains do not fit a wave), SEQUENTIAL
+PATHS = [0, 1]
+# every kernel at check_distance 8: auto (v5), SEQUENTIAL, PIPELINED_CHAINS (v4)
+PATHS_CD8 = [0, 1, 2]
 
 
 def make_engine(lanes, P, maxp, cd, d, frames, trace=True, path=0):
@@ -57,7 +61,7 @@ def check_lane(O, eng, inputs, lane, P, maxp, cd, d, frames, trace=None):
             assert int(ck[s]) == int(r["ring_cksums"][s]) and bytes(st[s]) == bytes(r["ring_states"][s])
 
 
-@pytest.mark.parametrize("path", PATHS)
+@pytest.mark.parametrize("path", PATHS_CD8)
 @pytest.mark.parametrize("name", sorted(CASES))
 def test_golden_cases(oracle, name, path):
     c = CASES[name]
@@ -83,9 +87,11 @@ def test_golden_cases(oracle, name, path):
 
 
 @pytest.mark.parametrize("path", PATHS)
-@pytest.mark.parametrize("chunks", [[300], [1] * 20 + [280], [7, 13, 280], [150, 150]])
-def test_chunking_is_invisible(oracle, chunks, path):
-    P, maxp, cd, d, F, lanes = 2, 8, 7, 2, 300, 64
+@pytest.mark.parametrize("cd", [7, 8])
+@pytest.mark.parametrize("chunks", [[300], [1] * 20 + [280], [7, 13, 280], [150, 150], [9, 3, 5, 283]])
+def test_chunking_is_invisible(oracle, chunks, path, cd):
+    """Launch boundaries anywhere (cd 8: inside the batched kernel's 8-step batch grid too)."""
+    P, maxp, d, F, lanes = 2, cd + 1, 2, 300, 64
     inputs = lane_inputs(oracle, 77, lanes, F, P, 0)
     eng = make_engine(lanes, P, maxp, cd, d, F, path=path)
     run_chunks(eng, inputs, chunks)
@@ -116,16 +122,18 @@ def test_streamed_inputs_small_queue(oracle):
         assert bytes(eng.state(lane)) == bytes(r["final_state"])
 
 
-@pytest.mark.parametrize("path,chunk,call", [(0, 120, 40), (1, 120, 40), (0, 16, 40),
-                                             (0, 16, 48), (0, 7, 9), (1, 7, 9),
-                                             (0, 120, 110)])
-def test_mismatch_detection_matches_reference(oracle, path, chunk, call):
+@pytest.mark.parametrize("path,chunk,call,cd", [(0, 120, 40, 7), (1, 120, 40, 7), (0, 16, 40, 7),
+                                                (0, 16, 48, 7), (0, 7, 9, 7), (1, 7, 9, 7),
+                                                (0, 120, 110, 7),
+                                                (0, 120, 40, 8), (0, 16, 49, 8), (0, 7, 10, 8),
+                                                (0, 13, 57, 8), (0, 120, 110, 8), (2, 16, 49, 8)])
+def test_mismatch_detection_matches_reference(oracle, path, chunk, call, cd):
     """A non-deterministic simulation on one lane: the SyncTest must report
     MismatchedChecksum{current_frame, mismatched_frames} exactly as the reference session
     (pipelined launches detect it and are replayed on the sequential kernel from a checkpoint;
     chunk 16 puts the failure in a later launch, call 48 on a launch's first chain)."""
     from ggrs_amd import MismatchedChecksum, SessionBuilder
-    P, maxp, cd, d, F, lanes, bad_lane = 2, 8, 7, 2, 120, 70, 66
+    P, maxp, d, F, lanes, bad_lane = 2, cd + 1, 2, 120, 70, 66
     inputs = lane_inputs(oracle, 9, lanes, F, P, 0)
     sess = (SessionBuilder().with_num_players(P).with_max_prediction_window(maxp)
             .with_check_distance(cd).with_input_delay(d).with_num_lanes(lanes)
@@ -158,14 +166,15 @@ def test_mismatch_detection_matches_reference(oracle, path, chunk, call):
     check_lane(oracle, sess.engine, inputs, bad_lane - 1, P, maxp, cd, d, F)
 
 
-@pytest.mark.parametrize("lanes,bad_lane,call", [(16384, 16383, 30), (16384, 0, 30), (12000, 6001, 77)])
-def test_mismatch_restore_when_grid_exceeds_residency(oracle, lanes, bad_lane, call):
+@pytest.mark.parametrize("lanes,bad_lane,call,cd", [(16384, 16383, 30, 7), (16384, 0, 30, 7), (12000, 6001, 77, 7),
+                                                    (40000, 39999, 31, 8), (40000, 17, 77, 8)])
+def test_mismatch_restore_when_grid_exceeds_residency(oracle, lanes, bad_lane, call, cd):
     """A mismatch in a launch whose grid has more blocks than fit the chip at once: blocks
     scheduled after the failing one must still take their launch checkpoint (they used
     to skip it and be restored from a stale shadow).  Every lane other than the corrupted one ends
     in the oracle's state; the corrupted lane halts exactly as the reference's session."""
     from ggrs_amd import MismatchedChecksum, SessionBuilder
-    P, maxp, cd, d, F = 2, 8, 7, 0, 120
+    P, maxp, d, F = 2, cd + 1, 0, 120
     rng = np.random.default_rng(lanes + call)
     inputs = rng.integers(0, 16, (F, lanes, P), dtype=np.uint8)
     sess = (SessionBuilder().with_num_players(P).with_max_prediction_window(maxp).with_check_distance(cd)
@@ -184,7 +193,7 @@ def test_mismatch_restore_when_grid_exceeds_residency(oracle, lanes, bad_lane, c
         check_lane(oracle, sess.engine, inputs, lane, P, maxp, cd, d, F)
 
 
-@pytest.mark.parametrize("path", PATHS)
+@pytest.mark.parametrize("path", PATHS_CD8)
 def test_full_size_config2(oracle, path):
     """Config 2 at full size: 4096 sessions, 8-frame rollback every frame (SyncTest cd 8,
     max_prediction 9), held-key inputs; sampled lanes bit-exact."""
@@ -201,8 +210,8 @@ def test_full_size_config2(oracle, path):
     assert (st == 0).all()
 
 
-@pytest.mark.parametrize("path", PATHS)
-@pytest.mark.parametrize("lanes,P", [(67, 2), (37, 4), (10, 3)])
+@pytest.mark.parametrize("path", PATHS_CD8)
+@pytest.mark.parametrize("lanes,P", [(67, 2), (37, 4), (10, 3), (13, 1)])
 def test_ragged_last_block_every_lane(oracle, path, lanes, P):
     """Lane counts that leave the last workgroup partly empty (idle lanes there map past the
     last session): every lane's trace and final state bit-exact, across an input restage."""
