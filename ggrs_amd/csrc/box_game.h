@@ -189,34 +189,43 @@ __device__ inline double rcp_f64_refined(double d) {
 //     position sum is never -0 (x >= +0, and x + v == 0 only as +0) nor NaN.
 //   * the turn's rem_euclid on [-RS, 2pi + RS] is one add or subtract of 2pi chosen by two
 //     compares (every rot in the domain, both directions: tests/native/remeuclid_kat_host.c).
+typedef float ggrs_f2 __attribute__((ext_vector_type(2)));
 __device__ inline void advance_player_lean(float& x, float& y, float& vx, float& vy, float& rot,
                                            uint32_t input) {
-  float vel_x = vx * kFriction;
-  float vel_y = vy * kFriction;
+  // the x/y pairs go through packed f32 ops (v_pk_mul_f32 / v_pk_add_f32: two IEEE f32 ops each,
+  // the same roundings as the scalar ops)
+  ggrs_f2 vel = ggrs_f2{vx, vy} * kFriction;
   float s, c;
   glibc_sincosf_domain(rot, &s, &c);
-  const float dx = kMovementSpeed * c, dy = kMovementSpeed * s;
+  const ggrs_f2 d = ggrs_f2{c, s} * kMovementSpeed;
   const uint32_t ud = input & (kInputUp | kInputDown), lr = input & (kInputLeft | kInputRight);
   const bool thrust = ud == kInputUp, brake = ud == kInputDown;
-  vel_x = vel_x + (thrust ? dx : (brake ? -dx : -0.0f));
-  vel_y = vel_y + (thrust ? dy : (brake ? -dy : -0.0f));
+  vel = vel + ggrs_f2{thrust ? d.x : (brake ? -d.x : -0.0f), thrust ? d.y : (brake ? -d.y : -0.0f)};
   const bool ccw = lr == kInputLeft, turn = ccw || lr == kInputRight;
   const float a = rot + (ccw ? -kRotationSpeed : kRotationSpeed);
   // rem_euclid(a, 2pi) for a in [-RS, 2pi + RS] (host KAT over every rot in the domain,
   // tests/native/remeuclid_kat_host.c)
-  const float r = a < 0.0f ? a + kTwoPi : (a >= kTwoPi ? a - kTwoPi : a);
+  // (as one add of +2pi / -2pi / +0: a - 2pi == a + (-2pi), and a + 0 == a since a is never -0)
+  const float r = a + (a < 0.0f ? kTwoPi : (a >= kTwoPi ? -kTwoPi : 0.0f));
   rot = turn ? r : rot;
-  const float mag2 = vel_x * vel_x + vel_y * vel_y;
-  if (mag2 > kMaxSpeed * kMaxSpeed) {
-    const float magnitude = sqrt_rn_above_49(mag2);
-    const double r = rcp_f64_refined((double)magnitude);
-    vel_x = (float)((double)(vel_x * kMaxSpeed) * r);
-    vel_y = (float)((double)(vel_y * kMaxSpeed) * r);
+  const ggrs_f2 sq = vel * vel;
+  const float mag2 = sq.x + sq.y;
+  // the clamp is rare (a few % of player steps): a wave-uniform test skips it with one branch on
+  // VCC instead of an exec-mask save / restore around it on every step
+  const bool clamp = mag2 > kMaxSpeed * kMaxSpeed;
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(clamp) != 0, 0)) {
+    if (clamp) {
+      const float magnitude = sqrt_rn_above_49(mag2);
+      const double rr = rcp_f64_refined((double)magnitude);
+      vel.x = (float)((double)(vel.x * kMaxSpeed) * rr);
+      vel.y = (float)((double)(vel.y * kMaxSpeed) * rr);
+    }
   }
-  x = __builtin_amdgcn_fmed3f(x + vel_x, 0.0f, kWindowWidth);
-  y = __builtin_amdgcn_fmed3f(y + vel_y, 0.0f, kWindowHeight);
-  vx = vel_x;
-  vy = vel_y;
+  const ggrs_f2 pos = ggrs_f2{x, y} + vel;
+  x = __builtin_amdgcn_fmed3f(pos.x, 0.0f, kWindowWidth);
+  y = __builtin_amdgcn_fmed3f(pos.y, 0.0f, kWindowHeight);
+  vx = vel.x;
+  vy = vel.y;
 }
 
 // Dispatch (every kernel): the lean branch-free form when every active lane's rot is in the

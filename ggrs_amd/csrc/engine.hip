@@ -591,8 +591,14 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
 #pragma unroll
   for (int q = 0; q < 5; q++) fo[q] = owner ? (uint32_t)((kq[q] * L + s) * 4) : kOob;
   const uint32_t fo_frame = (valid && pl == 0) ? (uint32_t)(s * 4) : kOob;
-  const uint32_t co = (valid && pl == 0) ? ck_base + (uint32_t)(s * 2) : kOob;
-  const uint32_t co_first = (valid && pl == 0 && j == CD - 1) ? first_base + (uint32_t)(s * 2) : kOob;
+  // checksum stores: the player-0 lane writes ring_ck; with two or more player lanes the player-1
+  // lane of role cd-1 writes the same checksum (the DPP combine leaves it on both) into first_ck
+  // in the same store instruction -- both at the ring slot's index
+  constexpr bool kMergedCk = Pp >= 2;
+  const uint32_t co = (valid && pl == 0)                                ? ck_base + (uint32_t)(s * 2)
+                      : (kMergedCk && valid && pl == 1 && j == CD - 1) ? first_base + (uint32_t)(s * 2)
+                                                                        : kOob;
+  const uint32_t co_first = (!kMergedCk && valid && pl == 0 && j == CD - 1) ? first_base + (uint32_t)(s * 2) : kOob;
   const uint64_t cmp_lanes = __ballot(valid && pl == 0 && j <= CD - 2);
   uint32_t wt[5];
 #pragma unroll
@@ -687,16 +693,22 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
     }
     if (kCore) acc |= pend_ck ^ pend_first;
     const uint32_t frame1 = (uint32_t)(t - CD + 1);
+    // rotation: role j takes role j-1's state, role 0 keeps its own.  At two players a session is
+    // one 16-lane DPP row (role j = lanes 2j, 2j+1): one row_shr:2 move per field, the row's first
+    // two lanes keep their value (bound_ctrl off); otherwise one ds_bpermute per field.
+    // (the DPP moves come after the state's last use below, in place)
     uint32_t nx[5];
+    if constexpr (Pp != 2) {
 #pragma unroll
-    for (int q = 0; q < 5; q++) nx[q] = (uint32_t)__builtin_amdgcn_ds_bpermute(src_rot, (int)w[q]);
+      for (int q = 0; q < 5; q++) nx[q] = (uint32_t)__builtin_amdgcn_ds_bpermute(src_rot, (int)w[q]);
+    }
     // role cd-1's post-advance state for the batch (every other lane writes the dump)
     {
       uint8_t* st = lds_stash + stash_w + slot_off;
       *reinterpret_cast<uint4*>(st) = make_uint4(w[0], w[1], w[2], w[3]);
       *reinterpret_cast<uint32_t*>(st + 16) = w[4];
     }
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (Pp != 2) __builtin_amdgcn_sched_barrier(0);  // LDS latency behind the sums
     uint32_t d1 = dot4_u8(frame1, wf1, c1), d2 = dot4_u8(frame1, wf2, c2);
 #pragma unroll
     for (int q = 0; q < 5; q++) {
@@ -712,7 +724,10 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
       d2 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d2, 0x4E, 0xF, 0xF, true);
     }
     const uint32_t ck = fletcher_from_doubled(d1, d2);
-    uint32_t first = (uint32_t)__builtin_amdgcn_ds_bpermute(src_first, (int)ck);
+    // role cd-1's first-seen checksum to every lane of the session (two players: DPP
+    // row_newbcast of the row's lane 14)
+    uint32_t first = Pp == 2 ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ck, 0x150 + (CD - 1) * Pp, 0xF, 0xF, true)
+                             : (uint32_t)__builtin_amdgcn_ds_bpermute(src_first, (int)ck);
     if (!kCore && rel + 1 < CD) first = lds_first[(rel + 1) * SPW + g];
     const uint32_t sru = (uint32_t)sr;
     auto stores = [&]() {
@@ -721,7 +736,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
       for (int q = 0; q < 5; q++) __builtin_amdgcn_raw_buffer_store_b32(w[q], rs_ring, fo[q], so, 0);
       __builtin_amdgcn_raw_buffer_store_b32(frame1, rs_ring, fo_frame, so, 0);
       __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ring, co, cso, 0);
-      __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ring, co_first, cso, 0);
+      if constexpr (!kMergedCk) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ring, co_first, cso, 0);
     };
     if (kCore) {
       stores();
@@ -733,7 +748,8 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
     pend_ck = ck;
     pend_first = first;
 #pragma unroll
-    for (int q = 0; q < 5; q++) w[q] = nx[q];
+    for (int q = 0; q < 5; q++)
+      w[q] = Pp == 2 ? (uint32_t)__builtin_amdgcn_update_dpp((int)w[q], (int)w[q], 0x112, 0xF, 0xF, false) : nx[q];
     sr = sr + 1 == R ? 0 : sr + 1;
   };
 

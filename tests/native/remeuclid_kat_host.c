@@ -2,7 +2,8 @@
  * rot in the lean step's domain [+0, 2pi] (bits 0 .. 0x40C90FDB) and both turn directions, the
  * branch-light form
  *     a = rot -/+ ROTATION_SPEED;  r = a < 0 ? a + 2pi : (a >= 2pi ? a - 2pi : a)
- * equals the reference's f32::rem_euclid(a, 2pi) (ex_game.rs:300-306; Rust: r = a % b, then
+ * and its one-add form r = a + (a < 0 ? 2pi : (a >= 2pi ? -2pi : +0)) (what box_game.h runs)
+ * equal the reference's f32::rem_euclid(a, 2pi) (ex_game.rs:300-306; Rust: r = a % b, then
  * r < 0 ? r + |b| : r, with % = fmodf), bit for bit.  Test infrastructure, compiled and run by
  * tests/test_step_kat.py.  Prints "bad <count>". */
 #include <math.h>
@@ -43,7 +44,10 @@ static void* work(void* arg) {
     for (int dir = 0; dir < 2; dir++) {
       const float a = dir ? rot + rs : rot - rs;
       const float mine = a < 0.0f ? a + two_pi : (a >= two_pi ? a - two_pi : a);
-      n += bits(mine) != bits(rem_euclid_ref(a, two_pi));
+      const volatile float zero = 0.0f;
+      const float one_add = a + (a < 0.0f ? two_pi : (a >= two_pi ? -two_pi : zero));
+      const uint32_t ref = bits(rem_euclid_ref(a, two_pi));
+      n += (bits(mine) != ref) + (bits(one_add) != ref);
     }
   }
   bad[id] = n;
