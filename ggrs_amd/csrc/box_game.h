@@ -190,13 +190,18 @@ __device__ inline double rcp_f64_refined(double d) {
 //   * the turn's rem_euclid on [-RS, 2pi + RS] is one add or subtract of 2pi chosen by two
 //     compares (every rot in the domain, both directions: tests/native/remeuclid_kat_host.c).
 typedef float ggrs_f2 __attribute__((ext_vector_type(2)));
-__device__ inline void advance_player_lean(float& x, float& y, float& vx, float& vy, float& rot,
-                                           uint32_t input) {
+struct NoHook {
+  __device__ void operator()(float) const {}
+};
+// advance_player_lean with sin/cos of the old rot supplied by the caller, and a hook that sees the
+// new rot before the speed clamp (the v5 kernel computes the NEXT step's sin/cos there: work that
+// does not depend on this step's velocity chain, in the same basic block as it).
+template <typename Hook = NoHook>
+__device__ inline void advance_player_lean_sc(float& x, float& y, float& vx, float& vy, float& rot,
+                                              uint32_t input, float s, float c, Hook&& hook = Hook()) {
   // the x/y pairs go through packed f32 ops (v_pk_mul_f32 / v_pk_add_f32: two IEEE f32 ops each,
   // the same roundings as the scalar ops)
   ggrs_f2 vel = ggrs_f2{vx, vy} * kFriction;
-  float s, c;
-  glibc_sincosf_domain(rot, &s, &c);
   const ggrs_f2 d = ggrs_f2{c, s} * kMovementSpeed;
   const uint32_t ud = input & (kInputUp | kInputDown), lr = input & (kInputLeft | kInputRight);
   const bool thrust = ud == kInputUp, brake = ud == kInputDown;
@@ -204,10 +209,11 @@ __device__ inline void advance_player_lean(float& x, float& y, float& vx, float&
   const bool ccw = lr == kInputLeft, turn = ccw || lr == kInputRight;
   const float a = rot + (ccw ? -kRotationSpeed : kRotationSpeed);
   // rem_euclid(a, 2pi) for a in [-RS, 2pi + RS] (host KAT over every rot in the domain,
-  // tests/native/remeuclid_kat_host.c)
-  // (as one add of +2pi / -2pi / +0: a - 2pi == a + (-2pi), and a + 0 == a since a is never -0)
+  // tests/native/remeuclid_kat_host.c), as one add of +2pi / -2pi / +0: a - 2pi == a + (-2pi),
+  // and a + 0 == a since a is never -0
   const float r = a + (a < 0.0f ? kTwoPi : (a >= kTwoPi ? -kTwoPi : 0.0f));
   rot = turn ? r : rot;
+  hook(rot);
   const ggrs_f2 sq = vel * vel;
   const float mag2 = sq.x + sq.y;
   // the clamp is rare (a few % of player steps): a wave-uniform test skips it with one branch on
@@ -226,6 +232,13 @@ __device__ inline void advance_player_lean(float& x, float& y, float& vx, float&
   y = __builtin_amdgcn_fmed3f(pos.y, 0.0f, kWindowHeight);
   vx = vel.x;
   vy = vel.y;
+}
+
+__device__ inline void advance_player_lean(float& x, float& y, float& vx, float& vy, float& rot,
+                                           uint32_t input) {
+  float s, c;
+  glibc_sincosf_domain(rot, &s, &c);
+  advance_player_lean_sc(x, y, vx, vy, rot, input, s, c);
 }
 
 // Dispatch (every kernel): the lean branch-free form when every active lane's rot is in the

@@ -254,6 +254,56 @@ __device__ inline __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t by
 constexpr int kStageFrames = 256;
 constexpr int kMaxRampFrames = 64;  // first-seen checksums of frames f0-cd .. f0-1 (cd <= 62)
 
+// LDS staging of input-queue rows: frames gf .. gf + nf - 1 (queue slot (gf + ff) % cap; every
+// staged frame is held by the queue at once, so nf <= cap and the slot wraps at most once) for the
+// block's sessions [s0, s0 + nsess): row ff's first `used` = nsess * Pp bytes are the sessions'
+// input records, bytes up to `row` are zero.  Every load of a thread is issued before its LDS
+// stores, so a stage costs one memory latency (a load-wait-store loop paid one per byte).
+// Full 8-byte rows whose source is 8-byte aligned move as one 64-bit load per row.
+template <int kRow>
+__device__ inline void stage_input_rows(uint8_t* lds, const uint8_t* inputs, int64_t L, int Pp, int32_t cap,
+                                        int32_t gf, int nf, int64_t s0, int used, int row_rt, int tid) {
+  const int row = kRow > 0 ? kRow : row_rt;
+  const int32_t q0 = gf % cap;
+  auto slot = [&](int ff) {
+    const int32_t q = q0 + ff;
+    return q >= cap ? q - cap : q;
+  };
+  if (kRow == 8 && used == 8 && ((L * Pp) & 7) == 0) {
+    for (int base = 0; base < nf; base += 4 * kWave) {
+      uint64_t v[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int ff = base + u * kWave + tid;
+        if (ff < nf) v[u] = *reinterpret_cast<const uint64_t*>(inputs + ((int64_t)slot(ff) * L + s0) * Pp);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int ff = base + u * kWave + tid;
+        if (ff < nf) *reinterpret_cast<uint64_t*>(lds + ff * 8) = v[u];
+      }
+    }
+    return;
+  }
+  const int total = nf * row;
+  for (int base = 0; base < total; base += 8 * kWave) {
+    uint8_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int q = base + u * kWave + tid;
+      if (q < total) {
+        const int ff = q / row, b = q - ff * row;
+        v[u] = b < used ? inputs[((int64_t)slot(ff) * L + s0) * Pp + b] : 0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int q = base + u * kWave + tid;
+      if (q < total) lds[q] = v[u];
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Pipelined SyncTest, v4: static chain roles.  Same schedule and the same Loads, Saves and
 // AdvanceFrames as v3, re-indexed so that no lane's role changes from step to step:
@@ -387,10 +437,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
     __syncthreads();
     const int32_t gf = t - cd;
     const int nf = (t_end - t) < kStageFrames ? (t_end - t) : kStageFrames;
-    for (int q = wl; q < nf * row; q += kWave) {
-      const int ff = q / row, b = q - ff * row;
-      lds_in[ff * row + b] = p.inputs[((int64_t)((gf + ff) % p.cap) * L + s0) * Pp + b];
-    }
+    stage_input_rows<0>(lds_in, p.inputs, L, Pp, p.cap, gf, nf, s0, row, row, wl);
     __syncthreads();
   };
 
@@ -658,17 +705,16 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
     __syncthreads();
     const int32_t gf = t - CD;
     const int nf = (t_stage_end - t) < kStageFrames + 1 ? (t_stage_end - t) : kStageFrames + 1;
-    const int used = nsess * Pp;
-    for (int q = wl; q < nf * ROW; q += kWave) {
-      const int ff = q / ROW, b = q - ff * ROW;
-      lds_in[q] = b < used ? p.inputs[((int64_t)((gf + ff) % p.cap) * L + s0) * Pp + b] : 0;
-    }
+    stage_input_rows<ROW>(lds_in, p.inputs, L, Pp, p.cap, gf, nf, s0, nsess * Pp, ROW, wl);
     chunk0 = t;
     __syncthreads();
   };
 
   uint32_t acc = 0;
   const uint32_t in_at = (uint32_t)in_lane;
+  // core steps: sin/cos of the rot each lane holds at the step's start, computed one step ahead
+  // (inside the previous step, from the rotated rot, before its speed clamp)
+  float sc_s = 0.0f, sc_c = 0.0f;
 
   auto step = [&](auto core_tag, int32_t t, uint32_t in, uint32_t slot_off) {
     constexpr bool kCore = decltype(core_tag)::value;
@@ -683,8 +729,17 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
       float x = __builtin_bit_cast(float, w[0]), y = __builtin_bit_cast(float, w[1]);
       float vx = __builtin_bit_cast(float, w[2]), vy = __builtin_bit_cast(float, w[3]);
       float rot = __builtin_bit_cast(float, w[4]);
-      if constexpr (kCore) advance_player_lean(x, y, vx, vy, rot, in);
-      else advance_player(x, y, vx, vy, rot, in);
+      if constexpr (kCore) {
+        // the next step's rot is this lane's new rot rotated one role up (role 0 keeps its own)
+        advance_player_lean_sc(x, y, vx, vy, rot, in, sc_s, sc_c, [&](float rn) {
+          const uint32_t rb = __builtin_bit_cast(uint32_t, rn);
+          const uint32_t nb = Pp == 2 ? (uint32_t)__builtin_amdgcn_update_dpp((int)rb, (int)rb, 0x112, 0xF, 0xF, false)
+                                      : (uint32_t)__builtin_amdgcn_ds_bpermute(src_rot, (int)rb);
+          glibc_sincosf_domain(__builtin_bit_cast(float, nb), &sc_s, &sc_c);
+        });
+      } else {
+        advance_player(x, y, vx, vy, rot, in);
+      }
       w[0] = __builtin_bit_cast(uint32_t, x);
       w[1] = __builtin_bit_cast(uint32_t, y);
       w[2] = __builtin_bit_cast(uint32_t, vx);
@@ -830,6 +885,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
     bad |= __ballot(pend_ck != pend_first) & pend_lanes;
     pend_ck = pend_first = 0;
     pend_lanes = cmp_lanes;
+    glibc_sincosf_domain(__builtin_bit_cast(float, w[4]), &sc_s, &sc_c);
     for (; t + kB <= core_end; t += kB) {
       if (((t - p.f0) & (kStageFrames - 1)) == 0) stage(t);
       const uint32_t ip = (uint32_t)(t - chunk0) * ROW + in_at;
