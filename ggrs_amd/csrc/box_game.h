@@ -234,6 +234,69 @@ __device__ inline void advance_player_lean_sc(float& x, float& y, float& vx, flo
   vy = vel.y;
 }
 
+// One player's input decoded for advance_player_rec: everything the step derives from Input.inp
+// (ex_game.rs:283-309), computed once per (frame, session, player) when the input is staged and
+// shared by every chain that replays the frame (the v5 SyncTest kernel replays each frame 9 times).
+//   delta: the turn's f32 addend (-RS, +RS) or +0.0 without a turn;
+//   thr:   the wrap threshold, 2pi with a turn, +inf without (a non-turning rot of exactly 2pi must
+//          stay 2pi: ex_game only applies rem_euclid when it turns);
+//   sgn:   0 (thrust), 0x80000000 (brake: the increment's sign flips), or 0x80000000 (neither:
+//          the increment is -0.0, see below);
+//   keep:  0xffffffff with thrust or brake, 0 without.
+struct InputRec {
+  uint32_t delta, thr, sgn, keep;
+};
+__host__ __device__ inline InputRec make_input_rec(uint32_t input) {
+  const uint32_t ud = input & (kInputUp | kInputDown), lr = input & (kInputLeft | kInputRight);
+  const bool thrust = ud == kInputUp, brake = ud == kInputDown;
+  const bool ccw = lr == kInputLeft, cw = lr == kInputRight;
+  InputRec r;
+  r.delta = ccw ? __builtin_bit_cast(uint32_t, -kRotationSpeed) : (cw ? __builtin_bit_cast(uint32_t, kRotationSpeed) : 0u);
+  r.thr = (ccw || cw) ? __builtin_bit_cast(uint32_t, kTwoPi) : 0x7f800000u;
+  r.sgn = thrust ? 0u : 0x80000000u;
+  r.keep = (thrust || brake) ? 0xffffffffu : 0u;
+  return r;
+}
+
+// advance_player_lean_sc from a staged InputRec, with the same IEEE results:
+//   * velocity increment (thrust ? d : brake ? -d : -0.0f) as bit operations:
+//     keep ? d ^ sgn : sgn, i.e. v_bfi(keep, d ^ sgn, sgn) -- with sgn = 0x80000000 and keep = 0
+//     the increment is -0.0 exactly as the select form;
+//   * turn: a = rot + delta (rot + 0.0 == rot: rot is never -0 in the domain), then
+//     r = a + (a < 0 ? 2pi : (a >= thr ? -2pi : +0)): without a turn a = rot <= 2pi < thr = inf
+//     and r = rot + 0 == rot; with a turn it is the one-add rem_euclid of advance_player_lean_sc.
+template <typename Hook = NoHook>
+__device__ inline void advance_player_rec(float& x, float& y, float& vx, float& vy, float& rot, const InputRec& in,
+                                          float s, float c, Hook&& hook = Hook()) {
+  ggrs_f2 vel = ggrs_f2{vx, vy} * kFriction;
+  const ggrs_f2 d = ggrs_f2{c, s} * kMovementSpeed;
+  // (elements copied out first: __builtin_bit_cast of an ext_vector element lvalue read element 0
+  // for both -- seen with this image's hipcc, caught by the device KAT)
+  const float dx = d.x, dy = d.y;
+  const uint32_t ix = ((__builtin_bit_cast(uint32_t, dx) ^ in.sgn) & in.keep) | (in.sgn & ~in.keep);
+  const uint32_t iy = ((__builtin_bit_cast(uint32_t, dy) ^ in.sgn) & in.keep) | (in.sgn & ~in.keep);
+  vel = vel + ggrs_f2{__builtin_bit_cast(float, ix), __builtin_bit_cast(float, iy)};
+  const float a = rot + __builtin_bit_cast(float, in.delta);
+  rot = a + (a < 0.0f ? kTwoPi : (a >= __builtin_bit_cast(float, in.thr) ? -kTwoPi : 0.0f));
+  hook(rot);
+  const ggrs_f2 sq = vel * vel;
+  const float mag2 = sq.x + sq.y;
+  const bool clamp = mag2 > kMaxSpeed * kMaxSpeed;
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(clamp) != 0, 0)) {
+    if (clamp) {
+      const float magnitude = sqrt_rn_above_49(mag2);
+      const double rr = rcp_f64_refined((double)magnitude);
+      vel.x = (float)((double)(vel.x * kMaxSpeed) * rr);
+      vel.y = (float)((double)(vel.y * kMaxSpeed) * rr);
+    }
+  }
+  const ggrs_f2 pos = ggrs_f2{x, y} + vel;
+  x = __builtin_amdgcn_fmed3f(pos.x, 0.0f, kWindowWidth);
+  y = __builtin_amdgcn_fmed3f(pos.y, 0.0f, kWindowHeight);
+  vx = vel.x;
+  vy = vel.y;
+}
+
 __device__ inline void advance_player_lean(float& x, float& y, float& vx, float& vy, float& rot,
                                            uint32_t input) {
   float s, c;

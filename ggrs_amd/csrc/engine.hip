@@ -605,7 +605,11 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
   constexpr int kB = 8;             // steps per batch (= role lanes that run it)
   constexpr int kEntry = 32;        // stash bytes per (session, player): 5 fields, 16-B aligned
   constexpr int kSlot = 8 * kEntry; // one step's stash (ROW entries)
-  __shared__ uint8_t lds_in[(kStageFrames + 1) * ROW];
+  // inputs staged kStage5 frames at a time (+1 slack row for the batch's look-ahead): the raw
+  // bytes (non-core steps) and their decoded InputRec (core steps), one per (frame, session, player)
+  constexpr int kStage5 = 128;
+  __shared__ uint8_t lds_in[(kStage5 + 1) * ROW];
+  __shared__ uint4 lds_rec[(kStage5 + 1) * ROW];
   __shared__ uint16_t lds_first[CD * SPW];
   __shared__ uint32_t lds_cell[kWave * 5];
   __shared__ __attribute__((aligned(16))) uint8_t lds_stash[2 * kB * kSlot];  // slots, then the dump
@@ -704,9 +708,14 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
   auto stage = [&](int32_t t) {
     __syncthreads();
     const int32_t gf = t - CD;
-    const int nf = (t_stage_end - t) < kStageFrames + 1 ? (t_stage_end - t) : kStageFrames + 1;
+    const int nf = (t_stage_end - t) < kStage5 + 1 ? (t_stage_end - t) : kStage5 + 1;
     stage_input_rows<ROW>(lds_in, p.inputs, L, Pp, p.cap, gf, nf, s0, nsess * Pp, ROW, wl);
     chunk0 = t;
+    __syncthreads();
+    for (int q = wl; q < nf * ROW; q += kWave) {
+      const InputRec r = make_input_rec(lds_in[q]);
+      lds_rec[q] = make_uint4(r.delta, r.thr, r.sgn, r.keep);
+    }
     __syncthreads();
   };
 
@@ -716,7 +725,9 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
   // (inside the previous step, from the rotated rot, before its speed clamp)
   float sc_s = 0.0f, sc_c = 0.0f;
 
-  auto step = [&](auto core_tag, int32_t t, uint32_t in, uint32_t slot_off) {
+  auto rec_of = [](const uint4 v) { return InputRec{v.x, v.y, v.z, v.w}; };
+  // core steps take the staged InputRec, non-core steps the raw input byte
+  auto step = [&](auto core_tag, int32_t t, auto in, uint32_t slot_off) {
     constexpr bool kCore = decltype(core_tag)::value;
     const int32_t rel = t - p.f0;
     const int32_t c = t - j;
@@ -731,14 +742,14 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
       float rot = __builtin_bit_cast(float, w[4]);
       if constexpr (kCore) {
         // the next step's rot is this lane's new rot rotated one role up (role 0 keeps its own)
-        advance_player_lean_sc(x, y, vx, vy, rot, in, sc_s, sc_c, [&](float rn) {
+        advance_player_rec(x, y, vx, vy, rot, rec_of(in), sc_s, sc_c, [&](float rn) {
           const uint32_t rb = __builtin_bit_cast(uint32_t, rn);
           const uint32_t nb = Pp == 2 ? (uint32_t)__builtin_amdgcn_update_dpp((int)rb, (int)rb, 0x112, 0xF, 0xF, false)
                                       : (uint32_t)__builtin_amdgcn_ds_bpermute(src_rot, (int)rb);
           glibc_sincosf_domain(__builtin_bit_cast(float, nb), &sc_s, &sc_c);
         });
       } else {
-        advance_player(x, y, vx, vy, rot, in);
+        advance_player(x, y, vx, vy, rot, (uint32_t)in);
       }
       w[0] = __builtin_bit_cast(uint32_t, x);
       w[1] = __builtin_bit_cast(uint32_t, y);
@@ -825,13 +836,18 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
       v[0] = a.x, v[1] = a.y, v[2] = a.z, v[3] = a.w;
       v[4] = *reinterpret_cast<const uint32_t*>(st + 16);
     }
-    const uint32_t in = lds_in[(uint32_t)(tb + (j & (kB - 1)) + 1 - chunk0) * ROW + in_at];
+    const uint32_t ri = (uint32_t)(tb + (j & (kB - 1)) + 1 - chunk0) * ROW + in_at;
     {
       float x = __builtin_bit_cast(float, v[0]), y = __builtin_bit_cast(float, v[1]);
       float vx = __builtin_bit_cast(float, v[2]), vy = __builtin_bit_cast(float, v[3]);
       float rot = __builtin_bit_cast(float, v[4]);
-      if constexpr (kCore) advance_player_lean(x, y, vx, vy, rot, in);
-      else advance_player(x, y, vx, vy, rot, in);
+      if constexpr (kCore) {
+        float bs, bc;
+        glibc_sincosf_domain(rot, &bs, &bc);
+        advance_player_rec(x, y, vx, vy, rot, rec_of(lds_rec[ri]), bs, bc);
+      } else {
+        advance_player(x, y, vx, vy, rot, lds_in[ri]);
+      }
       v[0] = __builtin_bit_cast(uint32_t, x);
       v[1] = __builtin_bit_cast(uint32_t, y);
       v[2] = __builtin_bit_cast(uint32_t, vx);
@@ -873,7 +889,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
   auto input_at = [&](int32_t t) -> uint32_t { return lds_in[(uint32_t)(t - chunk0) * ROW + in_at]; };
   auto general = [&](int32_t t) {
     const int32_t rel = t - p.f0;
-    if ((rel & (kStageFrames - 1)) == 0) stage(t);
+    if ((rel & (kStage5 - 1)) == 0) stage(t);
     step(std::false_type(), t, input_at(t), (uint32_t)(rel & (kB - 1)) * kSlot);
     if ((rel & (kB - 1)) == kB - 1) batch(std::false_type(), t - (kB - 1), kB);
   };
@@ -887,11 +903,11 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
     pend_lanes = cmp_lanes;
     glibc_sincosf_domain(__builtin_bit_cast(float, w[4]), &sc_s, &sc_c);
     for (; t + kB <= core_end; t += kB) {
-      if (((t - p.f0) & (kStageFrames - 1)) == 0) stage(t);
+      if (((t - p.f0) & (kStage5 - 1)) == 0) stage(t);
       const uint32_t ip = (uint32_t)(t - chunk0) * ROW + in_at;
-      uint32_t in[kB];
+      uint4 in[kB];
 #pragma unroll
-      for (int u = 0; u < kB; u++) in[u] = lds_in[ip + u * ROW];
+      for (int u = 0; u < kB; u++) in[u] = lds_rec[ip + u * ROW];
 #pragma unroll
       for (int u = 0; u < kB; u++) step(std::true_type(), t + u, in[u], (uint32_t)(u * kSlot));
       batch(std::true_type(), t, kB);

@@ -101,13 +101,24 @@ __global__ void lean_step_kernel(uint64_t seed, int iters, unsigned long long* b
     for (uint32_t in = 0; in < 16; in++) {
       float x1 = x, y1 = y, vx1 = vx, vy1 = vy, r1 = rot;
       float x2 = x, y2 = y, vx2 = vx, vy2 = vy, r2 = rot;
+      float x3 = x, y3 = y, vx3 = vx, vy3 = vy, r3 = rot;
       ggrs::advance_player_domain(x1, y1, vx1, vy1, r1, in);
       ggrs::advance_player_lean(x2, y2, vx2, vy2, r2, in);
+      {  // the staged-record form of the v5 SyncTest kernel
+        float s, c;
+        ggrs::glibc_sincosf_domain(r3, &s, &c);
+        ggrs::advance_player_rec(x3, y3, vx3, vy3, r3, ggrs::make_input_rec(in), s, c);
+      }
       local += (__builtin_bit_cast(uint32_t, x1) != __builtin_bit_cast(uint32_t, x2)) |
                (__builtin_bit_cast(uint32_t, y1) != __builtin_bit_cast(uint32_t, y2)) |
                (__builtin_bit_cast(uint32_t, vx1) != __builtin_bit_cast(uint32_t, vx2)) |
                (__builtin_bit_cast(uint32_t, vy1) != __builtin_bit_cast(uint32_t, vy2)) |
                (__builtin_bit_cast(uint32_t, r1) != __builtin_bit_cast(uint32_t, r2));
+      local += ((__builtin_bit_cast(uint32_t, x1) != __builtin_bit_cast(uint32_t, x3)) |
+                (__builtin_bit_cast(uint32_t, y1) != __builtin_bit_cast(uint32_t, y3)) |
+                (__builtin_bit_cast(uint32_t, vx1) != __builtin_bit_cast(uint32_t, vx3)) |
+                (__builtin_bit_cast(uint32_t, vy1) != __builtin_bit_cast(uint32_t, vy3)) |
+                (__builtin_bit_cast(uint32_t, r1) != __builtin_bit_cast(uint32_t, r3))) << 20;
     }
   }
   for (int off = 32; off > 0; off >>= 1) local += __shfl_down(local, off, 64);
