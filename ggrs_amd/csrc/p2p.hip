@@ -376,6 +376,7 @@ constexpr int kFlatBlock = 64;
 // rows per stage: a wave's steps in a stage are its slowest session's, so fewer, longer stages
 // cost less (128 rows: one stage per 64-call launch at back = 6)
 constexpr int kFlatRows = 128;
+constexpr int kFlatRowsLds = 64;  // with the LDS ring: 28 + 8 KB per block, four blocks per CU
 
 template <int P>
 struct LdsRowsFlat {
@@ -395,11 +396,21 @@ struct LdsRowsFlat {
 // kSparse: sparse saving (p2p_session.rs:666-702,819-843), as p2p_kernel does it: a rollback
 // loads the last save and saves only min_confirmed while replaying; before the call's own step,
 // check_last_saved_state either saves the current frame or replays again from the last save.
-template <int P, int kLocal, bool kPlain, bool kSparse>
+// kLds: the block's 64 session rings live in LDS for the launch (dynamic shared memory,
+// [R][pieces][64 lanes] uint4: a save is three conflict-free ds_write_b128, a rollback's load three
+// ds_read_b128); they are copied in from the HBM ring at the start and back at the end, so the HBM
+// ring is exact between launches.  A ring cell is only ever read by its own session's thread, so
+// the launch needs no other exchange.  Saves no longer go to HBM as partial lines (the PMC traffic
+// of the HBM-ring form was 1.7x its algorithmic bytes, nearly all WRITE_SIZE), and the rollback
+// cell needs no prefetch.  Used when R x cell fits 28 KB per block (four blocks per CU).
+template <int P, int kLocal, bool kPlain, bool kSparse, bool kLds>
 __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
   const uint32_t lmask = kLocal >= 0 ? (uint32_t)kLocal : p.local_mask;
   constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
-  __shared__ __attribute__((aligned(16))) uint8_t lds_rows[kFlatRows * kFlatBlock * Pp];
+  constexpr int kRows = kLds ? kFlatRowsLds : kFlatRows;
+  constexpr int PC = cell_dwords(P) / 4;  // 16-byte pieces per cell
+  __shared__ __attribute__((aligned(16))) uint8_t lds_rows[kRows * kFlatBlock * Pp];
+  extern __shared__ uint4 lds_ring[];  // kLds: [R][PC][kFlatBlock]
   const int64_t sess0 = (int64_t)blockIdx.x * kFlatBlock;
   const int64_t S = p.S;
   const bool live = sess0 + threadIdx.x < S;
@@ -426,12 +437,66 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
   uint4* const my_ring = reinterpret_cast<uint4*>(p.ring + (int64_t)sess * p.R * cell_dwords(P));
   auto cell = [&](int32_t slot) { return my_ring + slot * (cell_dwords(P) / 4); };
   auto next_slot = [&](int32_t x) { return x + 1 == p.R ? 0 : x + 1; };
+  // the ring cell of `slot`: HBM (session-major) or this lane's LDS column (piece stride 64)
+  const int lt = threadIdx.x;  // LDS column: idle threads keep their own, unused one
+  auto cell_load = [&](BoxState<P>& dst, int32_t slot) {
+    if constexpr (kLds) {
+      constexpr int F = state_fields(P);
+#pragma unroll
+      for (int k = 0; k < PC; k++) {
+        const uint4 v = lds_ring[(slot * PC + k) * kFlatBlock + lt];
+        const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          if (4 * k + i < F) dst.w[4 * k + i] = x[i];
+      }
+    } else {
+      load_cell<P>(dst, cell(slot));
+    }
+  };
+  auto cell_store = [&](const BoxState<P>& src, uint32_t ck, int32_t slot) {
+    if constexpr (kLds) {
+      constexpr int F = state_fields(P);
+#pragma unroll
+      for (int k = 0; k < PC; k++) {
+        uint32_t x[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) x[i] = 4 * k + i < F ? src.w[4 * k + i] : (4 * k + i == F ? ck : 0u);
+        lds_ring[(slot * PC + k) * kFlatBlock + lt] = make_uint4(x[0], x[1], x[2], x[3]);
+      }
+    } else {
+      store_cell<P>(src, ck, cell(slot));
+    }
+  };
+  auto cell_ck = [&](int32_t slot) -> uint16_t {
+    if constexpr (kLds) {
+      constexpr int F = state_fields(P);
+      const uint4 v = lds_ring[(slot * PC + F / 4) * kFlatBlock + lt];
+      const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+      return (uint16_t)x[F % 4];
+    } else {
+      return cell_checksum<P>(p, slot, sess);
+    }
+  };
+  // kLds: the block's rings into LDS (HBM pieces are contiguous per block: coalesced reads)
+  const int ring_pieces = p.R * PC;
+  if constexpr (kLds) {
+    const int n = nb * ring_pieces;
+    const uint4* src = reinterpret_cast<const uint4*>(p.ring) + sess0 * ring_pieces;
+#pragma unroll 4
+    for (int i = lt; i < n; i += kFlatBlock) {
+      const int sl = i / ring_pieces, rem = i - sl * ring_pieces;
+      lds_ring[rem * kFlatBlock + sl] = src[i];
+    }
+    __syncthreads();
+  }
   int32_t slot_f = p.f0 % p.R, slot_h = 0, pre_slot = 0;
   int32_t last_saved = kSparse ? p.last_saved[sess] : kNull;
   int32_t saved_slot = (kSparse && last_saved >= 0) ? last_saved % p.R : 0;
   auto save = [&](int32_t h, int32_t slot) {  // SaveGameState(h) into its cell
+    if (kLds) cell_store(st, fletcher16_state<P>(st), slot);  // idle threads: their own column
     if (live) {
-      store_cell<P>(st, fletcher16_state<P>(st), cell(slot));
+      if (!kLds) cell_store(st, fletcher16_state<P>(st), slot);
       if (kSparse) p.ring_frame[(int64_t)slot * S + sess] = h;  // GameStateCell.frame
     }
     if constexpr (kSparse) {
@@ -445,7 +510,7 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
   int32_t pre_frame = kNull;
   // prefetch(fr, slot): fr = f + 1 - D with 1 <= D < R, so its slot is slot_f + 1 - D mod R
   auto prefetch = [&](int32_t fr, int32_t slot) {
-    if (!kSparse && fr >= 0) {
+    if (!kSparse && !kLds && fr >= 0) {  // (an LDS cell is read where the rollback happens)
       load_cell<P>(pre, cell(slot));
       pre_frame = fr;
       pre_slot = slot;
@@ -460,7 +525,7 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
   // here instead of one per player per step (a foreign state takes the general step throughout)
   const bool lean_ok = __all(rot_in_domain<P>(st) && (pre_frame == kNull || rot_in_domain<P>(pre)));
   const int32_t f_end = p.f0 + p.n;
-  const int32_t calls_per_stage = kFlatRows - back;  // >= 1 (host)
+  const int32_t calls_per_stage = kRows - back;  // >= 1 (host)
   for (int32_t fs = p.f0; fs < f_end;) {
     const int32_t chunk_end = min(f_end, fs + calls_per_stage);
     const int32_t lo = max(0, fs - back);
@@ -492,13 +557,13 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
       load = from;
       if (kSparse) {
         slot_h = saved_slot;
-        load_cell<P>(st, cell(slot_h));
-      } else if (load == pre_frame) {
+        cell_load(st, slot_h);
+      } else if (!kLds && load == pre_frame) {
         st = pre;
         slot_h = pre_slot;
       } else {
         slot_h = load % p.R;
-        load_cell<P>(st, cell(slot_h));
+        cell_load(st, slot_h);
       }
 #pragma unroll
       for (int k = 0; k < P; k++) {  // reset_prediction (input_queue.rs:63-67)
@@ -525,7 +590,7 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
         if (!kPlain && p.desync_interval > 0 && live) {
           const int32_t fts = f - 1 - p.D;
           if (fts >= p.desync_interval && fts % p.desync_interval == 0)
-            p.hist[(int64_t)((fts / p.desync_interval) % kHist) * S + sess] = cell_checksum<P>(p, fts % p.R, sess);
+            p.hist[(int64_t)((fts / p.desync_interval) % kHist) * S + sess] = cell_ck(fts % p.R);
         }
         // 1. poll_remote_clients: the remote input of frame g = f - D (add_input_by_frame)
         const int32_t g = f - p.D;
@@ -582,6 +647,24 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
       }
     }
     fs = chunk_end;
+  }
+  if constexpr (kLds) {  // the rings back to HBM
+    __syncthreads();
+    const int n = nb * ring_pieces;
+    uint4* dst = reinterpret_cast<uint4*>(p.ring) + sess0 * ring_pieces;
+    for (int i = lt; i < n; i += kFlatBlock) {
+      const int sl = i / ring_pieces, rem = i - sl * ring_pieces;
+      dst[i] = lds_ring[rem * kFlatBlock + sl];
+    }
+  }
+  if constexpr (kLds) {  // the rings back to HBM
+    __syncthreads();
+    const int n = nb * ring_pieces;
+    uint4* dst = reinterpret_cast<uint4*>(p.ring) + sess0 * ring_pieces;
+    for (int i = lt; i < n; i += kFlatBlock) {
+      const int sl = i / ring_pieces, rem = i - sl * ring_pieces;
+      dst[i] = lds_ring[rem * kFlatBlock + sl];
+    }
   }
   if (!live) return;
   store_state<P>(st, p.cur + sess, S);
@@ -938,20 +1021,31 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
       constexpr int P = decltype(PC)::value;
       if (flat) {
         const dim3 grid((unsigned)grid_of(p.S, kFlatBlock));
-        auto go = [&](auto plain_tag) {
+        // the LDS ring when the block's rings fit 28 KB and a stage of 64 rows holds a call's reach
+        const size_t ring_lds = (size_t)e->R * (cell_dwords(P) / 4) * kFlatBlock * 16;
+        const bool lds = e->form != 3 && ring_lds <= 28 * 1024 && back + 1 <= kFlatRowsLds - 1;
+        auto go = [&](auto plain_tag, auto lds_tag) {
           constexpr bool kPl = decltype(plain_tag)::value;
+          constexpr bool kL = decltype(lds_tag)::value;
+          const size_t shm = kL ? ring_lds : 0;
           if (e->sparse) {
-            p2p_flat_kernel<P, -1, kPl, true><<<grid, kFlatBlock, 0, e->stream>>>(p);
+            p2p_flat_kernel<P, -1, kPl, true, kL><<<grid, kFlatBlock, shm, e->stream>>>(p);
           } else if constexpr (P == 2) {
-            if (p.local_mask == 1u) p2p_flat_kernel<P, 1, kPl, false><<<grid, kFlatBlock, 0, e->stream>>>(p);
-            else if (p.local_mask == 2u) p2p_flat_kernel<P, 2, kPl, false><<<grid, kFlatBlock, 0, e->stream>>>(p);
-            else p2p_flat_kernel<P, -1, kPl, false><<<grid, kFlatBlock, 0, e->stream>>>(p);
+            if (p.local_mask == 1u) p2p_flat_kernel<P, 1, kPl, false, kL><<<grid, kFlatBlock, shm, e->stream>>>(p);
+            else if (p.local_mask == 2u) p2p_flat_kernel<P, 2, kPl, false, kL><<<grid, kFlatBlock, shm, e->stream>>>(p);
+            else p2p_flat_kernel<P, -1, kPl, false, kL><<<grid, kFlatBlock, shm, e->stream>>>(p);
           } else {
-            p2p_flat_kernel<P, -1, kPl, false><<<grid, kFlatBlock, 0, e->stream>>>(p);
+            p2p_flat_kernel<P, -1, kPl, false, kL><<<grid, kFlatBlock, shm, e->stream>>>(p);
           }
         };
-        if (p.desync_interval == 0 && !p.trace && p.dbg_sess < 0) go(std::true_type());
-        else go(std::false_type());
+        const bool plain = p.desync_interval == 0 && !p.trace && p.dbg_sess < 0;
+        if (lds) {
+          if (plain) go(std::true_type(), std::true_type());
+          else go(std::false_type(), std::true_type());
+        } else {
+          if (plain) go(std::true_type(), std::false_type());
+          else go(std::false_type(), std::false_type());
+        }
       }
       else if (staged) p2p_kernel<P, true><<<grid_of(p.S, kP2PBlock), kP2PBlock, 0, e->stream>>>(p);
       else p2p_kernel<P, false><<<grid_of(p.S, kP2PBlock), kP2PBlock, 0, e->stream>>>(p);

@@ -210,7 +210,8 @@ class P2PEngine:
         self.set_kernel_form("unstaged" if on else "default")
 
     def set_kernel_form(self, form):
-        """"default" (flat whenever input rows can be staged), "flat" (each session's calls as its own step
-        sequence), "lockstep" (calls in lockstep, rows staged in LDS) or "unstaged" (lockstep, rows
-        from global memory)."""
+        """"default" (flat whenever input rows can be staged, with the block's session rings in LDS
+        for the launch where they fit 28 KB), "flat" (each session's calls as its own step sequence,
+        rings in HBM), "lockstep" (calls in lockstep, rows staged in LDS) or "unstaged" (lockstep,
+        rows from global memory)."""
         _lib.check(self._L.ggrs_p2p_set_unstaged(self._h, self.KERNEL_FORMS[form]))

@@ -433,7 +433,8 @@ int ggrs_p2p_set_sparse_saving(ggrs_p2p_engine_t* eng, int32_t on);
 /* kernel form (comparison and tests): 0 = default (each session's calls flattened into its own
  * step sequence, input rows staged in LDS, with or without sparse saving), 1 = calls in
  * lockstep with input rows read from global memory, 2 = calls in lockstep with staged rows,
- * 3 = the flattened form (what the default runs whenever input rows can be staged) */
+ * 3 = the flattened form with the session rings in HBM (the default keeps a block's rings in LDS
+ * for the launch when R x cell x 64 sessions fits 28 KB, else it runs this form) */
 int ggrs_p2p_set_unstaged(ggrs_p2p_engine_t* eng, int32_t form);
 /* test hook: the AdvanceFrame from `frame` of `session` flips the lowest bit of player 0's x on
  * every (re)simulation -- a deterministic desync of this peer (session -1: off) */

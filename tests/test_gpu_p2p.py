@@ -48,11 +48,12 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("form", ["flat", "lockstep", "unstaged"])
+@pytest.mark.parametrize("form", ["default", "flat", "lockstep", "unstaged"])
 @pytest.mark.parametrize("P,local,delay,mp,D,pred,model", CASES)
 def test_p2p_matches_oracle(oracle, P, local, delay, mp, D, pred, model, form):
-    """Every kernel form: per-session step sequences (default), calls in lockstep with input rows
-    staged in LDS, and in lockstep reading rows from global memory."""
+    """Every kernel form: per-session step sequences with the block's rings in LDS (default, where
+    they fit 28 KB) or in HBM ("flat"), calls in lockstep with input rows staged in LDS, and in
+    lockstep reading rows from global memory."""
     from ggrs_amd import P2PEngine
     S, frames = 300, 160
     rows = stream(S, frames, P, model)
@@ -123,7 +124,7 @@ SPARSE_CASES = [
 ]
 
 
-@pytest.mark.parametrize("form", ["flat", "lockstep"])
+@pytest.mark.parametrize("form", ["default", "flat", "lockstep"])
 @pytest.mark.parametrize("P,local,delay,mp,D,pred,model", SPARSE_CASES)
 def test_p2p_sparse_saving_matches_oracle(oracle, P, local, delay, mp, D, pred, model, form):
     """Sparse saving (builder.rs:160-169): rollbacks from the last save, saves only at
