@@ -64,6 +64,7 @@ def pmc_valu(workload):
         if d.get("valu_active_frac_of_wave_cycles") is None:
             return None
         return {"issue_frac": None if d.get("valu_issue_frac") is None else round(d["valu_issue_frac"], 4),
+                "wave_issue_frac": None if d.get("valu_wave_issue_frac") is None else round(d["valu_wave_issue_frac"], 4),
                 "active_frac_of_wave_cycles": round(d["valu_active_frac_of_wave_cycles"], 4),
                 "insts_per_wave": round(d["valu_insts_per_wave"], 1),
                 "wait_frac_of_wave_cycles": round(d["wait_any_frac"], 4), "profile": d.get("tag")}

@@ -657,15 +657,6 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
       dst[i] = lds_ring[rem * kFlatBlock + sl];
     }
   }
-  if constexpr (kLds) {  // the rings back to HBM
-    __syncthreads();
-    const int n = nb * ring_pieces;
-    uint4* dst = reinterpret_cast<uint4*>(p.ring) + sess0 * ring_pieces;
-    for (int i = lt; i < n; i += kFlatBlock) {
-      const int sl = i / ring_pieces, rem = i - sl * ring_pieces;
-      dst[i] = lds_ring[rem * kFlatBlock + sl];
-    }
-  }
   if (!live) return;
   store_state<P>(st, p.cur + sess, S);
 #pragma unroll

@@ -40,7 +40,7 @@ namespace {
 struct LaneBatchParams {
   int64_t L;
   int32_t R, W, LD, A, S, use_status, trace_cap;
-  int32_t sys_stores;          // results straight to host memory with system-scope stores (server)
+  int32_t wide;                // L % 8 == 0: a block's piece of every host row is whole 8-byte words
   const uint32_t* tokens;      // [W][L]
   const int32_t* load_frames;  // [LD][L]
   const uint8_t* inputs;       // [A][L][P]
@@ -140,227 +140,343 @@ __device__ inline void slice_advance(Slice& s, uint32_t in, bool owner) {
   }
 }
 
-// LDS: tokens [W][B] u32 | load frames [LD][B] i32 | cell tags [R][B] i32 | inputs [A][B] u32
-// | status [A][B] u32 (when used); B = kLaneBlock columns, column = session within the block
-__host__ __device__ inline size_t lane_batch_lds_bytes(int W, int LD, int R, int A, int use_status) {
-  return (size_t)kLaneBlock * 4 * ((size_t)W + LD + R + (size_t)A * (use_status ? 2 : 1));
+// LDS of a lane block (byte offsets, KS = the block's sessions, every row a multiple of 8 bytes):
+//   tokens [W][KS] u32 | load frames [LD][KS] i32 | cell tags [R][KS] i32 | inputs [A][kInPitch] u8
+//   | status [A][kInPitch] u8 (when used) | checksums out [S][KS] u16 | results [KS] i32
+// Input and status rows keep the host's byte layout (session-major, P bytes per session), so a
+// block stages its piece of every host row with wide copies.
+struct LaneLds {
+  int KS, in_pitch;
+  size_t tok, ld, tag, in, st, ck, res, bytes;
+  __host__ __device__ LaneLds(int P, int W, int LD, int R, int A, int S, int use_status) {
+    const int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
+    KS = kLaneBlock / Pp;
+    in_pitch = (KS * P + 15) & ~15;
+    tok = 0;
+    ld = tok + (size_t)4 * KS * W;
+    tag = ld + (size_t)4 * KS * LD;
+    in = tag + (size_t)4 * KS * R;
+    st = in + (size_t)in_pitch * A;
+    ck = st + (use_status ? (size_t)in_pitch * A : 0);
+    res = ck + (((size_t)2 * KS * S + 7) & ~(size_t)7);
+    bytes = res + (size_t)4 * KS;
+  }
+};
+
+// host memory is read and written with system-scope accesses: plain loads of pinned host memory may
+// be served from the device's L2 (the persistent server re-reads the same rows every batch), and
+// system-scope stores go straight out (sc0 sc1)
+template <typename T>
+__device__ inline T ld_sys(const T* ptr) {
+  return __hip_atomic_load(ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <typename T>
+__device__ inline void st_sys(T* ptr, T v) {
+  __hip_atomic_store(ptr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// One session's list on its Pp lanes: stage its rows into the session's LDS column, validate,
-// execute.  `st` is this lane's slice (in registers); the session only writes its own ring cells
-// and outputs.
+// Stage the block's rows into LDS.  Wide form (p.wide: L % 8 == 0, so every host row piece of a
+// block is whole 8-byte words): the block copies its pieces of the token, load-frame, input and
+// status rows as 8-byte system-scope loads spread over all its threads, kStage of them in flight
+// per thread (at 4096 lanes and a SyncTest list that is two loads per thread, one PCIe round trip);
+// otherwise every lane loads its own dword / bytes row by row.  The cell tags (the frame field of
+// each ring cell, device memory) are loaded per session.  Ends with a barrier.
 template <int P>
-__device__ inline void run_lane(const LaneBatchParams& p, Slice& st, int64_t lane, bool valid, uint32_t* lds) {
+__device__ inline void stage_rows(const LaneBatchParams& p, const LaneLds& g, uint8_t* lds, int64_t sess0, int nb,
+                                  int64_t ln, int col, int pl) {
+  const int t = threadIdx.x;
+  const int64_t L = p.L;
+  constexpr int F = state_fields(P);
+  const int nrow = p.W + p.LD, nbr = p.A * (p.use_status ? 2 : 1);  // u32 rows, byte rows
+  if (p.wide) {
+    const int tp = nb / 2, ip = nb * P / 8;  // 8-byte words per u32 row / per byte row
+    const int n_u32 = nrow * tp, total = n_u32 + nbr * ip;
+    auto where = [&](int c, const uint64_t*& src, uint64_t*& dst) {
+      if (c < n_u32) {
+        const int r = c / tp, k = c - r * tp;
+        const uint32_t* row = r < p.W ? p.tokens + (int64_t)r * L : (const uint32_t*)p.load_frames + (int64_t)(r - p.W) * L;
+        src = reinterpret_cast<const uint64_t*>(row + sess0) + k;
+        dst = reinterpret_cast<uint64_t*>(lds + g.tok + (size_t)4 * g.KS * r) + k;
+      } else {
+        c -= n_u32;
+        const int r = c / ip, k = c - r * ip;
+        const uint8_t* row = r < p.A ? p.inputs + ((int64_t)r * L + sess0) * P : p.status + ((int64_t)(r - p.A) * L + sess0) * P;
+        src = reinterpret_cast<const uint64_t*>(row) + k;
+        dst = reinterpret_cast<uint64_t*>(lds + g.in + (size_t)g.in_pitch * r) + k;
+      }
+    };
+    constexpr int kStage = 8;
+    for (int base = 0; base < total; base += kStage * kLaneBlock) {
+      uint64_t v[kStage];
+#pragma unroll
+      for (int u = 0; u < kStage; u++) {
+        const int c = base + u * kLaneBlock + t;
+        if (c < total) {
+          const uint64_t* s;
+          uint64_t* d;
+          where(c, s, d);
+          v[u] = ld_sys(s);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kStage; u++) {
+        const int c = base + u * kLaneBlock + t;
+        if (c < total) {
+          const uint64_t* s;
+          uint64_t* d;
+          where(c, s, d);
+          *d = v[u];
+        }
+      }
+    }
+  } else {
+    // one row per load, kStageChunk rows in flight: u32 rows (tokens, load frames) from lane 0 of
+    // the session, input / status bytes from each owner lane
+    constexpr int kStageChunk = 32;
+    uint32_t* tok = reinterpret_cast<uint32_t*>(lds + g.tok);
+    uint8_t* in = lds + g.in;
+    for (int base = 0; base < nrow + nbr; base += kStageChunk) {
+      uint32_t v[kStageChunk];
+#pragma unroll
+      for (int u = 0; u < kStageChunk; u++) {
+        const int i = base + u;
+        v[u] = 0;
+        if (i < nrow) {
+          v[u] = i < p.W ? ld_sys(p.tokens + (int64_t)i * L + ln) : (uint32_t)ld_sys(p.load_frames + (int64_t)(i - p.W) * L + ln);
+        } else if (i < nrow + nbr && pl < P) {
+          const int r = i - nrow;
+          const uint8_t* row = r < p.A ? p.inputs + (int64_t)r * L * P : p.status + (int64_t)(r - p.A) * L * P;
+          v[u] = ld_sys(row + ln * P + pl);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kStageChunk; u++) {
+        const int i = base + u;
+        if (i < nrow) {
+          if (pl == 0) tok[i * g.KS + col] = v[u];
+        } else if (i < nrow + nbr && pl < P) {
+          in[(size_t)g.in_pitch * (i - nrow) + col * P + pl] = (uint8_t)v[u];
+        }
+      }
+    }
+  }
+  {  // (the Pp lanes of a session store the same values)
+    int32_t* tag = reinterpret_cast<int32_t*>(lds + g.tag);
+    for (int r0 = 0; r0 < p.R; r0 += 16) {
+      int32_t v[16];
+#pragma unroll
+      for (int u = 0; u < 16; u++)
+        if (r0 + u < p.R) v[u] = (int32_t)p.ring[(int64_t)(r0 + u) * F * L + ln];
+#pragma unroll
+      for (int u = 0; u < 16; u++)
+        if (r0 + u < p.R) tag[(r0 + u) * g.KS + col] = v[u];
+    }
+  }
+  __syncthreads();
+}
+
+// Write the block's checksum rows (up to the most saves any of its sessions made) and lane
+// results back to host memory: 8-byte system-scope stores spread over the block (wide form), or
+// one element per store.  Returns after the stores have left (vmcnt(0)).
+__device__ inline void write_back(const LaneBatchParams& p, const LaneLds& g, const uint8_t* lds, int64_t sess0, int nb,
+                                  int rows) {
+  const int t = threadIdx.x;
+  const int64_t L = p.L;
+  const uint16_t* ck = reinterpret_cast<const uint16_t*>(lds + g.ck);
+  const int32_t* res = reinterpret_cast<const int32_t*>(lds + g.res);
+  if (p.wide) {
+    const int cp = nb / 4, rp = nb / 2;  // 8-byte words per checksum row / of the results
+    const int n_ck = rows * cp;
+    for (int c = t; c < n_ck + rp; c += kLaneBlock) {
+      if (c < n_ck) {
+        const int r = c / cp, k = c - r * cp;
+        st_sys(reinterpret_cast<uint64_t*>(p.cks + (int64_t)r * L + sess0) + k,
+               reinterpret_cast<const uint64_t*>(ck + (size_t)r * g.KS)[k]);
+      } else {
+        const int k = c - n_ck;
+        st_sys(reinterpret_cast<uint64_t*>(p.result + sess0) + k, reinterpret_cast<const uint64_t*>(res)[k]);
+      }
+    }
+  } else {
+    for (int c = t; c < (rows + 1) * nb; c += kLaneBlock) {
+      const int r = c / nb, j = c - r * nb;
+      if (r < rows) st_sys(p.cks + (int64_t)r * L + sess0 + j, ck[(size_t)r * g.KS + j]);
+      else st_sys(p.result + sess0 + j, res[j]);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this thread's stores have left
+}
+
+// One block of sessions fulfils its lists: stage, validate, execute, write back.  `st` is this
+// lane's slice (in registers); a session only writes its own ring cells and outputs.  Returns the
+// number of the block's sessions that failed validation (on thread 0; every thread takes part).
+template <int P>
+__device__ inline int run_lanes(const LaneBatchParams& p, Slice& st, uint8_t* lds) {
   constexpr int Pp = LaneGeom<P>::Pp;
+  constexpr int KS = LaneGeom<P>::kSessions;
   const int wl = threadIdx.x;
   const int col = wl / Pp, pl = wl % Pp;  // session column in the block, player
   const bool owner = pl < P;
   const int64_t L = p.L;
-  const int64_t ln = valid ? lane : 0;
+  const int64_t sess0 = (int64_t)blockIdx.x * KS;
+  const int nb = (int)min((int64_t)KS, L - sess0);
+  const int64_t lane = sess0 + col;
+  const bool valid = col < nb;
+  const int64_t ln = valid ? lane : sess0;
   const int R = p.R;
   constexpr int F = state_fields(P);
-  uint32_t* l_tok = lds;
-  int32_t* l_load = (int32_t*)(l_tok + p.W * kLaneBlock);
-  int32_t* l_tag = l_load + p.LD * kLaneBlock;
-  uint32_t* l_in = (uint32_t*)(l_tag + R * kLaneBlock);
-  uint32_t* l_st = l_in + p.A * kLaneBlock;
-  // Stage the session's rows -- tokens, load frames, inputs, status (host memory, one PCIe round
-  // trip each) and the cell tags (the frame field of each ring cell) -- as ONE sequence of rows
-  // loaded kStageChunk at a time with every load of a chunk in flight before the first LDS store (a
-  // load-store pair per row would wait out a PCIe round trip per row).  The Pp lanes of a session
-  // load the same addresses and store the same values into its column, so each lane only ever
-  // reads what it wrote itself: no barrier.
-  {
-    const int n_tok = p.W, n_ld = n_tok + p.LD, n_in = n_ld + p.A, n_st = n_in + (p.use_status ? p.A : 0);
-    const int n_rows = n_st + R;
-    // LDS order: tokens, loads, tags, inputs, status
-    auto lds_row = [&](int i) -> uint32_t* {
-      if (i < n_ld) return lds + i * kLaneBlock;
-      if (i < n_st) return lds + (i + R) * kLaneBlock;
-      return lds + (i - n_st + n_ld) * kLaneBlock;
-    };
-    // host rows are read with system-scope loads: plain loads of pinned host memory may be served
-    // from the device's L2, and the persistent server re-reads the same rows every batch
-    auto ld_sys = [](const auto* ptr) { return __hip_atomic_load(ptr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
-    if constexpr (P == 3) {  // 3-byte input rows: byte loads, row by row
-      auto bytes3 = [&](const uint8_t* row) {
-        const uint8_t* b = row + ln * 3;
-        return (uint32_t)ld_sys(b) | ((uint32_t)ld_sys(b + 1) << 8) | ((uint32_t)ld_sys(b + 2) << 16);
-      };
-      for (int i = 0; i < n_rows; i++) {
-        uint32_t v;
-        if (i < n_tok) v = ld_sys(p.tokens + (int64_t)i * L + ln);
-        else if (i < n_ld) v = (uint32_t)ld_sys(p.load_frames + (int64_t)(i - n_tok) * L + ln);
-        else if (i < n_in) v = bytes3(p.inputs + (int64_t)(i - n_ld) * L * P);
-        else if (i < n_st) v = bytes3(p.status + (int64_t)(i - n_in) * L * P);
-        else v = p.ring[(int64_t)(i - n_st) * F * L + ln];
-        lds_row(i)[col] = v;
-      }
-    } else {
-      // every row is one dword load per lane from a wave-uniform row base: 4-byte rows at 4 * lane,
-      // P-byte input / status rows at the dword holding byte P * lane (extracted after the loads)
-      const uint32_t boff = (uint32_t)(P * ln);
-      const uint32_t in_off = boff & ~3u, in_shift = 8u * (boff & 3u);
-      constexpr uint32_t kMask = P == 4 ? 0xffffffffu : ((1u << (8 * P)) - 1u);
-      auto row_base = [&](int i) -> const uint8_t* {
-        const uint8_t* tk = (const uint8_t*)p.tokens + (int64_t)i * L * 4;
-        const uint8_t* ld = (const uint8_t*)p.load_frames + (int64_t)(i - n_tok) * L * 4;
-        const uint8_t* in = p.inputs + (int64_t)(i - n_ld) * L * P;
-        const uint8_t* sb = p.status + (int64_t)(i - n_in) * L * P;
-        const uint8_t* rg = (const uint8_t*)p.ring + (int64_t)(i - n_st) * F * L * 4;
-        return i < n_tok ? tk : (i < n_ld ? ld : (i < n_in ? in : (i < n_st ? sb : rg)));
-      };
-      constexpr int kStageChunk = 32;  // the usual list (W <= 2, LD <= 2, A <= 18, R <= 10) in one chunk
-      for (int base = 0; base < n_rows; base += kStageChunk) {
-        uint32_t v[kStageChunk];
-#pragma unroll
-        for (int u = 0; u < kStageChunk; u++) {
-          const int i = min(base + u, n_rows - 1);
-          const bool bytes = i >= n_ld && i < n_st;
-          v[u] = ld_sys((const uint32_t*)(row_base(i) + (bytes ? in_off : 4u * (uint32_t)ln)));
-        }
-#pragma unroll
-        for (int u = 0; u < kStageChunk; u++) {
-          const int i = base + u;
-          if (i < n_rows) {
-            const bool bytes = i >= n_ld && i < n_st;
-            lds_row(i)[col] = bytes ? (v[u] >> in_shift) & kMask : v[u];
-          }
-        }
-      }
-    }
-  }
-  if (!valid) return;  // a session's Pp lanes are valid together
+  const LaneLds g(P, p.W, p.LD, R, p.A, p.S, p.use_status);
+  const uint32_t* l_tok = reinterpret_cast<const uint32_t*>(lds + g.tok);
+  const int32_t* l_load = reinterpret_cast<const int32_t*>(lds + g.ld);
+  int32_t* l_tag = reinterpret_cast<int32_t*>(lds + g.tag);
+  const uint8_t* l_in = lds + g.in;
+  const uint8_t* l_st = lds + g.st;
+  uint16_t* l_ck = reinterpret_cast<uint16_t*>(lds + g.ck);
+  int32_t* l_res = reinterpret_cast<int32_t*>(lds + g.res);
+  __shared__ int s_rows, s_fails;
+  // the checksum rows start zeroed (a session's rows past its own saves read 0)
+  for (int i = wl; i < p.S * KS / 2; i += kLaneBlock) reinterpret_cast<uint32_t*>(l_ck)[i] = 0u;
+  if (wl == 0) s_rows = s_fails = 0;
+  stage_rows<P>(p, g, lds, sess0, nb, ln, col, pl);
 
-  const int n_tok = p.W * GGRS_TOKENS_PER_WORD;
-  // the first two token words in registers (every list GGRS emits at max_prediction <= 15 fits
-  // them), longer lists read the rest from LDS
-  const uint32_t tw0 = l_tok[col], tw1 = p.W > 1 ? l_tok[kLaneBlock + col] : 0u;
-  auto token = [&](int k) -> uint32_t {
-    const uint32_t w = k < 16 ? tw0 : (k < 32 ? tw1 : l_tok[(k >> 4) * kLaneBlock + col]);
-    return (w >> (2 * (k & 15))) & 3u;
-  };
-  // (1) validation, nothing written.  Fast path for the lists GGRS emits (at most 32 requests,
-  // at most one Load, placed before any Save): per-kind counts from the 2-bit fields by popcount,
-  // and the Load's frame against the cell tag staged from the ring.  Anything else walks the list.
-  int32_t frame = (int32_t)st.frame;
-  int32_t err = -1;
-  bool walk = true;
-  if (p.W <= 2) {
-    const uint64_t w = (uint64_t)tw0 | ((uint64_t)tw1 << 32);
-    const uint64_t lo = w & 0x5555555555555555ull, hi = (w >> 1) & 0x5555555555555555ull;
-    const uint64_t end = lo & hi;
-    const uint64_t live = end ? ((end & (0 - end)) - 1) : ~0ull;  // fields before the first END
-    const uint64_t m_save = ~lo & ~hi & 0x5555555555555555ull & live, m_adv = lo & ~hi & live,
-                   m_load = hi & ~lo & live;
-    const int ns = __builtin_popcountll(m_save), na = __builtin_popcountll(m_adv),
-              nl = __builtin_popcountll(m_load);
-    if (ns <= p.S && na <= p.A && nl <= p.LD && nl <= 1 && (nl == 0 || !m_save || (m_load & (0 - m_load)) < (m_save & (0 - m_save)))) {
-      walk = false;
-      if (nl == 1) {
-        const int32_t f = l_load[col];
-        if (f < 0 || l_tag[(f % R) * kLaneBlock + col] != f) err = (int32_t)(__builtin_ctzll(m_load) >> 1);
+  int32_t result = 0;
+  int ns_done = 0;
+  if (valid) {
+    const int n_tok = p.W * GGRS_TOKENS_PER_WORD;
+    // the first two token words in registers (every list GGRS emits at max_prediction <= 15 fits
+    // them), longer lists read the rest from LDS
+    const uint32_t tw0 = p.W > 0 ? l_tok[col] : 0xffffffffu, tw1 = p.W > 1 ? l_tok[KS + col] : 0xffffffffu;
+    auto token = [&](int k) -> uint32_t {
+      const uint32_t w = k < 16 ? tw0 : (k < 32 ? tw1 : l_tok[(k >> 4) * KS + col]);
+      return (w >> (2 * (k & 15))) & 3u;
+    };
+    // (1) validation, nothing written.  Fast path for the lists GGRS emits (at most 32 requests,
+    // at most one Load, placed before any Save): per-kind counts from the 2-bit fields by popcount,
+    // and the Load's frame against the cell tag staged from the ring.  Anything else walks the list.
+    int32_t frame = (int32_t)st.frame;
+    int32_t err = -1;
+    bool walk = true;
+    if (p.W <= 2) {
+      const uint64_t w = (uint64_t)tw0 | ((uint64_t)tw1 << 32);
+      const uint64_t lo = w & 0x5555555555555555ull, hi = (w >> 1) & 0x5555555555555555ull;
+      const uint64_t end = lo & hi;
+      const uint64_t live = end ? ((end & (0 - end)) - 1) : ~0ull;  // fields before the first END
+      const uint64_t m_save = ~lo & ~hi & 0x5555555555555555ull & live, m_adv = lo & ~hi & live,
+                     m_load = hi & ~lo & live;
+      const int ns = __builtin_popcountll(m_save), na = __builtin_popcountll(m_adv),
+                nl = __builtin_popcountll(m_load);
+      if (ns <= p.S && na <= p.A && nl <= p.LD && nl <= 1 && (nl == 0 || !m_save || (m_load & (0 - m_load)) < (m_save & (0 - m_save)))) {
+        walk = false;
+        if (nl == 1) {
+          const int32_t f = l_load[col];
+          if (f < 0 || l_tag[(f % R) * KS + col] != f) err = (int32_t)(__builtin_ctzll(m_load) >> 1);
+        }
       }
     }
-  }
-  if (walk) {
-    int na = 0, ns = 0, nl = 0;
-    int32_t slot = frame % R;
-    for (int k = 0; k < n_tok; k++) {
-      const uint32_t t = token(k);
-      if (t == GGRS_TOK_END) break;
-      if (t == GGRS_TOK_SAVE) {
-        if (ns == p.S) { err = k; break; }
-        l_tag[slot * kLaneBlock + col] = frame;
-        ++ns;
-      } else if (t == GGRS_TOK_LOAD) {
-        if (nl == p.LD) { err = k; break; }
-        const int32_t f = l_load[nl * kLaneBlock + col];
-        if (f < 0 || l_tag[(f % R) * kLaneBlock + col] != f) { err = k; break; }  // sync_layer.rs:248
-        frame = f;
-        slot = f % R;
-        ++nl;
-      } else {
-        if (na == p.A) { err = k; break; }
-        ++frame;
-        slot = slot + 1 == R ? 0 : slot + 1;
-        ++na;
+    if (walk) {
+      // the walk records the saves it would make in the tag row (each lane of the session its own
+      // identical store: it only reads what it wrote itself)
+      int na = 0, ns = 0, nl = 0;
+      int32_t slot = frame % R;
+      for (int k = 0; k < n_tok; k++) {
+        const uint32_t t = token(k);
+        if (t == GGRS_TOK_END) break;
+        if (t == GGRS_TOK_SAVE) {
+          if (ns == p.S) { err = k; break; }
+          l_tag[slot * KS + col] = frame;
+          ++ns;
+        } else if (t == GGRS_TOK_LOAD) {
+          if (nl == p.LD) { err = k; break; }
+          const int32_t f = l_load[nl * KS + col];
+          if (f < 0 || l_tag[(f % R) * KS + col] != f) { err = k; break; }  // sync_layer.rs:248
+          frame = f;
+          slot = f % R;
+          ++nl;
+        } else {
+          if (na == p.A) { err = k; break; }
+          ++frame;
+          slot = slot + 1 == R ? 0 : slot + 1;
+          ++na;
+        }
       }
     }
-  }
-  auto put_result = [&](int32_t v) {
-    if (pl != 0) return;
-    if (p.sys_stores) __hip_atomic_store(&p.result[lane], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    else p.result[lane] = v;
-  };
-  if (err >= 0) {  // the session does not run (a reference session would have panicked here)
-    put_result(-(1 + err));
-    return;
-  }
-  // (2) execution: Game::handle_requests, requests strictly in order (ex_game.rs:79-99)
-  int na = 0, ns = 0, nl = 0;
-  int32_t slot = (int32_t)st.frame % R;
-  // this lane's field offsets inside a ring slot (frame on lane 0, player pl's five fields)
-  int64_t fo[5];
+    if (err >= 0) {  // the session does not run (a reference session would have panicked here)
+      result = -(1 + err);
+    } else {
+      // (2) execution: Game::handle_requests, requests strictly in order (ex_game.rs:79-99)
+      int na = 0, ns = 0, nl = 0;
+      int32_t slot = (int32_t)st.frame % R;
+      // this lane's field offsets inside a ring slot (frame on lane 0, player pl's five fields)
+      int64_t fo[5];
 #pragma unroll
-  for (int q = 0; q < 5; q++) fo[q] = (int64_t)slice_field<P>(pl, q) * L + lane;
-  const int64_t slot_stride = (int64_t)F * L;
-  auto save_cell = [&](uint32_t* cell) {
-    if (pl == 0) cell[lane] = st.frame;
-    if (owner) {
+      for (int q = 0; q < 5; q++) fo[q] = (int64_t)slice_field<P>(pl, q) * L + lane;
+      const int64_t slot_stride = (int64_t)F * L;
+      auto save_cell = [&](uint32_t* cell) {
+        if (pl == 0) cell[lane] = st.frame;
+        if (owner) {
 #pragma unroll
-      for (int q = 0; q < 5; q++) cell[fo[q]] = st.w[q];
+          for (int q = 0; q < 5; q++) cell[fo[q]] = st.w[q];
+        }
+      };
+      auto load_cell = [&](const uint32_t* cell) {
+        st.frame = cell[lane];
+#pragma unroll
+        for (int q = 0; q < 5; q++) st.w[q] = owner ? cell[fo[q]] : 0u;
+      };
+      for (int k = 0; k < n_tok; k++) {
+        const uint32_t t = token(k);
+        if (t == GGRS_TOK_END) break;
+        if (t == GGRS_TOK_SAVE) {  // save_game_state (:103-108): state + fletcher16 into the cell
+          save_cell(p.ring + slot * slot_stride);
+          const uint32_t ck = slice_fletcher<P>(st, pl);
+          if (pl == 0) {
+            p.ring_ck[(int64_t)slot * L + lane] = (uint16_t)ck;
+            l_ck[ns * KS + col] = (uint16_t)ck;
+          }
+          ++ns;
+        } else if (t == GGRS_TOK_LOAD) {  // load_game_state (:111-113)
+          const int32_t f = l_load[nl * KS + col];
+          slot = f % R;
+          load_cell(p.ring + slot * slot_stride);
+          ++nl;
+        } else {  // advance_frame (:115-127); Disconnected players spin (input 4, :277-281)
+          const size_t at = (size_t)g.in_pitch * na + col * P + pl;
+          uint32_t in = owner ? l_in[at] : 0u;
+          if (p.use_status && owner && l_st[at] == GGRS_STATUS_DISCONNECTED) in = 4u;
+          slice_advance(st, in, owner);
+          if (p.trace) {
+            const uint32_t ck = slice_fletcher<P>(st, pl);
+            if (pl == 0) p.trace[(int64_t)(((int32_t)st.frame - 1) % p.trace_cap) * L + lane] = (uint16_t)ck;
+          }
+          slot = slot + 1 == R ? 0 : slot + 1;
+          ++na;
+        }
+      }
+      result = (int32_t)st.frame;
+      ns_done = ns;
     }
-  };
-  auto load_cell = [&](const uint32_t* cell) {
-    st.frame = cell[lane];
-#pragma unroll
-    for (int q = 0; q < 5; q++) st.w[q] = owner ? cell[fo[q]] : 0u;
-  };
-  for (int k = 0; k < n_tok; k++) {
-    const uint32_t t = token(k);
-    if (t == GGRS_TOK_END) break;
-    if (t == GGRS_TOK_SAVE) {  // save_game_state (:103-108): state + fletcher16 into the cell
-      save_cell(p.ring + slot * slot_stride);
-      const uint32_t ck = slice_fletcher<P>(st, pl);
-      if (pl == 0) {
-        p.ring_ck[(int64_t)slot * L + lane] = (uint16_t)ck;
-        if (p.sys_stores)
-          __hip_atomic_store(&p.cks[(int64_t)ns * L + lane], (uint16_t)ck, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        else p.cks[(int64_t)ns * L + lane] = (uint16_t)ck;
-      }
-      ++ns;
-    } else if (t == GGRS_TOK_LOAD) {  // load_game_state (:111-113)
-      const int32_t f = l_load[nl * kLaneBlock + col];
-      slot = f % R;
-      load_cell(p.ring + slot * slot_stride);
-      ++nl;
-    } else {  // advance_frame (:115-127); Disconnected players spin (input 4, :277-281)
-      uint32_t in = (l_in[na * kLaneBlock + col] >> (8 * pl)) & 0xffu;
-      if (p.use_status && ((l_st[na * kLaneBlock + col] >> (8 * pl)) & 0xffu) == GGRS_STATUS_DISCONNECTED) in = 4u;
-      slice_advance(st, in, owner);
-      if (p.trace) {
-        const uint32_t ck = slice_fletcher<P>(st, pl);
-        if (pl == 0) p.trace[(int64_t)(((int32_t)st.frame - 1) % p.trace_cap) * L + lane] = (uint16_t)ck;
-      }
-      slot = slot + 1 == R ? 0 : slot + 1;
-      ++na;
+    if (pl == 0) {
+      l_res[col] = result;
+      if (ns_done) atomicMax(&s_rows, ns_done);
+      if (result < 0) atomicAdd(&s_fails, 1);
     }
   }
-  put_result((int32_t)st.frame);
+  __syncthreads();
+  write_back(p, g, lds, sess0, nb, s_rows);
+  return s_fails;
 }
 
 // One launch per batch.
 template <int P>
 __global__ __launch_bounds__(kLaneBlock) void lane_requests_kernel(LaneBatchParams p) {
-  extern __shared__ uint32_t lds[];
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   constexpr int Pp = LaneGeom<P>::Pp;
   const int pl = threadIdx.x % Pp;
   const int64_t lane = (int64_t)blockIdx.x * LaneGeom<P>::kSessions + threadIdx.x / Pp;
   const bool valid = lane < p.L;
   Slice st;
   load_slice<P>(st, p.cur + (valid ? lane : 0), p.L, pl);
-  run_lane<P>(p, st, lane, valid, lds);
+  run_lanes<P>(p, st, lds);
   if (valid) store_slice<P>(st, p.cur + lane, p.L, pl);
 }
 
@@ -372,9 +488,10 @@ __global__ __launch_bounds__(kLaneBlock) void lane_requests_kernel(LaneBatchPara
 //   * only block 0 polls host memory (64+ blocks polling it over PCIe slowed every round trip 4-10x,
 //     tools/server_probe.hip) and relays the word through device memory, where the other blocks
 //     poll it with agent-scope loads;
-//   * each lane writes its checksums and result with system-scope stores (no device-cache
-//     write-back needed), the block waits for them, and the last block to finish (a device-memory
-//     counter) stores the epoch into the host's done word.
+//   * each block writes its checksums and results with system-scope stores (no device-cache
+//     write-back needed) and waits for them; the last block to finish (a device-memory counter
+//     that also sums the blocks' failed sessions) stores the epoch and the batch's failure count
+//     into the host's 64-bit done word, so the host scans lane results only when one failed.
 // A lane's state stays in registers between batches and goes back to `cur` when the server exits:
 // on the quit bit, or when no batch arrived for `idle_ticks` of the constant wall clock (a watchdog
 // every block reaches, so an abandoned server drains by itself).
@@ -390,14 +507,13 @@ __host__ __device__ constexpr bool quit(uint64_t c) { return (c & kQuit) != 0; }
 
 struct ServerDev {  // device memory
   uint64_t relay;   // block 0's copy of the control word for the other blocks
-  uint32_t count;   // blocks finished, over this launch's batches
-  uint32_t pad;
+  uint64_t count;   // this batch: blocks finished (low 32 bits), failed sessions (high 32 bits)
 };
 
 template <int P>
-__global__ __launch_bounds__(kLaneBlock) void lane_server_kernel(LaneBatchParams p, const uint64_t* ctl, int32_t* done,
+__global__ __launch_bounds__(kLaneBlock) void lane_server_kernel(LaneBatchParams p, const uint64_t* ctl, uint64_t* done,
                                                             ServerDev* dev, int32_t start_epoch, int64_t idle_ticks) {
-  extern __shared__ uint32_t lds[];
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   __shared__ uint64_t s_ctl;
   const int wl = threadIdx.x;
   constexpr int Pp = LaneGeom<P>::Pp;
@@ -408,7 +524,6 @@ __global__ __launch_bounds__(kLaneBlock) void lane_server_kernel(LaneBatchParams
   Slice st;
   load_slice<P>(st, p.cur + (valid ? lane : 0), p.L, pl);
   int32_t last = start_epoch;
-  uint32_t batches = 0;
   for (;;) {
     if (wl == 0) {
       const int64_t t0 = wall_clock64();
@@ -444,17 +559,20 @@ __global__ __launch_bounds__(kLaneBlock) void lane_server_kernel(LaneBatchParams
     q.use_status = (int32_t)((c >> 44) & 1);
     q.A = (int32_t)((c >> 46) & 0xff);
     q.S = (int32_t)((c >> 54) & 0x1ff);
-    q.sys_stores = 1;
-    run_lane<P>(q, st, lane, valid, lds);
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this lane's result stores have left
+    const int fails = run_lanes<P>(q, st, lds);  // returns after this thread's host stores left
     __syncthreads();
     const int32_t e = ctlw::epoch(c);
     if (wl == 0) {
-      const uint32_t old = __hip_atomic_fetch_add(&dev->count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (old == (batches + 1) * nblocks - 1)  // the batch's last block: tell the host
-        __hip_atomic_store(done, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint64_t mine = 1ull | ((uint64_t)fails << 32);
+      const uint64_t old = __hip_atomic_fetch_add(&dev->count, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((uint32_t)old == nblocks - 1) {  // the batch's last block: reset the counter, tell the host
+        const uint64_t total = old + mine;
+        __hip_atomic_store(&dev->count, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // the reset is done before the host can publish again
+        __hip_atomic_store(done, (uint64_t)(uint32_t)e | (total & 0xffffffff00000000ull), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
-    ++batches;
     last = e;
   }
   if (valid) store_slice<P>(st, p.cur + lane, p.L, pl);
@@ -531,7 +649,7 @@ LaneBatchParams batch_params(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, i
   p.S = S;
   p.use_status = use_status;
   p.trace_cap = e->cfg.trace_capacity;
-  p.sys_stores = 0;
+  p.wide = p.L % 8 == 0;
   p.tokens = device_view(v.tokens);
   p.load_frames = device_view(v.load_frames);
   p.inputs = device_view(v.inputs);
@@ -562,16 +680,16 @@ int server_start(ggrs_engine* e) {
   }
   uint64_t* ctl = (uint64_t*)s.mem;
   __atomic_store_n(ctl, ctlw::pack(s.epoch, 0, 0, 0, 0, 0), __ATOMIC_RELEASE);
-  ServerDev init{ctlw::pack(s.epoch, 0, 0, 0, 0, 0), 0u, 0u};
+  ServerDev init{ctlw::pack(s.epoch, 0, 0, 0, 0, 0), 0ull};
   HIP_TRY(hipMemcpyAsync(s.dev, &init, sizeof init, hipMemcpyHostToDevice, e->stream));
   const LaneBatchHost& b = e->batch;
   LaneBatchParams p = batch_params(e, b.words, b.loads, b.adv, b.saves, 1);
   if (!p.tokens || !p.load_frames || !p.inputs || !p.status || !p.cks || !p.result)
     return set_error(GGRS_E_HIP, "hipHostGetDevicePointer failed for the lane batch");
   const uint64_t* dctl = device_view((const uint64_t*)ctl);
-  int32_t* ddone = device_view((int32_t*)(s.mem + 8));
+  uint64_t* ddone = device_view((uint64_t*)(s.mem + 8));
   if (!dctl || !ddone) return set_error(GGRS_E_HIP, "hipHostGetDevicePointer failed for the lane server");
-  const size_t lds = lane_batch_lds_bytes(b.words, b.loads, e->R, b.adv, 1);
+  const size_t lds = LaneLds(e->cfg.num_players, b.words, b.loads, e->R, b.adv, b.saves, 1).bytes;
   // every block must be resident at once (block 0 relays the batches to the others)
   int per_cu = 0, cus = 0;
   int rc = GGRS_OK;
@@ -595,8 +713,9 @@ int server_start(ggrs_engine* e) {
   return GGRS_OK;
 }
 
-// Publish one batch to the running server and spin until its last block reports it done.
-int server_run(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int use_status) {
+// Publish one batch to the running server and spin until its last block reports it done;
+// *fails = the batch's sessions that failed validation.
+int server_run(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int use_status, int32_t* fails) {
   LaneServerHost& s = e->server;
   if (s.running && now_s() - s.last_done > kServerIdleHost) {
     if (int rc = lane_server_stop(e)) return rc;
@@ -606,12 +725,13 @@ int server_run(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int 
     if (!s.enabled) return GGRS_E_STATE;  // caller falls back to a launch per batch
   }
   uint64_t* ctl = (uint64_t*)s.mem;
-  const int32_t* done = (const int32_t*)(s.mem + 8);
+  const uint64_t* done = (const uint64_t*)(s.mem + 8);
   const int32_t ep = ++s.epoch;
   __atomic_store_n(ctl, ctlw::pack(ep, W, LD, A, S, use_status), __ATOMIC_RELEASE);  // after the batch rows
   const double t0 = now_s();
   int spins = 0;
-  while (__atomic_load_n(done, __ATOMIC_ACQUIRE) != ep) {
+  uint64_t d;
+  while ((int32_t)(uint32_t)(d = __atomic_load_n(done, __ATOMIC_ACQUIRE)) != ep) {
     _mm_pause();
     if (++spins == 4096) {
       spins = 0;
@@ -622,20 +742,23 @@ int server_run(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int 
     }
   }
   s.last_done = now_s();
+  *fails = (int32_t)(d >> 32);
   return GGRS_OK;
 }
 
-// Launch over the engine's mapped batch with the given counts; waits for completion.
-int run_batch(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int use_status) {
+// Runs the engine's mapped batch with the given counts; waits for completion.  *fails = the
+// sessions that failed validation, or -1 when only the lane results tell (one launch per batch).
+int run_batch(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int use_status, int32_t* fails) {
   e->mode = kModeLaneRequests;
+  *fails = -1;
   if (e->server.enabled) {
-    const int rc = server_run(e, W, LD, A, S, use_status);
+    const int rc = server_run(e, W, LD, A, S, use_status, fails);
     if (rc != GGRS_E_STATE) return rc;  // GGRS_E_STATE: the grid cannot stay resident, launch instead
   }
   LaneBatchParams p = batch_params(e, W, LD, A, S, use_status);
   if (!p.tokens || !p.load_frames || !p.inputs || !p.status || !p.cks || !p.result)
     return set_error(GGRS_E_HIP, "hipHostGetDevicePointer failed for the lane batch");
-  const size_t lds = lane_batch_lds_bytes(W, LD, e->R, A, use_status);
+  const size_t lds = LaneLds(e->cfg.num_players, W, LD, e->R, A, S, use_status).bytes;
   const int64_t grid = grid_of(p.L, kLaneBlock / padded_players(e->cfg.num_players));
   int rc = launch_timed(e, [&] {
     dispatch_players(e->cfg.num_players, [&](auto PC) {
@@ -728,8 +851,10 @@ int ggrs_lane_batch_run(ggrs_engine_t* e, const ggrs_lane_batch_t* b, int32_t fl
     return set_error(GGRS_E_INVALID, "batch counts exceed the mapped shape");
   HIP_TRY(hipSetDevice(e->cfg.device));
   e->lane_frame.clear();  // the lanes' frames moved on the device only
-  rc = run_batch(e, b->token_words, b->load_slots, b->adv_rows, b->save_rows, (flags & GGRS_BATCH_STATUS) != 0);
+  int32_t fails = -1;
+  rc = run_batch(e, b->token_words, b->load_slots, b->adv_rows, b->save_rows, (flags & GGRS_BATCH_STATUS) != 0, &fails);
   if (rc) return rc;
+  if (fails == 0) return GGRS_OK;  // the server counted no failed lane: no scan of the results
   return report_failures(e, v.lane_result, n_failed);
 }
 
@@ -825,7 +950,8 @@ int ggrs_handle_requests_lanes(ggrs_engine_t* e, const ggrs_request_t* reqs, con
       for (int32_t w = 0; w < W; w++) v.tokens[(int64_t)w * L + l] = 0xffffffffu;
     }
   }
-  rc = run_batch(e, W, max_ld, max_adv, max_sv, status != nullptr);
+  int32_t fails = -1;
+  rc = run_batch(e, W, max_ld, max_adv, max_sv, status != nullptr, &fails);
   if (rc) return rc;
   // results: per-Save checksums in request order, lane results, the lanes' new frames
   int64_t sv_at = 0;

@@ -112,13 +112,14 @@ def test_p2p_lists_300_sessions_generic(oracle, sparse, server):
     assert fr.tolist() == [int(np.frombuffer(bytes(e["final_state"][:4]), np.int32)[0]) for e in exp]
 
 
-@pytest.mark.parametrize("server", [True, False])
-def test_p2p_lists_batch_form(oracle, server):
+@pytest.mark.parametrize("server,L", [(True, 257), (False, 257), (True, 320), (False, 320)])
+def test_p2p_lists_batch_form(oracle, server, L):
     """The same lists pre-encoded per lane into the engine's mapped batch (ggrs_lane_batch_run),
-    through the persistent lane server or one launch per batch."""
+    through the persistent lane server or one launch per batch; L = 320 (a multiple of 8) takes the
+    wide staging and write-back (8-byte host words per thread), 257 the per-lane form."""
     import time
     from ggrs_amd import Engine, encode_lane_lists
-    L, calls, P, maxp = 257, 80, 2, 8
+    calls, P, maxp = 80, 2, 8
     streams = p2p_lane_streams(oracle, L, calls, P, maxp, seed=7)
     exp = expected(oracle, streams, P, maxp)
     eng = Engine(L, P, maxp, 0, 0)
@@ -148,11 +149,13 @@ def test_p2p_lists_batch_form(oracle, server):
     check_final(eng, exp, range(0, L, 16))
 
 
-@pytest.mark.parametrize("P,local_mask", [(4, 0b0011), (3, 0b001), (1, 0b0)])
-def test_disconnected_status_and_player_counts(oracle, P, local_mask):
-    """InputStatus::Disconnected players spin (input 4, ex_game.rs:277-281), any player count."""
+@pytest.mark.parametrize("P,local_mask,L", [(4, 0b0011, 130), (3, 0b001, 130), (1, 0b0, 130), (4, 0b0011, 136),
+                                           (3, 0b001, 136), (1, 0b0, 264)])
+def test_disconnected_status_and_player_counts(oracle, P, local_mask, L):
+    """InputStatus::Disconnected players spin (input 4, ex_game.rs:277-281), any player count, in
+    the per-lane (L = 130) and wide (L % 8 == 0) staging forms."""
     from ggrs_amd import Engine
-    L, calls, maxp = 130, 60, 7
+    calls, maxp = 60, 7
     streams = p2p_lane_streams(oracle, L, calls, P, maxp, seed=11 + P, local_mask=local_mask)
     rng = np.random.default_rng(P)
     over = []
@@ -212,13 +215,16 @@ def test_synctest_lists_lanes_at_different_frames(oracle):
         assert ck.tolist() == r["ring_cksums"].tolist()
 
 
-def test_validation_fails_lanes_not_the_batch(oracle):
+@pytest.mark.parametrize("L,server", [(70, True), (72, True), (72, False)])
+def test_validation_fails_lanes_not_the_batch(oracle, L, server):
     """A Load of a frame the lane's cell does not hold (sync_layer.rs:248) and a Save of a frame
-    other than the state's (ex_game.rs:104) fail only their lanes, which are left untouched."""
+    other than the state's (ex_game.rs:104) fail only their lanes, which are left untouched (the
+    server reports the batch's failure count with its done word)."""
     from ggrs_amd import Engine, LanesFailed
-    L, calls, P, maxp = 70, 30, 2, 8
+    calls, P, maxp = 30, 2, 8
     streams = p2p_lane_streams(oracle, L, calls, P, maxp, seed=21)
     eng = Engine(L, P, maxp, 0, 0)
+    eng.set_lane_server(server)
     for c in range(20):
         reqs, off, inp, st, _ = call_lists(streams, c)
         eng.handle_requests_lanes(reqs, off, inp, st)
@@ -293,3 +299,34 @@ def test_lane_handler_mirror(oracle):
             got[l].extend(cks.tolist())
     for l in range(L):
         assert got[l] == exp[l]["save_cks"].tolist()
+
+
+@pytest.mark.parametrize("L,server", [(72, True), (72, False), (70, True)])
+def test_batch_form_failure_count(oracle, L, server):
+    """ggrs_lane_batch_run's failure count: the server's done word carries the batch's failed
+    sessions (the host scans lane results only then); failed lanes keep their state, the rest run."""
+    from ggrs_amd import Engine, encode_lane_lists
+    P, maxp = 2, 8
+    eng = Engine(L, P, maxp, 0, 0)
+    eng.set_lane_server(server)
+    batch = eng.lane_batch(1, 1, 2, 2)
+    inp, st = np.array([1, 2], np.uint8), np.zeros(2, np.uint8)
+    ok = [(REQ_SAVE, 0, None, None), (REQ_ADVANCE, 0, inp, st)]
+    for c in range(3):
+        enc = encode_lane_lists([[(k, c if k == REQ_SAVE else f, i, s) for k, f, i, s in ok]] * L, P)
+        batch.tokens[:1], batch.inputs[:1] = enc["tokens"], enc["inputs"]
+        assert batch.run(1, 0, 1, 1) == 0
+        assert (batch.lane_result == c + 1).all()
+    bad = {3: [(REQ_LOAD, 7, None, None)], L - 1: [(REQ_SAVE, 3, None, None), (REQ_LOAD, -1, None, None)]}
+    lists = [bad.get(l, [(REQ_SAVE, 3, None, None), (REQ_ADVANCE, 0, inp, st)]) for l in range(L)]
+    enc = encode_lane_lists(lists, P)
+    W, LD, A, S = enc["shape"]
+    batch.tokens[:W], batch.load_frames[:LD], batch.inputs[:A] = enc["tokens"], enc["load_frames"], enc["inputs"]
+    assert batch.run(W, LD, A, S) == 2
+    res = batch.lane_result.copy()
+    assert res[3] == -1 and res[L - 1] == -2
+    good = np.ones(L, bool)
+    good[[3, L - 1]] = False
+    assert (res[good] == 4).all()
+    fr = eng.lane_frames()
+    assert fr[3] == 3 and fr[L - 1] == 3 and (fr[good] == 4).all()

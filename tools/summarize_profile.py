@@ -85,6 +85,11 @@ def main(tag, workload, kernel="synctest_kernel", last="0", units="1"):
         # 2 cycles at best, MI355X_MICROARCH.md) over the chip's SIMD-cycles during the kernel
         clk = out.get("effective_clock_ghz") or 2.4
         out["valu_issue_frac"] = sq["SQ_INSTS_VALU"] * 2 / (1024 * avg_ns * clk)
+        # the same per wave at the rate ONE wave sustains alone (4 cycles per VALU instruction,
+        # MI355X_MICROARCH.md 'vector-instruction ISSUE cost'): the ceiling of a one-wave-per-SIMD
+        # kernel is 1.0 here (0.5 on valu_issue_frac)
+        if out.get("valu_insts_per_wave"):
+            out["valu_wave_issue_frac"] = out["valu_insts_per_wave"] * 4 / (avg_ns * clk)
     with open(os.path.join(dst, "summary.json"), "w") as fh:
         json.dump(out, fh, indent=1)
     if "hbm_bytes_per_launch" in out:
@@ -95,6 +100,7 @@ def main(tag, workload, kernel="synctest_kernel", last="0", units="1"):
                        "valu_active_frac_of_wave_cycles": out.get("valu_active_frac_of_wave_cycles"),
                        "valu_insts_per_wave": out.get("valu_insts_per_wave"),
                        "valu_issue_frac": out.get("valu_issue_frac"),
+                       "valu_wave_issue_frac": out.get("valu_wave_issue_frac"),
                        "wait_any_frac": out.get("wait_any_frac")}, fh, indent=1)
     for f in ("bench_trace.log",):
         if os.path.exists(os.path.join(src, f)):
