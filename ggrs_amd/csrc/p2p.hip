@@ -376,7 +376,12 @@ constexpr int kFlatBlock = 64;
 // rows per stage: a wave's steps in a stage are its slowest session's, so fewer, longer stages
 // cost less (128 rows: one stage per 64-call launch at back = 6)
 constexpr int kFlatRows = 128;
-constexpr int kFlatRowsLds = 64;  // with the LDS ring: 28 + 8 KB per block, four blocks per CU
+// with the LDS ring: 12 KB of rows (96 at two players: a 64-call launch is one stage) beside a
+// ring of at most 28 KB per block, four blocks per CU in 160 KB
+template <int P>
+constexpr int flat_rows_lds() {
+  return 12 * 1024 / (kFlatBlock * (P <= 1 ? 1 : (P == 2 ? 2 : 4)));
+}
 
 template <int P>
 struct LdsRowsFlat {
@@ -407,7 +412,7 @@ template <int P, int kLocal, bool kPlain, bool kSparse, bool kLds>
 __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
   const uint32_t lmask = kLocal >= 0 ? (uint32_t)kLocal : p.local_mask;
   constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
-  constexpr int kRows = kLds ? kFlatRowsLds : kFlatRows;
+  constexpr int kRows = kLds ? flat_rows_lds<P>() : kFlatRows;
   constexpr int PC = cell_dwords(P) / 4;  // 16-byte pieces per cell
   __shared__ __attribute__((aligned(16))) uint8_t lds_rows[kRows * kFlatBlock * Pp];
   extern __shared__ uint4 lds_ring[];  // kLds: [R][PC][kFlatBlock]
@@ -1012,9 +1017,9 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
       constexpr int P = decltype(PC)::value;
       if (flat) {
         const dim3 grid((unsigned)grid_of(p.S, kFlatBlock));
-        // the LDS ring when the block's rings fit 28 KB and a stage of 64 rows holds a call's reach
+        // the LDS ring when the block's rings fit 28 KB and a stage of rows holds a call's reach
         const size_t ring_lds = (size_t)e->R * (cell_dwords(P) / 4) * kFlatBlock * 16;
-        const bool lds = e->form != 3 && ring_lds <= 28 * 1024 && back + 1 <= kFlatRowsLds - 1;
+        const bool lds = e->form != 3 && ring_lds <= 28 * 1024 && back + 1 <= flat_rows_lds<P>() - 1;
         auto go = [&](auto plain_tag, auto lds_tag) {
           constexpr bool kPl = decltype(plain_tag)::value;
           constexpr bool kL = decltype(lds_tag)::value;
