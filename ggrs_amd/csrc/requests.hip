@@ -777,6 +777,17 @@ int check_mode(const ggrs_engine* e) {
   return GGRS_OK;
 }
 
+// the lane block's LDS for a batch shape must fit one workgroup's allotment on the device
+int check_lds(const ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S) {
+  int max_lds = 0;
+  HIP_TRY(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, e->cfg.device));
+  const size_t need = LaneLds(e->cfg.num_players, W, LD, e->R, A, S, 1).bytes + 64;  // + the static words
+  if (need > (size_t)max_lds)
+    return set_error(GGRS_E_INVALID, "lane batch shape (%d words, %d loads, %d advances, %d saves) needs %zu bytes "
+                                     "of LDS per lane block, more than the device's %d", W, LD, A, S, need, max_lds);
+  return GGRS_OK;
+}
+
 int check_shape(int32_t W, int32_t LD, int32_t A, int32_t S) {
   if (W < 0 || W > GGRS_BATCH_MAX_WORDS || LD < 0 || LD > GGRS_BATCH_MAX_LOADS || A < 0 || A > GGRS_BATCH_MAX_ADV ||
       S < 0 || S > GGRS_BATCH_MAX_SAVES)
@@ -828,6 +839,9 @@ int ggrs_lane_batch_map(ggrs_engine_t* e, int32_t W, int32_t LD, int32_t A, int3
   int rc = check_shape(W, LD, A, S);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(e->cfg.device));
+  if ((rc = check_lds(e, std::max(W, e->batch.words), std::max(LD, e->batch.loads), std::max(A, e->batch.adv),
+                      std::max(S, e->batch.saves))))
+    return rc;
   rc = map_batch(e, W, LD, A, S);
   if (rc) return rc;
   fill_batch_view(e, out);
@@ -893,6 +907,9 @@ int ggrs_handle_requests_lanes(ggrs_engine_t* e, const ggrs_request_t* reqs, con
   rc = check_shape(W, max_ld, max_adv, max_sv);
   if (rc) return rc;
   HIP_TRY(hipSetDevice(e->cfg.device));
+  if ((rc = check_lds(e, std::max(W, e->batch.words), std::max(max_ld, e->batch.loads),
+                      std::max(max_adv, e->batch.adv), std::max(max_sv, e->batch.saves))))
+    return rc;
   rc = map_batch(e, W, max_ld, max_adv, max_sv);
   if (rc) return rc;
   // every lane's frame at the start of its list: the Save frames are checked on the host

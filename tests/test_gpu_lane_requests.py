@@ -330,3 +330,16 @@ def test_batch_form_failure_count(oracle, L, server):
     assert (res[good] == 4).all()
     fr = eng.lane_frames()
     assert fr[3] == 3 and fr[L - 1] == 3 and (fr[good] == 4).all()
+
+
+def test_lane_batch_shape_beyond_lds_is_rejected(oracle):
+    """A batch shape whose lane block would need more LDS than a workgroup gets is GGRS_E_INVALID
+    at map time (not a failed launch); the largest shapes that fit still map."""
+    from ggrs_amd import Engine, GgrsError
+    eng = Engine(64, 2, 63, 0, 0)
+    with pytest.raises(GgrsError):
+        eng.lane_batch(32, 8, 128, 256)
+    b = eng.lane_batch(8, 2, 32, 32)
+    b.tokens[:1] = 0xFFFFFFFF  # every lane's list empty
+    assert b.run(1, 0, 0, 0) == 0
+    assert (b.lane_result == 0).all()
