@@ -131,3 +131,31 @@ def test_report_to_device_buffer(oracle):
     ck, bits = eng.report()
     assert (host[:200].view(np.uint16) == ck).all()
     assert (host[eng.report_ck_bytes:].view(np.uint64) == bits).all()
+
+
+def test_full_size_config4(oracle):
+    """Config 4 at full per-GPU size: 8192 four-player sessions x 16 branches = 131,072 lanes,
+    window 8.  Single rounds checked lane by lane against the oracle's adjust_gamestate replay on
+    sampled lanes, every sampled session's trunk and report; then the fused rounds launch (the bench
+    path) leaves every session's trunk checksum and survival word equal to the single rounds'."""
+    from ggrs_amd import BranchEngine, synth
+    S, B, P, mask, W, rounds = 8192, 16, 4, 0b1110, 8, 3
+    truth = synth.gen_inputs(5, S, 2 * rounds + W + 2, P, synth.MODEL_HELD)
+    eng = BranchEngine(S, num_players=P, remote_mask=mask, window=W, branches=B, alphabet=16)
+    eng.add_inputs(0, truth)
+    L = S * B
+    rng = np.random.default_rng(4)
+    lanes = sorted(set([0, 1, 15, 16, L // 2, L - 17, L - 1] + rng.integers(0, L, 9).tolist()))
+    run_rounds(oracle, eng, truth, rounds, lanes)
+    fused = BranchEngine(S, num_players=P, remote_mask=mask, window=W, branches=B, alphabet=16)
+    fused.add_inputs(0, truth)
+    fused.rounds(rounds)
+    fused.synchronize()
+    a, b = fused.report(), eng.report()
+    assert (a[0] == b[0]).all() and (a[1] == b[1]).all()
+    for s in (0, S // 3, S - 1):
+        st = oracle.state_new(P)
+        for f in range(rounds):
+            st = oracle.state_advance(st, truth[f, s])
+        assert bytes(fused.trunk(s)) == bytes(st)
+        assert int(a[0][s]) == oracle.fletcher16(bytes(st))

@@ -180,3 +180,22 @@ def test_lockstep_mode_matches_oracle(oracle, P, local, delay, D):
                          max_prediction=0, latency=D)
     assert eng.current_frame() == int.from_bytes(ref["final_state"][:4].tobytes(), "little") < frames
     check_against_oracle(eng, rows, [0, 1, 63, 64, 150, 299], frames)
+
+
+def test_full_size_p2p_bench_config(oracle):
+    """The P2P bench configuration at full size: 65,536 sessions, 2 players (1 remote, inputs 4
+    frames late), max_prediction 8, held-key inputs, 64-call launches on the default (LDS-ring,
+    plain) kernel; sampled sessions' final state, ring and rollback counts bit-exact."""
+    from ggrs_amd import P2PEngine, synth
+    S, frames, P = 65536, 128, 2
+    rows = synth.gen_inputs(9, S, frames, P, synth.MODEL_HELD)
+    eng = P2PEngine(S, num_players=P, local_players=(0,), input_delay=0, max_prediction=8, remote_latency=4,
+                    input_capacity=frames + 6)
+    eng.add_inputs(0, rows)
+    for _ in range(frames // 64):
+        eng.advance_frames(64)
+    rng = np.random.default_rng(2)
+    sessions = sorted(set([0, 1, 63, 64, S // 2, S - 1] + rng.integers(0, S, 8).tolist()))
+    check_against_oracle(eng, rows, sessions, frames, trace=False)
+    rb, _ = eng.stats()
+    assert rb.sum() > S  # rollbacks happen throughout
