@@ -31,7 +31,7 @@ EXPORTS = (
     "ggrs_abi_version", "ggrs_last_error", "ggrs_engine_create", "ggrs_engine_destroy",
     "ggrs_engine_config", "ggrs_add_local_inputs", "ggrs_add_local_inputs_device",
     "ggrs_synctest_advance_frames", "ggrs_handle_requests", "ggrs_synchronize",
-    "ggrs_current_frame", "ggrs_read_mismatches", "ggrs_read_save_checksums", "ggrs_read_state",
+    "ggrs_current_frame", "ggrs_read_mismatches", "ggrs_read_save_checksums", "ggrs_read_save_checksums_frames", "ggrs_read_state",
     "ggrs_read_ring", "ggrs_read_trace", "ggrs_debug_corrupt_on_load", "ggrs_last_launch_ms",
     "ggrs_timing_reset", "ggrs_timing_read", "ggrs_set_synctest_path",
     "ggrs_lane_batch_map", "ggrs_lane_batch_run", "ggrs_handle_requests_lanes", "ggrs_read_lane_frames",
@@ -133,6 +133,7 @@ def lib():
         L.ggrs_current_frame.argtypes = [vp, P(ctypes.c_int32)]
         L.ggrs_read_mismatches.argtypes = [vp, vp, vp, vp]
         L.ggrs_read_save_checksums.argtypes = [vp, ctypes.c_int32, vp]
+        L.ggrs_read_save_checksums_frames.argtypes = [vp, vp, ctypes.c_int32, vp]
         L.ggrs_read_state.argtypes = [vp, ctypes.c_int32, vp]
         L.ggrs_read_ring.argtypes = [vp, ctypes.c_int32, vp, vp, vp]
         L.ggrs_read_trace.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp]

@@ -1511,6 +1511,23 @@ int ggrs_read_save_checksums(ggrs_engine_t* e, int32_t frame, uint16_t* out) {
   return GGRS_OK;
 }
 
+int ggrs_read_save_checksums_frames(ggrs_engine_t* e, const int32_t* frames, int32_t n, uint16_t* out) {
+  if (!e || (n > 0 && (!frames || !out)) || n < 0) return set_error(GGRS_E_INVALID, "null argument or negative count");
+  { int rc_ = resolve(e); if (rc_) return rc_; }
+  if (e->mode == kModeLaneRequests)
+    return set_error(GGRS_E_STATE, "per-lane request lists return their save checksums from each call");
+  for (int32_t k = 0; k < n; k++)
+    if (frames[k] < 0 || e->ring_tag[frames[k] % e->R] != frames[k])
+      return set_error(GGRS_E_PRECONDITION, "no saved cell for frame %d", frames[k]);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const size_t L = e->cfg.num_lanes;
+  for (int32_t k = 0; k < n; k++)
+    HIP_TRY(hipMemcpyAsync(out + (size_t)k * L, e->ring_ck + (size_t)(frames[k] % e->R) * L, 2 * L,
+                           hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return GGRS_OK;
+}
+
 static int gather_lane(ggrs_engine_t* e, const uint32_t* base, int32_t lane, uint32_t* w) {
   const size_t L = e->cfg.num_lanes;
   for (int k = 0; k < e->F; k++)

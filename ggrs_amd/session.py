@@ -170,6 +170,13 @@ class Engine:
         _lib.check(self._L.ggrs_read_save_checksums(self._h, frame, _vp(out)))
         return out
 
+    def save_checksums_frames(self, frames):
+        """[len(frames)][num_lanes] checksums of the saved cells of `frames`, one transfer wait."""
+        fr = np.ascontiguousarray(frames, np.int32)
+        out = np.zeros((len(fr), self.num_lanes), np.uint16)
+        _lib.check(self._L.ggrs_read_save_checksums_frames(self._h, _vp(fr), len(fr), _vp(out)))
+        return out
+
     def state(self, lane):
         out = np.zeros(self.state_bytes, np.uint8)
         _lib.check(self._L.ggrs_read_state(self._h, lane, _vp(out)))
@@ -450,7 +457,8 @@ class BoxGameHandler:
         inp = np.stack(inputs) if inputs else None
         st = np.stack(status) if status else None
         self.engine.handle_requests(reqs, inp, st)
-        return {f: self.engine.save_checksums(f) for f in saves}
+        cks = self.engine.save_checksums_frames(saves) if saves else []
+        return {f: cks[k] for k, f in enumerate(saves)}
 
 
 class LaneBoxGameHandler:

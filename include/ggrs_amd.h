@@ -216,6 +216,9 @@ int ggrs_read_mismatches(ggrs_engine_t* eng, int32_t* lane_status, int32_t* mism
                          uint64_t* mismatch_mask);
 /* Checksum stored with the saved cell of `frame` for every lane (num_lanes u16). */
 int ggrs_read_save_checksums(ggrs_engine_t* eng, int32_t frame, uint16_t* out);
+/* The same for n frames in one device-to-host transfer wait: out [n][num_lanes] (a request list's
+ * saves, read once after ggrs_handle_requests instead of one synchronisation per save). */
+int ggrs_read_save_checksums_frames(ggrs_engine_t* eng, const int32_t* frames, int32_t n, uint16_t* out);
 /* Current game state of one lane as bincode bytes (36 + 20 * num_players). */
 int ggrs_read_state(ggrs_engine_t* eng, int32_t lane, uint8_t* out);
 /* Saved-state ring of one lane: frames[R], checksums[R], states[R][36 + 20 * num_players]. */

@@ -176,6 +176,7 @@ extern "C" {
     pub fn ggrs_read_mismatches(eng: *mut ggrs_engine_t, lane_status: *mut i32, mismatch_frame: *mut i32,
                                 mismatch_mask: *mut u64) -> i32;
     pub fn ggrs_read_save_checksums(eng: *mut ggrs_engine_t, frame: i32, out: *mut u16) -> i32;
+    pub fn ggrs_read_save_checksums_frames(eng: *mut ggrs_engine_t, frames: *const i32, n: i32, out: *mut u16) -> i32;
     pub fn ggrs_read_state(eng: *mut ggrs_engine_t, lane: i32, out: *mut u8) -> i32;
     pub fn ggrs_read_ring(eng: *mut ggrs_engine_t, lane: i32, frames: *mut i32, checksums: *mut u16,
                           states: *mut u8) -> i32;

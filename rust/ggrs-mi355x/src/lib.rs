@@ -292,12 +292,18 @@ impl BatchedBoxGame {
         check(unsafe {
             ggrs_handle_requests(self.eng, reqs.as_ptr(), reqs.len() as i32, inputs.as_ptr(), status.as_ptr())
         })?;
-        let mut cs = vec![0u16; self.lanes];
-        for (k, frame) in saves {
-            check(unsafe { ggrs_read_save_checksums(self.eng, frame, cs.as_mut_ptr()) })?;
+        // every save's checksums in one transfer wait: [saves][lanes]
+        let frames: Vec<i32> = saves.iter().map(|&(_, f)| f).collect();
+        let mut cs = vec![0u16; self.lanes * frames.len()];
+        if !frames.is_empty() {
+            check(unsafe {
+                ggrs_read_save_checksums_frames(self.eng, frames.as_ptr(), frames.len() as i32, cs.as_mut_ptr())
+            })?;
+        }
+        for (j, &(k, _)) in saves.iter().enumerate() {
             for (lane, reqs) in requests.iter().enumerate() {
                 if let GgrsRequest::SaveGameState { cell, frame } = &reqs[k] {
-                    cell.save(*frame, None, Some(cs[lane] as u128));
+                    cell.save(*frame, None, Some(cs[j * self.lanes + lane] as u128));
                 }
             }
         }

@@ -36,6 +36,9 @@ def test_handler_replays_synctest_stream(oracle):
     for f in range(F):
         saves = h.handle_requests(synctest_requests(f, cd, P, inputs, d))
         assert f in saves or cd == 0
+        if f == F - 1:  # the batched read equals one read per saved frame
+            for fr, ck in saves.items():
+                assert (eng.save_checksums(fr) == ck).all()
     for lane in (0, 50, 95):
         r = oracle.synctest_run(inputs[:, lane, :], P, maxp, cd, d)
         assert bytes(eng.state(lane)) == bytes(r["final_state"])
@@ -76,5 +79,8 @@ def test_request_preconditions(oracle):
     h.handle_requests([SaveGameState(0), AdvanceFrame(z), SaveGameState(1), AdvanceFrame(z)])
     h.handle_requests([LoadGameState(0), AdvanceFrame(z)])
     assert eng.current_frame() == 1
+    with pytest.raises(PreconditionError, match="no saved cell"):
+        eng.save_checksums_frames([0, 5])               # frame 5 was never saved
+    assert eng.save_checksums_frames([1, 0]).shape == (2, 4)
     ref = oracle.state_advance(oracle.state_new(2), [0, 0])
     assert bytes(eng.state(2)) == bytes(ref)
