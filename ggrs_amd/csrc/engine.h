@@ -74,6 +74,7 @@ struct ggrs_engine {
   // per-lane request lists
   LaneBatchHost batch;
   LaneServerHost server;
+  int max_lds_per_block = 0;        // the device's LDS per workgroup (read once, lane batches)
   std::vector<int32_t> lane_frame;  // each lane's frame, as ggrs_handle_requests_lanes last left it
                                     // (empty: unknown, read from the device when needed)
 };

@@ -778,9 +778,10 @@ int check_mode(const ggrs_engine* e) {
 }
 
 // the lane block's LDS for a batch shape must fit one workgroup's allotment on the device
-int check_lds(const ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S) {
-  int max_lds = 0;
-  HIP_TRY(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, e->cfg.device));
+int check_lds(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S) {
+  int& max_lds = e->max_lds_per_block;
+  if (max_lds == 0)
+    HIP_TRY(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, e->cfg.device));
   const size_t need = LaneLds(e->cfg.num_players, W, LD, e->R, A, S, 1).bytes + 64;  // + the static words
   if (need > (size_t)max_lds)
     return set_error(GGRS_E_INVALID, "lane batch shape (%d words, %d loads, %d advances, %d saves) needs %zu bytes "
