@@ -202,20 +202,38 @@ __global__ __launch_bounds__(kRoundsBlock) void rounds_kernel(RoundsParams rp) {
   // row_c = f_c % cap, slot_c = f_c % R of the round's trunk frame
   auto wrap_inc = [](int32_t x, int32_t m) { return x + 1 == m ? 0 : x + 1; };
   int32_t row_c = p.f_c % p.cap, slot_c = p.f_c % p.R;
+  // the last confirmed input row (f_c - 1) and the round's truth row (f_c); each round loads the
+  // next round's truth row while it speculates
+  uint32_t last = p.f_c > 0 ? load_inputs<P>(p.inputs, (int64_t)(row_c == 0 ? p.cap - 1 : row_c - 1) * p.S + s) : 0u;
+  uint32_t truth = load_inputs<P>(p.inputs, (int64_t)row_c * p.S + s);
+  const bool trunk_thread = (int)threadIdx.x < ns;
+  const int64_t s2 = s_first + (trunk_thread ? threadIdx.x : 0);
   for (int32_t r = 0; r < rp.n; ++r) {
     SpecParams q = p;
     q.f_c = p.f_c + r;
-    const int32_t row_prev = row_c == 0 ? p.cap - 1 : row_c - 1;
-    if ((r > 0 || p.check_prev) && survived) {  // speculate_kernel's check of the last survivors
-      const uint16_t mine = p.ring_ck[(int64_t)slot_c * p.L + lane];
-      if (mine != lds_ck[ls]) atomicCAS(&p.desync[s], -1, q.f_c);
+    const int32_t row_n = wrap_inc(row_c, p.cap);
+    const uint32_t truth_next = r + 1 < rp.n ? load_inputs<P>(p.inputs, (int64_t)row_n * p.S + s) : 0u;
+    // speculate_kernel's check of the last survivors: the cell of f_c is not re-saved by this
+    // round (its saves go to the W slots after it), so its load is issued here and compared after
+    // the replays, while its latency is hidden behind them
+    const bool check = (r > 0 || p.check_prev) && survived;
+    const uint16_t mine = check ? p.ring_ck[(int64_t)slot_c * p.L + lane] : (uint16_t)0;
+    // the confirm step's trunk replay (the next round's trunk: AdvanceFrame(f_c) with the true
+    // inputs) depends only on this round's trunk, so the block's trunk threads run it beside the
+    // speculation instead of after it; it reaches LDS after every lane has loaded the old trunk
+    BoxState<P> tr;
+    uint16_t tr_ck = 0;
+    if (trunk_thread) {
+#pragma unroll
+      for (int k = 0; k < F; k++) tr.w[k] = lds_trunk[threadIdx.x][k];
+      const uint32_t tin = load_inputs<P>(p.inputs, (int64_t)row_c * p.S + s2);
+      if (lean_ok) advance_state_lean<P>(tr, tin);
+      else advance_state<P>(tr, tin, 0u);
+      tr_ck = fletcher16_state<P>(tr);
     }
     BoxState<P> st;
 #pragma unroll
     for (int k = 0; k < F; k++) st.w[k] = lds_trunk[ls][k];  // LoadGameState(f_c)
-    // input rows: f_c - 1 (the last confirmed) and f_c + k, each read one frame ahead
-    const uint32_t last = q.f_c > 0 ? load_inputs<P>(p.inputs, (int64_t)row_prev * p.S + s) : 0u;
-    const uint32_t truth = load_inputs<P>(p.inputs, (int64_t)row_c * p.S + s);
     if (in_range) {
       uint32_t tk = truth;
       int32_t row_k = row_c, slot = slot_c;
@@ -232,7 +250,8 @@ __global__ __launch_bounds__(kRoundsBlock) void rounds_kernel(RoundsParams rp) {
         tk = next;
       }
     }
-    // confirm: survival of every lane, the trunk replayed with the true inputs of f_c
+    if (check && mine != lds_ck[ls]) atomicCAS(&p.desync[s], -1, q.f_c);
+    // confirm: survival of every lane
     bool survive = false;
     if (in_range) {
       survive = true;
@@ -250,26 +269,20 @@ __global__ __launch_bounds__(kRoundsBlock) void rounds_kernel(RoundsParams rp) {
       if (rp.copy_bits && r + 1 == rp.n) rp.copy_bits[lane >> 6] = bits;
     }
     survived = survive;
-    __syncthreads();  // every lane has read the trunk
-    if ((int)threadIdx.x < ns) {
-      const int64_t s2 = s_first + threadIdx.x;
-      BoxState<P> tr;
-#pragma unroll
-      for (int k = 0; k < F; k++) tr.w[k] = lds_trunk[threadIdx.x][k];
-      const uint32_t tin = load_inputs<P>(p.inputs, (int64_t)row_c * p.S + s2);
-      if (lean_ok) advance_state_lean<P>(tr, tin);
-      else advance_state<P>(tr, tin, 0u);
-      const uint16_t ck = fletcher16_state<P>(tr);
+    __syncthreads();  // every lane has read the trunk and its checksum
+    if (trunk_thread) {
 #pragma unroll
       for (int k = 0; k < F; k++) lds_trunk[threadIdx.x][k] = tr.w[k];
-      lds_ck[threadIdx.x] = ck;
+      lds_ck[threadIdx.x] = tr_ck;
       if (s2 * p.B >= lane0) {  // this block holds the session's branch-0 lane
         store_state<P>(tr, rp.trunk + s2, p.S);
-        rp.report_ck[s2] = ck;
-        if (rp.copy_ck && r + 1 == rp.n) rp.copy_ck[s2] = ck;
+        rp.report_ck[s2] = tr_ck;
+        if (rp.copy_ck && r + 1 == rp.n) rp.copy_ck[s2] = tr_ck;
       }
     }
     __syncthreads();
+    last = truth;
+    truth = truth_next;
     row_c = wrap_inc(row_c, p.cap);
     slot_c = wrap_inc(slot_c, p.R);
   }
