@@ -400,23 +400,25 @@ __device__ inline uint32_t fletcher_from_doubled(uint32_t d1, uint32_t d2) {
   return (r2 << 7) | (r1 >> 1);
 }
 
+// Doubled sums (byte weights <= 2 * 116 = 232 still fit v_dot4's u8 lanes; d2 <= 2 * 255 * n(n+1)/2
+// < 2^22 at P = 4), reduced by fletcher_from_doubled's full-rate 24-bit multiplies instead of two
+// `% 255` (a quarter-rate v_mul_hi_u32 each).
 template <int P>
 __device__ inline uint16_t fletcher16_state(const BoxState<P>& s) {
   constexpr int n = Fletcher<P>::n;
   constexpr int F = state_fields(P);
   // two independent accumulator pairs halve the dependent v_dot4 chain
-  uint32_t a1 = Fletcher<P>::kSum1Const, a2 = Fletcher<P>::kSum2Const, b1 = 0, b2 = 0;
+  uint32_t a1 = 2u * Fletcher<P>::kSum1Const, a2 = 2u * Fletcher<P>::kSum2Const, b1 = 0, b2 = 0;
 #pragma unroll
   for (int k = 0; k < F; k += 2) {
-    a1 = dot4_u8(s.w[k], 0x01010101u, a1);
-    a2 = dot4_u8(s.w[k], weights_at(n, fld_offset(P, k)), a2);
+    a1 = dot4_u8(s.w[k], 0x02020202u, a1);
+    a2 = dot4_u8(s.w[k], 2u * weights_at(n, fld_offset(P, k)), a2);
     if (k + 1 < F) {
-      b1 = dot4_u8(s.w[k + 1], 0x01010101u, b1);
-      b2 = dot4_u8(s.w[k + 1], weights_at(n, fld_offset(P, k + 1)), b2);
+      b1 = dot4_u8(s.w[k + 1], 0x02020202u, b1);
+      b2 = dot4_u8(s.w[k + 1], 2u * weights_at(n, fld_offset(P, k + 1)), b2);
     }
   }
-  const uint32_t s1 = a1 + b1, s2 = a2 + b2;
-  return (uint16_t)(((s2 % 255u) << 8) | (s1 % 255u));
+  return (uint16_t)fletcher_from_doubled(a1 + b1, a2 + b2);
 }
 
 // Host mirror of the same closed form (used by the C ABI's host-side helpers/tests).
