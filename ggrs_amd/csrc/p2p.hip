@@ -567,7 +567,10 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
         st = pre;
         slot_h = pre_slot;
       } else {
-        slot_h = load % p.R;
+        // load >= f - max_prediction (the remote input of frame f - D arrives at call f, D <
+        // max_prediction), so its slot is slot_f - (f - load) with at most one wrap
+        const int32_t sh = slot_f - (f - load);
+        slot_h = sh < 0 ? sh + p.R : sh;
         cell_load(st, slot_h);
       }
 #pragma unroll
