@@ -489,9 +489,10 @@ __global__ __launch_bounds__(kLaneBlock) void lane_requests_kernel(LaneBatchPara
 //     tools/server_probe.hip) and relays the word through device memory, where the other blocks
 //     poll it with agent-scope loads;
 //   * each block writes its checksums and results with system-scope stores (no device-cache
-//     write-back needed) and waits for them; the last block to finish (a device-memory counter
-//     that also sums the blocks' failed sessions) stores the epoch and the batch's failure count
-//     into the host's 64-bit done word, so the host scans lane results only when one failed.
+//     write-back needed), waits for them, and stores the epoch and its count of failed sessions
+//     into its own 64-bit done slot in host memory; the host waits for every slot (no device
+//     atomic or last-block hand-off on the way back) and scans lane results only when a block
+//     counted a failure.
 // A lane's state stays in registers between batches and goes back to `cur` when the server exits:
 // on the quit bit, or when no batch arrived for `idle_ticks` of the constant wall clock (a watchdog
 // every block reaches, so an abandoned server drains by itself).
@@ -507,11 +508,10 @@ __host__ __device__ constexpr bool quit(uint64_t c) { return (c & kQuit) != 0; }
 
 struct ServerDev {  // device memory
   uint64_t relay;   // block 0's copy of the control word for the other blocks
-  uint64_t count;   // this batch: blocks finished (low 32 bits), failed sessions (high 32 bits)
 };
 
 template <int P>
-__global__ __launch_bounds__(kLaneBlock) void lane_server_kernel(LaneBatchParams p, const uint64_t* ctl, uint64_t* done,
+__global__ __launch_bounds__(kLaneBlock) void lane_server_kernel(LaneBatchParams p, const uint64_t* ctl, uint64_t* slots,
                                                             ServerDev* dev, int32_t start_epoch, int64_t idle_ticks) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   __shared__ uint64_t s_ctl;
@@ -520,7 +520,6 @@ __global__ __launch_bounds__(kLaneBlock) void lane_server_kernel(LaneBatchParams
   const int pl = wl % Pp;
   const int64_t lane = (int64_t)blockIdx.x * LaneGeom<P>::kSessions + wl / Pp;
   const bool valid = lane < p.L;
-  const uint32_t nblocks = gridDim.x;
   Slice st;
   load_slice<P>(st, p.cur + (valid ? lane : 0), p.L, pl);
   int32_t last = start_epoch;
@@ -562,17 +561,9 @@ __global__ __launch_bounds__(kLaneBlock) void lane_server_kernel(LaneBatchParams
     const int fails = run_lanes<P>(q, st, lds);  // returns after this thread's host stores left
     __syncthreads();
     const int32_t e = ctlw::epoch(c);
-    if (wl == 0) {
-      const uint64_t mine = 1ull | ((uint64_t)fails << 32);
-      const uint64_t old = __hip_atomic_fetch_add(&dev->count, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((uint32_t)old == nblocks - 1) {  // the batch's last block: reset the counter, tell the host
-        const uint64_t total = old + mine;
-        __hip_atomic_store(&dev->count, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // the reset is done before the host can publish again
-        __hip_atomic_store(done, (uint64_t)(uint32_t)e | (total & 0xffffffff00000000ull), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-    }
+    if (wl == 0)  // this block's part of the batch is in host memory
+      __hip_atomic_store(&slots[blockIdx.x], (uint64_t)(uint32_t)e | ((uint64_t)(uint32_t)fails << 32), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
     last = e;
   }
   if (valid) store_slice<P>(st, p.cur + lane, p.L, pl);
@@ -670,9 +661,9 @@ int server_start(ggrs_engine* e) {
   LaneServerHost& s = e->server;
   const int64_t L = e->cfg.num_lanes;
   s.blocks = (int32_t)grid_of(L, kLaneBlock / padded_players(e->cfg.num_players));
-  if (!s.mem) {
-    HIP_TRY(hipHostMalloc((void**)&s.mem, 64, hipHostMallocMapped | hipHostMallocCoherent));
-    std::memset(s.mem, 0, 64);
+  if (!s.mem) {  // control word, then one 64-bit done slot per block
+    HIP_TRY(hipHostMalloc((void**)&s.mem, 64 + 8 * (size_t)s.blocks, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(s.mem, 0, 64 + 8 * (size_t)s.blocks);
     HIP_TRY(hipMalloc(&s.dev, sizeof(ServerDev)));
     int rate_khz = 0;
     HIP_TRY(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, e->cfg.device));
@@ -680,14 +671,14 @@ int server_start(ggrs_engine* e) {
   }
   uint64_t* ctl = (uint64_t*)s.mem;
   __atomic_store_n(ctl, ctlw::pack(s.epoch, 0, 0, 0, 0, 0), __ATOMIC_RELEASE);
-  ServerDev init{ctlw::pack(s.epoch, 0, 0, 0, 0, 0), 0ull};
+  ServerDev init{ctlw::pack(s.epoch, 0, 0, 0, 0, 0)};
   HIP_TRY(hipMemcpyAsync(s.dev, &init, sizeof init, hipMemcpyHostToDevice, e->stream));
   const LaneBatchHost& b = e->batch;
   LaneBatchParams p = batch_params(e, b.words, b.loads, b.adv, b.saves, 1);
   if (!p.tokens || !p.load_frames || !p.inputs || !p.status || !p.cks || !p.result)
     return set_error(GGRS_E_HIP, "hipHostGetDevicePointer failed for the lane batch");
   const uint64_t* dctl = device_view((const uint64_t*)ctl);
-  uint64_t* ddone = device_view((uint64_t*)(s.mem + 8));
+  uint64_t* ddone = device_view((uint64_t*)(s.mem + 64));
   if (!dctl || !ddone) return set_error(GGRS_E_HIP, "hipHostGetDevicePointer failed for the lane server");
   const size_t lds = LaneLds(e->cfg.num_players, b.words, b.loads, e->R, b.adv, b.saves, 1).bytes;
   // every block must be resident at once (block 0 relays the batches to the others)
@@ -725,13 +716,21 @@ int server_run(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int 
     if (!s.enabled) return GGRS_E_STATE;  // caller falls back to a launch per batch
   }
   uint64_t* ctl = (uint64_t*)s.mem;
-  const uint64_t* done = (const uint64_t*)(s.mem + 8);
+  const uint64_t* slots = (const uint64_t*)(s.mem + 64);
   const int32_t ep = ++s.epoch;
   __atomic_store_n(ctl, ctlw::pack(ep, W, LD, A, S, use_status), __ATOMIC_RELEASE);  // after the batch rows
   const double t0 = now_s();
   int spins = 0;
-  uint64_t d;
-  while ((int32_t)(uint32_t)(d = __atomic_load_n(done, __ATOMIC_ACQUIRE)) != ep) {
+  int32_t b = 0;
+  uint32_t failed = 0;
+  for (;;) {  // every block's slot holds this epoch (blocks finish in any order)
+    while (b < s.blocks) {
+      const uint64_t d = __atomic_load_n(&slots[b], __ATOMIC_ACQUIRE);
+      if ((int32_t)(uint32_t)d != ep) break;
+      failed += (uint32_t)(d >> 32);
+      ++b;
+    }
+    if (b == s.blocks) break;
     _mm_pause();
     if (++spins == 4096) {
       spins = 0;
@@ -742,7 +741,7 @@ int server_run(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int 
     }
   }
   s.last_done = now_s();
-  *fails = (int32_t)(d >> 32);
+  *fails = (int32_t)failed;
   return GGRS_OK;
 }
 
