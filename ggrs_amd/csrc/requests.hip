@@ -124,6 +124,26 @@ __device__ inline uint32_t slice_fletcher(const Slice& s, int pl) {
   return fletcher_from_doubled(d1, d2);
 }
 
+// State::advance for this lane's player through the lean step, with the sin/cos of its rot
+// supplied (sn, cs) and the NEXT step's computed by the step's hook as soon as the new rot exists
+// (rot does not depend on the velocity chain, so the two run side by side, as in the v5 SyncTest
+// kernel).  Only for states in the lean step's rotation domain (the caller's wave-wide test).
+__device__ inline void slice_advance_lean(Slice& s, uint32_t in, bool owner, float& sn, float& cs) {
+  s.frame = (uint32_t)((int32_t)s.frame + 1);
+  float x = __builtin_bit_cast(float, s.w[0]), y = __builtin_bit_cast(float, s.w[1]);
+  float vx = __builtin_bit_cast(float, s.w[2]), vy = __builtin_bit_cast(float, s.w[3]);
+  float rot = __builtin_bit_cast(float, s.w[4]);
+  const float s0 = sn, c0 = cs;
+  advance_player_lean_sc(x, y, vx, vy, rot, in, s0, c0, [&](float r) { glibc_sincosf_domain(r, &sn, &cs); });
+  if (owner) {
+    s.w[0] = __builtin_bit_cast(uint32_t, x);
+    s.w[1] = __builtin_bit_cast(uint32_t, y);
+    s.w[2] = __builtin_bit_cast(uint32_t, vx);
+    s.w[3] = __builtin_bit_cast(uint32_t, vy);
+    s.w[4] = __builtin_bit_cast(uint32_t, rot);
+  }
+}
+
 // State::advance for this lane's player (input byte `in`, already 4 for a Disconnected player)
 __device__ inline void slice_advance(Slice& s, uint32_t in, bool owner) {
   s.frame = (uint32_t)((int32_t)s.frame + 1);
@@ -423,6 +443,12 @@ __device__ inline int run_lanes(const LaneBatchParams& p, Slice& st, uint8_t* ld
 #pragma unroll
         for (int q = 0; q < 5; q++) st.w[q] = owner ? cell[fo[q]] : 0u;
       };
+      // every state a list steps is this lane's current one or a ring cell this engine saved, so one
+      // wave-wide rotation-domain test here selects the lean step for the whole list; the lean
+      // step carries sin/cos of the state's rot one step ahead (recomputed after a Load)
+      const bool lean = __all(st.w[4] <= kTwoPiBits);
+      float sn = 0.0f, cs = 1.0f;
+      if (lean) glibc_sincosf_domain(__builtin_bit_cast(float, st.w[4]), &sn, &cs);
       for (int k = 0; k < n_tok; k++) {
         const uint32_t t = token(k);
         if (t == GGRS_TOK_END) break;
@@ -438,12 +464,14 @@ __device__ inline int run_lanes(const LaneBatchParams& p, Slice& st, uint8_t* ld
           const int32_t f = l_load[nl * KS + col];
           slot = f % R;
           load_cell(p.ring + slot * slot_stride);
+          if (lean) glibc_sincosf_domain(__builtin_bit_cast(float, st.w[4]), &sn, &cs);
           ++nl;
         } else {  // advance_frame (:115-127); Disconnected players spin (input 4, :277-281)
           const size_t at = (size_t)g.in_pitch * na + col * P + pl;
           uint32_t in = owner ? l_in[at] : 0u;
           if (p.use_status && owner && l_st[at] == GGRS_STATUS_DISCONNECTED) in = 4u;
-          slice_advance(st, in, owner);
+          if (lean) slice_advance_lean(st, in, owner, sn, cs);
+          else slice_advance(st, in, owner);
           if (p.trace) {
             const uint32_t ck = slice_fletcher<P>(st, pl);
             if (pl == 0) p.trace[(int64_t)(((int32_t)st.frame - 1) % p.trace_cap) * L + lane] = (uint16_t)ck;
