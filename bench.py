@@ -102,7 +102,19 @@ def setup_dist(args):
             dist.init_process_group("gloo")
         else:
             torch.cuda.set_device(local_rank)
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            # RCCL prints a version banner to stdout when its first communicator is created; the
+            # driver reads rank 0's stdout as the ONE JSON line, so the banner goes to stderr
+            import ctypes
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+                dist.barrier()
+                ctypes.CDLL(None).fflush(None)
+            finally:
+                os.dup2(saved, 1)
+                os.close(saved)
     return world, rank, local_rank, torch, dist
 
 
@@ -133,7 +145,7 @@ def run_branch(args):
     # more than one rank: every round's report is all-gathered, stream-ordered behind the confirm
     # on the device (exchange.ReportExchange: no host synchronisation in the round loop, round r's
     # all-gather overlapping round r+1's speculation); one rank: rounds run fused in one launch
-    ex = exchange.ReportExchange(eng, peers=args.peers) if dist is not None else None
+    ex = exchange.ReportExchange(eng, peers=args.peers, batch=args.exchange_batch) if dist is not None else None
 
     def sync_all():
         eng.synchronize()
@@ -143,7 +155,7 @@ def run_branch(args):
 
     for _ in range(args.warmup * rps):
         if ex is not None:
-            ex.step()
+            ex.run(1)
         else:
             eng.speculate()
             eng.confirm()
@@ -156,8 +168,7 @@ def run_branch(args):
         for _ in range(args.steps):
             eng.rounds(rps)  # one GPU: no exchange between rounds, one fused launch per step
     else:
-        for _ in range(args.steps * rps):
-            ex.step()
+        ex.run(args.steps * rps)  # a batch of rounds per launch and per all-gather
         ex.drain()
     sync_all()
     t1 = time.perf_counter()
@@ -209,7 +220,10 @@ def run_branch(args):
                        "prefix_distinct_frames_per_s": round(distinct * rps * args.steps * world / elapsed, 1),
                        "rounds_per_step": rps,
                        "parallelism": f"sessions sharded over {world} GPU(s)" + (
-                           ", one stream-ordered RCCL all-gather of the reports per round" if dist is not None else "")},
+                           (", one stream-ordered RCCL all-gather of the reports per round" if args.exchange_batch == 1
+                            else f", {args.exchange_batch} rounds per launch and per stream-ordered RCCL all-gather"
+                                 " of their reports")
+                           if dist is not None else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": pmc_traffic(f"config{args.config}"),
@@ -814,6 +828,8 @@ def main():
     ap.add_argument("--no-lane-server", action="store_true", help="requests: a launch per call")
     ap.add_argument("--rounds-per-step", type=int, default=16, help="configs 3/4: rounds per step")
     ap.add_argument("--sessions", type=int, default=0, help="config 5: sessions per GPU (0 = 8192)")
+    ap.add_argument("--exchange-batch", type=int, default=1,
+                    help="configs 3/4 across ranks: rounds per report all-gather (1 = one per confirmation)")
     ap.add_argument("--peers", action="store_true",
                     help="configs 3/4 and p2p: rank r and r + world/2 run the same sessions (the two "
                          "machines of a match) and compare checksums exchanged over the process group")

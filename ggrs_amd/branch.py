@@ -58,6 +58,8 @@ def _bind(L):
     L.ggrs_branch_round.argtypes = [vp, vp]
     i32 = ctypes.c_int32
     L.ggrs_branch_compare_peer.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp]
+    L.ggrs_branch_compare_peer_rows.argtypes = [vp, vp, i32, i32, i32, i32, i32, i32, vp, vp]
+    L.ggrs_branch_rounds_reports.argtypes = [vp, i32, vp]
     for name in _lib.EXPORTS:
         if name.startswith("ggrs_branch_"):
             getattr(L, name).restype = ctypes.c_int
@@ -136,12 +138,26 @@ class BranchEngine:
         _lib.check(self._L.ggrs_branch_round(self._h, None))
         self._report_into(t)
 
+    def rounds_to_tensor(self, t, n):
+        """n rounds in one launch, round r's report written into row r of device uint8 tensor
+        `t` ([>= n][report_bytes], contiguous) by the kernel (ggrs_branch_rounds_reports)."""
+        if not t.is_cuda or not t.is_contiguous() or t.shape[-1] != self.report_bytes or t.shape[0] < n:
+            raise ValueError("rounds_to_tensor needs a contiguous device tensor [>= n][report_bytes]")
+        _lib.check(self._L.ggrs_branch_rounds_reports(self._h, n, ctypes.c_void_p(t.data_ptr())))
+
     def compare_peer(self, gathered, rank, peer, frame, count, first_frame):
         """Queue the peer checksum comparison of one all-gathered report block (device tensors:
         gathered [world][report_bytes] u8, count and first_frame int64 scalars)."""
         _lib.check(self._L.ggrs_branch_compare_peer(
             self._h, ctypes.c_void_p(gathered.data_ptr()), gathered.shape[0], rank, peer, frame,
             ctypes.c_void_p(count.data_ptr()), ctypes.c_void_p(first_frame.data_ptr())))
+
+    def compare_peer_rows(self, gathered, n_rows, rank, peer, first_frame, count, first):
+        """The same over a batch: gathered [world][rows][report_bytes] u8 (device), rows 0 ..
+        n_rows-1 compared, row k = frame first_frame + k; one launch."""
+        _lib.check(self._L.ggrs_branch_compare_peer_rows(
+            self._h, ctypes.c_void_p(gathered.data_ptr()), gathered.shape[0], gathered.shape[1], n_rows, rank, peer,
+            first_frame, ctypes.c_void_p(count.data_ptr()), ctypes.c_void_p(first.data_ptr())))
 
     def _report_into(self, t):
         ck, bits = self.report()

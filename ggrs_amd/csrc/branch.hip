@@ -162,8 +162,9 @@ struct RoundsParams {
   uint32_t* trunk;
   uint16_t* report_ck;
   uint64_t* report_bits;
-  uint16_t* copy_ck;    // optional second destination of the last round's report (the caller's
-  uint64_t* copy_bits;  // exchange buffer, same layout): saves a device-to-device copy per round
+  uint16_t* copy_ck;    // optional second destination of the reports (the caller's exchange
+  uint64_t* copy_bits;  // buffer, same layout): saves a device-to-device copy per round
+  int64_t copy_stride;  // bytes between rounds' reports there (0: only the last round's)
 };
 constexpr int kRoundsBlock = 256;
 
@@ -266,7 +267,8 @@ __global__ __launch_bounds__(kRoundsBlock) void rounds_kernel(RoundsParams rp) {
     const uint64_t bits = __ballot(survive);
     if (in_range && (threadIdx.x & 63) == 0) {
       rp.report_bits[lane >> 6] = bits;
-      if (rp.copy_bits && r + 1 == rp.n) rp.copy_bits[lane >> 6] = bits;
+      if (rp.copy_bits && (rp.copy_stride || r + 1 == rp.n))
+        reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(rp.copy_bits) + r * rp.copy_stride)[lane >> 6] = bits;
     }
     survived = survive;
     __syncthreads();  // every lane has read the trunk and its checksum
@@ -277,7 +279,8 @@ __global__ __launch_bounds__(kRoundsBlock) void rounds_kernel(RoundsParams rp) {
       if (s2 * p.B >= lane0) {  // this block holds the session's branch-0 lane
         store_state<P>(tr, rp.trunk + s2, p.S);
         rp.report_ck[s2] = tr_ck;
-        if (rp.copy_ck && r + 1 == rp.n) rp.copy_ck[s2] = tr_ck;
+        if (rp.copy_ck && (rp.copy_stride || r + 1 == rp.n))
+          reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(rp.copy_ck) + r * rp.copy_stride)[s2] = tr_ck;
       }
     }
     __syncthreads();
@@ -291,20 +294,31 @@ __global__ __launch_bounds__(kRoundsBlock) void rounds_kernel(RoundsParams rp) {
 // compare_local_checksums_against_peers (p2p_session.rs:904-937) over an all-gathered report
 // block: sessions whose trunk checksum differs between this rank's row and its peer's each count
 // one DesyncDetected (src/lib.rs:158-167); the first round with any is recorded.
-__global__ __launch_bounds__(256) void compare_peer_kernel(const uint8_t* gathered, int64_t row_bytes, int32_t rank,
-                                                           int32_t peer, int64_t S, int32_t frame,
+// gathered = [world][rows][report_bytes]; blockIdx.y = the row (round) compared.  Rows are
+// visited in any order, so the first round with a desync is an atomicMin over the rows' frames
+// (first starts at -1 = none: the min runs on frame + 1 and is stored back minus one).
+__global__ __launch_bounds__(256) void compare_peer_kernel(const uint8_t* gathered, int64_t report_bytes, int32_t rows,
+                                                           int32_t rank, int32_t peer, int64_t S, int32_t frame0,
                                                            unsigned long long* count, unsigned long long* first) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int32_t row = blockIdx.y;
   bool bad = false;
   if (s < S) {
-    const uint16_t* mine = (const uint16_t*)(gathered + (int64_t)rank * row_bytes);
-    const uint16_t* theirs = (const uint16_t*)(gathered + (int64_t)peer * row_bytes);
+    const uint16_t* mine = (const uint16_t*)(gathered + ((int64_t)rank * rows + row) * report_bytes);
+    const uint16_t* theirs = (const uint16_t*)(gathered + ((int64_t)peer * rows + row) * report_bytes);
     bad = mine[s] != theirs[s];
   }
   const uint64_t m = __ballot(bad);
   if ((threadIdx.x & 63) == 0 && m) {
     atomicAdd(count, (unsigned long long)__popcll(m));
-    atomicCAS(first, ~0ull, (unsigned long long)(int64_t)frame);
+    // first: -1 (all ones) or the earliest frame so far; as unsigned, frame + 1 orders -1 last
+    const unsigned long long f = (unsigned long long)(int64_t)(frame0 + row);
+    unsigned long long cur = *(volatile unsigned long long*)first;
+    while (cur + 1ull == 0ull || f < cur) {
+      const unsigned long long prev = atomicCAS(first, cur, f);
+      if (prev == cur) break;
+      cur = prev;
+    }
   }
 }
 
@@ -629,7 +643,7 @@ int ggrs_branch_timing_read(ggrs_branch_engine_t* e, float* total_ms, int32_t* l
 namespace {
 
 // n rounds in one rounds_kernel launch; the last round's report also to `copy` (may be null)
-int launch_rounds(ggrs_branch_engine* e, int32_t n_rounds, void* copy) {
+int launch_rounds(ggrs_branch_engine* e, int32_t n_rounds, void* copy, bool every_round = false) {
   RoundsParams rp;
   SpecParams& p = rp.sp;
   p.S = e->cfg.num_sessions;
@@ -658,6 +672,7 @@ int launch_rounds(ggrs_branch_engine* e, int32_t n_rounds, void* copy) {
   rp.report_bits = (uint64_t*)(e->report + report_ck_bytes(p.S));
   rp.copy_ck = copy ? (uint16_t*)copy : nullptr;
   rp.copy_bits = copy ? (uint64_t*)((uint8_t*)copy + report_ck_bytes(p.S)) : nullptr;
+  rp.copy_stride = every_round ? (int64_t)e->report_bytes : 0;
   // counted as the 2 n speculate + confirm launches it replaces
   int rc = branch_launch_timed(e, [&] {
     dispatch_players(p.P, [&](auto PC) {
@@ -701,6 +716,15 @@ int ggrs_branch_round(ggrs_branch_engine_t* e, void* report_device) {
   return launch_rounds(e, 1, report_device);
 }
 
+int ggrs_branch_rounds_reports(ggrs_branch_engine_t* e, int32_t n_rounds, void* reports_device) {
+  if (!e || !reports_device) return set_error(GGRS_E_INVALID, "null argument");
+  if (n_rounds < 0) return set_error(GGRS_E_INVALID, "negative round count");
+  if (n_rounds == 0) return GGRS_OK;
+  if (int rc = check_rounds_queued(e, n_rounds)) return rc;
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  return launch_rounds(e, n_rounds, reports_device, true);
+}
+
 int ggrs_branch_compare_peer(ggrs_branch_engine_t* e, const void* gathered, int32_t world, int32_t rank,
                              int32_t peer, int32_t frame, int64_t* count_device, int64_t* first_frame_device) {
   if (!e || !gathered || !count_device || !first_frame_device) return set_error(GGRS_E_INVALID, "null argument");
@@ -708,10 +732,29 @@ int ggrs_branch_compare_peer(ggrs_branch_engine_t* e, const void* gathered, int3
     return set_error(GGRS_E_INVALID, "rank %d / peer %d out of range for world %d", rank, peer, world);
   HIP_TRY(hipSetDevice(e->cfg.device));
   const int64_t S = e->cfg.num_sessions;
-  compare_peer_kernel<<<grid_of(S, 256), 256, 0, e->stream>>>((const uint8_t*)gathered, (int64_t)e->report_bytes,
+  compare_peer_kernel<<<grid_of(S, 256), 256, 0, e->stream>>>((const uint8_t*)gathered, (int64_t)e->report_bytes, 1,
                                                              rank, peer, S, frame,
                                                              (unsigned long long*)count_device,
                                                              (unsigned long long*)first_frame_device);
+  HIP_TRY(hipGetLastError());
+  return GGRS_OK;
+}
+
+int ggrs_branch_compare_peer_rows(ggrs_branch_engine_t* e, const void* gathered, int32_t world, int32_t rows_per_rank,
+                                  int32_t n_rows, int32_t rank, int32_t peer, int32_t first_frame,
+                                  int64_t* count_device, int64_t* first_frame_device) {
+  if (!e || !gathered || !count_device || !first_frame_device) return set_error(GGRS_E_INVALID, "null argument");
+  if (world < 2 || rank < 0 || rank >= world || peer < 0 || peer >= world || peer == rank)
+    return set_error(GGRS_E_INVALID, "rank %d / peer %d out of range for world %d", rank, peer, world);
+  if (rows_per_rank < 1 || n_rows < 0 || n_rows > rows_per_rank || n_rows > 65535)
+    return set_error(GGRS_E_INVALID, "%d rows of %d per rank", n_rows, rows_per_rank);
+  if (n_rows == 0) return GGRS_OK;
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const int64_t S = e->cfg.num_sessions;
+  const dim3 grid((unsigned)grid_of(S, 256), (unsigned)n_rows);
+  compare_peer_kernel<<<grid, 256, 0, e->stream>>>((const uint8_t*)gathered, (int64_t)e->report_bytes, rows_per_rank,
+                                                  rank, peer, S, first_frame, (unsigned long long*)count_device,
+                                                  (unsigned long long*)first_frame_device);
   HIP_TRY(hipGetLastError());
   return GGRS_OK;
 }

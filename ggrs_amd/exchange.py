@@ -109,20 +109,25 @@ def exchange_p2p_reports(detector, group=None):
 
 
 class ReportExchange:
-    """Stream-ordered exchange of branch-engine reports (configs 3/4 across GPUs), one all-gather
-    per confirmation with no host synchronisation in the round loop.
+    """Stream-ordered exchange of branch-engine reports (configs 3/4 across GPUs): one all-gather
+    per batch of `batch` confirmations (default 1: one per confirmation) with no host
+    synchronisation in the round loop.
 
     The engine runs on the caller's current stream (BranchEngine.set_stream), so per round r:
-      round(r) -> report buffer r % 2      -- one launch (speculate + confirm, ggrs_branch_round),
-                                              the kernel writing the report into the buffer
-      wait for all-gather(r-1)             -- a device-side stream wait (work.wait()), after which
-                                              its peer comparison is queued on the device
-                                              (ggrs_branch_compare_peer, one small kernel)
-      all-gather(r) of that buffer         -- async on the collective's stream, which orders itself
-                                              after the current stream
-    so round r-1's all-gather overlaps round r's kernel (it only needs round r-1's report), and the
-    double-buffered report of round r-1 is never overwritten before its all-gather has read it
-    (round r+1 writes it after the current stream has waited for that all-gather).
+      round(r) -> row r % batch of report buffer (r // batch) % 2  -- one launch (speculate +
+                                              confirm, ggrs_branch_round), the kernel writing the
+                                              report into the buffer
+    and after the batch's last round:
+      wait for the previous batch's all-gather -- a device-side stream wait (work.wait()), after
+                                              which its peer comparison is queued on the device
+                                              (ggrs_branch_compare_peer_rows, one small kernel)
+      all-gather of this batch's buffer      -- async on the collective's stream, which orders
+                                              itself after the current stream
+    so a batch's all-gather overlaps the next batch's kernels, and a buffer is never overwritten
+    before its all-gather has read it (the next batch writing into it is queued after the current
+    stream has waited for that all-gather).  The reference sends its checksum reports every
+    `DesyncDetection::On { interval }` frames (p2p_session.rs:939-962); `batch` plays that role
+    for the collective, amortising its latency (~20 us per all-gather on one MI355X) over rounds.
     With `peers` (rank r and rank r + world/2 run the same sessions, the two machines of each match)
     every round's session checksums are compared with the peer replica's on the device
     (compare_local_checksums_against_peers, p2p_session.rs:904-937): `desync_count` counts
@@ -130,9 +135,11 @@ class ReportExchange:
     Works over RCCL (device tensors) and gloo (CPU tensors, for tests; gloo's wait blocks the
     host, and the comparison runs as torch ops on the host)."""
 
-    def __init__(self, engine, group=None, peers=False, keep_history=False, device=None):
+    def __init__(self, engine, group=None, peers=False, keep_history=False, device=None, batch=1):
         import torch
         import torch.distributed as dist
+        if batch < 1:
+            raise ValueError(f"batch must be >= 1, got {batch}")
         self.eng = engine
         self.group = group
         self.world = dist.get_world_size(group)
@@ -143,10 +150,12 @@ class ReportExchange:
                                                  if self.nccl else torch.device("cpu"))
         n = engine.report_bytes
         self.S = engine.num_sessions
-        self.bufs = [torch.zeros(n, dtype=torch.uint8, device=dev) for _ in range(2)]
-        self.gathered = [torch.zeros((self.world, n), dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.batch = batch
+        self.bufs = [torch.zeros((batch, n), dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.gathered = [torch.zeros((self.world, batch, n), dtype=torch.uint8, device=dev) for _ in range(2)]
         self.work = [None, None]
-        self.frame_of = [None, None]
+        self.frame_of = [None, None]   # frame of the batch's first round
+        self.rows_of = [0, 0]          # rounds in the batch
         self.round = 0
         self.desync_count = torch.zeros((), dtype=torch.int64, device=dev)
         self.first_desync_round = torch.full((), -1, dtype=torch.int64, device=dev)
@@ -163,40 +172,79 @@ class ReportExchange:
         w.wait()
         self.work[k] = None
         g = self.gathered[k]
+        rows = self.rows_of[k]
         if self.history is not None:
-            self.history.append((self.frame_of[k], g.clone()))
+            for j in range(rows):
+                self.history.append((self.frame_of[k] + j, g[:, j].clone()))
         if self.peer is None:
             return
         if self.nccl:
-            self.eng.compare_peer(g, self.rank, self.peer, self.frame_of[k], self.desync_count,
-                                  self.first_desync_round)
+            self.eng.compare_peer_rows(g, rows, self.rank, self.peer, self.frame_of[k], self.desync_count,
+                                       self.first_desync_round)
             return
         ck = 2 * self.S
-        mine = g[self.rank, :ck].view(torch.int16)
-        theirs = g[self.peer, :ck].view(torch.int16)
-        n = (mine != theirs).sum()
-        first = torch.where((n > 0) & (self.first_desync_round < 0),
-                            torch.full_like(self.first_desync_round, self.frame_of[k]), self.first_desync_round)
-        self.desync_count += n
-        self.first_desync_round.copy_(first)
+        for j in range(rows):
+            mine = g[self.rank, j, :ck].view(torch.int16)
+            theirs = g[self.peer, j, :ck].view(torch.int16)
+            n = (mine != theirs).sum()
+            first = torch.where((n > 0) & (self.first_desync_round < 0),
+                                torch.full_like(self.first_desync_round, self.frame_of[k] + j),
+                                self.first_desync_round)
+            self.desync_count += n
+            self.first_desync_round.copy_(first)
 
-    def step(self):
-        """One round: the fused round kernel, finish the previous all-gather, start this one."""
+    def _start(self, k, rows):
         import torch.distributed as dist
-        k = self.round % 2
-        frame = self.eng.trunk_frame()
-        self.eng.round_to_tensor(self.bufs[k])
-        self._finish(1 - k)
+        self.rows_of[k] = rows
         if self.nccl:
-            self.work[k] = dist.all_gather_into_tensor(self.gathered[k].view(-1), self.bufs[k], group=self.group,
-                                                       async_op=True)
+            self.work[k] = dist.all_gather_into_tensor(self.gathered[k].view(-1), self.bufs[k].view(-1),
+                                                       group=self.group, async_op=True)
         else:  # gloo: CPU tensors
             parts = list(self.gathered[k].unbind(0))
             self.work[k] = dist.all_gather(parts, self.bufs[k], group=self.group, async_op=True)
-        self.frame_of[k] = frame
+
+    def step(self):
+        """One round: the fused round kernel; after a batch's last round, finish the previous
+        batch's all-gather and start this one's."""
+        k = (self.round // self.batch) % 2
+        j = self.round % self.batch
+        if j == 0:
+            self.frame_of[k] = self.eng.trunk_frame()
+        self.eng.round_to_tensor(self.bufs[k][j])
         self.round += 1
+        if j + 1 == self.batch:
+            self._finish(1 - k)
+            self._start(k, self.batch)
+
+    def run(self, n_rounds):
+        """n rounds, a batch's rounds as ONE fused launch (ggrs_branch_rounds_reports: every
+        round's report written into its row of the batch buffer by the kernel) followed by the
+        batch's all-gather -- the same reports, exchanges and comparisons as n step() calls.  Over
+        gloo (host tensors) it is n step() calls."""
+        if not self.nccl or not hasattr(self.eng, "rounds_to_tensor"):
+            for _ in range(n_rounds):
+                self.step()
+            return
+        while n_rounds > 0:
+            k = (self.round // self.batch) % 2
+            j = self.round % self.batch
+            m = min(self.batch - j, n_rounds)
+            if j == 0:
+                self.frame_of[k] = self.eng.trunk_frame()
+            self.eng.rounds_to_tensor(self.bufs[k][j:], m)
+            self.round += m
+            n_rounds -= m
+            if j + m == self.batch:
+                self._finish(1 - k)
+                self._start(k, self.batch)
 
     def drain(self):
-        """Finish the last all-gather (device-side wait) -- call before reading results."""
-        self._finish(self.round % 2)
-        self._finish(1 - self.round % 2)
+        """Start the gather of a partial last batch, finish every all-gather (device-side wait) --
+        call before reading results."""
+        k = (self.round // self.batch) % 2
+        j = self.round % self.batch
+        if j:
+            self._finish(1 - k)
+            self._start(k, j)
+        self._finish(k)
+        self._finish(1 - k)

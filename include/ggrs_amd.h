@@ -308,6 +308,10 @@ int ggrs_branch_set_stream(ggrs_branch_engine_t* eng, void* stream);
  * report_device (device pointer, same layout as ggrs_branch_confirm's copy; NULL = none) by the
  * kernel itself -- the per-round call of the multi-GPU exchange loop. */
 int ggrs_branch_round(ggrs_branch_engine_t* eng, void* report_device);
+/* n rounds as one launch (ggrs_branch_rounds) with every round's report also written by the
+ * kernel into row r of reports_device ([n][report_bytes], device) -- a batch of the multi-GPU
+ * exchange loop, all-gathered once. */
+int ggrs_branch_rounds_reports(ggrs_branch_engine_t* eng, int32_t n_rounds, void* reports_device);
 /* Desync detection between peer replicas (compare_local_checksums_against_peers,
  * p2p_session.rs:904-937): `gathered` = world all-gathered reports ([world][report_bytes], device);
  * sessions whose checksum differs between rows `rank` and `peer` are added to *count_device
@@ -315,6 +319,12 @@ int ggrs_branch_round(ggrs_branch_engine_t* eng, void* report_device);
  * still -1 and any differ.  Enqueued on the engine's stream, no host synchronisation. */
 int ggrs_branch_compare_peer(ggrs_branch_engine_t* eng, const void* gathered, int32_t world, int32_t rank,
                              int32_t peer, int32_t frame, int64_t* count_device, int64_t* first_frame_device);
+/* The same over a batch of rounds gathered at once: `gathered` = [world][rows_per_rank][report_bytes]
+ * (each rank's reports of rows_per_rank consecutive rounds, one all-gather per batch), rows 0 ..
+ * n_rows-1 compared, row k standing for frame first_frame + k; one launch. */
+int ggrs_branch_compare_peer_rows(ggrs_branch_engine_t* eng, const void* gathered, int32_t world,
+                                  int32_t rows_per_rank, int32_t n_rows, int32_t rank, int32_t peer,
+                                  int32_t first_frame, int64_t* count_device, int64_t* first_frame_device);
 
 /* ---------------------------------------------------------------------------------------------
  * Config-5 large-state stress game (defined by this build; ggrs_amd/csrc/particles.h):

@@ -208,6 +208,10 @@ extern "C" {
     pub fn ggrs_branch_set_round_launches(eng: *mut ggrs_branch_engine_t, on: i32) -> i32;
     pub fn ggrs_branch_set_stream(eng: *mut ggrs_branch_engine_t, stream: *mut c_void) -> i32;
     pub fn ggrs_branch_round(eng: *mut ggrs_branch_engine_t, report_device: *mut c_void) -> i32;
+    pub fn ggrs_branch_rounds_reports(eng: *mut ggrs_branch_engine_t, n_rounds: i32, reports_device: *mut c_void) -> i32;
+    pub fn ggrs_branch_compare_peer_rows(eng: *mut ggrs_branch_engine_t, gathered: *const c_void, world: i32,
+                                         rows_per_rank: i32, n_rows: i32, rank: i32, peer: i32, first_frame: i32,
+                                         count_device: *mut i64, first_frame_device: *mut i64) -> i32;
     pub fn ggrs_branch_compare_peer(eng: *mut ggrs_branch_engine_t, gathered: *const c_void, world: i32, rank: i32,
                                     peer: i32, frame: i32, count_device: *mut i64,
                                     first_frame_device: *mut i64) -> i32;

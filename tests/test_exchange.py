@@ -180,14 +180,14 @@ class FakeBranchEngine:
         self.frame += 1
 
 
-def report_exchange_worker(rank, world, port, out):
+def report_exchange_worker(rank, world, port, out, batch=1):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         # rank 0's session 7 desyncs from round 5 on: rank 0 and its peer count it every round
         eng = FakeBranchEngine(rank, corrupt=(7, 5, 0))
-        ex = exchange.ReportExchange(eng, peers=True, keep_history=True)
+        ex = exchange.ReportExchange(eng, peers=True, keep_history=True, batch=batch)
         rounds = 9
         for _ in range(rounds):
             ex.step()
@@ -208,14 +208,15 @@ def report_exchange_worker(rank, world, port, out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_report_exchange_stream_ordered_gloo(world):
-    """ReportExchange (configs 3/4 across GPUs): double-buffered async all-gathers, one per round,
-    results consumed a round later; contents, ordering and peer desync counts."""
+@pytest.mark.parametrize("world,batch", [(2, 1), (4, 1), (2, 4), (4, 3), (2, 9), (2, 16)])
+def test_report_exchange_stream_ordered_gloo(world, batch):
+    """ReportExchange (configs 3/4 across GPUs): double-buffered async all-gathers, one per batch
+    of rounds (9 rounds: full batches, a partial last batch, or one partial batch), results
+    consumed a batch later; contents, ordering and peer desync counts."""
     ctx = mp.get_context("spawn")
     out = ctx.Array("i", world)
     port = free_port()
-    procs = [ctx.Process(target=report_exchange_worker, args=(r, world, port, out)) for r in range(world)]
+    procs = [ctx.Process(target=report_exchange_worker, args=(r, world, port, out, batch)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

@@ -83,3 +83,73 @@ def test_compare_peer_kernel():
     e.compare_peer(g, 0, 1, 9, count, first)
     e.synchronize()
     assert int(count) == 3 and int(first) == 7
+
+
+@pytest.mark.parametrize("batch,fused", [(4, False), (5, False), (4, True), (5, True), (1, True)])
+def test_report_exchange_batched_world1_nccl(oracle, batch, fused):
+    """One all-gather per batch of rounds (12 rounds: full batches and a partial last one), the
+    rounds launched one by one or a batch per launch: the gathered reports still equal every
+    round's report of an exchange-free engine."""
+    import torch.distributed as dist
+    from ggrs_amd import BranchEngine, exchange, synth
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(free_port())
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        S, B, P, W, rounds = 64, 16, 4, 8, 12
+        truth = synth.gen_inputs(3, S, rounds + W + 1, P, synth.MODEL_HELD)
+        engs = []
+        for _ in range(2):
+            e = BranchEngine(S, num_players=P, remote_mask=0b1110, window=W, branches=B, alphabet=16,
+                             input_capacity=rounds + W + 3)
+            e.add_inputs(0, truth)
+            engs.append(e)
+        ex = exchange.ReportExchange(engs[0], peers=False, keep_history=True, batch=batch)
+        if fused:  # whole batches as one launch each (ggrs_branch_rounds_reports), in uneven pieces
+            for n in (3, 1, 8):
+                ex.run(n)
+        else:
+            for _ in range(rounds):
+                ex.step()
+        ex.drain()
+        torch.cuda.synchronize()
+        assert [f for f, _ in ex.history] == list(range(rounds))
+        for f, g in ex.history:
+            engs[1].speculate()
+            engs[1].confirm()
+            ck, bits = engs[1].report()
+            got_ck, got_bits = exchange.split_report(g[0].cpu().numpy(), S, engs[0].num_lanes)
+            assert (got_ck == ck).all() and (got_bits == bits).all(), f
+    finally:
+        dist.destroy_process_group()
+
+
+def test_compare_peer_rows_kernel():
+    """ggrs_branch_compare_peer_rows: a [world][rows][report] block compared row by row in one
+    launch; the count sums every row, the first frame is the earliest row with a difference."""
+    from ggrs_amd import BranchEngine, synth
+    S, B, P, W, rows = 300, 1, 2, 4, 5
+    e = BranchEngine(S, num_players=P, remote_mask=0b10, window=W, branches=B, alphabet=16, input_capacity=16)
+    e.add_inputs(0, synth.gen_inputs(0, S, W + 2, P, synth.MODEL_HELD))
+    buf = torch.zeros(e.report_bytes, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    e.round_to_tensor(buf)
+    e.synchronize()
+    g = buf.repeat(2, rows, 1).contiguous()  # [world 2][rows][report]
+    g[1, 3, 2 * 10] ^= 1     # row 3: session 10
+    g[1, 4, 2 * 11] ^= 4     # row 4: sessions 11 and 299
+    g[1, 4, 2 * 299 + 1] ^= 1
+    g[1, 1, 2 * 42] ^= 1     # row 1: session 42
+    count = torch.zeros((), dtype=torch.int64, device="cuda")
+    first = torch.full((), -1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+    e.compare_peer_rows(g, rows, 0, 1, 20, count, first)
+    e.synchronize()
+    assert int(count) == 4 and int(first) == 21
+    count.zero_()
+    first.fill_(-1)
+    torch.cuda.synchronize()
+    e.compare_peer_rows(g, 3, 0, 1, 30, count, first)  # rows 0..2 of 5 per rank
+    e.synchronize()
+    assert int(count) == 1 and int(first) == 31
