@@ -694,14 +694,18 @@ def run_requests(args):
         drv = ctypes.CDLL(gbuild.build_driver())
         drv.handler_drive_synctest.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
                                                ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
-                                               ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double)]
+                                               ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double),
+                                               ctypes.POINTER(ctypes.c_double)]
+        phases = np.zeros(3)
         inputs = np.ascontiguousarray(inputs)
 
         def run_calls(f, n):
             s, sec = ctypes.c_uint64(), ctypes.c_double()
+            ph = (ctypes.c_double * 3)()
             rc = drv.handler_drive_synctest(eng._h, ctypes.c_void_p(inputs.ctypes.data), L, P, cd, f, n,
-                                            ctypes.byref(s), ctypes.byref(sec))
+                                            ctypes.byref(s), ctypes.byref(sec), ph)
             assert rc == 0, rc
+            phases[:] = list(ph)  # of the last batch of calls (the timed one)
             sink[0] += s.value
     elif form == "batch":
         batch = eng.lane_batch(2, 1, cd + 1, cd + 1)
@@ -757,10 +761,10 @@ def run_requests(args):
     t0 = time.perf_counter()
     run_calls(f, args.steps * calls)  # every call returns with its results in host memory: synchronised
     f += args.steps * calls
+    eng.synchronize()  # stops the idle lane server (a device-wide barrier would wait out its watchdog)
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    eng.synchronize()
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -801,6 +805,8 @@ def run_requests(args):
                                    "back to host memory each call",
                        "sessions_per_gpu": L, "req_form": form, "lane_server": not args.no_lane_server,
                        "us_per_call": round(elapsed / (args.steps * calls) * 1e6, 2),
+                       **({"us_per_call_host_encode_run_handback": [round(x / (args.steps * calls) * 1e6, 2)
+                                                                    for x in phases]} if drv is not None else {}),
                        "parallelism": f"sessions sharded over {world} GPU(s)"},
             "roofline": roofline, "cpu_baseline": cpu_baseline, "parity": parity,
             "note": "latency-bound by construction (one launch and one PCIe round trip per call); the fused "

@@ -40,15 +40,18 @@ static int synctest_tokens(int32_t f, int32_t cd, uint32_t* words, int* nl, int*
 
 /* Runs calls f_begin .. f_begin+n_calls-1 for every lane.  inputs: [frames][L][P] user inputs
  * (input delay 0), resident in host memory.  Returns 0, or the failing ABI code; *seconds = wall
- * time of the calls, *sink = sum of every Save checksum handed back. */
+ * time of the calls, *sink = sum of every Save checksum handed back; phases (may be NULL) gets the
+ * seconds spent encoding, in ggrs_lane_batch_run, and handing checksums back. */
 int handler_drive_synctest(ggrs_engine_t* eng, const uint8_t* inputs, int32_t L, int32_t P, int32_t cd,
-                           int32_t f_begin, int32_t n_calls, uint64_t* sink, double* seconds) {
+                           int32_t f_begin, int32_t n_calls, uint64_t* sink, double* seconds, double* phases) {
+  double t_enc = 0, t_run = 0, t_back = 0;
   ggrs_lane_batch_t b;
   int rc = ggrs_lane_batch_map(eng, 2, 1, cd + 1, cd + 1, &b);
   if (rc) return rc;
   uint64_t acc = 0;
   const double t0 = now_s();
   for (int32_t f = f_begin; f < f_begin + n_calls; f++) {
+    const double ta = now_s();
     uint32_t words[4];
     int nl, na, ns;
     const int W = synctest_tokens(f, cd, words, &nl, &na, &ns);
@@ -64,16 +67,27 @@ int handler_drive_synctest(ggrs_engine_t* eng, const uint8_t* inputs, int32_t L,
     run.adv_rows = na;
     run.save_rows = ns;
     int32_t failed = 0;
+    const double tb = now_s();
     rc = ggrs_lane_batch_run(eng, &run, 0, &failed);
     if (rc) return rc;
+    const double tc = now_s();
     for (int k = 0; k < ns; k++) {  /* row sums in 32 bits: one vectorised pass over the row */
       const uint16_t* row = b.checksums + (size_t)k * L;
       uint32_t s = 0;
       for (int32_t l = 0; l < L; l++) s += row[l];
       acc += s;
     }
+    const double td = now_s();
+    t_enc += tb - ta;
+    t_run += tc - tb;
+    t_back += td - tc;
   }
   *seconds = now_s() - t0;
+  if (phases) {
+    phases[0] = t_enc;
+    phases[1] = t_run;
+    phases[2] = t_back;
+  }
   *sink = acc;
   return 0;
 }

@@ -23,8 +23,8 @@ struct LaneBatchHost {
 
 // the persistent lane server of requests.hip (ggrs_lane_server)
 struct LaneServerHost {
-  uint8_t* mem = nullptr;  // pinned, fine-grained, mapped: 64-bit control word | done word
-  void* dev = nullptr;     // device memory: relay word + finished-block counter
+  uint8_t* mem = nullptr;  // pinned, fine-grained, mapped: 64-bit control word | per-block done slots
+  void* dev = nullptr;     // device memory: the relay word
   bool enabled = true, running = false;
   int32_t epoch = 0;
   int32_t blocks = 0;

@@ -1473,6 +1473,9 @@ int ggrs_synchronize(ggrs_engine_t* e) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
   { int rc_ = resolve(e); if (rc_) return rc_; }
   HIP_TRY(hipSetDevice(e->cfg.device));
+  // an idle lane server is done with its work: stop it (it restarts with the next batch) instead of
+  // waiting out its idle watchdog
+  if (int rc = lane_server_stop(e)) return rc;
   HIP_TRY(hipStreamSynchronize(e->stream));
   return GGRS_OK;
 }
