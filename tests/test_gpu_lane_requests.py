@@ -343,3 +343,35 @@ def test_lane_batch_shape_beyond_lds_is_rejected(oracle):
     b.tokens[:1] = 0xFFFFFFFF  # every lane's list empty
     assert b.run(1, 0, 0, 0) == 0
     assert (b.lane_result == 0).all()
+
+
+def test_synchronize_stops_idle_server(oracle):
+    """ggrs_synchronize ends an idle lane server at once (not after its 1 s idle watchdog) and the
+    next batch restarts it with the lanes' states intact."""
+    import time
+    from ggrs_amd import Engine, encode_lane_lists
+    L, calls, P, maxp = 64, 30, 2, 8
+    streams = p2p_lane_streams(oracle, L, calls, P, maxp, seed=41)
+    exp = expected(oracle, streams, P, maxp)
+    eng = Engine(L, P, maxp, 0, 0)
+    batch = eng.lane_batch(2, 2, 2 * maxp + 2, 2 * maxp + 2)
+    got = [[] for _ in range(L)]
+    for c in range(calls):
+        lists = []
+        for s in streams:
+            idx = np.nonzero(s["call_of"] == c)[0]
+            lists.append([(int(s["kind"][i]), int(s["frame"][i]), s["inputs"][i], s["status"][i]) for i in idx])
+        enc = encode_lane_lists(lists, P)
+        W, LD, A, S = enc["shape"]
+        batch.tokens[:W], batch.load_frames[:LD] = enc["tokens"], enc["load_frames"]
+        batch.inputs[:A], batch.status[:A] = enc["inputs"], enc["status"]
+        assert batch.run(W, LD, A, S, status=True) == 0
+        for l, x in enumerate(lists):
+            got[l].extend(batch.checksums[:sum(1 for r in x if r[0] == REQ_SAVE), l].tolist())
+        if c in (5, 17):
+            t0 = time.perf_counter()
+            eng.synchronize()
+            assert time.perf_counter() - t0 < 0.3
+    for l in range(L):
+        assert got[l] == exp[l]["save_cks"].tolist(), f"lane {l}"
+    check_final(eng, exp, range(0, L, 7))
