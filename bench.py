@@ -912,6 +912,10 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc_traffic(workload),
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+                # SURVEY.md 8(d)'s per-resimulated-frame figure (S + 2) + S / cd + P (53.5 B at cd 8,
+                # two players) instead of this program's per-call count above (57.5 B per frame)
+                "frac_survey_bytes": round(lanes * fps * cd * ((4 + 20 * P + 2) + (4 + 20 * P) / cd + P)
+                                           / avg_launch_s / 1e9 / HBM_PEAK_GBS, 6),
                 "valu": pmc_valu(workload),
                 "note": "issue/latency-bound step kernel (f32 step + f64 glibc sincosf, one wave per "
                         "SIMD); the 2 MB ring fits L2/MALL, so HBM traffic is below the algorithmic bytes"}
