@@ -394,6 +394,39 @@ struct LdsRowsFlat {
   }
 };
 
+// sync_inputs for the flat kernel's LDS rows: the three rows a step may need (local h - delay,
+// confirmed h, last added) are read unconditionally, with indices clamped into the stage (every
+// index the reference reads lies in it: h >= f - D >= lo + delay), and the choices are selects --
+// no exec-mask branches around LDS reads in a wave whose lanes sit at different frames.
+template <int P>
+__device__ inline uint32_t sync_inputs_flat(const P2PParams& p, RemoteQueues<P>& q, int32_t h, int32_t last_added,
+                                            const LdsRowsFlat<P>& rows, uint32_t local_mask) {
+  const uint32_t local_row = rows(max(h - p.delay, rows.lo));
+  const uint32_t h_row = rows(h);
+  const uint32_t last_row = rows(max(last_added, rows.lo));
+  const bool confirmed = last_added != kNull && h <= last_added;
+  const bool prev = !(h == 0 || last_added == kNull);
+  uint32_t in = 0;
+#pragma unroll
+  for (int k = 0; k < P; k++) {
+    uint32_t v;
+    if ((local_mask >> k) & 1u) {
+      v = h >= p.delay ? (local_row >> (8 * k)) & 0xffu : 0u;
+    } else {
+      q.last_req[k] = h;
+      const bool predicting = q.pred_frame[k] >= 0;
+      const bool take_confirmed = !predicting && confirmed;
+      const bool start = !predicting && !confirmed;  // a new prediction from the last added input
+      const uint32_t start_in = prev ? (p.predictor == 0 ? (last_row >> (8 * k)) & 0xffu : 0u) : 0u;
+      q.pred_in[k] = start ? start_in : q.pred_in[k];
+      q.pred_frame[k] = start ? (prev ? last_added : kNull) + 1 : q.pred_frame[k];
+      v = take_confirmed ? (h_row >> (8 * k)) & 0xffu : q.pred_in[k];
+    }
+    in |= v << (8 * k);
+  }
+  return in;
+}
+
 // kLocal >= 0: the local-player mask as a compile-time constant (the two-player configurations),
 // so the per-player local/remote tests of the poll and of synchronized_inputs fold away.
 // kPlain: no desync history, display-checksum trace or debug flip in this launch (host-checked),
@@ -633,7 +666,7 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
       // one step: a replayed frame h or the call's own frame f (non-sparse: SaveGameState(f)
       // first), then AdvanceFrame with synchronized_inputs
       const int32_t fr = replaying ? h : f;
-      const uint32_t in = sync_inputs<P>(p, q, fr, last_added, rows, lmask);
+      const uint32_t in = sync_inputs_flat<P>(p, q, fr, last_added, rows, lmask);
       if (replaying ? (kSparse ? h == confirmed : h > load) : !kSparse) save(fr, replaying ? slot_h : slot_f);
       const uint32_t from = st.w[0];
       if (lean_ok) advance_state_lean<P>(st, in);
