@@ -637,17 +637,16 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
         const int32_t g = f - p.D;
         last_added = g >= 0 ? g : kNull;
         confirmed = g >= 0 ? g : kNull;  // confirmed_frame (:542-553)
-        if (g >= 0) {
-          const uint32_t row = rows(g);
+        {  // the row read unconditionally (clamped into the stage), its effects by selects
+          const uint32_t row = rows(max(g, lo));
 #pragma unroll
           for (int k = 0; k < P; k++) {
             if ((lmask >> k) & 1u) continue;
-            if (q.pred_frame[k] != kNull) {
-              const uint32_t v = (row >> (8 * k)) & 0xffu;
-              if (q.first_inc[k] == kNull && q.pred_in[k] != v) q.first_inc[k] = g;
-              if (q.pred_frame[k] == q.last_req[k] && q.first_inc[k] == kNull) q.pred_frame[k] = kNull;
-              else q.pred_frame[k] += 1;
-            }
+            const bool act = g >= 0 && q.pred_frame[k] != kNull;
+            const uint32_t v = (row >> (8 * k)) & 0xffu;
+            q.first_inc[k] = (act && q.first_inc[k] == kNull && q.pred_in[k] != v) ? g : q.first_inc[k];
+            const bool stop = q.pred_frame[k] == q.last_req[k] && q.first_inc[k] == kNull;
+            q.pred_frame[k] = act ? (stop ? kNull : q.pred_frame[k] + 1) : q.pred_frame[k];
           }
         }
         // 2. the first frame's save
