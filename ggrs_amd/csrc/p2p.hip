@@ -666,7 +666,14 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
       // first), then AdvanceFrame with synchronized_inputs
       const int32_t fr = replaying ? h : f;
       const uint32_t in = sync_inputs_flat<P>(p, q, fr, last_added, rows, lmask);
-      if (replaying ? (kSparse ? h == confirmed : h > load) : !kSparse) save(fr, replaying ? slot_h : slot_f);
+      if (kLds && !kSparse) {
+        // every step saves: the one replay step the reference does not save (h == load, the
+        // frame just loaded) rewrites the loaded cell with the same state and checksum, so the
+        // save needs no branch in a wave whose lanes sit at different frames
+        save(fr, replaying ? slot_h : slot_f);
+      } else if (replaying ? (kSparse ? h == confirmed : h > load) : !kSparse) {
+        save(fr, replaying ? slot_h : slot_f);
+      }
       const uint32_t from = st.w[0];
       if (lean_ok) advance_state_lean<P>(st, in);
       else advance_state<P>(st, in, 0u);
