@@ -678,7 +678,15 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
       if (lean_ok) advance_state_lean<P>(st, in);
       else advance_state<P>(st, in, 0u);
       if (dbg && (int32_t)from == p.dbg_frame) st.w[fld_x(P, 0)] ^= 1u;
-      if (replaying) {
+      if constexpr (kPlain && kLds && !kSparse) {  // the same bookkeeping as selects
+        const bool rep = replaying;
+        slot_h = rep ? next_slot(slot_h) : slot_h;
+        h = rep ? h + 1 : h;
+        replaying = rep && h != f;
+        slot_f = rep ? slot_f : next_slot(slot_f);
+        f = rep ? f : f + 1;
+        at_start = !rep;
+      } else if (replaying) {
         slot_h = next_slot(slot_h);
         if (++h == f) {
           replaying = false;
