@@ -95,26 +95,27 @@ def setup_dist(args):
     # on one GPU: a one-rank RCCL all-gather per round)
     if world > 1 or os.environ.get("GGRS_BENCH_DIST") == "1":
         import torch.distributed as dist
-        if os.environ.get("GGRS_BENCH_BACKEND") == "gloo":
+        gloo = os.environ.get("GGRS_BENCH_BACKEND") == "gloo"
+        if gloo:
             # rehearsal of N ranks on fewer GPUs: ranks share devices, collectives over gloo
             local_rank = local_rank % max(1, torch.cuda.device_count())
-            torch.cuda.set_device(local_rank)
-            dist.init_process_group("gloo")
-        else:
-            torch.cuda.set_device(local_rank)
-            # RCCL prints a version banner to stdout when its first communicator is created; the
-            # driver reads rank 0's stdout as the ONE JSON line, so the banner goes to stderr
-            import ctypes
-            sys.stdout.flush()
-            saved = os.dup(1)
-            os.dup2(2, 1)
-            try:
+        torch.cuda.set_device(local_rank)
+        # RCCL (and gloo) print connection banners to stdout while the group forms; the driver
+        # reads rank 0's stdout as the ONE JSON line, so they go to stderr
+        import ctypes
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            if gloo:
+                dist.init_process_group("gloo")
+            else:
                 dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-                dist.barrier()
-                ctypes.CDLL(None).fflush(None)
-            finally:
-                os.dup2(saved, 1)
-                os.close(saved)
+            dist.barrier()
+            ctypes.CDLL(None).fflush(None)
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
     return world, rank, local_rank, torch, dist
 
 
