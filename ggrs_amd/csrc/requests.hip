@@ -15,10 +15,12 @@
 // its frame, validated against the cell's tag -- the frame field of the lane's ring cell (ring
 // cells start as NULL_FRAME), i.e. GameStateCell.frame (sync_layer.rs:72-78, 248).
 //
-// The kernel: one thread per lane, one 64-lane wavefront per block.  The batch lives in pinned
-// host memory mapped into the device; every row the lane needs is staged into LDS up front (all
-// loads in flight at once: one PCIe round trip instead of one per request), the list is validated
-// against the lane's cell tags (also in LDS), then executed with the state in registers.
+// The kernel: 256-thread lane blocks, a session's players on Pp adjacent lanes.  The batch lives in
+// pinned host memory mapped into the device; each block copies its piece of every row into LDS up
+// front (8-byte words spread over the block's threads, all in flight: one PCIe round trip instead
+// of one per request), each session's list is validated against its cell tags (also in LDS), then
+// executed with the state in registers; checksums collect in LDS and go back to host memory with
+// the lane results as wide system-scope stores.
 #include <hip/hip_runtime.h>
 
 #include <immintrin.h>
