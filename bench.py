@@ -8,9 +8,14 @@ max_prediction 9), 2 players, held-key synthetic inputs.  One step = one fused l
 8 resimulated AdvanceFrames (the metric's unit), 8 SaveGameStates with fused Fletcher-16, the
 checksum comparisons, and the new frame's AdvanceFrame.
 
-Multi-GPU: one process per GPU (torch.distributed.run); sessions are sharded across ranks with no
-data-path collective (SyncTest has no exchange step), so scaling is weak and `value` is the sum
-of all ranks' resimulated session-frames over the max-over-ranks wall time.
+Multi-GPU: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) this process is one
+rank; run plainly with `--gpus N > 1` it first starts the N ranks itself (one torch.distributed.run
+child on 127.0.0.1, launched before anything imports torch or touches the GPU) and forwards rank
+0's line.  Sessions are sharded across ranks with no data-path collective (SyncTest has no
+exchange step), so scaling is weak and `value` is the sum of all ranks' resimulated
+session-frames over the max-over-ranks wall time; the line's `dist` records the process group's
+observed world size, backend and every rank's own figures.  GGRS_BENCH_BACKEND=gloo rehearses N
+ranks on fewer GPUs (ranks share devices).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--frames-per-step F]
     python bench.py --config 3|4 ...   # speculative branch rollback
@@ -81,6 +86,78 @@ def cpu_model():
     except OSError:
         pass
     return "unknown"
+
+
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_launch_cmd(argv, n, port, python=None):
+    """The child command `bench.py --gpus N` runs when it is not itself a rank: one
+    torch.distributed.run that starts N ranks of this script on this node (the driver's own
+    multi-GPU invocation), rendezvous on 127.0.0.1."""
+    return [python or sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def launch_ranks(argv, n, env=None, python=None):
+    """Run N ranks of this bench as ONE child process tree and forward rank 0's JSON line.
+
+    The parent never imports torch or touches the GPU (a process that has initialised the GPU must
+    not exec another program); it starts `torch.distributed.run` as a child, lets the ranks'
+    stderr through, sends any non-JSON stdout to stderr, prints the last JSON line with the
+    launch recorded in it, and returns the child's exit status (non-zero when any rank failed or
+    no line was printed)."""
+    import subprocess
+    env = dict(os.environ if env is None else env)
+    env.pop("WORLD_SIZE", None)
+    cmd = rank_launch_cmd(argv, n, free_port(), python)
+    print("launching: " + " ".join(cmd), file=sys.stderr)
+    proc = subprocess.run(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    line = None
+    for ln in proc.stdout.splitlines():
+        try:
+            obj = json.loads(ln)
+        except ValueError:
+            obj = None
+        if isinstance(obj, dict) and "metric" in obj:
+            line = obj
+        elif ln.strip():
+            print(ln, file=sys.stderr)
+    if proc.returncode != 0:
+        print(f"bench: a rank failed (torch.distributed.run exit {proc.returncode})", file=sys.stderr)
+        return proc.returncode
+    if line is None:
+        print("bench: rank 0 printed no JSON line", file=sys.stderr)
+        return 1
+    line["launch"] = {"launcher": "bench.py -> torch.distributed.run", "ranks_spawned": n}
+    print(json.dumps(line))
+    sys.stdout.flush()
+    return 0
+
+
+def rank_timings(dist, torch, elapsed, units):
+    """Max-over-ranks wall time plus every rank's own figures: (max elapsed, total units, rows).
+    One all-gather of (elapsed, units) per rank; gloo groups gather on the host."""
+    if dist is None:
+        return elapsed, units, [{"rank": 0, "elapsed_s": round(elapsed, 6), "value": round(units / elapsed, 1)}]
+    dev = "cpu" if dist.get_backend() == "gloo" else "cuda"
+    t = torch.tensor([elapsed, float(units)], dtype=torch.float64, device=dev)
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    rows = [o.tolist() for o in out]
+    per = [{"rank": r, "elapsed_s": round(e, 6), "value": round(u / e, 1)} for r, (e, u) in enumerate(rows)]
+    return max(e for e, _ in rows), sum(u for _, u in rows), per
+
+
+def dist_info(dist, per_rank):
+    """What the line records about the process group it was measured in."""
+    if dist is None:
+        return {"world_size": 1, "backend": None, "per_rank": per_rank}
+    return {"world_size": dist.get_world_size(), "backend": dist.get_backend(), "per_rank": per_rank}
 
 
 def setup_dist(args):
@@ -171,17 +248,14 @@ def run_branch(args):
     else:
         ex.run(args.steps * rps)  # a batch of rounds per launch and per all-gather
         ex.drain()
+    kernel_ms, launches = eng.timing_read()  # the end event right behind the last launch
     sync_all()
     t1 = time.perf_counter()
-    kernel_ms, launches = eng.timing_read()
     elapsed = t1 - t0
     n_desync = int(ex.desync_count.item()) if ex is not None else 0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
     resim_round = L * W + S
-    value = resim_round * rps * args.steps * world / elapsed
+    elapsed, total, per_rank = rank_timings(dist, torch, elapsed, resim_round * rps * args.steps)
+    value = total / elapsed
     Sp = 4 + 20 * P
     bytes_round = L * (Sp + W * (Sp + 2) + W * P) + S * (2 * Sp + 2 + P) + 8 * ((L + 63) // 64)
     avg_round_s = kernel_ms / 1e3 / max(launches, 1) * 2  # speculate + confirm launches per round
@@ -224,7 +298,9 @@ def run_branch(args):
                            (", one stream-ordered RCCL all-gather of the reports per round" if args.exchange_batch == 1
                             else f", {args.exchange_batch} rounds per launch and per stream-ordered RCCL all-gather"
                                  " of their reports")
-                           if dist is not None else "")},
+                           if dist is not None else ""),
+                       "exchange_batch": args.exchange_batch if dist is not None else None},
+            "dist": dist_info(dist, per_rank),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": pmc_traffic(f"config{args.config}"),
@@ -260,18 +336,15 @@ def run_particles(args):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         eng.synctest_advance_frames(1)
+    kernel_ms, launches = eng.timing_read()  # the end event right behind the last launch
     eng.synchronize()
     if dist is not None:
         dist.barrier()
     t1 = time.perf_counter()
-    kernel_ms, launches = eng.timing_read()
     elapsed = t1 - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, total, per_rank = rank_timings(dist, torch, elapsed, S * cd * args.steps)
     st, _, _ = eng.mismatches()
-    value = S * cd * args.steps * world / elapsed
+    value = total / elapsed
     Sb = 4 + 100 * N
     bytes_launch = S * (Sb + cd * (Sb + 2) + 2 + 4 * (cd - 1) + (cd + 1) * P)
     avg_s = kernel_ms / 1e3 / max(launches, 1)
@@ -301,6 +374,7 @@ def run_particles(args):
                        "sessions_per_gpu": S, "entities": N, "players": P, "check_distance": cd,
                        "hbm_ring_gb_per_gpu": round(S * Sb * (maxp + 1) / 1e9, 2),
                        "parallelism": f"sessions sharded over {world} GPU(s)"},
+            "dist": dist_info(dist, per_rank),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": pmc_traffic(f"config5_s{S}"),
@@ -359,25 +433,23 @@ def run_p2p(args):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    kernel_ms, launches = eng.timing_read()  # the end event right behind the last launch
     eng.synchronize()
     if dist is not None:
         dist.barrier()
     t1 = time.perf_counter()
-    kernel_ms, launches = eng.timing_read()
     elapsed = t1 - t0
     n_desync = len(events)
+    session_calls = S * calls * args.steps
+    elapsed, total, per_rank = rank_timings(dist, torch, elapsed, session_calls)
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        c = torch.tensor([n_desync], dtype=torch.int64, device="cuda")
+        c = torch.tensor([n_desync], dtype=torch.int64, device="cpu" if dist.get_backend() == "gloo" else "cuda")
         dist.all_reduce(c)
         n_desync = int(c.item())
     rb1, rs1 = eng.stats()
     resim = int((rs1 - rs0).sum())
     rollbacks = int((rb1 - rb0).sum())
-    session_calls = S * calls * args.steps
-    value = session_calls * world / elapsed
+    value = total / elapsed
     F = 5 * P + 1
     # HBM bytes per launch: the state in/out, every save (state + checksum), every rollback load,
     # the queue words in/out and the input rows each call reads (arrival + its own, + replays)
@@ -415,6 +487,7 @@ def run_p2p(args):
                        "sessions_per_gpu": S, "peers": peers, "sparse_saving": bool(args.sparse),
                        "parallelism": f"sessions sharded over {world} GPU(s)"
                                       + (f", peer ranks exchange checksum reports over {dist.get_backend()}" if peers else "")},
+            "dist": dist_info(dist, per_rank),
             "rollbacks_per_session_frame": round(rollbacks / session_calls, 5),
             "advances_per_sec": round((session_calls + resim) * world / elapsed, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
@@ -474,17 +547,14 @@ def run_codec(args):
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, total, per_rank = rank_timings(dist, torch, elapsed, N * args.steps)
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / len(evs)
     dec_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / len(evs)
     out, ln, dec, cnt, st = res
     ln_h = ln.cpu().numpy()
     pkt_bytes = int(ln_h.sum())
     ok = bool((st == 0).all().item()) and bool((cnt == d_cnt).all().item()) and bool((dec == d_pend).all().item())
-    value = N * args.steps * world / elapsed
+    value = total / elapsed
     # algorithmic HBM bytes: encode reads ref + pending + count, writes packets + lengths; decode
     # reads ref + packets + lengths, writes inputs + count + status
     enc_bytes = N * (B + W * B + 4) + pkt_bytes + 4 * N
@@ -523,6 +593,7 @@ def run_codec(args):
                        "packets_per_gpu": N, "pending": W, "input_bytes": B,
                        "mean_packet_bytes": round(pkt_bytes / N, 2),
                        "parallelism": f"packets sharded over {world} GPU(s)"},
+            "dist": dist_info(dist, per_rank),
             "kernel_ms": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4)},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
@@ -766,11 +837,8 @@ def run_requests(args):
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    value = L * cd * calls * args.steps * world / elapsed
+    elapsed, total, per_rank = rank_timings(dist, torch, elapsed, L * cd * calls * args.steps)
+    value = total / elapsed
     parity = None
     if rank == 0:
         try:
@@ -809,11 +877,34 @@ def run_requests(args):
                        **({"us_per_call_host_encode_run_handback": [round(x / (args.steps * calls) * 1e6, 2)
                                                                     for x in phases]} if drv is not None else {}),
                        "parallelism": f"sessions sharded over {world} GPU(s)"},
+            "dist": dist_info(dist, per_rank),
             "roofline": roofline, "cpu_baseline": cpu_baseline, "parity": parity,
             "note": "latency-bound by construction (one launch and one PCIe round trip per call); the fused "
                     "ggrs_synctest_advance_frames path is the default bench"}))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def run_launch_selftest(args):
+    """The launcher's own check, on the CPU: every rank joins a gloo group, the ranks' (RANK,
+    LOCAL_RANK, WORLD_SIZE) are all-gathered and rank 0 prints them as the one JSON line.  Rank
+    --selftest-fail-rank exits with status 3 before joining (exit-status propagation)."""
+    rank = int(os.environ.get("RANK", "0"))
+    if rank == args.selftest_fail_rank:
+        sys.exit(3)
+    import torch
+    import torch.distributed as dist
+    if "WORLD_SIZE" not in os.environ:  # one rank, in process
+        os.environ.update(RANK="0", WORLD_SIZE="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
+    dist.init_process_group("gloo")
+    me =torch.tensor([rank, int(os.environ.get("LOCAL_RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))])
+    out = [torch.empty_like(me) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, me)
+    if rank == 0:
+        print(json.dumps({"metric": "launch-selftest", "value": dist.get_world_size(), "n_gpus": dist.get_world_size(),
+                          "ranks": [o.tolist() for o in out],
+                          "master_addr": os.environ.get("MASTER_ADDR")}))
+    dist.destroy_process_group()
 
 
 def main():
@@ -835,8 +926,9 @@ def main():
     ap.add_argument("--no-lane-server", action="store_true", help="requests: a launch per call")
     ap.add_argument("--rounds-per-step", type=int, default=16, help="configs 3/4: rounds per step")
     ap.add_argument("--sessions", type=int, default=0, help="config 5: sessions per GPU (0 = 8192)")
-    ap.add_argument("--exchange-batch", type=int, default=1,
-                    help="configs 3/4 across ranks: rounds per report all-gather (1 = one per confirmation)")
+    ap.add_argument("--exchange-batch", type=int, default=0,
+                    help="configs 3/4 across ranks: rounds per report all-gather (1 = one per confirmation; "
+                         "0 = --rounds-per-step, one all-gather per step)")
     ap.add_argument("--peers", action="store_true",
                     help="configs 3/4 and p2p: rank r and r + world/2 run the same sessions (the two "
                          "machines of a match) and compare checksums exchanged over the process group")
@@ -845,9 +937,19 @@ def main():
     ap.add_argument("--sparse", action="store_true", help="p2p: sparse saving (SURVEY.md 8f row 4)")
     ap.add_argument("--req-form", choices=["native", "batch", "lanes", "lockstep"], default="native",
                     help="requests: the boundary form (run_requests docstring)")
-    ap.add_argument("--workload", choices=["synctest", "p2p", "codec", "requests"], default="synctest",
-                    help="p2p: the device P2P rollback decision (SURVEY.md 8f), --sessions per GPU")
+    ap.add_argument("--workload", choices=["synctest", "p2p", "codec", "requests", "launch-selftest"],
+                    default="synctest",
+                    help="p2p: the device P2P rollback decision (SURVEY.md 8f), --sessions per GPU; "
+                         "launch-selftest: the rank launcher alone (CPU, gloo; tests/test_bench_launch.py)")
+    ap.add_argument("--selftest-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.exchange_batch <= 0:
+        args.exchange_batch = args.rounds_per_step
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `bench.py --gpus N` run plainly: start the N ranks here (before anything touches the GPU)
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
+    if args.workload == "launch-selftest":
+        return run_launch_selftest(args)
     if args.workload == "p2p":
         return run_p2p(args)
     if args.workload == "codec":
@@ -888,19 +990,14 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         eng.synctest_advance_frames(fps)
+    kernel_ms, launches = eng.timing_read()  # the end event right behind the last launch
     barrier()
     t1 = time.perf_counter()
-    kernel_ms, launches = eng.timing_read()
     elapsed = t1 - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed, total_resim, per_rank = rank_timings(dist, torch, elapsed, lanes * cd * fps * args.steps)
 
     status, _, _ = eng.mismatches()
     halted = int((status != 0).sum())  # a halted lane would stop resimulating: must be none
-    resim_per_rank = lanes * cd * fps * args.steps
-    total_resim = resim_per_rank * world
     value = total_resim / elapsed
 
     # roofline of the one kernel that runs in the timed region (synctest_kernel<2>)
@@ -990,6 +1087,7 @@ def main():
                        "frames_per_step": fps, "players": P, "check_distance": cd,
                        "max_prediction": maxp, "kernel_path": args.path,
                        "parallelism": f"sessions sharded over {world} GPU(s)"},
+            "dist": dist_info(dist, per_rank),
             "roofline": roofline,
             "cpu_baseline": cpu_baseline,
             "halted_lanes": halted,
