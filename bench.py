@@ -731,53 +731,117 @@ def synctest_tokens(f, cd):
     return words, n, int(f > cd), toks.count(TOK_ADVANCE), toks.count(TOK_SAVE)
 
 
+def load_p2p_fixture():
+    """bench_native/fixtures/p2p_lists.npz (bench_native/make_p2p_fixture.py): M P2P sessions'
+    request lists per call, generated once by the oracle's P2PSession stream and committed."""
+    import numpy as np
+    with np.load(os.path.join(ROOT, "bench_native", "fixtures", "p2p_lists.npz")) as z:
+        d = {k: z[k] for k in z.files}
+    M, C = int(d["sessions"]), int(d["calls"])
+    reqs = np.stack([d["kind"].astype(np.int32), d["frame"]], axis=1)
+    # per (session, call): its list length, AdvanceFrames and SaveGameStates, and the batch shape
+    n_req = np.diff(d["req_off"], axis=1)
+    n_adv = np.diff(d["adv_off"], axis=1)
+    is_load = np.concatenate([[0], np.cumsum(d["kind"] == 1)])
+    is_save = np.concatenate([[0], np.cumsum(d["kind"] == 0)])
+    n_load = np.diff(is_load[d["req_off"]], axis=1)
+    n_save = np.diff(is_save[d["req_off"]], axis=1)
+    shape = np.array([-(-int(n_req.max()) // 16), int(n_load.max()), int(n_adv.max()), int(n_save.max())], np.int32)
+    return dict(M=M, C=C, P=int(d["players"]), maxp=int(d["max_prediction"]), reqs=np.ascontiguousarray(reqs),
+                req_off=np.ascontiguousarray(d["req_off"]), adv_off=np.ascontiguousarray(d["adv_off"]),
+                inputs=np.ascontiguousarray(d["inputs"]), status=np.ascontiguousarray(d["status"]),
+                kind=d["kind"], frame=d["frame"], n_adv=n_adv, shape=shape)
+
+
 def run_requests(args):
     """The request-level drop-in boundary (what the Rust request handler of INTEGRATION.md calls
-    once per advance_frame of every session): config-2 sessions, each call the request list
-    SyncTestSession emits at frame f (sync_test_session.rs:85-150: Load f-cd, cd x (Save, Advance)
-    with the first Save skipped, Save f, Advance) for every lane, handed over from host memory and
-    every Save's checksum handed back (what the handler passes to GameStateCell::save).
-      --req-form native  (default) the per-lane lists encoded into the engine's mapped batch by a
-                         C request handler (bench_native/handler_driver.c, what the Rust handler of
-                         INTEGRATION.md does per call: write request kinds, Load frames and input
-                         rows, ggrs_lane_batch_run, read every Save's checksum back), the batches
-                         served by the persistent lane server
-      --req-form batch   the same encoding written from Python (numpy) per call
+    once per advance_frame of every session), every Save's checksum handed back to host memory.
+      --req-form native  (default) SyncTest sessions (config 2: cd 8): every lane's list of
+                         SyncTestSession::advance_frame (sync_test_session.rs:85-150: Load f-cd,
+                         cd x (Save, Advance) with the first Save skipped, Save f, Advance) encoded
+                         into the engines' mapped batches by a C request handler
+                         (bench_native/handler_driver.c: request kinds, Load frames and input rows,
+                         ggrs_lane_batch_submit / _wait, every Save's checksum read back), the batches
+                         served by the persistent lane servers
+      --req-form p2p     every lane its own P2PSession's lists (rollbacks of differing depth,
+                         p2p_session.rs:265-426) from the committed oracle fixture
+                         (bench_native/fixtures/p2p_lists.npz), each lane encoded by ggrs_lane_encode
+                         (the Rust crate's encoder) with its Save frames checked
+      --req-form batch   the SyncTest encoding written from Python (numpy) per call
       --req-form lanes   ggrs_handle_requests_lanes: the GgrsRequest lists themselves (CSR)
       --req-form lockstep  ggrs_handle_requests: one list for every lane (lockstep sessions)
+    --req-groups G (native, p2p; default 2): the sessions served as G lane groups (G engines): each
+    group's batch is on the device while the host hands back and encodes the others';
+    --session-us T: host time per group and call spent in the modelled GGRS session logic (spin).
     One step = `calls` such calls; inputs are resident in host memory before the timed region."""
     world, rank, local_rank, torch, dist = setup_dist(args)
+    import ctypes
+
     import numpy as np
     from ggrs_amd import Engine, synth
     from ggrs_amd._lib import REQ_ADVANCE, REQ_LOAD, REQ_SAVE
     L, P, maxp, cd, calls = args.lanes, 2, 9, 8, 64
-    frames = cd + 1 + (args.warmup + args.steps) * calls
-    inputs = synth.gen_inputs(rank * L, L, frames, P, synth.MODEL_HELD)  # [frames][L][P]
     form = args.req_form
-    eng = Engine(L, P, maxp, cd if form == "lockstep" else 0, 0, device=local_rank, trace_capacity=0)
-    if args.no_lane_server:
-        eng.set_lane_server(False)  # one lane_requests_kernel launch per call (per-launch profiles)
+    G = args.req_groups if form in ("native", "p2p") else 1
+    if L % G:
+        raise SystemExit(f"--lanes {L} is not a multiple of --req-groups {G}")
     sink = np.zeros(1, np.uint64)
-
+    phases = np.zeros(4)
     drv = None
-    if form == "native":
-        import ctypes
+    fx = None
+    if form in ("native", "p2p"):
         from ggrs_amd import build as gbuild
         drv = ctypes.CDLL(gbuild.build_driver())
-        drv.handler_drive_synctest.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
-                                               ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
-                                               ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_double),
-                                               ctypes.POINTER(ctypes.c_double)]
-        phases = np.zeros(3)
+    if form == "p2p":
+        fx = load_p2p_fixture()
+        P, maxp = fx["P"], fx["maxp"]
+        if (args.warmup + args.steps) * calls > fx["C"]:
+            raise SystemExit(f"the P2P fixture holds {fx['C']} calls; --warmup + --steps must cover at most "
+                             f"{fx['C'] // calls} steps of {calls} calls")
+    frames = cd + 1 + (args.warmup + args.steps) * calls
+    inputs = synth.gen_inputs(rank * L, L, frames, P, synth.MODEL_HELD) if form != "p2p" else None  # [frames][L][P]
+    engs = [Engine(L // G, P, maxp, cd if form == "lockstep" else 0, 0, device=local_rank, trace_capacity=0)
+            for _ in range(G)]
+    eng = engs[0]
+    for e in engs:
+        if args.no_lane_server:
+            e.set_lane_server(False)  # one lane_requests_kernel launch per call (per-launch profiles)
+    handles = (ctypes.c_void_p * G)(*[e._h.value for e in engs])
+    dbl = ctypes.POINTER(ctypes.c_double)
+    u64 = ctypes.POINTER(ctypes.c_uint64)
+    lane_frames = np.zeros(L, np.int32)
+
+    def engine_of(lane):
+        return engs[lane // (L // G)], lane % (L // G)
+
+    if form == "native":
         inputs = np.ascontiguousarray(inputs)
+        drv.handler_drive_synctest_groups.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p] + \
+            [ctypes.c_int32] * 5 + [ctypes.c_double, u64, dbl, dbl]
 
         def run_calls(f, n):
             s, sec = ctypes.c_uint64(), ctypes.c_double()
-            ph = (ctypes.c_double * 3)()
-            rc = drv.handler_drive_synctest(eng._h, ctypes.c_void_p(inputs.ctypes.data), L, P, cd, f, n,
-                                            ctypes.byref(s), ctypes.byref(sec), ph)
+            ph = (ctypes.c_double * 4)()
+            rc = drv.handler_drive_synctest_groups(handles, G, ctypes.c_void_p(inputs.ctypes.data), L, P, cd, f, n,
+                                                   args.session_us, ctypes.byref(s), ctypes.byref(sec), ph)
             assert rc == 0, rc
             phases[:] = list(ph)  # of the last batch of calls (the timed one)
+            sink[0] += s.value
+    elif form == "p2p":
+        vp = ctypes.c_void_p
+        drv.handler_drive_p2p_groups.argtypes = [vp, ctypes.c_int32] + [ctypes.c_int32] * 4 + [vp] * 7 + \
+            [ctypes.c_int32, ctypes.c_int32, ctypes.c_double, u64, dbl, dbl]
+
+        def run_calls(c, n):
+            s, sec = ctypes.c_uint64(), ctypes.c_double()
+            ph = (ctypes.c_double * 4)()
+            ptr = lambda a: ctypes.c_void_p(a.ctypes.data)  # noqa: E731
+            rc = drv.handler_drive_p2p_groups(handles, G, L, P, fx["M"], fx["C"], ptr(fx["reqs"]), ptr(fx["req_off"]),
+                                              ptr(fx["adv_off"]), ptr(fx["inputs"]), ptr(fx["status"]),
+                                              ptr(fx["shape"]), ptr(lane_frames), c, n, args.session_us,
+                                              ctypes.byref(s), ctypes.byref(sec), ph)
+            assert rc == 0, (rc, eng._L.ggrs_last_error())
+            phases[:] = list(ph)
             sink[0] += s.value
     elif form == "batch":
         batch = eng.lane_batch(2, 1, cd + 1, cd + 1)
@@ -826,61 +890,103 @@ def run_requests(args):
         def run_calls(f, n):
             for k in range(n):
                 call(f + k)
-    f = cd + 1 + args.warmup * calls  # warm-up frames, then untimed steps
+    # warm-up calls, then the timed ones (SyncTest lists: the first cd + 1 frames carry no rollback)
+    f = (0 if form == "p2p" else cd + 1) + args.warmup * calls
     run_calls(0, f)
     if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
     run_calls(f, args.steps * calls)  # every call returns with its results in host memory: synchronised
+    f_timed = f
     f += args.steps * calls
-    eng.synchronize()  # stops the idle lane server (a device-wide barrier would wait out its watchdog)
+    for e in engs:
+        e.synchronize()  # stops the idle lane server (a device-wide barrier would wait out its watchdog)
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    elapsed, total, per_rank = rank_timings(dist, torch, elapsed, L * cd * calls * args.steps)
+    n_calls = args.steps * calls
+    if form == "p2p":
+        # session-frames: every call of every lane; resimulated: the AdvanceFrames of the rollbacks
+        m_of = np.arange(L) % fx["M"]
+        resim = int(np.maximum(fx["n_adv"][m_of][:, f_timed:f] - 1, 0).sum())
+        units = L * n_calls
+    else:
+        resim = L * cd * n_calls
+        units = resim
+    elapsed, total, per_rank = rank_timings(dist, torch, elapsed, units)
+    _, total_resim, _ = rank_timings(dist, torch, elapsed, resim) if form == "p2p" else (None, total, None)
     value = total / elapsed
     parity = None
     if rank == 0:
         try:
             from oracle import oracle as O
             O.build()
-            r = O.synctest_run(inputs[:f, 0, :], P, maxp, cd, 0)
-            parity = {"lane0_final_state_bit_exact": bytes(eng.state(0)) == bytes(r["final_state"]),
-                      "lane_last_final_state_bit_exact": bytes(eng.state(L - 1)) == bytes(
-                          O.synctest_run(inputs[:f, L - 1, :], P, maxp, cd, 0)["final_state"])}
+            if form == "p2p":
+                ok = {}
+                for lane in (0, L - 1):
+                    m = lane % fx["M"]
+                    a, b = int(fx["req_off"][m, 0]), int(fx["req_off"][m, f])
+                    kind = fx["kind"][a:b].astype(np.int32)
+                    inp = np.zeros((b - a, P), np.uint8)
+                    st = np.zeros((b - a, P), np.uint8)
+                    adv = np.nonzero(kind == REQ_ADVANCE)[0]
+                    a0 = int(fx["adv_off"][m, 0])
+                    inp[adv] = fx["inputs"][a0:a0 + len(adv)]
+                    st[adv] = fx["status"][a0:a0 + len(adv)]
+                    r = O.handler_run(kind, fx["frame"][a:b], inp, st, P, maxp)
+                    e, li = engine_of(lane)
+                    ok[f"lane{lane}_final_state_bit_exact"] = r["rc"] == 0 and bytes(e.state(li)) == bytes(
+                        r["final_state"])
+                parity = ok
+            else:
+                e_last, l_last = engine_of(L - 1)
+                r = O.synctest_run(inputs[:f, 0, :], P, maxp, cd, 0)
+                parity = {"lane0_final_state_bit_exact": bytes(eng.state(0)) == bytes(r["final_state"]),
+                          "lane_last_final_state_bit_exact": bytes(e_last.state(l_last)) == bytes(
+                              O.synctest_run(inputs[:f, L - 1, :], P, maxp, cd, 0)["final_state"])}
         except Exception as exc:
             parity = {"error": repr(exc)}
         cpu_baseline = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and form != "p2p":
             cpu_baseline = requests_cpu_baseline(args, synth, P, maxp, cd)
         # the device work of one call is the SyncTest frame's Load + cd x (Advance, Save) per lane:
         # its algorithmic HBM bytes over the call's wall time (PCIe round trip and host handler
         # included -- the call is latency-bound, so this is far below the HBM roofline)
-        call_s = elapsed / (args.steps * calls)
+        call_s = elapsed / n_calls
         per_call = L * bytes_per_synctest_call(P, cd)
         roofline = {"bound": "hbm", "achieved": round(per_call / call_s / 1e9, 3), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(per_call / call_s / 1e9 / HBM_PEAK_GBS, 6),
                     "traffic": pmc_traffic(f"requests_l{L}"), "algorithmic_bytes_per_call": per_call,
                     "note": "per call: one PCIe round trip (lists + inputs in, checksums out) around a "
-                            "microsecond-scale kernel; latency-bound by construction"}
-        print(json.dumps({
-            "metric": "resimulated session-frames/sec (node), request-level boundary", "value": round(value, 1),
-            "unit": "session-frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+                            "microsecond-scale kernel; latency-bound by construction"} if form != "p2p" else None
+        wl = (f"requests: {L} SyncTest sessions per GPU (cd {cd}, 2 players), each call every session's request "
+              f"list of one advance_frame (form {form})" if form != "p2p" else
+              f"requests: {L} P2P sessions per GPU (2 players, max_prediction {maxp}, remote inputs arriving in "
+              f"jittered bursts), each lane its own session's list per call from the committed oracle fixture "
+              f"({fx['M']} distinct sessions tiled over the lanes), encoded per lane by ggrs_lane_encode")
+        line = {
+            "metric": ("resimulated session-frames/sec (node), request-level boundary" if form != "p2p"
+                       else "P2P session-frames/sec (node), request-level boundary"),
+            "value": round(value, 1), "unit": "session-frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": f"requests: {L} SyncTest sessions per GPU (cd {cd}, 2 players), each call "
-                                   f"every session's request list of one advance_frame (form {form}), "
-                                   f"{calls} calls per step, lists and inputs from host memory, checksums "
-                                   "back to host memory each call",
-                       "sessions_per_gpu": L, "req_form": form, "lane_server": not args.no_lane_server,
-                       "us_per_call": round(elapsed / (args.steps * calls) * 1e6, 2),
-                       **({"us_per_call_host_encode_run_handback": [round(x / (args.steps * calls) * 1e6, 2)
-                                                                    for x in phases]} if drv is not None else {}),
+            "config": {"workload": wl + f", {calls} calls per step, lists and inputs from host memory, checksums "
+                                        "back to host memory each call",
+                       "sessions_per_gpu": L, "req_form": form, "lane_groups": G, "session_us_per_group_call":
+                           args.session_us, "lane_server": not args.no_lane_server,
+                       "us_per_call": round(elapsed / n_calls * 1e6, 2),
+                       **({"us_per_call_host_encode_device_handback_session": [round(x / n_calls * 1e6, 2)
+                                                                              for x in phases]}
+                          if drv is not None else {}),
                        "parallelism": f"sessions sharded over {world} GPU(s)"},
             "dist": dist_info(dist, per_rank),
             "roofline": roofline, "cpu_baseline": cpu_baseline, "parity": parity,
-            "note": "latency-bound by construction (one launch and one PCIe round trip per call); the fused "
-                    "ggrs_synctest_advance_frames path is the default bench"}))
+            "note": "latency-bound by construction (one PCIe round trip per call and lane group); the fused "
+                    "ggrs_synctest_advance_frames path is the default bench"}
+        if form == "p2p":
+            line["resimulated_session_frames_per_s"] = round(total_resim / elapsed, 1)
+            line["resimulated_per_session_frame"] = round(resim / units, 4)
+        print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
 
@@ -935,8 +1041,12 @@ def main():
     ap.add_argument("--p2p-form", choices=["default", "flat", "lockstep", "unstaged"], default="default",
                     help="p2p: kernel form (DESIGN.md section 3)")
     ap.add_argument("--sparse", action="store_true", help="p2p: sparse saving (SURVEY.md 8f row 4)")
-    ap.add_argument("--req-form", choices=["native", "batch", "lanes", "lockstep"], default="native",
+    ap.add_argument("--req-form", choices=["native", "p2p", "batch", "lanes", "lockstep"], default="native",
                     help="requests: the boundary form (run_requests docstring)")
+    ap.add_argument("--req-groups", type=int, default=2,
+                    help="requests (native, p2p): lane groups (engines) whose batches overlap the host's work")
+    ap.add_argument("--session-us", type=float, default=0.0,
+                    help="requests: modelled GGRS session-logic host time per lane group and call (us)")
     ap.add_argument("--workload", choices=["synctest", "p2p", "codec", "requests", "launch-selftest"],
                     default="synctest",
                     help="p2p: the device P2P rollback decision (SURVEY.md 8f), --sessions per GPU; "

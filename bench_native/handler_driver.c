@@ -2,10 +2,22 @@
  * workload (bench --workload requests).  What the Rust request handler of INTEGRATION.md does for L
  * GGRS sessions per advance_frame: encode every session's request list into the engine's mapped
  * lane batch (request kinds, Load frames, the AdvanceFrame input rows), run it through the C ABI
- * (ggrs_lane_batch_run) and hand every SaveGameState's checksum back (GameStateCell::save,
- * sync_layer.rs:18-24) -- here summed into a sink so the reads happen.  The lists are
- * SyncTestSession::advance_frame's (sync_test_session.rs:85-150): Load f-cd, Advance,
- * (Save, Advance) x (cd-1), Save f, Advance.  Bench infrastructure, not part of the engine. */
+ * and hand every SaveGameState's checksum back (GameStateCell::save, sync_layer.rs:18-24) -- here
+ * summed into a sink so the reads happen.  Bench infrastructure, not part of the engine.
+ *
+ * Lane groups: the sessions are served as G engines of L/G lanes each.  Per call, group g waits for
+ * its previous batch (ggrs_lane_batch_wait), hands its checksums back, spends the modelled session
+ * time (the GGRS session logic that produces the next lists), encodes its next lists and submits
+ * them (ggrs_lane_batch_submit) -- while the other groups' batches are on the device.  G = 1 is the
+ * plain synchronous handler.
+ *
+ * Two list sources:
+ *   synctest  SyncTestSession::advance_frame's lists (sync_test_session.rs:85-150): Load f-cd,
+ *             Advance, (Save, Advance) x (cd-1), Save f, Advance -- the same kinds for every lane,
+ *             written as token rows;
+ *   p2p       every lane its own P2PSession's lists (p2p_session.rs:265-426, rollbacks of differing
+ *             depth) from a fixture the oracle generated (bench_native/make_p2p_fixture.py), each
+ *             lane encoded by ggrs_lane_encode, the encoder the Rust crate uses. */
 #include <stdint.h>
 #include <string.h>
 #include <time.h>
@@ -16,6 +28,13 @@ static double now_s(void) {
   struct timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
   return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+static void spin_us(double us) {
+  if (us <= 0) return;
+  const double end = now_s() + us * 1e-6;
+  while (now_s() < end) {
+  }
 }
 
 /* 2-bit request kinds of the SyncTest list at frame f, least significant first */
@@ -38,55 +57,188 @@ static int synctest_tokens(int32_t f, int32_t cd, uint32_t* words, int* nl, int*
   return W;
 }
 
-/* Runs calls f_begin .. f_begin+n_calls-1 for every lane.  inputs: [frames][L][P] user inputs
- * (input delay 0), resident in host memory.  Returns 0, or the failing ABI code; *seconds = wall
- * time of the calls, *sink = sum of every Save checksum handed back; phases (may be NULL) gets the
- * seconds spent encoding, in ggrs_lane_batch_run, and handing checksums back. */
-int handler_drive_synctest(ggrs_engine_t* eng, const uint8_t* inputs, int32_t L, int32_t P, int32_t cd,
-                           int32_t f_begin, int32_t n_calls, uint64_t* sink, double* seconds, double* phases) {
-  double t_enc = 0, t_run = 0, t_back = 0;
-  ggrs_lane_batch_t b;
-  int rc = ggrs_lane_batch_map(eng, 2, 1, cd + 1, cd + 1, &b);
-  if (rc) return rc;
+#define MAX_GROUPS 8
+
+typedef struct {
+  ggrs_lane_batch_t b, run;
+  int pending;
+  int32_t base; /* first lane of the group in the global lane numbering */
+  int32_t lanes;
+  int32_t saves; /* SaveGameStates per lane of the pending batch (synctest) */
+} group_t;
+
+/* SyncTest lists.  inputs: [frames][L][P] user inputs (input delay 0), resident in host memory.
+ * Runs calls f_begin .. f_begin+n_calls-1 for every lane of every group.  Returns 0, or the failing
+ * ABI code; *seconds = wall time of the calls, *sink = sum of every Save checksum handed back;
+ * phases (may be NULL): seconds spent encoding, waiting for the device (submit + wait), handing
+ * checksums back, and in the modelled session logic. */
+int handler_drive_synctest_groups(ggrs_engine_t** engs, int32_t G, const uint8_t* inputs, int32_t L, int32_t P,
+                                  int32_t cd, int32_t f_begin, int32_t n_calls, double session_us, uint64_t* sink,
+                                  double* seconds, double* phases) {
+  if (G < 1 || G > MAX_GROUPS || L % G) return GGRS_E_INVALID;
+  group_t g[MAX_GROUPS];
+  const int32_t Lg = L / G;
+  for (int q = 0; q < G; q++) {
+    int rc = ggrs_lane_batch_map(engs[q], 2, 1, cd + 1, cd + 1, &g[q].b);
+    if (rc) return rc;
+    g[q].pending = 0;
+    g[q].base = q * Lg;
+    g[q].lanes = Lg;
+  }
+  double t_enc = 0, t_dev = 0, t_back = 0, t_sess = 0;
   uint64_t acc = 0;
   const double t0 = now_s();
-  for (int32_t f = f_begin; f < f_begin + n_calls; f++) {
-    const double ta = now_s();
-    uint32_t words[4];
-    int nl, na, ns;
-    const int W = synctest_tokens(f, cd, words, &nl, &na, &ns);
-    for (int j = 0; j < W; j++)
-      for (int32_t l = 0; l < L; l++) b.tokens[(size_t)j * L + l] = words[j];
-    if (nl)
-      for (int32_t l = 0; l < L; l++) b.load_frames[l] = f - cd;
-    const int32_t first = f - (na - 1); /* the frames the list's AdvanceFrames replay, in order */
-    memcpy(b.inputs, inputs + (size_t)first * L * P, (size_t)na * L * P);
-    ggrs_lane_batch_t run = b;
-    run.token_words = W;
-    run.load_slots = nl;
-    run.adv_rows = na;
-    run.save_rows = ns;
-    int32_t failed = 0;
-    const double tb = now_s();
-    rc = ggrs_lane_batch_run(eng, &run, 0, &failed);
-    if (rc) return rc;
-    const double tc = now_s();
-    for (int k = 0; k < ns; k++) {  /* row sums in 32 bits: one vectorised pass over the row */
-      const uint16_t* row = b.checksums + (size_t)k * L;
-      uint32_t s = 0;
-      for (int32_t l = 0; l < L; l++) s += row[l];
-      acc += s;
+  for (int32_t f = f_begin; f <= f_begin + n_calls; f++) {
+    for (int q = 0; q < G; q++) {
+      group_t* gq = &g[q];
+      if (gq->pending) {
+        const double ta = now_s();
+        int32_t failed = 0;
+        int rc = ggrs_lane_batch_wait(engs[q], &failed);
+        if (rc) return rc;
+        const double tb = now_s();
+        for (int k = 0; k < gq->saves; k++) { /* row sums in 32 bits: one vectorised pass per row */
+          const uint16_t* row = gq->b.checksums + (size_t)k * Lg;
+          uint32_t s = 0;
+          for (int32_t l = 0; l < Lg; l++) s += row[l];
+          acc += s;
+        }
+        const double tc = now_s();
+        spin_us(session_us); /* the GGRS session logic producing this group's next lists */
+        t_dev += tb - ta;
+        t_back += tc - tb;
+        t_sess += now_s() - tc;
+        gq->pending = 0;
+      }
+      if (f == f_begin + n_calls) continue; /* drained */
+      const double ta = now_s();
+      uint32_t words[4];
+      int nl, na, ns;
+      const int W = synctest_tokens(f, cd, words, &nl, &na, &ns);
+      for (int j = 0; j < W; j++)
+        for (int32_t l = 0; l < Lg; l++) gq->b.tokens[(size_t)j * Lg + l] = words[j];
+      if (nl)
+        for (int32_t l = 0; l < Lg; l++) gq->b.load_frames[l] = f - cd;
+      const int32_t first = f - (na - 1); /* the frames the list's AdvanceFrames replay, in order */
+      for (int a = 0; a < na; a++)
+        memcpy(gq->b.inputs + (size_t)a * Lg * P, inputs + ((size_t)(first + a) * L + gq->base) * P, (size_t)Lg * P);
+      gq->run = gq->b;
+      gq->run.token_words = W;
+      gq->run.load_slots = nl;
+      gq->run.adv_rows = na;
+      gq->run.save_rows = ns;
+      gq->saves = ns;
+      const double tb = now_s();
+      int rc = ggrs_lane_batch_submit(engs[q], &gq->run, 0);
+      if (rc) return rc;
+      gq->pending = 1;
+      t_enc += tb - ta;
+      t_dev += now_s() - tb;
     }
-    const double td = now_s();
-    t_enc += tb - ta;
-    t_run += tc - tb;
-    t_back += td - tc;
   }
   *seconds = now_s() - t0;
   if (phases) {
     phases[0] = t_enc;
-    phases[1] = t_run;
+    phases[1] = t_dev;
     phases[2] = t_back;
+    phases[3] = t_sess;
+  }
+  *sink = acc;
+  return 0;
+}
+
+/* The single-engine form kept for bench.py --req-groups 1 (one synchronous batch per call). */
+int handler_drive_synctest(ggrs_engine_t* eng, const uint8_t* inputs, int32_t L, int32_t P, int32_t cd,
+                           int32_t f_begin, int32_t n_calls, uint64_t* sink, double* seconds, double* phases) {
+  double ph[4];
+  int rc = handler_drive_synctest_groups(&eng, 1, inputs, L, P, cd, f_begin, n_calls, 0.0, sink, seconds, ph);
+  if (phases) {
+    phases[0] = ph[0];
+    phases[1] = ph[1];
+    phases[2] = ph[2];
+  }
+  return rc;
+}
+
+/* P2P lists from the fixture: M sessions' streams, lane l (global) plays session l % M.
+ *   reqs     [N] ggrs_request_t of every session's calls, back to back
+ *   req_off  [M][C + 1] start of session m's call c in reqs
+ *   adv_off  [M][C + 1] start of its AdvanceFrame rows in inputs / status
+ *   inputs, status [N_adv][P]
+ * Calls c_begin .. c_begin+n_calls-1.  lane_frames [L] in/out: every lane's frame (the encoder's
+ * Save-frame check); shape[4]: the batch shape to map (the fixture's largest list). */
+int handler_drive_p2p_groups(ggrs_engine_t** engs, int32_t G, int32_t L, int32_t P, int32_t M, int32_t C,
+                             const ggrs_request_t* reqs, const int64_t* req_off, const int64_t* adv_off,
+                             const uint8_t* inputs, const uint8_t* status, const int32_t* shape, int32_t* lane_frames,
+                             int32_t c_begin, int32_t n_calls, double session_us, uint64_t* sink, double* seconds,
+                             double* phases) {
+  if (G < 1 || G > MAX_GROUPS || L % G || c_begin < 0 || c_begin + n_calls > C) return GGRS_E_INVALID;
+  group_t g[MAX_GROUPS];
+  const int32_t Lg = L / G;
+  for (int q = 0; q < G; q++) {
+    int rc = ggrs_lane_batch_map(engs[q], shape[0], shape[1] > 0 ? shape[1] : 1, shape[2] > 0 ? shape[2] : 1,
+                                 shape[3] > 0 ? shape[3] : 1, &g[q].b);
+    if (rc) return rc;
+    g[q].pending = 0;
+    g[q].base = q * Lg;
+    g[q].lanes = Lg;
+  }
+  double t_enc = 0, t_dev = 0, t_back = 0, t_sess = 0;
+  uint64_t acc = 0;
+  int32_t prev_call[MAX_GROUPS];
+  const double t0 = now_s();
+  for (int32_t c = c_begin; c <= c_begin + n_calls; c++) {
+    for (int q = 0; q < G; q++) {
+      group_t* gq = &g[q];
+      if (gq->pending) {
+        const double ta = now_s();
+        int32_t failed = 0;
+        int rc = ggrs_lane_batch_wait(engs[q], &failed);
+        if (rc) return rc;
+        const double tb = now_s();
+        const int32_t pc = prev_call[q];
+        for (int32_t l = 0; l < Lg; l++) { /* every Save's checksum of the lane's list */
+          const int32_t lane = gq->base + l, m = lane % M;
+          const int64_t a = req_off[(int64_t)m * (C + 1) + pc], b = req_off[(int64_t)m * (C + 1) + pc + 1];
+          int si = 0;
+          for (int64_t k = a; k < b; k++)
+            if (reqs[k].kind == GGRS_REQ_SAVE) acc += gq->b.checksums[(size_t)si++ * Lg + l];
+          lane_frames[lane] = gq->b.lane_result[l];
+        }
+        const double tc = now_s();
+        spin_us(session_us);
+        t_dev += tb - ta;
+        t_back += tc - tb;
+        t_sess += now_s() - tc;
+        gq->pending = 0;
+      }
+      if (c == c_begin + n_calls) continue;
+      const double ta = now_s();
+      for (int32_t l = 0; l < Lg; l++) {
+        const int32_t lane = gq->base + l, m = lane % M;
+        const int64_t a = req_off[(int64_t)m * (C + 1) + c], b = req_off[(int64_t)m * (C + 1) + c + 1];
+        const int64_t ad = adv_off[(int64_t)m * (C + 1) + c];
+        int32_t bad = -1;
+        int rc = ggrs_lane_encode(&gq->b, Lg, P, l, reqs + a, (int32_t)(b - a), inputs + ad * P, status + ad * P,
+                                  lane_frames[lane], &bad);
+        if (rc) return rc; /* the fixture's lists are valid: any rejection is an error here */
+      }
+      gq->run = gq->b;
+      const double tb = now_s();
+      int rc = ggrs_lane_batch_submit(engs[q], &gq->run, GGRS_BATCH_STATUS);
+      if (rc) return rc;
+      gq->pending = 1;
+      prev_call[q] = c;
+      t_enc += tb - ta;
+      t_dev += now_s() - tb;
+    }
+  }
+  *seconds = now_s() - t0;
+  if (phases) {
+    phases[0] = t_enc;
+    phases[1] = t_dev;
+    phases[2] = t_back;
+    phases[3] = t_sess;
   }
   *sink = acc;
   return 0;

@@ -35,7 +35,8 @@ EXPORTS = (
     "ggrs_read_ring", "ggrs_read_trace", "ggrs_debug_corrupt_on_load", "ggrs_last_launch_ms",
     "ggrs_timing_reset", "ggrs_timing_read", "ggrs_set_synctest_path",
     "ggrs_lane_batch_map", "ggrs_lane_batch_run", "ggrs_handle_requests_lanes", "ggrs_read_lane_frames",
-    "ggrs_lane_server",
+    "ggrs_lane_server", "ggrs_lane_batch_submit", "ggrs_lane_batch_wait", "ggrs_lane_encode", "ggrs_lane_shape",
+    "ggrs_lane_batch_lds",
     "ggrs_branch_engine_create", "ggrs_branch_engine_destroy", "ggrs_branch_engine_config",
     "ggrs_branch_add_inputs", "ggrs_branch_speculate", "ggrs_branch_confirm",
     "ggrs_branch_report_bytes", "ggrs_branch_synchronize", "ggrs_branch_trunk_frame",
@@ -145,6 +146,11 @@ def lib():
         i32 = ctypes.c_int32
         L.ggrs_lane_batch_map.argtypes = [vp, i32, i32, i32, i32, P(LaneBatch)]
         L.ggrs_lane_batch_run.argtypes = [vp, P(LaneBatch), i32, P(i32)]
+        L.ggrs_lane_batch_submit.argtypes = [vp, P(LaneBatch), i32]
+        L.ggrs_lane_batch_wait.argtypes = [vp, P(i32)]
+        L.ggrs_lane_encode.argtypes = [P(LaneBatch), ctypes.c_int64, i32, ctypes.c_int64, vp, i32, vp, vp, i32, P(i32)]
+        L.ggrs_lane_shape.argtypes = [vp, i32, vp]
+        L.ggrs_lane_batch_lds.argtypes = [vp, i32, i32, i32, i32, P(ctypes.c_int64), P(ctypes.c_int64)]
         L.ggrs_handle_requests_lanes.argtypes = [vp, vp, vp, vp, vp, vp, vp]
         L.ggrs_read_lane_frames.argtypes = [vp, vp]
         L.ggrs_lane_server.argtypes = [vp, i32]

@@ -175,6 +175,14 @@ class BranchEngine:
     def set_round_launches(self, on=True):
         _lib.check(self._L.ggrs_branch_set_round_launches(self._h, int(bool(on))))
 
+    ROUND_FORMS = {"fused": 0, "per_round": 1, "full": 2}
+
+    def set_round_form(self, form):
+        """rounds(): "fused" (one launch; prefix-shared when the enumerated player is the only
+        remote one), "per_round" (2 n launches of speculate / confirm) or "full" (one launch, every
+        lane replaying and saving its whole window)."""
+        _lib.check(self._L.ggrs_branch_set_round_launches(self._h, self.ROUND_FORMS[form]))
+
     def synchronize(self):
         _lib.check(self._L.ggrs_branch_synchronize(self._h))
 

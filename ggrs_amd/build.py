@@ -16,7 +16,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "_obj")
 LIB = os.path.join(HERE, "libggrs_amd.so")
-UNITS = ("engine.hip", "requests.hip", "branch.hip", "particles.hip", "p2p.hip", "codec.hip")
+UNITS = ("engine.hip", "requests.hip", "branch.hip", "particles.hip", "p2p.hip", "codec.hip", "lane_encode.cpp")
 SOURCES = [os.path.join(CSRC, f) for f in UNITS]
 HEADERS = [os.path.join(CSRC, h) for h in ("box_game.h", "glibc_sincosf.h", "common.h", "particles.h")] + [
     os.path.join(ROOT, "include", "ggrs_amd.h")]

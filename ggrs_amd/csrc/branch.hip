@@ -82,6 +82,13 @@ __device__ inline uint32_t branch_inputs(const SpecParams& p, int64_t s, int32_t
   return branch_inputs_from<P>(p, truth, last, b, k);
 }
 
+// The lane whose ring holds branch b's depth-0 cell (the state after the first speculated frame):
+// the representative b mod A of its one-digit prefix (prefix_rounds_kernel saves only those), the
+// lane itself without enumeration.
+__device__ inline int64_t rep0_lane(const SpecParams& p, int64_t s, int32_t b) {
+  return s * p.B + (p.E > 0 ? (int64_t)(b % p.A) : (int64_t)b);
+}
+
 template <int P>
 __global__ __launch_bounds__(256) void speculate_kernel(SpecParams p) {
   const int64_t lane = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -90,8 +97,9 @@ __global__ __launch_bounds__(256) void speculate_kernel(SpecParams p) {
   const int32_t b = (int32_t)(lane - s * p.B);
   constexpr int F = state_fields(P);
   if (p.check_prev && ((p.prev_survive[lane >> 6] >> (lane & 63)) & 1ull)) {
-    // a surviving branch already saved the new trunk frame: it must match the replayed trunk
-    const uint16_t mine = p.ring_ck[(int64_t)(p.f_c % p.R) * p.L + lane];
+    // a surviving branch already saved the new trunk frame: it must match the replayed trunk (the
+    // cell of its depth-0 representative, which prefix-shared rounds save for every such branch)
+    const uint16_t mine = p.ring_ck[(int64_t)(p.f_c % p.R) * p.L + rep0_lane(p, s, b)];
     if (mine != p.trunk_ck[s]) atomicCAS(&p.desync[s], -1, p.f_c);
   }
   BoxState<P> st;
@@ -185,9 +193,8 @@ __global__ __launch_bounds__(kRoundsBlock) void rounds_kernel(RoundsParams rp) {
   const int ls = (int)(s - s_first);
   for (int q = threadIdx.x; q < ns * F; q += kRoundsBlock) {
     const int sl = q / F, k = q - sl * F;
-    lds_trunk[sl][k] = rp.trunk[(int64_t)k * p.S + s_first + sl];
+    lds_trunk[sl][k] = p.trunk[(int64_t)k * p.S + s_first + sl];
   }
-  if (threadIdx.x < ns) lds_ck[threadIdx.x] = p.trunk_ck[s_first + threadIdx.x];
   bool survived = p.check_prev && in_range && ((p.prev_survive[lane >> 6] >> (lane & 63)) & 1ull);
   // every state the launch steps descends from the block's trunks, which this engine produced:
   // one block-wide test of their rotation domain instead of a wave vote per player per step
@@ -195,8 +202,11 @@ __global__ __launch_bounds__(kRoundsBlock) void rounds_kernel(RoundsParams rp) {
   if ((int)threadIdx.x < ns) {
     BoxState<P> t0;
 #pragma unroll
-    for (int k = 0; k < F; k++) t0.w[k] = rp.trunk[(int64_t)k * p.S + s_first + threadIdx.x];
+    for (int k = 0; k < F; k++) t0.w[k] = p.trunk[(int64_t)k * p.S + s_first + threadIdx.x];
     trunk_ok = rot_in_domain<P>(t0);
+    // the trunk's checksum (the first round's survivor check) from the trunk itself: the report
+    // buffer may already hold another block's first-round checksum
+    lds_ck[threadIdx.x] = fletcher16_state<P>(t0);
   }
   const bool lean_ok = __syncthreads_and(trunk_ok);
   // input-queue rows and ring slots as wave-uniform counters (no runtime-divisor modulo per step):
@@ -209,6 +219,7 @@ __global__ __launch_bounds__(kRoundsBlock) void rounds_kernel(RoundsParams rp) {
   uint32_t truth = load_inputs<P>(p.inputs, (int64_t)row_c * p.S + s);
   const bool trunk_thread = (int)threadIdx.x < ns;
   const int64_t s2 = s_first + (trunk_thread ? threadIdx.x : 0);
+  const int64_t rep0 = in_range ? rep0_lane(p, s, b) : 0;
   for (int32_t r = 0; r < rp.n; ++r) {
     SpecParams q = p;
     q.f_c = p.f_c + r;
@@ -218,7 +229,10 @@ __global__ __launch_bounds__(kRoundsBlock) void rounds_kernel(RoundsParams rp) {
     // round (its saves go to the W slots after it), so its load is issued here and compared after
     // the replays, while its latency is hidden behind them
     const bool check = (r > 0 || p.check_prev) && survived;
-    const uint16_t mine = check ? p.ring_ck[(int64_t)slot_c * p.L + lane] : (uint16_t)0;
+    // (the first round's cell was saved by an earlier launch, possibly only by the representative
+    // of a prefix-shared launch; later rounds' by this lane itself -- another block's lanes may be
+    // at another round of this launch)
+    const uint16_t mine = check ? p.ring_ck[(int64_t)slot_c * p.L + (r == 0 ? rep0 : lane)] : (uint16_t)0;
     // the confirm step's trunk replay (the next round's trunk: AdvanceFrame(f_c) with the true
     // inputs) depends only on this round's trunk, so the block's trunk threads run it beside the
     // speculation instead of after it; it reaches LDS after every lane has loaded the old trunk
@@ -291,6 +305,353 @@ __global__ __launch_bounds__(kRoundsBlock) void rounds_kernel(RoundsParams rp) {
   }
 }
 
+// Prefix-shared rounds (ggrs_branch_rounds when the enumerated player is the only remote one,
+// config 3).  Two facts about a round make most of the rounds kernel's work common to many lanes:
+//   * players are independent in State::advance (ex_game.rs:276-331 updates player i from its own
+//     fields and input only) and every player except the enumerated one plays the session's
+//     confirmed local inputs, so the local players' states at frame f_c + k + 1 are the same in
+//     every branch of the session: the "common window" C_k;
+//   * branch b's enumerated player plays digits d_0 .. d_k up to frame f_c + k, so branches sharing
+//     their first k + 1 digits hold the same state after k + 1 frames: A^min(k+1, E) distinct cells
+//     per session at depth k (config 3: 16, 256, 4096, 65,536 of the 4 x 65,536 logical saves).
+// So each lane advances only its enumerated player (one player-step per frame instead of P), the
+// common window lives in LDS (per block and session: C_k for the frames f_c+1 .. f_c+W with the
+// doubled Fletcher sums of its fields, slot = frame % W) and slides by one frame per round (one
+// local-player step per round, the window lane), the trunk's enumerated player is replayed with the
+// confirmed input by a trunk lane (its local players are the window's first entry), and a cell at
+// depth k is saved only by the lanes whose branch number is below A^min(k+1, E) -- the prefix's
+// representative, branch b mod A^min(k+1, E) of the same session.  ggrs_branch_read_lane resolves a
+// lane's cell to its representative; every kernel's survivor check reads the representative
+// (depth 0: branch b mod A).  Rings (representatives), reports, trunks and desync records end
+// exactly as after the same rounds of speculate_kernel + confirm_kernel.
+// Block: kRoundsBlock branch lanes (four waves) + one extra wave for the per-session work (the
+// trunk's enumerated player replayed with the confirmed input; the window's new entry), so no
+// branch wave carries it: the branch waves meet the extra wave once per round, at a barrier before
+// the frame that needs the window's new entry.  The extra wave's input rows are loaded one round
+// ahead.  Saves are buffer stores at per-lane field offsets plus a wave-uniform slot offset.
+// Dynamic LDS per block (words): trunk enumerated player [2][ns][5], window [ns][W][5(P-1) + 2],
+// the first trunk's checksum [ns], the round's confirmed enumerated input [ns], and the input rows
+// of frames f_c .. f_c + n + W - 2 for the block's sessions [n + W - 1][ns] (staged in the prologue,
+// so the round loop issues no global load: a wave waiting on one would also wait for its saves,
+// which retire in order with loads on the vmcnt counter).
+constexpr int kPrefixBlock = kRoundsBlock + 64;
+constexpr int kPrefixItems = 1;  // (session, role) items per extra lane: 2 ns <= 64 * kPrefixItems
+constexpr uint32_t kPrefixOob = 0x40000000u;  // past every descriptor's range: a lane that never stores
+
+// A workgroup barrier ordering LDS only: __syncthreads() also waits for every global store the wave
+// has in flight (its fence covers global memory), which inside the round loop would stall each wave
+// on its saves; nothing in the loop reads another wave's global stores.
+__device__ inline void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+__device__ inline __amdgpu_buffer_rsrc_t prefix_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+template <int P, int EP>
+__global__ __launch_bounds__(kPrefixBlock) void prefix_rounds_kernel(RoundsParams rp) {
+  static_assert(EP >= 0 && EP < P, "enumerated player");
+  constexpr int F = state_fields(P);
+  constexpr int n_bytes = Fletcher<P>::n;
+  constexpr int FL = 5 * (P - 1);  // local-player fields of a window entry
+  constexpr int WS = FL + 2;       // + doubled Fletcher sums of the entry's common part
+  constexpr int e = EP;
+  extern __shared__ uint32_t lds_dyn[];
+  const SpecParams& p = rp.sp;
+  const int W = p.W;
+  const bool branch_wave = threadIdx.x < kRoundsBlock;  // wave-uniform
+  const int64_t lane0 = (int64_t)blockIdx.x * kRoundsBlock;
+  const int64_t lane = lane0 + (branch_wave ? threadIdx.x : 0);
+  const bool in_range = branch_wave && lane < p.L;
+  const int64_t s_first = lane0 / p.B;
+  const int64_t s_last = (min(p.L, lane0 + kRoundsBlock) - 1) / p.B;
+  const int ns = (int)(s_last - s_first + 1);
+  const int64_t s = in_range ? lane / p.B : s_first;
+  const int32_t b = in_range ? (int32_t)(lane - s * p.B) : 0;
+  const int ls = (int)(s - s_first);
+  uint32_t* lds_te = lds_dyn;                       // [2][ns][5]
+  uint32_t* lds_win = lds_te + 2 * ns * 5;          // [ns][W][WS]
+  uint32_t* lds_ck = lds_win + ns * W * WS;         // [ns] the launch's first trunk checksum
+  uint32_t* lds_tin = lds_ck + ns;                  // [ns]
+  uint32_t* lds_rows = lds_tin + ns;                // [n + W - 1][ns]
+  constexpr int kq[5] = {fld_x(P, e), fld_y(P, e), fld_vx(P, e), fld_vy(P, e), fld_rot(P, e)};
+  uint32_t wt[5];
+#pragma unroll
+  for (int q = 0; q < 5; q++) wt[q] = 2u * weights_at(n_bytes, fld_offset(P, kq[q]));
+  auto wrap_inc = [](int32_t x, int32_t m) { return x + 1 == m ? 0 : x + 1; };
+  auto win_entry = [&](int sl, int32_t wslot) { return lds_win + ((int64_t)sl * W + wslot) * WS; };
+  // a window entry: the local players' fields, then the doubled sums of frame + local fields +
+  // the length-prefix constants
+  auto write_entry = [&](uint32_t* dst, const uint32_t (&loc)[FL > 0 ? FL : 1], int32_t frame) {
+    uint32_t d1 = 2u * Fletcher<P>::kSum1Const, d2 = 2u * Fletcher<P>::kSum2Const;
+    d1 = dot4_u8((uint32_t)frame, 0x02020202u, d1);
+    d2 = dot4_u8((uint32_t)frame, 2u * weights_at(n_bytes, 0), d2);
+    int li = 0;
+#pragma unroll
+    for (int q = 0; q < P; q++) {
+      if (q == e) continue;
+      const int fk[5] = {fld_x(P, q), fld_y(P, q), fld_vx(P, q), fld_vy(P, q), fld_rot(P, q)};
+#pragma unroll
+      for (int u = 0; u < 5; u++) {
+        const uint32_t v = loc[5 * li + u];
+        d1 = dot4_u8(v, 0x02020202u, d1);
+        d2 = dot4_u8(v, 2u * weights_at(n_bytes, fld_offset(P, fk[u])), d2);
+        dst[5 * li + u] = v;
+      }
+      li++;
+    }
+    dst[FL] = d1;
+    dst[FL + 1] = d2;
+  };
+  auto step_locals = [&](uint32_t (&loc)[FL > 0 ? FL : 1], uint32_t in) {
+    int li = 0;
+#pragma unroll
+    for (int q = 0; q < P; q++) {
+      if (q == e) continue;
+      float x = __builtin_bit_cast(float, loc[5 * li]), y = __builtin_bit_cast(float, loc[5 * li + 1]);
+      float vx = __builtin_bit_cast(float, loc[5 * li + 2]), vy = __builtin_bit_cast(float, loc[5 * li + 3]);
+      float rot = __builtin_bit_cast(float, loc[5 * li + 4]);
+      advance_player(x, y, vx, vy, rot, (in >> (8 * q)) & 0xffu);
+      loc[5 * li] = __builtin_bit_cast(uint32_t, x);
+      loc[5 * li + 1] = __builtin_bit_cast(uint32_t, y);
+      loc[5 * li + 2] = __builtin_bit_cast(uint32_t, vx);
+      loc[5 * li + 3] = __builtin_bit_cast(uint32_t, vy);
+      loc[5 * li + 4] = __builtin_bit_cast(uint32_t, rot);
+      li++;
+    }
+  };
+  auto row_of = [&](int32_t row, int32_t k) {  // input row k frames after `row`, 0 <= k < cap
+    const int32_t r = row + k;
+    return r >= p.cap ? r - p.cap : r;
+  };
+  int32_t row_c = p.f_c % p.cap, slot_c = p.f_c % p.R, wslot_c = p.f_c % W;
+  // extra lane items: item q = xl + 64 i -> session q >> 1, role q & 1
+  const int xl = threadIdx.x - kRoundsBlock;
+  const int n_rows = rp.n + W - 1;
+  for (int i = threadIdx.x; i < n_rows * ns; i += kPrefixBlock) {
+    const int k = i / ns, xs = i - k * ns;
+    lds_rows[i] = load_inputs<P>(p.inputs, (int64_t)row_of(row_c, k) * p.S + s_first + xs);
+  }
+  __syncthreads();
+  // prologue (extra wave): the trunk's enumerated player and checksum (role 0), the window of
+  // round 0 (role 1): the trunk's local players at f_c, then W - 1 frames of confirmed inputs
+  bool trunk_ok = true;
+  if (!branch_wave) {
+#pragma unroll
+    for (int i = 0; i < kPrefixItems; i++) {
+      const int q = xl + 64 * i;
+      if (q >= 2 * ns) continue;
+      const int xs = q >> 1;
+      const int64_t xsess = s_first + xs;
+      BoxState<P> t0;
+#pragma unroll
+      for (int k = 0; k < F; k++) t0.w[k] = p.trunk[(int64_t)k * p.S + xsess];
+      trunk_ok = trunk_ok && rot_in_domain<P>(t0);
+      if ((q & 1) == 0) {
+#pragma unroll
+        for (int u = 0; u < 5; u++) lds_te[xs * 5 + u] = t0.w[kq[u]];
+        lds_ck[xs] = fletcher16_state<P>(t0);  // the first round's survivor check
+      } else {
+        uint32_t loc[FL > 0 ? FL : 1];
+        int li = 0;
+#pragma unroll
+        for (int qq = 0; qq < P; qq++) {
+          if (qq == e) continue;
+          const int fk[5] = {fld_x(P, qq), fld_y(P, qq), fld_vx(P, qq), fld_vy(P, qq), fld_rot(P, qq)};
+#pragma unroll
+          for (int u = 0; u < 5; u++) loc[5 * li + u] = t0.w[fk[u]];
+          li++;
+        }
+        int32_t ws = wslot_c;
+        write_entry(win_entry(xs, ws), loc, p.f_c);
+        for (int32_t k = 1; k < W; k++) {
+          step_locals(loc, lds_rows[(k - 1) * ns + xs]);
+          ws = wrap_inc(ws, W);
+          write_entry(win_entry(xs, ws), loc, p.f_c + k);
+        }
+      }
+    }
+  }
+  // every state the launch steps descends from the block's trunks (produced by this engine): one
+  // block-wide test of the rotation domain, then the lean step throughout
+  const bool lean_ok = __syncthreads_and(trunk_ok);
+  bool survived = p.check_prev && in_range && ((p.prev_survive[lane >> 6] >> (lane & 63)) & 1ull);
+  const int64_t rep0 = rep0_lane(p, s, b);
+  const int32_t digit0 = (int32_t)branch_digit(b, 0, p.A, p.E);
+  uint32_t e0[5] = {0, 0, 0, 0, 0};  // the enumerated player after the round's first frame
+  // the first round's survivor check reads the cell an earlier launch saved: loaded here, before
+  // the loop (a global load inside it would wait for the wave's saves)
+  const bool check0 = p.check_prev && survived;
+  const uint16_t mine0 = check0 ? p.ring_ck[(int64_t)slot_c * p.L + rep0] : (uint16_t)0;
+  // saves: ring [R][F][L] through one buffer descriptor; per-lane field offsets, slot offset uniform
+  const uint32_t slot_bytes = (uint32_t)(F * p.L * 4);
+  const __amdgpu_buffer_rsrc_t rs_ring = prefix_rsrc(p.ring, slot_bytes * (uint32_t)p.R);
+  const __amdgpu_buffer_rsrc_t rs_ck = prefix_rsrc(p.ring_ck, (uint32_t)(2 * p.L * p.R));
+  const uint32_t lo = in_range ? (uint32_t)(lane * 4) : kPrefixOob;
+  const uint32_t lo_ck = in_range ? (uint32_t)(lane * 2) : kPrefixOob;
+  const uint32_t fstride = (uint32_t)(p.L * 4);
+  for (int32_t r = 0; r < rp.n; ++r) {
+    const int32_t f_c = p.f_c + r;
+    const int buf = r & 1;
+    // the survivors' check (speculate_kernel's): in the first round against the cell an earlier
+    // launch saved (its representative's checksum vs the trunk's); in later rounds the lane compares
+    // its own depth-0 enumerated player of the previous round with the trunk's replayed one (the
+    // cell's local players ARE the trunk's: one window entry) -- the representative may sit in a
+    // block that is at another round of this launch
+    const int32_t wnext = wrap_inc(wslot_c, W);
+    if (!branch_wave) {
+      // (a) the trunk's enumerated player with the confirmed input of f_c (the confirm replay), and
+      // the window entry of frame f_c + W (into the slot frame f_c leaves); next round's rows
+#pragma unroll
+      for (int i = 0; i < kPrefixItems; i++) {
+        const int q = xl + 64 * i;
+        if (q >= 2 * ns) continue;
+        const int xs = q >> 1;
+        if ((q & 1) == 0) {
+          const uint32_t in = lds_rows[r * ns + xs];  // frame f_c
+          const uint32_t ein = (in >> (8 * e)) & 0xffu;
+          const uint32_t* te = lds_te + (buf * ns + xs) * 5;
+          float x = __builtin_bit_cast(float, te[0]), y = __builtin_bit_cast(float, te[1]);
+          float vx = __builtin_bit_cast(float, te[2]), vy = __builtin_bit_cast(float, te[3]);
+          float rot = __builtin_bit_cast(float, te[4]);
+          advance_player(x, y, vx, vy, rot, ein);
+          uint32_t* tn = lds_te + ((buf ^ 1) * ns + xs) * 5;
+          tn[0] = __builtin_bit_cast(uint32_t, x);
+          tn[1] = __builtin_bit_cast(uint32_t, y);
+          tn[2] = __builtin_bit_cast(uint32_t, vx);
+          tn[3] = __builtin_bit_cast(uint32_t, vy);
+          tn[4] = __builtin_bit_cast(uint32_t, rot);
+          lds_tin[xs] = ein;
+        } else {
+          const uint32_t in = lds_rows[(r + W - 1) * ns + xs];  // frame f_c + W - 1
+          const int32_t wprev = wslot_c == 0 ? W - 1 : wslot_c - 1;  // frame f_c + W - 1
+          const uint32_t* src = win_entry(xs, wprev);
+          uint32_t loc[FL > 0 ? FL : 1];
+#pragma unroll
+          for (int u = 0; u < FL; u++) loc[u] = src[u];
+          step_locals(loc, in);
+          write_entry(win_entry(xs, wslot_c), loc, f_c + W);
+        }
+      }
+    }
+    // LoadGameState(f_c): the trunk's enumerated player
+    float x = 0.0f, y = 0.0f, vx = 0.0f, vy = 0.0f, rot = 0.0f;
+    if (branch_wave) {
+      const uint32_t* te = lds_te + (buf * ns + ls) * 5;
+      x = __builtin_bit_cast(float, te[0]), y = __builtin_bit_cast(float, te[1]);
+      vx = __builtin_bit_cast(float, te[2]), vy = __builtin_bit_cast(float, te[3]);
+      rot = __builtin_bit_cast(float, te[4]);
+      if (r > 0 && survived) {
+        const bool same = te[0] == e0[0] && te[1] == e0[1] && te[2] == e0[2] && te[3] == e0[3] && te[4] == e0[4];
+        if (!same) atomicCAS(&p.desync[s], -1, f_c);
+      }
+    }
+    int32_t slot = slot_c, wslot = wslot_c;
+    int32_t pw = p.A;  // A^min(k+1, E): branches below it are depth k's representatives
+    for (int32_t k = 0; k < W; ++k) {
+      if (k == W - 1) lds_barrier();  // the window entry of frame f_c + W, the trunk replay
+      slot = wrap_inc(slot, p.R);     // frame f_c + k + 1
+      wslot = wrap_inc(wslot, W);
+      if (branch_wave) {
+        const uint32_t din = branch_digit(b, k, p.A, p.E);  // AdvanceFrame(f_c + k)
+        if (lean_ok) advance_player_lean(x, y, vx, vy, rot, din);
+        else advance_player_general(x, y, vx, vy, rot, din);
+        if (k == 0) {
+          e0[0] = __builtin_bit_cast(uint32_t, x);
+          e0[1] = __builtin_bit_cast(uint32_t, y);
+          e0[2] = __builtin_bit_cast(uint32_t, vx);
+          e0[3] = __builtin_bit_cast(uint32_t, vy);
+          e0[4] = __builtin_bit_cast(uint32_t, rot);
+        }
+        const bool rep = in_range && b < pw;
+        if (__builtin_amdgcn_ballot_w64(rep) != 0) {
+          // SaveGameState(f_c + k + 1): the common part from the window, the enumerated player's
+          // fields from this lane, the checksum from the entry's sums + this player's
+          const uint32_t* ent = win_entry(ls, wslot);
+          const uint32_t ev[5] = {__builtin_bit_cast(uint32_t, x), __builtin_bit_cast(uint32_t, y),
+                                  __builtin_bit_cast(uint32_t, vx), __builtin_bit_cast(uint32_t, vy),
+                                  __builtin_bit_cast(uint32_t, rot)};
+          uint32_t d1 = ent[FL], d2 = ent[FL + 1];
+#pragma unroll
+          for (int q = 0; q < 5; q++) {
+            d1 = dot4_u8(ev[q], 0x02020202u, d1);
+            d2 = dot4_u8(ev[q], wt[q], d2);
+          }
+          const uint32_t ck = fletcher_from_doubled(d1, d2);
+          if (rep) {  // per-lane field offsets, the slot's offset wave-uniform
+            const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)slot * slot_bytes);
+            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(f_c + k + 1), rs_ring, lo, so, 0);
+            int li = 0;
+#pragma unroll
+            for (int q = 0; q < P; q++) {
+              const int fk[5] = {fld_x(P, q), fld_y(P, q), fld_vx(P, q), fld_vy(P, q), fld_rot(P, q)};
+#pragma unroll
+              for (int u = 0; u < 5; u++)
+                __builtin_amdgcn_raw_buffer_store_b32(q == e ? ev[u] : ent[5 * li + u], rs_ring,
+                                                      lo + (uint32_t)fk[u] * fstride, so, 0);
+              if (q != e) li++;
+            }
+            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ck, lo_ck,
+                                                  __builtin_amdgcn_readfirstlane((uint32_t)slot * (uint32_t)(2 * p.L)), 0);
+          }
+        }
+      }
+      pw = pw >= p.B / p.A ? p.B : pw * p.A;
+    }
+    if (!branch_wave) {
+      // the new trunk: frame f_c + 1, the window's first entry, the replayed enumerated player
+#pragma unroll
+      for (int i = 0; i < kPrefixItems; i++) {
+        const int q = xl + 64 * i;
+        if (q >= 2 * ns || (q & 1)) continue;
+        const int xs = q >> 1;
+        const int64_t xsess = s_first + xs;
+        const uint32_t* tn = lds_te + ((buf ^ 1) * ns + xs) * 5;
+        const uint32_t* ent = win_entry(xs, wnext);
+        uint32_t d1 = ent[FL], d2 = ent[FL + 1];
+#pragma unroll
+        for (int u = 0; u < 5; u++) {
+          d1 = dot4_u8(tn[u], 0x02020202u, d1);
+          d2 = dot4_u8(tn[u], wt[u], d2);
+        }
+        const uint16_t tck = (uint16_t)fletcher_from_doubled(d1, d2);
+        if (xsess * p.B >= lane0) {  // this block holds the session's branch-0 lane
+          rp.trunk[xsess] = (uint32_t)(f_c + 1);
+          int li = 0;
+#pragma unroll
+          for (int qq = 0; qq < P; qq++) {
+            const int fk[5] = {fld_x(P, qq), fld_y(P, qq), fld_vx(P, qq), fld_vy(P, qq), fld_rot(P, qq)};
+#pragma unroll
+            for (int u = 0; u < 5; u++) rp.trunk[(int64_t)fk[u] * p.S + xsess] = qq == e ? tn[u] : ent[5 * li + u];
+            if (qq != e) li++;
+          }
+          rp.report_ck[xsess] = tck;
+          if (rp.copy_ck && (rp.copy_stride || r + 1 == rp.n))
+            reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(rp.copy_ck) + r * rp.copy_stride)[xsess] = tck;
+        }
+      }
+    } else {
+      // confirm: a lane survives iff it assumed the confirmed input of f_c (input_queue.rs:199-218)
+      const bool survive = in_range && (uint32_t)digit0 == lds_tin[ls];
+      const uint64_t bits = __ballot(survive);
+      if (in_range && (threadIdx.x & 63) == 0) {
+        rp.report_bits[lane >> 6] = bits;
+        if (rp.copy_bits && (rp.copy_stride || r + 1 == rp.n))
+          reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(rp.copy_bits) + r * rp.copy_stride)[lane >> 6] = bits;
+      }
+      if (r == 0 && check0 && mine0 != (uint16_t)lds_ck[ls]) atomicCAS(&p.desync[s], -1, f_c);
+      survived = survive;
+    }
+    lds_barrier();
+    row_c = wrap_inc(row_c, p.cap);
+    slot_c = wrap_inc(slot_c, p.R);
+    wslot_c = wnext;
+  }
+}
+
 // compare_local_checksums_against_peers (p2p_session.rs:904-937) over an all-gathered report
 // block: sessions whose trunk checksum differs between this rank's row and its peer's each count
 // one DesyncDetected (src/lib.rs:158-167); the first round with any is recorded.
@@ -331,13 +692,16 @@ struct ggrs_branch_engine {
   hipStream_t stream = nullptr;      // where every launch and copy goes (own_stream or the caller's)
   hipStream_t own_stream = nullptr;
   uint32_t* trunk = nullptr;
+  uint32_t* trunk_alt = nullptr;     // the fused rounds' output trunk (swapped in after the launch)
   uint32_t* ring = nullptr;
   uint16_t* ring_ck = nullptr;
   uint8_t* inputs = nullptr;
   uint8_t* report = nullptr;  // report_bytes: [S] u16 | pad to 8 | [words] u64
   size_t report_bytes = 0;
   uint64_t* prev_bits = nullptr;
-  bool per_round_launches = false;   // ggrs_branch_set_round_launches: rounds() as 2 n launches
+  int32_t round_form = 0;            // ggrs_branch_set_round_launches: 0 fused (prefix-shared when
+                                     // eligible), 1 = 2 n launches, 2 fused without prefix sharing
+  int32_t last_spec_fc = -1;         // trunk frame of the last speculation (read_lane's depth)
   int32_t* desync = nullptr;
   uint8_t* staging = nullptr;
   size_t staging_bytes = 0;
@@ -350,6 +714,18 @@ struct ggrs_branch_engine {
 namespace {
 
 size_t report_ck_bytes(int64_t S) { return ((size_t)S * 2 + 7) & ~(size_t)7; }
+constexpr size_t kPrefixLdsBytes = 32 * 1024;
+
+// prefix_rounds_kernel<P, EP> for the runtime enumerated player ep (0 <= ep < P)
+template <int P, typename Fn>
+void dispatch_enumerated(int ep, Fn&& fn) {
+  switch (ep) {
+    case 0: fn(std::integral_constant<int, 0>()); break;
+    case 1: if constexpr (P > 1) fn(std::integral_constant<int, 1>()); break;
+    case 2: if constexpr (P > 2) fn(std::integral_constant<int, 2>()); break;
+    default: if constexpr (P > 3) fn(std::integral_constant<int, 3>()); break;
+  }
+}
 int64_t report_words(int64_t L) { return (L + 63) / 64; }
 
 template <typename K>
@@ -369,7 +745,7 @@ int ggrs_branch_engine_destroy(ggrs_branch_engine_t* e) {
   if (!e) return GGRS_OK;
   (void)hipSetDevice(e->cfg.device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
-  void* bufs[] = {e->trunk, e->ring, e->ring_ck, e->inputs, e->report, e->prev_bits, e->desync, e->staging};
+  void* bufs[] = {e->trunk, e->trunk_alt, e->ring, e->ring_ck, e->inputs, e->report, e->prev_bits, e->desync, e->staging};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   e->timer.destroy();
@@ -430,6 +806,7 @@ int ggrs_branch_engine_create(const ggrs_branch_config_t* cfg, ggrs_branch_engin
   e->stream = e->own_stream;
   if (e->timer.create()) return fail(GGRS_E_HIP);
   CTRY(hipMalloc(&e->trunk, sizeof(uint32_t) * e->F * S));
+  CTRY(hipMalloc(&e->trunk_alt, sizeof(uint32_t) * e->F * S));
   CTRY(hipMalloc(&e->ring, sizeof(uint32_t) * (size_t)e->R * e->F * L));
   CTRY(hipMalloc(&e->ring_ck, sizeof(uint16_t) * (size_t)e->R * L));
   CTRY(hipMalloc(&e->inputs, (size_t)e->cap * S * e->Pp));
@@ -519,12 +896,14 @@ int ggrs_branch_speculate(ggrs_branch_engine_t* e) {
   p.prev_survive = (const uint64_t*)(e->report + report_ck_bytes(p.S));
   p.trunk_ck = (const uint16_t*)e->report;
   p.desync = e->desync;
-  return branch_launch_timed(e, [&] {
+  int rc = branch_launch_timed(e, [&] {
     dispatch_players(p.P, [&](auto PC) {
       constexpr int P = decltype(PC)::value;
       speculate_kernel<P><<<grid_of(p.L, 256), 256, 0, e->stream>>>(p);
     });
   });
+  if (rc == GGRS_OK) e->last_spec_fc = p.f_c;
+  return rc;
 }
 
 int ggrs_branch_confirm(ggrs_branch_engine_t* e, void* report_device) {
@@ -617,11 +996,23 @@ int ggrs_branch_read_lane(ggrs_branch_engine_t* e, int64_t lane, int32_t frame, 
   if (lane < 0 || lane >= e->L) return set_error(GGRS_E_INVALID, "lane out of range");
   HIP_TRY(hipSetDevice(e->cfg.device));
   const int slot = ((frame % e->R) + e->R) % e->R;
+  // the cell of `frame` was saved at depth k = frame - f_c - 1 of the last speculation from trunk
+  // frame f_c (the frame f_c itself at depth 0 of the one before); branches sharing their first
+  // k + 1 digits share it, held by the representative b mod A^min(k+1, E) (prefix_rounds_kernel)
+  int64_t cell_lane = lane;
+  if (e->E > 0 && e->last_spec_fc >= 0 && frame >= e->last_spec_fc && frame <= e->last_spec_fc + e->cfg.window) {
+    const int k = frame > e->last_spec_fc ? frame - e->last_spec_fc - 1 : 0;
+    int64_t pw = 1;
+    for (int q = 0; q < std::min(k + 1, e->E); q++) pw *= e->cfg.alphabet;
+    const int64_t B = e->cfg.branches, sess = lane / B;
+    cell_lane = sess * B + (lane - sess * B) % pw;
+  }
   std::vector<uint32_t> w(e->F);
   for (int k = 0; k < e->F; k++)
-    HIP_TRY(hipMemcpyAsync(&w[k], e->ring + ((size_t)slot * e->F + k) * e->L + lane, 4, hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipMemcpyAsync(&w[k], e->ring + ((size_t)slot * e->F + k) * e->L + cell_lane, 4, hipMemcpyDeviceToHost,
+                           e->stream));
   uint16_t ck = 0;
-  HIP_TRY(hipMemcpyAsync(&ck, e->ring_ck + (size_t)slot * e->L + lane, 2, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipMemcpyAsync(&ck, e->ring_ck + (size_t)slot * e->L + cell_lane, 2, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   if (checksum) *checksum = ck;
   if (out) serialize_state_bytes(w.data(), e->cfg.num_players, out);
@@ -667,20 +1058,57 @@ int launch_rounds(ggrs_branch_engine* e, int32_t n_rounds, void* copy, bool ever
   p.trunk_ck = (const uint16_t*)e->report;
   p.desync = e->desync;
   rp.n = n_rounds;
-  rp.trunk = e->trunk;
+  // the fused kernels read the trunks from p.trunk and write them to rp.trunk, another buffer: a
+  // block still reading its sessions' trunks must not see another block's later rounds
+  rp.trunk = e->trunk_alt;
   rp.report_ck = (uint16_t*)e->report;
   rp.report_bits = (uint64_t*)(e->report + report_ck_bytes(p.S));
   rp.copy_ck = copy ? (uint16_t*)copy : nullptr;
   rp.copy_bits = copy ? (uint64_t*)((uint8_t*)copy + report_ck_bytes(p.S)) : nullptr;
   rp.copy_stride = every_round ? (int64_t)e->report_bytes : 0;
+  // prefix sharing (prefix_rounds_kernel) when the enumerated player is the only remote one and
+  // its per-block window fits the LDS budget
+  const int ns_max = (int)std::min<int64_t>(kRoundsBlock / p.B + 2, p.S);
+  const size_t lds_fixed = (size_t)ns_max * (2 * 5 + (size_t)p.W * (5 * (p.P - 1) + 2) + 2);
+  // rounds per launch: their input rows ([n + W - 1][ns] words) must fit the budget as well
+  const int64_t rows_fit = ((int64_t)kPrefixLdsBytes / 4 - (int64_t)lds_fixed) / ns_max - (p.W - 1);
+  const int32_t n_chunk = (int32_t)std::max<int64_t>(0, std::min<int64_t>(n_rounds, rows_fit));
+  const size_t lds_words = lds_fixed + (size_t)ns_max * (n_chunk + p.W - 1);
+  const bool prefix = e->round_form == 0 && p.B > 1 && __builtin_popcount(p.remote_mask) == 1 && n_chunk >= 1 &&
+                      lds_words * 4 <= kPrefixLdsBytes && 2 * ns_max <= 64 * kPrefixItems &&
+                      (int64_t)p.R * e->F * p.L * 4 < ((int64_t)1 << 30);
+  if (prefix && n_chunk < n_rounds) {  // launches of n_chunk rounds (their input rows fit LDS)
+    for (int32_t r0 = 0; r0 < n_rounds; r0 += n_chunk) {
+      const int32_t m = std::min(n_chunk, n_rounds - r0);
+      void* c = !copy ? nullptr
+                      : (every_round ? (void*)((uint8_t*)copy + (size_t)r0 * e->report_bytes)
+                                     : (r0 + m == n_rounds ? copy : nullptr));
+      if (int rc = launch_rounds(e, m, c, every_round)) return rc;
+    }
+    return GGRS_OK;
+  }
   // counted as the 2 n speculate + confirm launches it replaces
   int rc = branch_launch_timed(e, [&] {
+    const dim3 grid((unsigned)grid_of(p.L, kRoundsBlock));
+    if (prefix) {
+      const size_t lds = lds_words * 4;
+      dispatch_players(p.P, [&](auto PC) {
+        constexpr int P = decltype(PC)::value;
+        dispatch_enumerated<P>(p.first_remote, [&](auto EC) {
+          constexpr int EP = decltype(EC)::value;
+          prefix_rounds_kernel<P, EP><<<grid, kPrefixBlock, lds, e->stream>>>(rp);
+        });
+      });
+      return;
+    }
     dispatch_players(p.P, [&](auto PC) {
       constexpr int P = decltype(PC)::value;
-      rounds_kernel<P><<<grid_of(p.L, kRoundsBlock), kRoundsBlock, 0, e->stream>>>(rp);
+      rounds_kernel<P><<<grid, kRoundsBlock, 0, e->stream>>>(rp);
     });
   }, 2 * n_rounds);
   if (rc) return rc;
+  std::swap(e->trunk, e->trunk_alt);
+  e->last_spec_fc = e->trunk_frame + n_rounds - 1;
   e->trunk_frame += n_rounds;
   e->have_prev = true;
   return GGRS_OK;
@@ -700,7 +1128,7 @@ int ggrs_branch_rounds(ggrs_branch_engine_t* e, int32_t n_rounds) {
   if (int rc = check_rounds_queued(e, n_rounds)) return rc;
   if (n_rounds == 0) return GGRS_OK;
   HIP_TRY(hipSetDevice(e->cfg.device));
-  if (!e->per_round_launches) return launch_rounds(e, n_rounds, nullptr);
+  if (e->round_form != 1) return launch_rounds(e, n_rounds, nullptr);
   int rc = GGRS_OK;
   for (int32_t r = 0; r < n_rounds && rc == GGRS_OK; r++) {
     rc = ggrs_branch_speculate(e);
@@ -777,7 +1205,9 @@ int ggrs_branch_set_stream(ggrs_branch_engine_t* e, void* stream) {
 
 int ggrs_branch_set_round_launches(ggrs_branch_engine_t* e, int32_t on) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
-  e->per_round_launches = on != 0;
+  if (on < 0 || on > 2) return set_error(GGRS_E_INVALID, "round form %d: 0 fused, 1 per-round launches, 2 fused "
+                                                         "without prefix sharing", on);
+  e->round_form = on;
   return GGRS_OK;
 }
 

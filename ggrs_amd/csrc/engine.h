@@ -30,6 +30,10 @@ struct LaneServerHost {
   int32_t blocks = 0;
   double last_done = 0.0;  // steady-clock seconds of the last finished batch
   int64_t idle_ticks = 0;  // the kernel's idle watchdog, in wall-clock ticks
+  int pending = 0;         // a submitted batch not yet waited for: 1 on the server, 2 as a launch
+  int32_t pending_epoch = 0;
+  double pending_t0 = 0.0;
+  bool failed = false;     // a batch timed out: the server may still hold it; no further batches
 };
 
 struct ggrs_engine {

@@ -734,9 +734,8 @@ int server_start(ggrs_engine* e) {
   return GGRS_OK;
 }
 
-// Publish one batch to the running server and spin until its last block reports it done;
-// *fails = the batch's sessions that failed validation.
-int server_run(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int use_status, int32_t* fails) {
+// Publish one batch to the running server (returns at once; server_collect waits for it).
+int server_publish(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int use_status) {
   LaneServerHost& s = e->server;
   if (s.running && now_s() - s.last_done > kServerIdleHost) {
     if (int rc = lane_server_stop(e)) return rc;
@@ -746,10 +745,22 @@ int server_run(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int 
     if (!s.enabled) return GGRS_E_STATE;  // caller falls back to a launch per batch
   }
   uint64_t* ctl = (uint64_t*)s.mem;
-  const uint64_t* slots = (const uint64_t*)(s.mem + 64);
   const int32_t ep = ++s.epoch;
   __atomic_store_n(ctl, ctlw::pack(ep, W, LD, A, S, use_status), __ATOMIC_RELEASE);  // after the batch rows
-  const double t0 = now_s();
+  s.pending = 1;
+  s.pending_epoch = ep;
+  s.pending_t0 = now_s();
+  return GGRS_OK;
+}
+
+// Spin until every block of the published batch reports it done; *fails = the batch's sessions
+// that failed validation.  A batch not done within 10 s marks the engine failed: the quit bit is
+// set, but the old server may still be inside that batch (and would see a new control word), so no
+// later batch is published on this engine.
+int server_collect(ggrs_engine* e, int32_t* fails) {
+  LaneServerHost& s = e->server;
+  const uint64_t* slots = (const uint64_t*)(s.mem + 64);
+  const int32_t ep = s.pending_epoch;
   int spins = 0;
   int32_t b = 0;
   uint32_t failed = 0;
@@ -764,24 +775,29 @@ int server_run(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int 
     _mm_pause();
     if (++spins == 4096) {
       spins = 0;
-      if (now_s() - t0 > 10.0) {
-        s.running = false;  // the kernel's watchdog ends it; the stream drains on its own
-        return set_error(GGRS_E_HIP, "lane server did not finish batch %d within 10 s", ep);
+      if (now_s() - s.pending_t0 > 10.0) {
+        uint64_t* ctl = (uint64_t*)s.mem;
+        __atomic_store_n(ctl, __atomic_load_n(ctl, __ATOMIC_ACQUIRE) | ctlw::kQuit, __ATOMIC_RELEASE);
+        s.running = false;
+        s.pending = 0;
+        s.failed = true;
+        return set_error(GGRS_E_HIP, "lane server did not finish batch %d within 10 s; the engine takes no "
+                                     "further batches", ep);
       }
     }
   }
+  s.pending = 0;
   s.last_done = now_s();
   *fails = (int32_t)failed;
   return GGRS_OK;
 }
 
-// Runs the engine's mapped batch with the given counts; waits for completion.  *fails = the
-// sessions that failed validation, or -1 when only the lane results tell (one launch per batch).
-int run_batch(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int use_status, int32_t* fails) {
+// Submits the engine's mapped batch with the given counts: to the lane server, or as one launch.
+int submit_batch(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int use_status) {
   e->mode = kModeLaneRequests;
-  *fails = -1;
+  if (e->server.failed) return set_error(GGRS_E_STATE, "an earlier lane batch timed out on this engine");
   if (e->server.enabled) {
-    const int rc = server_run(e, W, LD, A, S, use_status, fails);
+    const int rc = server_publish(e, W, LD, A, S, use_status);
     if (rc != GGRS_E_STATE) return rc;  // GGRS_E_STATE: the grid cannot stay resident, launch instead
   }
   LaneBatchParams p = batch_params(e, W, LD, A, S, use_status);
@@ -796,8 +812,27 @@ int run_batch(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int u
     });
   });
   if (rc) return rc;
-  HIP_TRY(hipStreamSynchronize(e->stream));
+  e->server.pending = 2;
   return GGRS_OK;
+}
+
+// Waits for the submitted batch; *fails = the sessions that failed validation, or -1 when only
+// the lane results tell (one launch per batch).
+int wait_batch(ggrs_engine* e, int32_t* fails) {
+  *fails = -1;
+  const int pending = e->server.pending;
+  if (pending == 1) return server_collect(e, fails);
+  if (pending == 2) {
+    e->server.pending = 0;
+    HIP_TRY(hipStreamSynchronize(e->stream));
+  }
+  return GGRS_OK;
+}
+
+int run_batch(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int use_status, int32_t* fails) {
+  *fails = -1;
+  if (int rc = submit_batch(e, W, LD, A, S, use_status)) return rc;
+  return wait_batch(e, fails);
 }
 
 int check_mode(const ggrs_engine* e) {
@@ -806,12 +841,28 @@ int check_mode(const ggrs_engine* e) {
   return GGRS_OK;
 }
 
+// the device's LDS per workgroup (read once per engine; a non-positive report is taken as the
+// 64 KiB every CDNA workgroup gets)
+int lds_limit(ggrs_engine* e, int* out) {
+  int& max_lds = e->max_lds_per_block;
+  if (max_lds == 0) {
+    int v = 0;
+    HIP_TRY(hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, e->cfg.device));
+    max_lds = v > 0 ? v : 65536;
+  }
+  *out = max_lds;
+  return GGRS_OK;
+}
+
+size_t lane_lds_need(const ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S) {
+  return LaneLds(e->cfg.num_players, W, LD, e->R, A, S, 1).bytes + 64;  // + the static words
+}
+
 // the lane block's LDS for a batch shape must fit one workgroup's allotment on the device
 int check_lds(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S) {
-  int& max_lds = e->max_lds_per_block;
-  if (max_lds == 0)
-    HIP_TRY(hipDeviceGetAttribute(&max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, e->cfg.device));
-  const size_t need = LaneLds(e->cfg.num_players, W, LD, e->R, A, S, 1).bytes + 64;  // + the static words
+  int max_lds = 0;
+  if (int rc = lds_limit(e, &max_lds)) return rc;
+  const size_t need = lane_lds_need(e, W, LD, A, S);
   if (need > (size_t)max_lds)
     return set_error(GGRS_E_INVALID, "lane batch shape (%d words, %d loads, %d advances, %d saves) needs %zu bytes "
                                      "of LDS per lane block, more than the device's %d", W, LD, A, S, need, max_lds);
@@ -852,6 +903,10 @@ namespace ggrs {
 
 int lane_server_stop(ggrs_engine* e) {
   LaneServerHost& s = e->server;
+  if (s.pending) {  // a submitted batch first runs to completion (a quit word would skip it)
+    int32_t fails;
+    if (int rc = wait_batch(e, &fails)) return rc;
+  }
   if (!s.running) return GGRS_OK;
   uint64_t* ctl = (uint64_t*)s.mem;
   __atomic_store_n(ctl, __atomic_load_n(ctl, __ATOMIC_ACQUIRE) | ctlw::kQuit, __ATOMIC_RELEASE);
@@ -878,11 +933,57 @@ int ggrs_lane_batch_map(ggrs_engine_t* e, int32_t W, int32_t LD, int32_t A, int3
   return GGRS_OK;
 }
 
+int ggrs_lane_batch_lds(ggrs_engine_t* e, int32_t W, int32_t LD, int32_t A, int32_t S, int64_t* need_bytes,
+                        int64_t* limit_bytes) {
+  if (!e || !need_bytes || !limit_bytes) return set_error(GGRS_E_INVALID, "null argument");
+  if (int rc = check_shape(W, LD, A, S)) return rc;
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  int lim = 0;
+  if (int rc = lds_limit(e, &lim)) return rc;
+  *need_bytes = (int64_t)lane_lds_need(e, W, LD, A, S);
+  *limit_bytes = lim;
+  return GGRS_OK;
+}
+
+int ggrs_lane_batch_submit(ggrs_engine_t* e, const ggrs_lane_batch_t* b, int32_t flags) {
+  if (!e || !b) return set_error(GGRS_E_INVALID, "null argument");
+  int rc = check_mode(e);
+  if (rc) return rc;
+  if (e->server.pending) return set_error(GGRS_E_STATE, "a submitted lane batch has not been waited for");
+  const LaneBatchHost& h = e->batch;
+  ggrs_lane_batch_t v;
+  if (!h.base) return set_error(GGRS_E_STATE, "no lane batch mapped (ggrs_lane_batch_map)");
+  fill_batch_view(e, &v);
+  if (b->tokens != v.tokens || b->load_frames != v.load_frames || b->inputs != v.inputs || b->status != v.status ||
+      b->checksums != v.checksums || b->lane_result != v.lane_result)
+    return set_error(GGRS_E_INVALID, "batch pointers are not this engine's current mapping");
+  if (b->token_words < 0 || b->token_words > h.words || b->load_slots < 0 || b->load_slots > h.loads ||
+      b->adv_rows < 0 || b->adv_rows > h.adv || b->save_rows < 0 || b->save_rows > h.saves)
+    return set_error(GGRS_E_INVALID, "batch counts exceed the mapped shape");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  e->lane_frame.clear();  // the lanes' frames move on the device only
+  return submit_batch(e, b->token_words, b->load_slots, b->adv_rows, b->save_rows, (flags & GGRS_BATCH_STATUS) != 0);
+}
+
+int ggrs_lane_batch_wait(ggrs_engine_t* e, int32_t* n_failed) {
+  if (!e) return set_error(GGRS_E_INVALID, "null argument");
+  if (n_failed) *n_failed = 0;
+  if (!e->server.pending) return set_error(GGRS_E_STATE, "no lane batch submitted");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  int32_t fails = -1;
+  if (int rc = wait_batch(e, &fails)) return rc;
+  if (fails == 0) return GGRS_OK;  // the server counted no failed lane: no scan of the results
+  ggrs_lane_batch_t v;
+  fill_batch_view(e, &v);
+  return report_failures(e, v.lane_result, n_failed);
+}
+
 int ggrs_lane_batch_run(ggrs_engine_t* e, const ggrs_lane_batch_t* b, int32_t flags, int32_t* n_failed) {
   if (!e || !b) return set_error(GGRS_E_INVALID, "null argument");
   if (n_failed) *n_failed = 0;
   int rc = check_mode(e);
   if (rc) return rc;
+  if (e->server.pending) return set_error(GGRS_E_STATE, "a submitted lane batch has not been waited for");
   const LaneBatchHost& h = e->batch;
   ggrs_lane_batch_t v;
   if (!h.base) return set_error(GGRS_E_STATE, "no lane batch mapped (ggrs_lane_batch_map)");

@@ -14,6 +14,7 @@ against GGRS reads the same here; every object drives ALL lanes of one engine (o
 There is no CPU path: the engine's HIP library must be built and a GPU present.
 """
 import ctypes
+import weakref
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -126,6 +127,7 @@ class Engine:
         cks = np.zeros(max(n_save, 1), np.uint16)
         res = np.zeros(self.num_lanes, np.int32)
         rc = self._L.ggrs_handle_requests_lanes(self._h, _vp(r), _vp(off), _vp(i), _vp(st), _vp(cks), _vp(res))
+        self._check_batches()  # the CSR form may have grown (and freed) the mapped lane batch
         if rc == _lib.GGRS_E_PRECONDITION:
             if check:
                 raise LanesFailed(self._L.ggrs_last_error().decode(errors="replace"), res)
@@ -134,8 +136,27 @@ class Engine:
         return cks[:n_save], res
 
     def lane_batch(self, token_words, load_slots, adv_rows, save_rows):
-        """The engine's mapped per-lane batch (ggrs_lane_batch_map) as numpy views."""
-        return LaneBatch(self, token_words, load_slots, adv_rows, save_rows)
+        """The engine's mapped per-lane batch (ggrs_lane_batch_map) as numpy views.  Views of an
+        earlier, smaller mapping are invalidated when this one grows it."""
+        b = LaneBatch(self, token_words, load_slots, adv_rows, save_rows)
+        self._check_batches()
+        self.__dict__.setdefault("_batches", []).append(weakref.ref(b))
+        return b
+
+    def _check_batches(self):
+        """Invalidate LaneBatch views whose mapping the engine has replaced (their memory is freed)."""
+        live = [w() for w in self.__dict__.get("_batches", [])]
+        live = [b for b in live if b is not None and b.valid]
+        if not live:
+            self._batches = []
+            return
+        cur = _lib.LaneBatch()
+        _lib.check(self._L.ggrs_lane_batch_map(self._h, 0, 0, 0, 0, ctypes.byref(cur)))
+        addr = ctypes.cast(cur.tokens, ctypes.c_void_p).value
+        for b in live:
+            if b.tokens_addr != addr:
+                b._invalidate()
+        self._batches = [weakref.ref(b) for b in live if b.valid]
 
     def set_lane_server(self, on=True):
         """ggrs_lane_server: per-lane batches through one persistent kernel (default) or one
@@ -229,6 +250,8 @@ class LaneBatch:
         _lib.check(engine._L.ggrs_lane_batch_map(engine._h, token_words, load_slots, adv_rows, save_rows,
                                                  ctypes.byref(b)))
         self._b = b
+        self.valid = True
+        self.tokens_addr = ctypes.cast(b.tokens, ctypes.c_void_p).value
         L, P = engine.num_lanes, engine.num_players
         W, LD, A, S = b.token_words, b.load_slots, b.adv_rows, b.save_rows
         view = np.ctypeslib.as_array
@@ -240,17 +263,64 @@ class LaneBatch:
         self.lane_result = view(b.lane_result, shape=(L,))
         self.shape = (W, LD, A, S)
 
+    def _invalidate(self):
+        self.valid = False
+        self.tokens = self.load_frames = self.inputs = self.status = self.checksums = self.lane_result = None
+
     def run(self, token_words=None, load_slots=None, adv_rows=None, save_rows=None, status=False):
         """ggrs_lane_batch_run with the given counts (default: the mapped shape); returns the number
         of lanes that failed validation (their lane_result < 0)."""
-        W, LD, A, S = self.shape
-        b = _lib.LaneBatch(W if token_words is None else token_words, LD if load_slots is None else load_slots,
-                           A if adv_rows is None else adv_rows, S if save_rows is None else save_rows,
-                           self._b.tokens, self._b.load_frames, self._b.inputs, self._b.status,
-                           self._b.checksums, self._b.lane_result)
+        if not self.valid:
+            raise _lib.GgrsError(_lib.GGRS_E_STATE, "lane batch views are stale: the engine re-mapped the "
+                                                           "batch (ggrs_lane_batch_map)")
+        b = self._run_struct(token_words, load_slots, adv_rows, save_rows)
         n = ctypes.c_int32()
         rc = self.engine._L.ggrs_lane_batch_run(self.engine._h, ctypes.byref(b), _lib.BATCH_STATUS if status else 0,
                                                 ctypes.byref(n))
+        if rc != _lib.GGRS_E_PRECONDITION:
+            _lib.check(rc)
+        return n.value
+
+
+    def encode(self, lane, reqs, inputs=None, status=None, lane_frame=NULL_FRAME):
+        """ggrs_lane_encode: lane `lane`'s ordered list -- reqs [(kind, frame)], inputs / status
+        [n_advance][P] -- into this batch (the C encoder the Rust handler and the bench driver
+        share).  lane_frame: the lane's frame before the list (NULL_FRAME skips the Save-frame
+        check).  Returns -1, or the index of the rejected Save (the lane was encoded empty)."""
+        if not self.valid:
+            raise _lib.GgrsError(_lib.GGRS_E_STATE, "lane batch views are stale")
+        P = self.engine.num_players
+        r = (_lib.Request * max(1, len(reqs)))(*[_lib.Request(int(k), int(f)) for k, f in reqs])
+        i = None if inputs is None else np.ascontiguousarray(inputs, np.uint8).reshape(-1)
+        st = None if status is None else np.ascontiguousarray(status, np.uint8).reshape(-1)
+        bad = ctypes.c_int32()
+        rc = self.engine._L.ggrs_lane_encode(ctypes.byref(self._b), self.engine.num_lanes, P, lane, r, len(reqs),
+                                             _vp(i), _vp(st), lane_frame, ctypes.byref(bad))
+        if rc == _lib.GGRS_E_PRECONDITION:
+            return bad.value
+        _lib.check(rc)
+        return -1
+
+    def _run_struct(self, token_words, load_slots, adv_rows, save_rows):
+        W, LD, A, S = self.shape
+        return _lib.LaneBatch(W if token_words is None else token_words, LD if load_slots is None else load_slots,
+                              A if adv_rows is None else adv_rows, S if save_rows is None else save_rows,
+                              self._b.tokens, self._b.load_frames, self._b.inputs, self._b.status,
+                              self._b.checksums, self._b.lane_result)
+
+    def submit(self, token_words=None, load_slots=None, adv_rows=None, save_rows=None, status=False):
+        """ggrs_lane_batch_submit: publish the batch and return at once (wait() collects it)."""
+        if not self.valid:
+            raise _lib.GgrsError(_lib.GGRS_E_STATE, "lane batch views are stale")
+        b = self._run_struct(token_words, load_slots, adv_rows, save_rows)
+        _lib.check(self.engine._L.ggrs_lane_batch_submit(self.engine._h, ctypes.byref(b),
+                                                         _lib.BATCH_STATUS if status else 0))
+
+    def wait(self):
+        """ggrs_lane_batch_wait: the submitted batch's results are in host memory; returns the
+        number of lanes that failed validation."""
+        n = ctypes.c_int32()
+        rc = self.engine._L.ggrs_lane_batch_wait(self.engine._h, ctypes.byref(n))
         if rc != _lib.GGRS_E_PRECONDITION:
             _lib.check(rc)
         return n.value

@@ -48,7 +48,9 @@
 extern "C" {
 #endif
 
-#define GGRS_ABI_VERSION 1
+/* 2: GGRS_PATH_* renumbered (2, 3 = the pipelined forms), lane batches submitted and waited for
+ * separately, host-side lane encoding, branch round forms */
+#define GGRS_ABI_VERSION 2
 
 #define GGRS_OK 0
 #define GGRS_E_INVALID (-1)      /* GgrsError::InvalidRequest: bad argument or configuration */
@@ -188,6 +190,35 @@ int ggrs_lane_batch_map(ggrs_engine_t* eng, int32_t token_words, int32_t load_sl
  * them are not read).  flags: GGRS_BATCH_STATUS.  Returns when checksums and lane_result are in
  * host memory; GGRS_E_PRECONDITION when *n_failed lanes failed validation (the rest ran). */
 int ggrs_lane_batch_run(ggrs_engine_t* eng, const ggrs_lane_batch_t* batch, int32_t flags, int32_t* n_failed);
+/* LDS one lane block needs for a batch shape, and the device's limit per workgroup (bytes): shapes
+ * with need > limit are GGRS_E_INVALID at ggrs_lane_batch_map. */
+int ggrs_lane_batch_lds(ggrs_engine_t* eng, int32_t token_words, int32_t load_slots, int32_t adv_rows,
+                        int32_t save_rows, int64_t* need_bytes, int64_t* limit_bytes);
+/* ggrs_lane_batch_run in two halves.  _submit publishes the batch (to the lane server, or enqueues
+ * one launch) and returns at once; _wait returns when its checksums and lane_result are in host
+ * memory, with ggrs_lane_batch_run's result.  Between them the caller must not touch this batch's
+ * memory, but may work on another engine's: a handler serving its sessions as two lane groups (two
+ * engines) encodes and hands back one group while the other's batch is on the device.  Any other
+ * call on the engine first waits for a submitted batch. */
+int ggrs_lane_batch_submit(ggrs_engine_t* eng, const ggrs_lane_batch_t* batch, int32_t flags);
+int ggrs_lane_batch_wait(ggrs_engine_t* eng, int32_t* n_failed);
+/* Host-side encoding of one session's ordered request list (src/lib.rs:171-195) into column `lane`
+ * of a lane batch -- the per-session work of a request handler, shared by every caller (the Rust
+ * crate, the bench's C driver).  reqs[n_reqs]; inputs / status: [n_advance][num_players], one row
+ * per AdvanceFrame in order (status NULL = Confirmed).  Writes every token word of the batch (END
+ * after the list), the lane's Load frames and input / status rows.  lane_frame = the lane's frame
+ * before the list (its previous lane_result; 0 for a fresh engine; GGRS_NULL_FRAME skips the check):
+ * the batch carries no Save frames, so each SaveGameState's frame is checked here against the frame
+ * the list has reached (Game::handle_requests' assert, ex_game.rs:104); on a mismatch the lane is
+ * encoded with an empty list (it will not run), *bad_request = the request's index and the call
+ * returns GGRS_E_PRECONDITION.  GGRS_E_INVALID: the list does not fit the batch's shape.  No device
+ * access: usable without a GPU. */
+int ggrs_lane_encode(const ggrs_lane_batch_t* batch, int64_t num_lanes, int32_t num_players, int64_t lane,
+                     const ggrs_request_t* reqs, int32_t n_reqs, const uint8_t* inputs, const uint8_t* status,
+                     int32_t lane_frame, int32_t* bad_request);
+/* The batch shape one list needs: shape = {token words (ceil(n_reqs / 16): a list of exactly 16 W
+ * requests needs no END token), Loads, AdvanceFrames, SaveGameStates}. */
+int ggrs_lane_shape(const ggrs_request_t* reqs, int32_t n_reqs, int32_t* shape);
 /* The generic form.  reqs: every lane's requests back to back, offsets: [num_lanes + 1]
  * (offsets[0] = 0).  inputs / status: [n_advance][num_players], one row per AdvanceFrame in the
  * same (lane, request) order; status NULL = all Confirmed.  save_checksums (may be NULL): one per
@@ -287,7 +318,8 @@ int ggrs_branch_read_report(ggrs_branch_engine_t* eng, uint16_t* checksums, uint
  * replayed trunk (a desync), or -1 */
 int ggrs_branch_read_desync(ggrs_branch_engine_t* eng, int32_t* first_frame);
 int ggrs_branch_read_trunk(ggrs_branch_engine_t* eng, int32_t session, uint8_t* out);
-/* the saved state (bincode) and checksum of `frame` in one lane's ring */
+/* the saved state (bincode) and checksum of `frame` in one lane's ring (after prefix-shared rounds:
+ * the cell of the lane's prefix representative, which holds the same state) */
 int ggrs_branch_read_lane(ggrs_branch_engine_t* eng, int64_t lane, int32_t frame, uint16_t* checksum,
                           uint8_t* out);
 int ggrs_branch_timing_reset(ggrs_branch_engine_t* eng);
@@ -295,8 +327,12 @@ int ggrs_branch_timing_read(ggrs_branch_engine_t* eng, float* total_ms, int32_t*
 /* n_rounds x (ggrs_branch_speculate, ggrs_branch_confirm without a report copy) issued back to
  * back from native code; while timing is collected one event pair brackets the whole batch */
 int ggrs_branch_rounds(ggrs_branch_engine_t* eng, int32_t n_rounds);
-/* rounds() as one launch (default: every block replays the trunks of its own sessions, so no
- * launch boundary is needed between rounds) or, on != 0, as 2 n launches of speculate / confirm */
+/* rounds() as one launch (on = 0, default: every block replays the trunks of its own sessions, so
+ * no launch boundary is needed between rounds; when the enumerated player is the only remote one the
+ * launch is prefix-shared -- each lane advances only that player, the local players' frames are
+ * computed once per block and session, and a cell at depth k is saved once per distinct k+1-digit
+ * prefix, by branch b mod A^min(k+1, E); ggrs_branch_read_lane resolves a lane's cell to it), as
+ * 2 n launches of speculate / confirm (on = 1), or as one launch without prefix sharing (on = 2) */
 int ggrs_branch_set_round_launches(ggrs_branch_engine_t* eng, int32_t on);
 /* Enqueue every launch and copy from now on on `stream` (a hipStream_t; NULL = the engine's own),
  * e.g. the stream a collective library orders its all-gather after: speculate, confirm (with its

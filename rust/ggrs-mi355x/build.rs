@@ -19,6 +19,7 @@ fn main() {
         .arg(csrc.join("particles.hip"))
         .arg(csrc.join("p2p.hip"))
         .arg(csrc.join("codec.hip"))
+        .arg(csrc.join("lane_encode.cpp"))
         .status()
         .expect("hipcc not found");
     assert!(status.success(), "hipcc failed");

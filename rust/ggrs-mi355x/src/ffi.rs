@@ -4,7 +4,7 @@
 #![allow(non_camel_case_types)]
 use std::os::raw::{c_char, c_void};
 
-pub const GGRS_ABI_VERSION: i32 = 1;
+pub const GGRS_ABI_VERSION: i32 = 2;
 
 pub const GGRS_OK: i32 = 0;
 pub const GGRS_E_INVALID: i32 = -1;
@@ -169,6 +169,14 @@ extern "C" {
     pub fn ggrs_handle_requests_lanes(eng: *mut ggrs_engine_t, reqs: *const ggrs_request_t, offsets: *const i32,
                                       inputs: *const u8, status: *const u8, save_checksums: *mut u16,
                                       lane_result: *mut i32) -> i32;
+    pub fn ggrs_lane_batch_lds(eng: *mut ggrs_engine_t, token_words: i32, load_slots: i32, adv_rows: i32,
+                               save_rows: i32, need_bytes: *mut i64, limit_bytes: *mut i64) -> i32;
+    pub fn ggrs_lane_batch_submit(eng: *mut ggrs_engine_t, batch: *const ggrs_lane_batch_t, flags: i32) -> i32;
+    pub fn ggrs_lane_batch_wait(eng: *mut ggrs_engine_t, n_failed: *mut i32) -> i32;
+    pub fn ggrs_lane_encode(batch: *const ggrs_lane_batch_t, num_lanes: i64, num_players: i32, lane: i64,
+                            reqs: *const ggrs_request_t, n_reqs: i32, inputs: *const u8, status: *const u8,
+                            lane_frame: i32, bad_request: *mut i32) -> i32;
+    pub fn ggrs_lane_shape(reqs: *const ggrs_request_t, n_reqs: i32, shape: *mut i32) -> i32;
     pub fn ggrs_lane_server(eng: *mut ggrs_engine_t, on: i32) -> i32;
     pub fn ggrs_read_lane_frames(eng: *mut ggrs_engine_t, frames: *mut i32) -> i32;
     pub fn ggrs_synchronize(eng: *mut ggrs_engine_t) -> i32;

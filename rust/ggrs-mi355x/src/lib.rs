@@ -48,7 +48,33 @@ pub struct BatchedBoxGame {
     eng: *mut ggrs_engine_t,
     lanes: usize,
     players: usize,
-    batch: Option<ggrs_lane_batch_t>,
+    /// every lane's frame after its last list (lane_result): the start frame the Save frames of
+    /// its next list are checked against (ex_game.rs:104), since the batch carries no Save frames
+    lane_frames: Vec<i32>,
+}
+
+/// One lane's list as the C ABI takes it: requests, and one input / status row per AdvanceFrame.
+fn lane_list<T>(list: &[GgrsRequest<T>], reqs: &mut Vec<ggrs_request_t>, inputs: &mut Vec<u8>, status: &mut Vec<u8>)
+where
+    T: Config,
+    T::Input: InputByte,
+{
+    reqs.clear();
+    inputs.clear();
+    status.clear();
+    for r in list {
+        match r {
+            GgrsRequest::SaveGameState { frame, .. } => reqs.push(ggrs_request_t { kind: GGRS_REQ_SAVE, frame: *frame }),
+            GgrsRequest::LoadGameState { frame, .. } => reqs.push(ggrs_request_t { kind: GGRS_REQ_LOAD, frame: *frame }),
+            GgrsRequest::AdvanceFrame { inputs: v } => {
+                reqs.push(ggrs_request_t { kind: GGRS_REQ_ADVANCE, frame: 0 });
+                for (inp, st) in v {
+                    inputs.push(inp.input_byte());
+                    status.push(status_byte(st));
+                }
+            }
+        }
+    }
 }
 
 impl BatchedBoxGame {
@@ -67,124 +93,90 @@ impl BatchedBoxGame {
         };
         let mut eng = std::ptr::null_mut();
         check(unsafe { ggrs_engine_create(&cfg, &mut eng) })?;
-        Ok(Self { eng, lanes, players, batch: None })
+        Ok(Self { eng, lanes, players, lane_frames: vec![0; lanes] })
     }
 
     /// `requests[l]` is session l's request list from its `advance_frame()`; lists may differ in
     /// kinds, frames and length.  Ok(None) when every lane ran; Ok(Some(failed)) when some lanes'
-    /// lists were rejected (those lanes did not run).
+    /// lists were rejected (those lanes did not run): a SaveGameState of a frame other than the one
+    /// the list has reached (checked while encoding, ggrs_lane_encode), or a Load of a frame the
+    /// lane's cell does not hold (checked on the device).
     pub fn handle_requests<T>(&mut self, requests: &[Vec<GgrsRequest<T>>]) -> Result<Option<FailedLanes>, EngineError>
     where
         T: Config,
         T::Input: InputByte,
     {
         assert_eq!(requests.len(), self.lanes);
-        // shape of the batch: the largest per-lane counts
-        let (mut nt, mut nl, mut na, mut ns) = (0usize, 0usize, 0usize, 0usize);
+        // every lane's list in the ABI's form, and the batch shape: the largest per-lane counts
+        let mut lists = Vec::with_capacity(self.lanes);
+        let mut shape = [0i32; 4];
         for list in requests {
-            let (mut l, mut a, mut s) = (0, 0, 0);
-            for r in list {
-                match r {
-                    GgrsRequest::SaveGameState { .. } => s += 1,
-                    GgrsRequest::LoadGameState { .. } => l += 1,
-                    GgrsRequest::AdvanceFrame { .. } => a += 1,
-                }
+            let (mut reqs, mut inputs, mut status) = (Vec::new(), Vec::new(), Vec::new());
+            lane_list(list, &mut reqs, &mut inputs, &mut status);
+            let mut s = [0i32; 4];
+            check(unsafe { ggrs_lane_shape(reqs.as_ptr(), reqs.len() as i32, s.as_mut_ptr()) })?;
+            for k in 0..4 {
+                shape[k] = shape[k].max(s[k]);
             }
-            nt = nt.max(list.len());
-            nl = nl.max(l);
-            na = na.max(a);
-            ns = ns.max(s);
+            lists.push((reqs, inputs, status));
         }
-        let tpw = GGRS_TOKENS_PER_WORD as usize;
-        let words = (nt + 1 + tpw - 1) / tpw; // room for the END token
-        if words > GGRS_BATCH_MAX_WORDS as usize || nl > GGRS_BATCH_MAX_LOADS as usize
-            || na > GGRS_BATCH_MAX_ADV as usize || ns > GGRS_BATCH_MAX_SAVES as usize {
+        if shape[0] > GGRS_BATCH_MAX_WORDS || shape[1] > GGRS_BATCH_MAX_LOADS || shape[2] > GGRS_BATCH_MAX_ADV
+            || shape[3] > GGRS_BATCH_MAX_SAVES {
             return self.handle_requests_csr(requests);
         }
-        let (w, ld, a, s) = (words.max(1), nl.max(1), na.max(1), ns.max(1));
-        let b = self.map_batch(w as i32, ld as i32, a as i32, s as i32)?;
-        let (l_n, p_n) = (self.lanes, self.players);
-        unsafe {
-            for (lane, list) in requests.iter().enumerate() {
-                let mut tok = vec![0u32; w];
-                let (mut k, mut li, mut ai) = (0usize, 0usize, 0usize);
-                for r in list {
-                    let t = match r {
-                        GgrsRequest::SaveGameState { .. } => GGRS_TOK_SAVE,
-                        GgrsRequest::LoadGameState { frame, .. } => {
-                            *b.load_frames.add(li * l_n + lane) = *frame;
-                            li += 1;
-                            GGRS_TOK_LOAD
-                        }
-                        GgrsRequest::AdvanceFrame { inputs } => {
-                            for (p, (inp, st)) in inputs.iter().enumerate() {
-                                *b.inputs.add((ai * l_n + lane) * p_n + p) = inp.input_byte();
-                                *b.status.add((ai * l_n + lane) * p_n + p) = status_byte(st);
-                            }
-                            ai += 1;
-                            GGRS_TOK_ADVANCE
-                        }
-                    };
-                    tok[k / tpw] |= t << (2 * (k % tpw));
-                    k += 1;
-                }
-                while k < w * tpw {
-                    tok[k / tpw] |= GGRS_TOK_END << (2 * (k % tpw));
-                    k += 1;
-                }
-                for (i, v) in tok.iter().enumerate() {
-                    *b.tokens.add(i * l_n + lane) = *v;
-                }
+        let (w, ld, a, s) = (shape[0].max(1), shape[1].max(1), shape[2].max(1), shape[3].max(1));
+        // mapped afresh on every call: a CSR call may have grown (and freed) the previous mapping
+        let mut b = ggrs_lane_batch_t {
+            token_words: 0, load_slots: 0, adv_rows: 0, save_rows: 0,
+            tokens: std::ptr::null_mut(), load_frames: std::ptr::null_mut(), inputs: std::ptr::null_mut(),
+            status: std::ptr::null_mut(), checksums: std::ptr::null_mut(), lane_result: std::ptr::null_mut(),
+        };
+        check(unsafe { ggrs_lane_batch_map(self.eng, w, ld, a, s, &mut b) })?;
+        let mut failed = Vec::new();
+        for (lane, (reqs, inputs, status)) in lists.iter().enumerate() {
+            let mut bad = -1i32;
+            let rc = unsafe {
+                ggrs_lane_encode(&b, self.lanes as i64, self.players as i32, lane as i64, reqs.as_ptr(),
+                                 reqs.len() as i32, inputs.as_ptr(), status.as_ptr(), self.lane_frames[lane], &mut bad)
+            };
+            match rc {
+                GGRS_OK => {}
+                GGRS_E_PRECONDITION => failed.push((lane, bad as usize)),
+                _ => return Err(EngineError(rc, last_error())),
             }
         }
         let mut run = b;
-        run.token_words = w as i32;
-        run.load_slots = ld as i32;
-        run.adv_rows = a as i32;
-        run.save_rows = s as i32;
+        run.token_words = w;
+        run.load_slots = ld;
+        run.adv_rows = a;
+        run.save_rows = s;
         let mut n_failed = 0i32;
         let rc = unsafe { ggrs_lane_batch_run(self.eng, &run, GGRS_BATCH_STATUS, &mut n_failed) };
         if rc != GGRS_OK && rc != GGRS_E_PRECONDITION {
             return Err(EngineError(rc, last_error()));
         }
         // every Save's checksum back to its GameStateCell, lane by lane; failed lanes report
-        let mut failed = Vec::new();
+        let rejected: std::collections::HashSet<usize> = failed.iter().map(|&(l, _)| l).collect();
         for (lane, list) in requests.iter().enumerate() {
             let res = unsafe { *b.lane_result.add(lane) };
             if res < 0 {
                 failed.push((lane, (-res - 1) as usize));
                 continue;
             }
+            self.lane_frames[lane] = res;
+            if rejected.contains(&lane) {
+                continue;
+            }
             let mut si = 0usize;
             for r in list {
                 if let GgrsRequest::SaveGameState { cell, frame } = r {
-                    let cs = unsafe { *b.checksums.add(si * l_n + lane) };
+                    let cs = unsafe { *b.checksums.add(si * self.lanes + lane) };
                     cell.save(*frame, None, Some(cs as u128));
                     si += 1;
                 }
             }
         }
         Ok(if failed.is_empty() { None } else { Some(FailedLanes { lanes: failed }) })
-    }
-
-    fn map_batch(&mut self, w: i32, ld: i32, a: i32, s: i32) -> Result<ggrs_lane_batch_t, EngineError> {
-        if let Some(b) = self.batch {
-            if b.token_words >= w && b.load_slots >= ld && b.adv_rows >= a && b.save_rows >= s {
-                return Ok(b);
-            }
-        }
-        let (w, ld, a, s) = match self.batch {
-            Some(b) => (w.max(b.token_words), ld.max(b.load_slots), a.max(b.adv_rows), s.max(b.save_rows)),
-            None => (w, ld, a, s),
-        };
-        let mut out = ggrs_lane_batch_t {
-            token_words: 0, load_slots: 0, adv_rows: 0, save_rows: 0,
-            tokens: std::ptr::null_mut(), load_frames: std::ptr::null_mut(), inputs: std::ptr::null_mut(),
-            status: std::ptr::null_mut(), checksums: std::ptr::null_mut(), lane_result: std::ptr::null_mut(),
-        };
-        check(unsafe { ggrs_lane_batch_map(self.eng, w, ld, a, s, &mut out) })?;
-        self.batch = Some(out);
-        Ok(out)
     }
 
     /// The generic per-lane form (ggrs_handle_requests_lanes): any list length.
@@ -235,6 +227,8 @@ impl BatchedBoxGame {
             let ok = result[lane] >= 0;
             if !ok {
                 failed.push((lane, (-result[lane] - 1) as usize));
+            } else {
+                self.lane_frames[lane] = result[lane];
             }
             for r in list {
                 if let GgrsRequest::SaveGameState { cell, frame } = r {

@@ -159,3 +159,78 @@ def test_full_size_config4(oracle):
             st = oracle.state_advance(st, truth[f, s])
         assert bytes(fused.trunk(s)) == bytes(st)
         assert int(a[0][s]) == oracle.fletcher16(bytes(st))
+
+
+@pytest.mark.parametrize("S,B,A,P,mask,W", [(1, 16 ** 4, 16, 2, 0b10, 4), (200, 16, 16, 2, 0b01, 6),
+                                           (7, 729, 3, 4, 0b0100, 6), (40, 9, 3, 3, 0b001, 2),
+                                           (5, 16, 16, 2, 0b10, 1), (33, 64, 4, 4, 0b1000, 5)])
+def test_prefix_rounds_equal_full_rounds(oracle, S, B, A, P, mask, W):
+    """Prefix-shared rounds (one remote player, enumerated: every lane advances only that player,
+    the local players' window and the depth-k representatives' cells shared) leave every lane's
+    cell -- resolved to its representative -- every trunk, report, survivor set and desync record
+    exactly as the full replay and as per-round speculate + confirm; sampled lanes equal the oracle's
+    adjust_gamestate replay."""
+    from ggrs_amd import BranchEngine, synth
+    n = 7
+    truth = synth.gen_inputs(13, S, 2 * n + W + 3, P, synth.MODEL_HELD)
+    engs = {f: BranchEngine(S, num_players=P, remote_mask=mask, window=W, branches=B, alphabet=A)
+            for f in ("fused", "full", "per_round")}
+    for f, e in engs.items():
+        e.add_inputs(0, truth)
+        e.set_round_form(f)
+        e.rounds(2)   # the second launch starts from a previous confirm (survivor check)
+        e.rounds(n - 2)
+        e.synchronize()
+    L = S * B
+    rng = np.random.default_rng(5)
+    lanes = sorted(set([0, 1, A - 1, A, B - 1, B % L, L // 2, L - 1] + rng.integers(0, L, 12).tolist()))
+    ref = engs["per_round"]
+    for f, e in engs.items():
+        assert e.trunk_frame() == n
+        a, b = e.report(), ref.report()
+        assert (a[0] == b[0]).all() and (a[1] == b[1]).all(), f
+        assert (e.desync() == -1).all(), f
+        for s in (0, S // 2, S - 1):
+            assert bytes(e.trunk(s)) == bytes(ref.trunk(s)), (f, s)
+        for lane in lanes:
+            for fr in range(n - 1, n + W):
+                x, y = e.lane_state(lane, fr), ref.lane_state(lane, fr)
+                assert x[0] == y[0] and bytes(x[1]) == bytes(y[1]), (f, lane, fr)
+    # against the oracle: the last round's replay from trunk frame n - 1
+    fused = engs["fused"]
+    for lane in lanes[:6]:
+        s = lane // B
+        st = oracle.state_new(P)
+        for fr in range(n - 1):
+            st = oracle.state_advance(st, truth[fr, s])
+        states, cks, _ = oracle.p2p_replay(st, n - 1, branch_inputs(fused, truth, n - 1, lane, W))
+        for k in range(W):
+            ck, got = fused.lane_state(lane, n + k)
+            assert ck == int(cks[k]) and bytes(got) == bytes(states[k]), (lane, k)
+
+
+def test_config3_fused_rounds_full_size(oracle):
+    """Config 3 through the bench's path (fused prefix-shared rounds): 16 rounds, then sampled
+    lanes of the last window against the oracle's replay, the trunk and the survivor count."""
+    from ggrs_amd import BranchEngine, synth
+    eng = BranchEngine(1, num_players=2, remote_mask=0b10, window=4, branches=16 ** 4, alphabet=16)
+    n = 16
+    truth = synth.gen_inputs(0, 1, n + 8, 2, synth.MODEL_HELD)
+    eng.add_inputs(0, truth)
+    eng.rounds(n)
+    eng.synchronize()
+    st = oracle.state_new(2)
+    for fr in range(n - 1):
+        st = oracle.state_advance(st, truth[fr, 0])
+    rng = np.random.default_rng(9)
+    for lane in sorted(set([0, 15, 16, 255, 256, 4095, 4096, 65535] + rng.integers(0, 65536, 8).tolist())):
+        states, cks, _ = oracle.p2p_replay(st, n - 1, branch_inputs(eng, truth, n - 1, lane, 4))
+        for k in range(4):
+            ck, got = eng.lane_state(lane, n + k)
+            assert ck == int(cks[k]) and bytes(got) == bytes(states[k]), (lane, k)
+    st = oracle.state_advance(st, truth[n - 1, 0])
+    assert bytes(eng.trunk(0)) == bytes(st)
+    ck, _ = eng.report()
+    assert int(ck[0]) == oracle.fletcher16(bytes(st))
+    assert eng.survivors().sum() == 16 ** 3
+    assert (eng.desync() == -1).all()

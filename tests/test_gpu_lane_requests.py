@@ -335,11 +335,24 @@ def test_batch_form_failure_count(oracle, L, server):
 def test_lane_batch_shape_beyond_lds_is_rejected(oracle):
     """A batch shape whose lane block would need more LDS than a workgroup gets is GGRS_E_INVALID
     at map time (not a failed launch); the largest shapes that fit still map."""
+    import ctypes
     from ggrs_amd import Engine, GgrsError
     eng = Engine(64, 2, 63, 0, 0)
+
+    def lds(shape):
+        need, lim = ctypes.c_int64(), ctypes.c_int64()
+        assert eng._L.ggrs_lane_batch_lds(eng._h, *shape, ctypes.byref(need), ctypes.byref(lim)) == 0
+        return need.value, lim.value
+
+    big, small = (32, 8, 128, 256), (8, 2, 32, 32)
+    # LaneLds at 2 players, ring 64: 184,832 bytes + 64 static for the big shape, over any
+    # CDNA workgroup's LDS (160 KiB on gfx950); the small one well under it
+    need, lim = lds(big)
+    assert need == 184896 and need > lim, (need, lim)
+    assert lds(small)[0] < lim
     with pytest.raises(GgrsError):
-        eng.lane_batch(32, 8, 128, 256)
-    b = eng.lane_batch(8, 2, 32, 32)
+        eng.lane_batch(*big)
+    b = eng.lane_batch(*small)
     b.tokens[:1] = 0xFFFFFFFF  # every lane's list empty
     assert b.run(1, 0, 0, 0) == 0
     assert (b.lane_result == 0).all()
@@ -375,3 +388,97 @@ def test_synchronize_stops_idle_server(oracle):
     for l in range(L):
         assert got[l] == exp[l]["save_cks"].tolist(), f"lane {l}"
     check_final(eng, exp, range(0, L, 7))
+
+
+def call_list_tuples(streams, c):
+    """Per lane: call c's requests [(kind, frame)], and its AdvanceFrame input / status rows."""
+    out = []
+    for s in streams:
+        idx = np.nonzero(s["call_of"] == c)[0]
+        k = s["kind"][idx]
+        adv = idx[k == REQ_ADVANCE]
+        out.append(([(int(s["kind"][i]), int(s["frame"][i])) for i in idx], s["inputs"][adv], s["status"][adv]))
+    return out
+
+
+@pytest.mark.parametrize("server", [True, False])
+def test_two_lane_groups_submit_wait(oracle, server):
+    """A handler serving its sessions as two lane groups (two engines): group A's batch is on the
+    device (ggrs_lane_batch_submit) while group B's lists are encoded (ggrs_lane_encode, the
+    shared C encoder, with every Save frame checked against the lane's frame) and submitted; then
+    both are collected (ggrs_lane_batch_wait).  Every Save's checksum, final state and ring equal
+    the oracle handler's."""
+    from ggrs_amd import Engine
+    G, calls, P, maxp = 136, 60, 2, 8
+    streams = p2p_lane_streams(oracle, 2 * G, calls, P, maxp, seed=23)
+    exp = expected(oracle, streams, P, maxp)
+    groups = [streams[:G], streams[G:]]
+    engs = [Engine(G, P, maxp, 0, 0) for _ in range(2)]
+    batches = []
+    for e in engs:
+        e.set_lane_server(server)
+        batches.append(e.lane_batch(2, 2, 2 * maxp + 2, 2 * maxp + 2))
+    frames = [np.zeros(G, np.int32) for _ in range(2)]
+    got = [[] for _ in range(2 * G)]
+    for c in range(calls):
+        per = [call_list_tuples(g, c) for g in groups]
+        for gi in range(2):
+            b = batches[gi]
+            for l, (reqs, inp, st) in enumerate(per[gi]):
+                assert b.encode(l, reqs, inp, st, int(frames[gi][l])) == -1
+            b.submit(status=True)
+        for gi in range(2):
+            b = batches[gi]
+            assert b.wait() == 0
+            assert (b.lane_result >= 0).all()
+            frames[gi][:] = b.lane_result
+            for l, (reqs, _, _) in enumerate(per[gi]):
+                n = sum(1 for k, _ in reqs if k == REQ_SAVE)
+                got[gi * G + l].extend(b.checksums[:n, l].tolist())
+    for l in range(2 * G):
+        assert got[l] == exp[l]["save_cks"].tolist(), f"lane {l}"
+    check_final(engs[0], exp[:G], range(0, G, 9))
+    check_final(engs[1], exp[G:], range(0, G, 9))
+
+
+def test_encoder_rejects_a_bad_save_frame_on_device(oracle):
+    """A Save of a frame other than the one the list reaches (ex_game.rs:104) is rejected by the
+    encoder: that lane runs an empty list (state untouched), the others run."""
+    from ggrs_amd import Engine
+    L, P, maxp = 72, 2, 8
+    eng = Engine(L, P, maxp, 0, 0)
+    b = eng.lane_batch(1, 1, 2, 2)
+    bad_lane = 5
+    for l in range(L):
+        reqs = [(REQ_SAVE, 0 if l != bad_lane else 3), (REQ_ADVANCE, 0)]
+        r = b.encode(l, reqs, np.full((1, P), 1, np.uint8), None, 0)
+        assert r == (0 if l == bad_lane else -1)
+    b.submit()
+    assert b.wait() == 0
+    fr = eng.lane_frames()
+    assert fr[bad_lane] == 0 and (np.delete(fr, bad_lane) == 1).all()
+
+
+def test_csr_growth_invalidates_batch_views(oracle):
+    """ADVICE r2: a CSR call whose list needs a larger batch re-maps (and frees) the lane batch;
+    views of the old mapping are invalidated instead of writing into freed pinned memory, and a
+    fresh batch runs a short list afterwards."""
+    from ggrs_amd import Engine, GgrsError
+    L, P, maxp = 16, 1, 8
+    eng = Engine(L, P, maxp, 0, 0)
+    old = eng.lane_batch(2, 1, 4, 4)
+    # 100 x (Save f, Advance) per lane: 13 token words, 100 advances -- larger than the mapping
+    n = 100
+    reqs = np.array([(REQ_SAVE, f // 2) if f % 2 == 0 else (REQ_ADVANCE, 0) for f in range(2 * n)] * L, np.int32)
+    off = np.arange(0, (L + 1) * 2 * n, 2 * n, dtype=np.int32)
+    inp = np.ones((n * L, P), np.uint8)
+    cks, res = eng.handle_requests_lanes(reqs, off, inp)
+    assert (res == n).all()
+    assert not old.valid and old.tokens is None
+    with pytest.raises(GgrsError):
+        old.run()
+    b = eng.lane_batch(1, 1, 1, 1)
+    for l in range(L):
+        assert b.encode(l, [(REQ_SAVE, n), (REQ_ADVANCE, 0)], np.ones((1, P), np.uint8), None, n) == -1
+    assert b.run(1, 0, 1, 1) == 0
+    assert (eng.lane_frames() == n + 1).all()

@@ -143,5 +143,5 @@ def test_build_rs_compiles_every_unit():
     leaves its symbols undefined in the crate's library)."""
     from ggrs_amd import build
     src = open(os.path.join(ROOT, "rust", "ggrs-mi355x", "build.rs")).read()
-    units = set(re.findall(r'csrc\.join\("(\w+\.hip)"\)', src))
+    units = set(re.findall(r'csrc\.join\("(\w+\.(?:hip|cpp))"\)', src))
     assert units == set(build.UNITS)
