@@ -520,16 +520,17 @@ def run_codec(args):
     dev = torch.device("cuda", local_rank)
     d_ref, d_pend, d_cnt = (torch.from_numpy(x).to(dev) for x in (ref, pend, count))
     stride = codec.max_packet_bytes(B, W)
+    chunked = args.codec_layout == "chunked"  # each 256-packet block's packets back to back
     evs = []
 
     def step(timed):
         e = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if timed else None
         if timed:
             e[0].record()
-        out, ln = codec.encode(d_ref, d_pend, d_cnt, stride)
+        out, ln = codec.encode(d_ref, d_pend, d_cnt, stride, chunked=chunked)
         if timed:
             e[1].record()
-        dec, cnt, st = codec.decode(d_ref, out, ln, W)
+        dec, cnt, st = codec.decode(d_ref, out, ln, W, chunked=chunked)
         if timed:
             e[2].record()
             evs.append(e)
@@ -567,8 +568,9 @@ def run_codec(args):
         try:
             from oracle import oracle as O
             O.build()
-            out_h = out.cpu().numpy()
-            same = all(out_h[p, :ln_h[p]].tobytes() ==
+            flat = out.cpu().numpy().reshape(-1)
+            off = codec.chunk_offsets(ln_h, stride) if chunked else np.arange(N, dtype=np.int64) * stride
+            same = all(flat[off[p]:off[p] + ln_h[p]].tobytes() ==
                        O.codec_encode(ref[p].tobytes(), [pend[p, k].tobytes() for k in range(W)])
                        for p in (0, 1, N // 2, N - 1))
             parity = {"round_trip_all_packets": ok, "packets_0_1_mid_last_bytes_equal_oracle": bool(same)}
@@ -590,14 +592,14 @@ def run_codec(args):
             "vs_baseline": None, "dtype": "u8", "data": "synthetic",
             "config": {"workload": f"codec: {N} endpoint packets per GPU, {W} pending inputs x {B} bytes, "
                                    f"held-key inputs; encode + decode per step",
-                       "packets_per_gpu": N, "pending": W, "input_bytes": B,
+                       "packets_per_gpu": N, "pending": W, "input_bytes": B, "layout": args.codec_layout,
                        "mean_packet_bytes": round(pkt_bytes / N, 2),
                        "parallelism": f"packets sharded over {world} GPU(s)"},
             "dist": dist_info(dist, per_rank),
             "kernel_ms": {"encode": round(enc_ms, 4), "decode": round(dec_ms, 4)},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                         "traffic": pmc_traffic(f"codec_{dom}_n{N}"),
+                         "traffic": pmc_traffic(f"codec_{dom}_n{N}" + ("" if chunked else "_strided")),
                          "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": round(dom_ms, 4)},
             "cpu_baseline": cpu_baseline, "parity": parity,
         }
@@ -1043,6 +1045,8 @@ def main():
     ap.add_argument("--sparse", action="store_true", help="p2p: sparse saving (SURVEY.md 8f row 4)")
     ap.add_argument("--req-form", choices=["native", "p2p", "batch", "lanes", "lockstep"], default="native",
                     help="requests: the boundary form (run_requests docstring)")
+    ap.add_argument("--codec-layout", choices=["chunked", "strided"], default="chunked",
+                    help="codec: packet layout (chunked: each 256-packet block's packets back to back)")
     ap.add_argument("--req-groups", type=int, default=2,
                     help="requests (native, p2p): lane groups (engines) whose batches overlap the host's work")
     ap.add_argument("--session-us", type=float, default=0.0,

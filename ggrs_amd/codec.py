@@ -23,6 +23,8 @@ def _bind(L):
     vp, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
     L.ggrs_codec_encode.argtypes = [vp, vp, vp, i64, i32, i32, vp, i32, vp, vp]
     L.ggrs_codec_decode.argtypes = [vp, vp, vp, i64, i32, i32, i32, vp, vp, vp, vp]
+    L.ggrs_codec_encode_chunked.argtypes = [vp, vp, vp, i64, i32, i32, vp, i32, vp, vp]
+    L.ggrs_codec_decode_chunked.argtypes = [vp, vp, vp, i64, i32, i32, i32, vp, vp, vp, vp]
     L.ggrs_codec_max_packet_bytes.argtypes = [i32, i32]
     L.ggrs_codec_max_packet_bytes.restype = i32
     L.ggrs_codec_set_direct.argtypes = [i32]
@@ -44,9 +46,10 @@ def max_packet_bytes(input_bytes, max_inputs):
     return L.ggrs_codec_max_packet_bytes(input_bytes, max_inputs)
 
 
-def encode(ref, pending, count, stride=None):
+def encode(ref, pending, count, stride=None, chunked=False):
     """ref [N][B], pending [N][W][B] (uint8, cuda), count [N] int32 -> (packets [N][stride] u8,
-    lengths [N] int32: packet bytes, or a negative GGRS_CODEC_E_* code)."""
+    lengths [N] int32: packet bytes, or a negative GGRS_CODEC_E_* code).  chunked: the packets of
+    each block of 256 back to back, dword-padded (chunk_offsets locates them)."""
     import torch
     L = _lib.lib()
     _bind(L)
@@ -58,12 +61,12 @@ def encode(ref, pending, count, stride=None):
     stride = stride or max_packet_bytes(B, W)
     out = torch.empty((N, stride), dtype=torch.uint8, device=pending.device)
     out_len = torch.empty(N, dtype=torch.int32, device=pending.device)
-    _lib.check(L.ggrs_codec_encode(_p(ref), _p(pending), _p(count), N, B, W, _p(out), stride, _p(out_len),
-                                   _stream(pending)))
+    fn = L.ggrs_codec_encode_chunked if chunked else L.ggrs_codec_encode
+    _lib.check(fn(_p(ref), _p(pending), _p(count), N, B, W, _p(out), stride, _p(out_len), _stream(pending)))
     return out, out_len
 
 
-def decode(ref, packets, lengths, max_inputs):
+def decode(ref, packets, lengths, max_inputs, chunked=False):
     """ref [N][B], packets [N][stride] u8, lengths [N] int32 -> (inputs [N][max_inputs][B] u8,
     count [N] int32, status [N] int32: 0 or a GGRS_CODEC_* code)."""
     import torch
@@ -76,9 +79,25 @@ def decode(ref, packets, lengths, max_inputs):
     out = torch.zeros((N, max_inputs, B), dtype=torch.uint8, device=packets.device)
     cnt = torch.empty(N, dtype=torch.int32, device=packets.device)
     st = torch.empty(N, dtype=torch.int32, device=packets.device)
-    _lib.check(L.ggrs_codec_decode(_p(ref), _p(packets), _p(lengths), N, stride, B, max_inputs, _p(out), _p(cnt),
-                                   _p(st), _stream(packets)))
+    fn = L.ggrs_codec_decode_chunked if chunked else L.ggrs_codec_decode
+    _lib.check(fn(_p(ref), _p(packets), _p(lengths), N, stride, B, max_inputs, _p(out), _p(cnt), _p(st),
+                  _stream(packets)))
     return out, cnt, st
+
+
+def chunk_offsets(lengths, stride):
+    """Byte offset of every packet in the chunked layout (numpy int64 [N]): block b = i // 256
+    starts at 256 * b * stride; inside it the packets' lengths padded to 4 bytes, back to back (a
+    length outside [1, stride] takes none)."""
+    import numpy as np
+    n = np.asarray(lengths, np.int64)
+    cb = np.where((n >= 1) & (n <= stride), (n + 3) & ~3, 0)
+    N = len(n)
+    out = np.zeros(N, np.int64)
+    for b0 in range(0, N, 256):
+        c = cb[b0:b0 + 256]
+        out[b0:b0 + 256] = 256 * (b0 // 256) * stride + np.concatenate([[0], np.cumsum(c)[:-1]])
+    return out
 
 
 KERNEL_FORMS = {"default": 0, "direct": 1, "staged": 2}

@@ -351,7 +351,9 @@ __device__ inline __amdgpu_buffer_rsrc_t prefix_rsrc(const void* base, uint32_t 
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 
-template <int P, int EP>
+// WT > 0: the window length as a compile-time constant (config 3's W = 4): the round's steps are
+// unrolled, so one step's rotation / sin-cos work overlaps the previous step's velocity chain.
+template <int P, int EP, int WT>
 __global__ __launch_bounds__(kPrefixBlock) void prefix_rounds_kernel(RoundsParams rp) {
   static_assert(EP >= 0 && EP < P, "enumerated player");
   constexpr int F = state_fields(P);
@@ -361,7 +363,8 @@ __global__ __launch_bounds__(kPrefixBlock) void prefix_rounds_kernel(RoundsParam
   constexpr int e = EP;
   extern __shared__ uint32_t lds_dyn[];
   const SpecParams& p = rp.sp;
-  const int W = p.W;
+  const int W = WT > 0 ? WT : p.W;
+  constexpr int kUnroll = WT > 0 ? WT : 1;
   const bool branch_wave = threadIdx.x < kRoundsBlock;  // wave-uniform
   const int64_t lane0 = (int64_t)blockIdx.x * kRoundsBlock;
   const int64_t lane = lane0 + (branch_wave ? threadIdx.x : 0);
@@ -502,7 +505,11 @@ __global__ __launch_bounds__(kPrefixBlock) void prefix_rounds_kernel(RoundsParam
     // cell's local players ARE the trunk's: one window entry) -- the representative may sit in a
     // block that is at another round of this launch
     const int32_t wnext = wrap_inc(wslot_c, W);
+#ifdef GGRS_EXP_PFX_NOEXTRA
+    if (false) {
+#else
     if (!branch_wave) {
+#endif
       // (a) the trunk's enumerated player with the confirmed input of f_c (the confirm replay), and
       // the window entry of frame f_c + W (into the slot frame f_c leaves); next round's rows
 #pragma unroll
@@ -551,8 +558,11 @@ __global__ __launch_bounds__(kPrefixBlock) void prefix_rounds_kernel(RoundsParam
     }
     int32_t slot = slot_c, wslot = wslot_c;
     int32_t pw = p.A;  // A^min(k+1, E): branches below it are depth k's representatives
+#pragma unroll kUnroll
     for (int32_t k = 0; k < W; ++k) {
+#ifndef GGRS_EXP_PFX_NOBAR1
       if (k == W - 1) lds_barrier();  // the window entry of frame f_c + W, the trunk replay
+#endif
       slot = wrap_inc(slot, p.R);     // frame f_c + k + 1
       wslot = wrap_inc(wslot, W);
       if (branch_wave) {
@@ -581,7 +591,11 @@ __global__ __launch_bounds__(kPrefixBlock) void prefix_rounds_kernel(RoundsParam
             d2 = dot4_u8(ev[q], wt[q], d2);
           }
           const uint32_t ck = fletcher_from_doubled(d1, d2);
+#ifdef GGRS_EXP_PFX_NOSTORE
+          if (false) {
+#else
           if (rep) {  // per-lane field offsets, the slot's offset wave-uniform
+#endif
             const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)slot * slot_bytes);
             __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(f_c + k + 1), rs_ring, lo, so, 0);
             int li = 0;
@@ -1096,7 +1110,8 @@ int launch_rounds(ggrs_branch_engine* e, int32_t n_rounds, void* copy, bool ever
         constexpr int P = decltype(PC)::value;
         dispatch_enumerated<P>(p.first_remote, [&](auto EC) {
           constexpr int EP = decltype(EC)::value;
-          prefix_rounds_kernel<P, EP><<<grid, kPrefixBlock, lds, e->stream>>>(rp);
+          if (p.W == 4) prefix_rounds_kernel<P, EP, 4><<<grid, kPrefixBlock, lds, e->stream>>>(rp);
+          else prefix_rounds_kernel<P, EP, 0><<<grid, kPrefixBlock, lds, e->stream>>>(rp);
         });
       });
       return;

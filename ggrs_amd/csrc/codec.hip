@@ -556,13 +556,45 @@ __host__ __device__ inline int swar_out_pitch(int stride, int ndw) {
   return odd_dword_pitch(stride > 9 + 12 * ndw ? stride : 9 + 12 * ndw);
 }
 
-template <int B, int NDW>
+// Chunked packet layout (ggrs_codec_encode_chunked / _decode_chunked): the packets of the 256-packet
+// block b lie back to back from byte b * 256 * stride, each padded to whole dwords (a packet whose
+// length is outside [1, stride] -- an error code -- takes no bytes), so a block's packets are one
+// contiguous run of exactly their bytes: encode writes and decode reads the packets' own bytes with
+// coalesced dword copies, instead of whole stride-byte rows (a received datagram buffer holds the
+// packets back to back as well).  The byte offsets follow from the lengths by a block-wide scan.
+__device__ inline int chunk_bytes(int64_t len, int stride) {
+  return (len >= 1 && len <= stride) ? (int)((len + 3) & ~3ll) : 0;
+}
+// exclusive prefix sum over the block (blockDim.x <= 1024, a multiple of 64); *total = the sum
+__device__ inline int block_excl_scan(int v, int* wsum, int* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  int base = 0, tot = 0;
+  for (int w = 0; w < (int)(blockDim.x >> 6); w++) {
+    const int sw = wsum[w];
+    base += w < wid ? sw : 0;
+    tot += sw;
+  }
+  *total = tot;
+  return base + x - v;
+}
+
+template <int B, int NDW, bool kChunked>
 __global__ __launch_bounds__(256) void encode_swar_kernel(EncodeParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int T = blockDim.x, W = p.W, WB = W * B, stride = p.stride;
   const int out_pitch = swar_out_pitch(stride, NDW), x_pitch = odd_dword_pitch(4 * NDW);
   uint8_t* l_out = smem;                    // [T][out_pitch]
   uint8_t* l_x = l_out + T * out_pitch;     // [T][x_pitch] delta bytes, for literal copies
+  uint8_t* l_chunk = l_x + T * x_pitch;     // kChunked: [T * stride] the block's packets back to back
+  __shared__ int wsum[4];
   const int64_t pk0 = (int64_t)blockIdx.x * T;
   const int np = (int)((p.N - pk0) < T ? (p.N - pk0) : T);
   for (int q = threadIdx.x; q < np * out_pitch / 4; q += T) reinterpret_cast<uint32_t*>(l_out)[q] = 0;
@@ -570,6 +602,7 @@ __global__ __launch_bounds__(256) void encode_swar_kernel(EncodeParams p) {
   const int64_t pk = pk0 + t;
   uint32_t cw[NDW], xw[NDW];
   int32_t n = 0;
+  int32_t code = 0;  // the packet's length or error code
   uint32_t rw = 0;
   if (t < np) {
     n = p.count[pk];
@@ -589,7 +622,6 @@ __global__ __launch_bounds__(256) void encode_swar_kernel(EncodeParams p) {
   }
   __syncthreads();  // output rows zeroed
   if (t < np) {
-    int32_t code;
     if (n < 0 || n > W) {
       code = GGRS_CODEC_E_INVALID;
     } else {
@@ -633,11 +665,24 @@ __global__ __launch_bounds__(256) void encode_swar_kernel(EncodeParams p) {
     }
     p.out_len[pk] = code;
   }
-  __syncthreads();
-  lds_to_block(p.out + pk0 * stride, l_out, out_pitch, np, stride);
+  if constexpr (kChunked) {
+    int total;
+    const int cb = t < np ? chunk_bytes(code, stride) : 0;
+    const int off = block_excl_scan(cb, wsum, &total);  // (its barrier also orders the row writes)
+    const uint32_t* row = reinterpret_cast<const uint32_t*>(l_out + t * out_pitch);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(l_chunk + off);
+    for (int k = 0; k < cb / 4; k++) dst[k] = row[k];
+    __syncthreads();
+    uint32_t* out32 = reinterpret_cast<uint32_t*>(p.out + pk0 * stride);
+    const uint32_t* c32 = reinterpret_cast<const uint32_t*>(l_chunk);
+    for (int q = t; q < total / 4; q += T) out32[q] = c32[q];
+  } else {
+    __syncthreads();
+    lds_to_block(p.out + pk0 * stride, l_out, out_pitch, np, stride);
+  }
 }
 
-template <int B, int NDW>
+template <int B, int NDW, bool kChunked>
 __global__ __launch_bounds__(256) void decode_swar_kernel(DecodeParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int T = blockDim.x, W = p.W, WB = W * B, stride = p.stride;
@@ -648,12 +693,22 @@ __global__ __launch_bounds__(256) void decode_swar_kernel(DecodeParams p) {
   uint8_t* l_out = l_x + T * x_pitch;       // [T][out_pitch] decoded inputs
   const int64_t pk0 = (int64_t)blockIdx.x * T;
   const int np = (int)((p.N - pk0) < T ? (p.N - pk0) : T);
-  block_to_lds(l_in, in_pitch, p.packets + pk0 * stride, np, stride);
-  __syncthreads();
   const int t = threadIdx.x;
+  int d_off = t * in_pitch;
+  if constexpr (kChunked) {  // the block's packets back to back: one coalesced copy of their bytes
+    __shared__ int wsum[4];
+    int total;
+    const int cb = t < np ? chunk_bytes(p.len[pk0 + t], stride) : 0;
+    d_off = block_excl_scan(cb, wsum, &total);
+    const uint32_t* s32 = reinterpret_cast<const uint32_t*>(p.packets + pk0 * stride);
+    for (int q = t; q < total / 4; q += T) reinterpret_cast<uint32_t*>(l_in)[q] = s32[q];
+  } else {
+    block_to_lds(l_in, in_pitch, p.packets + pk0 * stride, np, stride);
+  }
+  __syncthreads();
   if (t < np) {
     const int64_t pk = pk0 + t;
-    const uint8_t* d = l_in + t * in_pitch;
+    const uint8_t* d = l_in + d_off;
     constexpr int kCap = 4 * NDW;  // scratch bytes: any valid packet expands to <= W * B of them
     uint8_t* xb = l_x + t * x_pitch;
     uint32_t* xr32 = reinterpret_cast<uint32_t*>(xb);
@@ -761,8 +816,8 @@ __global__ __launch_bounds__(256) void decode_swar_kernel(DecodeParams p) {
   lds_to_block(p.out + pk0 * (int64_t)WB, l_out, out_pitch, np, WB);
 }
 
-size_t encode_swar_bytes(int ndw, int stride) {
-  return (size_t)256 * (swar_out_pitch(stride, ndw) + odd_dword_pitch(4 * ndw));
+size_t encode_swar_bytes(int ndw, int stride, bool chunked = false) {
+  return (size_t)256 * (swar_out_pitch(stride, ndw) + odd_dword_pitch(4 * ndw) + (chunked ? stride : 0));
 }
 size_t decode_swar_bytes(int ndw, int B, int W, int stride) {
   return (size_t)256 * (odd_dword_pitch(stride) + odd_dword_pitch(4 * ndw) + odd_dword_pitch(W * B));
@@ -777,25 +832,37 @@ int swar_ndw(int B, int W, int stride) {
   return n;
 }
 
-template <int B>
+template <int B, bool C>
 void launch_encode_swar(int ndw, int64_t grid, size_t lds, hipStream_t s, const EncodeParams& p) {
   switch (ndw) {
-    case 1: encode_swar_kernel<B, 1><<<grid, 256, lds, s>>>(p); break;
-    case 2: encode_swar_kernel<B, 2><<<grid, 256, lds, s>>>(p); break;
-    case 4: encode_swar_kernel<B, 4><<<grid, 256, lds, s>>>(p); break;
-    case 8: encode_swar_kernel<B, 8><<<grid, 256, lds, s>>>(p); break;
-    default: encode_swar_kernel<B, 16><<<grid, 256, lds, s>>>(p); break;
+    case 1: encode_swar_kernel<B, 1, C><<<grid, 256, lds, s>>>(p); break;
+    case 2: encode_swar_kernel<B, 2, C><<<grid, 256, lds, s>>>(p); break;
+    case 4: encode_swar_kernel<B, 4, C><<<grid, 256, lds, s>>>(p); break;
+    case 8: encode_swar_kernel<B, 8, C><<<grid, 256, lds, s>>>(p); break;
+    default: encode_swar_kernel<B, 16, C><<<grid, 256, lds, s>>>(p); break;
   }
 }
-template <int B>
+template <int B, bool C>
 void launch_decode_swar(int ndw, int64_t grid, size_t lds, hipStream_t s, const DecodeParams& p) {
   switch (ndw) {
-    case 1: decode_swar_kernel<B, 1><<<grid, 256, lds, s>>>(p); break;
-    case 2: decode_swar_kernel<B, 2><<<grid, 256, lds, s>>>(p); break;
-    case 4: decode_swar_kernel<B, 4><<<grid, 256, lds, s>>>(p); break;
-    case 8: decode_swar_kernel<B, 8><<<grid, 256, lds, s>>>(p); break;
-    default: decode_swar_kernel<B, 16><<<grid, 256, lds, s>>>(p); break;
+    case 1: decode_swar_kernel<B, 1, C><<<grid, 256, lds, s>>>(p); break;
+    case 2: decode_swar_kernel<B, 2, C><<<grid, 256, lds, s>>>(p); break;
+    case 4: decode_swar_kernel<B, 4, C><<<grid, 256, lds, s>>>(p); break;
+    case 8: decode_swar_kernel<B, 8, C><<<grid, 256, lds, s>>>(p); break;
+    default: decode_swar_kernel<B, 16, C><<<grid, 256, lds, s>>>(p); break;
   }
+}
+template <bool C>
+void encode_swar_any(int B, int ndw, int64_t grid, size_t lds, hipStream_t s, const EncodeParams& p) {
+  if (B == 1) launch_encode_swar<1, C>(ndw, grid, lds, s, p);
+  else if (B == 2) launch_encode_swar<2, C>(ndw, grid, lds, s, p);
+  else launch_encode_swar<4, C>(ndw, grid, lds, s, p);
+}
+template <bool C>
+void decode_swar_any(int B, int ndw, int64_t grid, size_t lds, hipStream_t s, const DecodeParams& p) {
+  if (B == 1) launch_decode_swar<1, C>(ndw, grid, lds, s, p);
+  else if (B == 2) launch_decode_swar<2, C>(ndw, grid, lds, s, p);
+  else launch_decode_swar<4, C>(ndw, grid, lds, s, p);
 }
 
 // LDS bytes for a block of T threads, or 0 when the staged form does not apply
@@ -826,10 +893,7 @@ int ggrs_codec_encode(const uint8_t* ref, const uint8_t* pending, const int32_t*
   const bool al = aligned4(pending) && aligned4(out);
   if (g_codec_mode == 0 && ndw && al && encode_swar_bytes(ndw, out_stride) <= kLdsBudget) {
     const size_t lds = encode_swar_bytes(ndw, out_stride);
-    const int64_t grid = grid_of(n_packets, 256);
-    if (input_bytes == 1) launch_encode_swar<1>(ndw, grid, lds, (hipStream_t)stream, p);
-    else if (input_bytes == 2) launch_encode_swar<2>(ndw, grid, lds, (hipStream_t)stream, p);
-    else launch_encode_swar<4>(ndw, grid, lds, (hipStream_t)stream, p);
+    encode_swar_any<false>(input_bytes, ndw, grid_of(n_packets, 256), lds, (hipStream_t)stream, p);
     HIP_TRY(hipGetLastError());
     return GGRS_OK;
   }
@@ -854,10 +918,7 @@ int ggrs_codec_decode(const uint8_t* ref, const uint8_t* packets, const int32_t*
   const bool al = aligned4(packets) && aligned4(out);
   if (g_codec_mode == 0 && ndw && al && decode_swar_bytes(ndw, input_bytes, max_inputs, packet_stride) <= kLdsBudget) {
     const size_t lds = decode_swar_bytes(ndw, input_bytes, max_inputs, packet_stride);
-    const int64_t grid = grid_of(n_packets, 256);
-    if (input_bytes == 1) launch_decode_swar<1>(ndw, grid, lds, (hipStream_t)stream, p);
-    else if (input_bytes == 2) launch_decode_swar<2>(ndw, grid, lds, (hipStream_t)stream, p);
-    else launch_decode_swar<4>(ndw, grid, lds, (hipStream_t)stream, p);
+    decode_swar_any<false>(input_bytes, ndw, grid_of(n_packets, 256), lds, (hipStream_t)stream, p);
     HIP_TRY(hipGetLastError());
     return GGRS_OK;
   }
@@ -866,6 +927,42 @@ int ggrs_codec_decode(const uint8_t* ref, const uint8_t* packets, const int32_t*
     decode_lds_kernel<<<grid_of(n_packets, 256), 256, lds, (hipStream_t)stream>>>(p);
   else
     decode_kernel<<<grid_of(n_packets, 256), 256, 0, (hipStream_t)stream>>>(p);
+  HIP_TRY(hipGetLastError());
+  return GGRS_OK;
+}
+
+int ggrs_codec_encode_chunked(const uint8_t* ref, const uint8_t* pending, const int32_t* count, int64_t n_packets,
+                              int32_t input_bytes, int32_t max_inputs, uint8_t* out, int32_t out_stride,
+                              int32_t* out_len, void* stream) {
+  if (n_packets < 0 || input_bytes < 1 || max_inputs < 0 || out_stride < 9)
+    return set_error(GGRS_E_INVALID, "codec: need n_packets >= 0, input_bytes >= 1, max_inputs >= 0, stride >= 9");
+  if (n_packets == 0) return GGRS_OK;
+  if (!ref || !pending || !count || !out || !out_len) return set_error(GGRS_E_INVALID, "null argument");
+  const int ndw = swar_ndw(input_bytes, max_inputs, out_stride);
+  if (!ndw || !aligned4(pending) || !aligned4(out) || encode_swar_bytes(ndw, out_stride, true) > kLdsBudget)
+    return set_error(GGRS_E_INVALID, "codec: the chunked layout needs 1-, 2- or 4-byte inputs, W * B <= 64 and "
+                                     "multiple of 4, a stride multiple of 4 and dword-aligned buffers");
+  EncodeParams p{ref, pending, count, out, out_len, n_packets, input_bytes, max_inputs, out_stride};
+  encode_swar_any<true>(input_bytes, ndw, grid_of(n_packets, 256), encode_swar_bytes(ndw, out_stride, true),
+                        (hipStream_t)stream, p);
+  HIP_TRY(hipGetLastError());
+  return GGRS_OK;
+}
+
+int ggrs_codec_decode_chunked(const uint8_t* ref, const uint8_t* packets, const int32_t* packet_len, int64_t n_packets,
+                              int32_t packet_stride, int32_t input_bytes, int32_t max_inputs, uint8_t* out,
+                              int32_t* count, int32_t* status, void* stream) {
+  if (n_packets < 0 || input_bytes < 1 || max_inputs < 0 || packet_stride < 0)
+    return set_error(GGRS_E_INVALID, "codec: need n_packets >= 0, input_bytes >= 1, max_inputs >= 0");
+  if (n_packets == 0) return GGRS_OK;
+  if (!ref || !packets || !packet_len || !out || !count || !status) return set_error(GGRS_E_INVALID, "null argument");
+  const int ndw = swar_ndw(input_bytes, max_inputs, packet_stride);
+  const size_t lds = ndw ? decode_swar_bytes(ndw, input_bytes, max_inputs, packet_stride) : 0;
+  if (!ndw || !aligned4(packets) || !aligned4(out) || lds > kLdsBudget)
+    return set_error(GGRS_E_INVALID, "codec: the chunked layout needs 1-, 2- or 4-byte inputs, W * B <= 64 and "
+                                     "multiple of 4, a stride multiple of 4 and dword-aligned buffers");
+  DecodeParams p{ref, packets, packet_len, out, count, status, n_packets, input_bytes, max_inputs, packet_stride};
+  decode_swar_any<true>(input_bytes, ndw, grid_of(n_packets, 256), lds, (hipStream_t)stream, p);
   HIP_TRY(hipGetLastError());
   return GGRS_OK;
 }

@@ -514,6 +514,20 @@ int ggrs_codec_encode(const uint8_t* ref, const uint8_t* pending, const int32_t*
 int ggrs_codec_decode(const uint8_t* ref, const uint8_t* packets, const int32_t* packet_len, int64_t n_packets,
                       int32_t packet_stride, int32_t input_bytes, int32_t max_inputs, uint8_t* out, int32_t* count,
                       int32_t* status, void* stream);
+/* The same with the chunked packet layout: the packets of each block of 256 (packets
+ * 256 b .. 256 b + 255) lie back to back from byte 256 * b * stride of out / packets, each padded to
+ * a multiple of 4 bytes; a packet whose length is outside [1, stride] (an error code) takes no
+ * bytes.  Packet i's offset is 256 * (i / 256) * stride plus the padded lengths of the block's
+ * packets before it, so the lengths alone locate every packet; the kernels move exactly the
+ * packets' bytes instead of whole stride-byte rows.  Requires input_bytes in {1, 2, 4},
+ * max_inputs * input_bytes <= 64 and a multiple of 4, stride a multiple of 4, dword-aligned
+ * buffers (GGRS_E_INVALID otherwise). */
+int ggrs_codec_encode_chunked(const uint8_t* ref, const uint8_t* pending, const int32_t* count, int64_t n_packets,
+                              int32_t input_bytes, int32_t max_inputs, uint8_t* out, int32_t out_stride,
+                              int32_t* out_len, void* stream);
+int ggrs_codec_decode_chunked(const uint8_t* ref, const uint8_t* packets, const int32_t* packet_len, int64_t n_packets,
+                              int32_t packet_stride, int32_t input_bytes, int32_t max_inputs, uint8_t* out,
+                              int32_t* count, int32_t* status, void* stream);
 /* an out_stride that every packet of max_inputs inputs fits (a multiple of 16) */
 int32_t ggrs_codec_max_packet_bytes(int32_t input_bytes, int32_t max_inputs);
 /* kernel forms (for tests and comparison; process-wide): 0 = default (lane-cooperative where

@@ -273,6 +273,12 @@ extern "C" {
     pub fn ggrs_codec_decode(ref_: *const u8, packets: *const u8, packet_len: *const i32, n_packets: i64,
                              packet_stride: i32, input_bytes: i32, max_inputs: i32, out: *mut u8,
                              count: *mut i32, status: *mut i32, stream: *mut c_void) -> i32;
+    pub fn ggrs_codec_encode_chunked(ref_: *const u8, pending: *const u8, count: *const i32, n_packets: i64,
+                                     input_bytes: i32, max_inputs: i32, out: *mut u8, out_stride: i32,
+                                     out_len: *mut i32, stream: *mut c_void) -> i32;
+    pub fn ggrs_codec_decode_chunked(ref_: *const u8, packets: *const u8, packet_len: *const i32, n_packets: i64,
+                                     packet_stride: i32, input_bytes: i32, max_inputs: i32, out: *mut u8,
+                                     count: *mut i32, status: *mut i32, stream: *mut c_void) -> i32;
     pub fn ggrs_codec_max_packet_bytes(input_bytes: i32, max_inputs: i32) -> i32;
     pub fn ggrs_codec_set_direct(mode: i32) -> i32;
 }

@@ -135,3 +135,57 @@ def test_encode_errors(oracle, kernels, W, B):
             assert ln[p] == codec.E_CAP, p
         else:
             assert ln[p] == len(want) and out[p, :ln[p]].tobytes() == want, p
+
+
+@pytest.mark.parametrize("N,W,B,held", [(5000, 8, 1, True), (3000, 16, 2, False), (4000, 8, 2, True),
+                                         (3000, 8, 4, True), (2000, 12, 1, True), (777, 4, 1, False)])
+def test_chunked_layout_matches_oracle(oracle, N, W, B, held):
+    """The chunked layout (each 256-packet block's packets back to back, dword-padded): every
+    packet's bytes at its chunk offset equal the oracle's encoding, and the chunked decode returns
+    what the strided decode returns."""
+    from ggrs_amd import codec
+    rng = np.random.default_rng(N * 3 + W + B)
+    ref, pend, count = batch(rng, N, W, B, held)
+    out, ln = codec.encode(gpu(ref), gpu(pend), gpu(count), chunked=True)
+    stride = out.shape[1]
+    flat, lh = out.cpu().numpy().reshape(-1), ln.cpu().numpy()
+    off = codec.chunk_offsets(lh, stride)
+    for p in range(N):
+        want = oracle.codec_encode(ref[p].tobytes(), [pend[p, k].tobytes() for k in range(count[p])])
+        assert lh[p] == len(want), p
+        assert flat[off[p]:off[p] + lh[p]].tobytes() == want, p
+        pad = (-int(lh[p])) % 4
+        assert not flat[off[p] + lh[p]:off[p] + lh[p] + pad].any(), p  # padding is zero
+    dec, cnt, st = codec.decode(gpu(ref), out, ln, max_inputs=W, chunked=True)
+    dec, cnt, st = dec.cpu().numpy(), cnt.cpu().numpy(), st.cpu().numpy()
+    assert (st == 0).all() and (cnt == count).all()
+    for p in range(N):
+        assert (dec[p, :count[p]] == pend[p, :count[p]]).all(), p
+
+
+def test_chunked_decode_hostile_lengths_match_strided(oracle):
+    """Lengths outside [1, stride] take no bytes in the chunked layout and give the strided decode's
+    error codes; mutated packets at their chunk offsets decode as the strided form of the same bytes."""
+    from ggrs_amd import codec
+    rng = np.random.default_rng(77)
+    N, W, B = 3000, 16, 2
+    ref, pend, count = batch(rng, N, W, B)
+    out, ln = codec.encode(gpu(ref), gpu(pend), gpu(count))  # strided
+    pk, lh = out.cpu().numpy().copy(), ln.cpu().numpy().copy()
+    stride = pk.shape[1]
+    for p in range(N):
+        if rng.random() < 0.3:
+            pk[p, int(rng.integers(0, max(lh[p], 1)))] = rng.integers(0, 256)
+    bad = rng.random(N) < 0.1
+    lh[bad] = rng.choice([-5, 0, stride + 4, 10 ** 6], int(bad.sum())).astype(np.int32)
+    # the same packets in the chunked layout
+    off = codec.chunk_offsets(lh, stride)
+    flat = np.zeros(N * stride, np.uint8)
+    for p in range(N):
+        if 1 <= lh[p] <= stride:
+            flat[off[p]:off[p] + lh[p]] = pk[p, :lh[p]]
+    a = codec.decode(gpu(ref), gpu(pk), gpu(lh), max_inputs=W)
+    b = codec.decode(gpu(ref), gpu(flat.reshape(N, stride)), gpu(lh), max_inputs=W, chunked=True)
+    for x, y in zip(a, b):
+        assert (x.cpu().numpy() == y.cpu().numpy()).all()
+    assert (b[2].cpu().numpy()[bad] != 0).all()
