@@ -248,9 +248,10 @@ def run_branch(args):
     else:
         ex.run(args.steps * rps)  # a batch of rounds per launch and per all-gather
         ex.drain()
-    kernel_ms, launches = eng.timing_read()  # the end event right behind the last launch
+    eng.timing_stop()  # the end event right behind the last launch, no wait inside the span
     sync_all()
     t1 = time.perf_counter()
+    kernel_ms, launches = eng.timing_read()
     elapsed = t1 - t0
     n_desync = int(ex.desync_count.item()) if ex is not None else 0
     resim_round = L * W + S
@@ -336,11 +337,12 @@ def run_particles(args):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         eng.synctest_advance_frames(1)
-    kernel_ms, launches = eng.timing_read()  # the end event right behind the last launch
+    eng.timing_stop()  # the end event right behind the last launch, no wait inside the span
     eng.synchronize()
     if dist is not None:
         dist.barrier()
     t1 = time.perf_counter()
+    kernel_ms, launches = eng.timing_read()
     elapsed = t1 - t0
     elapsed, total, per_rank = rank_timings(dist, torch, elapsed, S * cd * args.steps)
     st, _, _ = eng.mismatches()
@@ -433,11 +435,12 @@ def run_p2p(args):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    kernel_ms, launches = eng.timing_read()  # the end event right behind the last launch
+    eng.timing_stop()  # the end event right behind the last launch, no wait inside the span
     eng.synchronize()
     if dist is not None:
         dist.barrier()
     t1 = time.perf_counter()
+    kernel_ms, launches = eng.timing_read()
     elapsed = t1 - t0
     n_desync = len(events)
     session_calls = S * calls * args.steps
@@ -1104,9 +1107,10 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         eng.synctest_advance_frames(fps)
-    kernel_ms, launches = eng.timing_read()  # the end event right behind the last launch
+    eng.timing_stop()  # the end event right behind the last launch, no wait inside the span
     barrier()
     t1 = time.perf_counter()
+    kernel_ms, launches = eng.timing_read()
     elapsed = t1 - t0
     elapsed, total_resim, per_rank = rank_timings(dist, torch, elapsed, lanes * cd * fps * args.steps)
 

@@ -33,7 +33,7 @@ EXPORTS = (
     "ggrs_synctest_advance_frames", "ggrs_handle_requests", "ggrs_synchronize",
     "ggrs_current_frame", "ggrs_read_mismatches", "ggrs_read_save_checksums", "ggrs_read_save_checksums_frames", "ggrs_read_state",
     "ggrs_read_ring", "ggrs_read_trace", "ggrs_debug_corrupt_on_load", "ggrs_last_launch_ms",
-    "ggrs_timing_reset", "ggrs_timing_read", "ggrs_set_synctest_path",
+    "ggrs_timing_reset", "ggrs_timing_stop", "ggrs_timing_read", "ggrs_set_synctest_path",
     "ggrs_lane_batch_map", "ggrs_lane_batch_run", "ggrs_handle_requests_lanes", "ggrs_read_lane_frames",
     "ggrs_lane_server", "ggrs_lane_batch_submit", "ggrs_lane_batch_wait", "ggrs_lane_encode", "ggrs_lane_shape",
     "ggrs_lane_batch_lds",
@@ -41,18 +41,18 @@ EXPORTS = (
     "ggrs_branch_add_inputs", "ggrs_branch_speculate", "ggrs_branch_confirm",
     "ggrs_branch_report_bytes", "ggrs_branch_synchronize", "ggrs_branch_trunk_frame",
     "ggrs_branch_read_report", "ggrs_branch_read_desync", "ggrs_branch_read_trunk",
-    "ggrs_branch_read_lane", "ggrs_branch_timing_reset", "ggrs_branch_timing_read",
+    "ggrs_branch_read_lane", "ggrs_branch_timing_reset", "ggrs_branch_timing_stop", "ggrs_branch_timing_read",
     "ggrs_branch_rounds", "ggrs_branch_set_round_launches", "ggrs_branch_set_stream",
     "ggrs_branch_round", "ggrs_branch_rounds_reports", "ggrs_branch_compare_peer", "ggrs_branch_compare_peer_rows",
     "ggrs_particle_engine_create", "ggrs_particle_engine_destroy", "ggrs_particle_add_local_inputs",
     "ggrs_particle_synctest_advance_frames", "ggrs_particle_synchronize",
     "ggrs_particle_current_frame", "ggrs_particle_read_mismatches", "ggrs_particle_read_state",
     "ggrs_particle_read_saved", "ggrs_particle_debug_corrupt_on_load",
-    "ggrs_particle_timing_reset", "ggrs_particle_timing_read",
+    "ggrs_particle_timing_reset", "ggrs_particle_timing_stop", "ggrs_particle_timing_read",
     "ggrs_p2p_engine_create", "ggrs_p2p_engine_destroy", "ggrs_p2p_engine_config",
     "ggrs_p2p_add_inputs", "ggrs_p2p_advance_frames", "ggrs_p2p_current_frame", "ggrs_p2p_calls",
     "ggrs_p2p_synchronize", "ggrs_p2p_read_state", "ggrs_p2p_read_ring", "ggrs_p2p_read_stats",
-    "ggrs_p2p_read_trace", "ggrs_p2p_timing_reset", "ggrs_p2p_timing_read",
+    "ggrs_p2p_read_trace", "ggrs_p2p_timing_reset", "ggrs_p2p_timing_stop", "ggrs_p2p_timing_read",
     "ggrs_p2p_set_desync_detection", "ggrs_p2p_local_checksums", "ggrs_p2p_compare_checksums",
     "ggrs_p2p_debug_desync", "ggrs_p2p_set_sparse_saving", "ggrs_p2p_set_unstaged",
     "ggrs_codec_encode", "ggrs_codec_decode", "ggrs_codec_encode_chunked", "ggrs_codec_decode_chunked", "ggrs_codec_max_packet_bytes", "ggrs_codec_set_direct",
@@ -141,6 +141,7 @@ def lib():
         L.ggrs_debug_corrupt_on_load.argtypes = [vp, ctypes.c_int32, ctypes.c_int32]
         L.ggrs_last_launch_ms.argtypes = [vp, P(ctypes.c_float)]
         L.ggrs_timing_reset.argtypes = [vp]
+        L.ggrs_timing_stop.argtypes = [vp]
         L.ggrs_set_synctest_path.argtypes = [vp, ctypes.c_int32]
         L.ggrs_timing_read.argtypes = [vp, P(ctypes.c_float), P(ctypes.c_int32)]
         i32 = ctypes.c_int32

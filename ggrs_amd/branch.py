@@ -51,6 +51,7 @@ def _bind(L):
     L.ggrs_branch_read_trunk.argtypes = [vp, ctypes.c_int32, vp]
     L.ggrs_branch_read_lane.argtypes = [vp, ctypes.c_int64, ctypes.c_int32, P(ctypes.c_uint16), vp]
     L.ggrs_branch_timing_reset.argtypes = [vp]
+    L.ggrs_branch_timing_stop.argtypes = [vp]
     L.ggrs_branch_timing_read.argtypes = [vp, P(ctypes.c_float), P(ctypes.c_int32)]
     L.ggrs_branch_rounds.argtypes = [vp, ctypes.c_int32]
     L.ggrs_branch_set_round_launches.argtypes = [vp, ctypes.c_int32]
@@ -219,6 +220,10 @@ class BranchEngine:
 
     def timing_reset(self):
         _lib.check(self._L.ggrs_branch_timing_reset(self._h))
+
+    def timing_stop(self):
+        """Record the span's end behind the last launch without waiting (timing_read reports it)."""
+        _lib.check(self._L.ggrs_branch_timing_stop(self._h))
 
     def timing_read(self):
         ms, n = ctypes.c_float(), ctypes.c_int32()

@@ -1039,6 +1039,12 @@ int ggrs_branch_timing_reset(ggrs_branch_engine_t* e) {
   return e->timer.reset(e->stream);
 }
 
+int ggrs_branch_timing_stop(ggrs_branch_engine_t* e) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  return e->timer.stop(e->stream);
+}
+
 int ggrs_branch_timing_read(ggrs_branch_engine_t* e, float* total_ms, int32_t* launches) {
   if (!e || !total_ms || !launches) return set_error(GGRS_E_INVALID, "null argument");
   HIP_TRY(hipSetDevice(e->cfg.device));

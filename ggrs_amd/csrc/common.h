@@ -28,7 +28,7 @@ constexpr int kWave = 64;
 // (a pair per launch cost ~7.8 us of a 0.26 ms SyncTest launch).
 struct SpanTimer {
   hipEvent_t begin = nullptr, end = nullptr;
-  bool collecting = false, open = false;
+  bool collecting = false, open = false, stopped = false;
   int32_t launches = 0;
   int create() {
     HIP_TRY(hipEventCreate(&begin));
@@ -55,21 +55,31 @@ struct SpanTimer {
     HIP_TRY(hipStreamSynchronize(s));
     collecting = true;
     open = false;
+    stopped = false;
     launches = 0;
+    return GGRS_OK;
+  }
+  // the span's end event right behind the last launch, without waiting (read then reports it)
+  int stop(hipStream_t s) {
+    if (open && !stopped) {
+      HIP_TRY(hipEventRecord(end, s));
+      stopped = true;
+    }
+    collecting = false;
     return GGRS_OK;
   }
   // span milliseconds (launch gaps included) and fused launches; stops collecting
   int read(hipStream_t s, float* ms, int32_t* n) {
     *ms = 0.0f;
     if (open) {
-      HIP_TRY(hipEventRecord(end, s));
+      if (!stopped) HIP_TRY(hipEventRecord(end, s));
       HIP_TRY(hipEventSynchronize(end));
       HIP_TRY(hipEventElapsedTime(ms, begin, end));
     } else {
       HIP_TRY(hipStreamSynchronize(s));
     }
     *n = launches;
-    collecting = open = false;
+    collecting = open = stopped = false;
     launches = 0;
     return GGRS_OK;
   }

@@ -71,7 +71,7 @@ struct ggrs_engine {
   // timing: between ggrs_timing_reset and ggrs_timing_read one event pair brackets every fused
   // launch of the span (no per-launch events in the timed path)
   hipEvent_t ev_begin = nullptr, ev_end = nullptr;
-  bool collecting = false, span_open = false;
+  bool collecting = false, span_open = false, span_stopped = false;
   int32_t span_launches = 0;
   float last_span_ms = -1.0f;
   int32_t last_span_launches = 0;

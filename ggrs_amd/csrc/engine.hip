@@ -1618,7 +1618,20 @@ int ggrs_timing_reset(ggrs_engine_t* e) {
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->collecting = true;
   e->span_open = false;
+  e->span_stopped = false;
   e->span_launches = 0;
+  return GGRS_OK;
+}
+
+int ggrs_timing_stop(ggrs_engine_t* e) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  if (int rc = lane_server_stop(e)) return rc;
+  if (e->span_open && !e->span_stopped) {
+    HIP_TRY(hipEventRecord(e->ev_end, e->stream));
+    e->span_stopped = true;
+  }
+  e->collecting = false;
   return GGRS_OK;
 }
 
@@ -1628,7 +1641,7 @@ int ggrs_timing_read(ggrs_engine_t* e, float* total_ms, int32_t* launches) {
   if (int rc = lane_server_stop(e)) return rc;
   float ms = 0.0f;
   if (e->span_open) {
-    HIP_TRY(hipEventRecord(e->ev_end, e->stream));
+    if (!e->span_stopped) HIP_TRY(hipEventRecord(e->ev_end, e->stream));
     HIP_TRY(hipEventSynchronize(e->ev_end));
     HIP_TRY(hipEventElapsedTime(&ms, e->ev_begin, e->ev_end));
   } else {
@@ -1640,6 +1653,7 @@ int ggrs_timing_read(ggrs_engine_t* e, float* total_ms, int32_t* launches) {
   e->last_span_launches = e->span_launches;
   e->collecting = false;
   e->span_open = false;
+  e->span_stopped = false;
   e->span_launches = 0;
   return GGRS_OK;
 }

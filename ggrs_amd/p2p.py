@@ -55,6 +55,7 @@ def _bind(L):
     L.ggrs_p2p_read_stats.argtypes = [vp, vp, vp]
     L.ggrs_p2p_read_trace.argtypes = [vp, i32, i32, vp]
     L.ggrs_p2p_timing_reset.argtypes = [vp]
+    L.ggrs_p2p_timing_stop.argtypes = [vp]
     L.ggrs_p2p_timing_read.argtypes = [vp, P(ctypes.c_float), P(i32)]
     L.ggrs_p2p_set_desync_detection.argtypes = [vp, i32]
     L.ggrs_p2p_local_checksums.argtypes = [vp, i32, vp, i32]
@@ -156,6 +157,10 @@ class P2PEngine:
 
     def timing_reset(self):
         _lib.check(self._L.ggrs_p2p_timing_reset(self._h))
+
+    def timing_stop(self):
+        """Record the span's end behind the last launch without waiting (timing_read reports it)."""
+        _lib.check(self._L.ggrs_p2p_timing_stop(self._h))
 
     def timing_read(self):
         ms, n = ctypes.c_float(), ctypes.c_int32()

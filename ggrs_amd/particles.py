@@ -40,6 +40,7 @@ def _bind(L):
     L.ggrs_particle_read_saved.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, P(ctypes.c_uint16), vp]
     L.ggrs_particle_debug_corrupt_on_load.argtypes = [vp, ctypes.c_int32, ctypes.c_int32]
     L.ggrs_particle_timing_reset.argtypes = [vp]
+    L.ggrs_particle_timing_stop.argtypes = [vp]
     L.ggrs_particle_timing_read.argtypes = [vp, P(ctypes.c_float), P(ctypes.c_int32)]
     for name in _lib.EXPORTS:
         if name.startswith("ggrs_particle_"):
@@ -117,6 +118,10 @@ class ParticleEngine:
 
     def timing_reset(self):
         _lib.check(self._L.ggrs_particle_timing_reset(self._h))
+
+    def timing_stop(self):
+        """Record the span's end behind the last launch without waiting (timing_read reports it)."""
+        _lib.check(self._L.ggrs_particle_timing_stop(self._h))
 
     def timing_read(self):
         ms, n = ctypes.c_float(), ctypes.c_int32()

@@ -218,6 +218,10 @@ class Engine:
     def timing_reset(self):
         _lib.check(self._L.ggrs_timing_reset(self._h))
 
+    def timing_stop(self):
+        """Record the span's end behind the last launch without waiting (timing_read reports it)."""
+        _lib.check(self._L.ggrs_timing_stop(self._h))
+
     def timing_read(self):
         """(summed device ms of the fused launches since timing_reset, launch count)."""
         ms, n = ctypes.c_float(), ctypes.c_int32()

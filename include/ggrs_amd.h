@@ -270,6 +270,10 @@ int ggrs_last_launch_ms(ggrs_engine_t* eng, float* ms);
  * whole span (no per-launch events); _read synchronises, returns the span's milliseconds (launch
  * gaps included) and the number of fused launches in it, and stops collecting. */
 int ggrs_timing_reset(ggrs_engine_t* eng);
+/* Close the span without waiting: records its end event right behind the last launch (a caller
+ * that then synchronises the stream itself reads the same span without an extra host round trip
+ * inside its own wall clock).  _read after _stop reports that span. */
+int ggrs_timing_stop(ggrs_engine_t* eng);
 int ggrs_timing_read(ggrs_engine_t* eng, float* total_ms, int32_t* launches);
 
 /* ---------------------------------------------------------------------------------------------
@@ -323,6 +327,7 @@ int ggrs_branch_read_trunk(ggrs_branch_engine_t* eng, int32_t session, uint8_t* 
 int ggrs_branch_read_lane(ggrs_branch_engine_t* eng, int64_t lane, int32_t frame, uint16_t* checksum,
                           uint8_t* out);
 int ggrs_branch_timing_reset(ggrs_branch_engine_t* eng);
+int ggrs_branch_timing_stop(ggrs_branch_engine_t* eng); /* as ggrs_timing_stop */
 int ggrs_branch_timing_read(ggrs_branch_engine_t* eng, float* total_ms, int32_t* launches);
 /* n_rounds x (ggrs_branch_speculate, ggrs_branch_confirm without a report copy) issued back to
  * back from native code; while timing is collected one event pair brackets the whole batch */
@@ -398,6 +403,7 @@ int ggrs_particle_read_saved(ggrs_particle_engine_t* eng, int32_t session, int32
                              uint8_t* out);
 int ggrs_particle_debug_corrupt_on_load(ggrs_particle_engine_t* eng, int32_t session, int32_t frame);
 int ggrs_particle_timing_reset(ggrs_particle_engine_t* eng);
+int ggrs_particle_timing_stop(ggrs_particle_engine_t* eng); /* as ggrs_timing_stop */
 int ggrs_particle_timing_read(ggrs_particle_engine_t* eng, float* total_ms, int32_t* launches);
 
 /* ---------------------------------------------------------------------------------------------
@@ -452,6 +458,7 @@ int ggrs_p2p_read_stats(ggrs_p2p_engine_t* eng, int32_t* rollbacks, int64_t* res
  * first_frame .. first_frame+n-1 (ex_game.rs:121-126) */
 int ggrs_p2p_read_trace(ggrs_p2p_engine_t* eng, int32_t first_frame, int32_t n, uint16_t* out);
 int ggrs_p2p_timing_reset(ggrs_p2p_engine_t* eng);
+int ggrs_p2p_timing_stop(ggrs_p2p_engine_t* eng); /* as ggrs_timing_stop */
 int ggrs_p2p_timing_read(ggrs_p2p_engine_t* eng, float* total_ms, int32_t* launches);
 
 /* ---- P2P desync detection (SessionBuilder::with_desync_detection_mode, builder.rs:197-203;

@@ -192,6 +192,7 @@ extern "C" {
     pub fn ggrs_debug_corrupt_on_load(eng: *mut ggrs_engine_t, lane: i32, frame: i32) -> i32;
     pub fn ggrs_last_launch_ms(eng: *mut ggrs_engine_t, ms: *mut f32) -> i32;
     pub fn ggrs_timing_reset(eng: *mut ggrs_engine_t) -> i32;
+    pub fn ggrs_timing_stop(eng: *mut ggrs_engine_t) -> i32;
     pub fn ggrs_timing_read(eng: *mut ggrs_engine_t, total_ms: *mut f32, launches: *mut i32) -> i32;
 
     // ---- speculative branch rollback (configs 3/4)
@@ -211,6 +212,7 @@ extern "C" {
     pub fn ggrs_branch_read_lane(eng: *mut ggrs_branch_engine_t, lane: i64, frame: i32, checksum: *mut u16,
                                  out: *mut u8) -> i32;
     pub fn ggrs_branch_timing_reset(eng: *mut ggrs_branch_engine_t) -> i32;
+    pub fn ggrs_branch_timing_stop(eng: *mut ggrs_branch_engine_t) -> i32;
     pub fn ggrs_branch_timing_read(eng: *mut ggrs_branch_engine_t, total_ms: *mut f32, launches: *mut i32) -> i32;
     pub fn ggrs_branch_rounds(eng: *mut ggrs_branch_engine_t, n_rounds: i32) -> i32;
     pub fn ggrs_branch_set_round_launches(eng: *mut ggrs_branch_engine_t, on: i32) -> i32;
@@ -240,6 +242,7 @@ extern "C" {
                                     out: *mut u8) -> i32;
     pub fn ggrs_particle_debug_corrupt_on_load(eng: *mut ggrs_particle_engine_t, session: i32, frame: i32) -> i32;
     pub fn ggrs_particle_timing_reset(eng: *mut ggrs_particle_engine_t) -> i32;
+    pub fn ggrs_particle_timing_stop(eng: *mut ggrs_particle_engine_t) -> i32;
     pub fn ggrs_particle_timing_read(eng: *mut ggrs_particle_engine_t, total_ms: *mut f32, launches: *mut i32) -> i32;
 
     // ---- P2P sessions on the device
@@ -257,6 +260,7 @@ extern "C" {
     pub fn ggrs_p2p_read_stats(eng: *mut ggrs_p2p_engine_t, rollbacks: *mut i32, resim_frames: *mut i64) -> i32;
     pub fn ggrs_p2p_read_trace(eng: *mut ggrs_p2p_engine_t, first_frame: i32, n: i32, out: *mut u16) -> i32;
     pub fn ggrs_p2p_timing_reset(eng: *mut ggrs_p2p_engine_t) -> i32;
+    pub fn ggrs_p2p_timing_stop(eng: *mut ggrs_p2p_engine_t) -> i32;
     pub fn ggrs_p2p_timing_read(eng: *mut ggrs_p2p_engine_t, total_ms: *mut f32, launches: *mut i32) -> i32;
     pub fn ggrs_p2p_set_desync_detection(eng: *mut ggrs_p2p_engine_t, interval: i32) -> i32;
     pub fn ggrs_p2p_local_checksums(eng: *mut ggrs_p2p_engine_t, frame: i32, out: *mut u16, out_on_device: i32) -> i32;
