@@ -53,6 +53,41 @@ __global__ __launch_bounds__(64) void cvt_1(double* out, int seed) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = a;
 }
 
+KERNEL(dpp_1, 1, "v_mov_b32_dpp %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf", unsigned, "v")
+
+// v_add_f32 -> v_cmp (VCC) -> s_cbranch_vccnz (never taken): the VALU -> branch round trip
+__global__ __launch_bounds__(64) void cmpbr_1(double* out, int seed) {
+  float a = (float)threadIdx.x + 1.0f, b = (float)seed;
+  for (int i = 0; i < ITER; i++) {
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      asm volatile("v_add_f32 %0, %0, %1\n\tv_cmp_lt_f32 vcc, 1e30, %0\n\ts_cbranch_vccnz 0f\n0:" : "+v"(a) : "v"(b) : "vcc");
+    }
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a;
+}
+
+// f32 -> f64 -> *c -> i32 -> f64 -> fma: the reduction head of glibc_sincosf_domain, dependent
+__global__ __launch_bounds__(64) void red_1(double* out, int seed) {
+  float a = (float)threadIdx.x + 1.0f;
+  double d, e;
+  int n;
+  for (int i = 0; i < ITER; i++) {
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      asm volatile("v_cvt_f64_f32 %0, %1" : "=v"(d) : "v"(a));
+      asm volatile("v_mul_f64 %0, %1, %1" : "=v"(e) : "v"(d));
+      asm volatile("v_cvt_i32_f64 %0, %1" : "=v"(n) : "v"(e));
+      asm volatile("v_cvt_f64_i32 %0, %1" : "=v"(e) : "v"(n));
+      asm volatile("v_fma_f64 %0, %1, %1, %0" : "+v"(d) : "v"(e));
+      asm volatile("v_mul_f64 %0, %0, %0" : "+v"(d));
+      asm volatile("v_fma_f64 %0, %0, %0, %0" : "+v"(d));
+      asm volatile("v_cvt_f32_f64 %0, %1" : "=v"(a) : "v"(d));
+    }
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a;
+}
+
 typedef void (*Kf)(double*, int);
 struct Case { const char* name; Kf k; };
 
@@ -62,7 +97,9 @@ int main() {
                   {"v_fma_f64 8 chains", f64_8}, {"v_mul_f64 1 chain", mul64_1}, {"v_fma_f32 1 chain", f32_1},
                   {"v_fma_f32 2 chains", f32_2}, {"v_add_f32 1 chain", add32_1}, {"v_add_f32 2 chains", add32_2},
                   {"v_dot4 1 chain", dot4_1}, {"v_add_u32 1 chain", u32_1}, {"v_pk_add_f32 1 chain", pk_1},
-                  {"cvt f32<->f64 1 chain", cvt_1}};
+                  {"cvt f32<->f64 1 chain", cvt_1}, {"dpp row_shr 1 chain", dpp_1},
+                  {"add+cmp+cbranch 1 chain (per 3)", cmpbr_1},
+                  {"sincos head 1 chain (per 8)", red_1}};
   double* out;
   hipMalloc(&out, sizeof(double) * 64 * 8192);
   hipEvent_t e0, e1;
