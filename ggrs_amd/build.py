@@ -24,18 +24,26 @@ HEADERS = [os.path.join(CSRC, h) for h in ("box_game.h", "glibc_sincosf.h", "com
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC", "-std=c++17",
          "-Wall", "-Wno-unused-function"]
+# The step kernels run one wave per SIMD, so a VALU instruction that waits on the previous one's
+# result stalls the SIMD; LLVM's max-ilp machine scheduler interleaves the step's independent
+# chains (the next sin/cos, the Fletcher sums, the stores) instead of the default
+# occupancy-oriented order.  Measured on MI355X (profiles/r03b): the v5 SyncTest launch 0.1951 ->
+# 0.1794 ms, the P2P flat kernel 0.1295 -> 0.1209 ms, config 3 2.4 -> 2.3 us per round, config 4
+# unchanged; the lane-server unit (requests.hip) was slower with it and keeps the default.
+ILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
+UNIT_FLAGS = {"engine.hip": ILP, "p2p.hip": ILP, "branch.hip": ILP}
 
 
 def needs_build():
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(f) > t for f in SOURCES + HEADERS)
+    return any(os.path.getmtime(f) > t for f in SOURCES + HEADERS + [os.path.abspath(__file__)])
 
 
 def _compile(src, extra, verbose, obj_dir=OBJ):
     obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
-    cmd = [HIPCC, *FLAGS, *extra, "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-c", "-o", obj, src]
+    cmd = [HIPCC, *FLAGS, *UNIT_FLAGS.get(os.path.basename(src), []), *extra, "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-c", "-o", obj, src]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

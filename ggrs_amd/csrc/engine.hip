@@ -260,6 +260,13 @@ constexpr int kMaxRampFrames = 64;  // first-seen checksums of frames f0-cd .. f
 // input records, bytes up to `row` are zero.  Every load of a thread is issued before its LDS
 // stores, so a stage costs one memory latency (a load-wait-store loop paid one per byte).
 // Full 8-byte rows whose source is 8-byte aligned move as one 64-bit load per row.
+// s_waitcnt vmcnt(0) (gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15) at the end of a stage.  A
+// thread's loads whose LDS store is skipped (row past the stage) stay counted at the stage's exit,
+// so the compiler's wait pass put a vmcnt(0) into the step loop's first block, where the first
+// write of those registers is -- there it waited, every 8 steps, for all the ring stores in flight
+// (the v5 kernel's SQ_WAIT_ANY).  Draining here, once per stage, clears that state.
+__device__ inline void drain_loads() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 template <int kRow>
 __device__ inline void stage_input_rows(uint8_t* lds, const uint8_t* inputs, int64_t L, int Pp, int32_t cap,
                                         int32_t gf, int nf, int64_t s0, int used, int row_rt, int tid) {
@@ -283,6 +290,7 @@ __device__ inline void stage_input_rows(uint8_t* lds, const uint8_t* inputs, int
         if (ff < nf) *reinterpret_cast<uint64_t*>(lds + ff * 8) = v[u];
       }
     }
+    drain_loads();
     return;
   }
   const int total = nf * row;
@@ -302,6 +310,7 @@ __device__ inline void stage_input_rows(uint8_t* lds, const uint8_t* inputs, int
       if (q < total) lds[q] = v[u];
     }
   }
+  drain_loads();
 }
 
 // ------------------------------------------------------------------------------------------
@@ -747,6 +756,9 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
           const uint32_t nb = Pp == 2 ? (uint32_t)__builtin_amdgcn_update_dpp((int)rb, (int)rb, 0x112, 0xF, 0xF, false)
                                       : (uint32_t)__builtin_amdgcn_ds_bpermute(src_rot, (int)rb);
           glibc_sincosf_domain(__builtin_bit_cast(float, nb), &sc_s, &sc_c);
+#ifdef GGRS_EXP_PIN
+          asm volatile("" ::"v"(sc_s), "v"(sc_c));
+#endif
         });
       } else {
         advance_player(x, y, vx, vy, rot, (uint32_t)in);

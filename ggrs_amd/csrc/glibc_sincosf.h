@@ -195,9 +195,21 @@ __host__ __device__ inline void glibc_sincosf_small(float y, float* sinp, float*
 // n = 0 and x - 0*hpi = x exactly, and the |y| < 2^-12 shortcut (sin = y, cos = 1) is what the
 // polynomials round to there.  Verified against libm on every f32 of the domain
 // (tests/native/sincosf_kat_host.cpp, bad_domain).
+//
+// The reduction without integer conversions: reduce_fast's n = ((int32_t)(x * hpi_inv) +
+// 2^23) >> 24 is floor(x * hpi_inv * 2^-24 + 1/2) for x >= 0 (floor((floor(r) + k) / m) =
+// floor((r + k) / m) for integers k, m), and on this domain it equals round-to-nearest of the
+// exact product x * (hpi_inv * 2^-24): fma(x, hpi_inv * 2^-24, 1.5 * 2^52) leaves n in the low
+// mantissa bits (n <= 4, so the low dword IS n) and subtracting 1.5 * 2^52 gives (double)n
+// exactly.  Checked on every f32 of the domain (n and the reduced x both identical: the host KAT
+// below compares the whole function with libm).  On gfx950 this replaces v_mul_f64 +
+// v_cvt_i32_f64 + v_add_u32 + v_ashrrev + v_cvt_f64_i32 (the two conversions cost ~40 cycles of
+// dependent latency each, tools/microbench/vdep.hip) with v_fma_f64 + v_add_f64.
 __host__ __device__ inline void glibc_sincosf_domain(float y, float* sinp, float* cosp) {
-  int n;
-  const double x = reduce_fast((double)y, &n);
+  const double xin = (double)y;
+  const double t = __builtin_fma(xin, GGRS_SC_HPI_INV * 0x1p-24, 0x1.8p52);
+  const uint32_t n = (uint32_t)__builtin_bit_cast(uint64_t, t);
+  const double x = __builtin_fma(-(t - 0x1.8p52), GGRS_SC_HPI, xin);
   const double x2 = x * x;
   const float S = (float)sin_poly(x, x2);
   const float C = (float)cos_poly(x2);

@@ -427,6 +427,7 @@ class SyncTestSession:
         self._pending = {}
         self._added = 0
         self._reported = np.zeros(engine.num_lanes, bool)
+        self._unchecked = False  # frames advanced since the device's mismatch state was last read
 
     def num_players(self):
         return self.engine.num_players
@@ -452,8 +453,10 @@ class SyncTestSession:
     def advance_frame(self):
         """:85-150 + the handler's execution of the returned requests, on every lane.  Error order
         as the reference: a lane's MismatchedChecksum (:89-102) before the missing-input
-        InvalidRequest (:108-113)."""
-        self.raise_on_mismatch()
+        InvalidRequest (:108-113).  The device's mismatch state is re-read only when frames were
+        advanced without a check since the last one (advance_frames(check=True) already read it)."""
+        if self._unchecked:
+            self.raise_on_mismatch()
         if len(self._pending) != self.engine.num_players:
             raise InvalidRequest(-1, "Missing local input while calling advance_frame().")
         frame = np.stack([self._pending[p] for p in range(self.engine.num_players)], axis=1)[None]
@@ -471,11 +474,13 @@ class SyncTestSession:
         """n fused advance_frame calls.  With check=True, raise MismatchedChecksum if a lane
         halted (each lane reported once)."""
         self.engine.synctest_advance_frames(n)
+        self._unchecked = True
         if check:
             self.raise_on_mismatch()
 
     def raise_on_mismatch(self):
         st, mf, mm = self.engine.mismatches()
+        self._unchecked = False
         bad = (st == LANE_MISMATCH) & ~self._reported
         if bad.any():
             self._reported |= bad
