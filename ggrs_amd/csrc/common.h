@@ -85,6 +85,18 @@ struct SpanTimer {
   }
 };
 
+// XCD-aware block order.  The dispatcher deals workgroup i to XCD i % 8 (MI355X: 8 XCDs, each
+// with its own L2), so neighbouring blocks -- whose sessions share 64-byte lines of every SoA
+// row (ring fields, checksums, input rows) -- would sit on different XCDs: each XCD fetches the
+// shared line, and partial-line writes from several L2s reach HBM separately.  xcd_block maps
+// workgroup i to the logical block that gives XCD x a contiguous range of logical blocks
+// (q = n / 8 each, the first n % 8 XCDs one more): a bijection of [0, n).
+constexpr int kXcds = 8;
+__device__ inline int64_t xcd_block(int64_t i, int64_t n) {
+  const int64_t q = n / kXcds, r = n % kXcds, x = i % kXcds, k = i / kXcds;
+  return x * q + (x < r ? x : r) + k;
+}
+
 inline int padded_players(int p) { return p <= 1 ? 1 : (p == 2 ? 2 : 4); }
 inline int64_t grid_of(int64_t n, int64_t block) { return (n + block - 1) / block; }
 

@@ -614,25 +614,80 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
   constexpr int kB = 8;             // steps per batch (= role lanes that run it)
   constexpr int kEntry = 32;        // stash bytes per (session, player): 5 fields, 16-B aligned
   constexpr int kSlot = 8 * kEntry; // one step's stash (ROW entries)
-  // inputs staged kStage5 frames at a time (+1 slack row for the batch's look-ahead): the raw
-  // bytes (non-core steps) and their decoded InputRec (core steps), one per (frame, session, player)
+  // inputs: the raw bytes of up to kRaw frames (the whole launch at n <= kRaw - CD, read in the
+  // prologue beside every other global read: one memory latency per launch), and their decoded
+  // InputRec for kStage5 frames at a time (+1 slack row for the batch's look-ahead), decoded from
+  // LDS every kStage5 steps; the non-core steps read the raw bytes
   constexpr int kStage5 = 128;
-  __shared__ uint8_t lds_in[(kStage5 + 1) * ROW];
+  constexpr int kRaw = 528;
+  __shared__ __attribute__((aligned(16))) uint8_t lds_raw[kRaw * ROW];
   __shared__ uint4 lds_rec[(kStage5 + 1) * ROW];
   __shared__ uint16_t lds_first[CD * SPW];
-  __shared__ uint32_t lds_cell[kWave * 5];
   __shared__ __attribute__((aligned(16))) uint8_t lds_stash[2 * kB * kSlot];  // slots, then the dump
-  const int32_t failed_f0 = *p.fail_f0;
-  if (failed_f0 >= 0 && failed_f0 != p.f0) return;
+#ifdef GGRS_EXP_STAMPS  // timing experiment only: phase stamps printed by two blocks
+  uint64_t ts[8];
+  int nts = 0;
+  ts[nts++] = __builtin_amdgcn_s_memtime();
+#define GGRS_STAMP() (ts[nts++] = __builtin_amdgcn_s_memtime())
+#else
+#define GGRS_STAMP() ((void)0)
+#endif
   const int wl = threadIdx.x;
   const int R = p.R;
   const int g = wl / G, r = wl - g * G;
   const int j = r / Pp, pl = r - j * Pp;  // static role, player
   const int64_t L = p.L;
-  const int64_t s0 = (int64_t)blockIdx.x * SPW;
+  const int64_t blk = xcd_block(blockIdx.x, gridDim.x);
+  const int64_t s0 = blk * SPW;
   const int64_t s = s0 + g;
   const int nsess = (int)((L - s0) < SPW ? (L - s0) : SPW);
-  const bool valid = s < L && p.lane_status[s] == GGRS_LANE_RUNNING;
+  const int32_t g0 = p.f0 - CD;
+  const int32_t t_stage_end = p.f0 + p.n + CD;  // inputs are staged up to v4's last step
+  const int raw_rows = kRaw < p.cap ? kRaw : p.cap;  // a chunk of queue rows is held at once
+  // The prologue's global reads, issued together (one memory latency instead of one per phase):
+  // the launch checkpoint's rows, the first-seen checksums of frames g0 .. g0 + cd - 1, the cell
+  // of frame g0, and the raw input rows; then the early-outs, the checkpoint's stores and the LDS.
+  // Fast form for full blocks of 8-byte-aligned input rows; otherwise the generic copies.
+  constexpr int kCkRegs = 16;  // checkpoint words per thread in the fast form
+  constexpr int kRawRegs = (kRaw + kWave - 1) / kWave;
+  const int ck_words32 = (1 + R) * F * SPW, ck_words16 = R * SPW;  // 16-bit rows as word pairs
+  const bool fast = nsess == SPW && ((L * Pp) & 7) == 0 && (L & 1) == 0 && ck_words32 + ck_words16 <= kCkRegs * kWave;
+  const int32_t failed_f0 = *p.fail_f0;
+  const int32_t lstat = p.lane_status[s < L ? s : L - 1];
+  uint32_t ckv[kCkRegs];
+  uint2 rawv[kRawRegs];
+  uint16_t firstv = 0;
+  const int nraw = (t_stage_end - p.f0) < raw_rows ? (t_stage_end - p.f0) : raw_rows;
+  const int32_t slot_g0 = g0 % R;
+  const int32_t q0 = g0 % p.cap;
+  if (fast) {
+#pragma unroll
+    for (int i = 0; i < kCkRegs; i++) {
+      const int q = wl + i * kWave;
+      if (q < ck_words32) {
+        const int row = q / SPW, ss = q % SPW;  // SPW is a power of two: shifts
+        ckv[i] = row < F ? p.cur[(int64_t)row * L + s0 + ss] : p.ring[(int64_t)(row - F) * L + s0 + ss];
+      } else if (q < ck_words32 + ck_words16) {
+        const int e16 = 2 * (q - ck_words32), row = e16 / SPW, ss = e16 % SPW;
+        const uint16_t* src = row < R ? p.ring_ck + (int64_t)row * L : p.first_ck + (int64_t)(row - R) * L;
+        ckv[i] = *reinterpret_cast<const uint32_t*>(src + s0 + ss);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kRawRegs; i++) {
+      const int ff = wl + i * kWave;
+      if (ff < nraw) {
+        const int32_t slot = q0 + ff >= p.cap ? q0 + ff - p.cap : q0 + ff;
+        rawv[i] = *reinterpret_cast<const uint2*>(p.inputs + ((int64_t)slot * L + s0) * Pp);
+      }
+    }
+  }
+  if (wl < CD * nsess) {
+    const int gg = wl / nsess, ss = wl - gg * nsess;
+    const int32_t sl = slot_g0 + gg >= R ? slot_g0 + gg - R : slot_g0 + gg;
+    firstv = p.first_ck[(int64_t)sl * L + s0 + ss];
+  }
+  const bool valid = s < L && lstat == GGRS_LANE_RUNNING;
   const bool owner = valid && pl < P;
   const int64_t sl = valid ? s : 0;
   const int plc = pl < P ? pl : 0;
@@ -677,30 +732,57 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
   const int32_t tcap = p.trace_cap > 0 ? p.trace_cap : 1;
   const int32_t jm = j % tcap;
 
-  {
-    const CheckpointMap m{L, R, F, SPW, p.cur, p.ring, p.ring_ck, p.first_ck};
-    checkpoint_sessions(m, p.shadow + (int64_t)blockIdx.x * p.block_bytes, s0, nsess, wl, kWave);
-  }
-  if (failed_f0 >= 0) return;
-  const int32_t g0 = p.f0 - CD;
-  for (int q = wl; q < CD * nsess; q += kWave) {
-    const int gg = q / nsess, ss = q - gg * nsess;
-    lds_first[gg * SPW + ss] = p.first_ck[(int64_t)((g0 + gg) % R) * L + s0 + ss];
-  }
-  {
-    const uint32_t* cell = p.ring + (int64_t)(g0 % R) * F * L + sl;
-#pragma unroll
-    for (int q = 0; q < 5; q++) lds_cell[wl * 5 + q] = cell[kq[q] * L];
-  }
-  __syncthreads();
+  // the cell of frame g0 (every role's Load): read straight into the lane's registers
   uint32_t w[5];
+  {
+    const uint32_t* cell = p.ring + (int64_t)slot_g0 * F * L + sl;
 #pragma unroll
-  for (int q = 0; q < 5; q++) w[q] = lds_cell[wl * 5 + q];
+    for (int q = 0; q < 5; q++) w[q] = cell[kq[q] * L];
+  }
+  if (failed_f0 >= 0 && failed_f0 != p.f0) return;
+  {
+    uint8_t* piece = p.shadow + blk * p.block_bytes;
+    if (fast) {
+#pragma unroll
+      for (int i = 0; i < kCkRegs; i++) {
+        const int q = wl + i * kWave;
+        if (q < ck_words32 + ck_words16) reinterpret_cast<uint32_t*>(piece)[q] = ckv[i];
+      }
+    } else {
+      const CheckpointMap m{L, R, F, SPW, p.cur, p.ring, p.ring_ck, p.first_ck};
+      checkpoint_sessions(m, piece, s0, nsess, wl, kWave);
+    }
+  }
+  GGRS_STAMP();
+  if (failed_f0 >= 0) return;
+  if (wl < CD * nsess) {
+    const int gg = wl / nsess, ss = wl - gg * nsess;
+    lds_first[gg * SPW + ss] = firstv;
+  }
+  int32_t raw0 = p.f0;  // step whose frame (raw0 - cd) is lds_raw's row 0
+  if (fast) {
+#pragma unroll
+    for (int i = 0; i < kRawRegs; i++) {
+      const int ff = wl + i * kWave;
+      if (ff < nraw) reinterpret_cast<uint2*>(lds_raw)[ff] = rawv[i];
+    }
+  } else {
+    stage_input_rows<ROW>(lds_raw, p.inputs, L, Pp, p.cap, g0, nraw, s0, nsess * Pp, ROW, wl);
+  }
+  // the block is one wave: LDS written by one lane and read by another needs only the wave's own
+  // in-order LDS queue and a compiler fence (a __syncthreads would also wait for the checkpoint's
+  // stores; inside the step loop, for every ring store in flight)
+  auto wave_lds_sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  wave_lds_sync();
+  GGRS_STAMP();
 
   uint64_t bad = 0;
   uint32_t pend_ck = 0, pend_first = 0;
   uint64_t pend_lanes = 0;
-  const int32_t t_stage_end = p.f0 + p.n + CD;  // inputs are staged up to v4's last step
   const int32_t t_end = t_stage_end - 1;        // the last step role cd-1 works in
   const int in_lane = g * Pp + pl;
   int32_t sr = __builtin_amdgcn_readfirstlane((g0 + 1) % R);
@@ -712,20 +794,26 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
   const int32_t ramp_end = min(p.f0 + CD, t_end);
   const bool lean_ok = __all(w[4] <= kTwoPiBits);
   const int32_t core_end = (corrupt_here || !lean_ok) ? ramp_end : max(ramp_end, p.f0 + p.n);
-  int32_t chunk0 = p.f0;  // step of the staged chunk's row 0
+  int32_t chunk0 = p.f0;  // step of lds_rec's row 0
 
+  // decode the records of steps t .. t + kStage5 (from lds_raw; a launch longer than the raw chunk
+  // re-reads its raw rows first, the only global read inside the step loop)
   auto stage = [&](int32_t t) {
-    __syncthreads();
-    const int32_t gf = t - CD;
     const int nf = (t_stage_end - t) < kStage5 + 1 ? (t_stage_end - t) : kStage5 + 1;
-    stage_input_rows<ROW>(lds_in, p.inputs, L, Pp, p.cap, gf, nf, s0, nsess * Pp, ROW, wl);
-    chunk0 = t;
-    __syncthreads();
+    if (t - raw0 + nf > raw_rows) {
+      wave_lds_sync();
+      const int nr = (t_stage_end - t) < raw_rows ? (t_stage_end - t) : raw_rows;
+      stage_input_rows<ROW>(lds_raw, p.inputs, L, Pp, p.cap, t - CD, nr, s0, nsess * Pp, ROW, wl);
+      raw0 = t;
+    }
+    wave_lds_sync();
+    const uint8_t* src = lds_raw + (t - raw0) * ROW;
     for (int q = wl; q < nf * ROW; q += kWave) {
-      const InputRec r = make_input_rec(lds_in[q]);
+      const InputRec r = make_input_rec(src[q]);
       lds_rec[q] = make_uint4(r.delta, r.thr, r.sgn, r.keep);
     }
-    __syncthreads();
+    chunk0 = t;
+    wave_lds_sync();
   };
 
   uint32_t acc = 0;
@@ -849,6 +937,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
       v[4] = *reinterpret_cast<const uint32_t*>(st + 16);
     }
     const uint32_t ri = (uint32_t)(tb + (j & (kB - 1)) + 1 - chunk0) * ROW + in_at;
+    const uint32_t rr = (uint32_t)(tb + (j & (kB - 1)) + 1 - raw0) * ROW + in_at;
     {
       float x = __builtin_bit_cast(float, v[0]), y = __builtin_bit_cast(float, v[1]);
       float vx = __builtin_bit_cast(float, v[2]), vy = __builtin_bit_cast(float, v[3]);
@@ -858,7 +947,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
         glibc_sincosf_domain(rot, &bs, &bc);
         advance_player_rec(x, y, vx, vy, rot, rec_of(lds_rec[ri]), bs, bc);
       } else {
-        advance_player(x, y, vx, vy, rot, lds_in[ri]);
+        advance_player(x, y, vx, vy, rot, lds_raw[rr]);
       }
       v[0] = __builtin_bit_cast(uint32_t, x);
       v[1] = __builtin_bit_cast(uint32_t, y);
@@ -898,7 +987,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
     sb = sb >= tcap ? sb - tcap : sb;
   };
 
-  auto input_at = [&](int32_t t) -> uint32_t { return lds_in[(uint32_t)(t - chunk0) * ROW + in_at]; };
+  auto input_at = [&](int32_t t) -> uint32_t { return lds_raw[(uint32_t)(t - raw0) * ROW + in_at]; };
   auto general = [&](int32_t t) {
     const int32_t rel = t - p.f0;
     if ((rel & (kStage5 - 1)) == 0) stage(t);
@@ -909,6 +998,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
   for (; t < ramp_end; ++t) general(t);
   // core blocks of 8 steps + their batch, aligned to the batch grid
   for (; t < core_end && ((t - p.f0) & (kB - 1)) != 0; ++t) general(t);
+  GGRS_STAMP();
   if (t + kB <= core_end) {
     bad |= __ballot(pend_ck != pend_first) & pend_lanes;
     pend_ck = pend_first = 0;
@@ -926,6 +1016,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
     }
     bad |= __ballot(acc != 0) & cmp_lanes;
   }
+  GGRS_STAMP();
   for (; t < t_end; ++t) general(t);
   {
     const int rem = (t_end - p.f0) & (kB - 1);
@@ -933,6 +1024,14 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
   }
   bad |= __ballot(pend_ck != pend_first) & pend_lanes;
   if (bad && wl == __builtin_ctzll(bad)) atomicCAS(p.fail_f0, -1, p.f0);
+#ifdef GGRS_EXP_STAMPS
+  GGRS_STAMP();
+  if (wl == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1))
+    printf("STAMPS block %d ckpt %llu loads %llu ramp %llu core %llu tail %llu\n", (int)blockIdx.x,
+           (unsigned long long)(ts[1] - ts[0]), (unsigned long long)(ts[2] - ts[1]), (unsigned long long)(ts[3] - ts[2]),
+           (unsigned long long)(ts[4] - ts[3]), (unsigned long long)(ts[5] - ts[4]));
+#endif
+#undef GGRS_STAMP
 }
 
 struct RequestParams {

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 3: config-2 kernel check: SyncTest GPU tests, then the default bench three times.
 set -u
-TAG=$1
+TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R && mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests/test_gpu_sincosf.py tests/test_gpu_synctest.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_$TAG.log; exit 10; }
