@@ -353,7 +353,8 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
   const int j = r / Pp, pl = r - j * Pp;  // static role, player
   const int64_t L = p.L;
   const int spw = p.spw;
-  const int64_t s0 = (int64_t)blockIdx.x * spw;
+  const int64_t blk = xcd_block(blockIdx.x, gridDim.x);
+  const int64_t s0 = blk * spw;
   const int64_t s = s0 + g;
   const int nsess = (int)((L - s0) < spw ? (L - s0) : spw);
   const bool valid = g < spw && s < L && p.lane_status[s] == GGRS_LANE_RUNNING;
@@ -399,7 +400,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
   // copies the whole shadow back), before any of this launch's stores
   {
     const CheckpointMap m{L, R, F, spw, p.cur, p.ring, p.ring_ck, p.first_ck};
-    checkpoint_sessions(m, p.shadow + (int64_t)blockIdx.x * p.block_bytes, s0, nsess, wl, kWave);
+    checkpoint_sessions(m, p.shadow + blk * p.block_bytes, s0, nsess, wl, kWave);
   }
   if (failed_f0 >= 0) return;  // this launch is replayed from its checkpoint anyway
   const int32_t g0 = p.f0 - cd;
