@@ -308,6 +308,59 @@ __device__ inline void advance_player_lean(float& x, float& y, float& vx, float&
   advance_player_lean_sc(x, y, vx, vy, rot, input, s, c);
 }
 
+// N independent player steps (advance_player_lean each, the same IEEE ops in the same order per
+// player) with ONE speed-clamp branch: every player's step up to the clamp test, then the rare
+// clamp block for the players that need it, then every position update.  One clamp branch per
+// player step would cut the N step chains into N basic blocks, which the scheduler cannot
+// interleave; with one, a wave alone on its SIMD issues the N chains side by side.
+// v[i] = {x, y, vx, vy, rot} bits of player step i, in[i] its input.
+template <int N>
+__device__ inline void advance_players_lean(uint32_t (&v)[N][5], const uint32_t (&in)[N],
+                                            const SincosConsts& K = sincos_consts_vgpr()) {
+  ggrs_f2 vel[N];
+  float mag2[N];
+  bool any = false;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    float rot = __builtin_bit_cast(float, v[i][4]);
+    float s, c;
+    glibc_sincosf_domain_k(rot, &s, &c, K);
+    ggrs_f2 ve = ggrs_f2{__builtin_bit_cast(float, v[i][2]), __builtin_bit_cast(float, v[i][3])} * kFriction;
+    const ggrs_f2 d = ggrs_f2{c, s} * kMovementSpeed;
+    const uint32_t ud = in[i] & (kInputUp | kInputDown), lr = in[i] & (kInputLeft | kInputRight);
+    const bool thrust = ud == kInputUp, brake = ud == kInputDown;
+    ve = ve + ggrs_f2{thrust ? d.x : (brake ? -d.x : -0.0f), thrust ? d.y : (brake ? -d.y : -0.0f)};
+    const bool ccw = lr == kInputLeft, turn = ccw || lr == kInputRight;
+    const float a = rot + (ccw ? -kRotationSpeed : kRotationSpeed);
+    const float r = a + (a < 0.0f ? kTwoPi : (a >= kTwoPi ? -kTwoPi : 0.0f));
+    v[i][4] = __builtin_bit_cast(uint32_t, turn ? r : rot);
+    const ggrs_f2 sq = ve * ve;
+    mag2[i] = sq.x + sq.y;
+    any = any || mag2[i] > kMaxSpeed * kMaxSpeed;
+    vel[i] = ve;
+  }
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(any) != 0, 0)) {
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      if (mag2[i] > kMaxSpeed * kMaxSpeed) {
+        const float magnitude = sqrt_rn_above_49(mag2[i]);
+        const double rr = rcp_f64_refined((double)magnitude);
+        vel[i].x = (float)((double)(vel[i].x * kMaxSpeed) * rr);
+        vel[i].y = (float)((double)(vel[i].y * kMaxSpeed) * rr);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    const ggrs_f2 pos = ggrs_f2{__builtin_bit_cast(float, v[i][0]), __builtin_bit_cast(float, v[i][1])} + vel[i];
+    v[i][0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_fmed3f(pos.x, 0.0f, kWindowWidth));
+    v[i][1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_fmed3f(pos.y, 0.0f, kWindowHeight));
+    const float vx = vel[i].x, vy = vel[i].y;
+    v[i][2] = __builtin_bit_cast(uint32_t, vx);
+    v[i][3] = __builtin_bit_cast(uint32_t, vy);
+  }
+}
+
 // Dispatch (every kernel): the lean branch-free form when every active lane's rot is in the
 // domain (always, for states this engine produced), else the general form for the whole wave.
 // advance_player_domain stays as the KAT reference of the lean form.

@@ -83,7 +83,7 @@ __device__ inline uint32_t branch_inputs(const SpecParams& p, int64_t s, int32_t
 }
 
 // The lane whose ring holds branch b's depth-0 cell (the state after the first speculated frame):
-// the representative b mod A of its one-digit prefix (prefix_rounds_kernel saves only those), the
+// the representative b mod A of its one-digit prefix (prefix_pipe_kernel saves only those), the
 // lane itself without enumeration.
 __device__ inline int64_t rep0_lane(const SpecParams& p, int64_t s, int32_t b) {
   return s * p.B + (p.E > 0 ? (int64_t)(b % p.A) : (int64_t)b);
@@ -305,365 +305,279 @@ __global__ __launch_bounds__(kRoundsBlock) void rounds_kernel(RoundsParams rp) {
   }
 }
 
-// Prefix-shared rounds (ggrs_branch_rounds when the enumerated player is the only remote one,
-// config 3).  Two facts about a round make most of the rounds kernel's work common to many lanes:
+// Prefix-shared rounds, pipelined (ggrs_branch_rounds when the enumerated player is the only
+// remote one: config 3).  Two facts about a round make most of its work common to many lanes:
 //   * players are independent in State::advance (ex_game.rs:276-331 updates player i from its own
 //     fields and input only) and every player except the enumerated one plays the session's
-//     confirmed local inputs, so the local players' states at frame f_c + k + 1 are the same in
-//     every branch of the session: the "common window" C_k;
+//     confirmed inputs, so the local players' part of every depth-k cell is the trunk's local
+//     players one frame later -- the same in every branch of the session;
 //   * branch b's enumerated player plays digits d_0 .. d_k up to frame f_c + k, so branches sharing
 //     their first k + 1 digits hold the same state after k + 1 frames: A^min(k+1, E) distinct cells
-//     per session at depth k (config 3: 16, 256, 4096, 65,536 of the 4 x 65,536 logical saves).
-// So each lane advances only its enumerated player (one player-step per frame instead of P), the
-// common window lives in LDS (per block and session: C_k for the frames f_c+1 .. f_c+W with the
-// doubled Fletcher sums of its fields, slot = frame % W) and slides by one frame per round (one
-// local-player step per round, the window lane), the trunk's enumerated player is replayed with the
-// confirmed input by a trunk lane (its local players are the window's first entry), and a cell at
-// depth k is saved only by the lanes whose branch number is below A^min(k+1, E) -- the prefix's
-// representative, branch b mod A^min(k+1, E) of the same session.  ggrs_branch_read_lane resolves a
-// lane's cell to its representative; every kernel's survivor check reads the representative
-// (depth 0: branch b mod A).  Rings (representatives), reports, trunks and desync records end
-// exactly as after the same rounds of speculate_kernel + confirm_kernel.
-// Block: kRoundsBlock branch lanes (four waves) + one extra wave for the per-session work (the
-// trunk's enumerated player replayed with the confirmed input; the window's new entry), so no
-// branch wave carries it: the branch waves meet the extra wave once per round, at a barrier before
-// the frame that needs the window's new entry.  The extra wave's input rows are loaded one round
-// ahead.  Saves are buffer stores at per-lane field offsets plus a wave-uniform slot offset.
-// Dynamic LDS per block (words): trunk enumerated player [2][ns][5], window [ns][W][5(P-1) + 2],
-// the first trunk's checksum [ns], the round's confirmed enumerated input [ns], and the input rows
-// of frames f_c .. f_c + n + W - 2 for the block's sessions [n + W - 1][ns] (staged in the prologue,
-// so the round loop issues no global load: a wave waiting on one would also wait for its saves,
-// which retire in order with loads on the vmcnt counter).
-constexpr int kPrefixBlock = kRoundsBlock + 64;
-constexpr int kPrefixItems = 1;  // (session, role) items per extra lane: 2 ns <= 64 * kPrefixItems
-constexpr uint32_t kPrefixOob = 0x40000000u;  // past every descriptor's range: a lane that never stores
-
-// A workgroup barrier ordering LDS only: __syncthreads() also waits for every global store the wave
-// has in flight (its fence covers global memory), which inside the round loop would stall each wave
-// on its saves; nothing in the loop reads another wave's global stores.
-__device__ inline void lds_barrier() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
+//     per session at depth k (config 3: 16, 256, 4096, 65,536 of the 4 x 65,536 logical saves),
+//     saved by the prefix's representative, branch b mod A^min(k+1, E) of the same session
+//     (ggrs_branch_read_lane resolves a lane's cell to it).
+// A round is W dependent steps (speculated frames); consecutive rounds are independent given their
+// trunks, and round r's trunk is the confirmed replay of round r - 1's -- inputs only.  So the
+// kernel runs the rounds as a pipeline: super-step u advances, on every lane, stage k of round
+// u - k for every k < W (W independent enumerated-player steps, the only state chains: stage k
+// takes stage k - 1's state of the previous super-step, stage 0 the trunk) and the trunk itself
+// one frame (all players, confirmed inputs: the local players of every cell saved in super-step
+// u, the next round's stage-0 state, the round's report).  Every stage of super-step u saves the
+// same frame f_c + u + 1 (round u - k's depth k), in sequential order (the deepest stage -- the
+// oldest round -- first, as the rounds would), so rings, ring checksums, trunks, reports, survivor
+// sets and desync records end exactly as after n rounds of speculate_kernel + confirm_kernel.
+// One wave per SIMD runs W + P independent player steps per super-step instead of W dependent
+// ones per round, and no lane waits for another wave: no LDS window, no barrier in the loop (the
+// trunk is replayed on every lane of the session -- the SIMD runs the whole wave's instruction
+// stream once whatever its lanes hold).  The launch's input rows are staged in LDS in the prologue
+// (a global load inside the loop would wait for the wave's saves: loads and stores retire in
+// order on the vmcnt counter).  WT > 0 fixes W at compile time (config 3: W = 4); WT = 0 serves
+// W <= kPipeMaxW with uniform per-stage guards.
+constexpr int kPipeMaxW = 8;
+constexpr uint32_t kPipeOob = 0x40000000u;  // past every descriptor's range: a lane that never stores
 
 __device__ inline __amdgpu_buffer_rsrc_t prefix_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 
-// WT > 0: the window length as a compile-time constant (config 3's W = 4): the round's steps are
-// unrolled, so one step's rotation / sin-cos work overlaps the previous step's velocity chain.
 template <int P, int EP, int WT>
-__global__ __launch_bounds__(kPrefixBlock) void prefix_rounds_kernel(RoundsParams rp) {
+__global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams rp) {
   static_assert(EP >= 0 && EP < P, "enumerated player");
   constexpr int F = state_fields(P);
   constexpr int n_bytes = Fletcher<P>::n;
-  constexpr int FL = 5 * (P - 1);  // local-player fields of a window entry
-  constexpr int WS = FL + 2;       // + doubled Fletcher sums of the entry's common part
   constexpr int e = EP;
-  extern __shared__ uint32_t lds_dyn[];
+  constexpr int KW = WT > 0 ? WT : kPipeMaxW;
+  extern __shared__ uint32_t lds_rows[];  // [n + W - 1][ns]: confirmed inputs of f_c .. f_c + n + W - 2
   const SpecParams& p = rp.sp;
   const int W = WT > 0 ? WT : p.W;
-  constexpr int kUnroll = WT > 0 ? WT : 1;
-  const bool branch_wave = threadIdx.x < kRoundsBlock;  // wave-uniform
+  const int n = rp.n;
   const int64_t lane0 = (int64_t)blockIdx.x * kRoundsBlock;
-  const int64_t lane = lane0 + (branch_wave ? threadIdx.x : 0);
-  const bool in_range = branch_wave && lane < p.L;
+  const int64_t lane = lane0 + threadIdx.x;
+  const bool in_range = lane < p.L;
   const int64_t s_first = lane0 / p.B;
   const int64_t s_last = (min(p.L, lane0 + kRoundsBlock) - 1) / p.B;
   const int ns = (int)(s_last - s_first + 1);
   const int64_t s = in_range ? lane / p.B : s_first;
   const int32_t b = in_range ? (int32_t)(lane - s * p.B) : 0;
   const int ls = (int)(s - s_first);
-  uint32_t* lds_te = lds_dyn;                       // [2][ns][5]
-  uint32_t* lds_win = lds_te + 2 * ns * 5;          // [ns][W][WS]
-  uint32_t* lds_ck = lds_win + ns * W * WS;         // [ns] the launch's first trunk checksum
-  uint32_t* lds_tin = lds_ck + ns;                  // [ns]
-  uint32_t* lds_rows = lds_tin + ns;                // [n + W - 1][ns]
+  // the prologue's global reads issued together (one memory latency): the lane's trunk, the
+  // survivor bit and cell checksum of the first round's check, the launch's input rows
+  BoxState<P> T;  // the trunk of the lane's session at frame f_c + u (every lane holds its own copy)
+  load_state<P>(T, p.trunk + s, p.S);
+  // (the first round's cell was saved by an earlier launch: its representative's; read whether or
+  // not the lane survived, so that no load waits for another)
+  const uint64_t prev_bits = p.check_prev && in_range ? p.prev_survive[lane >> 6] : 0ull;
+  const uint16_t cell0 = p.check_prev ? p.ring_ck[(int64_t)(p.f_c % p.R) * p.L + rep0_lane(p, s, b)] : (uint16_t)0;
+  {
+    const int n_rows = n + W - 1;
+    const int32_t row0 = p.f_c % p.cap;
+    for (int i = threadIdx.x; i < n_rows * ns; i += kRoundsBlock) {
+      const int k = i / ns, xs = i - k * ns;
+      const int32_t row = row0 + k >= p.cap ? row0 + k - p.cap : row0 + k;
+      lds_rows[i] = load_inputs<P>(p.inputs, (int64_t)row * p.S + s_first + xs);
+    }
+  }
+  __syncthreads();
+  bool survived = p.check_prev && in_range && ((prev_bits >> (lane & 63)) & 1ull);
+  const bool check0 = p.check_prev && survived;
+  const uint16_t mine0 = check0 ? cell0 : (uint16_t)0;
+  // every state a wave steps descends from its lanes' trunks (produced by this engine): one test of
+  // their rotation domain per wave, then the lean step throughout
+  const bool lean_ok = __all(rot_in_domain<P>(T));
   constexpr int kq[5] = {fld_x(P, e), fld_y(P, e), fld_vx(P, e), fld_vy(P, e), fld_rot(P, e)};
   uint32_t wt[5];
 #pragma unroll
   for (int q = 0; q < 5; q++) wt[q] = 2u * weights_at(n_bytes, fld_offset(P, kq[q]));
-  auto wrap_inc = [](int32_t x, int32_t m) { return x + 1 == m ? 0 : x + 1; };
-  auto win_entry = [&](int sl, int32_t wslot) { return lds_win + ((int64_t)sl * W + wslot) * WS; };
-  // a window entry: the local players' fields, then the doubled sums of frame + local fields +
-  // the length-prefix constants
-  auto write_entry = [&](uint32_t* dst, const uint32_t (&loc)[FL > 0 ? FL : 1], int32_t frame) {
-    uint32_t d1 = 2u * Fletcher<P>::kSum1Const, d2 = 2u * Fletcher<P>::kSum2Const;
-    d1 = dot4_u8((uint32_t)frame, 0x02020202u, d1);
-    d2 = dot4_u8((uint32_t)frame, 2u * weights_at(n_bytes, 0), d2);
-    int li = 0;
+  // per-stage constants: the digit stage k plays, and whether this lane represents its depth-k prefix
+  // (per-lane conditions live as VGPR offsets and one scalar bit set, not as 64-bit lane masks:
+  // the loop's scalar registers would otherwise spill to VGPR lanes)
+  uint32_t din[KW], off[KW], off_ck[KW];
+  uint32_t wave_reps = 0;  // bit k: some lane of this wave represents its depth-k prefix
+  {
+    int32_t pw = p.A;  // A^min(k+1, E), capped at B
 #pragma unroll
-    for (int q = 0; q < P; q++) {
-      if (q == e) continue;
-      const int fk[5] = {fld_x(P, q), fld_y(P, q), fld_vx(P, q), fld_vy(P, q), fld_rot(P, q)};
-#pragma unroll
-      for (int u = 0; u < 5; u++) {
-        const uint32_t v = loc[5 * li + u];
-        d1 = dot4_u8(v, 0x02020202u, d1);
-        d2 = dot4_u8(v, 2u * weights_at(n_bytes, fld_offset(P, fk[u])), d2);
-        dst[5 * li + u] = v;
-      }
-      li++;
-    }
-    dst[FL] = d1;
-    dst[FL + 1] = d2;
-  };
-  auto step_locals = [&](uint32_t (&loc)[FL > 0 ? FL : 1], uint32_t in) {
-    int li = 0;
-#pragma unroll
-    for (int q = 0; q < P; q++) {
-      if (q == e) continue;
-      float x = __builtin_bit_cast(float, loc[5 * li]), y = __builtin_bit_cast(float, loc[5 * li + 1]);
-      float vx = __builtin_bit_cast(float, loc[5 * li + 2]), vy = __builtin_bit_cast(float, loc[5 * li + 3]);
-      float rot = __builtin_bit_cast(float, loc[5 * li + 4]);
-      advance_player(x, y, vx, vy, rot, (in >> (8 * q)) & 0xffu);
-      loc[5 * li] = __builtin_bit_cast(uint32_t, x);
-      loc[5 * li + 1] = __builtin_bit_cast(uint32_t, y);
-      loc[5 * li + 2] = __builtin_bit_cast(uint32_t, vx);
-      loc[5 * li + 3] = __builtin_bit_cast(uint32_t, vy);
-      loc[5 * li + 4] = __builtin_bit_cast(uint32_t, rot);
-      li++;
-    }
-  };
-  auto row_of = [&](int32_t row, int32_t k) {  // input row k frames after `row`, 0 <= k < cap
-    const int32_t r = row + k;
-    return r >= p.cap ? r - p.cap : r;
-  };
-  int32_t row_c = p.f_c % p.cap, slot_c = p.f_c % p.R, wslot_c = p.f_c % W;
-  // extra lane items: item q = xl + 64 i -> session q >> 1, role q & 1
-  const int xl = threadIdx.x - kRoundsBlock;
-  const int n_rows = rp.n + W - 1;
-  for (int i = threadIdx.x; i < n_rows * ns; i += kPrefixBlock) {
-    const int k = i / ns, xs = i - k * ns;
-    lds_rows[i] = load_inputs<P>(p.inputs, (int64_t)row_of(row_c, k) * p.S + s_first + xs);
-  }
-  __syncthreads();
-  // prologue (extra wave): the trunk's enumerated player and checksum (role 0), the window of
-  // round 0 (role 1): the trunk's local players at f_c, then W - 1 frames of confirmed inputs
-  bool trunk_ok = true;
-  if (!branch_wave) {
-#pragma unroll
-    for (int i = 0; i < kPrefixItems; i++) {
-      const int q = xl + 64 * i;
-      if (q >= 2 * ns) continue;
-      const int xs = q >> 1;
-      const int64_t xsess = s_first + xs;
-      BoxState<P> t0;
-#pragma unroll
-      for (int k = 0; k < F; k++) t0.w[k] = p.trunk[(int64_t)k * p.S + xsess];
-      trunk_ok = trunk_ok && rot_in_domain<P>(t0);
-      if ((q & 1) == 0) {
-#pragma unroll
-        for (int u = 0; u < 5; u++) lds_te[xs * 5 + u] = t0.w[kq[u]];
-        lds_ck[xs] = fletcher16_state<P>(t0);  // the first round's survivor check
-      } else {
-        uint32_t loc[FL > 0 ? FL : 1];
-        int li = 0;
-#pragma unroll
-        for (int qq = 0; qq < P; qq++) {
-          if (qq == e) continue;
-          const int fk[5] = {fld_x(P, qq), fld_y(P, qq), fld_vx(P, qq), fld_vy(P, qq), fld_rot(P, qq)};
-#pragma unroll
-          for (int u = 0; u < 5; u++) loc[5 * li + u] = t0.w[fk[u]];
-          li++;
-        }
-        int32_t ws = wslot_c;
-        write_entry(win_entry(xs, ws), loc, p.f_c);
-        for (int32_t k = 1; k < W; k++) {
-          step_locals(loc, lds_rows[(k - 1) * ns + xs]);
-          ws = wrap_inc(ws, W);
-          write_entry(win_entry(xs, ws), loc, p.f_c + k);
-        }
-      }
+    for (int k = 0; k < KW; k++) {
+      din[k] = branch_digit(b, k, p.A, p.E);
+      const bool rep = in_range && b < pw;
+      off[k] = rep ? (uint32_t)(lane * 4) : kPipeOob;
+      off_ck[k] = rep ? (uint32_t)(lane * 2) : kPipeOob;
+      wave_reps |= (__builtin_amdgcn_ballot_w64(rep) != 0 ? 1u : 0u) << k;
+      pw = pw >= p.B / p.A ? p.B : pw * p.A;
     }
   }
-  // every state the launch steps descends from the block's trunks (produced by this engine): one
-  // block-wide test of the rotation domain, then the lean step throughout
-  const bool lean_ok = __syncthreads_and(trunk_ok);
-  bool survived = p.check_prev && in_range && ((p.prev_survive[lane >> 6] >> (lane & 63)) & 1ull);
-  const int64_t rep0 = rep0_lane(p, s, b);
-  const int32_t digit0 = (int32_t)branch_digit(b, 0, p.A, p.E);
-  uint32_t e0[5] = {0, 0, 0, 0, 0};  // the enumerated player after the round's first frame
-  // the first round's survivor check reads the cell an earlier launch saved: loaded here, before
-  // the loop (a global load inside it would wait for the wave's saves)
-  const bool check0 = p.check_prev && survived;
-  const uint16_t mine0 = check0 ? p.ring_ck[(int64_t)slot_c * p.L + rep0] : (uint16_t)0;
-  // saves: ring [R][F][L] through one buffer descriptor; per-lane field offsets, slot offset uniform
+  wave_reps = __builtin_amdgcn_readfirstlane(wave_reps);
   const uint32_t slot_bytes = (uint32_t)(F * p.L * 4);
   const __amdgpu_buffer_rsrc_t rs_ring = prefix_rsrc(p.ring, slot_bytes * (uint32_t)p.R);
   const __amdgpu_buffer_rsrc_t rs_ck = prefix_rsrc(p.ring_ck, (uint32_t)(2 * p.L * p.R));
-  const uint32_t lo = in_range ? (uint32_t)(lane * 4) : kPrefixOob;
-  const uint32_t lo_ck = in_range ? (uint32_t)(lane * 2) : kPrefixOob;
   const uint32_t fstride = (uint32_t)(p.L * 4);
-  for (int32_t r = 0; r < rp.n; ++r) {
-    const int32_t f_c = p.f_c + r;
-    const int buf = r & 1;
-    // the survivors' check (speculate_kernel's): in the first round against the cell an earlier
-    // launch saved (its representative's checksum vs the trunk's); in later rounds the lane compares
-    // its own depth-0 enumerated player of the previous round with the trunk's replayed one (the
-    // cell's local players ARE the trunk's: one window entry) -- the representative may sit in a
-    // block that is at another round of this launch
-    const int32_t wnext = wrap_inc(wslot_c, W);
-#ifdef GGRS_EXP_PFX_NOEXTRA
-    if (false) {
-#else
-    if (!branch_wave) {
-#endif
-      // (a) the trunk's enumerated player with the confirmed input of f_c (the confirm replay), and
-      // the window entry of frame f_c + W (into the slot frame f_c leaves); next round's rows
+  const bool branch0 = in_range && b == 0;  // writes the session's trunk and report
+  // per-lane destinations (VGPR pointers: the loop's scalar registers are taken by its counters,
+  // descriptors and masks, and uniform pointers kept there spilled to VGPR lanes)
+  uint64_t* const bits_dst = rp.report_bits + (lane >> 6);
+  uint8_t* const bits_copy = rp.copy_bits ? reinterpret_cast<uint8_t*>(rp.copy_bits + (lane >> 6)) : nullptr;
+  uint32_t* const trunk_dst = rp.trunk + s;
+  uint16_t* const ck_dst = rp.report_ck + s;
+  uint8_t* const ck_copy = rp.copy_ck ? reinterpret_cast<uint8_t*>(rp.copy_ck + s) : nullptr;
+  int32_t* const desync_dst = p.desync + s;
+  const int64_t copy_stride = rp.copy_stride;
+
+  // the doubled Fletcher sums of a cell's common part (frame + local players + length prefixes)
+  auto common_sums = [&](const BoxState<P>& t, uint32_t& d1, uint32_t& d2) {
+    d1 = 2u * Fletcher<P>::kSum1Const;
+    d2 = 2u * Fletcher<P>::kSum2Const;
 #pragma unroll
-      for (int i = 0; i < kPrefixItems; i++) {
-        const int q = xl + 64 * i;
-        if (q >= 2 * ns) continue;
-        const int xs = q >> 1;
-        if ((q & 1) == 0) {
-          const uint32_t in = lds_rows[r * ns + xs];  // frame f_c
-          const uint32_t ein = (in >> (8 * e)) & 0xffu;
-          const uint32_t* te = lds_te + (buf * ns + xs) * 5;
-          float x = __builtin_bit_cast(float, te[0]), y = __builtin_bit_cast(float, te[1]);
-          float vx = __builtin_bit_cast(float, te[2]), vy = __builtin_bit_cast(float, te[3]);
-          float rot = __builtin_bit_cast(float, te[4]);
-          advance_player(x, y, vx, vy, rot, ein);
-          uint32_t* tn = lds_te + ((buf ^ 1) * ns + xs) * 5;
-          tn[0] = __builtin_bit_cast(uint32_t, x);
-          tn[1] = __builtin_bit_cast(uint32_t, y);
-          tn[2] = __builtin_bit_cast(uint32_t, vx);
-          tn[3] = __builtin_bit_cast(uint32_t, vy);
-          tn[4] = __builtin_bit_cast(uint32_t, rot);
-          lds_tin[xs] = ein;
-        } else {
-          const uint32_t in = lds_rows[(r + W - 1) * ns + xs];  // frame f_c + W - 1
-          const int32_t wprev = wslot_c == 0 ? W - 1 : wslot_c - 1;  // frame f_c + W - 1
-          const uint32_t* src = win_entry(xs, wprev);
-          uint32_t loc[FL > 0 ? FL : 1];
+    for (int k = 0; k < F; k++) {
+      bool mine = false;
 #pragma unroll
-          for (int u = 0; u < FL; u++) loc[u] = src[u];
-          step_locals(loc, in);
-          write_entry(win_entry(xs, wslot_c), loc, f_c + W);
-        }
-      }
+      for (int q = 0; q < 5; q++) mine = mine || k == kq[q];
+      if (mine) continue;
+      d1 = dot4_u8(t.w[k], 0x02020202u, d1);
+      d2 = dot4_u8(t.w[k], 2u * weights_at(n_bytes, fld_offset(P, k)), d2);
     }
-    // LoadGameState(f_c): the trunk's enumerated player
-    float x = 0.0f, y = 0.0f, vx = 0.0f, vy = 0.0f, rot = 0.0f;
-    if (branch_wave) {
-      const uint32_t* te = lds_te + (buf * ns + ls) * 5;
-      x = __builtin_bit_cast(float, te[0]), y = __builtin_bit_cast(float, te[1]);
-      vx = __builtin_bit_cast(float, te[2]), vy = __builtin_bit_cast(float, te[3]);
-      rot = __builtin_bit_cast(float, te[4]);
-      if (r > 0 && survived) {
-        const bool same = te[0] == e0[0] && te[1] == e0[1] && te[2] == e0[2] && te[3] == e0[3] && te[4] == e0[4];
-        if (!same) atomicCAS(&p.desync[s], -1, f_c);
-      }
+  };
+  auto enum_ck = [&](uint32_t d1, uint32_t d2, const uint32_t (&v)[5]) {
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+      d1 = dot4_u8(v[q], 0x02020202u, d1);
+      d2 = dot4_u8(v[q], wt[q], d2);
     }
-    int32_t slot = slot_c, wslot = wslot_c;
-    int32_t pw = p.A;  // A^min(k+1, E): branches below it are depth k's representatives
-#pragma unroll kUnroll
-    for (int32_t k = 0; k < W; ++k) {
-#ifndef GGRS_EXP_PFX_NOBAR1
-      if (k == W - 1) lds_barrier();  // the window entry of frame f_c + W, the trunk replay
-#endif
-      slot = wrap_inc(slot, p.R);     // frame f_c + k + 1
-      wslot = wrap_inc(wslot, W);
-      if (branch_wave) {
-        const uint32_t din = branch_digit(b, k, p.A, p.E);  // AdvanceFrame(f_c + k)
-        if (lean_ok) advance_player_lean(x, y, vx, vy, rot, din);
-        else advance_player_general(x, y, vx, vy, rot, din);
-        if (k == 0) {
-          e0[0] = __builtin_bit_cast(uint32_t, x);
-          e0[1] = __builtin_bit_cast(uint32_t, y);
-          e0[2] = __builtin_bit_cast(uint32_t, vx);
-          e0[3] = __builtin_bit_cast(uint32_t, vy);
-          e0[4] = __builtin_bit_cast(uint32_t, rot);
+    return fletcher_from_doubled(d1, d2);
+  };
+
+  auto run = [&](auto lean_tag) {
+    constexpr bool kLean = decltype(lean_tag)::value;
+    auto adv = [&](uint32_t (&v)[5], uint32_t in) {
+      float x = __builtin_bit_cast(float, v[0]), y = __builtin_bit_cast(float, v[1]);
+      float vx = __builtin_bit_cast(float, v[2]), vy = __builtin_bit_cast(float, v[3]);
+      float rot = __builtin_bit_cast(float, v[4]);
+      if constexpr (kLean) advance_player_lean(x, y, vx, vy, rot, in);
+      else advance_player_general(x, y, vx, vy, rot, in);
+      v[0] = __builtin_bit_cast(uint32_t, x);
+      v[1] = __builtin_bit_cast(uint32_t, y);
+      v[2] = __builtin_bit_cast(uint32_t, vx);
+      v[3] = __builtin_bit_cast(uint32_t, vy);
+      v[4] = __builtin_bit_cast(uint32_t, rot);
+    };
+    uint32_t est[KW][5];  // stage k: the enumerated player of round u - k after its step k
+#pragma unroll
+    for (int k = 0; k < KW; k++)
+#pragma unroll
+      for (int q = 0; q < 5; q++) est[k][q] = 0u;
+    int32_t slot = p.f_c % p.R;
+    const SincosConsts sck = sincos_consts_vgpr();
+    // one super-step; kGuard: some stage belongs to no round of this launch (ramp / drain)
+    auto super_step = [&](int32_t u, auto guard_tag) {
+      constexpr bool kGuard = decltype(guard_tag)::value;
+      auto active = [&](int k) { return !kGuard || (k < W && u - k >= 0 && u - k < n); };
+      const int32_t f_c = p.f_c + u;  // round u's trunk frame; every save is frame f_c + 1
+      const uint32_t row = lds_rows[u * ns + ls];
+      slot = slot + 1 == p.R ? 0 : slot + 1;
+      if (active(0)) {
+        // speculate_kernel's check of round u - 1's survivors: their depth-0 enumerated player
+        // against the replayed trunk's (the cell's local players ARE the trunk's)
+        if (u > 0 && survived) {
+          bool same = true;
+#pragma unroll
+          for (int q = 0; q < 5; q++) same = same && est[0][q] == T.w[kq[q]];
+          if (!same) atomicCAS(desync_dst, -1, f_c);
         }
-        const bool rep = in_range && b < pw;
-        if (__builtin_amdgcn_ballot_w64(rep) != 0) {
-          // SaveGameState(f_c + k + 1): the common part from the window, the enumerated player's
-          // fields from this lane, the checksum from the entry's sums + this player's
-          const uint32_t* ent = win_entry(ls, wslot);
-          const uint32_t ev[5] = {__builtin_bit_cast(uint32_t, x), __builtin_bit_cast(uint32_t, y),
-                                  __builtin_bit_cast(uint32_t, vx), __builtin_bit_cast(uint32_t, vy),
-                                  __builtin_bit_cast(uint32_t, rot)};
-          uint32_t d1 = ent[FL], d2 = ent[FL + 1];
+        if (u == 0 && check0) {
+          uint32_t d1, d2, v[5];
+          common_sums(T, d1, d2);
 #pragma unroll
-          for (int q = 0; q < 5; q++) {
-            d1 = dot4_u8(ev[q], 0x02020202u, d1);
-            d2 = dot4_u8(ev[q], wt[q], d2);
-          }
-          const uint32_t ck = fletcher_from_doubled(d1, d2);
-#ifdef GGRS_EXP_PFX_NOSTORE
-          if (false) {
-#else
-          if (rep) {  // per-lane field offsets, the slot's offset wave-uniform
-#endif
-            const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)slot * slot_bytes);
-            __builtin_amdgcn_raw_buffer_store_b32((uint32_t)(f_c + k + 1), rs_ring, lo, so, 0);
-            int li = 0;
-#pragma unroll
-            for (int q = 0; q < P; q++) {
-              const int fk[5] = {fld_x(P, q), fld_y(P, q), fld_vx(P, q), fld_vy(P, q), fld_rot(P, q)};
-#pragma unroll
-              for (int u = 0; u < 5; u++)
-                __builtin_amdgcn_raw_buffer_store_b32(q == e ? ev[u] : ent[5 * li + u], rs_ring,
-                                                      lo + (uint32_t)fk[u] * fstride, so, 0);
-              if (q != e) li++;
-            }
-            __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ck, lo_ck,
-                                                  __builtin_amdgcn_readfirstlane((uint32_t)slot * (uint32_t)(2 * p.L)), 0);
-          }
+          for (int q = 0; q < 5; q++) v[q] = T.w[kq[q]];
+          if (mine0 != (uint16_t)enum_ck(d1, d2, v)) atomicCAS(desync_dst, -1, f_c);
         }
       }
-      pw = pw >= p.B / p.A ? p.B : pw * p.A;
-    }
-    if (!branch_wave) {
-      // the new trunk: frame f_c + 1, the window's first entry, the replayed enumerated player
+      // the stages' steps (round u - k's AdvanceFrame(f_c) with digit k: stage k takes stage k - 1's
+      // state of the previous super-step, stage 0 the trunk's enumerated player) and the trunk's
+      // confirmed replay of frame f_c (every player), as independent player steps
+      constexpr int NS = KW + P;
+      uint32_t xs[NS][5], xin[NS];
 #pragma unroll
-      for (int i = 0; i < kPrefixItems; i++) {
-        const int q = xl + 64 * i;
-        if (q >= 2 * ns || (q & 1)) continue;
-        const int xs = q >> 1;
-        const int64_t xsess = s_first + xs;
-        const uint32_t* tn = lds_te + ((buf ^ 1) * ns + xs) * 5;
-        const uint32_t* ent = win_entry(xs, wnext);
-        uint32_t d1 = ent[FL], d2 = ent[FL + 1];
+      for (int k = 0; k < KW; k++) {
 #pragma unroll
-        for (int u = 0; u < 5; u++) {
-          d1 = dot4_u8(tn[u], 0x02020202u, d1);
-          d2 = dot4_u8(tn[u], wt[u], d2);
-        }
-        const uint16_t tck = (uint16_t)fletcher_from_doubled(d1, d2);
-        if (xsess * p.B >= lane0) {  // this block holds the session's branch-0 lane
-          rp.trunk[xsess] = (uint32_t)(f_c + 1);
-          int li = 0;
-#pragma unroll
-          for (int qq = 0; qq < P; qq++) {
-            const int fk[5] = {fld_x(P, qq), fld_y(P, qq), fld_vx(P, qq), fld_vy(P, qq), fld_rot(P, qq)};
-#pragma unroll
-            for (int u = 0; u < 5; u++) rp.trunk[(int64_t)fk[u] * p.S + xsess] = qq == e ? tn[u] : ent[5 * li + u];
-            if (qq != e) li++;
-          }
-          rp.report_ck[xsess] = tck;
-          if (rp.copy_ck && (rp.copy_stride || r + 1 == rp.n))
-            reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(rp.copy_ck) + r * rp.copy_stride)[xsess] = tck;
-        }
+        for (int q = 0; q < 5; q++) xs[k][q] = k == 0 ? T.w[kq[q]] : est[k - 1][q];
+        xin[k] = din[k];
       }
-    } else {
-      // confirm: a lane survives iff it assumed the confirmed input of f_c (input_queue.rs:199-218)
-      const bool survive = in_range && (uint32_t)digit0 == lds_tin[ls];
-      const uint64_t bits = __ballot(survive);
-      if (in_range && (threadIdx.x & 63) == 0) {
-        rp.report_bits[lane >> 6] = bits;
-        if (rp.copy_bits && (rp.copy_stride || r + 1 == rp.n))
-          reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(rp.copy_bits) + r * rp.copy_stride)[lane >> 6] = bits;
+#pragma unroll
+      for (int q = 0; q < P; q++) {
+        const int fk[5] = {fld_x(P, q), fld_y(P, q), fld_vx(P, q), fld_vy(P, q), fld_rot(P, q)};
+#pragma unroll
+        for (int u5 = 0; u5 < 5; u5++) xs[KW + q][u5] = T.w[fk[u5]];
+        xin[KW + q] = (row >> (8 * q)) & 0xffu;
       }
-      if (r == 0 && check0 && mine0 != (uint16_t)lds_ck[ls]) atomicCAS(&p.desync[s], -1, f_c);
-      survived = survive;
-    }
-    lds_barrier();
-    row_c = wrap_inc(row_c, p.cap);
-    slot_c = wrap_inc(slot_c, p.R);
-    wslot_c = wnext;
-  }
+      if constexpr (kLean) {
+        advance_players_lean<NS>(xs, xin, sck);
+      } else {
+#pragma unroll
+        for (int i = 0; i < NS; i++) adv(xs[i], xin[i]);
+      }
+#pragma unroll
+      for (int k = 0; k < KW; k++)
+#pragma unroll
+        for (int q = 0; q < 5; q++) est[k][q] = xs[k][q];
+      BoxState<P> Tn;
+      Tn.w[0] = (uint32_t)(f_c + 1);
+#pragma unroll
+      for (int q = 0; q < P; q++) {
+        const int fk[5] = {fld_x(P, q), fld_y(P, q), fld_vx(P, q), fld_vy(P, q), fld_rot(P, q)};
+#pragma unroll
+        for (int u5 = 0; u5 < 5; u5++) Tn.w[fk[u5]] = xs[KW + q][u5];
+      }
+      uint32_t c1, c2;
+      common_sums(Tn, c1, c2);
+      // SaveGameState(f_c + 1) of every stage, the oldest round first; a depth-k cell only by the
+      // representatives of its prefix (wave-uniform skip when a wave holds none)
+      const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)slot * slot_bytes);
+      const uint32_t so_ck = __builtin_amdgcn_readfirstlane((uint32_t)slot * (uint32_t)(2 * p.L));
+#pragma unroll
+      for (int k = KW - 1; k >= 0; k--) {
+        if (!active(k) || k >= W) continue;
+        if (!((wave_reps >> k) & 1u)) continue;
+        const uint32_t ck = enum_ck(c1, c2, est[k]);
+        const uint32_t o = off[k], o_ck = off_ck[k];
+#pragma unroll
+        for (int f = 0; f < F; f++) {
+          uint32_t v = Tn.w[f];
+#pragma unroll
+          for (int q = 0; q < 5; q++)
+            if (f == kq[q]) v = est[k][q];
+          __builtin_amdgcn_raw_buffer_store_b32(v, rs_ring, o + (uint32_t)f * fstride, so, 0);
+        }
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ck, o_ck, so_ck, 0);
+      }
+      if (active(0)) {
+        // confirm of round u: a lane survives iff it assumed the confirmed input of f_c
+        // (input_queue.rs:199-218); branch 0 writes the new trunk and its checksum
+        const bool survive = in_range && din[0] == ((row >> (8 * e)) & 0xffu);
+        const uint64_t bits = __ballot(survive);
+        if (in_range && (threadIdx.x & 63) == 0) {
+          *bits_dst = bits;
+          if (bits_copy && (copy_stride || u + 1 == n))
+            *reinterpret_cast<uint64_t*>(bits_copy + u * copy_stride) = bits;
+        }
+        if (branch0) {
+          uint32_t v[5];
+#pragma unroll
+          for (int q = 0; q < 5; q++) v[q] = Tn.w[kq[q]];
+          const uint16_t tck = (uint16_t)enum_ck(c1, c2, v);
+          store_state<P>(Tn, trunk_dst, p.S);
+          *ck_dst = tck;
+          if (ck_copy && (copy_stride || u + 1 == n)) *reinterpret_cast<uint16_t*>(ck_copy + u * copy_stride) = tck;
+        }
+        survived = survive;
+      }
+      T = Tn;
+    };
+    const int32_t steady0 = W - 1 < n ? W - 1 : n;  // first super-step with every stage active
+    int32_t u = 0;
+    for (; u < steady0; ++u) super_step(u, std::true_type());
+    for (; u < n; ++u) super_step(u, std::false_type());
+    for (; u < n + W - 1; ++u) super_step(u, std::true_type());
+  };
+  if (lean_ok) run(std::true_type());
+  else run(std::false_type());
 }
 
 // compare_local_checksums_against_peers (p2p_session.rs:904-937) over an all-gathered report
@@ -730,7 +644,7 @@ namespace {
 size_t report_ck_bytes(int64_t S) { return ((size_t)S * 2 + 7) & ~(size_t)7; }
 constexpr size_t kPrefixLdsBytes = 32 * 1024;
 
-// prefix_rounds_kernel<P, EP> for the runtime enumerated player ep (0 <= ep < P)
+// prefix_pipe_kernel<P, EP> for the runtime enumerated player ep (0 <= ep < P)
 template <int P, typename Fn>
 void dispatch_enumerated(int ep, Fn&& fn) {
   switch (ep) {
@@ -1012,7 +926,7 @@ int ggrs_branch_read_lane(ggrs_branch_engine_t* e, int64_t lane, int32_t frame, 
   const int slot = ((frame % e->R) + e->R) % e->R;
   // the cell of `frame` was saved at depth k = frame - f_c - 1 of the last speculation from trunk
   // frame f_c (the frame f_c itself at depth 0 of the one before); branches sharing their first
-  // k + 1 digits share it, held by the representative b mod A^min(k+1, E) (prefix_rounds_kernel)
+  // k + 1 digits share it, held by the representative b mod A^min(k+1, E) (prefix_pipe_kernel)
   int64_t cell_lane = lane;
   if (e->E > 0 && e->last_spec_fc >= 0 && frame >= e->last_spec_fc && frame <= e->last_spec_fc + e->cfg.window) {
     const int k = frame > e->last_spec_fc ? frame - e->last_spec_fc - 1 : 0;
@@ -1086,17 +1000,14 @@ int launch_rounds(ggrs_branch_engine* e, int32_t n_rounds, void* copy, bool ever
   rp.copy_ck = copy ? (uint16_t*)copy : nullptr;
   rp.copy_bits = copy ? (uint64_t*)((uint8_t*)copy + report_ck_bytes(p.S)) : nullptr;
   rp.copy_stride = every_round ? (int64_t)e->report_bytes : 0;
-  // prefix sharing (prefix_rounds_kernel) when the enumerated player is the only remote one and
-  // its per-block window fits the LDS budget
+  // prefix sharing (prefix_pipe_kernel) when the enumerated player is the only remote one, the
+  // window fits its stage registers and the launch's input rows ([n + W - 1][ns] words) fit LDS
   const int ns_max = (int)std::min<int64_t>(kRoundsBlock / p.B + 2, p.S);
-  const size_t lds_fixed = (size_t)ns_max * (2 * 5 + (size_t)p.W * (5 * (p.P - 1) + 2) + 2);
-  // rounds per launch: their input rows ([n + W - 1][ns] words) must fit the budget as well
-  const int64_t rows_fit = ((int64_t)kPrefixLdsBytes / 4 - (int64_t)lds_fixed) / ns_max - (p.W - 1);
+  const int64_t rows_fit = (int64_t)kPrefixLdsBytes / 4 / ns_max - (p.W - 1);
   const int32_t n_chunk = (int32_t)std::max<int64_t>(0, std::min<int64_t>(n_rounds, rows_fit));
-  const size_t lds_words = lds_fixed + (size_t)ns_max * (n_chunk + p.W - 1);
+  const size_t lds_words = (size_t)ns_max * (n_chunk + p.W - 1);
   const bool prefix = e->round_form == 0 && p.B > 1 && __builtin_popcount(p.remote_mask) == 1 && n_chunk >= 1 &&
-                      lds_words * 4 <= kPrefixLdsBytes && 2 * ns_max <= 64 * kPrefixItems &&
-                      (int64_t)p.R * e->F * p.L * 4 < ((int64_t)1 << 30);
+                      p.W <= kPipeMaxW && (int64_t)p.R * e->F * p.L * 4 < ((int64_t)1 << 30);
   if (prefix && n_chunk < n_rounds) {  // launches of n_chunk rounds (their input rows fit LDS)
     for (int32_t r0 = 0; r0 < n_rounds; r0 += n_chunk) {
       const int32_t m = std::min(n_chunk, n_rounds - r0);
@@ -1116,8 +1027,8 @@ int launch_rounds(ggrs_branch_engine* e, int32_t n_rounds, void* copy, bool ever
         constexpr int P = decltype(PC)::value;
         dispatch_enumerated<P>(p.first_remote, [&](auto EC) {
           constexpr int EP = decltype(EC)::value;
-          if (p.W == 4) prefix_rounds_kernel<P, EP, 4><<<grid, kPrefixBlock, lds, e->stream>>>(rp);
-          else prefix_rounds_kernel<P, EP, 0><<<grid, kPrefixBlock, lds, e->stream>>>(rp);
+          if (p.W == 4) prefix_pipe_kernel<P, EP, 4><<<grid, kRoundsBlock, lds, e->stream>>>(rp);
+          else prefix_pipe_kernel<P, EP, 0><<<grid, kRoundsBlock, lds, e->stream>>>(rp);
         });
       });
       return;

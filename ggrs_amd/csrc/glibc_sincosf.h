@@ -221,4 +221,47 @@ __host__ __device__ inline void glibc_sincosf_domain(float y, float* sinp, float
 }
 constexpr uint32_t kTwoPiBits = 0x40c90fdbu;  // bits of (float)(2*pi)
 
+// glibc_sincosf_domain with its binary64 constants held in (vector) registers chosen by the
+// caller: the same operations in the same order, so the same results.  A loop that runs several
+// sin/cos per iteration beside many uniform values otherwise keeps these ten 64-bit constants in
+// scalar registers, where they spill to VGPR lanes and come back through v_readlane each use.
+struct SincosConsts {
+  double hpi_inv24, magic, hpi, s1, s2, s3, c1, c2, c3, c4;
+};
+__host__ __device__ inline double in_vgpr(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(x));
+#endif
+  return x;
+}
+__host__ __device__ inline SincosConsts sincos_consts_vgpr() {
+  return SincosConsts{in_vgpr(GGRS_SC_HPI_INV * 0x1p-24), in_vgpr(0x1.8p52), in_vgpr(GGRS_SC_HPI),
+                      in_vgpr(GGRS_SC_S1),  in_vgpr(GGRS_SC_S2), in_vgpr(GGRS_SC_S3),
+                      in_vgpr(GGRS_SC_C1),  in_vgpr(GGRS_SC_C2), in_vgpr(GGRS_SC_C3), in_vgpr(GGRS_SC_C4)};
+}
+__host__ __device__ inline void glibc_sincosf_domain_k(float y, float* sinp, float* cosp, const SincosConsts& K) {
+  const double xin = (double)y;
+  const double t = __builtin_fma(xin, K.hpi_inv24, K.magic);
+  const uint32_t n = (uint32_t)__builtin_bit_cast(uint64_t, t);
+  const double x = __builtin_fma(-(t - K.magic), K.hpi, xin);
+  const double x2 = x * x;
+  // sin_poly / cos_poly with the constants from K (the same fma / mul tree)
+  const double x3 = x * x2;
+  const double s1 = __builtin_fma(x2, K.s3, K.s2);
+  const double x7 = x3 * x2;
+  const double ss = __builtin_fma(x3, K.s1, x);
+  const float S = (float)__builtin_fma(x7, s1, ss);
+  const double x4 = x2 * x2;
+  const double c2 = __builtin_fma(x2, K.c4, K.c3);
+  const double c1 = __builtin_fma(x2, K.c1, GGRS_SC_C0);
+  const double x6 = x4 * x2;
+  const double cc = __builtin_fma(x4, K.c2, c1);
+  const float C = (float)__builtin_fma(x6, c2, cc);
+  const float sv = (n & 1) ? C : S;
+  const float cv = (n & 1) ? -S : C;
+  const bool flip = (n & 2) != 0;
+  *sinp = flip ? -sv : sv;
+  *cosp = flip ? -cv : cv;
+}
+
 }  // namespace ggrs

@@ -160,8 +160,21 @@ class ReportExchange:
         self.desync_count = torch.zeros((), dtype=torch.int64, device=dev)
         self.first_desync_round = torch.full((), -1, dtype=torch.int64, device=dev)
         self.history = [] if keep_history else None
+        # One dedicated stream carries the engine's rounds, the all-gathers' stream waits, the
+        # history copies and the comparisons.  The caller's current stream may be the null stream
+        # (handle 0), which set_stream reads as "the engine's own stream": the rounds would then
+        # be unordered with the all-gather that reads their reports (a gather could read the last
+        # round's row before the kernel wrote it).  It starts behind the caller's work so far.
+        self.stream = None
         if self.nccl:
-            engine.set_stream(torch.cuda.current_stream().cuda_stream)
+            self.stream = torch.cuda.Stream(device=dev)
+            self.stream.wait_stream(torch.cuda.current_stream(dev))
+            engine.set_stream(self.stream.cuda_stream)
+
+    def _on_stream(self):
+        import contextlib
+        import torch
+        return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
 
     def _finish(self, k):
         """Wait (device-side) for the all-gather in slot k and queue its comparison."""
@@ -206,6 +219,10 @@ class ReportExchange:
     def step(self):
         """One round: the fused round kernel; after a batch's last round, finish the previous
         batch's all-gather and start this one's."""
+        with self._on_stream():
+            self._step()
+
+    def _step(self):
         k = (self.round // self.batch) % 2
         j = self.round % self.batch
         if j == 0:
@@ -225,6 +242,10 @@ class ReportExchange:
             for _ in range(n_rounds):
                 self.step()
             return
+        with self._on_stream():
+            self._run(n_rounds)
+
+    def _run(self, n_rounds):
         while n_rounds > 0:
             k = (self.round // self.batch) % 2
             j = self.round % self.batch
@@ -240,11 +261,15 @@ class ReportExchange:
 
     def drain(self):
         """Start the gather of a partial last batch, finish every all-gather (device-side wait) --
-        call before reading results."""
-        k = (self.round // self.batch) % 2
-        j = self.round % self.batch
-        if j:
+        call before reading results.  The caller's current stream is then ordered after all of it."""
+        import torch
+        with self._on_stream():
+            k = (self.round // self.batch) % 2
+            j = self.round % self.batch
+            if j:
+                self._finish(1 - k)
+                self._start(k, j)
+            self._finish(k)
             self._finish(1 - k)
-            self._start(k, j)
-        self._finish(k)
-        self._finish(1 - k)
+        if self.stream is not None:
+            torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)

@@ -32,6 +32,8 @@ int main(int argc, char** argv) {
       if (w <= ggrs::kTwoPiBits) {
         float s3, c3; ggrs::glibc_sincosf_domain(f, &s3, &c3);
         if (bits(s3) != bits(a) || bits(c3) != bits(c)) { if (bd < 3) printf("domain %a\n", f); bd++; }
+        float s4, c4; ggrs::glibc_sincosf_domain_k(f, &s4, &c4, ggrs::sincos_consts_vgpr());
+        if (bits(s4) != bits(a) || bits(c4) != bits(c)) { if (bd < 3) printf("domain_k %a\n", f); bd++; }
       }
     }
     bad_s += bs; bad_c += bc; bad_f += bf; bad_d += bd;
