@@ -339,6 +339,9 @@ __device__ inline void advance_players_lean(uint32_t (&v)[N][5], const uint32_t 
     any = any || mag2[i] > kMaxSpeed * kMaxSpeed;
     vel[i] = ve;
   }
+#ifdef GGRS_EXP_NOCLAMP  // timing experiments only (tools/exp_build.sh): results then differ
+  any = false;
+#endif
   if (__builtin_expect(__builtin_amdgcn_ballot_w64(any) != 0, 0)) {
 #pragma unroll
     for (int i = 0; i < N; i++) {

@@ -88,6 +88,33 @@ __global__ __launch_bounds__(64) void red_1(double* out, int seed) {
   out[blockIdx.x * blockDim.x + threadIdx.x] = a;
 }
 
+// single-wave issue cost of INDEPENDENT instructions: 8 chains, 64 instructions per loop iteration
+// (loop overhead 1/64 of the figure)
+#define WIDE(NAME, ASM, T, C)                                                         \
+  __global__ __launch_bounds__(64) void NAME(double* out, int seed) {                 \
+    T a[8];                                                                           \
+    _Pragma("unroll") for (int k = 0; k < 8; k++) a[k] = (T)(threadIdx.x + k + 1);     \
+    T b = (T)seed;                                                                    \
+    for (int i = 0; i < ITER / 8; i++) {                                              \
+      _Pragma("unroll") for (int u = 0; u < 8; u++) {                                 \
+        _Pragma("unroll") for (int k = 0; k < 8; k++) asm volatile(ASM : "+" C(a[k]) : C(b)); \
+      }                                                                               \
+    }                                                                                 \
+    double s = 0;                                                                     \
+    _Pragma("unroll") for (int k = 0; k < 8; k++) s += (double)a[k];                  \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;                                   \
+  }
+WIDE(w_f64fma, "v_fma_f64 %0, %0, %1, %1", double, "v")
+WIDE(w_f64mul, "v_mul_f64 %0, %0, %1", double, "v")
+WIDE(w_f32fma, "v_fma_f32 %0, %0, %1, %1", float, "v")
+WIDE(w_f32add, "v_add_f32 %0, %0, %1", float, "v")
+WIDE(w_pkmul, "v_pk_mul_f32 %0, %0, %1", double, "v")
+WIDE(w_dot4, "v_dot4_u32_u8 %0, %1, %1, %0", unsigned, "v")
+WIDE(w_u32add, "v_add_u32 %0, %0, %1", unsigned, "v")
+
+
+
+
 typedef void (*Kf)(double*, int);
 struct Case { const char* name; Kf k; };
 
@@ -99,7 +126,11 @@ int main() {
                   {"v_dot4 1 chain", dot4_1}, {"v_add_u32 1 chain", u32_1}, {"v_pk_add_f32 1 chain", pk_1},
                   {"cvt f32<->f64 1 chain", cvt_1}, {"dpp row_shr 1 chain", dpp_1},
                   {"add+cmp+cbranch 1 chain (per 3)", cmpbr_1},
-                  {"sincos head 1 chain (per 8)", red_1}};
+                  {"sincos head 1 chain (per 8)", red_1},
+                  {"INDEPENDENT v_fma_f64 x8", w_f64fma}, {"INDEPENDENT v_mul_f64 x8", w_f64mul},
+                  {"INDEPENDENT v_fma_f32 x8", w_f32fma}, {"INDEPENDENT v_add_f32 x8", w_f32add},
+                  {"INDEPENDENT v_pk_mul_f32 x8", w_pkmul}, {"INDEPENDENT v_dot4 x8", w_dot4},
+                  {"INDEPENDENT v_add_u32 x8", w_u32add}};
   double* out;
   hipMalloc(&out, sizeof(double) * 64 * 8192);
   hipEvent_t e0, e1;
