@@ -82,11 +82,30 @@ __device__ inline uint32_t branch_inputs(const SpecParams& p, int64_t s, int32_t
   return branch_inputs_from<P>(p, truth, last, b, k);
 }
 
-// The lane whose ring holds branch b's depth-0 cell (the state after the first speculated frame):
-// the representative b mod A of its one-digit prefix (prefix_pipe_kernel saves only those), the
-// lane itself without enumeration.
+// The branch whose cell holds branch b's depth-k state (B = A^E): branches sharing their first
+// k + 1 digits share it, and prefix_pipe_kernel saves it once, by the prefix's representative.
+// The representatives of depth k < E - 1 are the A^(k+1) consecutive branches starting at
+// base_k = A^(k+2) + ... + A^(E-1) (depth E - 2 at branch 0, each shallower depth right after the
+// deeper one's range): base_k is a multiple of A^(k+1), so branch base_k + (b mod A^(k+1)) has
+// b's prefix, and every depth's representatives fill whole waves of their own -- no wave
+// represents two depths below E - 1, so no wave saves more than two cells per super-step (with
+// every shallow depth at branch 0, branch 0's wave saved W of them and set the launch's pace).
+// Depth >= E - 1 (and no enumeration): b itself.
+__host__ __device__ inline int64_t rep_branch(int64_t b, int k, int64_t A, int E) {
+  if (E <= 0 || k >= E - 1) return b;
+  int64_t q = 1, base = 0;
+  for (int j = 0; j < E - 1; j++) {
+    q *= A;                        // A^(j+1)
+    if (j > k) base += q;          // depths deeper than k, below E - 1
+  }
+  int64_t qk = 1;
+  for (int j = 0; j <= k; j++) qk *= A;  // A^(k+1)
+  return base + b % qk;
+}
+
+// The lane whose ring holds branch b's depth-0 cell (the state after the first speculated frame).
 __device__ inline int64_t rep0_lane(const SpecParams& p, int64_t s, int32_t b) {
-  return s * p.B + (p.E > 0 ? (int64_t)(b % p.A) : (int64_t)b);
+  return s * p.B + rep_branch(b, 0, p.A, p.E);
 }
 
 template <int P>
@@ -314,7 +333,7 @@ __global__ __launch_bounds__(kRoundsBlock) void rounds_kernel(RoundsParams rp) {
 //   * branch b's enumerated player plays digits d_0 .. d_k up to frame f_c + k, so branches sharing
 //     their first k + 1 digits hold the same state after k + 1 frames: A^min(k+1, E) distinct cells
 //     per session at depth k (config 3: 16, 256, 4096, 65,536 of the 4 x 65,536 logical saves),
-//     saved by the prefix's representative, branch b mod A^min(k+1, E) of the same session
+//     saved by the prefix's representative (rep_branch) of the same session
 //     (ggrs_branch_read_lane resolves a lane's cell to it).
 // A round is W dependent steps (speculated frames); consecutive rounds are independent given their
 // trunks, and round r's trunk is the confirmed replay of round r - 1's -- inputs only.  So the
@@ -360,6 +379,9 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
   const int64_t s = in_range ? lane / p.B : s_first;
   const int32_t b = in_range ? (int32_t)(lane - s * p.B) : 0;
   const int ls = (int)(s - s_first);
+#ifdef GGRS_EXP_STAMPS  // timing experiment only: phase stamps printed by two waves
+  const uint64_t ts0 = __builtin_amdgcn_s_memtime();
+#endif
   // the prologue's global reads issued together (one memory latency): the lane's trunk, the
   // survivor bit and cell checksum of the first round's check, the launch's input rows
   BoxState<P> T;  // the trunk of the lane's session at frame f_c + u (every lane holds its own copy)
@@ -378,6 +400,9 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
     }
   }
   __syncthreads();
+#ifdef GGRS_EXP_STAMPS
+  const uint64_t ts1 = __builtin_amdgcn_s_memtime();
+#endif
   bool survived = p.check_prev && in_range && ((prev_bits >> (lane & 63)) & 1ull);
   const bool check0 = p.check_prev && survived;
   const uint16_t mine0 = check0 ? cell0 : (uint16_t)0;
@@ -394,15 +419,13 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
   uint32_t din[KW], off[KW], off_ck[KW];
   uint32_t wave_reps = 0;  // bit k: some lane of this wave represents its depth-k prefix
   {
-    int32_t pw = p.A;  // A^min(k+1, E), capped at B
 #pragma unroll
     for (int k = 0; k < KW; k++) {
       din[k] = branch_digit(b, k, p.A, p.E);
-      const bool rep = in_range && b < pw;
+      const bool rep = in_range && rep_branch(b, k, p.A, p.E) == b;
       off[k] = rep ? (uint32_t)(lane * 4) : kPipeOob;
       off_ck[k] = rep ? (uint32_t)(lane * 2) : kPipeOob;
       wave_reps |= (__builtin_amdgcn_ballot_w64(rep) != 0 ? 1u : 0u) << k;
-      pw = pw >= p.B / p.A ? p.B : pw * p.A;
     }
   }
   wave_reps = __builtin_amdgcn_readfirstlane(wave_reps);
@@ -578,6 +601,12 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
   };
   if (lean_ok) run(std::true_type());
   else run(std::false_type());
+#ifdef GGRS_EXP_STAMPS
+  const uint64_t ts2 = __builtin_amdgcn_s_memtime();
+  if ((threadIdx.x & 63) == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1))
+    printf("PSTAMPS block %d wave %d prologue %llu loop %llu\n", (int)blockIdx.x, (int)(threadIdx.x >> 6),
+           (unsigned long long)(ts1 - ts0), (unsigned long long)(ts2 - ts1));
+#endif
 }
 
 // compare_local_checksums_against_peers (p2p_session.rs:904-937) over an all-gathered report
@@ -926,14 +955,12 @@ int ggrs_branch_read_lane(ggrs_branch_engine_t* e, int64_t lane, int32_t frame, 
   const int slot = ((frame % e->R) + e->R) % e->R;
   // the cell of `frame` was saved at depth k = frame - f_c - 1 of the last speculation from trunk
   // frame f_c (the frame f_c itself at depth 0 of the one before); branches sharing their first
-  // k + 1 digits share it, held by the representative b mod A^min(k+1, E) (prefix_pipe_kernel)
+  // k + 1 digits share it, held by the prefix's representative (rep_branch, prefix_pipe_kernel)
   int64_t cell_lane = lane;
   if (e->E > 0 && e->last_spec_fc >= 0 && frame >= e->last_spec_fc && frame <= e->last_spec_fc + e->cfg.window) {
     const int k = frame > e->last_spec_fc ? frame - e->last_spec_fc - 1 : 0;
-    int64_t pw = 1;
-    for (int q = 0; q < std::min(k + 1, e->E); q++) pw *= e->cfg.alphabet;
     const int64_t B = e->cfg.branches, sess = lane / B;
-    cell_lane = sess * B + (lane - sess * B) % pw;
+    cell_lane = sess * B + rep_branch(lane - sess * B, k, e->cfg.alphabet, e->E);
   }
   std::vector<uint32_t> w(e->F);
   for (int k = 0; k < e->F; k++)
