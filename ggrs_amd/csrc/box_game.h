@@ -301,6 +301,41 @@ __device__ inline void advance_player_rec(float& x, float& y, float& vx, float& 
   vy = vel.y;
 }
 
+// advance_player_rec from glibc_sincosf_domain_raw's unsigned values and quadrant signs: the
+// velocity increment keep ? (d ^ q ^ sgn) : sgn of advance_player_rec (d = MOVEMENT_SPEED times the
+// signed sin/cos) with d = MOVEMENT_SPEED x the raw value, whose sign q is applied as a bit flip
+// after the multiplication (RN(k * -v) == -RN(k * v) exactly): (d & keep) ^ (sgn ^ (q & keep)).
+template <typename Hook = NoHook>
+__device__ inline void advance_player_rec_q(float& x, float& y, float& vx, float& vy, float& rot, const InputRec& in,
+                                            float sr, float cr, uint32_t qs, uint32_t qc, Hook&& hook = Hook()) {
+  ggrs_f2 vel = ggrs_f2{vx, vy} * kFriction;
+  const ggrs_f2 d = ggrs_f2{cr, sr} * kMovementSpeed;
+  const float dx = d.x, dy = d.y;
+  const uint32_t wx = in.sgn ^ (qc & in.keep), wy = in.sgn ^ (qs & in.keep);
+  const uint32_t ix = (__builtin_bit_cast(uint32_t, dx) & in.keep) ^ wx;
+  const uint32_t iy = (__builtin_bit_cast(uint32_t, dy) & in.keep) ^ wy;
+  vel = vel + ggrs_f2{__builtin_bit_cast(float, ix), __builtin_bit_cast(float, iy)};
+  const float a = rot + __builtin_bit_cast(float, in.delta);
+  rot = a + (a < 0.0f ? kTwoPi : (a >= __builtin_bit_cast(float, in.thr) ? -kTwoPi : 0.0f));
+  hook(rot);
+  const ggrs_f2 sq = vel * vel;
+  const float mag2 = sq.x + sq.y;
+  const bool clamp = mag2 > kMaxSpeed * kMaxSpeed;
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(clamp) != 0, 0)) {
+    if (clamp) {
+      const float magnitude = sqrt_rn_above_49(mag2);
+      const double rr = rcp_f64_refined((double)magnitude);
+      vel.x = (float)((double)(vel.x * kMaxSpeed) * rr);
+      vel.y = (float)((double)(vel.y * kMaxSpeed) * rr);
+    }
+  }
+  const ggrs_f2 pos = ggrs_f2{x, y} + vel;
+  x = __builtin_amdgcn_fmed3f(pos.x, 0.0f, kWindowWidth);
+  y = __builtin_amdgcn_fmed3f(pos.y, 0.0f, kWindowHeight);
+  vx = vel.x;
+  vy = vel.y;
+}
+
 __device__ inline void advance_player_lean(float& x, float& y, float& vx, float& vy, float& rot,
                                            uint32_t input) {
   float s, c;

@@ -821,7 +821,8 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
   const uint32_t in_at = (uint32_t)in_lane;
   // core steps: sin/cos of the rot each lane holds at the step's start, computed one step ahead
   // (inside the previous step, from the rotated rot, before its speed clamp)
-  float sc_s = 0.0f, sc_c = 0.0f;
+  float sc_s = 0.0f, sc_c = 0.0f;  // the raw polynomial values (glibc_sincosf_domain_raw)
+  uint32_t sc_qs = 0u, sc_qc = 0u;   // and their quadrant signs
 
   auto rec_of = [](const uint4 v) { return InputRec{v.x, v.y, v.z, v.w}; };
   // core steps take the staged InputRec, non-core steps the raw input byte
@@ -840,11 +841,11 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
       float rot = __builtin_bit_cast(float, w[4]);
       if constexpr (kCore) {
         // the next step's rot is this lane's new rot rotated one role up (role 0 keeps its own)
-        advance_player_rec(x, y, vx, vy, rot, rec_of(in), sc_s, sc_c, [&](float rn) {
+        advance_player_rec_q(x, y, vx, vy, rot, rec_of(in), sc_s, sc_c, sc_qs, sc_qc, [&](float rn) {
           const uint32_t rb = __builtin_bit_cast(uint32_t, rn);
           const uint32_t nb = Pp == 2 ? (uint32_t)__builtin_amdgcn_update_dpp((int)rb, (int)rb, 0x112, 0xF, 0xF, false)
                                       : (uint32_t)__builtin_amdgcn_ds_bpermute(src_rot, (int)rb);
-          glibc_sincosf_domain(__builtin_bit_cast(float, nb), &sc_s, &sc_c);
+          glibc_sincosf_domain_raw(__builtin_bit_cast(float, nb), &sc_s, &sc_c, &sc_qs, &sc_qc);
 #ifdef GGRS_EXP_PIN
           asm volatile("" ::"v"(sc_s), "v"(sc_c));
 #endif
@@ -945,8 +946,9 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
       float rot = __builtin_bit_cast(float, v[4]);
       if constexpr (kCore) {
         float bs, bc;
-        glibc_sincosf_domain(rot, &bs, &bc);
-        advance_player_rec(x, y, vx, vy, rot, rec_of(lds_rec[ri]), bs, bc);
+        uint32_t bqs, bqc;
+        glibc_sincosf_domain_raw(rot, &bs, &bc, &bqs, &bqc);
+        advance_player_rec_q(x, y, vx, vy, rot, rec_of(lds_rec[ri]), bs, bc, bqs, bqc);
       } else {
         advance_player(x, y, vx, vy, rot, lds_raw[rr]);
       }
@@ -1004,7 +1006,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
     bad |= __ballot(pend_ck != pend_first) & pend_lanes;
     pend_ck = pend_first = 0;
     pend_lanes = cmp_lanes;
-    glibc_sincosf_domain(__builtin_bit_cast(float, w[4]), &sc_s, &sc_c);
+    glibc_sincosf_domain_raw(__builtin_bit_cast(float, w[4]), &sc_s, &sc_c, &sc_qs, &sc_qc);
     for (; t + kB <= core_end; t += kB) {
       if (((t - p.f0) & (kStage5 - 1)) == 0) stage(t);
       const uint32_t ip = (uint32_t)(t - chunk0) * ROW + in_at;

@@ -32,6 +32,8 @@ int main(int argc, char** argv) {
       if (w <= ggrs::kTwoPiBits) {
         float s3, c3; ggrs::glibc_sincosf_domain(f, &s3, &c3);
         if (bits(s3) != bits(a) || bits(c3) != bits(c)) { if (bd < 3) printf("domain %a\n", f); bd++; }
+        float s5, c5; uint32_t q5s, q5c; ggrs::glibc_sincosf_domain_raw(f, &s5, &c5, &q5s, &q5c);
+        if ((bits(s5) ^ q5s) != bits(a) || (bits(c5) ^ q5c) != bits(c)) { if (bd < 3) printf("domain_raw %a\n", f); bd++; }
         float s4, c4; ggrs::glibc_sincosf_domain_k(f, &s4, &c4, ggrs::sincos_consts_vgpr());
         if (bits(s4) != bits(a) || bits(c4) != bits(c)) { if (bd < 3) printf("domain_k %a\n", f); bd++; }
       }
