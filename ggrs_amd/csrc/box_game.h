@@ -399,6 +399,56 @@ __device__ inline void advance_players_lean(uint32_t (&v)[N][5], const uint32_t 
   }
 }
 
+// advance_players_lean from decoded inputs (InputRec, make_input_rec) and the raw sin/cos with its
+// quadrant signs folded into the increment (advance_player_rec_q's arithmetic): the same IEEE ops.
+template <int N>
+__device__ inline void advance_players_rec(uint32_t (&v)[N][5], const InputRec (&in)[N],
+                                           const SincosConsts& K = sincos_consts_vgpr()) {
+  ggrs_f2 vel[N];
+  float mag2[N];
+  bool any = false;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    const float rot = __builtin_bit_cast(float, v[i][4]);
+    float sr, cr;
+    uint32_t qs, qc;
+    glibc_sincosf_domain_raw_k(rot, &sr, &cr, &qs, &qc, K);
+    ggrs_f2 ve = ggrs_f2{__builtin_bit_cast(float, v[i][2]), __builtin_bit_cast(float, v[i][3])} * kFriction;
+    const ggrs_f2 d = ggrs_f2{cr, sr} * kMovementSpeed;
+    const float dx = d.x, dy = d.y;
+    const uint32_t wx = in[i].sgn ^ (qc & in[i].keep), wy = in[i].sgn ^ (qs & in[i].keep);
+    const uint32_t ix = (__builtin_bit_cast(uint32_t, dx) & in[i].keep) ^ wx;
+    const uint32_t iy = (__builtin_bit_cast(uint32_t, dy) & in[i].keep) ^ wy;
+    ve = ve + ggrs_f2{__builtin_bit_cast(float, ix), __builtin_bit_cast(float, iy)};
+    const float a = rot + __builtin_bit_cast(float, in[i].delta);
+    v[i][4] = __builtin_bit_cast(uint32_t, a + (a < 0.0f ? kTwoPi : (a >= __builtin_bit_cast(float, in[i].thr) ? -kTwoPi : 0.0f)));
+    const ggrs_f2 sq = ve * ve;
+    mag2[i] = sq.x + sq.y;
+    any = any || mag2[i] > kMaxSpeed * kMaxSpeed;
+    vel[i] = ve;
+  }
+  if (__builtin_expect(__builtin_amdgcn_ballot_w64(any) != 0, 0)) {
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+      if (mag2[i] > kMaxSpeed * kMaxSpeed) {
+        const float magnitude = sqrt_rn_above_49(mag2[i]);
+        const double rr = rcp_f64_refined((double)magnitude);
+        vel[i].x = (float)((double)(vel[i].x * kMaxSpeed) * rr);
+        vel[i].y = (float)((double)(vel[i].y * kMaxSpeed) * rr);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    const ggrs_f2 pos = ggrs_f2{__builtin_bit_cast(float, v[i][0]), __builtin_bit_cast(float, v[i][1])} + vel[i];
+    v[i][0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_fmed3f(pos.x, 0.0f, kWindowWidth));
+    v[i][1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_fmed3f(pos.y, 0.0f, kWindowHeight));
+    const float vx = vel[i].x, vy = vel[i].y;
+    v[i][2] = __builtin_bit_cast(uint32_t, vx);
+    v[i][3] = __builtin_bit_cast(uint32_t, vy);
+  }
+}
+
 // Dispatch (every kernel): the lean branch-free form when every active lane's rot is in the
 // domain (always, for states this engine produced), else the general form for the whole wave.
 // advance_player_domain stays as the KAT reference of the lean form.

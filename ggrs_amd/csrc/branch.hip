@@ -417,11 +417,13 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
   // (per-lane conditions live as VGPR offsets and one scalar bit set, not as 64-bit lane masks:
   // the loop's scalar registers would otherwise spill to VGPR lanes)
   uint32_t din[KW], off[KW], off_ck[KW];
+  InputRec srec[KW];  // stage k's input decoded once: its digit is the lane's for the launch
   uint32_t wave_reps = 0;  // bit k: some lane of this wave represents its depth-k prefix
   {
 #pragma unroll
     for (int k = 0; k < KW; k++) {
       din[k] = branch_digit(b, k, p.A, p.E);
+      srec[k] = make_input_rec(din[k]);
       const bool rep = in_range && rep_branch(b, k, p.A, p.E) == b;
       off[k] = rep ? (uint32_t)(lane * 4) : kPipeOob;
       off_ck[k] = rep ? (uint32_t)(lane * 2) : kPipeOob;
@@ -517,11 +519,13 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
       // confirmed replay of frame f_c (every player), as independent player steps
       constexpr int NS = KW + P;
       uint32_t xs[NS][5], xin[NS];
+      InputRec xrec[NS];
 #pragma unroll
       for (int k = 0; k < KW; k++) {
 #pragma unroll
         for (int q = 0; q < 5; q++) xs[k][q] = k == 0 ? T.w[kq[q]] : est[k - 1][q];
         xin[k] = din[k];
+        xrec[k] = srec[k];
       }
 #pragma unroll
       for (int q = 0; q < P; q++) {
@@ -529,9 +533,10 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
 #pragma unroll
         for (int u5 = 0; u5 < 5; u5++) xs[KW + q][u5] = T.w[fk[u5]];
         xin[KW + q] = (row >> (8 * q)) & 0xffu;
+        xrec[KW + q] = make_input_rec(xin[KW + q]);
       }
       if constexpr (kLean) {
-        advance_players_lean<NS>(xs, xin, sck);
+        advance_players_rec<NS>(xs, xrec, sck);
       } else {
 #pragma unroll
         for (int i = 0; i < NS; i++) adv(xs[i], xin[i]);

@@ -221,38 +221,6 @@ __host__ __device__ inline void glibc_sincosf_domain(float y, float* sinp, float
 }
 constexpr uint32_t kTwoPiBits = 0x40c90fdbu;  // bits of (float)(2*pi)
 
-// glibc_sincosf_domain's two polynomial values before the quadrant's swap and signs are applied,
-// for callers that fold the signs into later bit operations: with S, C the polynomials and n the
-// quadrant, sin = sr ^ qs and cos = cr ^ qc as bits, where sr = n odd ? C : S, cr = n odd ? S : C,
-// qs = bit 1 of n at bit 31, qc = (bit 0 ^ bit 1) of n at bit 31 (the four quadrants' (sin, cos):
-// (S, C), (C, -S), (-S, -C), (-C, S)).  The swap is a bit-field select on a mask from n's bit 0.
-__host__ __device__ inline void glibc_sincosf_domain_raw(float y, float* sr, float* cr, uint32_t* qs, uint32_t* qc) {
-  const double xin = (double)y;
-  const double t = __builtin_fma(xin, GGRS_SC_HPI_INV * 0x1p-24, 0x1.8p52);
-  const uint32_t n = (uint32_t)__builtin_bit_cast(uint64_t, t);
-  const double x = __builtin_fma(-(t - 0x1.8p52), GGRS_SC_HPI, xin);
-  const double x2 = x * x;
-  const uint32_t S = __builtin_bit_cast(uint32_t, (float)sin_poly(x, x2));
-  const uint32_t C = __builtin_bit_cast(uint32_t, (float)cos_poly(x2));
-#if defined(__HIP_DEVICE_COMPILE__)
-  // one v_bfe_i32 (all ones in odd quadrants) and two v_bfi_b32 (the compiler expanded the
-  // equivalent and/or form into nine instructions)
-  uint32_t m, srb, crb;
-  asm("v_bfe_i32 %0, %1, 0, 1" : "=v"(m) : "v"(n));
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(srb) : "v"(m), "v"(C), "v"(S));
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(crb) : "v"(m), "v"(S), "v"(C));
-  *sr = __builtin_bit_cast(float, srb);
-  *cr = __builtin_bit_cast(float, crb);
-#else
-  const uint32_t m = 0u - (n & 1u);  // all ones in odd quadrants
-  *sr = __builtin_bit_cast(float, (m & C) | (~m & S));
-  *cr = __builtin_bit_cast(float, (m & S) | (~m & C));
-#endif
-  const uint32_t l30 = n << 30, l31 = n << 31;
-  *qs = l30 & 0x80000000u;
-  *qc = (l30 ^ l31) & 0x80000000u;
-}
-
 // glibc_sincosf_domain with its binary64 constants held in (vector) registers chosen by the
 // caller: the same operations in the same order, so the same results.  A loop that runs several
 // sin/cos per iteration beside many uniform values otherwise keeps these ten 64-bit constants in
@@ -294,6 +262,55 @@ __host__ __device__ inline void glibc_sincosf_domain_k(float y, float* sinp, flo
   const bool flip = (n & 2) != 0;
   *sinp = flip ? -sv : sv;
   *cosp = flip ? -cv : cv;
+}
+
+// glibc_sincosf_domain's two polynomial values before the quadrant's swap and signs are applied,
+// for callers that fold the signs into later bit operations: with S, C the polynomials and n the
+// quadrant, sin = sr ^ qs and cos = cr ^ qc as bits, where sr = n odd ? C : S, cr = n odd ? S : C,
+// qs = bit 1 of n at bit 31, qc = (bit 0 ^ bit 1) of n at bit 31 (the four quadrants' (sin, cos):
+// (S, C), (C, -S), (-S, -C), (-C, S)).  The swap is a bit-field select on a mask from n's bit 0.
+// The constants come from K (glibc_sincosf_domain_k's operations, in the same order).
+__host__ __device__ inline void glibc_sincosf_domain_raw_k(float y, float* sr, float* cr, uint32_t* qs, uint32_t* qc,
+                                                           const SincosConsts& K) {
+  const double xin = (double)y;
+  const double t = __builtin_fma(xin, K.hpi_inv24, K.magic);
+  const uint32_t n = (uint32_t)__builtin_bit_cast(uint64_t, t);
+  const double x = __builtin_fma(-(t - K.magic), K.hpi, xin);
+  const double x2 = x * x;
+  const double x3 = x * x2;
+  const double s1 = __builtin_fma(x2, K.s3, K.s2);
+  const double x7 = x3 * x2;
+  const double ss = __builtin_fma(x3, K.s1, x);
+  const uint32_t S = __builtin_bit_cast(uint32_t, (float)__builtin_fma(x7, s1, ss));
+  const double x4 = x2 * x2;
+  const double c2 = __builtin_fma(x2, K.c4, K.c3);
+  const double c1 = __builtin_fma(x2, K.c1, GGRS_SC_C0);
+  const double x6 = x4 * x2;
+  const double cc = __builtin_fma(x4, K.c2, c1);
+  const uint32_t C = __builtin_bit_cast(uint32_t, (float)__builtin_fma(x6, c2, cc));
+#if defined(__HIP_DEVICE_COMPILE__)
+  // one v_bfe_i32 (all ones in odd quadrants) and two v_bfi_b32 (the compiler expanded the
+  // equivalent and/or form into nine instructions)
+  uint32_t m, srb, crb;
+  asm("v_bfe_i32 %0, %1, 0, 1" : "=v"(m) : "v"(n));
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(srb) : "v"(m), "v"(C), "v"(S));
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(crb) : "v"(m), "v"(S), "v"(C));
+  *sr = __builtin_bit_cast(float, srb);
+  *cr = __builtin_bit_cast(float, crb);
+#else
+  const uint32_t m = 0u - (n & 1u);  // all ones in odd quadrants
+  *sr = __builtin_bit_cast(float, (m & C) | (~m & S));
+  *cr = __builtin_bit_cast(float, (m & S) | (~m & C));
+#endif
+  const uint32_t l30 = n << 30, l31 = n << 31;
+  *qs = l30 & 0x80000000u;
+  *qc = (l30 ^ l31) & 0x80000000u;
+}
+// the same with the constants as literals
+__host__ __device__ inline void glibc_sincosf_domain_raw(float y, float* sr, float* cr, uint32_t* qs, uint32_t* qc) {
+  constexpr SincosConsts K{GGRS_SC_HPI_INV * 0x1p-24, 0x1.8p52, GGRS_SC_HPI, GGRS_SC_S1, GGRS_SC_S2,
+                           GGRS_SC_S3, GGRS_SC_C1, GGRS_SC_C2, GGRS_SC_C3, GGRS_SC_C4};
+  glibc_sincosf_domain_raw_k(y, sr, cr, qs, qc, K);
 }
 
 }  // namespace ggrs
