@@ -306,11 +306,11 @@ __host__ __device__ inline void glibc_sincosf_domain_raw_k(float y, float* sr, f
   *qs = l30 & 0x80000000u;
   *qc = (l30 ^ l31) & 0x80000000u;
 }
-// the same with the constants as literals
+// the constants as literals (folded into the instructions or scalar registers)
+constexpr SincosConsts kSincosLiteral{GGRS_SC_HPI_INV * 0x1p-24, 0x1.8p52, GGRS_SC_HPI, GGRS_SC_S1, GGRS_SC_S2,
+                                      GGRS_SC_S3, GGRS_SC_C1, GGRS_SC_C2, GGRS_SC_C3, GGRS_SC_C4};
 __host__ __device__ inline void glibc_sincosf_domain_raw(float y, float* sr, float* cr, uint32_t* qs, uint32_t* qc) {
-  constexpr SincosConsts K{GGRS_SC_HPI_INV * 0x1p-24, 0x1.8p52, GGRS_SC_HPI, GGRS_SC_S1, GGRS_SC_S2,
-                           GGRS_SC_S3, GGRS_SC_C1, GGRS_SC_C2, GGRS_SC_C3, GGRS_SC_C4};
-  glibc_sincosf_domain_raw_k(y, sr, cr, qs, qc, K);
+  glibc_sincosf_domain_raw_k(y, sr, cr, qs, qc, kSincosLiteral);
 }
 
 }  // namespace ggrs
