@@ -785,6 +785,8 @@ def run_requests(args):
       --req-form lockstep  ggrs_handle_requests: one list for every lane (lockstep sessions)
     --req-groups G (native, p2p; default 2): the sessions served as G lane groups (G engines): each
     group's batch is on the device while the host hands back and encodes the others';
+    --req-threads T (native; default 1): host threads, thread t serving groups t*G/T .. (a game
+    server runs its sessions' GGRS instances on several cores; each group is its own engine);
     --session-us T: host time per group and call spent in the modelled GGRS session logic (spin).
     One step = `calls` such calls; inputs are resident in host memory before the timed region."""
     world, rank, local_rank, torch, dist = setup_dist(args)
@@ -798,6 +800,9 @@ def run_requests(args):
     G = args.req_groups if form in ("native", "p2p") else 1
     if L % G:
         raise SystemExit(f"--lanes {L} is not a multiple of --req-groups {G}")
+    T = args.req_threads if form == "native" else 1
+    if T < 1 or G % T:
+        raise SystemExit(f"--req-groups {G} is not a multiple of --req-threads {T}")
     sink = np.zeros(1, np.uint64)
     phases = np.zeros(4)
     drv = None
@@ -831,12 +836,20 @@ def run_requests(args):
         inputs = np.ascontiguousarray(inputs)
         drv.handler_drive_synctest_groups.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p] + \
             [ctypes.c_int32] * 5 + [ctypes.c_double, u64, dbl, dbl]
+        drv.handler_drive_synctest_threads.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
+                                                       ctypes.c_void_p] + [ctypes.c_int32] * 5 + \
+            [ctypes.c_double, u64, dbl, dbl]
 
         def run_calls(f, n):
             s, sec = ctypes.c_uint64(), ctypes.c_double()
             ph = (ctypes.c_double * 4)()
-            rc = drv.handler_drive_synctest_groups(handles, G, ctypes.c_void_p(inputs.ctypes.data), L, P, cd, f, n,
-                                                   args.session_us, ctypes.byref(s), ctypes.byref(sec), ph)
+            if T > 1:
+                rc = drv.handler_drive_synctest_threads(handles, G, T, ctypes.c_void_p(inputs.ctypes.data), L, P, cd,
+                                                        f, n, args.session_us, ctypes.byref(s), ctypes.byref(sec), ph)
+                ph = [x / T for x in ph]  # thread-seconds -> per-call wall shares
+            else:
+                rc = drv.handler_drive_synctest_groups(handles, G, ctypes.c_void_p(inputs.ctypes.data), L, P, cd, f,
+                                                       n, args.session_us, ctypes.byref(s), ctypes.byref(sec), ph)
             assert rc == 0, rc
             phases[:] = list(ph)  # of the last batch of calls (the timed one)
             sink[0] += s.value
@@ -985,7 +998,8 @@ def run_requests(args):
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": wl + f", {calls} calls per step, lists and inputs from host memory, checksums "
                                         "back to host memory each call",
-                       "sessions_per_gpu": L, "req_form": form, "lane_groups": G, "session_us_per_group_call":
+                       "sessions_per_gpu": L, "req_form": form, "lane_groups": G, "host_threads": T,
+                       "session_us_per_group_call":
                            args.session_us, "lane_server": not args.no_lane_server,
                        "us_per_call": round(elapsed / n_calls * 1e6, 2),
                        **({"us_per_call_host_encode_device_handback_session": [round(x / n_calls * 1e6, 2)
@@ -1059,7 +1073,9 @@ def main():
     ap.add_argument("--codec-layout", choices=["chunked", "strided"], default="chunked",
                     help="codec: packet layout (chunked: each 256-packet block's packets back to back)")
     ap.add_argument("--req-groups", type=int, default=2,
-                    help="requests (native, p2p): lane groups (engines) whose batches overlap the host's work")
+                    help="requests (native, p2p): lane groups (engines) whose batches overlap the host's work; at most 4 with the lane server (one persistent server per hardware queue)")
+    ap.add_argument("--req-threads", type=int, default=1,
+                    help="requests (native): host threads serving the lane groups (G a multiple of it)")
     ap.add_argument("--session-us", type=float, default=0.0,
                     help="requests: modelled GGRS session-logic host time per lane group and call (us)")
     ap.add_argument("--workload", choices=["synctest", "p2p", "codec", "requests", "launch-selftest"],

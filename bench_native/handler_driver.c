@@ -72,9 +72,10 @@ typedef struct {
  * ABI code; *seconds = wall time of the calls, *sink = sum of every Save checksum handed back;
  * phases (may be NULL): seconds spent encoding, waiting for the device (submit + wait), handing
  * checksums back, and in the modelled session logic. */
-int handler_drive_synctest_groups(ggrs_engine_t** engs, int32_t G, const uint8_t* inputs, int32_t L, int32_t P,
-                                  int32_t cd, int32_t f_begin, int32_t n_calls, double session_us, uint64_t* sink,
-                                  double* seconds, double* phases) {
+/* groups of lanes lane0 .. lane0 + L - 1 of input rows L_all lanes wide */
+static int drive_groups(ggrs_engine_t** engs, int32_t G, const uint8_t* inputs, int32_t L, int32_t L_all, int32_t lane0,
+                        int32_t P, int32_t cd, int32_t f_begin, int32_t n_calls, double session_us, uint64_t* sink,
+                        double* seconds, double* phases) {
   if (G < 1 || G > MAX_GROUPS || L % G) return GGRS_E_INVALID;
   group_t g[MAX_GROUPS];
   const int32_t Lg = L / G;
@@ -82,7 +83,7 @@ int handler_drive_synctest_groups(ggrs_engine_t** engs, int32_t G, const uint8_t
     int rc = ggrs_lane_batch_map(engs[q], 2, 1, cd + 1, cd + 1, &g[q].b);
     if (rc) return rc;
     g[q].pending = 0;
-    g[q].base = q * Lg;
+    g[q].base = lane0 + q * Lg;
     g[q].lanes = Lg;
   }
   double t_enc = 0, t_dev = 0, t_back = 0, t_sess = 0;
@@ -121,7 +122,7 @@ int handler_drive_synctest_groups(ggrs_engine_t** engs, int32_t G, const uint8_t
         for (int32_t l = 0; l < Lg; l++) gq->b.load_frames[l] = f - cd;
       const int32_t first = f - (na - 1); /* the frames the list's AdvanceFrames replay, in order */
       for (int a = 0; a < na; a++)
-        memcpy(gq->b.inputs + (size_t)a * Lg * P, inputs + ((size_t)(first + a) * L + gq->base) * P, (size_t)Lg * P);
+        memcpy(gq->b.inputs + (size_t)a * Lg * P, inputs + ((size_t)(first + a) * L_all + gq->base) * P, (size_t)Lg * P);
       gq->run = gq->b;
       gq->run.token_words = W;
       gq->run.load_slots = nl;
@@ -145,6 +146,83 @@ int handler_drive_synctest_groups(ggrs_engine_t** engs, int32_t G, const uint8_t
   }
   *sink = acc;
   return 0;
+}
+
+int handler_drive_synctest_groups(ggrs_engine_t** engs, int32_t G, const uint8_t* inputs, int32_t L, int32_t P,
+                                  int32_t cd, int32_t f_begin, int32_t n_calls, double session_us, uint64_t* sink,
+                                  double* seconds, double* phases) {
+  return drive_groups(engs, G, inputs, L, L, 0, P, cd, f_begin, n_calls, session_us, sink, seconds, phases);
+}
+
+/* Host threads: T threads, thread t serving groups t, t + T, ... through the loop above (a game
+ * server runs its sessions' GGRS instances on several cores; each engine is one lane group and the
+ * library keeps no state shared between engines).  The threads start together; *seconds is the
+ * slowest thread's wall time, *sink and phases sum over threads (phases: thread-seconds). */
+#include <pthread.h>
+
+typedef struct {
+  ggrs_engine_t* engs[MAX_GROUPS];
+  int32_t G;
+  const uint8_t* inputs;
+  int32_t L, L_all, lane0, P, cd, f_begin, n_calls;
+  double session_us;
+  uint64_t sink;
+  double seconds, phases[4];
+  int rc;
+  pthread_barrier_t* start;
+} thread_job_t;
+
+static void* drive_thread(void* arg) {
+  thread_job_t* j = (thread_job_t*)arg;
+  pthread_barrier_wait(j->start);
+  j->rc = drive_groups(j->engs, j->G, j->inputs, j->L, j->L_all, j->lane0, j->P, j->cd, j->f_begin, j->n_calls,
+                       j->session_us, &j->sink, &j->seconds, j->phases);
+  return NULL;
+}
+
+int handler_drive_synctest_threads(ggrs_engine_t** engs, int32_t G, int32_t T, const uint8_t* inputs, int32_t L,
+                                   int32_t P, int32_t cd, int32_t f_begin, int32_t n_calls, double session_us,
+                                   uint64_t* sink, double* seconds, double* phases) {
+  if (T < 1 || T > G || G % T || G > MAX_GROUPS || L % G) return GGRS_E_INVALID;
+  thread_job_t jobs[MAX_GROUPS];
+  pthread_t th[MAX_GROUPS];
+  pthread_barrier_t start;
+  pthread_barrier_init(&start, NULL, (unsigned)T);
+  const int32_t per = G / T, Lg = L / G;
+  for (int t = 0; t < T; t++) {
+    thread_job_t* j = &jobs[t];
+    memset(j, 0, sizeof *j);
+    for (int q = 0; q < per; q++) j->engs[q] = engs[t * per + q];
+    j->G = per;
+    j->inputs = inputs;  /* the thread's groups: lanes t*per*Lg .. of rows L lanes wide */
+    j->L = per * Lg;
+    j->L_all = L;
+    j->lane0 = t * per * Lg;
+    j->P = P;
+    j->cd = cd;
+    j->f_begin = f_begin;
+    j->n_calls = n_calls;
+    j->session_us = session_us;
+    j->start = &start;
+    if (pthread_create(&th[t], NULL, drive_thread, j)) return GGRS_E_STATE;
+  }
+  int rc = 0;
+  double worst = 0;
+  uint64_t acc = 0;
+  double ph[4] = {0, 0, 0, 0};
+  for (int t = 0; t < T; t++) {
+    pthread_join(th[t], NULL);
+    if (jobs[t].rc && !rc) rc = jobs[t].rc;
+    if (jobs[t].seconds > worst) worst = jobs[t].seconds;
+    acc += jobs[t].sink;
+    for (int k = 0; k < 4; k++) ph[k] += jobs[t].phases[k];
+  }
+  pthread_barrier_destroy(&start);
+  *seconds = worst;
+  *sink = acc;
+  if (phases)
+    for (int k = 0; k < 4; k++) phases[k] = ph[k];
+  return rc;
 }
 
 /* The single-engine form kept for bench.py --req-groups 1 (one synchronous batch per call). */
