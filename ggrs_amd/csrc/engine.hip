@@ -603,6 +603,16 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v4_kernel(PipeParams
 //     and stores their display checksums; the launch's last chain also writes the current state.
 // 16 lanes per session at cd 8 / two players: four sessions per wave, 1024 waves for 4096
 // sessions, one per SIMD; the batch adds about one step's work per 8 steps.
+// v5 step kinds: std::false_type the general step (raw input, per-step domain test, stores only for
+// the launch's chains), std::true_type the core step, EdgeStep the core step's arithmetic for the
+// launch's first and last steps (some roles hold chains of other launches: their stores write the
+// same bytes the launch's own chains store at the same step -- every role replays the same frame
+// from the same state -- but their comparisons, first-seen sources and display checksums are the
+// general step's)
+struct EdgeStep : std::true_type {};
+template <class T> struct IsEdge : std::false_type {};
+template <> struct IsEdge<EdgeStep> : std::true_type {};
+
 template <int P>
 __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams p) {
   constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
@@ -828,13 +838,12 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
   // core steps take the staged InputRec, non-core steps the raw input byte
   auto step = [&](auto core_tag, int32_t t, auto in, uint32_t slot_off) {
     constexpr bool kCore = decltype(core_tag)::value;
+    constexpr bool kEdge = IsEdge<decltype(core_tag)>::value;
     const int32_t rel = t - p.f0;
     const int32_t c = t - j;
-    const bool active = kCore ? valid : (valid && c >= p.f0 && c < p.f0 + p.n);
-    if (!kCore) {
-      bad |= __ballot(pend_ck != pend_first) & pend_lanes;
-      w[0] ^= (t == p.corrupt_frame) ? corrupt_on : 0u;
-    }
+    const bool active = (kCore && !kEdge) ? valid : (valid && c >= p.f0 && c < p.f0 + p.n);
+    if (!kCore || kEdge) bad |= __ballot(pend_ck != pend_first) & pend_lanes;
+    if (!kCore) w[0] ^= (t == p.corrupt_frame) ? corrupt_on : 0u;
     {
       float x = __builtin_bit_cast(float, w[0]), y = __builtin_bit_cast(float, w[1]);
       float vx = __builtin_bit_cast(float, w[2]), vy = __builtin_bit_cast(float, w[3]);
@@ -859,7 +868,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
       w[3] = __builtin_bit_cast(uint32_t, vy);
       w[4] = __builtin_bit_cast(uint32_t, rot);
     }
-    if (kCore) acc |= pend_ck ^ pend_first;
+    if (kCore && !kEdge) acc |= pend_ck ^ pend_first;
     const uint32_t frame1 = (uint32_t)(t - CD + 1);
     // rotation: role j takes role j-1's state, role 0 keeps its own.  At two players a session is
     // one 16-lane DPP row (role j = lanes 2j, 2j+1): one row_shr:2 move per field, the row's first
@@ -896,7 +905,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
     // row_newbcast of the row's lane 14)
     uint32_t first = Pp == 2 ? (uint32_t)__builtin_amdgcn_update_dpp(0, (int)ck, 0x150 + (CD - 1) * Pp, 0xF, 0xF, true)
                              : (uint32_t)__builtin_amdgcn_ds_bpermute(src_first, (int)ck);
-    if (!kCore && rel + 1 < CD) first = lds_first[(rel + 1) * SPW + g];
+    if ((!kCore || kEdge) && rel + 1 < CD) first = lds_first[(rel + 1) * SPW + g];
     const uint32_t sru = (uint32_t)sr;
     auto stores = [&]() {
       const uint32_t so = sru * slot_bytes, cso = sru * ck_slot_bytes;
@@ -908,7 +917,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
     };
     if (kCore) {
       stores();
-      pend_lanes = cmp_lanes;
+      pend_lanes = kEdge ? cmp_lanes & __ballot(active) : cmp_lanes;
     } else {
       if (active) stores();
       pend_lanes = cmp_lanes & __ballot(active);
@@ -926,11 +935,12 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
   // with input cb, which step tb + j + 1 reads -- and stores the display checksum of frame cb + 1.
   auto batch = [&](auto core_tag, int32_t tb, int count) {
     constexpr bool kCore = decltype(core_tag)::value;
+    constexpr bool kEdge = IsEdge<decltype(core_tag)>::value;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int32_t cb = tb + j - (CD - 1);
-    const bool act = kCore ? (valid && j < kB) : (valid && j < count && cb >= p.f0 && cb < p.f0 + p.n);
+    const bool act = (kCore && !kEdge) ? (valid && j < kB) : (valid && j < count && cb >= p.f0 && cb < p.f0 + p.n);
     uint32_t v[5];
     {
       const uint8_t* st = lds_stash + stash_r;
@@ -978,7 +988,7 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
     ti = ti >= tcap ? ti - tcap : ti;
     const uint32_t tro = act ? co_trace + (uint32_t)ti * ck_slot_bytes : kOob;
     __builtin_amdgcn_raw_buffer_store_b16((uint16_t)ck, rs_ring, tro, 0, 0);
-    if (!kCore && act && cb == p.f0 + p.n - 1) {  // the launch's last call: the current state
+    if ((!kCore || kEdge) && act && cb == p.f0 + p.n - 1) {  // the launch's last call: the current state
       uint32_t* cur = p.cur + s;
       if (owner) {
 #pragma unroll
@@ -998,9 +1008,30 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
     if ((rel & (kB - 1)) == kB - 1) batch(std::false_type(), t - (kB - 1), kB);
   };
   int32_t t = p.f0;
-  for (; t < ramp_end; ++t) general(t);
-  // core blocks of 8 steps + their batch, aligned to the batch grid
-  for (; t < core_end && ((t - p.f0) & (kB - 1)) != 0; ++t) general(t);
+  // lean launches of whole 8-step blocks run their first and last steps as edge steps (the core
+  // step's code, already warm in the instruction cache, with the general step's bookkeeping);
+  // others take the general step there
+  const bool edge_ok = core_end == p.f0 + p.n && (p.n & (kB - 1)) == 0 && p.n >= 2 * kB;
+  auto edge_block = [&](int32_t tb, int count) {
+    if (((tb - p.f0) & (kStage5 - 1)) == 0 || tb + count + 1 > chunk0 + kStage5 + 1) stage(tb);
+    const uint32_t ip = (uint32_t)(tb - chunk0) * ROW + in_at;
+    uint4 in[kB];
+#pragma unroll
+    for (int u = 0; u < kB; u++) in[u] = lds_rec[ip + u * ROW];
+#pragma unroll
+    for (int u = 0; u < kB; u++)
+      if (u < count) step(EdgeStep(), tb + u, in[u], (uint32_t)(u * kSlot));
+    batch(EdgeStep(), tb, count);
+  };
+  if (edge_ok) {
+    glibc_sincosf_domain_raw(__builtin_bit_cast(float, w[4]), &sc_s, &sc_c, &sc_qs, &sc_qc);
+    edge_block(t, kB);
+    t += kB;
+  } else {
+    for (; t < ramp_end; ++t) general(t);
+    // core blocks of 8 steps + their batch, aligned to the batch grid
+    for (; t < core_end && ((t - p.f0) & (kB - 1)) != 0; ++t) general(t);
+  }
   GGRS_STAMP();
   if (t + kB <= core_end) {
     bad |= __ballot(pend_ck != pend_first) & pend_lanes;
@@ -1020,8 +1051,10 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
     bad |= __ballot(acc != 0) & cmp_lanes;
   }
   GGRS_STAMP();
-  for (; t < t_end; ++t) general(t);
-  {
+  if (edge_ok) {
+    edge_block(t, t_end - t);  // the last cd - 1 steps and their batch
+  } else {
+    for (; t < t_end; ++t) general(t);
     const int rem = (t_end - p.f0) & (kB - 1);
     if (rem) batch(std::false_type(), t_end - rem, rem);
   }
