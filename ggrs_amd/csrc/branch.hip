@@ -360,6 +360,18 @@ __device__ inline __amdgpu_buffer_rsrc_t prefix_rsrc(const void* base, uint32_t 
 }
 
 template <int P, int EP, int WT>
+__global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams rp);
+
+// f(integral_constant<int, 0>) .. f(integral_constant<int, N - 1>)
+template <int N, int I = 0, typename Fn>
+__device__ inline void static_for(Fn&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>());
+    static_for<N, I + 1>(f);
+  }
+}
+
+template <int P, int EP, int WT>
 __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams rp) {
   static_assert(EP >= 0 && EP < P, "enumerated player");
   constexpr int F = state_fields(P);
@@ -490,10 +502,16 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
       for (int q = 0; q < 5; q++) est[k][q] = 0u;
     int32_t slot = p.f_c % p.R;
     const SincosConsts sck = sincos_consts_vgpr();
-    // one super-step; kGuard: some stage belongs to no round of this launch (ramp / drain)
-    auto super_step = [&](int32_t u, auto guard_tag) {
+    // one super-step; kGuard: some stage belongs to no round of this launch (ramp / drain).  Only
+    // stages [K0, K1) are stepped (the ramp and drain of a compile-time W step just the stages that
+    // hold a round: a stage without one feeds only stages without one), and the trunk's enumerated
+    // player only when kTE (in the drain no round reads the trunk's own enumerated player: stage 0
+    // is idle and every save replaces those fields with its stage's)
+    auto super_step = [&](int32_t u, auto guard_tag, auto k0_c, auto k1_c, auto te_c) {
       constexpr bool kGuard = decltype(guard_tag)::value;
-      auto active = [&](int k) { return !kGuard || (k < W && u - k >= 0 && u - k < n); };
+      constexpr int K0 = decltype(k0_c)::value, K1 = decltype(k1_c)::value;
+      constexpr bool kTE = decltype(te_c)::value;
+      auto active = [&](int k) { return k >= K0 && k < K1 && (!kGuard || (k < W && u - k >= 0 && u - k < n)); };
       const int32_t f_c = p.f_c + u;  // round u's trunk frame; every save is frame f_c + 1
       const uint32_t row = lds_rows[u * ns + ls];
       slot = slot + 1 == p.R ? 0 : slot + 1;
@@ -517,23 +535,27 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
       // the stages' steps (round u - k's AdvanceFrame(f_c) with digit k: stage k takes stage k - 1's
       // state of the previous super-step, stage 0 the trunk's enumerated player) and the trunk's
       // confirmed replay of frame f_c (every player), as independent player steps
-      constexpr int NS = KW + P;
+      // xs: stages K0 .. K1 - 1, then the trunk's players (all, or all but the enumerated one)
+      constexpr int NK = K1 - K0, NT = kTE ? P : P - 1, NS = NK + NT;
       uint32_t xs[NS][5], xin[NS];
       InputRec xrec[NS];
 #pragma unroll
-      for (int k = 0; k < KW; k++) {
+      for (int k = K0; k < K1; k++) {
 #pragma unroll
-        for (int q = 0; q < 5; q++) xs[k][q] = k == 0 ? T.w[kq[q]] : est[k - 1][q];
-        xin[k] = din[k];
-        xrec[k] = srec[k];
+        for (int q = 0; q < 5; q++) xs[k - K0][q] = k == 0 ? T.w[kq[q]] : est[k - 1][q];
+        xin[k - K0] = din[k];
+        xrec[k - K0] = srec[k];
       }
+      auto trunk_index = [](int q) { return NK + (kTE || q < e ? q : q - 1); };
 #pragma unroll
       for (int q = 0; q < P; q++) {
+        if (!kTE && q == e) continue;
         const int fk[5] = {fld_x(P, q), fld_y(P, q), fld_vx(P, q), fld_vy(P, q), fld_rot(P, q)};
+        const int i = trunk_index(q);
 #pragma unroll
-        for (int u5 = 0; u5 < 5; u5++) xs[KW + q][u5] = T.w[fk[u5]];
-        xin[KW + q] = (row >> (8 * q)) & 0xffu;
-        xrec[KW + q] = make_input_rec(xin[KW + q]);
+        for (int u5 = 0; u5 < 5; u5++) xs[i][u5] = T.w[fk[u5]];
+        xin[i] = (row >> (8 * q)) & 0xffu;
+        xrec[i] = make_input_rec(xin[i]);
       }
       if constexpr (kLean) {
         advance_players_rec<NS>(xs, xrec, sck);
@@ -542,16 +564,17 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
         for (int i = 0; i < NS; i++) adv(xs[i], xin[i]);
       }
 #pragma unroll
-      for (int k = 0; k < KW; k++)
+      for (int k = K0; k < K1; k++)
 #pragma unroll
-        for (int q = 0; q < 5; q++) est[k][q] = xs[k][q];
-      BoxState<P> Tn;
+        for (int q = 0; q < 5; q++) est[k][q] = xs[k - K0][q];
+      BoxState<P> Tn = T;  // (!kTE: the enumerated player's fields stay stale, never read)
       Tn.w[0] = (uint32_t)(f_c + 1);
 #pragma unroll
       for (int q = 0; q < P; q++) {
+        if (!kTE && q == e) continue;
         const int fk[5] = {fld_x(P, q), fld_y(P, q), fld_vx(P, q), fld_vy(P, q), fld_rot(P, q)};
 #pragma unroll
-        for (int u5 = 0; u5 < 5; u5++) Tn.w[fk[u5]] = xs[KW + q][u5];
+        for (int u5 = 0; u5 < 5; u5++) Tn.w[fk[u5]] = xs[trunk_index(q)][u5];
       }
       uint32_t c1, c2;
       common_sums(Tn, c1, c2);
@@ -598,11 +621,27 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
       }
       T = Tn;
     };
-    const int32_t steady0 = W - 1 < n ? W - 1 : n;  // first super-step with every stage active
-    int32_t u = 0;
-    for (; u < steady0; ++u) super_step(u, std::true_type());
-    for (; u < n; ++u) super_step(u, std::false_type());
-    for (; u < n + W - 1; ++u) super_step(u, std::true_type());
+    using Z = std::integral_constant<int, 0>;
+    using KWc = std::integral_constant<int, KW>;
+    if (WT > 0 && n >= W - 1) {
+      // compile-time W, a full ramp: super-step u < W - 1 steps stages [0, u + 1), drain super-step
+      // n + j stages [j + 1, W) without the trunk's enumerated player
+      static_for<(WT > 0 ? WT - 1 : 0)>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        super_step(j, std::true_type(), Z(), std::integral_constant<int, j + 1>(), std::true_type());
+      });
+      for (int32_t u = W - 1; u < n; ++u) super_step(u, std::false_type(), Z(), KWc(), std::true_type());
+      static_for<(WT > 0 ? WT - 1 : 0)>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        super_step(n + j, std::true_type(), std::integral_constant<int, j + 1>(), KWc(), std::false_type());
+      });
+    } else {
+      const int32_t steady0 = W - 1 < n ? W - 1 : n;  // first super-step with every stage active
+      int32_t u = 0;
+      for (; u < steady0; ++u) super_step(u, std::true_type(), Z(), KWc(), std::true_type());
+      for (; u < n; ++u) super_step(u, std::false_type(), Z(), KWc(), std::true_type());
+      for (; u < n + W - 1; ++u) super_step(u, std::true_type(), Z(), KWc(), std::true_type());
+    }
   };
   if (lean_ok) run(std::true_type());
   else run(std::false_type());

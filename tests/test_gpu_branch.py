@@ -209,6 +209,39 @@ def test_prefix_rounds_equal_full_rounds(oracle, S, B, A, P, mask, W):
             assert ck == int(cks[k]) and bytes(got) == bytes(states[k]), (lane, k)
 
 
+@pytest.mark.parametrize("splits", [(3, 1, 3), (4, 2, 8), (1, 1, 1, 5)])
+def test_prefix_pipe_ramp_forms(splits):
+    """The pipelined prefix kernel at W = 4 (compile-time W: a launch of n >= W - 1 rounds steps
+    only the stages that hold a round in its ramp and drain, shorter launches take the guarded
+    form): launches of n = W - 1 exactly, fewer and more rounds leave every trunk, report and
+    sampled cell as per-round speculate + confirm."""
+    from ggrs_amd import BranchEngine, synth
+    S, B, A, P, mask, W = 3, 16 ** 3, 16, 2, 0b10, 4
+    n = sum(splits)
+    truth = synth.gen_inputs(21, S, 2 * n + W + 3, P, synth.MODEL_HELD)
+    engs = {f: BranchEngine(S, num_players=P, remote_mask=mask, window=W, branches=B, alphabet=A)
+            for f in ("fused", "per_round")}
+    for f, e in engs.items():
+        e.add_inputs(0, truth)
+        e.set_round_form(f)
+        for k in splits:
+            e.rounds(k)
+        e.synchronize()
+    a, b = engs["fused"], engs["per_round"]
+    assert a.trunk_frame() == b.trunk_frame() == n
+    ra, rb = a.report(), b.report()
+    assert (ra[0] == rb[0]).all() and (ra[1] == rb[1]).all()
+    assert (a.desync() == b.desync()).all()
+    for s in range(S):
+        assert bytes(a.trunk(s)) == bytes(b.trunk(s)), s
+    rng = np.random.default_rng(9)
+    L = S * B
+    for lane in sorted(set([0, 1, A, B - 1, L - 1] + rng.integers(0, L, 16).tolist())):
+        for fr in range(n - 1, n + W):
+            x, y = a.lane_state(lane, fr), b.lane_state(lane, fr)
+            assert x[0] == y[0] and bytes(x[1]) == bytes(y[1]), (lane, fr)
+
+
 def test_config3_fused_rounds_full_size(oracle):
     """Config 3 through the bench's path (fused prefix-shared rounds): 16 rounds, then sampled
     lanes of the last window against the oracle's replay, the trunk and the survivor count."""
