@@ -501,6 +501,10 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
 #pragma unroll
       for (int q = 0; q < 5; q++) est[k][q] = 0u;
     int32_t slot = p.f_c % p.R;
+    // the confirmed row of super-step u, read one super-step ahead (its LDS latency behind the
+    // previous super-step's steps rather than in front of this one's trunk replay)
+    const int32_t last_row = n + W - 2;
+    uint32_t row_next = lds_rows[ls];
     const SincosConsts sck = sincos_consts_vgpr();
     // one super-step; kGuard: some stage belongs to no round of this launch (ramp / drain).  Only
     // stages [K0, K1) are stepped (the ramp and drain of a compile-time W step just the stages that
@@ -513,7 +517,8 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
       constexpr bool kTE = decltype(te_c)::value;
       auto active = [&](int k) { return k >= K0 && k < K1 && (!kGuard || (k < W && u - k >= 0 && u - k < n)); };
       const int32_t f_c = p.f_c + u;  // round u's trunk frame; every save is frame f_c + 1
-      const uint32_t row = lds_rows[u * ns + ls];
+      const uint32_t row = row_next;
+      row_next = lds_rows[min(u + 1, last_row) * ns + ls];
       slot = slot + 1 == p.R ? 0 : slot + 1;
       if (active(0)) {
         // speculate_kernel's check of round u - 1's survivors: their depth-0 enumerated player
