@@ -207,6 +207,129 @@ BRANCH_CONFIGS = {
 }
 
 
+class _StubReportEngine:
+    """A CPU stand-in for BranchEngine's report interface (launch-selftest only): the exchange leg's
+    collective path and record shape checked without a GPU.  Round r's report is a deterministic
+    function of (session group, r), so peer replicas agree and the desync count must be 0."""
+
+    def __init__(self, group, S=64, L=1024):
+        import numpy as np
+        self.np = np
+        self.group, self.num_sessions, self.num_lanes = group, S, L
+        self.report_bytes = ((2 * S + 7) & ~7) + 8 * ((L + 63) // 64)
+        self.r = 0
+
+    def trunk_frame(self):
+        return self.r
+
+    def round_to_tensor(self, t):
+        import torch
+        v = (self.np.arange(self.report_bytes, dtype=self.np.uint32) * 7 + self.r * 13 + self.group) & 0xFF
+        t.copy_(torch.from_numpy(v.astype(self.np.uint8)))
+        self.r += 1
+
+    def rounds(self, n):
+        self.r += n
+
+    def synchronize(self):
+        pass
+
+
+def exchange_leg(torch, dist, make_engine, rounds, batch, gpu):
+    """The config-4 report exchange across the ranks of the current process group (SURVEY.md 8e,
+    the analogue of the ChecksumReport send/receive, p2p_session.rs:904-975 and
+    protocol.rs:692-698): `rounds` rounds with one stream-ordered all-gather of `batch` rounds'
+    reports (exchange.ReportExchange, peers on when the world size is even: rank r and r + world/2
+    run the same sessions and compare checksums on the device), then the same rounds with no
+    exchange, then the all-gather alone on the same buffers.  Max over ranks of each span.
+    Returns the line's `exchange` record."""
+    from ggrs_amd import exchange
+    world, rank = dist.get_world_size(), dist.get_rank()
+    peers = world >= 2 and world % 2 == 0
+    group = rank % (world // 2) if peers else rank
+    eng = make_engine(group)
+
+    def sync():
+        eng.synchronize()
+        if gpu:
+            torch.cuda.synchronize()
+        dist.barrier()
+
+    def span(fn):
+        sync()
+        t0 = time.perf_counter()
+        fn()
+        sync()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda" if gpu else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    ex = exchange.ReportExchange(eng, peers=peers, batch=batch)
+    ex.run(batch)  # warm-up batch (the communicator's first collective included)
+    ex.drain()
+
+    def with_exchange():
+        ex.run(rounds)
+        ex.drain()
+    t_ex = span(with_exchange)
+
+    def without():
+        for _ in range(rounds // batch):
+            eng.rounds(batch)
+        if rounds % batch:
+            eng.rounds(rounds % batch)
+    t_plain = span(without)
+    n_ag = max(1, rounds // batch)
+    buf, out = ex.bufs[0], ex.gathered[0]
+
+    def gathers():
+        for _ in range(n_ag):
+            if gpu:
+                dist.all_gather_into_tensor(out.view(-1), buf.view(-1))
+            else:
+                dist.all_gather(list(out.unbind(0)), buf)
+    stream = ex.stream if ex.stream is not None else None
+    if stream is not None:
+        with torch.cuda.stream(stream):
+            t_ag = span(gathers)
+    else:
+        t_ag = span(gathers)
+    cnt = ex.desync_count.detach().clone().to("cuda" if gpu else "cpu").reshape(1)
+    dist.all_reduce(cnt)
+    gathered_bytes = world * batch * eng.report_bytes
+    return {
+        "what": "config-4 batched ReportExchange after the timed region (not in value): per rank "
+                f"{eng.num_sessions} sessions x {eng.num_lanes // eng.num_sessions} branches, one "
+                f"all-gather of {batch} rounds' reports (checksums + survival bits)"
+                + (", peer ranks r and r + world/2 compare checksums" if peers else ""),
+        "world_size": world, "backend": dist.get_backend(), "peers": peers,
+        "engine": type(eng).__name__,
+        "rounds": rounds, "batch": batch, "allgathers": n_ag,
+        "us_per_round_with_allgather": round(t_ex / rounds * 1e6, 3),
+        "us_per_round_without_allgather": round(t_plain / rounds * 1e6, 3),
+        "report_bytes_per_round_per_rank": eng.report_bytes,
+        "gathered_bytes_per_allgather": gathered_bytes,
+        "us_per_allgather_alone": round(t_ag / n_ag * 1e6, 3),
+        "allgather_bytes_per_s": round(gathered_bytes * n_ag / t_ag, 1),
+        "desyncs": int(cnt.item()),
+    }
+
+
+def branch_exchange_engine(torch, local_rank, rounds):
+    """The config-4 branch engine of rank group g (the sessions it shards), for exchange_leg."""
+    from ggrs_amd import BranchEngine, synth
+    c = BRANCH_CONFIGS[4]
+    S, B, P, W = c["sessions"], c["branches"], c["players"], c["window"]
+
+    def make(group):
+        truth = synth.gen_inputs(group * S, S, rounds + W + 2, P, synth.MODEL_HELD)
+        eng = BranchEngine(S, num_players=P, remote_mask=c["remote_mask"], window=W, branches=B, alphabet=16,
+                           input_capacity=rounds + W + 4, device=local_rank)
+        eng.add_inputs(0, truth)
+        return eng
+    return make
+
+
 def run_branch(args):
     world, rank, local_rank, torch, dist = setup_dist(args)
     from ggrs_amd import BranchEngine, exchange, synth
@@ -399,13 +522,17 @@ def run_particles(args):
 
 def run_p2p(args):
     """P2P rollback decision on the device (ggrs_p2p_*): S sessions of one peer, 2 players (one
-    remote, inputs arrive 4 frames late), max_prediction 8, held-key inputs.  One step = 64
-    advance_frame calls on every session: poll, misprediction check, rollback + resimulation
-    where the session's prediction failed, save, advance."""
+    remote, inputs arrive --latency frames late, default 4), --max-prediction (default 8),
+    repeat-last prediction, held-key inputs.  One step = 64 advance_frame calls on every session:
+    poll, misprediction check, rollback + resimulation where the session's prediction failed, save,
+    advance.  BASELINE config 2's P2P form: --sessions 4096 --latency 8 --max-prediction 9."""
     world, rank, local_rank, torch, dist = setup_dist(args)
     from ggrs_amd import P2PEngine, synth
     S = args.sessions or 65536
-    P, D, maxp, calls = 2, 4, 8, 64
+    P, D, maxp, calls = 2, args.latency, args.max_prediction, 64
+    if not 0 <= D <= maxp:
+        raise SystemExit(f"--latency {D} must be in 0..--max-prediction {maxp} (p2p_session.rs:296-310: "
+                         "a session cannot run further ahead of its confirmed inputs)")
     frames = (args.warmup + args.steps) * calls
     # --peers: rank r and rank r + world/2 are the two machines of the same matches (local player
     # 0 on one, 1 on the other, the same inputs); their checksum reports (desync detection,
@@ -465,9 +592,10 @@ def run_p2p(args):
     # HBM bytes per launch: the state in/out, every save (state + checksum), every rollback load,
     # the queue words in/out and the input rows each call reads (arrival + its own, + replays)
     # (sparse saving: about one save per call, at min_confirmed, and replays save nothing)
-    replay_saves = 0 if args.sparse else (D - 1) * (4 * F + 2)
+    # every replayed frame but the first is saved (p2p_session.rs:690-711)
+    replay_saves = 0 if args.sparse else (resim - rollbacks) // args.steps * (4 * F + 2)
     bytes_launch = (2 * 4 * F * S + (session_calls // args.steps) * (4 * F + 2) * 1
-                    + (rollbacks // args.steps) * (4 * F + replay_saves)
+                    + (rollbacks // args.steps) * 4 * F + replay_saves
                     + 2 * 16 * P * S + (session_calls // args.steps) * 2 * 2 + (resim // args.steps) * 2 * 2)
     avg_s = kernel_ms / 1e3 / max(launches, 1)
     achieved = bytes_launch / avg_s / 1e9
@@ -500,10 +628,14 @@ def run_p2p(args):
                                       + (f", peer ranks exchange checksum reports over {dist.get_backend()}" if peers else "")},
             "dist": dist_info(dist, per_rank),
             "rollbacks_per_session_frame": round(rollbacks / session_calls, 5),
+            # the replayed AdvanceFrames the sessions actually executed (p2p_session.rs:690-711)
+            "resimulated_session_frames_per_s": round(resim * world / elapsed, 1),
+            "resimulated_per_session_frame": round(resim / session_calls, 5),
             "advances_per_sec": round((session_calls + resim) * world / elapsed, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                         "traffic": pmc_traffic(f"p2p_s{S}" + ("_sparse" if args.sparse else "")),
+                         "traffic": pmc_traffic(f"p2p_s{S}" + ("" if (D, maxp) == (4, 8) else f"_d{D}_m{maxp}")
+                                               + ("_sparse" if args.sparse else "")),
                          "algorithmic_bytes_per_launch": bytes_launch,
                          "avg_launch_ms": round(avg_s * 1e3, 4)},
             "cpu_baseline": cpu_baseline, "parity": parity,
@@ -1033,10 +1165,11 @@ def run_launch_selftest(args):
     me =torch.tensor([rank, int(os.environ.get("LOCAL_RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))])
     out = [torch.empty_like(me) for _ in range(dist.get_world_size())]
     dist.all_gather(out, me)
+    xleg = exchange_leg(torch, dist, lambda g: _StubReportEngine(g), 24, 8, False)
     if rank == 0:
         print(json.dumps({"metric": "launch-selftest", "value": dist.get_world_size(), "n_gpus": dist.get_world_size(),
                           "ranks": [o.tolist() for o in out],
-                          "master_addr": os.environ.get("MASTER_ADDR")}))
+                          "master_addr": os.environ.get("MASTER_ADDR"), "exchange": xleg}))
     dist.destroy_process_group()
 
 
@@ -1062,12 +1195,20 @@ def main():
     ap.add_argument("--exchange-batch", type=int, default=0,
                     help="configs 3/4 across ranks: rounds per report all-gather (1 = one per confirmation; "
                          "0 = --rounds-per-step, one all-gather per step)")
+    ap.add_argument("--no-exchange-leg", action="store_true",
+                    help="config 2 across ranks: skip the config-4 report all-gather leg (the line's exchange key)")
+    ap.add_argument("--exchange-rounds", type=int, default=256,
+                    help="config 2 across ranks: rounds of the exchange leg (gloo: at most 32)")
+    ap.add_argument("--exchange-leg-batch", type=int, default=16,
+                    help="config 2 across ranks: rounds per all-gather in the exchange leg")
     ap.add_argument("--peers", action="store_true",
                     help="configs 3/4 and p2p: rank r and r + world/2 run the same sessions (the two "
                          "machines of a match) and compare checksums exchanged over the process group")
     ap.add_argument("--p2p-form", choices=["default", "flat", "lockstep", "unstaged"], default="default",
                     help="p2p: kernel form (DESIGN.md section 3)")
     ap.add_argument("--sparse", action="store_true", help="p2p: sparse saving (SURVEY.md 8f row 4)")
+    ap.add_argument("--latency", type=int, default=4, help="p2p: frames the remote player's inputs arrive late")
+    ap.add_argument("--max-prediction", type=int, default=8, help="p2p: max_prediction (builder.rs:130-147)")
     ap.add_argument("--req-form", choices=["native", "p2p", "batch", "lanes", "lockstep"], default="native",
                     help="requests: the boundary form (run_requests docstring)")
     ap.add_argument("--codec-layout", choices=["chunked", "strided"], default="chunked",
@@ -1208,6 +1349,15 @@ def main():
         except Exception as exc:  # the oracle is optional on the measurement path
             parity = {"error": repr(exc)}
 
+    xleg = None
+    if dist is not None and not args.no_exchange_leg:
+        # the one collective the north star names, measured beside (not inside) the headline:
+        # the config-4 report all-gather across this run's ranks
+        gpu = dist.get_backend() != "gloo"
+        n = args.exchange_rounds if gpu else min(args.exchange_rounds, 32)
+        xleg = exchange_leg(torch, dist, branch_exchange_engine(torch, local_rank, 2 * n + 32), n,
+                            args.exchange_leg_batch, gpu)
+
     if rank == 0:
         line = {
             "metric": "resimulated session-frames/sec (node)",
@@ -1235,6 +1385,8 @@ def main():
             "halted_lanes": halted,
             "parity": parity,
         }
+        if xleg is not None:
+            line["exchange"] = xleg
         print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()

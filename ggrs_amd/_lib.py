@@ -42,7 +42,7 @@ EXPORTS = (
     "ggrs_branch_report_bytes", "ggrs_branch_synchronize", "ggrs_branch_trunk_frame",
     "ggrs_branch_read_report", "ggrs_branch_read_desync", "ggrs_branch_read_trunk",
     "ggrs_branch_read_lane", "ggrs_branch_timing_reset", "ggrs_branch_timing_stop", "ggrs_branch_timing_read",
-    "ggrs_branch_rounds", "ggrs_branch_set_round_launches", "ggrs_branch_set_stream",
+    "ggrs_branch_rounds", "ggrs_branch_set_round_launches", "ggrs_branch_set_stream", "ggrs_branch_use_own_stream",
     "ggrs_branch_round", "ggrs_branch_rounds_reports", "ggrs_branch_compare_peer", "ggrs_branch_compare_peer_rows",
     "ggrs_particle_engine_create", "ggrs_particle_engine_destroy", "ggrs_particle_add_local_inputs",
     "ggrs_particle_synctest_advance_frames", "ggrs_particle_synchronize",

@@ -56,6 +56,7 @@ def _bind(L):
     L.ggrs_branch_rounds.argtypes = [vp, ctypes.c_int32]
     L.ggrs_branch_set_round_launches.argtypes = [vp, ctypes.c_int32]
     L.ggrs_branch_set_stream.argtypes = [vp, vp]
+    L.ggrs_branch_use_own_stream.argtypes = [vp]
     L.ggrs_branch_round.argtypes = [vp, vp]
     i32 = ctypes.c_int32
     L.ggrs_branch_compare_peer.argtypes = [vp, vp, i32, i32, i32, i32, vp, vp]
@@ -118,8 +119,13 @@ class BranchEngine:
 
     def set_stream(self, stream_ptr):
         """Enqueue all work on this hipStream_t (an int handle, e.g. torch.cuda.current_stream()
-        .cuda_stream; None or 0 = the engine's own stream)."""
+        .cuda_stream; 0 or None = HIP's null stream, which is what torch's default stream reports).
+        Work queued before the switch is ordered before work queued after it."""
         _lib.check(self._L.ggrs_branch_set_stream(self._h, ctypes.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def use_own_stream(self):
+        """Back to the engine's own non-blocking stream (the one it was created with)."""
+        _lib.check(self._L.ggrs_branch_use_own_stream(self._h))
 
     def confirm_to_tensor(self, t):
         """confirm() with the round's report written into torch uint8 tensor `t`: a device tensor

@@ -41,25 +41,30 @@ def needs_build():
     return any(os.path.getmtime(f) > t for f in SOURCES + HEADERS + [os.path.abspath(__file__)])
 
 
-def _compile(src, extra, verbose, obj_dir=OBJ):
+def _compile(src, extra, verbose, obj_dir=OBJ, csrc=CSRC):
     obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
-    cmd = [HIPCC, *FLAGS, *UNIT_FLAGS.get(os.path.basename(src), []), *extra, "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-c", "-o", obj, src]
+    cmd = [HIPCC, *FLAGS, *UNIT_FLAGS.get(os.path.basename(src), []), *extra, "-I", os.path.join(ROOT, "include"), "-I", csrc, "-c", "-o", obj, src]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     return obj
 
 
-def build(force=False, verbose=False, out=LIB, extra=()):
+def build(force=False, verbose=False, out=LIB, extra=(), csrc=CSRC):
     """Compile every unit for gfx950 and link `out` (default: the product library).  `extra`
-    flags are for experiment builds only (tools/exp_build.sh), which write elsewhere."""
+    flags and another source directory `csrc` are for experiment builds only
+    (tools/exp_build.sh: a scratch copy of csrc/ with tools/exp/*.patch applied), which write
+    elsewhere."""
+    if csrc != CSRC and out == LIB:
+        raise ValueError("an experiment source tree must not overwrite the product library")
     if out == LIB and not extra and not force and not needs_build():
         return LIB
     obj_dir = OBJ if out == LIB else out + ".obj"  # experiment builds keep their own objects
     os.makedirs(obj_dir, exist_ok=True)
     jobs = min(len(SOURCES), max(1, os.cpu_count() or 1), 16)
+    srcs = [os.path.join(csrc, f) for f in UNITS]
     with ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, list(extra), verbose, obj_dir), SOURCES))
+        objs = list(ex.map(lambda s: _compile(s, list(extra), verbose, obj_dir, csrc), srcs))
     cmd = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out + ".tmp", *objs]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

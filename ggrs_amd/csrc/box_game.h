@@ -219,7 +219,6 @@ __device__ inline void advance_player_lean_sc(float& x, float& y, float& vx, flo
   // the clamp is rare (a few % of player steps): a wave-uniform test skips it with one branch on
   // VCC instead of an exec-mask save / restore around it on every step
   const bool clamp = mag2 > kMaxSpeed * kMaxSpeed;
-#ifndef GGRS_EXP_NOCLAMP  // timing experiments only (tools/exp_build.sh): results then differ
   if (__builtin_expect(__builtin_amdgcn_ballot_w64(clamp) != 0, 0)) {
     if (clamp) {
       const float magnitude = sqrt_rn_above_49(mag2);
@@ -228,9 +227,6 @@ __device__ inline void advance_player_lean_sc(float& x, float& y, float& vx, flo
       vel.y = (float)((double)(vel.y * kMaxSpeed) * rr);
     }
   }
-#else
-  (void)clamp;
-#endif
   const ggrs_f2 pos = ggrs_f2{x, y} + vel;
   x = __builtin_amdgcn_fmed3f(pos.x, 0.0f, kWindowWidth);
   y = __builtin_amdgcn_fmed3f(pos.y, 0.0f, kWindowHeight);
@@ -374,9 +370,6 @@ __device__ inline void advance_players_lean(uint32_t (&v)[N][5], const uint32_t 
     any = any || mag2[i] > kMaxSpeed * kMaxSpeed;
     vel[i] = ve;
   }
-#ifdef GGRS_EXP_NOCLAMP  // timing experiments only (tools/exp_build.sh): results then differ
-  any = false;
-#endif
   if (__builtin_expect(__builtin_amdgcn_ballot_w64(any) != 0, 0)) {
 #pragma unroll
     for (int i = 0; i < N; i++) {

@@ -391,9 +391,6 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
   const int64_t s = in_range ? lane / p.B : s_first;
   const int32_t b = in_range ? (int32_t)(lane - s * p.B) : 0;
   const int ls = (int)(s - s_first);
-#ifdef GGRS_EXP_STAMPS  // timing experiment only: phase stamps printed by two waves
-  const uint64_t ts0 = __builtin_amdgcn_s_memtime();
-#endif
   // the prologue's global reads issued together (one memory latency): the lane's trunk, the
   // survivor bit and cell checksum of the first round's check, the launch's input rows
   BoxState<P> T;  // the trunk of the lane's session at frame f_c + u (every lane holds its own copy)
@@ -412,9 +409,6 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
     }
   }
   __syncthreads();
-#ifdef GGRS_EXP_STAMPS
-  const uint64_t ts1 = __builtin_amdgcn_s_memtime();
-#endif
   bool survived = p.check_prev && in_range && ((prev_bits >> (lane & 63)) & 1ull);
   const bool check0 = p.check_prev && survived;
   const uint16_t mine0 = check0 ? cell0 : (uint16_t)0;
@@ -650,12 +644,6 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
   };
   if (lean_ok) run(std::true_type());
   else run(std::false_type());
-#ifdef GGRS_EXP_STAMPS
-  const uint64_t ts2 = __builtin_amdgcn_s_memtime();
-  if ((threadIdx.x & 63) == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1))
-    printf("PSTAMPS block %d wave %d prologue %llu loop %llu\n", (int)blockIdx.x, (int)(threadIdx.x >> 6),
-           (unsigned long long)(ts1 - ts0), (unsigned long long)(ts2 - ts1));
-#endif
 }
 
 // compare_local_checksums_against_peers (p2p_session.rs:904-937) over an all-gathered report
@@ -750,7 +738,7 @@ extern "C" {
 int ggrs_branch_engine_destroy(ggrs_branch_engine_t* e) {
   if (!e) return GGRS_OK;
   (void)hipSetDevice(e->cfg.device);
-  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  if (e->own_stream) (void)hipStreamSynchronize(e->stream);  // the current stream, the null stream too
   void* bufs[] = {e->trunk, e->trunk_alt, e->ring, e->ring_ck, e->inputs, e->report, e->prev_bits, e->desync, e->staging};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -1195,20 +1183,34 @@ int ggrs_branch_compare_peer_rows(ggrs_branch_engine_t* e, const void* gathered,
   return GGRS_OK;
 }
 
-int ggrs_branch_set_stream(ggrs_branch_engine_t* e, void* stream) {
-  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+namespace {
+// Every launch and copy from now on goes to `s`; work already queued on the old stream comes first
+// (the new stream waits for it on the device).
+int switch_stream(ggrs_branch_engine_t* e, hipStream_t s) {
   HIP_TRY(hipSetDevice(e->cfg.device));
-  hipStream_t s = stream ? (hipStream_t)stream : e->own_stream;
   if (s == e->stream) return GGRS_OK;
-  // work already queued on the old stream comes first: the new stream waits for it on the device
+  if (e->timer.collecting) return set_error(GGRS_E_STATE, "cannot switch streams while timing a span");
   hipEvent_t ev;
   HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   HIP_TRY(hipEventRecord(ev, e->stream));
   HIP_TRY(hipStreamWaitEvent(s, ev, 0));
   HIP_TRY(hipEventDestroy(ev));
-  if (e->timer.collecting) return set_error(GGRS_E_STATE, "cannot switch streams while timing a span");
   e->stream = s;
   return GGRS_OK;
+}
+}  // namespace
+
+// NULL is HIP's null stream (what torch.cuda.current_stream() reports as handle 0), not the engine's
+// own stream: the own stream is non-blocking, so mapping NULL to it left a caller on the null stream
+// unordered with the engine's launches (ABI 2; ggrs_branch_use_own_stream selects it explicitly).
+int ggrs_branch_set_stream(ggrs_branch_engine_t* e, void* stream) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  return switch_stream(e, (hipStream_t)stream);
+}
+
+int ggrs_branch_use_own_stream(ggrs_branch_engine_t* e) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  return switch_stream(e, e->own_stream);
 }
 
 int ggrs_branch_set_round_launches(ggrs_branch_engine_t* e, int32_t on) {

@@ -635,14 +635,6 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
   __shared__ uint4 lds_rec[(kStage5 + 1) * ROW];
   __shared__ uint16_t lds_first[CD * SPW];
   __shared__ __attribute__((aligned(16))) uint8_t lds_stash[2 * kB * kSlot];  // slots, then the dump
-#ifdef GGRS_EXP_STAMPS  // timing experiment only: phase stamps printed by two blocks
-  uint64_t ts[8];
-  int nts = 0;
-  ts[nts++] = __builtin_amdgcn_s_memtime();
-#define GGRS_STAMP() (ts[nts++] = __builtin_amdgcn_s_memtime())
-#else
-#define GGRS_STAMP() ((void)0)
-#endif
   const int wl = threadIdx.x;
   const int R = p.R;
   const int g = wl / G, r = wl - g * G;
@@ -764,7 +756,6 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
       checkpoint_sessions(m, piece, s0, nsess, wl, kWave);
     }
   }
-  GGRS_STAMP();
   if (failed_f0 >= 0) return;
   if (wl < CD * nsess) {
     const int gg = wl / nsess, ss = wl - gg * nsess;
@@ -789,7 +780,6 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
   wave_lds_sync();
-  GGRS_STAMP();
 
   uint64_t bad = 0;
   uint32_t pend_ck = 0, pend_first = 0;
@@ -855,9 +845,6 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
           const uint32_t nb = Pp == 2 ? (uint32_t)__builtin_amdgcn_update_dpp((int)rb, (int)rb, 0x112, 0xF, 0xF, false)
                                       : (uint32_t)__builtin_amdgcn_ds_bpermute(src_rot, (int)rb);
           glibc_sincosf_domain_raw(__builtin_bit_cast(float, nb), &sc_s, &sc_c, &sc_qs, &sc_qc);
-#ifdef GGRS_EXP_PIN
-          asm volatile("" ::"v"(sc_s), "v"(sc_c));
-#endif
         });
       } else {
         advance_player(x, y, vx, vy, rot, (uint32_t)in);
@@ -1032,7 +1019,6 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
     // core blocks of 8 steps + their batch, aligned to the batch grid
     for (; t < core_end && ((t - p.f0) & (kB - 1)) != 0; ++t) general(t);
   }
-  GGRS_STAMP();
   if (t + kB <= core_end) {
     bad |= __ballot(pend_ck != pend_first) & pend_lanes;
     pend_ck = pend_first = 0;
@@ -1050,7 +1036,6 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
     }
     bad |= __ballot(acc != 0) & cmp_lanes;
   }
-  GGRS_STAMP();
   if (edge_ok) {
     edge_block(t, t_end - t);  // the last cd - 1 steps and their batch
   } else {
@@ -1060,14 +1045,6 @@ __global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams
   }
   bad |= __ballot(pend_ck != pend_first) & pend_lanes;
   if (bad && wl == __builtin_ctzll(bad)) atomicCAS(p.fail_f0, -1, p.f0);
-#ifdef GGRS_EXP_STAMPS
-  GGRS_STAMP();
-  if (wl == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1))
-    printf("STAMPS block %d ckpt %llu loads %llu ramp %llu core %llu tail %llu\n", (int)blockIdx.x,
-           (unsigned long long)(ts[1] - ts[0]), (unsigned long long)(ts[2] - ts[1]), (unsigned long long)(ts[3] - ts[2]),
-           (unsigned long long)(ts[4] - ts[3]), (unsigned long long)(ts[5] - ts[4]));
-#endif
-#undef GGRS_STAMP
 }
 
 struct RequestParams {

@@ -785,6 +785,7 @@ __global__ void init_queue_kernel(int32_t* queue, int64_t n_per_field, int32_t P
 struct ggrs_p2p_engine {
   ggrs_p2p_config_t cfg{};
   int Pp = 1, F = 1, R = 2, cap = 256;
+  int num_cus = 256;                 // the device's CUs (LDS-ring occupancy rule)
   hipStream_t stream = nullptr;
   uint32_t* cur = nullptr;
   uint32_t* ring = nullptr;
@@ -936,6 +937,8 @@ int ggrs_p2p_engine_create(const ggrs_p2p_config_t* cfg, ggrs_p2p_engine_t** out
   const int P = c.num_players;
   CTRY(hipSetDevice(c.device));
   CTRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+  CTRY(hipDeviceGetAttribute(&e->num_cus, hipDeviceAttributeMultiprocessorCount, c.device));
+  if (e->num_cus < 1) e->num_cus = 1;
   if (e->timer.create()) return fail(GGRS_E_HIP);
   CTRY(hipMalloc(&e->cur, sizeof(uint32_t) * e->F * S));
   CTRY(hipMalloc(&e->ring, sizeof(uint32_t) * (size_t)e->R * cell_dwords(P) * S));
@@ -1067,9 +1070,16 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
       constexpr int P = decltype(PC)::value;
       if (flat) {
         const dim3 grid((unsigned)grid_of(p.S, kFlatBlock));
-        // the LDS ring when the block's rings fit 28 KB and a stage of rows holds a call's reach
+        // the LDS ring when a stage of rows holds a call's reach and the block's rings fit: 28 KB
+        // (four blocks, one per SIMD, in a CU's 160 KB beside 12 KB of rows each), or more when the
+        // grid puts fewer blocks on each CU (config 2's P2P shape: 4096 sessions = 64 blocks, R = 10:
+        // 30 KB of rings)
         const size_t ring_lds = (size_t)e->R * (cell_dwords(P) / 4) * kFlatBlock * 16;
-        const bool lds = e->form != 3 && ring_lds <= 28 * 1024 && back + 1 <= flat_rows_lds<P>() - 1;
+        const size_t rows_lds = (size_t)flat_rows_lds<P>() * kFlatBlock * (P <= 1 ? 1 : (P == 2 ? 2 : 4));
+        const int64_t per_cu = (grid.x + e->num_cus - 1) / e->num_cus;
+        const bool fits = ring_lds <= 28 * 1024 ||
+                          (ring_lds + rows_lds <= 64 * 1024 && per_cu * (int64_t)(ring_lds + rows_lds) <= 160 * 1024);
+        const bool lds = e->form != 3 && fits && back + 1 <= flat_rows_lds<P>() - 1;
         auto go = [&](auto plain_tag, auto lds_tag) {
           constexpr bool kPl = decltype(plain_tag)::value;
           constexpr bool kL = decltype(lds_tag)::value;

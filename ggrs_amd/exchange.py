@@ -135,7 +135,8 @@ class ReportExchange:
     Works over RCCL (device tensors) and gloo (CPU tensors, for tests; gloo's wait blocks the
     host, and the comparison runs as torch ops on the host)."""
 
-    def __init__(self, engine, group=None, peers=False, keep_history=False, device=None, batch=1):
+    def __init__(self, engine, group=None, peers=False, keep_history=False, device=None, batch=1,
+                 dedicated_stream=True):
         import torch
         import torch.distributed as dist
         if batch < 1:
@@ -160,16 +161,20 @@ class ReportExchange:
         self.desync_count = torch.zeros((), dtype=torch.int64, device=dev)
         self.first_desync_round = torch.full((), -1, dtype=torch.int64, device=dev)
         self.history = [] if keep_history else None
-        # One dedicated stream carries the engine's rounds, the all-gathers' stream waits, the
-        # history copies and the comparisons.  The caller's current stream may be the null stream
-        # (handle 0), which set_stream reads as "the engine's own stream": the rounds would then
-        # be unordered with the all-gather that reads their reports (a gather could read the last
-        # round's row before the kernel wrote it).  It starts behind the caller's work so far.
+        # With dedicated_stream one stream of the exchange's own carries the engine's rounds, the
+        # all-gathers' stream waits, the history copies and the comparisons (it starts behind the
+        # caller's work so far); without it all of that runs on the caller's current stream, which
+        # may be the null stream (handle 0: ggrs_branch_set_stream binds the engine to HIP's null
+        # stream, ABI 3).  Either way the rounds that write a report are stream-ordered before the
+        # all-gather that reads it (RCCL's stream waits for the current stream).
         self.stream = None
         if self.nccl:
-            self.stream = torch.cuda.Stream(device=dev)
-            self.stream.wait_stream(torch.cuda.current_stream(dev))
-            engine.set_stream(self.stream.cuda_stream)
+            if dedicated_stream:
+                self.stream = torch.cuda.Stream(device=dev)
+                self.stream.wait_stream(torch.cuda.current_stream(dev))
+                engine.set_stream(self.stream.cuda_stream)
+            else:
+                engine.set_stream(torch.cuda.current_stream(dev).cuda_stream)
 
     def _on_stream(self):
         import contextlib

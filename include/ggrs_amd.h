@@ -50,7 +50,7 @@ extern "C" {
 
 /* 2: GGRS_PATH_* renumbered (2, 3 = the pipelined forms), lane batches submitted and waited for
  * separately, host-side lane encoding, branch round forms */
-#define GGRS_ABI_VERSION 2
+#define GGRS_ABI_VERSION 3
 
 #define GGRS_OK 0
 #define GGRS_E_INVALID (-1)      /* GgrsError::InvalidRequest: bad argument or configuration */
@@ -339,12 +339,17 @@ int ggrs_branch_rounds(ggrs_branch_engine_t* eng, int32_t n_rounds);
  * prefix, by branch b mod A^min(k+1, E); ggrs_branch_read_lane resolves a lane's cell to it), as
  * 2 n launches of speculate / confirm (on = 1), or as one launch without prefix sharing (on = 2) */
 int ggrs_branch_set_round_launches(ggrs_branch_engine_t* eng, int32_t on);
-/* Enqueue every launch and copy from now on on `stream` (a hipStream_t; NULL = the engine's own),
+/* Enqueue every launch and copy from now on on `stream` (a hipStream_t; NULL = HIP's null stream,
+ * as torch.cuda.current_stream() reports its default stream -- ABI 3; before it NULL meant the
+ * engine's own non-blocking stream, which does not order with the null stream),
  * e.g. the stream a collective library orders its all-gather after: speculate, confirm (with its
  * report copy) and the report exchange then follow each other on the device with no host
  * synchronisation (multi-GPU configs 3/4, ggrs_amd/exchange.py ReportExchange).  Work queued
  * before the switch is ordered before work queued after it. */
 int ggrs_branch_set_stream(ggrs_branch_engine_t* eng, void* stream);
+/* Back to the engine's own (non-blocking) stream, the one it was created with; work queued before
+ * the switch is ordered before work queued after it. */
+int ggrs_branch_use_own_stream(ggrs_branch_engine_t* eng);
 /* One round (speculate + confirm) as one launch; the round's report is also written to
  * report_device (device pointer, same layout as ggrs_branch_confirm's copy; NULL = none) by the
  * kernel itself -- the per-round call of the multi-GPU exchange loop. */

@@ -4,7 +4,7 @@
 #![allow(non_camel_case_types)]
 use std::os::raw::{c_char, c_void};
 
-pub const GGRS_ABI_VERSION: i32 = 2;
+pub const GGRS_ABI_VERSION: i32 = 3;
 
 pub const GGRS_OK: i32 = 0;
 pub const GGRS_E_INVALID: i32 = -1;
@@ -217,6 +217,7 @@ extern "C" {
     pub fn ggrs_branch_rounds(eng: *mut ggrs_branch_engine_t, n_rounds: i32) -> i32;
     pub fn ggrs_branch_set_round_launches(eng: *mut ggrs_branch_engine_t, on: i32) -> i32;
     pub fn ggrs_branch_set_stream(eng: *mut ggrs_branch_engine_t, stream: *mut c_void) -> i32;
+    pub fn ggrs_branch_use_own_stream(eng: *mut ggrs_branch_engine_t) -> i32;
     pub fn ggrs_branch_round(eng: *mut ggrs_branch_engine_t, report_device: *mut c_void) -> i32;
     pub fn ggrs_branch_rounds_reports(eng: *mut ggrs_branch_engine_t, n_rounds: i32, reports_device: *mut c_void) -> i32;
     pub fn ggrs_branch_compare_peer_rows(eng: *mut ggrs_branch_engine_t, gathered: *const c_void, world: i32,

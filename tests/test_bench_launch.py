@@ -65,3 +65,29 @@ def test_single_rank_runs_in_process():
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]  # gloo's banner aside
     d = json.loads(lines[-1])
     assert d["n_gpus"] == 1 and "launch" not in d
+
+
+EXCHANGE_KEYS = {"what", "world_size", "backend", "peers", "engine", "rounds", "batch", "allgathers",
+                 "us_per_round_with_allgather", "us_per_round_without_allgather", "report_bytes_per_round_per_rank",
+                 "gathered_bytes_per_allgather", "us_per_allgather_alone", "allgather_bytes_per_s", "desyncs"}
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_exchange_leg_record(n):
+    """The `exchange` key a multi-rank bench line carries: bench.exchange_leg
+    runs the batched ReportExchange across the ranks (here over gloo with a CPU report engine, on
+    the GPU box the config-4 BranchEngine over RCCL) and records the world size the process group
+    saw, per-round times with and without the all-gather, gathered bytes and the desync count."""
+    r = _run("--gpus", str(n))
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.strip()][0])
+    x = d["exchange"]
+    assert set(x) == EXCHANGE_KEYS
+    assert x["world_size"] == n and x["backend"] == "gloo"
+    assert x["peers"] == (n % 2 == 0)
+    assert x["rounds"] == 24 and x["batch"] == 8 and x["allgathers"] == 3
+    assert x["gathered_bytes_per_allgather"] == n * 8 * x["report_bytes_per_round_per_rank"]
+    assert x["desyncs"] == 0
+    for k in ("us_per_round_with_allgather", "us_per_round_without_allgather", "us_per_allgather_alone",
+              "allgather_bytes_per_s"):
+        assert x[k] > 0

@@ -153,3 +153,45 @@ def test_compare_peer_rows_kernel():
     e.compare_peer_rows(g, 3, 0, 1, 30, count, first)  # rows 0..2 of 5 per rank
     e.synchronize()
     assert int(count) == 1 and int(first) == 31
+
+
+def test_report_exchange_null_stream_world1_nccl(oracle):
+    """The engine bound to torch's current stream when that is the null stream (handle 0) and NO
+    dedicated exchange stream: ggrs_branch_set_stream(NULL) is HIP's null stream (ABI 3), so the
+    fused rounds that write each batch's reports are ordered before the RCCL all-gather that reads
+    them; the gathered reports equal an exchange-free engine's every round (protocol.rs:692-698:
+    the report sent is the saved cell's)."""
+    import torch.distributed as dist
+    from ggrs_amd import BranchEngine, exchange, synth
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(free_port())
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        assert torch.cuda.current_stream().cuda_stream == 0
+        S, B, P, W, rounds = 512, 16, 4, 8, 24
+        truth = synth.gen_inputs(5, S, rounds + W + 1, P, synth.MODEL_HELD)
+        engs = []
+        for _ in range(2):
+            e = BranchEngine(S, num_players=P, remote_mask=0b1110, window=W, branches=B, alphabet=16,
+                             input_capacity=rounds + W + 3)
+            e.add_inputs(0, truth)
+            engs.append(e)
+        ex = exchange.ReportExchange(engs[0], peers=False, keep_history=True, batch=4, dedicated_stream=False)
+        assert ex.stream is None
+        for n in (4, 3, 5, 8, 4):
+            ex.run(n)
+        ex.drain()
+        torch.cuda.synchronize()
+        assert [f for f, _ in ex.history] == list(range(rounds))
+        for f, g in ex.history:
+            engs[1].speculate()
+            engs[1].confirm()
+            ck, bits = engs[1].report()
+            got_ck, got_bits = exchange.split_report(g[0].cpu().numpy(), S, engs[0].num_lanes)
+            assert (got_ck == ck).all() and (got_bits == bits).all(), f
+        engs[0].use_own_stream()
+        engs[0].synchronize()
+        assert bytes(engs[0].trunk(0)) == bytes(engs[1].trunk(0))
+    finally:
+        dist.destroy_process_group()

@@ -199,3 +199,26 @@ def test_full_size_p2p_bench_config(oracle):
     check_against_oracle(eng, rows, sessions, frames, trace=False)
     rb, _ = eng.stats()
     assert rb.sum() > S  # rollbacks happen throughout
+
+
+@pytest.mark.parametrize("form", ["default", "flat"])
+def test_config2_p2p_shape(oracle, form):
+    """BASELINE config 2 in its P2P form: 4096 sessions, 2 players, the remote
+    player's inputs 8 frames late, max_prediction 9, repeat-last prediction
+    (input_queue.rs:128-161), held-key inputs, 64-call launches -- the shape `bench.py --workload
+    p2p --sessions 4096 --latency 8 --max-prediction 9` measures.  Sampled sessions' final state,
+    ring, trace and rollback/resimulation counts bit-exact against the oracle's P2PSession."""
+    from ggrs_amd import P2PEngine, synth
+    S, frames, P = 4096, 192, 2
+    rows = synth.gen_inputs(0, S, frames, P, synth.MODEL_HELD)
+    eng = P2PEngine(S, num_players=P, local_players=(0,), input_delay=0, max_prediction=9, remote_latency=8,
+                    input_capacity=frames + 10, trace_capacity=frames)
+    eng.set_kernel_form(form)
+    eng.add_inputs(0, rows)
+    for _ in range(frames // 64):
+        eng.advance_frames(64)
+    rng = np.random.default_rng(4)
+    sessions = sorted(set([0, 1, 63, 64, 2047, S - 1] + rng.integers(0, S, 10).tolist()))
+    check_against_oracle(eng, rows, sessions, frames)
+    rb, rs = eng.stats()
+    assert rb.sum() > 0 and rs.sum() >= 8 * rb.sum() - 8 * S  # rollbacks of up to 8 frames

@@ -1,0 +1,22 @@
+#!/bin/bash
+# Round 4 first check: the null-stream exchange test, config-2 P2P parity, the ABI test, then the
+# config-2 P2P bench line, the gloo 2-rank bench with its exchange key and the one-rank RCCL one.
+set -u
+TAG=${1:-r04a}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R && mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
+  tests/test_gpu_exchange.py tests/test_abi.py "tests/test_gpu_p2p.py::test_config2_p2p_shape" \
+  > gpurun_out/pytest_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_$TAG.log; exit 10; }
+tail -3 gpurun_out/pytest_$TAG.log
+timeout -k 10 300 python -u bench.py --workload p2p --sessions 4096 --latency 8 --max-prediction 9 \
+  > gpurun_out/bench_${TAG}_p2pc2.json 2> gpurun_out/bench_${TAG}_p2pc2.err || { tail -20 gpurun_out/bench_${TAG}_p2pc2.err; exit 11; }
+cat gpurun_out/bench_${TAG}_p2pc2.json
+GGRS_BENCH_BACKEND=gloo timeout -k 10 300 python -u bench.py --gpus 2 --steps 10 \
+  > gpurun_out/bench_${TAG}_gloo2.json 2> gpurun_out/bench_${TAG}_gloo2.err || { tail -20 gpurun_out/bench_${TAG}_gloo2.err; exit 12; }
+cat gpurun_out/bench_${TAG}_gloo2.json
+GGRS_BENCH_DIST=1 timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+  --master-addr 127.0.0.1 --master-port 29611 bench.py --no-cpu-baseline \
+  > gpurun_out/bench_${TAG}_dist1.json 2> gpurun_out/bench_${TAG}_dist1.err || { tail -20 gpurun_out/bench_${TAG}_dist1.err; exit 13; }
+cat gpurun_out/bench_${TAG}_dist1.json
+echo r04a done
