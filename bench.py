@@ -932,6 +932,9 @@ def run_requests(args):
     G = args.req_groups if form in ("native", "p2p") else 1
     if L % G:
         raise SystemExit(f"--lanes {L} is not a multiple of --req-groups {G}")
+    if G > 4 and not args.no_lane_server:
+        print(f"note: --req-groups {G}: at most 4 lane servers run on a device (GPU_MAX_HW_QUEUES); the other "
+              "groups' batches run as one launch each", file=sys.stderr)
     T = args.req_threads if form == "native" else 1
     if T < 1 or G % T:
         raise SystemExit(f"--req-groups {G} is not a multiple of --req-threads {T}")

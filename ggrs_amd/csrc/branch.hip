@@ -515,13 +515,24 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
       row_next = lds_rows[min(u + 1, last_row) * ns + ls];
       slot = slot + 1 == p.R ? 0 : slot + 1;
       if (active(0)) {
-        // speculate_kernel's check of round u - 1's survivors: their depth-0 enumerated player
-        // against the replayed trunk's (the cell's local players ARE the trunk's)
-        if (u > 0 && survived) {
-          bool same = true;
+        // speculate_kernel's check of round u - 1's survivors: the Fletcher-16 of their depth-0
+        // cell against the replayed trunk's (GGRS compares checksums, p2p_session.rs:904-937).  The
+        // cell's local players ARE the trunk's, so equal enumerated-player bits mean equal
+        // checksums; only a lane whose bits differ (wave-uniform branch, never taken in a
+        // deterministic run) compares the two checksums, so a collision is no desync here either
+        // 
+        bool same = true;
 #pragma unroll
-          for (int q = 0; q < 5; q++) same = same && est[0][q] == T.w[kq[q]];
-          if (!same) atomicCAS(desync_dst, -1, f_c);
+        for (int q = 0; q < 5; q++) same = same && est[0][q] == T.w[kq[q]];
+        const bool differs = u > 0 && survived && !same;
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(differs) != 0, 0)) {
+          if (differs) {
+            uint32_t d1, d2, v[5];
+            common_sums(T, d1, d2);
+#pragma unroll
+            for (int q = 0; q < 5; q++) v[q] = T.w[kq[q]];
+            if (enum_ck(d1, d2, est[0]) != enum_ck(d1, d2, v)) atomicCAS(desync_dst, -1, f_c);
+          }
         }
         if (u == 0 && check0) {
           uint32_t d1, d2, v[5];

@@ -34,6 +34,9 @@ struct LaneServerHost {
   int32_t pending_epoch = 0;
   double pending_t0 = 0.0;
   bool failed = false;     // a batch timed out: the server may still hold it; no further batches
+  bool counted = false;    // this engine's server holds one of the device's server slots
+  bool orphan = false;     // a submitted batch was collected by another call (lane_server_stop):
+  int32_t orphan_fails = 0;  // its failure count, returned by the next ggrs_lane_batch_wait
 };
 
 struct ggrs_engine {
@@ -88,6 +91,8 @@ namespace ggrs {
 // Ends the persistent lane server (requests.hip) if it runs: every other use of the engine's stream
 // or device buffers must come after it.
 int lane_server_stop(ggrs_engine* e);
+// give back the engine's lane-server slot on the device (engine destruction)
+void lane_server_release(ggrs_engine* e);
 
 // Counts one fused launch of a timed span; the span's first launch records its begin event.
 template <typename K>

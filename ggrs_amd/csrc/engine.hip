@@ -1162,6 +1162,7 @@ int ggrs_engine_destroy(ggrs_engine_t* e) {
   if (!e) return GGRS_OK;
   (void)hipSetDevice(e->cfg.device);
   (void)lane_server_stop(e);
+  lane_server_release(e);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   void* bufs[] = {e->arena, e->shadow, e->fail_f0, e->inputs, e->lane_status,
                   e->mis_frame, e->mis_mask, e->staging};  // trace lives in the arena allocation

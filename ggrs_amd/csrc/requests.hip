@@ -21,6 +21,8 @@
 // of one per request), each session's list is validated against its cell tags (also in LDS), then
 // executed with the state in registers; checksums collect in LDS and go back to host memory with
 // the lane results as wide system-scope stores.
+#include <atomic>
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <immintrin.h>
@@ -687,6 +689,41 @@ LaneBatchParams batch_params(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, i
 constexpr double kServerIdleHost = 0.25;  // the host restarts a server idle this long (s) ...
 constexpr double kServerIdleKernel = 1.0; // ... well before the kernel's own watchdog ends it
 
+// Lane servers running per device.  Each persistent server holds a hardware queue; HIP spreads a
+// process's streams over GPU_MAX_HW_QUEUES of them (default 4), so a server beyond that shares an
+// in-order queue with another and waits for it to go idle.  Engines beyond the limit
+// serve their batches with one launch each.
+constexpr int kMaxDevices = 64;
+std::atomic<int> g_servers[kMaxDevices];
+
+int server_limit() {
+  static const int lim = [] {
+    const char* v = std::getenv("GPU_MAX_HW_QUEUES");
+    const int n = v ? std::atoi(v) : 0;
+    return n > 0 ? n : 4;
+  }();
+  return lim;
+}
+
+// take one of the device's server slots (false: all taken)
+bool server_slot_take(ggrs_engine* e) {
+  const int d = e->cfg.device;
+  if (d < 0 || d >= kMaxDevices) return false;
+  int n = g_servers[d].load();
+  while (n < server_limit())
+    if (g_servers[d].compare_exchange_weak(n, n + 1)) {
+      e->server.counted = true;
+      return true;
+    }
+  return false;
+}
+
+void server_slot_release(ggrs_engine* e) {
+  if (!e->server.counted) return;
+  e->server.counted = false;
+  g_servers[e->cfg.device].fetch_sub(1);
+}
+
 int server_start(ggrs_engine* e) {
   LaneServerHost& s = e->server;
   const int64_t L = e->cfg.num_lanes;
@@ -723,12 +760,16 @@ int server_start(ggrs_engine* e) {
     s.enabled = false;  // too many lanes to keep resident: one launch per batch instead
     return GGRS_OK;
   }
+  if (!server_slot_take(e)) return GGRS_E_STATE;  // every server slot taken: this batch as a launch
   dispatch_players(e->cfg.num_players, [&](auto PC) {
     constexpr int P = decltype(PC)::value;
     lane_server_kernel<P><<<s.blocks, kLaneBlock, lds, e->stream>>>(p, dctl, ddone, (ServerDev*)s.dev, s.epoch,
                                                                 s.idle_ticks);
   });
-  HIP_TRY(hipGetLastError());
+  if (hipError_t err = hipGetLastError(); err != hipSuccess) {
+    server_slot_release(e);
+    return set_error(GGRS_E_HIP, "lane server launch: %s", hipGetErrorString(err));
+  }
   s.running = true;
   s.last_done = now_s();
   return GGRS_OK;
@@ -741,7 +782,7 @@ int server_publish(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, 
     if (int rc = lane_server_stop(e)) return rc;
   }
   if (!s.running) {
-    if (int rc = server_start(e)) return rc;
+    if (int rc = server_start(e)) return rc;  // GGRS_E_STATE: no server slot free right now
     if (!s.enabled) return GGRS_E_STATE;  // caller falls back to a launch per batch
   }
   uint64_t* ctl = (uint64_t*)s.mem;
@@ -796,9 +837,12 @@ int server_collect(ggrs_engine* e, int32_t* fails) {
 int submit_batch(ggrs_engine* e, int32_t W, int32_t LD, int32_t A, int32_t S, int use_status) {
   e->mode = kModeLaneRequests;
   if (e->server.failed) return set_error(GGRS_E_STATE, "an earlier lane batch timed out on this engine");
+  e->server.orphan = false;  // a new batch: an earlier collected result is no longer waited for
   if (e->server.enabled) {
     const int rc = server_publish(e, W, LD, A, S, use_status);
-    if (rc != GGRS_E_STATE) return rc;  // GGRS_E_STATE: the grid cannot stay resident, launch instead
+    // GGRS_E_STATE: the grid cannot stay resident, or every server slot of the device is taken:
+    // launch instead
+    if (rc != GGRS_E_STATE) return rc;
   }
   LaneBatchParams p = batch_params(e, W, LD, A, S, use_status);
   if (!p.tokens || !p.load_frames || !p.inputs || !p.status || !p.cks || !p.result)
@@ -906,14 +950,22 @@ int lane_server_stop(ggrs_engine* e) {
   if (s.pending) {  // a submitted batch first runs to completion (a quit word would skip it)
     int32_t fails;
     if (int rc = wait_batch(e, &fails)) return rc;
+    s.orphan = true;  // the caller's ggrs_lane_batch_wait gets this batch's result
+    s.orphan_fails = fails;
   }
-  if (!s.running) return GGRS_OK;
+  if (!s.running) {
+    if (!s.failed) server_slot_release(e);  // a timed-out server may still hold its queue
+    return GGRS_OK;
+  }
   uint64_t* ctl = (uint64_t*)s.mem;
   __atomic_store_n(ctl, __atomic_load_n(ctl, __ATOMIC_ACQUIRE) | ctlw::kQuit, __ATOMIC_RELEASE);
   s.running = false;
   HIP_TRY(hipStreamSynchronize(e->stream));  // every block leaves its loop and stores its lanes' state
-return GGRS_OK;
+  server_slot_release(e);
+  return GGRS_OK;
 }
+
+void lane_server_release(ggrs_engine* e) { server_slot_release(e); }
 
 }  // namespace ggrs
 
@@ -968,10 +1020,16 @@ int ggrs_lane_batch_submit(ggrs_engine_t* e, const ggrs_lane_batch_t* b, int32_t
 int ggrs_lane_batch_wait(ggrs_engine_t* e, int32_t* n_failed) {
   if (!e) return set_error(GGRS_E_INVALID, "null argument");
   if (n_failed) *n_failed = 0;
-  if (!e->server.pending) return set_error(GGRS_E_STATE, "no lane batch submitted");
-  HIP_TRY(hipSetDevice(e->cfg.device));
   int32_t fails = -1;
-  if (int rc = wait_batch(e, &fails)) return rc;
+  if (!e->server.pending) {
+    // the batch was already collected by another call on the engine (which waits for it first)
+    if (!e->server.orphan) return set_error(GGRS_E_STATE, "no lane batch submitted");
+    e->server.orphan = false;
+    fails = e->server.orphan_fails;
+  } else {
+    HIP_TRY(hipSetDevice(e->cfg.device));
+    if (int rc = wait_batch(e, &fails)) return rc;
+  }
   if (fails == 0) return GGRS_OK;  // the server counted no failed lane: no scan of the results
   ggrs_lane_batch_t v;
   fill_batch_view(e, &v);

@@ -199,7 +199,8 @@ int ggrs_lane_batch_lds(ggrs_engine_t* eng, int32_t token_words, int32_t load_sl
  * memory, with ggrs_lane_batch_run's result.  Between them the caller must not touch this batch's
  * memory, but may work on another engine's: a handler serving its sessions as two lane groups (two
  * engines) encodes and hands back one group while the other's batch is on the device.  Any other
- * call on the engine first waits for a submitted batch. */
+ * call on the engine first waits for a submitted batch; its result is kept, and the next _wait
+ * returns it (failed lanes included) instead of GGRS_E_STATE. */
 int ggrs_lane_batch_submit(ggrs_engine_t* eng, const ggrs_lane_batch_t* batch, int32_t flags);
 int ggrs_lane_batch_wait(ggrs_engine_t* eng, int32_t* n_failed);
 /* Host-side encoding of one session's ordered request list (src/lib.rs:171-195) into column `lane`
@@ -232,7 +233,10 @@ int ggrs_handle_requests_lanes(ggrs_engine_t* eng, const ggrs_request_t* reqs, c
  * and spins on per-block done flags, so a call costs one PCIe round trip instead of a launch plus a
  * stream synchronisation.  It ends (lanes' states back in device memory) before any other call
  * touches the engine's stream, when the host has been idle for 0.25 s, or by its own watchdog
- * after 1 s without a batch.  on = 0: one launch per batch. */
+ * after 1 s without a batch.  on = 0: one launch per batch.  At most GPU_MAX_HW_QUEUES (default 4)
+ * servers run on one device at a time (each holds a hardware queue; a second server on the same
+ * in-order queue would wait for the first to go idle): an engine that finds them all taken serves
+ * its batches with one launch each until a server stops. */
 int ggrs_lane_server(ggrs_engine_t* eng, int32_t on);
 /* Every lane's current frame (its state's frame field): [num_lanes]. */
 int ggrs_read_lane_frames(ggrs_engine_t* eng, int32_t* frames);
@@ -272,7 +276,9 @@ int ggrs_last_launch_ms(ggrs_engine_t* eng, float* ms);
 int ggrs_timing_reset(ggrs_engine_t* eng);
 /* Close the span without waiting: records its end event right behind the last launch (a caller
  * that then synchronises the stream itself reads the same span without an extra host round trip
- * inside its own wall clock).  _read after _stop reports that span. */
+ * inside its own wall clock).  _read after _stop reports that span.  Exception: a running lane
+ * server is stopped first (the event would otherwise queue behind the persistent kernel), which
+ * waits for a submitted batch and for the server to leave its loop. */
 int ggrs_timing_stop(ggrs_engine_t* eng);
 int ggrs_timing_read(ggrs_engine_t* eng, float* total_ms, int32_t* launches);
 

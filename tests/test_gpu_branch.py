@@ -267,3 +267,50 @@ def test_config3_fused_rounds_full_size(oracle):
     assert int(ck[0]) == oracle.fletcher16(bytes(st))
     assert eng.survivors().sum() == 16 ** 3
     assert (eng.desync() == -1).all()
+
+
+def test_prefix_rounds_chunked_launches_and_reports(oracle):
+    """More rounds than one prefix launch's LDS holds input rows for (ns_max sessions per block x
+    (n + W - 1) rows > 32 KiB: launch_rounds splits them into chunks), with every round's report
+    written to a device buffer (ggrs_branch_rounds_reports, the per-round copy offsets of each
+    chunk): reports, trunks, desync records and sampled cells equal per-round speculate + confirm
+    (ADVICE r3)."""
+    import torch
+    from ggrs_amd import BranchEngine, synth
+    S, B, A, P, mask, W, n = 300, 4, 4, 2, 0b10, 5, 130
+    truth = synth.gen_inputs(17, S, n + W + 3, P, synth.MODEL_HELD)
+    engs, bufs = {}, {}
+    for f in ("fused", "per_round"):
+        e = BranchEngine(S, num_players=P, remote_mask=mask, window=W, branches=B, alphabet=A,
+                         input_capacity=n + W + 4)
+        e.add_inputs(0, truth)
+        e.set_round_form(f)
+        bufs[f] = torch.zeros((n, e.report_bytes), dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        if f == "fused":
+            e.rounds_to_tensor(bufs[f], n)
+        else:  # separate speculate / confirm launches, each confirm copying its report
+            for r in range(n):
+                e.speculate()
+                e.confirm(bufs[f][r].data_ptr())
+        e.synchronize()
+        engs[f] = e
+    a, b = engs["fused"], engs["per_round"]
+    assert a.trunk_frame() == b.trunk_frame() == n
+    assert torch.equal(bufs["fused"], bufs["per_round"])
+    assert (a.desync() == -1).all() and (b.desync() == -1).all()
+    ra, rb = a.report(), b.report()
+    assert (ra[0] == rb[0]).all() and (ra[1] == rb[1]).all()
+    assert bytes(bufs["fused"][-1, :2 * S].cpu().numpy()) == ra[0].tobytes()
+    for s in (0, 1, S // 2, S - 1):
+        assert bytes(a.trunk(s)) == bytes(b.trunk(s)), s
+    st = oracle.state_new(P)
+    for fr in range(n):
+        st = oracle.state_advance(st, truth[fr, 0])
+    assert bytes(a.trunk(0)) == bytes(st)
+    rng = np.random.default_rng(11)
+    L = S * B
+    for lane in sorted(set([0, 1, A, B - 1, L - 1] + rng.integers(0, L, 12).tolist())):
+        for fr in range(n - 1, n + W):
+            x, y = a.lane_state(lane, fr), b.lane_state(lane, fr)
+            assert x[0] == y[0] and bytes(x[1]) == bytes(y[1]), (lane, fr)

@@ -6,7 +6,7 @@ TAG=${1:-r04a}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R && mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
-  tests/test_gpu_exchange.py tests/test_abi.py "tests/test_gpu_p2p.py::test_config2_p2p_shape" \
+  tests/test_gpu_exchange.py tests/test_abi.py "tests/test_gpu_p2p.py::test_config2_p2p_shape" tests/test_gpu_branch.py tests/test_gpu_lane_requests.py \
   > gpurun_out/pytest_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_$TAG.log; exit 10; }
 tail -3 gpurun_out/pytest_$TAG.log
 timeout -k 10 300 python -u bench.py --workload p2p --sessions 4096 --latency 8 --max-prediction 9 \
