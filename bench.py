@@ -935,8 +935,11 @@ def run_requests(args):
     if G > 4 and not args.no_lane_server:
         print(f"note: --req-groups {G}: at most 4 lane servers run on a device (GPU_MAX_HW_QUEUES); the other "
               "groups' batches run as one launch each", file=sys.stderr)
-    T = args.req_threads if form == "native" else 1
-    if T < 1 or G % T:
+    T = args.req_threads if form in ("native", "p2p") else 1
+    if args.req_deferred and form != "p2p":
+        raise SystemExit("--req-deferred is for P2P lists only: a SyncTestSession reads the previous call's "
+                         "checksums (sync_test_session.rs:173-190)")
+    if T < 1 or (form == "native" and G % T):
         raise SystemExit(f"--req-groups {G} is not a multiple of --req-threads {T}")
     sink = np.zeros(1, np.uint64)
     phases = np.zeros(4)
@@ -991,7 +994,7 @@ def run_requests(args):
     elif form == "p2p":
         vp = ctypes.c_void_p
         drv.handler_drive_p2p_groups.argtypes = [vp, ctypes.c_int32] + [ctypes.c_int32] * 4 + [vp] * 7 + \
-            [ctypes.c_int32, ctypes.c_int32, ctypes.c_double, u64, dbl, dbl]
+            [ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_int32, ctypes.c_int32, u64, dbl, dbl]
 
         def run_calls(c, n):
             s, sec = ctypes.c_uint64(), ctypes.c_double()
@@ -1000,7 +1003,7 @@ def run_requests(args):
             rc = drv.handler_drive_p2p_groups(handles, G, L, P, fx["M"], fx["C"], ptr(fx["reqs"]), ptr(fx["req_off"]),
                                               ptr(fx["adv_off"]), ptr(fx["inputs"]), ptr(fx["status"]),
                                               ptr(fx["shape"]), ptr(lane_frames), c, n, args.session_us,
-                                              ctypes.byref(s), ctypes.byref(sec), ph)
+                                              int(args.req_deferred), T, ctypes.byref(s), ctypes.byref(sec), ph)
             assert rc == 0, (rc, eng._L.ggrs_last_error())
             phases[:] = list(ph)
             sink[0] += s.value
@@ -1134,6 +1137,7 @@ def run_requests(args):
             "config": {"workload": wl + f", {calls} calls per step, lists and inputs from host memory, checksums "
                                         "back to host memory each call",
                        "sessions_per_gpu": L, "req_form": form, "lane_groups": G, "host_threads": T,
+                       "deferred_handback": bool(args.req_deferred),
                        "session_us_per_group_call":
                            args.session_us, "lane_server": not args.no_lane_server,
                        "us_per_call": round(elapsed / n_calls * 1e6, 2),
@@ -1219,7 +1223,11 @@ def main():
     ap.add_argument("--req-groups", type=int, default=2,
                     help="requests (native, p2p): lane groups (engines) whose batches overlap the host's work; at most 4 with the lane server (one persistent server per hardware queue)")
     ap.add_argument("--req-threads", type=int, default=1,
-                    help="requests (native): host threads serving the lane groups (G a multiple of it)")
+                    help="requests: host threads -- native: serving the lane groups (G a multiple of it); "
+                         "p2p: encoding and handing back each group's lanes")
+    ap.add_argument("--req-deferred", action="store_true",
+                    help="requests (p2p): deferred checksum hand-back (handle_requests_deferred): the session "
+                         "logic (--session-us) overlaps the batch on the device")
     ap.add_argument("--session-us", type=float, default=0.0,
                     help="requests: modelled GGRS session-logic host time per lane group and call (us)")
     ap.add_argument("--workload", choices=["synctest", "p2p", "codec", "requests", "launch-selftest"],

@@ -244,13 +244,18 @@ int handler_drive_synctest(ggrs_engine_t* eng, const uint8_t* inputs, int32_t L,
  *   adv_off  [M][C + 1] start of its AdvanceFrame rows in inputs / status
  *   inputs, status [N_adv][P]
  * Calls c_begin .. c_begin+n_calls-1.  lane_frames [L] in/out: every lane's frame (the encoder's
- * Save-frame check); shape[4]: the batch shape to map (the fixture's largest list). */
+ * Save-frame check); shape[4]: the batch shape to map (the fixture's largest list).
+ * deferred: the handler's deferred hand-back (rust/ggrs-mi355x handle_requests_deferred): a call
+ * submits its batch and returns, the modelled session logic runs while the batch is on the device,
+ * and the next call collects it (checksums into the cells) before encoding its own lists;
+ * synchronous: the session logic runs after the call's checksums are back.  threads > 1: the lanes
+ * of a group are encoded and handed back by that many host threads (OpenMP). */
 int handler_drive_p2p_groups(ggrs_engine_t** engs, int32_t G, int32_t L, int32_t P, int32_t M, int32_t C,
                              const ggrs_request_t* reqs, const int64_t* req_off, const int64_t* adv_off,
                              const uint8_t* inputs, const uint8_t* status, const int32_t* shape, int32_t* lane_frames,
-                             int32_t c_begin, int32_t n_calls, double session_us, uint64_t* sink, double* seconds,
-                             double* phases) {
-  if (G < 1 || G > MAX_GROUPS || L % G || c_begin < 0 || c_begin + n_calls > C) return GGRS_E_INVALID;
+                             int32_t c_begin, int32_t n_calls, double session_us, int32_t deferred, int32_t threads,
+                             uint64_t* sink, double* seconds, double* phases) {
+  if (G < 1 || G > MAX_GROUPS || L % G || c_begin < 0 || c_begin + n_calls > C || threads < 1) return GGRS_E_INVALID;
   group_t g[MAX_GROUPS];
   const int32_t Lg = L / G;
   for (int q = 0; q < G; q++) {
@@ -275,16 +280,19 @@ int handler_drive_p2p_groups(ggrs_engine_t** engs, int32_t G, int32_t L, int32_t
         if (rc) return rc;
         const double tb = now_s();
         const int32_t pc = prev_call[q];
+        uint64_t part = 0;
+#pragma omp parallel for num_threads(threads) schedule(static) reduction(+ : part) if (threads > 1)
         for (int32_t l = 0; l < Lg; l++) { /* every Save's checksum of the lane's list */
           const int32_t lane = gq->base + l, m = lane % M;
           const int64_t a = req_off[(int64_t)m * (C + 1) + pc], b = req_off[(int64_t)m * (C + 1) + pc + 1];
           int si = 0;
           for (int64_t k = a; k < b; k++)
-            if (reqs[k].kind == GGRS_REQ_SAVE) acc += gq->b.checksums[(size_t)si++ * Lg + l];
+            if (reqs[k].kind == GGRS_REQ_SAVE) part += gq->b.checksums[(size_t)si++ * Lg + l];
           lane_frames[lane] = gq->b.lane_result[l];
         }
+        acc += part;
         const double tc = now_s();
-        spin_us(session_us);
+        if (!deferred) spin_us(session_us); /* the session logic after the call returned its checksums */
         t_dev += tb - ta;
         t_back += tc - tb;
         t_sess += now_s() - tc;
@@ -292,6 +300,8 @@ int handler_drive_p2p_groups(ggrs_engine_t** engs, int32_t G, int32_t L, int32_t
       }
       if (c == c_begin + n_calls) continue;
       const double ta = now_s();
+      int enc_rc = 0;
+#pragma omp parallel for num_threads(threads) schedule(static) if (threads > 1)
       for (int32_t l = 0; l < Lg; l++) {
         const int32_t lane = gq->base + l, m = lane % M;
         const int64_t a = req_off[(int64_t)m * (C + 1) + c], b = req_off[(int64_t)m * (C + 1) + c + 1];
@@ -299,8 +309,12 @@ int handler_drive_p2p_groups(ggrs_engine_t** engs, int32_t G, int32_t L, int32_t
         int32_t bad = -1;
         int rc = ggrs_lane_encode(&gq->b, Lg, P, l, reqs + a, (int32_t)(b - a), inputs + ad * P, status + ad * P,
                                   lane_frames[lane], &bad);
-        if (rc) return rc; /* the fixture's lists are valid: any rejection is an error here */
+        if (rc) {
+#pragma omp critical
+          enc_rc = rc; /* the fixture's lists are valid: any rejection is an error here */
+        }
       }
+      if (enc_rc) return enc_rc;
       gq->run = gq->b;
       const double tb = now_s();
       int rc = ggrs_lane_batch_submit(engs[q], &gq->run, GGRS_BATCH_STATUS);
@@ -309,6 +323,11 @@ int handler_drive_p2p_groups(ggrs_engine_t** engs, int32_t G, int32_t L, int32_t
       prev_call[q] = c;
       t_enc += tb - ta;
       t_dev += now_s() - tb;
+      if (deferred) { /* the call has returned: the session logic overlaps the batch on the device */
+        const double td = now_s();
+        spin_us(session_us);
+        t_sess += now_s() - td;
+      }
     }
   }
   *seconds = now_s() - t0;

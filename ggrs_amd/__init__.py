@@ -9,6 +9,7 @@ from .session import (AdvanceFrame, BoxGameHandler, Engine, LaneBatch, LaneBoxGa
                       LanesFailed, LoadGameState, MismatchedChecksum, SaveGameState, SessionBuilder,
                       SyncTestSession, encode_lane_lists)
 
+from .handler import BatchedHandler, GameStateCell  # noqa: F401
 from .branch import BranchEngine  # noqa: F401
 from .particles import ParticleEngine  # noqa: F401
 from .p2p import P2PEngine  # noqa: F401

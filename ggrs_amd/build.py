@@ -83,7 +83,7 @@ def build_driver(force=False, verbose=False):
             os.path.getmtime(DRIVER_SRC), os.path.getmtime(LIB)):
         return DRIVER_LIB
     # -O3 -mavx2: the handler's per-call loops over L lanes (token rows, checksum hand-back) vectorise
-    cmd = ["gcc", "-O3", "-mavx2", "-pthread", "-shared", "-fPIC", "-I", os.path.join(ROOT, "include"), "-o", DRIVER_LIB + ".tmp",
+    cmd = ["gcc", "-O3", "-mavx2", "-pthread", "-fopenmp", "-shared", "-fPIC", "-I", os.path.join(ROOT, "include"), "-o", DRIVER_LIB + ".tmp",
            DRIVER_SRC, "-L", HERE, "-lggrs_amd", "-Wl,-rpath,$ORIGIN/../ggrs_amd"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

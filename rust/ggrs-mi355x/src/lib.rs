@@ -10,6 +10,8 @@
 //! when a list exceeds the batch limits, through the generic CSR form (ggrs_handle_requests_lanes).
 //! `handle_requests_lockstep` is the one-list-for-all form for sessions known to be in lockstep; it
 //! checks that assumption and returns an error instead of misaligning lanes when it does not hold.
+//! `handle_requests_deferred` (P2PSessions only) returns before the device does: checksums reach
+//! their cells on the next call, so the PCIe round trip overlaps the caller's session logic.
 pub mod ffi;
 
 use ffi::*;
@@ -44,6 +46,10 @@ pub struct FailedLanes {
     pub lanes: Vec<(usize, usize)>,
 }
 
+/// Deferred mode: the submitted batch's SaveGameStates, per lane in request order, each a closure
+/// that hands the cell its checksum (`cell.save(frame, None, Some(checksum))`).
+type PendingSaves = Vec<(usize, Vec<Box<dyn FnOnce(u128)>>)>;
+
 pub struct BatchedBoxGame {
     eng: *mut ggrs_engine_t,
     lanes: usize,
@@ -51,6 +57,9 @@ pub struct BatchedBoxGame {
     /// every lane's frame after its last list (lane_result): the start frame the Save frames of
     /// its next list are checked against (ex_game.rs:104), since the batch carries no Save frames
     lane_frames: Vec<i32>,
+    /// deferred mode: the batch submitted by the last call and its saves, collected by the next
+    /// call (or flush)
+    pending: Option<(ggrs_lane_batch_t, PendingSaves)>,
 }
 
 /// One lane's list as the C ABI takes it: requests, and one input / status row per AdvanceFrame.
@@ -93,15 +102,15 @@ impl BatchedBoxGame {
         };
         let mut eng = std::ptr::null_mut();
         check(unsafe { ggrs_engine_create(&cfg, &mut eng) })?;
-        Ok(Self { eng, lanes, players, lane_frames: vec![0; lanes] })
+        Ok(Self { eng, lanes, players, lane_frames: vec![0; lanes], pending: None })
     }
 
-    /// `requests[l]` is session l's request list from its `advance_frame()`; lists may differ in
-    /// kinds, frames and length.  Ok(None) when every lane ran; Ok(Some(failed)) when some lanes'
-    /// lists were rejected (those lanes did not run): a SaveGameState of a frame other than the one
-    /// the list has reached (checked while encoding, ggrs_lane_encode), or a Load of a frame the
-    /// lane's cell does not hold (checked on the device).
-    pub fn handle_requests<T>(&mut self, requests: &[Vec<GgrsRequest<T>>]) -> Result<Option<FailedLanes>, EngineError>
+    /// Every lane's list encoded into the engine's mapped batch: Ok(None) when some list exceeds the
+    /// batch limits (the caller takes the CSR form), else the batch with the call's row counts and
+    /// the lanes the encoder rejected (a SaveGameState of a frame other than the one the list has
+    /// reached, ggrs_lane_encode).
+    fn encode_batch<T>(&mut self, requests: &[Vec<GgrsRequest<T>>])
+        -> Result<Option<(ggrs_lane_batch_t, Vec<(usize, usize)>)>, EngineError>
     where
         T: Config,
         T::Input: InputByte,
@@ -122,7 +131,7 @@ impl BatchedBoxGame {
         }
         if shape[0] > GGRS_BATCH_MAX_WORDS || shape[1] > GGRS_BATCH_MAX_LOADS || shape[2] > GGRS_BATCH_MAX_ADV
             || shape[3] > GGRS_BATCH_MAX_SAVES {
-            return self.handle_requests_csr(requests);
+            return Ok(None);
         }
         let (w, ld, a, s) = (shape[0].max(1), shape[1].max(1), shape[2].max(1), shape[3].max(1));
         // mapped afresh on every call: a CSR call may have grown (and freed) the previous mapping
@@ -150,13 +159,31 @@ impl BatchedBoxGame {
         run.load_slots = ld;
         run.adv_rows = a;
         run.save_rows = s;
+        Ok(Some((run, failed)))
+    }
+
+    /// `requests[l]` is session l's request list from its `advance_frame()`; lists may differ in
+    /// kinds, frames and length.  Ok(None) when every lane ran; Ok(Some(failed)) when some lanes'
+    /// lists were rejected (those lanes did not run): a SaveGameState of a frame other than the one
+    /// the list has reached (checked while encoding, ggrs_lane_encode), or a Load of a frame the
+    /// lane's cell does not hold (checked on the device).  Returns with every checksum in its cell.
+    pub fn handle_requests<T>(&mut self, requests: &[Vec<GgrsRequest<T>>]) -> Result<Option<FailedLanes>, EngineError>
+    where
+        T: Config,
+        T::Input: InputByte,
+    {
+        let mut failed = self.flush()?.map(|f| f.lanes).unwrap_or_default();
+        let Some((b, enc_failed)) = self.encode_batch(requests)? else {
+            return Ok(merge_failed(failed, self.handle_requests_csr(requests)?));
+        };
         let mut n_failed = 0i32;
-        let rc = unsafe { ggrs_lane_batch_run(self.eng, &run, GGRS_BATCH_STATUS, &mut n_failed) };
+        let rc = unsafe { ggrs_lane_batch_run(self.eng, &b, GGRS_BATCH_STATUS, &mut n_failed) };
         if rc != GGRS_OK && rc != GGRS_E_PRECONDITION {
             return Err(EngineError(rc, last_error()));
         }
         // every Save's checksum back to its GameStateCell, lane by lane; failed lanes report
-        let rejected: std::collections::HashSet<usize> = failed.iter().map(|&(l, _)| l).collect();
+        let rejected: std::collections::HashSet<usize> = enc_failed.iter().map(|&(l, _)| l).collect();
+        failed.extend(enc_failed);
         for (lane, list) in requests.iter().enumerate() {
             let res = unsafe { *b.lane_result.add(lane) };
             if res < 0 {
@@ -179,6 +206,75 @@ impl BatchedBoxGame {
         Ok(if failed.is_empty() { None } else { Some(FailedLanes { lanes: failed }) })
     }
 
+    /// Deferred hand-back, for P2PSessions only: encodes and submits the batch, saves every cell as
+    /// `cell.save(frame, None, None)` and returns at once, so the device round trip overlaps the
+    /// caller's session logic until the next call; that call (or `flush`) waits for the batch and
+    /// fills `Some(checksum)` into these cells in request order.  A P2PSession reads a cell's
+    /// checksum only for confirmed frames at its desync interval and retries on a later call while
+    /// it is None (check_checksum_send_interval, p2p_session.rs:939-963); a confirmed frame is never
+    /// re-saved, so the report it sends is the same.  Not for SyncTestSessions: checksums_consistent
+    /// reads the previous call's cells (sync_test_session.rs:173-190).  Lanes the device rejects
+    /// are reported by the call that collects their batch.
+    pub fn handle_requests_deferred<T>(&mut self, requests: &[Vec<GgrsRequest<T>>])
+        -> Result<Option<FailedLanes>, EngineError>
+    where
+        T: Config,
+        T::Input: InputByte,
+        T::State: 'static,
+    {
+        let mut failed = self.flush()?.map(|f| f.lanes).unwrap_or_default();
+        let Some((b, enc_failed)) = self.encode_batch(requests)? else {
+            return Ok(merge_failed(failed, self.handle_requests_csr(requests)?));
+        };
+        check(unsafe { ggrs_lane_batch_submit(self.eng, &b, GGRS_BATCH_STATUS) })?;
+        let rejected: std::collections::HashSet<usize> = enc_failed.iter().map(|&(l, _)| l).collect();
+        failed.extend(enc_failed);
+        let mut pending: PendingSaves = Vec::with_capacity(self.lanes);
+        for (lane, list) in requests.iter().enumerate() {
+            if rejected.contains(&lane) {
+                continue;
+            }
+            let mut saves: Vec<Box<dyn FnOnce(u128)>> = Vec::new();
+            for r in list {
+                if let GgrsRequest::SaveGameState { cell, frame } = r {
+                    cell.save(*frame, None, None);
+                    let (c, f) = (cell.clone(), *frame);
+                    saves.push(Box::new(move |cs| c.save(f, None, Some(cs))));
+                }
+            }
+            pending.push((lane, saves));
+        }
+        self.pending = Some((b, pending));
+        Ok(if failed.is_empty() { None } else { Some(FailedLanes { lanes: failed }) })
+    }
+
+    /// Collects the batch a deferred call submitted, if any: waits for it, hands every Save's
+    /// checksum to its cell in request order and records every lane's frame.  Ok(Some(failed)):
+    /// the lanes the device rejected in that batch.
+    pub fn flush(&mut self) -> Result<Option<FailedLanes>, EngineError> {
+        let Some((b, pending)) = self.pending.take() else {
+            return Ok(None);
+        };
+        let mut n_failed = 0i32;
+        let rc = unsafe { ggrs_lane_batch_wait(self.eng, &mut n_failed) };
+        if rc != GGRS_OK && rc != GGRS_E_PRECONDITION {
+            return Err(EngineError(rc, last_error()));
+        }
+        let mut failed = Vec::new();
+        for (lane, saves) in pending {
+            let res = unsafe { *b.lane_result.add(lane) };
+            if res < 0 {
+                failed.push((lane, (-res - 1) as usize));
+                continue;
+            }
+            self.lane_frames[lane] = res;
+            for (si, save) in saves.into_iter().enumerate() {
+                save(unsafe { *b.checksums.add(si * self.lanes + lane) } as u128);
+            }
+        }
+        Ok(if failed.is_empty() { None } else { Some(FailedLanes { lanes: failed }) })
+    }
+
     /// The generic per-lane form (ggrs_handle_requests_lanes): any list length.
     pub fn handle_requests_csr<T>(&mut self, requests: &[Vec<GgrsRequest<T>>]) -> Result<Option<FailedLanes>, EngineError>
     where
@@ -186,6 +282,7 @@ impl BatchedBoxGame {
         T::Input: InputByte,
     {
         assert_eq!(requests.len(), self.lanes);
+        let earlier = self.flush()?;
         let mut reqs = Vec::new();
         let mut offsets = vec![0i32];
         let mut inputs = Vec::new();
@@ -239,7 +336,8 @@ impl BatchedBoxGame {
                 }
             }
         }
-        Ok(if failed.is_empty() { None } else { Some(FailedLanes { lanes: failed }) })
+        Ok(merge_failed(earlier.map(|f| f.lanes).unwrap_or_default(),
+                        if failed.is_empty() { None } else { Some(FailedLanes { lanes: failed }) }))
     }
 
     /// One list for every lane (ggrs_handle_requests: one launch, the lists' kinds and frames
@@ -252,6 +350,9 @@ impl BatchedBoxGame {
         T::Input: InputByte,
     {
         assert_eq!(requests.len(), self.lanes);
+        if let Some(f) = self.flush()? {
+            return Err(EngineError(GGRS_E_PRECONDITION, format!("lanes {:?} of the previous deferred batch failed", f.lanes)));
+        }
         let shape = |r: &GgrsRequest<T>| match r {
             GgrsRequest::SaveGameState { frame, .. } => (GGRS_REQ_SAVE, *frame),
             GgrsRequest::LoadGameState { frame, .. } => (GGRS_REQ_LOAD, *frame),
@@ -325,8 +426,17 @@ impl BatchedBoxGame {
     }
 }
 
+/// The failures collected from an earlier deferred batch followed by this call's.
+fn merge_failed(mut earlier: Vec<(usize, usize)>, now: Option<FailedLanes>) -> Option<FailedLanes> {
+    if let Some(f) = now {
+        earlier.extend(f.lanes);
+    }
+    if earlier.is_empty() { None } else { Some(FailedLanes { lanes: earlier }) }
+}
+
 impl Drop for BatchedBoxGame {
     fn drop(&mut self) {
+        let _ = self.flush();  // a deferred batch's checksums still reach their cells
         unsafe { ggrs_engine_destroy(self.eng) };
     }
 }

@@ -482,3 +482,43 @@ def test_csr_growth_invalidates_batch_views(oracle):
         assert b.encode(l, [(REQ_SAVE, n), (REQ_ADVANCE, 0)], np.ones((1, P), np.uint8), None, n) == -1
     assert b.run(1, 0, 1, 1) == 0
     assert (eng.lane_frames() == n + 1).all()
+
+
+@pytest.mark.parametrize("deferred", [False, True])
+def test_batched_handler_cells(oracle, deferred):
+    """ggrs_amd.handler.BatchedHandler (the Rust crate's BatchedBoxGame mirrored) over the engine's
+    lane batch and lane server: every SaveGameState's checksum reaches its GameStateCell in request
+    order -- at once, or (deferred, P2P sessions) on the next call -- and equals the oracle
+    handler's (Game::handle_requests, ex_game.rs:79-127)."""
+    from ggrs_amd import Engine
+    from ggrs_amd.handler import BatchedHandler, GameStateCell
+    L, calls, P, maxp = 128, 60, 2, 8
+    streams = p2p_lane_streams(oracle, L, calls, P, maxp, seed=41)
+    exp = expected(oracle, streams, P, maxp)
+    eng = Engine(L, P, maxp, 0, 0)
+    h = BatchedHandler(L, P, lambda shape: eng.lane_batch(*shape), deferred=deferred)
+    cells = [[] for _ in range(L)]  # every saved cell of lane l, in request order
+    prev = []
+    for c in range(calls):
+        lists, saved = [], []
+        for l, s in enumerate(streams):
+            x = []
+            for i in np.nonzero(s["call_of"] == c)[0]:
+                k, f = int(s["kind"][i]), int(s["frame"][i])
+                if k == REQ_ADVANCE:
+                    x.append(("advance", s["inputs"][i], s["status"][i]))
+                else:
+                    cell = GameStateCell()  # one cell object per request: it holds that save's value
+                    x.append(("save" if k == REQ_SAVE else "load", cell, f))
+                    if k == REQ_SAVE:
+                        saved.append(cell)
+                        cells[l].append(cell)
+            lists.append(x)
+        assert h.handle_requests(lists) == []
+        assert all((cell.checksum is None) == deferred for cell in saved)
+        assert all(cell.checksum is not None for cell in prev)  # the previous call's, collected
+        prev = saved
+    assert h.flush() == []
+    for l in range(L):
+        assert [cell.checksum for cell in cells[l]] == exp[l]["save_cks"].tolist(), f"lane {l}"
+    check_final(eng, exp, range(0, L, 9))

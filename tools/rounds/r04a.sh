@@ -19,4 +19,11 @@ GGRS_BENCH_DIST=1 timeout -k 10 300 python -u -m torch.distributed.run --nnodes=
   --master-addr 127.0.0.1 --master-port 29611 bench.py --no-cpu-baseline \
   > gpurun_out/bench_${TAG}_dist1.json 2> gpurun_out/bench_${TAG}_dist1.err || { tail -20 gpurun_out/bench_${TAG}_dist1.err; exit 13; }
 cat gpurun_out/bench_${TAG}_dist1.json
+i=0
+for a in "--req-groups 1" "--req-groups 1 --req-deferred" "--req-groups 1 --session-us 20" "--req-groups 1 --session-us 20 --req-deferred" "--req-groups 2 --req-threads 8 --req-deferred" "--req-groups 1 --req-threads 8 --req-deferred --session-us 20"; do
+  timeout -k 10 200 python -u bench.py --workload requests --req-form p2p --no-cpu-baseline $a \
+    > gpurun_out/bench_${TAG}_req$i.json 2> gpurun_out/bench_${TAG}_req$i.err || { tail -20 gpurun_out/bench_${TAG}_req$i.err; exit 14; }
+  python3 -c "import json,sys; d=json.load(open(sys.argv[1])); c=d['config']; print(sys.argv[2], '%.4g' % d['value'], c['us_per_call'], c.get('us_per_call_host_encode_device_handback_session'))" gpurun_out/bench_${TAG}_req$i.json "$a"
+  i=$((i+1))
+done
 echo r04a done
