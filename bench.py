@@ -1211,7 +1211,7 @@ def main():
     ap.add_argument("--peers", action="store_true",
                     help="configs 3/4 and p2p: rank r and r + world/2 run the same sessions (the two "
                          "machines of a match) and compare checksums exchanged over the process group")
-    ap.add_argument("--p2p-form", choices=["default", "flat", "lockstep", "unstaged"], default="default",
+    ap.add_argument("--p2p-form", choices=["default", "flat", "lockstep", "unstaged", "chains"], default="default",
                     help="p2p: kernel form (DESIGN.md section 3)")
     ap.add_argument("--sparse", action="store_true", help="p2p: sparse saving (SURVEY.md 8f row 4)")
     ap.add_argument("--latency", type=int, default=4, help="p2p: frames the remote player's inputs arrive late")

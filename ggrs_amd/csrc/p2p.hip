@@ -726,6 +726,191 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
   if (kSparse) p.last_saved[sess] = last_saved;
 }
 
+// ------------------------------------------------------------------------------------------
+// Chains form (few sessions: the flat kernel runs one thread per session, so 4096 sessions fill 64
+// of the chip's 1024 SIMDs).  With the remote inputs of frame g arriving exactly at call g + D,
+// the state a call works on is a function of the inputs alone: after call c every remote player's
+// input of frame h is the real one for h <= g = c - D and the prediction made from frame g after
+// it (repeat-last: input[g]; PredictDefault: 0; lib.rs:390-406) -- a misprediction rolls back to
+// g and replays with exactly those inputs (adjust_gamestate, p2p_session.rs:658-714), and without
+// one every confirmation matched the prediction, so the frames already simulated used them too.
+// So call c = LoadGameState(g) of the confirmed state T_g (cell g holds it from call c - 1 on),
+// then D + 1 advances: frame g with the real remote inputs, frames g + 1 .. c with the prediction
+// input[g] -- whether or not the reference rolls back at c -- exactly the chain of a SyncTest call
+// with check_distance D, except that the predicted remote inputs differ per chain.  The kernel runs
+// it as the v4 SyncTest pipeline: per session K = D + 1 chain roles x Pp player lanes; at step t
+// role j holds chain t - j at frame t - D and advances it with the local input of frame t - D and
+// the remote input of frame t - D - j (role 0: the confirmed input of frame t - D; roles j >= 1:
+// the prediction of chain t - j, repeat-last input[t - j - D]); then the chains move one role up
+// and role 0 keeps its own: T_{t-D+1}, which chain t + 1 loads at step t + 1.
+// Ring: after call c the cell of every frame h in (g, c] holds chain c's state at h (a cell
+// re-saved by a rollback gets chain c's state; one not re-saved already held the same bytes, for
+// the reason above), and the cells of frames <= g hold the confirmed states.  So frame t - D + 1
+// is stored once, at step t, by the newest chain of the launch that holds it (role 0 inside the
+// launch, role t - (f0 + n - 1) in its tail), with its Fletcher-16 -- the cell the reference ends
+// the launch with.  Rollbacks (a remote input of frame t - D unlike the prediction made for it,
+// counted by role 0) and resimulated frames (D per rollback) are the reference's; the queue's
+// prediction state is written in its canonical form at the end.  Preconditions (host): plain
+// launches (no desync detection, trace or debug flip, never sparse saving), f0 >= D (the first D
+// calls run on the flat kernel), K * Pp <= 64.
+constexpr uint32_t kChainOob = 0x40000000u;  // past every descriptor's range: a lane that never stores
+constexpr int kChainLdsRows = 16 * 1024;      // bytes of staged input rows per block
+
+template <int P>
+__global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t spw) {
+  constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
+  constexpr int F = state_fields(P);
+  constexpr int C = cell_dwords(P);
+  constexpr int n_bytes = Fletcher<P>::n;
+  extern __shared__ uint8_t lds_rows[];  // [rows][spw * Pp]: input rows lo .. f0 + n - 1
+  const int D = p.D, G = (D + 1) * Pp;
+  const int wl = threadIdx.x;
+  const int g = wl / G, r = wl - g * G;
+  const int j = r / Pp, pl = r - j * Pp;  // static role, player lane
+  const int64_t S = p.S;
+  const int64_t s0 = xcd_block(blockIdx.x, gridDim.x) * spw;
+  const int nsess = (int)((S - s0) < spw ? (S - s0) : spw);
+  const bool valid = g < nsess;
+  const bool owner = valid && pl < P;
+  const int64_t s = valid ? s0 + g : s0;
+  const int plc = pl < P ? pl : 0;
+  const bool local = ((p.local_mask >> plc) & 1u) != 0;
+  const int kq[5] = {fld_x(P, plc), fld_y(P, plc), fld_vx(P, plc), fld_vy(P, plc), fld_rot(P, plc)};
+  const int row_bytes = spw * Pp;
+  // rows lo .. f0 + n - 1: role D reads frame t - 2D, the local players user input t - D - delay
+  const int32_t lo = p.f0 - 2 * D - p.delay;
+  const int32_t nrows = p.f0 + p.n - lo;
+  {
+    const int used = nsess * Pp;
+    for (int i = wl; i < nrows * row_bytes; i += kWave) {
+      const int rr = i / row_bytes, b = i - rr * row_bytes;
+      const int32_t row = lo + rr;
+      lds_rows[i] = (row >= 0 && b < used) ? p.inputs[((int64_t)(row % p.cap) * S + s0) * Pp + b] : (uint8_t)0;
+    }
+  }
+  // every role starts from T_{f0-D}, the cell chain f0 loads (roles > 0 hold chains of the previous
+  // launch: stepped, never stored)
+  uint32_t w[5];
+  {
+    const uint32_t* cell = p.ring + ((int64_t)s * p.R + (p.f0 - D) % p.R) * C;
+#pragma unroll
+    for (int q = 0; q < 5; q++) w[q] = cell[kq[q]];
+  }
+  // the remote players' prediction before the launch (the input of frame f0 - 1 - D, or 0)
+  uint32_t prev_in = (uint32_t)p.queue[(1 * P + plc) * S + s];
+  __syncthreads();
+  const bool lean_ok = __all(w[4] <= kTwoPiBits);
+  // the input a lane's chain reads at step t: row t - back
+  const int32_t back = local ? D + p.delay : D + j;
+  const bool zero_in = !local && j >= 1 && p.predictor != 0;  // PredictDefault's prediction
+  const int in_col = valid ? g * Pp + (pl < P ? pl : 0) : 0;  // (lanes past the wave's sessions: column 0)
+  // store offsets: a lane's fields of its session's cell (session-major ring, slot offset in soffset)
+  const uint32_t cell_base = (uint32_t)((uint64_t)s * p.R * C * 4);
+  uint32_t fo[5];
+#pragma unroll
+  for (int q = 0; q < 5; q++) fo[q] = owner ? cell_base + (uint32_t)kq[q] * 4 : kChainOob;
+  const bool lead = valid && pl == 0;  // the session's frame field, checksum and padding
+  const uint32_t fo_frame = lead ? cell_base : kChainOob;
+  const uint32_t fo_ck = lead ? cell_base + F * 4 : kChainOob;
+  const __amdgpu_buffer_rsrc_t rs_ring =
+      __builtin_amdgcn_make_buffer_rsrc(p.ring, (short)0, (int)((uint64_t)S * p.R * C * 4), 0x00020000);
+  uint32_t wt[5];
+#pragma unroll
+  for (int q = 0; q < 5; q++) wt[q] = owner ? 2u * weights_at(n_bytes, fld_offset(P, kq[q])) : 0u;
+  const uint32_t one2 = owner ? 0x02020202u : 0u;
+  const uint32_t wf1 = pl == 0 ? 0x02020202u : 0u, wf2 = pl == 0 ? 2u * weights_at(n_bytes, 0) : 0u;
+  const uint32_t c1 = pl == 0 ? 2u * Fletcher<P>::kSum1Const : 0u;
+  const uint32_t c2 = pl == 0 ? 2u * Fletcher<P>::kSum2Const : 0u;
+  const int src_rot = (j == 0 ? wl : g * G + (j - 1) * Pp + pl) * 4;
+  const bool counts = valid && j == 0 && pl < P && !local;  // role 0's remote lanes see each arrival
+  const uint32_t pmask = (1u << Pp) - 1u;
+  const int gbase = g * G;
+  int32_t rollbacks = 0;
+  const int32_t t_last = p.f0 + p.n - 1;  // the launch's last call
+  const int32_t t_end = t_last + D + 1;
+  int32_t slot = __builtin_amdgcn_readfirstlane((p.f0 - D + 1) % p.R);  // slot of frame t - D + 1
+  for (int32_t t = p.f0; t < t_end; ++t) {
+    const int32_t row = t - back;
+    const uint32_t in = (row >= 0 && !zero_in) ? (uint32_t)lds_rows[(row - lo) * row_bytes + in_col] : 0u;
+    if (t <= t_last) {
+      // poll of call t: the arriving input of frame t - D against the prediction made for it
+      // (add_input_by_frame, input_queue.rs:190-230); any remote player's miss rolls the session back
+      const bool miss = counts && in != (p.predictor == 0 ? prev_in : 0u);
+      const uint64_t mb = __ballot(miss);
+      if (j == 0 && pl == 0 && valid && ((uint32_t)(mb >> gbase) & pmask)) rollbacks += 1;
+      prev_in = in;
+    }
+    // AdvanceFrame(t - D) of chain t - j
+    {
+      float x = __builtin_bit_cast(float, w[0]), y = __builtin_bit_cast(float, w[1]);
+      float vx = __builtin_bit_cast(float, w[2]), vy = __builtin_bit_cast(float, w[3]);
+      float rot = __builtin_bit_cast(float, w[4]);
+      if (lean_ok) advance_player_lean(x, y, vx, vy, rot, in);
+      else advance_player(x, y, vx, vy, rot, in);
+      w[0] = __builtin_bit_cast(uint32_t, x);
+      w[1] = __builtin_bit_cast(uint32_t, y);
+      w[2] = __builtin_bit_cast(uint32_t, vx);
+      w[3] = __builtin_bit_cast(uint32_t, vy);
+      w[4] = __builtin_bit_cast(uint32_t, rot);
+    }
+    uint32_t nx[5];
+#pragma unroll
+    for (int q = 0; q < 5; q++) nx[q] = (uint32_t)__builtin_amdgcn_ds_bpermute(src_rot, (int)w[q]);
+    __builtin_amdgcn_sched_barrier(0);  // the rotation's LDS latency behind the checksum and stores
+    const uint32_t frame1 = (uint32_t)(t - D + 1);
+    const int js = t > t_last ? t - t_last : 0;  // the newest chain of the launch holding frame1
+    if (js < D) {
+      uint32_t d1 = dot4_u8(frame1, wf1, c1), d2 = dot4_u8(frame1, wf2, c2);
+#pragma unroll
+      for (int q = 0; q < 5; q++) {
+        d1 = dot4_u8(w[q], one2, d1);
+        d2 = dot4_u8(w[q], wt[q], d2);
+      }
+      if constexpr (Pp >= 2) {
+        d1 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d1, 0xB1, 0xF, 0xF, true);  // xor 1
+        d2 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d2, 0xB1, 0xF, 0xF, true);
+      }
+      if constexpr (Pp >= 4) {
+        d1 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d1, 0x4E, 0xF, 0xF, true);  // xor 2
+        d2 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d2, 0x4E, 0xF, 0xF, true);
+      }
+      const uint32_t ck = fletcher_from_doubled(d1, d2);
+      const bool me = j == js;
+      const uint32_t so = (uint32_t)slot * (uint32_t)(C * 4);
+#pragma unroll
+      for (int q = 0; q < 5; q++) __builtin_amdgcn_raw_buffer_store_b32(w[q], rs_ring, me ? fo[q] : kChainOob, so, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(frame1, rs_ring, me ? fo_frame : kChainOob, so, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(ck, rs_ring, me ? fo_ck : kChainOob, so, 0);
+#pragma unroll
+      for (int k = F + 1; k < C; k++) __builtin_amdgcn_raw_buffer_store_b32(0u, rs_ring, me ? fo_ck + (k - F) * 4 : kChainOob, so, 0);
+    } else if (t == t_end - 1 && j == D) {
+      // role D: chain f0 + n - 1 after its call's own AdvanceFrame -- the current state
+      if (owner) {
+#pragma unroll
+        for (int q = 0; q < 5; q++) p.cur[(int64_t)kq[q] * S + s] = w[q];
+      }
+      if (lead) p.cur[s] = frame1;
+    }
+#pragma unroll
+    for (int q = 0; q < 5; q++) w[q] = nx[q];
+    slot = slot + 1 == p.R ? 0 : slot + 1;
+  }
+  if (valid && j == 0 && pl == 0) {
+    p.rollbacks[s] += rollbacks;
+    p.resim[s] += (int64_t)rollbacks * D;
+  }
+  if (counts) {
+    // the remote queue after call f0 + n - 1 (canonical): predicting from frame g + 1 with the
+    // input of frame g = f0 + n - 1 - D, no incorrect frame, last request = the call's own frame
+    const int32_t gl = t_last - D;
+    const uint32_t last_in = (uint32_t)lds_rows[(gl - lo) * row_bytes + in_col];
+    p.queue[(0 * P + plc) * S + s] = gl + 1;
+    p.queue[(1 * P + plc) * S + s] = (int32_t)(p.predictor == 0 ? last_in : 0u);
+    p.queue[(2 * P + plc) * S + s] = kNull;
+    p.queue[(3 * P + plc) * S + s] = t_last;
+  }
+}
+
 // Lockstep mode (max_prediction 0; builder.rs:134-147, p2p_session.rs:301-310,393-407): a call
 // never saves, loads or resimulates; it advances only when the current frame's inputs are confirmed
 // from every player.  Which calls advance, and which input rows their AdvanceFrame reads, depend
@@ -805,7 +990,9 @@ struct ggrs_p2p_engine {
   int64_t dbg_sess = -1;
   int32_t dbg_frame = -1;
   int32_t sparse = 0;
-  int32_t form = 0;  // ggrs_p2p_set_unstaged: 0 default (flat), 1 global input reads, 2 lockstep staged
+  int32_t form = 0;  // ggrs_p2p_set_unstaged: 0 default (flat, or chains for few sessions), 1 global
+                     // input reads, 2 lockstep staged, 3 flat with HBM rings, 4 chains
+  bool dbg_ever = false;  // a debug flip was armed: the states may no longer be the canonical ones
   int32_t* last_saved = nullptr;  // [S], sparse saving only
   int32_t* ring_frame = nullptr;  // [R][S], sparse saving only
   // lockstep mode (max_prediction 0): the session-uniform control flow, replayed on the host
@@ -1057,6 +1244,47 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
     e->current_frame += n;
     return GGRS_OK;
   }
+  // the chains form: forced (form 4), or by default when the flat kernel's one thread per session
+  // would leave most SIMDs idle
+  const int P = e->cfg.num_players;
+  const int G = (p.D + 1) * padded_players(P);
+  const bool chains_ok = !e->sparse && e->desync_interval == 0 && !p.trace && !e->dbg_ever && G <= kWave &&
+                         (uint64_t)p.S * e->R * cell_dwords(P) * 4 < ((uint64_t)1 << 30);
+  const bool chains = chains_ok && (e->form == 4 || (e->form == 0 && grid_of(p.S, kFlatBlock) <= e->num_cus));
+  if (e->form == 4 && !chains_ok)
+    return set_error(GGRS_E_STATE, "the chains form needs plain launches (no desync detection, trace, debug flip or "
+                                   "sparse saving), (remote_latency + 1) x padded players <= 64 lanes and a ring < 1 GiB");
+  if (chains) {
+    if (p.f0 < p.D) {  // the first D calls (no remote input yet) on the flat kernel
+      const int32_t m = std::min(n, p.D - p.f0);
+      const int32_t form = e->form;
+      e->form = 3;
+      int rc = ggrs_p2p_advance_frames(e, m);
+      e->form = form;
+      if (rc || m == n) return rc;
+      return ggrs_p2p_advance_frames(e, n - m);
+    }
+    const int spw = kWave / G;
+    const int row_bytes = spw * padded_players(P);
+    // a launch's rows (f0 - 2D - delay .. f0 + n - 1) must fit the block's LDS: longer runs split
+    const int32_t max_n = kChainLdsRows / row_bytes - 2 * p.D - p.delay;
+    if (max_n < 1) return set_error(GGRS_E_INVALID, "remote_latency / input_delay too large for the chains form");
+    if (n > max_n) {
+      int rc = ggrs_p2p_advance_frames(e, max_n);
+      if (rc) return rc;
+      return ggrs_p2p_advance_frames(e, n - max_n);
+    }
+    const size_t lds = (size_t)(n + 2 * p.D + p.delay) * row_bytes;
+    int rc = p2p_launch_timed(e, [&] {
+      dispatch_players(P, [&](auto PC) {
+        constexpr int PP = decltype(PC)::value;
+        p2p_chains_kernel<PP><<<(unsigned)grid_of(p.S, spw), kWave, lds, e->stream>>>(p, spw);
+      });
+    });
+    if (rc) return rc;
+    e->current_frame += n;
+    return GGRS_OK;
+  }
   int rc = p2p_launch_timed(e, [&] {
     // stage input rows in LDS unless a call reaches further back than a stage holds
     const int32_t back = (e->sparse ? e->R - 1 : p.D) + p.delay;
@@ -1154,8 +1382,8 @@ int ggrs_p2p_set_sparse_saving(ggrs_p2p_engine_t* e, int32_t on) {
 
 int ggrs_p2p_set_unstaged(ggrs_p2p_engine_t* e, int32_t form) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
-  if (form < 0 || form > 3)
-    return set_error(GGRS_E_INVALID, "kernel form %d (0 default, 1 unstaged, 2 lockstep, 3 flat)", form);
+  if (form < 0 || form > 4)
+    return set_error(GGRS_E_INVALID, "kernel form %d (0 default, 1 unstaged, 2 lockstep, 3 flat, 4 chains)", form);
   e->form = form;
   return GGRS_OK;
 }
@@ -1165,6 +1393,7 @@ int ggrs_p2p_debug_desync(ggrs_p2p_engine_t* e, int32_t session, int32_t frame) 
   if (session >= e->cfg.num_sessions) return set_error(GGRS_E_INVALID, "session out of range");
   e->dbg_sess = session;
   e->dbg_frame = session < 0 ? -1 : frame;
+  if (session >= 0) e->dbg_ever = true;
   return GGRS_OK;
 }
 

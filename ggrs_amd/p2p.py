@@ -208,7 +208,7 @@ class P2PEngine:
         _lib.check(self._L.ggrs_p2p_set_sparse_saving(self._h, int(bool(on))))
         self.sparse_saving = bool(on)
 
-    KERNEL_FORMS = {"default": 0, "unstaged": 1, "lockstep": 2, "flat": 3}
+    KERNEL_FORMS = {"default": 0, "unstaged": 1, "lockstep": 2, "flat": 3, "chains": 4}
 
     def set_unstaged(self, on=True):
         """Calls in lockstep with input rows read from global memory (for comparison)."""
@@ -216,7 +216,9 @@ class P2PEngine:
 
     def set_kernel_form(self, form):
         """"default" (flat whenever input rows can be staged, with the block's session rings in LDS
-        for the launch where they fit 28 KB), "flat" (each session's calls as its own step sequence,
-        rings in HBM), "lockstep" (calls in lockstep, rows staged in LDS) or "unstaged" (lockstep,
-        rows from global memory)."""
+        for the launch where they fit; the chains form instead when the sessions fill at most one
+        wave per CU), "flat" (each session's calls as its own step sequence, rings in HBM),
+        "lockstep" (calls in lockstep, rows staged in LDS), "unstaged" (lockstep, rows from global
+        memory) or "chains" (every call as a chain of remote_latency + 1 advances from the confirmed
+        state, chains pipelined over lanes; plain launches only)."""
         _lib.check(self._L.ggrs_p2p_set_unstaged(self._h, self.KERNEL_FORMS[form]))

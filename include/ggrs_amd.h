@@ -501,7 +501,13 @@ int ggrs_p2p_set_sparse_saving(ggrs_p2p_engine_t* eng, int32_t on);
  * step sequence, input rows staged in LDS, with or without sparse saving), 1 = calls in
  * lockstep with input rows read from global memory, 2 = calls in lockstep with staged rows,
  * 3 = the flattened form with the session rings in HBM (the default keeps a block's rings in LDS
- * for the launch when R x cell x 64 sessions fits 28 KB, else it runs this form) */
+ * for the launch when they fit beside the other blocks on the CU, else it runs this form),
+ * 4 = chains: every call as the chain of remote_latency + 1 advances from the confirmed state that
+ * the fixed-latency network makes it (LoadGameState(f - D), D frames replayed, the call's own
+ * advance), (D + 1) x players lanes per session, for engines whose sessions would fill at most one
+ * wave per CU in the flattened form (the default picks it there); plain launches only -- no desync
+ * detection, trace, debug flip or sparse saving (GGRS_E_STATE when forced otherwise); the first D
+ * calls run on the flattened form.  Same states, rings, statistics and queues as every other form. */
 int ggrs_p2p_set_unstaged(ggrs_p2p_engine_t* eng, int32_t form);
 /* test hook: the AdvanceFrame from `frame` of `session` flips the lowest bit of player 0's x on
  * every (re)simulation -- a deterministic desync of this peer (session -1: off) */

@@ -201,7 +201,7 @@ def test_full_size_p2p_bench_config(oracle):
     assert rb.sum() > S  # rollbacks happen throughout
 
 
-@pytest.mark.parametrize("form", ["default", "flat"])
+@pytest.mark.parametrize("form", ["default", "flat", "chains"])
 def test_config2_p2p_shape(oracle, form):
     """BASELINE config 2 in its P2P form: 4096 sessions, 2 players, the remote
     player's inputs 8 frames late, max_prediction 9, repeat-last prediction
@@ -212,13 +212,48 @@ def test_config2_p2p_shape(oracle, form):
     S, frames, P = 4096, 192, 2
     rows = synth.gen_inputs(0, S, frames, P, synth.MODEL_HELD)
     eng = P2PEngine(S, num_players=P, local_players=(0,), input_delay=0, max_prediction=9, remote_latency=8,
-                    input_capacity=frames + 10, trace_capacity=frames)
+                    input_capacity=frames + 10)
     eng.set_kernel_form(form)
     eng.add_inputs(0, rows)
     for _ in range(frames // 64):
         eng.advance_frames(64)
     rng = np.random.default_rng(4)
     sessions = sorted(set([0, 1, 63, 64, 2047, S - 1] + rng.integers(0, S, 10).tolist()))
-    check_against_oracle(eng, rows, sessions, frames)
+    check_against_oracle(eng, rows, sessions, frames, trace=False)
     rb, rs = eng.stats()
     assert rb.sum() > 0 and rs.sum() >= 8 * rb.sum() - 8 * S  # rollbacks of up to 8 frames
+
+
+@pytest.mark.parametrize("P,local,delay,mp,D,pred,model", CASES)
+def test_p2p_chains_form_matches_oracle(oracle, P, local, delay, mp, D, pred, model):
+    """The chains form (every call as the chain of D + 1 advances from the confirmed state,
+    pipelined over (D + 1) x players lanes per session) in launches of uneven length -- the first
+    D calls on the flattened form, launches shorter than D, a launch split for its LDS rows --
+    then alternating with the flattened form: states, rings, rollback and resimulation counts
+    bit-exact against the oracle's P2PSession after every launch."""
+    from ggrs_amd import P2PEngine
+    S, frames = 300, 170
+    rows = stream(S, frames, P, model, seed_base=0x6060)
+    eng = P2PEngine(S, num_players=P, local_players=local, input_delay=delay, max_prediction=mp,
+                    remote_latency=D, predictor=pred, input_capacity=frames + 8)
+    eng.add_inputs(0, rows)
+    done = 0
+    for k, (n, form) in enumerate([(2, "chains"), (1, "chains"), (9, "chains"), (40, "chains"), (3, "flat"),
+                                   (1, "chains"), (50, "chains"), (20, "flat"), (44, "chains")]):
+        eng.set_kernel_form(form)
+        eng.advance_frames(n)
+        done += n
+        if k in (3, 6, 8):
+            check_against_oracle(eng, rows[:done], [0, 1, 63, 64, 150, 299], done, trace=False)
+    assert done == frames
+
+
+def test_p2p_chains_form_rejects_non_plain(oracle):
+    """Forcing the chains form where it does not apply is an error, not a silent fallback."""
+    from ggrs_amd import P2PEngine
+    from ggrs_amd._lib import GgrsError
+    eng = P2PEngine(8, num_players=2, local_players=(0,), max_prediction=8, remote_latency=4, trace_capacity=16)
+    eng.add_inputs(0, stream(8, 16, 2, 1))
+    eng.set_kernel_form("chains")
+    with pytest.raises(GgrsError):
+        eng.advance_frames(8)

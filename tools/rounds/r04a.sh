@@ -6,12 +6,20 @@ TAG=${1:-r04a}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R && mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
-  tests/test_gpu_exchange.py tests/test_abi.py "tests/test_gpu_p2p.py::test_config2_p2p_shape" tests/test_gpu_branch.py tests/test_gpu_lane_requests.py \
+  tests/test_gpu_exchange.py tests/test_abi.py tests/test_gpu_p2p.py tests/test_gpu_branch.py tests/test_gpu_lane_requests.py \
   > gpurun_out/pytest_$TAG.log 2>&1 || { tail -30 gpurun_out/pytest_$TAG.log; exit 10; }
 tail -3 gpurun_out/pytest_$TAG.log
 timeout -k 10 300 python -u bench.py --workload p2p --sessions 4096 --latency 8 --max-prediction 9 \
   > gpurun_out/bench_${TAG}_p2pc2.json 2> gpurun_out/bench_${TAG}_p2pc2.err || { tail -20 gpurun_out/bench_${TAG}_p2pc2.err; exit 11; }
 cat gpurun_out/bench_${TAG}_p2pc2.json
+timeout -k 10 300 python -u bench.py --workload p2p --sessions 4096 --latency 8 --max-prediction 9 --p2p-form flat --no-cpu-baseline \
+  > gpurun_out/bench_${TAG}_p2pc2flat.json 2> gpurun_out/bench_${TAG}_p2pc2flat.err || { tail -20 gpurun_out/bench_${TAG}_p2pc2flat.err; exit 11; }
+cat gpurun_out/bench_${TAG}_p2pc2flat.json
+for S in 16384 65536; do
+timeout -k 10 300 python -u bench.py --workload p2p --sessions $S --p2p-form chains --no-cpu-baseline \
+  > gpurun_out/bench_${TAG}_p2pch$S.json 2> gpurun_out/bench_${TAG}_p2pch$S.err || { tail -20 gpurun_out/bench_${TAG}_p2pch$S.err; exit 11; }
+python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], '%.4g' % d['value'], d['roofline']['avg_launch_ms'])" gpurun_out/bench_${TAG}_p2pch$S.json chains$S
+done
 GGRS_BENCH_BACKEND=gloo timeout -k 10 300 python -u bench.py --gpus 2 --steps 10 \
   > gpurun_out/bench_${TAG}_gloo2.json 2> gpurun_out/bench_${TAG}_gloo2.err || { tail -20 gpurun_out/bench_${TAG}_gloo2.err; exit 12; }
 cat gpurun_out/bench_${TAG}_gloo2.json
