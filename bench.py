@@ -378,6 +378,31 @@ def run_branch(args):
     elapsed = t1 - t0
     n_desync = int(ex.desync_count.item()) if ex is not None else 0
     resim_round = L * W + S
+    general = None
+    if args.config == 3 and ex is None:
+        # the same rounds without player separability (round form "full": every lane replays every
+        # player of its window and saves every logical cell, what a game whose players interact needs;
+        # GGRS's Config::State contract gives no separability) -- beside the headline, not in it
+        g_eng = BranchEngine(S, num_players=P, remote_mask=c["remote_mask"], window=W, branches=B,
+                             alphabet=16, input_capacity=rounds + W + 3, device=local_rank)
+        g_eng.add_inputs(0, truth)
+        g_eng.set_round_form("full")
+        for _ in range(args.warmup):
+            g_eng.rounds(rps)
+        g_eng.synchronize()
+        g_eng.timing_reset()
+        tg0 = time.perf_counter()
+        for _ in range(args.steps):
+            g_eng.rounds(rps)
+        g_eng.timing_stop()
+        g_eng.synchronize()
+        tg = time.perf_counter() - tg0
+        g_ms, g_launches = g_eng.timing_read()
+        general = {"general_form_frames_per_s": round(resim_round * rps * args.steps / tg, 1),
+                   "us_per_round": round(tg / (rps * args.steps) * 1e6, 3),
+                   "kernel_us_per_round": round(g_ms * 1e3 / (rps * args.steps), 3),
+                   "kernel": "rounds_kernel (fused rounds, every lane all players, every logical save)"}
+        g_eng.close()
     elapsed, total, per_rank = rank_timings(dist, torch, elapsed, resim_round * rps * args.steps)
     value = total / elapsed
     Sp = 4 + 20 * P
@@ -440,6 +465,9 @@ def run_branch(args):
                          "avg_kernel_ms_per_round": round(avg_round_s * 1e3, 4)},
             "cpu_baseline": cpu_baseline, "parity": parity,
         }
+        if general is not None:
+            line["general_form"] = general
+            line["config"]["general_form_frames_per_s"] = general["general_form_frames_per_s"]
         print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
@@ -1211,7 +1239,8 @@ def main():
     ap.add_argument("--peers", action="store_true",
                     help="configs 3/4 and p2p: rank r and r + world/2 run the same sessions (the two "
                          "machines of a match) and compare checksums exchanged over the process group")
-    ap.add_argument("--p2p-form", choices=["default", "flat", "lockstep", "unstaged", "chains"], default="default",
+    ap.add_argument("--p2p-form", choices=["default", "flat", "lockstep", "unstaged", "chains", "flat_queues", "canonical"],
+                    default="default",
                     help="p2p: kernel form (DESIGN.md section 3)")
     ap.add_argument("--sparse", action="store_true", help="p2p: sparse saving (SURVEY.md 8f row 4)")
     ap.add_argument("--latency", type=int, default=4, help="p2p: frames the remote player's inputs arrive late")

@@ -51,7 +51,7 @@ EXPORTS = (
     "ggrs_particle_timing_reset", "ggrs_particle_timing_stop", "ggrs_particle_timing_read",
     "ggrs_p2p_engine_create", "ggrs_p2p_engine_destroy", "ggrs_p2p_engine_config",
     "ggrs_p2p_add_inputs", "ggrs_p2p_advance_frames", "ggrs_p2p_current_frame", "ggrs_p2p_calls",
-    "ggrs_p2p_synchronize", "ggrs_p2p_read_state", "ggrs_p2p_read_ring", "ggrs_p2p_read_stats",
+    "ggrs_p2p_synchronize", "ggrs_p2p_read_state", "ggrs_p2p_read_ring", "ggrs_p2p_read_stats", "ggrs_p2p_read_queues",
     "ggrs_p2p_read_trace", "ggrs_p2p_timing_reset", "ggrs_p2p_timing_stop", "ggrs_p2p_timing_read",
     "ggrs_p2p_set_desync_detection", "ggrs_p2p_local_checksums", "ggrs_p2p_compare_checksums",
     "ggrs_p2p_debug_desync", "ggrs_p2p_set_sparse_saving", "ggrs_p2p_set_unstaged",

@@ -727,6 +727,172 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_flat_kernel(P2PParams p) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Canonical flat form (plain launches, full saving, f0 >= D: the default for many sessions).  With
+// the remote inputs of frame g arriving exactly at call g + D, the InputQueue state the flat
+// kernel carries is a function of the inputs (the chains form's argument, below): before call c
+// the prediction made for frame g = c - D is the input of frame g - 1 (repeat-last; 0 for
+// PredictDefault), so call c rolls back iff some remote player's input of frame g differs from it
+// (add_input_by_frame's first_incorrect, input_queue.rs:190-230 -- always frame g); a rollback
+// loads cell g and replays frames g .. c - 1, frame g with the confirmed remote inputs and every
+// later frame -- like the call's own -- with the prediction made from frame g (lib.rs:390-406);
+// without one every frame keeps that prediction.  So each call is: one LDS row read, one compare,
+// then the same Loads, Saves and AdvanceFrames as the reference in the same order, with none of the
+// per-player queue bookkeeping (pred_frame / first_incorrect / last_requested updates and selects)
+// in the step loop; the queues are written back in their canonical form at the end.  Rings in LDS
+// as the kLds flat kernel (every step saves: the first replay step rewrites the loaded cell with its
+// own bytes), input rows staged per stage of calls.
+template <int P, int kLocal>
+__global__ __launch_bounds__(kFlatBlock) void p2p_canon_kernel(P2PParams p) {
+  const uint32_t lmask = kLocal >= 0 ? (uint32_t)kLocal : p.local_mask;
+  constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
+  constexpr int kRows = flat_rows_lds<P>();
+  constexpr int PC = cell_dwords(P) / 4;
+  constexpr int F = state_fields(P);
+  __shared__ __attribute__((aligned(16))) uint8_t lds_rows[kRows * kFlatBlock * Pp];
+  extern __shared__ uint4 lds_ring[];  // [R][PC][kFlatBlock]
+  const int64_t sess0 = (int64_t)blockIdx.x * kFlatBlock;
+  const int64_t S = p.S;
+  const bool live = sess0 + threadIdx.x < S;
+  const int64_t sess = live ? sess0 + threadIdx.x : sess0;
+  const int nb = (int)((S - sess0) < kFlatBlock ? (S - sess0) : kFlatBlock);
+  const int lt = threadIdx.x;
+  const int tid = live ? lt : 0;
+  // byte masks of the local and remote players' inputs in a packed row
+  uint32_t lbytes = 0;
+#pragma unroll
+  for (int k = 0; k < P; k++) lbytes |= ((lmask >> k) & 1u) ? 0xffu << (8 * k) : 0u;
+  const uint32_t rbytes = (P == 4 ? 0xffffffffu : ((1u << (8 * P)) - 1u)) & ~lbytes;
+  BoxState<P> st;
+  load_state<P>(st, p.cur + sess, S);
+  // the prediction in effect before the launch: the remote inputs of frame f0 - 1 - D (canonical
+  // queues; PredictDefault predicts 0)
+  uint32_t prev_rem = 0;
+#pragma unroll
+  for (int k = 0; k < P; k++)
+    if (!((lmask >> k) & 1u)) prev_rem |= ((uint32_t)p.queue[(1 * P + k) * S + sess] & 0xffu) << (8 * k);
+  const int ring_pieces = p.R * PC;
+  {
+    const int n = nb * ring_pieces;
+    const uint4* src = reinterpret_cast<const uint4*>(p.ring) + sess0 * ring_pieces;
+#pragma unroll 4
+    for (int i = lt; i < n; i += kFlatBlock) {
+      const int sl = i / ring_pieces, rem = i - sl * ring_pieces;
+      lds_ring[rem * kFlatBlock + sl] = src[i];
+    }
+  }
+  __syncthreads();
+  auto cell_load = [&](int32_t slot) {
+#pragma unroll
+    for (int k = 0; k < PC; k++) {
+      const uint4 v = lds_ring[(slot * PC + k) * kFlatBlock + lt];
+      const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        if (4 * k + i < F) st.w[4 * k + i] = x[i];
+    }
+  };
+  auto cell_store = [&](int32_t slot) {
+    const uint32_t ck = fletcher16_state<P>(st);
+#pragma unroll
+    for (int k = 0; k < PC; k++) {
+      uint32_t x[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) x[i] = 4 * k + i < F ? st.w[4 * k + i] : (4 * k + i == F ? ck : 0u);
+      lds_ring[(slot * PC + k) * kFlatBlock + lt] = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+  };
+  auto next_slot = [&](int32_t x) { return x + 1 == p.R ? 0 : x + 1; };
+  const bool lean_ok = __all(rot_in_domain<P>(st));
+  int32_t rollbacks = 0;
+  int32_t slot_f = p.f0 % p.R, slot_h = 0;
+  const int32_t f_end = p.f0 + p.n;
+  const int32_t back = p.D + p.delay;
+  const int32_t calls_per_stage = kRows - back;  // >= 1 (host)
+  for (int32_t fs = p.f0; fs < f_end;) {
+    const int32_t chunk_end = min(f_end, fs + calls_per_stage);
+    const int32_t lo = max(0, fs - back);
+    {
+      __syncthreads();
+      const int nrows = chunk_end - lo, row_bytes = nb * Pp;
+      if (nb == kFlatBlock && ((S * Pp) & 15) == 0) {
+        constexpr int kPieces = kFlatBlock * Pp / 16;
+#pragma unroll 4
+        for (int c = lt; c < nrows * kPieces; c += kFlatBlock) {
+          const int r = c / kPieces, k = c - r * kPieces;
+          const uint4* src = reinterpret_cast<const uint4*>(p.inputs + ((int64_t)((lo + r) % p.cap) * S + sess0) * Pp);
+          reinterpret_cast<uint4*>(lds_rows + r * kFlatBlock * Pp)[k] = src[k];
+        }
+      } else {
+        for (int c = lt; c < nrows * row_bytes; c += kFlatBlock) {
+          const int r = c / row_bytes, b = c - r * row_bytes;
+          lds_rows[r * kFlatBlock * Pp + b] = p.inputs[((int64_t)((lo + r) % p.cap) * S + sess0) * Pp + b];
+        }
+      }
+      __syncthreads();
+    }
+    const LdsRowsFlat<P> rows{lds_rows, lo, tid};
+    int32_t f = fs, h = 0, g = 0;
+    bool at_start = true, replaying = false;
+    uint32_t rem_conf = 0, rem_pred = 0;
+    while (f < chunk_end) {
+      if (at_start) {
+        // poll of call f: the remote inputs of frame g = f - D against the prediction made for them
+        g = f - p.D;
+        rem_conf = rows(g) & rbytes;
+        const bool miss = rem_conf != (p.predictor == 0 ? prev_rem : 0u);
+        prev_rem = rem_conf;
+        rem_pred = p.predictor == 0 ? rem_conf : 0u;
+        if (miss) {  // adjust_gamestate: LoadGameState(g), replay g .. f - 1
+          const int32_t sh = slot_f - p.D;
+          slot_h = sh < 0 ? sh + p.R : sh;
+          cell_load(slot_h);
+          h = g;
+          replaying = true;
+          rollbacks += 1;
+        }
+        at_start = false;
+      }
+      const int32_t fr = replaying ? h : f;
+      const uint32_t rem = (replaying && h == g) ? rem_conf : rem_pred;
+      const uint32_t local = fr >= p.delay ? rows(max(fr - p.delay, rows.lo)) & lbytes : 0u;
+      cell_store(replaying ? slot_h : slot_f);  // SaveGameState(fr) (the first replay step: same bytes)
+      if (lean_ok) advance_state_lean<P>(st, local | rem);
+      else advance_state<P>(st, local | rem, 0u);
+      const bool rep = replaying;
+      slot_h = rep ? next_slot(slot_h) : slot_h;
+      h = rep ? h + 1 : h;
+      replaying = rep && h != f;
+      slot_f = rep ? slot_f : next_slot(slot_f);
+      f = rep ? f : f + 1;
+      at_start = !rep;
+    }
+    fs = chunk_end;
+  }
+  __syncthreads();
+  {
+    const int n = nb * ring_pieces;
+    uint4* dst = reinterpret_cast<uint4*>(p.ring) + sess0 * ring_pieces;
+    for (int i = lt; i < n; i += kFlatBlock) {
+      const int sl = i / ring_pieces, rem = i - sl * ring_pieces;
+      dst[i] = lds_ring[rem * kFlatBlock + sl];
+    }
+  }
+  if (!live) return;
+  store_state<P>(st, p.cur + sess, S);
+  const int32_t t_last = f_end - 1;
+#pragma unroll
+  for (int k = 0; k < P; k++) {
+    if ((lmask >> k) & 1u) continue;
+    p.queue[(0 * P + k) * S + sess] = t_last - p.D + 1;
+    p.queue[(1 * P + k) * S + sess] = (int32_t)(p.predictor == 0 ? (prev_rem >> (8 * k)) & 0xffu : 0u);
+    p.queue[(2 * P + k) * S + sess] = kNull;
+    p.queue[(3 * P + k) * S + sess] = t_last;
+  }
+  p.rollbacks[sess] += rollbacks;
+  p.resim[sess] += (int64_t)rollbacks * p.D;
+}
+
+// ------------------------------------------------------------------------------------------
 // Chains form (few sessions: the flat kernel runs one thread per session, so 4096 sessions fill 64
 // of the chip's 1024 SIMDs).  With the remote inputs of frame g arriving exactly at call g + D,
 // the state a call works on is a function of the inputs alone: after call c every remote player's
@@ -990,8 +1156,9 @@ struct ggrs_p2p_engine {
   int64_t dbg_sess = -1;
   int32_t dbg_frame = -1;
   int32_t sparse = 0;
-  int32_t form = 0;  // ggrs_p2p_set_unstaged: 0 default (flat, or chains for few sessions), 1 global
-                     // input reads, 2 lockstep staged, 3 flat with HBM rings, 4 chains
+  int32_t form = 0;  // ggrs_p2p_set_unstaged: 0 default (canonical flat, or chains for few sessions),
+                     // 1 global input reads, 2 lockstep staged, 3 flat with HBM rings, 4 chains,
+                     // 5 flat with LDS rings and the queue bookkeeping, 6 canonical flat
   bool dbg_ever = false;  // a debug flip was armed: the states may no longer be the canonical ones
   int32_t* last_saved = nullptr;  // [S], sparse saving only
   int32_t* ring_frame = nullptr;  // [R][S], sparse saving only
@@ -1248,22 +1415,25 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
   // would leave most SIMDs idle
   const int P = e->cfg.num_players;
   const int G = (p.D + 1) * padded_players(P);
-  const bool chains_ok = !e->sparse && e->desync_interval == 0 && !p.trace && !e->dbg_ever && G <= kWave &&
-                         (uint64_t)p.S * e->R * cell_dwords(P) * 4 < ((uint64_t)1 << 30);
+  // plain history: the session's states are the canonical ones the remote inputs determine
+  const bool plain_hist = !e->sparse && e->desync_interval == 0 && !p.trace && !e->dbg_ever;
+  const bool chains_ok = plain_hist && G <= kWave && (uint64_t)p.S * e->R * cell_dwords(P) * 4 < ((uint64_t)1 << 30);
   const bool chains = chains_ok && (e->form == 4 || (e->form == 0 && grid_of(p.S, kFlatBlock) <= e->num_cus));
   if (e->form == 4 && !chains_ok)
     return set_error(GGRS_E_STATE, "the chains form needs plain launches (no desync detection, trace, debug flip or "
                                    "sparse saving), (remote_latency + 1) x padded players <= 64 lanes and a ring < 1 GiB");
+  // the canonical flat kernel needs the same plain history and the remote inputs flowing (f0 >= D)
+  const bool canon_ok = plain_hist && (e->form == 0 || e->form == 6);
+  if ((chains || canon_ok) && p.f0 < p.D) {  // the first D calls (no remote input yet): general flat
+    const int32_t m = std::min(n, p.D - p.f0);
+    const int32_t form = e->form;
+    e->form = 5;
+    int rc = ggrs_p2p_advance_frames(e, m);
+    e->form = form;
+    if (rc || m == n) return rc;
+    return ggrs_p2p_advance_frames(e, n - m);
+  }
   if (chains) {
-    if (p.f0 < p.D) {  // the first D calls (no remote input yet) on the flat kernel
-      const int32_t m = std::min(n, p.D - p.f0);
-      const int32_t form = e->form;
-      e->form = 3;
-      int rc = ggrs_p2p_advance_frames(e, m);
-      e->form = form;
-      if (rc || m == n) return rc;
-      return ggrs_p2p_advance_frames(e, n - m);
-    }
     const int spw = kWave / G;
     const int row_bytes = spw * padded_players(P);
     // a launch's rows (f0 - 2D - delay .. f0 + n - 1) must fit the block's LDS: longer runs split
@@ -1293,7 +1463,7 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
     // whatever frame each lane is at (1.82e10 vs lockstep 1.26e10 session-frames/s at 65,536
     // sessions, 1.98e10 vs 1.89e10 at 131,072; with the frame-major ring of round 1 the flat
     // form's partial lines went out to HBM 3.5x over -- DESIGN.md section 5)
-    const bool flat = staged && (e->form == 0 || e->form == 3);
+    const bool flat = staged && (e->form == 0 || e->form == 3 || e->form == 5 || e->form == 6);
     dispatch_players(e->cfg.num_players, [&](auto PC) {
       constexpr int P = decltype(PC)::value;
       if (flat) {
@@ -1323,6 +1493,17 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
           }
         };
         const bool plain = p.desync_interval == 0 && !p.trace && p.dbg_sess < 0;
+        if (lds && canon_ok && !e->sparse && plain) {  // the canonical flat kernel (f0 >= D here)
+          const size_t shm = ring_lds;
+          if constexpr (P == 2) {
+            if (p.local_mask == 1u) p2p_canon_kernel<P, 1><<<grid, kFlatBlock, shm, e->stream>>>(p);
+            else if (p.local_mask == 2u) p2p_canon_kernel<P, 2><<<grid, kFlatBlock, shm, e->stream>>>(p);
+            else p2p_canon_kernel<P, -1><<<grid, kFlatBlock, shm, e->stream>>>(p);
+          } else {
+            p2p_canon_kernel<P, -1><<<grid, kFlatBlock, shm, e->stream>>>(p);
+          }
+          return;
+        }
         if (lds) {
           if (plain) go(std::true_type(), std::true_type());
           else go(std::false_type(), std::true_type());
@@ -1382,8 +1563,9 @@ int ggrs_p2p_set_sparse_saving(ggrs_p2p_engine_t* e, int32_t on) {
 
 int ggrs_p2p_set_unstaged(ggrs_p2p_engine_t* e, int32_t form) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
-  if (form < 0 || form > 4)
-    return set_error(GGRS_E_INVALID, "kernel form %d (0 default, 1 unstaged, 2 lockstep, 3 flat, 4 chains)", form);
+  if (form < 0 || form > 6)
+    return set_error(GGRS_E_INVALID, "kernel form %d (0 default, 1 unstaged, 2 lockstep, 3 flat HBM rings, 4 chains, "
+                                     "5 flat LDS rings with the queue bookkeeping, 6 canonical flat)", form);
   e->form = form;
   return GGRS_OK;
 }
@@ -1538,6 +1720,15 @@ int ggrs_p2p_read_stats(ggrs_p2p_engine_t* e, int32_t* rollbacks, int64_t* resim
   const int64_t S = e->cfg.num_sessions;
   if (rollbacks) HIP_TRY(hipMemcpyAsync(rollbacks, e->rollbacks, 4 * S, hipMemcpyDeviceToHost, e->stream));
   if (resim_frames) HIP_TRY(hipMemcpyAsync(resim_frames, e->resim, 8 * S, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  return GGRS_OK;
+}
+
+int ggrs_p2p_read_queues(ggrs_p2p_engine_t* e, int32_t* out) {
+  if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const size_t bytes = sizeof(int32_t) * 4 * e->cfg.num_players * (size_t)e->cfg.num_sessions;
+  HIP_TRY(hipMemcpyAsync(out, e->queue, bytes, hipMemcpyDeviceToHost, e->stream));
   HIP_TRY(hipStreamSynchronize(e->stream));
   return GGRS_OK;
 }

@@ -53,6 +53,7 @@ def _bind(L):
     L.ggrs_p2p_read_state.argtypes = [vp, i32, vp]
     L.ggrs_p2p_read_ring.argtypes = [vp, i32, vp, vp, vp]
     L.ggrs_p2p_read_stats.argtypes = [vp, vp, vp]
+    L.ggrs_p2p_read_queues.argtypes = [vp, vp]
     L.ggrs_p2p_read_trace.argtypes = [vp, i32, i32, vp]
     L.ggrs_p2p_timing_reset.argtypes = [vp]
     L.ggrs_p2p_timing_stop.argtypes = [vp]
@@ -144,6 +145,13 @@ class P2PEngine:
         _lib.check(self._L.ggrs_p2p_read_ring(self._h, session, _vp(frames), _vp(cks), _vp(states)))
         return frames, cks, states
 
+    def queues(self):
+        """[4][P][S] int32: every session's InputQueue prediction frame, prediction input, first
+        incorrect frame and last requested frame."""
+        out = np.zeros((4, self.num_players, self.num_sessions), np.int32)
+        _lib.check(self._L.ggrs_p2p_read_queues(self._h, _vp(out)))
+        return out
+
     def stats(self):
         rb = np.zeros(self.num_sessions, np.int32)
         rs = np.zeros(self.num_sessions, np.int64)
@@ -208,7 +216,8 @@ class P2PEngine:
         _lib.check(self._L.ggrs_p2p_set_sparse_saving(self._h, int(bool(on))))
         self.sparse_saving = bool(on)
 
-    KERNEL_FORMS = {"default": 0, "unstaged": 1, "lockstep": 2, "flat": 3, "chains": 4}
+    KERNEL_FORMS = {"default": 0, "unstaged": 1, "lockstep": 2, "flat": 3, "chains": 4, "flat_queues": 5,
+                    "canonical": 6}
 
     def set_unstaged(self, on=True):
         """Calls in lockstep with input rows read from global memory (for comparison)."""
@@ -219,6 +228,8 @@ class P2PEngine:
         for the launch where they fit; the chains form instead when the sessions fill at most one
         wave per CU), "flat" (each session's calls as its own step sequence, rings in HBM),
         "lockstep" (calls in lockstep, rows staged in LDS), "unstaged" (lockstep, rows from global
-        memory) or "chains" (every call as a chain of remote_latency + 1 advances from the confirmed
-        state, chains pipelined over lanes; plain launches only)."""
+        memory), "chains" (every call as a chain of remote_latency + 1 advances from the confirmed
+        state, chains pipelined over lanes; plain launches only), "flat_queues" (the flattened form
+        with LDS rings stepping the InputQueue bookkeeping) or "canonical" (the flattened form with
+        the rollback decision read off the inputs, the default's choice for plain launches)."""
         _lib.check(self._L.ggrs_p2p_set_unstaged(self._h, self.KERNEL_FORMS[form]))

@@ -465,6 +465,9 @@ int ggrs_p2p_read_ring(ggrs_p2p_engine_t* eng, int32_t session, int32_t* frames,
                        uint8_t* states);
 /* per session: number of rollbacks (adjust_gamestate calls) and resimulated frames so far */
 int ggrs_p2p_read_stats(ggrs_p2p_engine_t* eng, int32_t* rollbacks, int64_t* resim_frames);
+/* every session's InputQueue prediction state, [4][num_players][num_sessions] i32: prediction.frame,
+ * prediction.input, first_incorrect_frame, last_requested_frame (input_queue.rs:10-37) */
+int ggrs_p2p_read_queues(ggrs_p2p_engine_t* eng, int32_t* out);
 /* [n][num_sessions] fletcher16 of each session's state after the final AdvanceFrame of calls
  * first_frame .. first_frame+n-1 (ex_game.rs:121-126) */
 int ggrs_p2p_read_trace(ggrs_p2p_engine_t* eng, int32_t first_frame, int32_t n, uint16_t* out);
@@ -507,7 +510,12 @@ int ggrs_p2p_set_sparse_saving(ggrs_p2p_engine_t* eng, int32_t on);
  * advance), (D + 1) x players lanes per session, for engines whose sessions would fill at most one
  * wave per CU in the flattened form (the default picks it there); plain launches only -- no desync
  * detection, trace, debug flip or sparse saving (GGRS_E_STATE when forced otherwise); the first D
- * calls run on the flattened form.  Same states, rings, statistics and queues as every other form. */
+ * calls run on the flattened form.  Same states, rings, statistics and queues as every other form.
+ * 5 = the flattened form with LDS rings, stepping every remote InputQueue's bookkeeping per frame;
+ * 6 = canonical flattened form (the default for plain launches that do not take the chains form):
+ * the rollback decision of call f is the remote input of frame f - D against the prediction made
+ * from frame f - D - 1, the replay's remote inputs the confirmed and then the predicted ones -- the
+ * queue state the fixed-latency network implies, written back at the end. */
 int ggrs_p2p_set_unstaged(ggrs_p2p_engine_t* eng, int32_t form);
 /* test hook: the AdvanceFrame from `frame` of `session` flips the lowest bit of player 0's x on
  * every (re)simulation -- a deterministic desync of this peer (session -1: off) */

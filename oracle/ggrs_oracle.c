@@ -23,11 +23,12 @@
  * Floating point: compiled with -O2 -ffp-contract=off (Rust never contracts) and linked against
  * this image's glibc 2.35 libm, whose sinf/cosf/fmodf are what Rust's f32::sin/cos/% call.
  *
- * Parity pinning: the reference holds no numeric golden vectors.  This
- * restatement is pinned by (a) the reference's own structural tests restated in
- * tests/test_oracle.py (request counts 1/2/6/16 and order, frame advance, random checksums ->
- * MismatchedChecksum, input-delay semantics) and (b) an independent pure-Python restatement
- * (oracle/pyoracle.py) that generated the committed fixtures in tests/golden/.
+ * Parity pinning: the reference holds no numeric golden vectors, so the
+ * ex_game arithmetic (states and checksums) is PARITY UNPINNED.  The structure is pinned by the
+ * reference's own tests restated in tests/test_oracle.py (request counts 1/2/6/16 and order, frame
+ * advance, random checksums -> MismatchedChecksum, input-delay semantics); the numbers agree with
+ * an independent pure-Python restatement (oracle/pyoracle.py, which generated the committed
+ * fixtures in tests/golden/) and libm's own KAT -- evidence, not a pin against reference output.
  */
 #include <math.h>
 #include <pthread.h>

@@ -259,6 +259,7 @@ extern "C" {
     pub fn ggrs_p2p_read_ring(eng: *mut ggrs_p2p_engine_t, session: i32, frames: *mut i32, checksums: *mut u16,
                               states: *mut u8) -> i32;
     pub fn ggrs_p2p_read_stats(eng: *mut ggrs_p2p_engine_t, rollbacks: *mut i32, resim_frames: *mut i64) -> i32;
+    pub fn ggrs_p2p_read_queues(eng: *mut ggrs_p2p_engine_t, out: *mut i32) -> i32;
     pub fn ggrs_p2p_read_trace(eng: *mut ggrs_p2p_engine_t, first_frame: i32, n: i32, out: *mut u16) -> i32;
     pub fn ggrs_p2p_timing_reset(eng: *mut ggrs_p2p_engine_t) -> i32;
     pub fn ggrs_p2p_timing_stop(eng: *mut ggrs_p2p_engine_t) -> i32;

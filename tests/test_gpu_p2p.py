@@ -68,15 +68,19 @@ def test_p2p_matches_oracle(oracle, P, local, delay, mp, D, pred, model, form):
     check_against_oracle(eng, rows, [0, 1, 63, 64, 150, 299], frames)
 
 
-@pytest.mark.parametrize("P,local,delay,mp,D,pred,model", [CASES[0], CASES[1], CASES[3], CASES[6]])
-def test_p2p_plain_launches_match_oracle(oracle, P, local, delay, mp, D, pred, model):
-    """Launches without trace, desync history or debug flip run the flat kernel's plain
-    specialisation: final states, rings and rollback counts bit-exact with the oracle."""
+@pytest.mark.parametrize("form", ["default", "flat_queues", "canonical", "chains"])
+@pytest.mark.parametrize("P,local,delay,mp,D,pred,model", CASES)
+def test_p2p_plain_launches_match_oracle(oracle, P, local, delay, mp, D, pred, model, form):
+    """Launches without trace, desync history or debug flip: the flat kernel's plain
+    specialisation stepping the queues, the canonical flat kernel (rollback decision read off the
+    inputs), the chains form, and the default's choice among them (chains at 300 sessions): final
+    states, rings, rollback counts and queue states bit-exact with the oracle."""
     from ggrs_amd import P2PEngine
     S, frames = 300, 160
     rows = stream(S, frames, P, model, seed_base=0x7070)
     eng = P2PEngine(S, num_players=P, local_players=local, input_delay=delay, max_prediction=mp,
                     remote_latency=D, predictor=pred)
+    eng.set_kernel_form(form)
     eng.add_inputs(0, rows)
     for n in (3, 45, 112):
         eng.advance_frames(n)
@@ -257,3 +261,26 @@ def test_p2p_chains_form_rejects_non_plain(oracle):
     eng.set_kernel_form("chains")
     with pytest.raises(GgrsError):
         eng.advance_frames(8)
+
+
+def test_p2p_forms_interleave_with_equal_queues(oracle):
+    """Every plain form leaves the InputQueue state the others continue from: launches alternate
+    between the queue-stepping flat kernel, the canonical flat kernel and the chains form, with
+    the device queue words equal to the queue-stepping kernel's after each launch."""
+    from ggrs_amd import P2PEngine
+    S, frames, P = 200, 150, 2
+    rows = stream(S, frames, P, 1, seed_base=0x8181)
+    engs = {}
+    for k in ("flat_queues", "mixed"):
+        e = P2PEngine(S, num_players=P, local_players=(1,), input_delay=1, max_prediction=8, remote_latency=3,
+                      input_capacity=frames + 8)
+        e.add_inputs(0, rows)
+        engs[k] = e
+    engs["flat_queues"].set_kernel_form("flat_queues")
+    for k, n in enumerate((5, 17, 1, 30, 2, 40, 55)):
+        engs["mixed"].set_kernel_form(("canonical", "chains", "flat_queues")[k % 3])
+        for e in engs.values():
+            e.advance_frames(n)
+        qa, qb = engs["flat_queues"].queues(), engs["mixed"].queues()
+        assert (qa == qb).all(), k
+    check_against_oracle(engs["mixed"], rows, [0, 1, 63, 64, 150, 199], frames, trace=False)

@@ -16,10 +16,14 @@ timeout -k 10 300 python -u bench.py --workload p2p --sessions 4096 --latency 8 
   > gpurun_out/bench_${TAG}_p2pc2flat.json 2> gpurun_out/bench_${TAG}_p2pc2flat.err || { tail -20 gpurun_out/bench_${TAG}_p2pc2flat.err; exit 11; }
 cat gpurun_out/bench_${TAG}_p2pc2flat.json
 for S in 16384 65536; do
-timeout -k 10 300 python -u bench.py --workload p2p --sessions $S --p2p-form chains --no-cpu-baseline \
-  > gpurun_out/bench_${TAG}_p2pch$S.json 2> gpurun_out/bench_${TAG}_p2pch$S.err || { tail -20 gpurun_out/bench_${TAG}_p2pch$S.err; exit 11; }
-python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], '%.4g' % d['value'], d['roofline']['avg_launch_ms'])" gpurun_out/bench_${TAG}_p2pch$S.json chains$S
+for F in chains canonical flat_queues; do
+timeout -k 10 300 python -u bench.py --workload p2p --sessions $S --p2p-form $F --no-cpu-baseline \
+  > gpurun_out/bench_${TAG}_p2p${F}$S.json 2> gpurun_out/bench_${TAG}_p2p${F}$S.err || { tail -20 gpurun_out/bench_${TAG}_p2p${F}$S.err; exit 11; }
+python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], '%.4g' % d['value'], d['roofline']['avg_launch_ms'])" gpurun_out/bench_${TAG}_p2p${F}$S.json $F$S
 done
+done
+timeout -k 10 300 python -u bench.py --workload p2p --sparse --no-cpu-baseline > gpurun_out/bench_${TAG}_p2psparse.json 2> gpurun_out/bench_${TAG}_p2psparse.err || { tail -20 gpurun_out/bench_${TAG}_p2psparse.err; exit 11; }
+python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('sparse', '%.4g' % d['value'], d['roofline']['avg_launch_ms'])" gpurun_out/bench_${TAG}_p2psparse.json
 GGRS_BENCH_BACKEND=gloo timeout -k 10 300 python -u bench.py --gpus 2 --steps 10 \
   > gpurun_out/bench_${TAG}_gloo2.json 2> gpurun_out/bench_${TAG}_gloo2.err || { tail -20 gpurun_out/bench_${TAG}_gloo2.err; exit 12; }
 cat gpurun_out/bench_${TAG}_gloo2.json
