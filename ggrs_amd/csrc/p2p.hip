@@ -836,6 +836,17 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_canon_kernel(P2PParams p) {
     uint32_t rem_conf = 0, rem_pred = 0;
     while (f < chunk_end) {
       if (at_start) {
+        // check_checksum_send_interval (p2p_session.rs:939-975), before any rollback of this call
+        // (as p2p_kernel); a launch-uniform switch
+        if (p.desync_interval > 0) {
+          const int32_t fts = f - 1 - p.D;
+          if (live && fts >= p.desync_interval && fts % p.desync_interval == 0) {
+            const int32_t cs = fts % p.R;
+            const uint4 v = lds_ring[(cs * PC + F / 4) * kFlatBlock + lt];
+            const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+            p.hist[(int64_t)((fts / p.desync_interval) % kHist) * S + sess] = (uint16_t)x[F % 4];
+          }
+        }
         // poll of call f: the remote inputs of frame g = f - D against the prediction made for them
         g = f - p.D;
         rem_conf = rows(g) & rbytes;
@@ -1415,9 +1426,11 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
   // would leave most SIMDs idle
   const int P = e->cfg.num_players;
   const int G = (p.D + 1) * padded_players(P);
-  // plain history: the session's states are the canonical ones the remote inputs determine
-  const bool plain_hist = !e->sparse && e->desync_interval == 0 && !p.trace && !e->dbg_ever;
-  const bool chains_ok = plain_hist && G <= kWave && (uint64_t)p.S * e->R * cell_dwords(P) * 4 < ((uint64_t)1 << 30);
+  // plain history: the session's states are the canonical ones the remote inputs determine (the
+  // canonical flat kernel also keeps the desync history; the chains form does not)
+  const bool plain_hist = !e->sparse && !p.trace && !e->dbg_ever;
+  const bool chains_ok = plain_hist && e->desync_interval == 0 && G <= kWave &&
+                         (uint64_t)p.S * e->R * cell_dwords(P) * 4 < ((uint64_t)1 << 30);
   const bool chains = chains_ok && (e->form == 4 || (e->form == 0 && grid_of(p.S, kFlatBlock) <= e->num_cus));
   if (e->form == 4 && !chains_ok)
     return set_error(GGRS_E_STATE, "the chains form needs plain launches (no desync detection, trace, debug flip or "
@@ -1493,7 +1506,7 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
           }
         };
         const bool plain = p.desync_interval == 0 && !p.trace && p.dbg_sess < 0;
-        if (lds && canon_ok && !e->sparse && plain) {  // the canonical flat kernel (f0 >= D here)
+        if (lds && canon_ok) {  // the canonical flat kernel (f0 >= D here)
           const size_t shm = ring_lds;
           if constexpr (P == 2) {
             if (p.local_mask == 1u) p2p_canon_kernel<P, 1><<<grid, kFlatBlock, shm, e->stream>>>(p);
