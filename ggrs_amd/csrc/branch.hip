@@ -359,7 +359,7 @@ __device__ inline __amdgpu_buffer_rsrc_t prefix_rsrc(const void* base, uint32_t 
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
 
-template <int P, int EP, int WT>
+template <int P, int EP, int WT, bool kPair>
 __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams rp);
 
 // f(integral_constant<int, 0>) .. f(integral_constant<int, N - 1>)
@@ -371,9 +371,14 @@ __device__ inline void static_for(Fn&& f) {
   }
 }
 
-template <int P, int EP, int WT>
+// kPair (two players, an even branch count: lanes 2i and 2i + 1 belong to the same session): the
+// trunk's two players are split over the lane pair -- the even lane steps player 0, the odd lane
+// player 1, and each takes the other's new fields with one DPP swap per field -- instead of every
+// lane stepping both (the trunk is the same on every lane of a session).
+template <int P, int EP, int WT, bool kPair>
 __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams rp) {
   static_assert(EP >= 0 && EP < P, "enumerated player");
+  static_assert(!kPair || P == 2, "the lane-pair trunk split is for two players");
   constexpr int F = state_fields(P);
   constexpr int n_bytes = Fletcher<P>::n;
   constexpr int e = EP;
@@ -442,6 +447,7 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
   const __amdgpu_buffer_rsrc_t rs_ck = prefix_rsrc(p.ring_ck, (uint32_t)(2 * p.L * p.R));
   const uint32_t fstride = (uint32_t)(p.L * 4);
   const bool branch0 = in_range && b == 0;  // writes the session's trunk and report
+  const bool podd = (threadIdx.x & 1) != 0;  // kPair: this lane steps the trunk's player 1
   // per-lane destinations (VGPR pointers: the loop's scalar registers are taken by its counters,
   // descriptors and masks, and uniform pointers kept there spilled to VGPR lanes)
   uint64_t* const bits_dst = rp.report_bits + (lane >> 6);
@@ -546,7 +552,8 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
       // state of the previous super-step, stage 0 the trunk's enumerated player) and the trunk's
       // confirmed replay of frame f_c (every player), as independent player steps
       // xs: stages K0 .. K1 - 1, then the trunk's players (all, or all but the enumerated one)
-      constexpr int NK = K1 - K0, NT = kTE ? P : P - 1, NS = NK + NT;
+      constexpr bool kSplit = kPair && kTE;  // the trunk's two players over the lane pair
+      constexpr int NK = K1 - K0, NT = kSplit ? 1 : (kTE ? P : P - 1), NS = NK + NT;
       uint32_t xs[NS][5], xin[NS];
       InputRec xrec[NS];
 #pragma unroll
@@ -557,15 +564,24 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
         xrec[k - K0] = srec[k];
       }
       auto trunk_index = [](int q) { return NK + (kTE || q < e ? q : q - 1); };
+      constexpr int fk0[5] = {fld_x(P, 0), fld_y(P, 0), fld_vx(P, 0), fld_vy(P, 0), fld_rot(P, 0)};
+      constexpr int fk1[5] = {fld_x(P, 1 % P), fld_y(P, 1 % P), fld_vx(P, 1 % P), fld_vy(P, 1 % P), fld_rot(P, 1 % P)};
+      if constexpr (kSplit) {
 #pragma unroll
-      for (int q = 0; q < P; q++) {
-        if (!kTE && q == e) continue;
-        const int fk[5] = {fld_x(P, q), fld_y(P, q), fld_vx(P, q), fld_vy(P, q), fld_rot(P, q)};
-        const int i = trunk_index(q);
+        for (int u5 = 0; u5 < 5; u5++) xs[NK][u5] = podd ? T.w[fk1[u5]] : T.w[fk0[u5]];
+        xin[NK] = (podd ? row >> 8 : row) & 0xffu;
+        xrec[NK] = make_input_rec(xin[NK]);
+      } else {
 #pragma unroll
-        for (int u5 = 0; u5 < 5; u5++) xs[i][u5] = T.w[fk[u5]];
-        xin[i] = (row >> (8 * q)) & 0xffu;
-        xrec[i] = make_input_rec(xin[i]);
+        for (int q = 0; q < P; q++) {
+          if (!kTE && q == e) continue;
+          const int fk[5] = {fld_x(P, q), fld_y(P, q), fld_vx(P, q), fld_vy(P, q), fld_rot(P, q)};
+          const int i = trunk_index(q);
+#pragma unroll
+          for (int u5 = 0; u5 < 5; u5++) xs[i][u5] = T.w[fk[u5]];
+          xin[i] = (row >> (8 * q)) & 0xffu;
+          xrec[i] = make_input_rec(xin[i]);
+        }
       }
       if constexpr (kLean) {
         advance_players_rec<NS>(xs, xrec, sck);
@@ -579,12 +595,22 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
         for (int q = 0; q < 5; q++) est[k][q] = xs[k - K0][q];
       BoxState<P> Tn = T;  // (!kTE: the enumerated player's fields stay stale, never read)
       Tn.w[0] = (uint32_t)(f_c + 1);
+      if constexpr (kSplit) {
 #pragma unroll
-      for (int q = 0; q < P; q++) {
-        if (!kTE && q == e) continue;
-        const int fk[5] = {fld_x(P, q), fld_y(P, q), fld_vx(P, q), fld_vy(P, q), fld_rot(P, q)};
+        for (int u5 = 0; u5 < 5; u5++) {
+          const uint32_t mine = xs[NK][u5];
+          const uint32_t other = (uint32_t)__builtin_amdgcn_mov_dpp((int)mine, 0xB1, 0xF, 0xF, false);  // xor 1
+          Tn.w[fk0[u5]] = podd ? other : mine;
+          Tn.w[fk1[u5]] = podd ? mine : other;
+        }
+      } else {
 #pragma unroll
-        for (int u5 = 0; u5 < 5; u5++) Tn.w[fk[u5]] = xs[trunk_index(q)][u5];
+        for (int q = 0; q < P; q++) {
+          if (!kTE && q == e) continue;
+          const int fk[5] = {fld_x(P, q), fld_y(P, q), fld_vx(P, q), fld_vy(P, q), fld_rot(P, q)};
+#pragma unroll
+          for (int u5 = 0; u5 < 5; u5++) Tn.w[fk[u5]] = xs[trunk_index(q)][u5];
+        }
       }
       uint32_t c1, c2;
       common_sums(Tn, c1, c2);
@@ -1102,8 +1128,15 @@ int launch_rounds(ggrs_branch_engine* e, int32_t n_rounds, void* copy, bool ever
         constexpr int P = decltype(PC)::value;
         dispatch_enumerated<P>(p.first_remote, [&](auto EC) {
           constexpr int EP = decltype(EC)::value;
-          if (p.W == 4) prefix_pipe_kernel<P, EP, 4><<<grid, kRoundsBlock, lds, e->stream>>>(rp);
-          else prefix_pipe_kernel<P, EP, 0><<<grid, kRoundsBlock, lds, e->stream>>>(rp);
+          // lane pairs share a session when the branch count is even (two players only)
+          const bool pair = P == 2 && (p.B & 1) == 0;
+          if (pair) {
+            if (p.W == 4) prefix_pipe_kernel<P, EP, 4, P == 2><<<grid, kRoundsBlock, lds, e->stream>>>(rp);
+            else prefix_pipe_kernel<P, EP, 0, P == 2><<<grid, kRoundsBlock, lds, e->stream>>>(rp);
+          } else {
+            if (p.W == 4) prefix_pipe_kernel<P, EP, 4, false><<<grid, kRoundsBlock, lds, e->stream>>>(rp);
+            else prefix_pipe_kernel<P, EP, 0, false><<<grid, kRoundsBlock, lds, e->stream>>>(rp);
+          }
         });
       });
       return;
