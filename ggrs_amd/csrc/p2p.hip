@@ -958,11 +958,23 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
   const int32_t lo = p.f0 - 2 * D - p.delay;
   const int32_t nrows = p.f0 + p.n - lo;
   {
-    const int used = nsess * Pp;
-    for (int i = wl; i < nrows * row_bytes; i += kWave) {
-      const int rr = i / row_bytes, b = i - rr * row_bytes;
-      const int32_t row = lo + rr;
-      lds_rows[i] = (row >= 0 && b < used) ? p.inputs[((int64_t)(row % p.cap) * S + s0) * Pp + b] : (uint8_t)0;
+    // eight loads in flight per thread before their LDS stores (one memory latency per 512 bytes)
+    constexpr int kBatch = 8;
+    const int used = nsess * Pp, total = nrows * row_bytes;
+    for (int i0 = 0; i0 < total; i0 += kBatch * kWave) {
+      uint8_t v[kBatch];
+#pragma unroll
+      for (int u = 0; u < kBatch; u++) {
+        const int i = i0 + u * kWave + wl;
+        const int rr = i / row_bytes, b = i - rr * row_bytes;
+        const int32_t row = lo + rr;
+        v[u] = (i < total && row >= 0 && b < used) ? p.inputs[((int64_t)(row % p.cap) * S + s0) * Pp + b] : (uint8_t)0;
+      }
+#pragma unroll
+      for (int u = 0; u < kBatch; u++) {
+        const int i = i0 + u * kWave + wl;
+        if (i < total) lds_rows[i] = v[u];
+      }
     }
   }
   // every role starts from T_{f0-D}, the cell chain f0 loads (roles > 0 hold chains of the previous
@@ -1006,10 +1018,16 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
   const int32_t t_last = p.f0 + p.n - 1;  // the launch's last call
   const int32_t t_end = t_last + D + 1;
   int32_t slot = __builtin_amdgcn_readfirstlane((p.f0 - D + 1) % p.R);  // slot of frame t - D + 1
-  for (int32_t t = p.f0; t < t_end; ++t) {
+  const uint32_t ck_pad = fo_ck + 4;  // (P = 4: the cell's padding dwords after the checksum)
+  // One step t.  kCore: a call of the launch (t <= t_last): its poll, and role 0 -- the newest chain
+  // -- stores frame t - D + 1; the tail steps' storing role is t - t_last.  kLean: the states are in
+  // the lean step's rotation domain (every role starts from the loaded cell, which this engine wrote).
+  auto step = [&](int32_t t, auto core_tag, auto lean_tag) {
+    constexpr bool kCore = decltype(core_tag)::value;
+    constexpr bool kLean = decltype(lean_tag)::value;
     const int32_t row = t - back;
     const uint32_t in = (row >= 0 && !zero_in) ? (uint32_t)lds_rows[(row - lo) * row_bytes + in_col] : 0u;
-    if (t <= t_last) {
+    if constexpr (kCore) {
       // poll of call t: the arriving input of frame t - D against the prediction made for it
       // (add_input_by_frame, input_queue.rs:190-230); any remote player's miss rolls the session back
       const bool miss = counts && in != (p.predictor == 0 ? prev_in : 0u);
@@ -1022,7 +1040,7 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
       float x = __builtin_bit_cast(float, w[0]), y = __builtin_bit_cast(float, w[1]);
       float vx = __builtin_bit_cast(float, w[2]), vy = __builtin_bit_cast(float, w[3]);
       float rot = __builtin_bit_cast(float, w[4]);
-      if (lean_ok) advance_player_lean(x, y, vx, vy, rot, in);
+      if constexpr (kLean) advance_player_lean(x, y, vx, vy, rot, in);
       else advance_player(x, y, vx, vy, rot, in);
       w[0] = __builtin_bit_cast(uint32_t, x);
       w[1] = __builtin_bit_cast(uint32_t, y);
@@ -1035,8 +1053,8 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
     for (int q = 0; q < 5; q++) nx[q] = (uint32_t)__builtin_amdgcn_ds_bpermute(src_rot, (int)w[q]);
     __builtin_amdgcn_sched_barrier(0);  // the rotation's LDS latency behind the checksum and stores
     const uint32_t frame1 = (uint32_t)(t - D + 1);
-    const int js = t > t_last ? t - t_last : 0;  // the newest chain of the launch holding frame1
-    if (js < D) {
+    const int js = kCore ? 0 : t - t_last;  // the newest chain of the launch holding frame1
+    if (kCore || js < D) {
       uint32_t d1 = dot4_u8(frame1, wf1, c1), d2 = dot4_u8(frame1, wf2, c2);
 #pragma unroll
       for (int q = 0; q < 5; q++) {
@@ -1052,14 +1070,15 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
         d2 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d2, 0x4E, 0xF, 0xF, true);
       }
       const uint32_t ck = fletcher_from_doubled(d1, d2);
-      const bool me = j == js;
+      const bool me = kCore ? j == 0 : j == js;
       const uint32_t so = (uint32_t)slot * (uint32_t)(C * 4);
 #pragma unroll
       for (int q = 0; q < 5; q++) __builtin_amdgcn_raw_buffer_store_b32(w[q], rs_ring, me ? fo[q] : kChainOob, so, 0);
       __builtin_amdgcn_raw_buffer_store_b32(frame1, rs_ring, me ? fo_frame : kChainOob, so, 0);
       __builtin_amdgcn_raw_buffer_store_b32(ck, rs_ring, me ? fo_ck : kChainOob, so, 0);
 #pragma unroll
-      for (int k = F + 1; k < C; k++) __builtin_amdgcn_raw_buffer_store_b32(0u, rs_ring, me ? fo_ck + (k - F) * 4 : kChainOob, so, 0);
+      for (int k = F + 1; k < C; k++)
+        __builtin_amdgcn_raw_buffer_store_b32(0u, rs_ring, me && lead ? ck_pad + (k - F - 1) * 4 : kChainOob, so, 0);
     } else if (t == t_end - 1 && j == D) {
       // role D: chain f0 + n - 1 after its call's own AdvanceFrame -- the current state
       if (owner) {
@@ -1071,7 +1090,14 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
 #pragma unroll
     for (int q = 0; q < 5; q++) w[q] = nx[q];
     slot = slot + 1 == p.R ? 0 : slot + 1;
-  }
+  };
+  auto run = [&](auto lean_tag) {
+    int32_t t = p.f0;
+    for (; t <= t_last; ++t) step(t, std::true_type(), lean_tag);
+    for (; t < t_end; ++t) step(t, std::false_type(), lean_tag);
+  };
+  if (lean_ok) run(std::true_type());
+  else run(std::false_type());
   if (valid && j == 0 && pl == 0) {
     p.rollbacks[s] += rollbacks;
     p.resim[s] += (int64_t)rollbacks * D;
