@@ -362,6 +362,13 @@ __device__ inline __amdgpu_buffer_rsrc_t prefix_rsrc(const void* base, uint32_t 
 template <int P, int EP, int WT, bool kPair>
 __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams rp);
 
+// A session's desync record keeps the earliest frame with a disagreeing survivor.  The prefix kernel
+// spreads one session over many blocks, which reach a super-step at different times, so the record
+// is a minimum (NULL_FRAME = -1 is the largest unsigned value), not a first-come CAS.
+__device__ inline void desync_min(int32_t* dst, int32_t frame) {
+  atomicMin(reinterpret_cast<unsigned int*>(dst), (unsigned int)frame);
+}
+
 // f(integral_constant<int, 0>) .. f(integral_constant<int, N - 1>)
 template <int N, int I = 0, typename Fn>
 __device__ inline void static_for(Fn&& f) {
@@ -537,7 +544,7 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
             common_sums(T, d1, d2);
 #pragma unroll
             for (int q = 0; q < 5; q++) v[q] = T.w[kq[q]];
-            if (enum_ck(d1, d2, est[0]) != enum_ck(d1, d2, v)) atomicCAS(desync_dst, -1, f_c);
+            if (enum_ck(d1, d2, est[0]) != enum_ck(d1, d2, v)) desync_min(desync_dst, f_c);
           }
         }
         if (u == 0 && check0) {
@@ -545,7 +552,7 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
           common_sums(T, d1, d2);
 #pragma unroll
           for (int q = 0; q < 5; q++) v[q] = T.w[kq[q]];
-          if (mine0 != (uint16_t)enum_ck(d1, d2, v)) atomicCAS(desync_dst, -1, f_c);
+          if (mine0 != (uint16_t)enum_ck(d1, d2, v)) desync_min(desync_dst, f_c);
         }
       }
       // the stages' steps (round u - k's AdvanceFrame(f_c) with digit k: stage k takes stage k - 1's
