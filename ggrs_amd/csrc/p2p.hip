@@ -933,14 +933,24 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_canon_kernel(P2PParams p) {
 constexpr uint32_t kChainOob = 0x40000000u;  // past every descriptor's range: a lane that never stores
 constexpr int kChainLdsRows = 16 * 1024;      // bytes of staged input rows per block
 
-template <int P>
+//   kB (2 <= D <= 8): roles 0 .. D - 1 only, as the v5 SyncTest kernel does: role D -- each chain's
+// last AdvanceFrame, the call's own frame, whose state no other role consumes -- leaves the
+// lockstep; role D - 1's post-advance state is stashed in LDS every step and every D steps one
+// batch sub-step advances the D stashed states (role lane j takes step j's).  D x Pp lanes per
+// session instead of (D + 1) x Pp (config 2's P2P shape, D = 8 and two players: four sessions
+// per wave instead of three), one extra step's work per D steps.
+constexpr int kStashEntry = 32;  // bytes per (session, player) entry of a stash slot: 5 fields
+
+template <int P, bool kB>
 __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t spw) {
   constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
   constexpr int F = state_fields(P);
   constexpr int C = cell_dwords(P);
   constexpr int n_bytes = Fletcher<P>::n;
-  extern __shared__ uint8_t lds_rows[];  // [rows][spw * Pp]: input rows lo .. f0 + n - 1
-  const int D = p.D, G = (D + 1) * Pp;
+  // [rows][spw * Pp]: input rows lo .. f0 + n - 1; kB: then (D + 1) stash slots (the last the
+  // dump every lane other than role D - 1 writes) of kWave entries
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds_rows[];
+  const int D = p.D, G = (kB ? D : D + 1) * Pp;
   const int wl = threadIdx.x;
   const int g = wl / G, r = wl - g * G;
   const int j = r / Pp, pl = r - j * Pp;  // static role, player lane
@@ -1012,11 +1022,19 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
   const uint32_t c2 = pl == 0 ? 2u * Fletcher<P>::kSum2Const : 0u;
   const int src_rot = (j == 0 ? wl : g * G + (j - 1) * Pp + pl) * 4;
   const bool counts = valid && j == 0 && pl < P && !local;  // role 0's remote lanes see each arrival
+  // kB stash: slot of step t = (t - f0) mod D; lane entry g * Pp + pl
+  uint8_t* const stash = lds_rows + (((nrows * row_bytes) + 15) & ~15);
+  const uint32_t entry = (uint32_t)(g * Pp + pl) * kStashEntry;
+  const uint32_t stash_w = (valid && j == D - 1) ? entry : (uint32_t)(D * kWave * kStashEntry) + (uint32_t)wl * kStashEntry;
+  // batch: role lane j advances slot j's chain c = tb + j - (D - 1) at its own frame c, with the
+  // local input of frame c and the remote prediction of chain c (the input of frame c - D)
+  const int32_t back_b = local ? p.delay : D;
+  const bool zero_b = !local && p.predictor != 0;
   const uint32_t pmask = (1u << Pp) - 1u;
   const int gbase = g * G;
   int32_t rollbacks = 0;
   const int32_t t_last = p.f0 + p.n - 1;  // the launch's last call
-  const int32_t t_end = t_last + D + 1;
+  const int32_t t_end = t_last + D + (kB ? 0 : 1);  // kB: role D's last advance is the batch's
   int32_t slot = __builtin_amdgcn_readfirstlane((p.f0 - D + 1) % p.R);  // slot of frame t - D + 1
   const uint32_t ck_pad = fo_ck + 4;  // (P = 4: the cell's padding dwords after the checksum)
   // One step t.  kCore: a call of the launch (t <= t_last): its poll, and role 0 -- the newest chain
@@ -1051,6 +1069,12 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
     uint32_t nx[5];
 #pragma unroll
     for (int q = 0; q < 5; q++) nx[q] = (uint32_t)__builtin_amdgcn_ds_bpermute(src_rot, (int)w[q]);
+    if constexpr (kB) {  // role D - 1's post-advance state (its chain's own frame) for the batch
+      uint8_t* st = stash + (uint32_t)((t - p.f0) % D) * (uint32_t)(kWave * kStashEntry) + stash_w;
+      if (stash_w >= (uint32_t)(D * kWave * kStashEntry)) st = stash + stash_w;  // the dump slot
+      *reinterpret_cast<uint4*>(st) = make_uint4(w[0], w[1], w[2], w[3]);
+      *reinterpret_cast<uint32_t*>(st + 16) = w[4];
+    }
     __builtin_amdgcn_sched_barrier(0);  // the rotation's LDS latency behind the checksum and stores
     const uint32_t frame1 = (uint32_t)(t - D + 1);
     const int js = kCore ? 0 : t - t_last;  // the newest chain of the launch holding frame1
@@ -1079,7 +1103,7 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
 #pragma unroll
       for (int k = F + 1; k < C; k++)
         __builtin_amdgcn_raw_buffer_store_b32(0u, rs_ring, me && lead ? ck_pad + (k - F - 1) * 4 : kChainOob, so, 0);
-    } else if (t == t_end - 1 && j == D) {
+    } else if (!kB && t == t_end - 1 && j == D) {
       // role D: chain f0 + n - 1 after its call's own AdvanceFrame -- the current state
       if (owner) {
 #pragma unroll
@@ -1091,10 +1115,50 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
     for (int q = 0; q < 5; q++) w[q] = nx[q];
     slot = slot + 1 == p.R ? 0 : slot + 1;
   };
+  // kB: the batch over the stashes of steps tb .. tb + count - 1 (role D's AdvanceFrames)
+  auto batch = [&](int32_t tb, int count, auto lean_tag) {
+    constexpr bool kLean = decltype(lean_tag)::value;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int32_t c = tb + j - (D - 1);
+    const bool act = valid && j < count;
+    const uint8_t* st = stash + (uint32_t)((tb - p.f0 + j) % D) * (uint32_t)(kWave * kStashEntry) + entry;
+    const uint4 a = *reinterpret_cast<const uint4*>(st);
+    uint32_t v[5] = {a.x, a.y, a.z, a.w, *reinterpret_cast<const uint32_t*>(st + 16)};
+    const int32_t row = c - back_b;
+    const uint32_t in = (row >= lo && !zero_b && j < count) ? (uint32_t)lds_rows[(row - lo) * row_bytes + in_col] : 0u;
+    float x = __builtin_bit_cast(float, v[0]), y = __builtin_bit_cast(float, v[1]);
+    float vx = __builtin_bit_cast(float, v[2]), vy = __builtin_bit_cast(float, v[3]);
+    float rot = __builtin_bit_cast(float, v[4]);
+    if constexpr (kLean) advance_player_lean(x, y, vx, vy, rot, in);
+    else advance_player(x, y, vx, vy, rot, in);
+    if (act && c == t_last) {  // the launch's last call: the current state
+      v[0] = __builtin_bit_cast(uint32_t, x);
+      v[1] = __builtin_bit_cast(uint32_t, y);
+      v[2] = __builtin_bit_cast(uint32_t, vx);
+      v[3] = __builtin_bit_cast(uint32_t, vy);
+      v[4] = __builtin_bit_cast(uint32_t, rot);
+      if (owner) {
+#pragma unroll
+        for (int q = 0; q < 5; q++) p.cur[(int64_t)kq[q] * S + s] = v[q];
+      }
+      if (lead) p.cur[s] = (uint32_t)(c + 1);
+    }
+  };
   auto run = [&](auto lean_tag) {
     int32_t t = p.f0;
-    for (; t <= t_last; ++t) step(t, std::true_type(), lean_tag);
-    for (; t < t_end; ++t) step(t, std::false_type(), lean_tag);
+    for (; t <= t_last; ++t) {
+      step(t, std::true_type(), lean_tag);
+      if (kB && (t - p.f0) % D == D - 1) batch(t - (D - 1), D, lean_tag);
+    }
+    for (; t < t_end; ++t) {
+      step(t, std::false_type(), lean_tag);
+      if (kB && ((t - p.f0) % D == D - 1 || t == t_end - 1)) {
+        const int count = (t - p.f0) % D + 1;
+        batch(t - (count - 1), count, lean_tag);
+      }
+    }
   };
   if (lean_ok) run(std::true_type());
   else run(std::false_type());
@@ -1451,7 +1515,9 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
   // the chains form: forced (form 4), or by default when the flat kernel's one thread per session
   // would leave most SIMDs idle
   const int P = e->cfg.num_players;
-  const int G = (p.D + 1) * padded_players(P);
+  // the chains form's lanes per session: D roles + the batch for 2 <= D <= 8, else D + 1 roles
+  const bool chain_batch = p.D >= 2 && p.D <= 8;
+  const int G = (chain_batch ? p.D : p.D + 1) * padded_players(P);
   // plain history: the session's states are the canonical ones the remote inputs determine (the
   // canonical flat kernel also keeps the desync history; the chains form does not)
   const bool plain_hist = !e->sparse && !p.trace && !e->dbg_ever;
@@ -1483,11 +1549,13 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
       if (rc) return rc;
       return ggrs_p2p_advance_frames(e, n - max_n);
     }
-    const size_t lds = (size_t)(n + 2 * p.D + p.delay) * row_bytes;
+    size_t lds = (size_t)(n + 2 * p.D + p.delay) * row_bytes;
+    if (chain_batch) lds = ((lds + 15) & ~(size_t)15) + (size_t)(p.D + 1) * kWave * kStashEntry;
     int rc = p2p_launch_timed(e, [&] {
       dispatch_players(P, [&](auto PC) {
         constexpr int PP = decltype(PC)::value;
-        p2p_chains_kernel<PP><<<(unsigned)grid_of(p.S, spw), kWave, lds, e->stream>>>(p, spw);
+        if (chain_batch) p2p_chains_kernel<PP, true><<<(unsigned)grid_of(p.S, spw), kWave, lds, e->stream>>>(p, spw);
+        else p2p_chains_kernel<PP, false><<<(unsigned)grid_of(p.S, spw), kWave, lds, e->stream>>>(p, spw);
       });
     });
     if (rc) return rc;
