@@ -269,15 +269,14 @@ __device__ inline void drain_loads() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
 template <int kRow>
 __device__ inline void stage_input_rows(uint8_t* lds, const uint8_t* inputs, int64_t L, int Pp, int32_t cap,
-                                        int32_t gf, int nf, int64_t s0, int used, int row_rt, int tid,
-                                        int nthreads = kWave) {
+                                        int32_t gf, int nf, int64_t s0, int used, int row_rt, int tid) {
   const int row = kRow > 0 ? kRow : row_rt;
   const int32_t q0 = gf % cap;
   auto slot = [&](int ff) {
     const int32_t q = q0 + ff;
     return q >= cap ? q - cap : q;
   };
-  if (kRow == 8 && used == 8 && ((L * Pp) & 7) == 0 && nthreads == kWave) {
+  if (kRow == 8 && used == 8 && ((L * Pp) & 7) == 0) {
     for (int base = 0; base < nf; base += 4 * kWave) {
       uint64_t v[4];
 #pragma unroll
@@ -295,11 +294,11 @@ __device__ inline void stage_input_rows(uint8_t* lds, const uint8_t* inputs, int
     return;
   }
   const int total = nf * row;
-  for (int base = 0; base < total; base += 8 * nthreads) {
+  for (int base = 0; base < total; base += 8 * kWave) {
     uint8_t v[8];
 #pragma unroll
     for (int u = 0; u < 8; u++) {
-      const int q = base + u * nthreads + tid;
+      const int q = base + u * kWave + tid;
       if (q < total) {
         const int ff = q / row, b = q - ff * row;
         v[u] = b < used ? inputs[((int64_t)slot(ff) * L + s0) * Pp + b] : 0;
@@ -307,7 +306,7 @@ __device__ inline void stage_input_rows(uint8_t* lds, const uint8_t* inputs, int
     }
 #pragma unroll
     for (int u = 0; u < 8; u++) {
-      const int q = base + u * nthreads + tid;
+      const int q = base + u * kWave + tid;
       if (q < total) lds[q] = v[u];
     }
   }
@@ -614,14 +613,14 @@ struct EdgeStep : std::true_type {};
 template <class T> struct IsEdge : std::false_type {};
 template <> struct IsEdge<EdgeStep> : std::true_type {};
 
-template <int P, int KW>
-__global__ __launch_bounds__(KW) void synctest_pipelined_v5_kernel(PipeParams p) {
+template <int P>
+__global__ __launch_bounds__(kWave) void synctest_pipelined_v5_kernel(PipeParams p) {
   constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
   constexpr int F = state_fields(P);
   constexpr int n_bytes = Fletcher<P>::n;
   constexpr int CD = 8;             // check_distance this kernel is built for (the host checks)
   constexpr int G = CD * Pp;        // lanes per session
-  constexpr int SPW = KW / G;       // sessions per block (a block is one wave of KW threads)
+  constexpr int SPW = kWave / G;    // sessions per wave
   constexpr int ROW = SPW * Pp;     // staged input bytes per frame (= 8)
   constexpr int kB = 8;             // steps per batch (= role lanes that run it)
   constexpr int kEntry = 32;        // stash bytes per (session, player): 5 fields, 16-B aligned
@@ -653,15 +652,13 @@ __global__ __launch_bounds__(KW) void synctest_pipelined_v5_kernel(PipeParams p)
   // of frame g0, and the raw input rows; then the early-outs, the checkpoint's stores and the LDS.
   // Fast form for full blocks of 8-byte-aligned input rows; otherwise the generic copies.
   constexpr int kCkRegs = 16;  // checkpoint words per thread in the fast form
-  constexpr int kRawRegs = (kRaw + KW - 1) / KW;
+  constexpr int kRawRegs = (kRaw + kWave - 1) / kWave;
   const int ck_words32 = (1 + R) * F * SPW, ck_words16 = R * SPW;  // 16-bit rows as word pairs
-  const bool fast = nsess == SPW && ((L * Pp) & 7) == 0 && (L & 1) == 0 && ck_words32 + ck_words16 <= kCkRegs * KW;
+  const bool fast = nsess == SPW && ((L * Pp) & 7) == 0 && (L & 1) == 0 && ck_words32 + ck_words16 <= kCkRegs * kWave;
   const int32_t failed_f0 = *p.fail_f0;
   const int32_t lstat = p.lane_status[s < L ? s : L - 1];
   uint32_t ckv[kCkRegs];
-  using RawT = std::conditional_t<ROW == 8, uint2, uint32_t>;  // one staged input row
-  static_assert(ROW == 8 || ROW == 4, "input rows of 4 or 8 bytes");
-  RawT rawv[kRawRegs];
+  uint2 rawv[kRawRegs];
   uint16_t firstv = 0;
   const int nraw = (t_stage_end - p.f0) < raw_rows ? (t_stage_end - p.f0) : raw_rows;
   const int32_t slot_g0 = g0 % R;
@@ -669,7 +666,7 @@ __global__ __launch_bounds__(KW) void synctest_pipelined_v5_kernel(PipeParams p)
   if (fast) {
 #pragma unroll
     for (int i = 0; i < kCkRegs; i++) {
-      const int q = wl + i * KW;
+      const int q = wl + i * kWave;
       if (q < ck_words32) {
         const int row = q / SPW, ss = q % SPW;  // SPW is a power of two: shifts
         ckv[i] = row < F ? p.cur[(int64_t)row * L + s0 + ss] : p.ring[(int64_t)(row - F) * L + s0 + ss];
@@ -681,10 +678,10 @@ __global__ __launch_bounds__(KW) void synctest_pipelined_v5_kernel(PipeParams p)
     }
 #pragma unroll
     for (int i = 0; i < kRawRegs; i++) {
-      const int ff = wl + i * KW;
+      const int ff = wl + i * kWave;
       if (ff < nraw) {
         const int32_t slot = q0 + ff >= p.cap ? q0 + ff - p.cap : q0 + ff;
-        rawv[i] = *reinterpret_cast<const RawT*>(p.inputs + ((int64_t)slot * L + s0) * Pp);
+        rawv[i] = *reinterpret_cast<const uint2*>(p.inputs + ((int64_t)slot * L + s0) * Pp);
       }
     }
   }
@@ -751,12 +748,12 @@ __global__ __launch_bounds__(KW) void synctest_pipelined_v5_kernel(PipeParams p)
     if (fast) {
 #pragma unroll
       for (int i = 0; i < kCkRegs; i++) {
-        const int q = wl + i * KW;
+        const int q = wl + i * kWave;
         if (q < ck_words32 + ck_words16) reinterpret_cast<uint32_t*>(piece)[q] = ckv[i];
       }
     } else {
       const CheckpointMap m{L, R, F, SPW, p.cur, p.ring, p.ring_ck, p.first_ck};
-      checkpoint_sessions(m, piece, s0, nsess, wl, KW);
+      checkpoint_sessions(m, piece, s0, nsess, wl, kWave);
     }
   }
   if (failed_f0 >= 0) return;
@@ -768,11 +765,11 @@ __global__ __launch_bounds__(KW) void synctest_pipelined_v5_kernel(PipeParams p)
   if (fast) {
 #pragma unroll
     for (int i = 0; i < kRawRegs; i++) {
-      const int ff = wl + i * KW;
-      if (ff < nraw) reinterpret_cast<RawT*>(lds_raw)[ff] = rawv[i];
+      const int ff = wl + i * kWave;
+      if (ff < nraw) reinterpret_cast<uint2*>(lds_raw)[ff] = rawv[i];
     }
   } else {
-    stage_input_rows<ROW>(lds_raw, p.inputs, L, Pp, p.cap, g0, nraw, s0, nsess * Pp, ROW, wl, KW);
+    stage_input_rows<ROW>(lds_raw, p.inputs, L, Pp, p.cap, g0, nraw, s0, nsess * Pp, ROW, wl);
   }
   // the block is one wave: LDS written by one lane and read by another needs only the wave's own
   // in-order LDS queue and a compiler fence (a __syncthreads would also wait for the checkpoint's
@@ -807,12 +804,12 @@ __global__ __launch_bounds__(KW) void synctest_pipelined_v5_kernel(PipeParams p)
     if (t - raw0 + nf > raw_rows) {
       wave_lds_sync();
       const int nr = (t_stage_end - t) < raw_rows ? (t_stage_end - t) : raw_rows;
-      stage_input_rows<ROW>(lds_raw, p.inputs, L, Pp, p.cap, t - CD, nr, s0, nsess * Pp, ROW, wl, KW);
+      stage_input_rows<ROW>(lds_raw, p.inputs, L, Pp, p.cap, t - CD, nr, s0, nsess * Pp, ROW, wl);
       raw0 = t;
     }
     wave_lds_sync();
     const uint8_t* src = lds_raw + (t - raw0) * ROW;
-    for (int q = wl; q < nf * ROW; q += KW) {
+    for (int q = wl; q < nf * ROW; q += kWave) {
       const InputRec r = make_input_rec(src[q]);
       lds_rec[q] = make_uint4(r.delta, r.thr, r.sgn, r.keep);
     }
@@ -1124,16 +1121,6 @@ bool pipe_buffers_fit(const ggrs_engine* e) {
   return (uint64_t)e->F * 4 * L * e->R < kOob && ring_span < kOob && trace_span < kOob;
 }
 
-// v5's block: one wave of 64 threads, or of 32 (half the sessions per wave, twice the waves: two
-// waves per SIMD where one wave of 64 per SIMD would leave the SIMD issuing below its rate)
-int v5_block_threads(const ggrs_engine* e) {
-  static const int forced = [] {
-    const char* v = getenv("GGRS_V5_THREADS");
-    return v ? atoi(v) : 0;
-  }();
-  return forced == 32 ? 32 : kWave;
-}
-
 int v4_sessions_per_block(const ggrs_engine* e) {
   const int K = e->cfg.check_distance + 1;
   if (e->cfg.check_distance < 2 || K * e->Pp > kWave || !pipe_buffers_fit(e)) return 0;
@@ -1142,7 +1129,7 @@ int v4_sessions_per_block(const ggrs_engine* e) {
 
 int v5_sessions_per_block(const ggrs_engine* e) {
   if (e->cfg.check_distance != 8 || !pipe_buffers_fit(e)) return 0;
-  return v5_block_threads(e) / (8 * e->Pp);
+  return kWave / (8 * e->Pp);
 }
 
 // Which pipelined kernel a launch takes (4, 5, or 0 = sequential only).  The default picks v5
@@ -1376,14 +1363,6 @@ static int launch_sequential(ggrs_engine_t* e, int32_t f0, int32_t n) {
   });
 }
 
-template <int P>
-static void v5_launch(ggrs_engine_t* e, const PipeParams& p, int64_t grid) {
-  if (v5_block_threads(e) == 32)
-    synctest_pipelined_v5_kernel<P, 32><<<grid, 32, 0, e->stream>>>(p);
-  else
-    synctest_pipelined_v5_kernel<P, kWave><<<grid, kWave, 0, e->stream>>>(p);
-}
-
 static int launch_pipelined(ggrs_engine_t* e, int32_t f0, int32_t n) {
   PipeParams p;
   p.L = e->cfg.num_lanes;
@@ -1413,10 +1392,10 @@ static int launch_pipelined(ggrs_engine_t* e, int32_t f0, int32_t n) {
   return launch_timed(e, [&] {
     if (kernel == 5) {
       switch (e->cfg.num_players) {
-        case 1: v5_launch<1>(e, p, grid); break;
-        case 2: v5_launch<2>(e, p, grid); break;
-        case 3: v5_launch<3>(e, p, grid); break;
-        default: v5_launch<4>(e, p, grid); break;
+        case 1: synctest_pipelined_v5_kernel<1><<<grid, kWave, 0, e->stream>>>(p); break;
+        case 2: synctest_pipelined_v5_kernel<2><<<grid, kWave, 0, e->stream>>>(p); break;
+        case 3: synctest_pipelined_v5_kernel<3><<<grid, kWave, 0, e->stream>>>(p); break;
+        default: synctest_pipelined_v5_kernel<4><<<grid, kWave, 0, e->stream>>>(p); break;
       }
       return;
     }
