@@ -941,16 +941,27 @@ constexpr int kChainLdsRows = 16 * 1024;      // bytes of staged input rows per 
 // per wave instead of three), one extra step's work per D steps.
 constexpr int kStashEntry = 32;  // bytes per (session, player) entry of a stash slot: 5 fields
 
-template <int P, bool kB>
+//   kD = 8 at two players (config 2's P2P shape; the host picks it when remote_latency is 8): D
+// is a compile-time constant and a session's 16 lanes are one DPP row, so the lean steps run as
+// the v5 SyncTest kernel's do -- the rotation one row_shr:2 move per field (no LDS round trip),
+// every input byte decoded once per launch into an InputRec in LDS, and each step's sin/cos
+// computed one step ahead, inside the previous step, from the rotated rot.  Same operations on
+// the same values as the general step: the same bits.
+constexpr int kChainFastLds = 40 * 1024;  // the kD form's LDS budget per block (four blocks per CU)
+
+template <int P, bool kB, int kD = 0>
 __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t spw) {
   constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
   constexpr int F = state_fields(P);
   constexpr int C = cell_dwords(P);
   constexpr int n_bytes = Fletcher<P>::n;
+  constexpr bool kFast = kB && kD == 8 && Pp == 2;
+  static_assert(kD == 0 || kFast, "the compile-time latency form is the D = 8, two-player one");
   // [rows][spw * Pp]: input rows lo .. f0 + n - 1; kB: then (D + 1) stash slots (the last the
-  // dump every lane other than role D - 1 writes) of kWave entries
+  // dump every lane other than role D - 1 writes) of kWave entries; kFast: then the rows' InputRecs
+  // and one more, the record of input 0 (PredictDefault's prediction)
   extern __shared__ __attribute__((aligned(16))) uint8_t lds_rows[];
-  const int D = p.D, G = (kB ? D : D + 1) * Pp;
+  const int D = kD ? kD : p.D, G = (kB ? D : D + 1) * Pp;
   const int wl = threadIdx.x;
   const int g = wl / G, r = wl - g * G;
   const int j = r / Pp, pl = r - j * Pp;  // static role, player lane
@@ -998,6 +1009,15 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
   // the remote players' prediction before the launch (the input of frame f0 - 1 - D, or 0)
   uint32_t prev_in = (uint32_t)p.queue[(1 * P + plc) * S + s];
   __syncthreads();
+  const int n_entries = nrows * row_bytes;
+  uint4* const lds_rec = reinterpret_cast<uint4*>(lds_rows + (((n_entries + 15) & ~15) + (D + 1) * kWave * kStashEntry));
+  if constexpr (kFast) {
+    for (int i = wl; i <= n_entries; i += kWave) {
+      const InputRec r = make_input_rec(i < n_entries ? lds_rows[i] : 0u);
+      lds_rec[i] = make_uint4(r.delta, r.thr, r.sgn, r.keep);
+    }
+    __syncthreads();
+  }
   const bool lean_ok = __all(w[4] <= kTwoPiBits);
   // the input a lane's chain reads at step t: row t - back
   const int32_t back = local ? D + p.delay : D + j;
@@ -1160,8 +1180,133 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
       }
     }
   };
-  if (lean_ok) run(std::true_type());
-  else run(std::false_type());
+  // kFast: the lean steps as the v5 SyncTest kernel runs them (see above the kernel)
+  auto run_fast = [&] {
+    const uint32_t zero_idx = (uint32_t)n_entries;  // InputRec of input 0
+    auto rec_idx = [&](int32_t t) -> uint32_t {
+      return zero_in ? zero_idx : (uint32_t)((t - back - lo) * row_bytes + in_col);
+    };
+    float sc_s, sc_c;
+    uint32_t sc_qs, sc_qc;
+    glibc_sincosf_domain_raw(__builtin_bit_cast(float, w[4]), &sc_s, &sc_c, &sc_qs, &sc_qc);
+    auto fstep = [&](int32_t t, auto core_tag, const uint4 rv) {
+      constexpr bool kCore = decltype(core_tag)::value;
+      if constexpr (kCore) {
+        const uint32_t in = (uint32_t)lds_rows[(t - back - lo) * row_bytes + in_col];
+        const bool miss = counts && in != (p.predictor == 0 ? prev_in : 0u);
+        const uint64_t mb = __ballot(miss);
+        if (j == 0 && pl == 0 && valid && ((uint32_t)(mb >> gbase) & pmask)) rollbacks += 1;
+        prev_in = in;
+      }
+      {
+        float x = __builtin_bit_cast(float, w[0]), y = __builtin_bit_cast(float, w[1]);
+        float vx = __builtin_bit_cast(float, w[2]), vy = __builtin_bit_cast(float, w[3]);
+        float rot = __builtin_bit_cast(float, w[4]);
+        // the next step's rot is this lane's new rot one role up (role 0 keeps its own)
+        advance_player_rec_q(x, y, vx, vy, rot, InputRec{rv.x, rv.y, rv.z, rv.w}, sc_s, sc_c, sc_qs, sc_qc,
+                             [&](float rn) {
+                               const uint32_t rb = __builtin_bit_cast(uint32_t, rn);
+                               const uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp((int)rb, (int)rb, 0x112, 0xF, 0xF, false);
+                               glibc_sincosf_domain_raw(__builtin_bit_cast(float, nb), &sc_s, &sc_c, &sc_qs, &sc_qc);
+                             });
+        w[0] = __builtin_bit_cast(uint32_t, x);
+        w[1] = __builtin_bit_cast(uint32_t, y);
+        w[2] = __builtin_bit_cast(uint32_t, vx);
+        w[3] = __builtin_bit_cast(uint32_t, vy);
+        w[4] = __builtin_bit_cast(uint32_t, rot);
+      }
+      {  // role D - 1's post-advance state for the batch (every other lane writes its dump entry)
+        uint8_t* st = stash + stash_w;
+        if (stash_w < (uint32_t)(D * kWave * kStashEntry)) st += (uint32_t)((t - p.f0) & (D - 1)) * (uint32_t)(kWave * kStashEntry);
+        *reinterpret_cast<uint4*>(st) = make_uint4(w[0], w[1], w[2], w[3]);
+        *reinterpret_cast<uint32_t*>(st + 16) = w[4];
+      }
+      const uint32_t frame1 = (uint32_t)(t - D + 1);
+      const int js = kCore ? 0 : t - t_last;
+      if (kCore || js < D) {
+        uint32_t d1 = dot4_u8(frame1, wf1, c1), d2 = dot4_u8(frame1, wf2, c2);
+#pragma unroll
+        for (int q = 0; q < 5; q++) {
+          d1 = dot4_u8(w[q], one2, d1);
+          d2 = dot4_u8(w[q], wt[q], d2);
+        }
+        d1 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d1, 0xB1, 0xF, 0xF, true);  // xor 1
+        d2 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)d2, 0xB1, 0xF, 0xF, true);
+        const uint32_t ck = fletcher_from_doubled(d1, d2);
+        const bool me = kCore ? j == 0 : j == js;
+        const uint32_t so = (uint32_t)slot * (uint32_t)(C * 4);
+#pragma unroll
+        for (int q = 0; q < 5; q++) __builtin_amdgcn_raw_buffer_store_b32(w[q], rs_ring, me ? fo[q] : kChainOob, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(frame1, rs_ring, me ? fo_frame : kChainOob, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(ck, rs_ring, me ? fo_ck : kChainOob, so, 0);
+#pragma unroll
+        for (int k = F + 1; k < C; k++)
+          __builtin_amdgcn_raw_buffer_store_b32(0u, rs_ring, me && lead ? ck_pad + (k - F - 1) * 4 : kChainOob, so, 0);
+      }
+#pragma unroll
+      for (int q = 0; q < 5; q++) w[q] = (uint32_t)__builtin_amdgcn_update_dpp((int)w[q], (int)w[q], 0x112, 0xF, 0xF, false);
+      slot = slot + 1 == p.R ? 0 : slot + 1;
+    };
+    auto fbatch = [&](int32_t tb, int count) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const int32_t c = tb + j - (D - 1);
+      const bool act = valid && j < count;
+      const uint8_t* st = stash + (uint32_t)((tb - p.f0 + j) & (D - 1)) * (uint32_t)(kWave * kStashEntry) + entry;
+      const uint4 a = *reinterpret_cast<const uint4*>(st);
+      uint32_t v[5] = {a.x, a.y, a.z, a.w, *reinterpret_cast<const uint32_t*>(st + 16)};
+      const int32_t row = c - back_b;
+      const uint32_t ri = (row >= lo && !zero_b && j < count) ? (uint32_t)((row - lo) * row_bytes + in_col) : zero_idx;
+      const uint4 rv = lds_rec[ri];
+      float x = __builtin_bit_cast(float, v[0]), y = __builtin_bit_cast(float, v[1]);
+      float vx = __builtin_bit_cast(float, v[2]), vy = __builtin_bit_cast(float, v[3]);
+      float rot = __builtin_bit_cast(float, v[4]);
+      float bs, bc;
+      uint32_t bqs, bqc;
+      glibc_sincosf_domain_raw(rot, &bs, &bc, &bqs, &bqc);
+      advance_player_rec_q(x, y, vx, vy, rot, InputRec{rv.x, rv.y, rv.z, rv.w}, bs, bc, bqs, bqc);
+      if (act && c == t_last) {  // the launch's last call: the current state
+        v[0] = __builtin_bit_cast(uint32_t, x);
+        v[1] = __builtin_bit_cast(uint32_t, y);
+        v[2] = __builtin_bit_cast(uint32_t, vx);
+        v[3] = __builtin_bit_cast(uint32_t, vy);
+        v[4] = __builtin_bit_cast(uint32_t, rot);
+        if (owner) {
+#pragma unroll
+          for (int q = 0; q < 5; q++) p.cur[(int64_t)kq[q] * S + s] = v[q];
+        }
+        if (lead) p.cur[s] = (uint32_t)(c + 1);
+      }
+    };
+    int32_t t = p.f0;
+    // whole blocks of D calls: their D input records read up front, then the batch
+    for (; t + D - 1 <= t_last; t += D) {
+      uint4 in[kD > 0 ? kD : 1];
+#pragma unroll
+      for (int u = 0; u < kD; u++) in[u] = lds_rec[rec_idx(t + u)];
+#pragma unroll
+      for (int u = 0; u < kD; u++) fstep(t + u, std::true_type(), in[u]);
+      fbatch(t, D);
+    }
+    for (; t <= t_last; ++t) {
+      fstep(t, std::true_type(), lds_rec[rec_idx(t)]);
+      if ((t - p.f0) % D == D - 1) fbatch(t - (D - 1), D);
+    }
+    for (; t < t_end; ++t) {
+      fstep(t, std::false_type(), lds_rec[rec_idx(t)]);
+      if ((t - p.f0) % D == D - 1 || t == t_end - 1) {
+        const int count = (t - p.f0) % D + 1;
+        fbatch(t - (count - 1), count);
+      }
+    }
+  };
+  if (lean_ok) {
+    if constexpr (kFast) run_fast();
+    else run(std::true_type());
+  } else {
+    run(std::false_type());
+  }
   if (valid && j == 0 && pl == 0) {
     p.rollbacks[s] += rollbacks;
     p.resim[s] += (int64_t)rollbacks * D;
@@ -1549,11 +1694,31 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
       if (rc) return rc;
       return ggrs_p2p_advance_frames(e, n - max_n);
     }
+    // config 2's P2P shape (latency 8, two players): the compile-time form, whose decoded input
+    // records cap a launch's rows by its LDS budget
+    const bool fast = chain_batch && p.D == 8 && P == 2;
+    if (fast) {
+      const size_t fixed = (size_t)(p.D + 1) * kWave * kStashEntry + 16 + 16;  // stash, alignment, input-0 record
+      const int32_t fast_n = (int32_t)((kChainFastLds - fixed) / ((size_t)row_bytes * 17)) - 2 * p.D - p.delay;
+      if (fast_n >= 1 && n > fast_n) {
+        int rc = ggrs_p2p_advance_frames(e, fast_n);
+        if (rc) return rc;
+        return ggrs_p2p_advance_frames(e, n - fast_n);
+      }
+    }
     size_t lds = (size_t)(n + 2 * p.D + p.delay) * row_bytes;
+    const size_t n_entries = lds;
     if (chain_batch) lds = ((lds + 15) & ~(size_t)15) + (size_t)(p.D + 1) * kWave * kStashEntry;
+    if (fast) lds += (n_entries + 1) * 16;
     int rc = p2p_launch_timed(e, [&] {
       dispatch_players(P, [&](auto PC) {
         constexpr int PP = decltype(PC)::value;
+        if constexpr (PP == 2) {
+          if (fast) {
+            p2p_chains_kernel<PP, true, 8><<<(unsigned)grid_of(p.S, spw), kWave, lds, e->stream>>>(p, spw);
+            return;
+          }
+        }
         if (chain_batch) p2p_chains_kernel<PP, true><<<(unsigned)grid_of(p.S, spw), kWave, lds, e->stream>>>(p, spw);
         else p2p_chains_kernel<PP, false><<<(unsigned)grid_of(p.S, spw), kWave, lds, e->stream>>>(p, spw);
       });

@@ -252,6 +252,38 @@ def test_p2p_chains_form_matches_oracle(oracle, P, local, delay, mp, D, pred, mo
     assert done == frames
 
 
+CHAINS8_CASES = [
+    # P, local players, delay, max_prediction, latency 8, predictor, input model
+    (2, (0,), 0, 9, 8, 0, 1),
+    (2, (1,), 2, 9, 8, 1, 0),
+    (2, (), 1, 10, 8, 0, 0),
+]
+
+
+@pytest.mark.parametrize("P,local,delay,mp,D,pred,model", CHAINS8_CASES)
+def test_p2p_chains_latency8_matches_oracle(oracle, P, local, delay, mp, D, pred, model):
+    """The chains form's compile-time latency-8 kernel (config 2's P2P shape: DPP rotation, decoded
+    input records, sin/cos one step ahead) in launches of uneven length -- shorter than a batch,
+    not a multiple of 8, one split for its LDS budget (160 calls) -- with a partial last block
+    (301 sessions), PredictDefault, input delay and no local player: bit-exact against the
+    oracle's P2PSession after every checked launch."""
+    from ggrs_amd import P2PEngine
+    S, frames = 301, 258
+    rows = stream(S, frames, P, model, seed_base=0x7171)
+    eng = P2PEngine(S, num_players=P, local_players=local, input_delay=delay, max_prediction=mp,
+                    remote_latency=D, predictor=pred, input_capacity=frames + 8)
+    eng.add_inputs(0, rows)
+    done = 0
+    for k, (n, form) in enumerate([(2, "chains"), (7, "chains"), (9, "chains"), (160, "chains"), (3, "flat"),
+                                   (13, "chains"), (64, "chains")]):
+        eng.set_kernel_form(form)
+        eng.advance_frames(n)
+        done += n
+        if k in (2, 3, 6):
+            check_against_oracle(eng, rows[:done], [0, 1, 3, 4, 150, 299, 300], done, trace=False)
+    assert done == frames
+
+
 def test_p2p_chains_form_rejects_non_plain(oracle):
     """Forcing the chains form where it does not apply is an error, not a silent fallback."""
     from ggrs_amd import P2PEngine
