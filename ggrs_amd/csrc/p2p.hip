@@ -1010,7 +1010,12 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
   uint32_t prev_in = (uint32_t)p.queue[(1 * P + plc) * S + s];
   __syncthreads();
   const int n_entries = nrows * row_bytes;
-  uint4* const lds_rec = reinterpret_cast<uint4*>(lds_rows + (((n_entries + 15) & ~15) + (D + 1) * kWave * kStashEntry));
+  // kFast layout after the rows: the stash as D slots of spw x Pp entries, then D dump slots (the
+  // lanes other than role D - 1 all write one dump entry of the step's dump slot, so every step's
+  // stash store has the same static offset as its slot), then the decoded input records
+  const uint32_t fslot = (uint32_t)(row_bytes * kStashEntry);
+  uint8_t* const fstash = lds_rows + ((n_entries + 15) & ~15);
+  uint4* const lds_rec = reinterpret_cast<uint4*>(fstash + 2 * D * fslot);
   if constexpr (kFast) {
     for (int i = wl; i <= n_entries; i += kWave) {
       const InputRec r = make_input_rec(i < n_entries ? lds_rows[i] : 0u);
@@ -1182,20 +1187,27 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
   };
   // kFast: the lean steps as the v5 SyncTest kernel runs them (see above the kernel)
   auto run_fast = [&] {
-    const uint32_t zero_idx = (uint32_t)n_entries;  // InputRec of input 0
-    auto rec_idx = [&](int32_t t) -> uint32_t {
-      return zero_in ? zero_idx : (uint32_t)((t - back - lo) * row_bytes + in_col);
-    };
+    // a lane's input record and raw byte of call f0 + rel sit at base + rel x stride (PredictDefault
+    // roles: the record of input 0, stride 0)
+    const uint32_t zero_idx = (uint32_t)n_entries;
+    const int32_t row0 = p.f0 - back - lo;  // the lane's row of call f0
+    const uint32_t rec_base = (zero_in ? zero_idx : (uint32_t)(row0 * row_bytes + in_col)) * 16u;
+    const uint32_t rec_stride = zero_in ? 0u : (uint32_t)row_bytes * 16u;
+    const uint32_t raw_base = (uint32_t)(row0 * row_bytes + in_col);
+    const uint8_t* const rec_bytes = reinterpret_cast<const uint8_t*>(lds_rec);
+    auto rec_at = [&](int32_t rel) { return *reinterpret_cast<const uint4*>(rec_bytes + rec_base + (uint32_t)rel * rec_stride); };
+    auto raw_at = [&](int32_t rel) { return (uint32_t)lds_rows[raw_base + (uint32_t)rel * (uint32_t)row_bytes]; };
+    const uint32_t stash_w8 = (valid && j == D - 1) ? entry : (uint32_t)D * fslot;
     float sc_s, sc_c;
     uint32_t sc_qs, sc_qc;
     glibc_sincosf_domain_raw(__builtin_bit_cast(float, w[4]), &sc_s, &sc_c, &sc_qs, &sc_qc);
-    auto fstep = [&](int32_t t, auto core_tag, const uint4 rv) {
+    auto fstep = [&](int32_t t, auto core_tag, const uint4 rv, uint32_t in, uint32_t slot_off) {
       constexpr bool kCore = decltype(core_tag)::value;
       if constexpr (kCore) {
-        const uint32_t in = (uint32_t)lds_rows[(t - back - lo) * row_bytes + in_col];
-        const bool miss = counts && in != (p.predictor == 0 ? prev_in : 0u);
-        const uint64_t mb = __ballot(miss);
-        if (j == 0 && pl == 0 && valid && ((uint32_t)(mb >> gbase) & pmask)) rollbacks += 1;
+        // poll of call t, branch-free: a remote lane of role 0 whose arriving input differs from the
+        // prediction; either player lane's miss rolls the session back (xor-1 lane = the other player)
+        const uint32_t m = (counts && in != (p.predictor == 0 ? prev_in : 0u)) ? 1u : 0u;
+        rollbacks += (int32_t)(m | (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0xB1, 0xF, 0xF, true));
         prev_in = in;
       }
       {
@@ -1215,9 +1227,8 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
         w[3] = __builtin_bit_cast(uint32_t, vy);
         w[4] = __builtin_bit_cast(uint32_t, rot);
       }
-      {  // role D - 1's post-advance state for the batch (every other lane writes its dump entry)
-        uint8_t* st = stash + stash_w;
-        if (stash_w < (uint32_t)(D * kWave * kStashEntry)) st += (uint32_t)((t - p.f0) & (D - 1)) * (uint32_t)(kWave * kStashEntry);
+      {  // role D - 1's post-advance state for the batch (every other lane: the dump slot)
+        uint8_t* st = fstash + stash_w8 + slot_off;
         *reinterpret_cast<uint4*>(st) = make_uint4(w[0], w[1], w[2], w[3]);
         *reinterpret_cast<uint32_t*>(st + 16) = w[4];
       }
@@ -1253,7 +1264,7 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       const int32_t c = tb + j - (D - 1);
       const bool act = valid && j < count;
-      const uint8_t* st = stash + (uint32_t)((tb - p.f0 + j) & (D - 1)) * (uint32_t)(kWave * kStashEntry) + entry;
+      const uint8_t* st = fstash + (uint32_t)((tb - p.f0 + j) & (D - 1)) * fslot + entry;
       const uint4 a = *reinterpret_cast<const uint4*>(st);
       uint32_t v[5] = {a.x, a.y, a.z, a.w, *reinterpret_cast<const uint32_t*>(st + 16)};
       const int32_t row = c - back_b;
@@ -1280,23 +1291,30 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
       }
     };
     int32_t t = p.f0;
-    // whole blocks of D calls: their D input records read up front, then the batch
+    // whole blocks of D calls: their input records and bytes read up front, then the batch
     for (; t + D - 1 <= t_last; t += D) {
+      const int32_t rel = t - p.f0;
       uint4 in[kD > 0 ? kD : 1];
+      uint32_t raw[kD > 0 ? kD : 1];
 #pragma unroll
-      for (int u = 0; u < kD; u++) in[u] = lds_rec[rec_idx(t + u)];
+      for (int u = 0; u < kD; u++) {
+        in[u] = rec_at(rel + u);
+        raw[u] = raw_at(rel + u);
+      }
 #pragma unroll
-      for (int u = 0; u < kD; u++) fstep(t + u, std::true_type(), in[u]);
+      for (int u = 0; u < kD; u++) fstep(t + u, std::true_type(), in[u], raw[u], (uint32_t)u * fslot);
       fbatch(t, D);
     }
     for (; t <= t_last; ++t) {
-      fstep(t, std::true_type(), lds_rec[rec_idx(t)]);
-      if ((t - p.f0) % D == D - 1) fbatch(t - (D - 1), D);
+      const int32_t rel = t - p.f0;
+      fstep(t, std::true_type(), rec_at(rel), raw_at(rel), (uint32_t)(rel & (D - 1)) * fslot);
+      if ((rel & (D - 1)) == D - 1) fbatch(t - (D - 1), D);
     }
     for (; t < t_end; ++t) {
-      fstep(t, std::false_type(), lds_rec[rec_idx(t)]);
-      if ((t - p.f0) % D == D - 1 || t == t_end - 1) {
-        const int count = (t - p.f0) % D + 1;
+      const int32_t rel = t - p.f0;
+      fstep(t, std::false_type(), rec_at(rel), 0u, (uint32_t)(rel & (D - 1)) * fslot);
+      if ((rel & (D - 1)) == D - 1 || t == t_end - 1) {
+        const int count = (rel & (D - 1)) + 1;
         fbatch(t - (count - 1), count);
       }
     }
@@ -1698,7 +1716,7 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
     // records cap a launch's rows by its LDS budget
     const bool fast = chain_batch && p.D == 8 && P == 2;
     if (fast) {
-      const size_t fixed = (size_t)(p.D + 1) * kWave * kStashEntry + 16 + 16;  // stash, alignment, input-0 record
+      const size_t fixed = (size_t)2 * p.D * row_bytes * kStashEntry + 16 + 16;  // stash, alignment, input-0 record
       const int32_t fast_n = (int32_t)((kChainFastLds - fixed) / ((size_t)row_bytes * 17)) - 2 * p.D - p.delay;
       if (fast_n >= 1 && n > fast_n) {
         int rc = ggrs_p2p_advance_frames(e, fast_n);
@@ -1709,7 +1727,8 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
     size_t lds = (size_t)(n + 2 * p.D + p.delay) * row_bytes;
     const size_t n_entries = lds;
     if (chain_batch) lds = ((lds + 15) & ~(size_t)15) + (size_t)(p.D + 1) * kWave * kStashEntry;
-    if (fast) lds += (n_entries + 1) * 16;
+    if (fast)  // rows, the stash's 2D slots of row_bytes entries, the input records
+      lds = ((n_entries + 15) & ~(size_t)15) + (size_t)2 * p.D * row_bytes * kStashEntry + (n_entries + 1) * 16;
     int rc = p2p_launch_timed(e, [&] {
       dispatch_players(P, [&](auto PC) {
         constexpr int PP = decltype(PC)::value;

@@ -264,17 +264,17 @@ CHAINS8_CASES = [
 def test_p2p_chains_latency8_matches_oracle(oracle, P, local, delay, mp, D, pred, model):
     """The chains form's compile-time latency-8 kernel (config 2's P2P shape: DPP rotation, decoded
     input records, sin/cos one step ahead) in launches of uneven length -- shorter than a batch,
-    not a multiple of 8, one split for its LDS budget (160 calls) -- with a partial last block
+    not a multiple of 8, one split for its LDS budget (300 calls) -- with a partial last block
     (301 sessions), PredictDefault, input delay and no local player: bit-exact against the
     oracle's P2PSession after every checked launch."""
     from ggrs_amd import P2PEngine
-    S, frames = 301, 258
+    S, frames = 301, 398
     rows = stream(S, frames, P, model, seed_base=0x7171)
     eng = P2PEngine(S, num_players=P, local_players=local, input_delay=delay, max_prediction=mp,
                     remote_latency=D, predictor=pred, input_capacity=frames + 8)
     eng.add_inputs(0, rows)
     done = 0
-    for k, (n, form) in enumerate([(2, "chains"), (7, "chains"), (9, "chains"), (160, "chains"), (3, "flat"),
+    for k, (n, form) in enumerate([(2, "chains"), (7, "chains"), (9, "chains"), (300, "chains"), (3, "flat"),
                                    (13, "chains"), (64, "chains")]):
         eng.set_kernel_form(form)
         eng.advance_frames(n)
