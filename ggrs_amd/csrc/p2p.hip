@@ -771,13 +771,24 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_canon_kernel(P2PParams p) {
   for (int k = 0; k < P; k++)
     if (!((lmask >> k) & 1u)) prev_rem |= ((uint32_t)p.queue[(1 * P + k) * S + sess] & 0xffu) << (8 * k);
   const int ring_pieces = p.R * PC;
+  // Only the cells the launch may read before it Saves them come in: a rollback at call f loads
+  // frame f - D, the desync history reads frame f - 1 - D, and every frame >= f0 is saved by its
+  // own call first, so the cells of frames f0 - 1 - D .. f0 - 1 (from frame 0; D + 1 < R).  Only
+  // the cells the launch saves go back (frames f0 .. f0 + n - 1, the last R of them); the other
+  // cells stay as they are in HBM.
+  const uint4* const gring = reinterpret_cast<const uint4*>(p.ring) + sess0 * ring_pieces;
   {
-    const int n = nb * ring_pieces;
-    const uint4* src = reinterpret_cast<const uint4*>(p.ring) + sess0 * ring_pieces;
+    const int32_t first_in = max(0, p.f0 - 1 - p.D);
+    const int in_pieces = (p.f0 - first_in) * PC;
+    const int slot_in = first_in % p.R;
+    const int n = nb * in_pieces;
 #pragma unroll 4
     for (int i = lt; i < n; i += kFlatBlock) {
-      const int sl = i / ring_pieces, rem = i - sl * ring_pieces;
-      lds_ring[rem * kFlatBlock + sl] = src[i];
+      const int sl = i / in_pieces, q = i - sl * in_pieces;
+      const int d = q / PC, k = q - d * PC;
+      const int slot = slot_in + d >= p.R ? slot_in + d - p.R : slot_in + d;
+      const int rem = slot * PC + k;
+      lds_ring[rem * kFlatBlock + sl] = gring[sl * ring_pieces + rem];
     }
   }
   __syncthreads();
@@ -881,11 +892,17 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_canon_kernel(P2PParams p) {
   }
   __syncthreads();
   {
-    const int n = nb * ring_pieces;
-    uint4* dst = reinterpret_cast<uint4*>(p.ring) + sess0 * ring_pieces;
+    const int saved = p.n < p.R ? p.n : p.R;  // frames f_end - saved .. f_end - 1
+    const int out_pieces = saved * PC;
+    const int slot_out = (f_end - saved) % p.R;
+    const int n = nb * out_pieces;
+    uint4* const dst = reinterpret_cast<uint4*>(p.ring) + sess0 * ring_pieces;
     for (int i = lt; i < n; i += kFlatBlock) {
-      const int sl = i / ring_pieces, rem = i - sl * ring_pieces;
-      dst[i] = lds_ring[rem * kFlatBlock + sl];
+      const int sl = i / out_pieces, q = i - sl * out_pieces;
+      const int d = q / PC, k = q - d * PC;
+      const int slot = slot_out + d >= p.R ? slot_out + d - p.R : slot_out + d;
+      const int rem = slot * PC + k;
+      dst[sl * ring_pieces + rem] = lds_ring[rem * kFlatBlock + sl];
     }
   }
   if (!live) return;
