@@ -85,6 +85,11 @@ struct SpanTimer {
   }
 };
 
+// Cache-policy operand of the raw buffer store builtins on gfx950: sc1, a write-through store.
+// Used for saves a launch does not read back from L2 soon, so they drain to memory while the
+// kernel runs rather than in the end-of-kernel write-back of every dirtied L2 line.
+constexpr int kStoreWriteThrough = 16;
+
 // XCD-aware block order.  The dispatcher deals workgroup i to XCD i % 8 (MI355X: 8 XCDs, each
 // with its own L2), so neighbouring blocks -- whose sessions share 64-byte lines of every SoA
 // row (ring fields, checksums, input rows) -- would sit on different XCDs: each XCD fetches the
