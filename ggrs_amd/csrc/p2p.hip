@@ -995,6 +995,17 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
   // rows lo .. f0 + n - 1: role D reads frame t - 2D, the local players user input t - D - delay
   const int32_t lo = p.f0 - 2 * D - p.delay;
   const int32_t nrows = p.f0 + p.n - lo;
+  // (issued before the row staging: their memory latency behind its loads)
+  // every role starts from T_{f0-D}, the cell chain f0 loads (roles > 0 hold chains of the previous
+  // launch: stepped, never stored)
+  uint32_t w[5];
+  {
+    const uint32_t* cell = p.ring + ((int64_t)s * p.R + (p.f0 - D) % p.R) * C;
+#pragma unroll
+    for (int q = 0; q < 5; q++) w[q] = cell[kq[q]];
+  }
+  // the remote players' prediction before the launch (the input of frame f0 - 1 - D, or 0)
+  uint32_t prev_in = (uint32_t)p.queue[(1 * P + plc) * S + s];
   {
     // eight loads in flight per thread before their LDS stores (one memory latency per 512 bytes)
     constexpr int kBatch = 8;
@@ -1015,16 +1026,6 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
       }
     }
   }
-  // every role starts from T_{f0-D}, the cell chain f0 loads (roles > 0 hold chains of the previous
-  // launch: stepped, never stored)
-  uint32_t w[5];
-  {
-    const uint32_t* cell = p.ring + ((int64_t)s * p.R + (p.f0 - D) % p.R) * C;
-#pragma unroll
-    for (int q = 0; q < 5; q++) w[q] = cell[kq[q]];
-  }
-  // the remote players' prediction before the launch (the input of frame f0 - 1 - D, or 0)
-  uint32_t prev_in = (uint32_t)p.queue[(1 * P + plc) * S + s];
   __syncthreads();
   const int n_entries = nrows * row_bytes;
   // kFast layout after the rows: the stash as D slots of spw x Pp entries, then D dump slots (the
