@@ -694,11 +694,21 @@ __global__ __launch_bounds__(256) void decode_swar_kernel(DecodeParams p) {
   const int64_t pk0 = (int64_t)blockIdx.x * T;
   const int np = (int)((p.N - pk0) < T ? (p.N - pk0) : T);
   const int t = threadIdx.x;
+  // the packet's length and reference input, read first: their memory latency beside the packet
+  // copy's instead of after it
+  int64_t len = 0;
+  uint32_t rw = 0;
+  if (t < np) {
+    len = p.len[pk0 + t];
+    const uint8_t* rp = p.ref + (pk0 + t) * B;  // (byte loads: the caller's pointer may be unaligned)
+#pragma unroll
+    for (int b = 0; b < B; b++) rw |= (uint32_t)rp[b] << (8 * b);
+  }
   int d_off = t * in_pitch;
   if constexpr (kChunked) {  // the block's packets back to back: one coalesced copy of their bytes
     __shared__ int wsum[4];
     int total;
-    const int cb = t < np ? chunk_bytes(p.len[pk0 + t], stride) : 0;
+    const int cb = t < np ? chunk_bytes(len, stride) : 0;
     d_off = block_excl_scan(cb, wsum, &total);
     const uint32_t* s32 = reinterpret_cast<const uint32_t*>(p.packets + pk0 * stride);
     for (int q = t; q < total / 4; q += T) reinterpret_cast<uint32_t*>(l_in)[q] = s32[q];
@@ -714,7 +724,6 @@ __global__ __launch_bounds__(256) void decode_swar_kernel(DecodeParams p) {
     uint32_t* xr32 = reinterpret_cast<uint32_t*>(xb);
 #pragma unroll
     for (int k = 0; k < NDW; k++) xr32[k] = 0;  // 0x00 runs need no writes
-    const int64_t len = p.len[pk];
     int64_t cnt = 0;
     int32_t status = GGRS_CODEC_OK;
     if (len < 0 || len > stride || len < 1 || d[0] != 0) {
@@ -782,9 +791,6 @@ __global__ __launch_bounds__(256) void decode_swar_kernel(DecodeParams p) {
     uint32_t* orow = reinterpret_cast<uint32_t*>(l_out + t * out_pitch);
     if (status == GGRS_CODEC_OK) {
       const int xl = (int)cnt * B;
-      uint32_t rw = 0;
-#pragma unroll
-      for (int b = 0; b < B; b++) rw |= (uint32_t)p.ref[pk * B + b] << (8 * b);
       const uint32_t refpat = B == 1 ? rw * 0x01010101u : (B == 2 ? rw * 0x00010001u : rw);
       const uint32_t* xr = xr32;
       uint32_t carry = 0;  // the previous dword's last input, repeated
