@@ -692,6 +692,7 @@ def run_codec(args):
     d_ref, d_pend, d_cnt = (torch.from_numpy(x).to(dev) for x in (ref, pend, count))
     stride = codec.max_packet_bytes(B, W)
     chunked = args.codec_layout == "chunked"  # each 256-packet block's packets back to back
+    dec_buf = torch.empty((N, W, B), dtype=torch.uint8, device=dev)  # decoded inputs, reused per step
     evs = []
 
     def step(timed):
@@ -701,7 +702,7 @@ def run_codec(args):
         out, ln = codec.encode(d_ref, d_pend, d_cnt, stride, chunked=chunked)
         if timed:
             e[1].record()
-        dec, cnt, st = codec.decode(d_ref, out, ln, W, chunked=chunked)
+        dec, cnt, st = codec.decode(d_ref, out, ln, W, chunked=chunked, out=dec_buf)
         if timed:
             e[2].record()
             evs.append(e)

@@ -66,9 +66,11 @@ def encode(ref, pending, count, stride=None, chunked=False):
     return out, out_len
 
 
-def decode(ref, packets, lengths, max_inputs, chunked=False):
+def decode(ref, packets, lengths, max_inputs, chunked=False, out=None):
     """ref [N][B], packets [N][stride] u8, lengths [N] int32 -> (inputs [N][max_inputs][B] u8,
-    count [N] int32, status [N] int32: 0 or a GGRS_CODEC_* code)."""
+    count [N] int32, status [N] int32: 0 or a GGRS_CODEC_* code).  `out` (optional): a contiguous
+    u8 tensor [N][max_inputs][B] on the packets' device to decode into; every row is written whole
+    (slots past count and failed packets' rows are zero), so it needs no clearing."""
     import torch
     L = _lib.lib()
     _bind(L)
@@ -76,7 +78,11 @@ def decode(ref, packets, lengths, max_inputs, chunked=False):
     stride = packets.shape[1]
     ref, packets = ref.contiguous(), packets.contiguous()
     lengths = lengths.to(torch.int32).contiguous()
-    out = torch.zeros((N, max_inputs, B), dtype=torch.uint8, device=packets.device)
+    if out is None:
+        out = torch.empty((N, max_inputs, B), dtype=torch.uint8, device=packets.device)
+    elif (tuple(out.shape) != (N, max_inputs, B) or out.dtype != torch.uint8 or not out.is_contiguous()
+          or out.device != packets.device):
+        raise ValueError(f"out must be a contiguous uint8 tensor of shape {(N, max_inputs, B)} on {packets.device}")
     cnt = torch.empty(N, dtype=torch.int32, device=packets.device)
     st = torch.empty(N, dtype=torch.int32, device=packets.device)
     fn = L.ggrs_codec_decode_chunked if chunked else L.ggrs_codec_decode

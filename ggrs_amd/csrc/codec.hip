@@ -145,7 +145,9 @@ __device__ inline bool get_varint(const uint8_t* in, int64_t n, int64_t& pos, ui
 __global__ __launch_bounds__(256) void decode_kernel(DecodeParams p) {
   const int64_t pk = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (pk >= p.N) return;
+  uint8_t* const orow = p.out + pk * (int64_t)p.W * p.B;
   auto fail = [&](int32_t code) {
+    for (int64_t b = 0; b < (int64_t)p.W * p.B; b++) orow[b] = 0;  // every form writes whole rows
     p.status[pk] = code;
     p.count[pk] = 0;
   };
@@ -233,6 +235,7 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeParams p) {
       q += rl;
     }
   }
+  for (int64_t b = i; b < (int64_t)p.W * B; b++) o[b] = 0;  // the slots past count
   p.count[pk] = (int32_t)count;
   p.status[pk] = GGRS_CODEC_OK;
 }

@@ -542,7 +542,9 @@ int ggrs_codec_encode(const uint8_t* ref, const uint8_t* pending, const int32_t*
                       void* stream);
 /* decode: ref [n][input_bytes], packets [n][packet_stride] with packet_len [n] bytes ->
  * out [n][max_inputs][input_bytes], count [n], status [n] (GGRS_CODEC_OK or an error code;
- * never faults on hostile bytes -- decode_arbitrary_input_never_panics, compression.rs:205-213) */
+ * never faults on hostile bytes -- decode_arbitrary_input_never_panics, compression.rs:205-213).
+ * Every row of out is written whole: the slots past count, and a failed packet's row, are zero
+ * (out needs no clearing beforehand). */
 int ggrs_codec_decode(const uint8_t* ref, const uint8_t* packets, const int32_t* packet_len, int64_t n_packets,
                       int32_t packet_stride, int32_t input_bytes, int32_t max_inputs, uint8_t* out, int32_t* count,
                       int32_t* status, void* stream);

@@ -113,6 +113,31 @@ def test_hostile_packets_match_oracle(oracle, kernels, mode):
     assert len(seen) >= 2
 
 
+@pytest.mark.parametrize("W,B", [(16, 2), (8, 1), (33, 4), (3, 7)])
+def test_decode_writes_whole_rows(kernels, W, B):
+    """Every kernel form writes each output row whole into a dirty buffer: the decoded inputs, zero
+    past count, and an all-zero row for a rejected packet (the ABI's out needs no clearing)."""
+    from ggrs_amd import codec
+    rng = np.random.default_rng(W * 10 + B)
+    N = 1000
+    ref, pend, count = batch(rng, N, W, B)
+    out, ln = codec.encode(gpu(ref), gpu(pend), gpu(count))
+    ln = ln.cpu().numpy().copy()
+    bad = rng.random(N) < 0.2
+    ln[bad] = -1  # rejected: E_INVALID
+    dirty = torch.full((N, W, B), 0xAB, dtype=torch.uint8, device="cuda")
+    dec, cnt, st = codec.decode(gpu(ref), out, gpu(ln), max_inputs=W, out=dirty)
+    assert dec.data_ptr() == dirty.data_ptr()
+    dec, cnt, st = dec.cpu().numpy(), cnt.cpu().numpy(), st.cpu().numpy()
+    for p in range(N):
+        if bad[p]:
+            assert st[p] != 0 and cnt[p] == 0 and (dec[p] == 0).all(), p
+        else:
+            assert st[p] == 0 and cnt[p] == count[p], p
+            assert (dec[p, :count[p]] == pend[p, :count[p]]).all(), p
+            assert (dec[p, count[p]:] == 0).all(), p
+
+
 @pytest.mark.parametrize("W,B", [(8, 2), (16, 4), (33, 4), (1, 7)])
 def test_encode_errors(oracle, kernels, W, B):
     """count outside 0..W -> E_INVALID; a stride too small for the packet -> E_CAP; every other
