@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4: codec decode with its length / reference loads issued first; codec GPU tests and bench
+# Round 4: codec decode (prefetched length / reference, whole-row writes, reused output); codec GPU tests and bench
 # line (twice); config 4 and config 3 (general form) after the rounds_kernel experiment's removal.
 set -u
 TAG=${1:-r04l}
