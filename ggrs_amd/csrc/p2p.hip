@@ -1732,11 +1732,12 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
     }
     // config 2's P2P shape (latency 8, two players): the compile-time form, whose decoded input
     // records cap a launch's rows by its LDS budget
-    const bool fast = chain_batch && p.D == 8 && P == 2;
+    const size_t fast_fixed = (size_t)2 * 8 * row_bytes * kStashEntry + 16 + 16;  // stash, alignment, input-0 record
+    const int32_t fast_n = (int32_t)((kChainFastLds - fast_fixed) / ((size_t)row_bytes * 17)) - 2 * p.D - p.delay;
+    // (an input delay so long that no call fits the budget: the general form)
+    const bool fast = chain_batch && p.D == 8 && P == 2 && fast_n >= 1;
     if (fast) {
-      const size_t fixed = (size_t)2 * p.D * row_bytes * kStashEntry + 16 + 16;  // stash, alignment, input-0 record
-      const int32_t fast_n = (int32_t)((kChainFastLds - fixed) / ((size_t)row_bytes * 17)) - 2 * p.D - p.delay;
-      if (fast_n >= 1 && n > fast_n) {
+      if (n > fast_n) {
         int rc = ggrs_p2p_advance_frames(e, fast_n);
         if (rc) return rc;
         return ggrs_p2p_advance_frames(e, n - fast_n);
