@@ -29,9 +29,12 @@ FLAGS = ["-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC", "-std=c++
 # chains (the next sin/cos, the Fletcher sums, the stores) instead of the default
 # occupancy-oriented order.  Measured on MI355X (profiles/r03b): the v5 SyncTest launch 0.1951 ->
 # 0.1794 ms, the P2P flat kernel 0.1295 -> 0.1209 ms, config 3 2.4 -> 2.3 us per round, config 4
-# unchanged; the lane-server unit (requests.hip) was slower with it and keeps the default.
+# unchanged; the lane-server unit (requests.hip) was slower with it and keeps the default.  Round 4
+# (profiles/r04o, the whole library A/B twice): the default scheduler cost config 2 3 %, the P2P
+# kernels 4-6 %, and gained config 3's pipelined prefix kernel (lane-pair trunk split,
+# write-through saves) 3 %: 25.8 -> 25.0 us per 16-round step, so branch.hip keeps the default.
 ILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
-UNIT_FLAGS = {"engine.hip": ILP, "p2p.hip": ILP, "branch.hip": ILP}
+UNIT_FLAGS = {"engine.hip": ILP, "p2p.hip": ILP}
 
 
 def needs_build():
