@@ -921,6 +921,194 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_canon_kernel(P2PParams p) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Canonical flat form with sparse saving (plain launches, f0 >= D): the canonical kernel's call
+// (one row read and compare for the rollback decision, the inputs from the rows by the frame's
+// position against g = f - D) with the flat kernel's sparse schedule (p2p_session.rs:658-714,
+// 819-843): a rollback loads the LAST SAVE and replays from it -- frames <= g with their confirmed
+// remote inputs, later frames with the prediction input[g] (repeat-last) or 0 (PredictDefault) --
+// saving only min_confirmed (frame g); check_last_saved_state replays again from the last save
+// when the call would leave it max_prediction frames behind (the current frame is never
+// confirmed here: g < f).  The whole ring comes in and goes back (a load reaches up to R - 1
+// frames back); cell frame tags go to HBM as the flat kernel writes them.
+template <int P, int kLocal>
+__global__ __launch_bounds__(kFlatBlock) void p2p_canon_sparse_kernel(P2PParams p) {
+  const uint32_t lmask = kLocal >= 0 ? (uint32_t)kLocal : p.local_mask;
+  constexpr int Pp = P <= 1 ? 1 : (P == 2 ? 2 : 4);
+  constexpr int kRows = flat_rows_lds<P>();
+  constexpr int PC = cell_dwords(P) / 4;
+  constexpr int F = state_fields(P);
+  __shared__ __attribute__((aligned(16))) uint8_t lds_rows[kRows * kFlatBlock * Pp];
+  extern __shared__ uint4 lds_ring[];  // [R][PC][kFlatBlock]
+  const int64_t sess0 = (int64_t)blockIdx.x * kFlatBlock;
+  const int64_t S = p.S;
+  const bool live = sess0 + threadIdx.x < S;
+  const int64_t sess = live ? sess0 + threadIdx.x : sess0;
+  const int nb = (int)((S - sess0) < kFlatBlock ? (S - sess0) : kFlatBlock);
+  const int lt = threadIdx.x;
+  const int tid = live ? lt : 0;
+  uint32_t lbytes = 0;
+#pragma unroll
+  for (int k = 0; k < P; k++) lbytes |= ((lmask >> k) & 1u) ? 0xffu << (8 * k) : 0u;
+  const uint32_t rbytes = (P == 4 ? 0xffffffffu : ((1u << (8 * P)) - 1u)) & ~lbytes;
+  BoxState<P> st;
+  load_state<P>(st, p.cur + sess, S);
+  uint32_t prev_rem = 0;
+#pragma unroll
+  for (int k = 0; k < P; k++)
+    if (!((lmask >> k) & 1u)) prev_rem |= ((uint32_t)p.queue[(1 * P + k) * S + sess] & 0xffu) << (8 * k);
+  int32_t last_saved = p.last_saved[sess];
+  int32_t saved_slot = last_saved >= 0 ? last_saved % p.R : 0;
+  const int ring_pieces = p.R * PC;
+  {
+    const int n = nb * ring_pieces;
+    const uint4* src = reinterpret_cast<const uint4*>(p.ring) + sess0 * ring_pieces;
+#pragma unroll 4
+    for (int i = lt; i < n; i += kFlatBlock) {
+      const int sl = i / ring_pieces, rem = i - sl * ring_pieces;
+      lds_ring[rem * kFlatBlock + sl] = src[i];
+    }
+  }
+  __syncthreads();
+  auto cell_load = [&](int32_t slot) {
+#pragma unroll
+    for (int k = 0; k < PC; k++) {
+      const uint4 v = lds_ring[(slot * PC + k) * kFlatBlock + lt];
+      const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        if (4 * k + i < F) st.w[4 * k + i] = x[i];
+    }
+  };
+  auto save = [&](int32_t h, int32_t slot) {  // SaveGameState(h): the cell and its frame tag
+    const uint32_t ck = fletcher16_state<P>(st);
+#pragma unroll
+    for (int k = 0; k < PC; k++) {
+      uint32_t x[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) x[i] = 4 * k + i < F ? st.w[4 * k + i] : (4 * k + i == F ? ck : 0u);
+      lds_ring[(slot * PC + k) * kFlatBlock + lt] = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+    if (live) p.ring_frame[(int64_t)slot * S + sess] = h;
+    last_saved = h;
+    saved_slot = slot;
+  };
+  auto next_slot = [&](int32_t x) { return x + 1 == p.R ? 0 : x + 1; };
+  const bool lean_ok = __all(rot_in_domain<P>(st));
+  int32_t rollbacks = 0;
+  int64_t resim = 0;
+  int32_t slot_f = p.f0 % p.R, slot_h = 0;
+  const int32_t f_end = p.f0 + p.n;
+  const int32_t back = p.R - 1 + p.delay;       // a replay reaches back to the last save
+  const int32_t calls_per_stage = kRows - back;  // >= 1 (host)
+  for (int32_t fs = p.f0; fs < f_end;) {
+    const int32_t chunk_end = min(f_end, fs + calls_per_stage);
+    const int32_t lo = max(0, fs - back);
+    {
+      __syncthreads();
+      const int nrows = chunk_end - lo, row_bytes = nb * Pp;
+      if (nb == kFlatBlock && ((S * Pp) & 15) == 0) {
+        constexpr int kPieces = kFlatBlock * Pp / 16;
+#pragma unroll 4
+        for (int c = lt; c < nrows * kPieces; c += kFlatBlock) {
+          const int r = c / kPieces, k = c - r * kPieces;
+          const uint4* src = reinterpret_cast<const uint4*>(p.inputs + ((int64_t)((lo + r) % p.cap) * S + sess0) * Pp);
+          reinterpret_cast<uint4*>(lds_rows + r * kFlatBlock * Pp)[k] = src[k];
+        }
+      } else {
+        for (int c = lt; c < nrows * row_bytes; c += kFlatBlock) {
+          const int r = c / row_bytes, b = c - r * row_bytes;
+          lds_rows[r * kFlatBlock * Pp + b] = p.inputs[((int64_t)((lo + r) % p.cap) * S + sess0) * Pp + b];
+        }
+      }
+      __syncthreads();
+    }
+    const LdsRowsFlat<P> rows{lds_rows, lo, tid};
+    int32_t f = fs, h = 0, g = 0;
+    bool at_start = true, replaying = false, window_done = false;
+    uint32_t rem_pred = 0;
+    // adjust_gamestate from the last save (sparse: frame_to_load = last_saved_frame)
+    auto begin_replay = [&]() {
+      slot_h = saved_slot;
+      cell_load(slot_h);
+      h = last_saved;
+      replaying = true;
+      rollbacks += 1;
+      resim += f - last_saved;
+    };
+    // check_last_saved_state: the current frame f is unconfirmed (g < f), so a save that would
+    // leave the window means a replay from it
+    auto window_check = [&]() {
+      window_done = true;
+      if (f - last_saved >= p.R - 1) begin_replay();
+    };
+    while (f < chunk_end) {
+      if (at_start) {
+        if (p.desync_interval > 0) {  // check_checksum_send_interval (as the canonical kernel)
+          const int32_t fts = f - 1 - p.D;
+          if (live && fts >= p.desync_interval && fts % p.desync_interval == 0) {
+            const int32_t cs = fts % p.R;
+            const uint4 v = lds_ring[(cs * PC + F / 4) * kFlatBlock + lt];
+            const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+            p.hist[(int64_t)((fts / p.desync_interval) % kHist) * S + sess] = (uint16_t)x[F % 4];
+          }
+        }
+        g = f - p.D;
+        const uint32_t rem_conf = rows(g) & rbytes;
+        const bool miss = rem_conf != (p.predictor == 0 ? prev_rem : 0u);
+        prev_rem = rem_conf;
+        rem_pred = p.predictor == 0 ? rem_conf : 0u;
+        window_done = false;
+        if (miss) begin_replay();
+        if (!replaying) window_check();
+        at_start = false;
+      }
+      const int32_t fr = replaying ? h : f;
+      // frames <= g: the confirmed remote inputs; later ones: the prediction made from frame g
+      const uint32_t rem = fr <= g ? rows(max(fr, rows.lo)) & rbytes : rem_pred;
+      const uint32_t local = fr >= p.delay ? rows(max(fr - p.delay, rows.lo)) & lbytes : 0u;
+      if (replaying && h == g) save(h, slot_h);  // sparse: only min_confirmed, while replaying
+      if (lean_ok) advance_state_lean<P>(st, local | rem);
+      else advance_state<P>(st, local | rem, 0u);
+      if (replaying) {
+        slot_h = next_slot(slot_h);
+        if (++h == f) {
+          replaying = false;
+          if (!window_done) window_check();  // may replay again from the last save
+        }
+      } else {
+        slot_f = next_slot(slot_f);
+        ++f;
+        at_start = true;
+      }
+    }
+    fs = chunk_end;
+  }
+  __syncthreads();
+  {
+    const int n = nb * ring_pieces;
+    uint4* dst = reinterpret_cast<uint4*>(p.ring) + sess0 * ring_pieces;
+    for (int i = lt; i < n; i += kFlatBlock) {
+      const int sl = i / ring_pieces, rem = i - sl * ring_pieces;
+      dst[i] = lds_ring[rem * kFlatBlock + sl];
+    }
+  }
+  if (!live) return;
+  store_state<P>(st, p.cur + sess, S);
+  const int32_t t_last = f_end - 1;
+#pragma unroll
+  for (int k = 0; k < P; k++) {
+    if ((lmask >> k) & 1u) continue;
+    p.queue[(0 * P + k) * S + sess] = t_last - p.D + 1;
+    p.queue[(1 * P + k) * S + sess] = (int32_t)(p.predictor == 0 ? (prev_rem >> (8 * k)) & 0xffu : 0u);
+    p.queue[(2 * P + k) * S + sess] = kNull;
+    p.queue[(3 * P + k) * S + sess] = t_last;
+  }
+  p.rollbacks[sess] += rollbacks;
+  p.resim[sess] += resim;
+  p.last_saved[sess] = last_saved;
+}
+
+// ------------------------------------------------------------------------------------------
 // Chains form (few sessions: the flat kernel runs one thread per session, so 4096 sessions fill 64
 // of the chip's 1024 SIMDs).  With the remote inputs of frame g arriving exactly at call g + D,
 // the state a call works on is a function of the inputs alone: after call c every remote player's
@@ -1710,7 +1898,9 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
                                    "sparse saving), (remote_latency + 1) x padded players <= 64 lanes and a ring < 1 GiB");
   // the canonical flat kernel needs the same plain history and the remote inputs flowing (f0 >= D)
   const bool canon_ok = plain_hist && (e->form == 0 || e->form == 6);
-  if ((chains || canon_ok) && p.f0 < p.D) {  // the first D calls (no remote input yet): general flat
+  // and its sparse-saving form the same launches with sparse saving on
+  const bool canon_sparse_ok = e->sparse && !p.trace && !e->dbg_ever && (e->form == 0 || e->form == 6);
+  if ((chains || canon_ok || canon_sparse_ok) && p.f0 < p.D) {  // the first D calls (no remote input yet): general flat
     const int32_t m = std::min(n, p.D - p.f0);
     const int32_t form = e->form;
     e->form = 5;
@@ -1803,6 +1993,17 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
           }
         };
         const bool plain = p.desync_interval == 0 && !p.trace && p.dbg_sess < 0;
+        if (lds && canon_sparse_ok) {  // the canonical flat kernel with sparse saving (f0 >= D here)
+          const size_t shm = ring_lds;
+          if constexpr (P == 2) {
+            if (p.local_mask == 1u) p2p_canon_sparse_kernel<P, 1><<<grid, kFlatBlock, shm, e->stream>>>(p);
+            else if (p.local_mask == 2u) p2p_canon_sparse_kernel<P, 2><<<grid, kFlatBlock, shm, e->stream>>>(p);
+            else p2p_canon_sparse_kernel<P, -1><<<grid, kFlatBlock, shm, e->stream>>>(p);
+          } else {
+            p2p_canon_sparse_kernel<P, -1><<<grid, kFlatBlock, shm, e->stream>>>(p);
+          }
+          return;
+        }
         if (lds && canon_ok) {  // the canonical flat kernel (f0 >= D here)
           const size_t shm = ring_lds;
           if constexpr (P == 2) {

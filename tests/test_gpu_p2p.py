@@ -147,10 +147,13 @@ def test_p2p_sparse_saving_matches_oracle(oracle, P, local, delay, mp, D, pred, 
     check_against_oracle(eng, rows, [0, 1, 63, 64, 150, 299], frames)
 
 
-@pytest.mark.parametrize("P,local,delay,mp,D,pred,model", SPARSE_CASES[:2])
-def test_p2p_sparse_plain_launches_match_oracle(oracle, P, local, delay, mp, D, pred, model):
-    """Sparse saving in launches without trace/desync/debug (the flat kernel's plain sparse
-    specialisation): states, rings with their frame tags, and rollback counts bit-exact."""
+@pytest.mark.parametrize("form", ["default", "flat_queues", "mixed"])
+@pytest.mark.parametrize("P,local,delay,mp,D,pred,model", SPARSE_CASES)
+def test_p2p_sparse_plain_launches_match_oracle(oracle, P, local, delay, mp, D, pred, model, form):
+    """Sparse saving in launches without trace/debug: the canonical sparse kernel (default), the
+    queue-stepping flat kernel's plain sparse specialisation, and the two alternating launch by
+    launch ("mixed": each continues from the other's queues, last save and ring tags): states,
+    rings with their frame tags, and rollback / resimulation counts bit-exact."""
     from ggrs_amd import P2PEngine
     S, frames = 300, 200
     rows = stream(S, frames, P, model, seed_base=0x3131)
@@ -158,7 +161,11 @@ def test_p2p_sparse_plain_launches_match_oracle(oracle, P, local, delay, mp, D, 
                     remote_latency=D, predictor=pred)
     eng.set_sparse_saving(True)
     eng.add_inputs(0, rows)
-    for n in (2, 61, 137):
+    for k, n in enumerate((2, 61, 5, 1, 131)):
+        if form == "mixed":
+            eng.set_kernel_form(("canonical", "flat_queues")[k % 2])
+        elif form != "default":
+            eng.set_kernel_form(form)
         eng.advance_frames(n)
     check_against_oracle(eng, rows, [0, 1, 63, 64, 150, 299], frames, trace=False)
 
