@@ -231,5 +231,6 @@ class P2PEngine:
         memory), "chains" (every call as a chain of remote_latency + 1 advances from the confirmed
         state, chains pipelined over lanes; plain launches only), "flat_queues" (the flattened form
         with LDS rings stepping the InputQueue bookkeeping) or "canonical" (the flattened form with
-        the rollback decision read off the inputs, the default's choice for plain launches)."""
+        the rollback decision read off the inputs, the default's choice for plain launches, sparse
+        saving included)."""
         _lib.check(self._L.ggrs_p2p_set_unstaged(self._h, self.KERNEL_FORMS[form]))

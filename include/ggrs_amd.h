@@ -515,7 +515,8 @@ int ggrs_p2p_set_sparse_saving(ggrs_p2p_engine_t* eng, int32_t on);
  * 6 = canonical flattened form (the default for plain launches that do not take the chains form):
  * the rollback decision of call f is the remote input of frame f - D against the prediction made
  * from frame f - D - 1, the replay's remote inputs the confirmed and then the predicted ones -- the
- * queue state the fixed-latency network implies, written back at the end. */
+ * queue state the fixed-latency network implies, written back at the end; with sparse saving on
+ * (no trace or debug flip) the same form replays from the last save and saves min_confirmed. */
 int ggrs_p2p_set_unstaged(ggrs_p2p_engine_t* eng, int32_t form);
 /* test hook: the AdvanceFrame from `frame` of `session` flips the lowest bit of player 0's x on
  * every (re)simulation -- a deterministic desync of this peer (session -1: off) */
