@@ -1146,9 +1146,8 @@ constexpr int kChainLdsRows = 16 * 1024;      // bytes of staged input rows per 
 // per wave instead of three), one extra step's work per D steps.
 constexpr int kStashEntry = 32;  // bytes per (session, player) entry of a stash slot: 5 fields
 
-//   kD = 8 or 4 at two players (config 2's P2P shape is 8; the host picks these when
-// remote_latency is one of them): D is a compile-time constant and a session's 2D lanes lie in
-// one DPP row (two sessions per row at D = 4), so the lean steps run as
+//   kD = 8 at two players (config 2's P2P shape; the host picks it when remote_latency is 8): D
+// is a compile-time constant and a session's 16 lanes are one DPP row, so the lean steps run as
 // the v5 SyncTest kernel's do -- the rotation one row_shr:2 move per field (no LDS round trip),
 // every input byte decoded once per launch into an InputRec in LDS, and each step's sin/cos
 // computed one step ahead, inside the previous step, from the rotated rot.  Same operations on
@@ -1161,8 +1160,8 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
   constexpr int F = state_fields(P);
   constexpr int C = cell_dwords(P);
   constexpr int n_bytes = Fletcher<P>::n;
-  constexpr bool kFast = kB && (kD == 8 || kD == 4) && Pp == 2;
-  static_assert(kD == 0 || kFast, "the compile-time latency forms are D = 4 and 8 at two players");
+  constexpr bool kFast = kB && kD == 8 && Pp == 2;
+  static_assert(kD == 0 || kFast, "the compile-time latency form is the D = 8, two-player one");
   // [rows][spw * Pp]: input rows lo .. f0 + n - 1; kB: then (D + 1) stash slots (the last the
   // dump every lane other than role D - 1 writes) of kWave entries; kFast: then the rows' InputRecs
   // and one more, the record of input 0 (PredictDefault's prediction)
@@ -1408,15 +1407,6 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
     float sc_s, sc_c;
     uint32_t sc_qs, sc_qc;
     glibc_sincosf_domain_raw(__builtin_bit_cast(float, w[4]), &sc_s, &sc_c, &sc_qs, &sc_qc);
-    // the rotation: role j takes role j - 1's value, role 0 keeps its own -- one row_shr:2 DPP move
-    // (a row's first two lanes keep theirs); at D = 4 a 16-lane row holds two sessions, and the
-    // second one's role-0 lanes select their own value back
-    const bool role0 = j == 0;
-    auto rot_up = [&](uint32_t v) -> uint32_t {
-      const uint32_t m = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x112, 0xF, 0xF, false);
-      if constexpr (kD == 8) return m;
-      else return role0 ? v : m;
-    };
     auto fstep = [&](int32_t t, auto core_tag, const uint4 rv, uint32_t in, uint32_t slot_off) {
       constexpr bool kCore = decltype(core_tag)::value;
       if constexpr (kCore) {
@@ -1434,7 +1424,8 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
         advance_player_rec_q(x, y, vx, vy, rot, InputRec{rv.x, rv.y, rv.z, rv.w}, sc_s, sc_c, sc_qs, sc_qc,
                              [&](float rn) {
                                const uint32_t rb = __builtin_bit_cast(uint32_t, rn);
-                               glibc_sincosf_domain_raw(__builtin_bit_cast(float, rot_up(rb)), &sc_s, &sc_c, &sc_qs, &sc_qc);
+                               const uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp((int)rb, (int)rb, 0x112, 0xF, 0xF, false);
+                               glibc_sincosf_domain_raw(__builtin_bit_cast(float, nb), &sc_s, &sc_c, &sc_qs, &sc_qc);
                              });
         w[0] = __builtin_bit_cast(uint32_t, x);
         w[1] = __builtin_bit_cast(uint32_t, y);
@@ -1470,7 +1461,7 @@ __global__ __launch_bounds__(kWave) void p2p_chains_kernel(P2PParams p, int32_t 
           __builtin_amdgcn_raw_buffer_store_b32(0u, rs_ring, me && lead ? ck_pad + (k - F - 1) * 4 : kChainOob, so, 0);
       }
 #pragma unroll
-      for (int q = 0; q < 5; q++) w[q] = rot_up(w[q]);
+      for (int q = 0; q < 5; q++) w[q] = (uint32_t)__builtin_amdgcn_update_dpp((int)w[q], (int)w[q], 0x112, 0xF, 0xF, false);
       slot = slot + 1 == p.R ? 0 : slot + 1;
     };
     auto fbatch = [&](int32_t tb, int count) {
@@ -1931,10 +1922,10 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
     }
     // config 2's P2P shape (latency 8, two players): the compile-time form, whose decoded input
     // records cap a launch's rows by its LDS budget
-    const size_t fast_fixed = (size_t)2 * p.D * row_bytes * kStashEntry + 16 + 16;  // stash, alignment, input-0 record
+    const size_t fast_fixed = (size_t)2 * 8 * row_bytes * kStashEntry + 16 + 16;  // stash, alignment, input-0 record
     const int32_t fast_n = (int32_t)((kChainFastLds - fast_fixed) / ((size_t)row_bytes * 17)) - 2 * p.D - p.delay;
     // (an input delay so long that no call fits the budget: the general form)
-    const bool fast = chain_batch && (p.D == 8 || p.D == 4) && P == 2 && fast_n >= 1;
+    const bool fast = chain_batch && p.D == 8 && P == 2 && fast_n >= 1;
     if (fast) {
       if (n > fast_n) {
         int rc = ggrs_p2p_advance_frames(e, fast_n);
@@ -1952,8 +1943,7 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
         constexpr int PP = decltype(PC)::value;
         if constexpr (PP == 2) {
           if (fast) {
-            if (p.D == 8) p2p_chains_kernel<PP, true, 8><<<(unsigned)grid_of(p.S, spw), kWave, lds, e->stream>>>(p, spw);
-            else p2p_chains_kernel<PP, true, 4><<<(unsigned)grid_of(p.S, spw), kWave, lds, e->stream>>>(p, spw);
+            p2p_chains_kernel<PP, true, 8><<<(unsigned)grid_of(p.S, spw), kWave, lds, e->stream>>>(p, spw);
             return;
           }
         }

@@ -260,20 +260,17 @@ def test_p2p_chains_form_matches_oracle(oracle, P, local, delay, mp, D, pred, mo
 
 
 CHAINS8_CASES = [
-    # P, local players, delay, max_prediction, latency 8 or 4, predictor, input model
+    # P, local players, delay, max_prediction, latency 8, predictor, input model
     (2, (0,), 0, 9, 8, 0, 1),
     (2, (1,), 2, 9, 8, 1, 0),
     (2, (), 1, 10, 8, 0, 0),
-    (2, (0,), 0, 8, 4, 0, 1),
-    (2, (1,), 3, 6, 4, 1, 0),
 ]
 
 
 @pytest.mark.parametrize("P,local,delay,mp,D,pred,model", CHAINS8_CASES)
 def test_p2p_chains_latency8_matches_oracle(oracle, P, local, delay, mp, D, pred, model):
-    """The chains form's compile-time latency kernels (8: config 2's P2P shape, one session per DPP
-    row; 4: two sessions per row -- DPP rotation, decoded input records, sin/cos one step ahead)
-    in launches of uneven length -- shorter than a batch,
+    """The chains form's compile-time latency-8 kernel (config 2's P2P shape: DPP rotation, decoded
+    input records, sin/cos one step ahead) in launches of uneven length -- shorter than a batch,
     not a multiple of 8, one split for its LDS budget (300 calls) -- with a partial last block
     (301 sessions), PredictDefault, input delay and no local player: bit-exact against the
     oracle's P2PSession after every checked launch."""
