@@ -35,7 +35,11 @@ FLAGS = ["-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC", "-std=c++
 # write-through saves) 3 %: 25.8 -> 25.0 us per 16-round step, so branch.hip keeps the default.
 # max-ilp on every unit (profiles/r04q, r04r): codec and the request boundary unchanged, and the
 # particle unit's checksums CHANGE (its GPU parity tests fail: the ring states and checksums differ
-# from frame ~50 on; root cause not found), so particles.hip must stay on the default scheduler.
+# from frame ~50 on), so particles.hip must stay on the default scheduler.  The failure follows
+# particles.h's two inline-asm 24-bit multiply-adds: with them written as __umul24 / __mul24 the
+# max-ilp build passes every particle test (profiles/r04v).  The engine and P2P units, which use
+# inline asm too (fletcher_from_doubled, the sincosf quadrant select), pass all their parity tests
+# under max-ilp; their kernels are re-verified by the GPU suite on every build.
 ILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
 UNIT_FLAGS = {"engine.hip": ILP, "p2p.hip": ILP}
 
