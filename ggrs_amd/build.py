@@ -39,7 +39,9 @@ FLAGS = ["-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC", "-std=c++
 # particles.h's two inline-asm 24-bit multiply-adds: with them written as __umul24 / __mul24 the
 # max-ilp build passes every particle test (profiles/r04v).  The engine and P2P units, which use
 # inline asm too (fletcher_from_doubled, the sincosf quadrant select), pass all their parity tests
-# under max-ilp; their kernels are re-verified by the GPU suite on every build.
+# under max-ilp; their kernels are re-verified by the GPU suite on every build.  Also measured on
+# every unit (profiles/r04w): max-memory-clause, config 2 and the P2P chains 3 % slower, config 3
+# equal; iterative-ilp crashes this hipcc on particles.hip.
 ILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
 UNIT_FLAGS = {"engine.hip": ILP, "p2p.hip": ILP}
 
