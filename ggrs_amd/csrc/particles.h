@@ -71,17 +71,13 @@ __device__ inline void advance_entity(uint32_t (&w)[kFields], uint32_t input) {
 // (as box_game.h fletcher_from_doubled).  Adds s1d = 2 (A_e mod 255), s2d = 2 (x mod 255), each < 510.
 constexpr uint32_t kJ2Bias = 2u * 255u * 4951u;
 
-__device__ inline uint32_t mad_u24(uint32_t a, uint32_t b, uint32_t c) {
-  uint32_t r;
-  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
+// (24-bit multiply-adds written with __umul24 / __mul24, not inline asm: the inline-asm form
+// gave wrong checksums under LLVM's max-ilp scheduler -- profiles/r04r, r04v -- and this unit is
+// HBM-bound, so the compiler's choice of instructions costs nothing measurable)
+__device__ inline uint32_t mad_u24(uint32_t a, uint32_t b, uint32_t c) { return __umul24(a, b) + c; }
 __device__ inline uint32_t rem255_doubled(uint32_t x2) {  // 2 (x mod 255) for x2 = 2x < 2^24
   const uint32_t q = mulhi_u24(x2, 0x808081u);
-  uint32_t r;
-  const int32_t m510 = -510;
-  asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(q), "s"(m510), "v"(x2));
-  return r;
+  return (uint32_t)(__mul24((int32_t)q, -510) + (int32_t)x2);
 }
 __device__ inline void fletcher_entity_mod(uint32_t& s1d, uint32_t& s2d, const uint32_t (&w)[kFields], uint32_t c_e) {
   uint32_t a2 = 0, j2 = 0;
