@@ -558,9 +558,10 @@ def run_p2p(args):
     from ggrs_amd import P2PEngine, synth
     S = args.sessions or 65536
     P, D, maxp, calls = 2, args.latency, args.max_prediction, 64
-    if not 0 <= D <= maxp:
-        raise SystemExit(f"--latency {D} must be in 0..--max-prediction {maxp} (p2p_session.rs:296-310: "
-                         "a session cannot run further ahead of its confirmed inputs)")
+    if not (1 <= D <= maxp - 1 or (maxp == 0 and D >= 1)):
+        raise SystemExit(f"--latency {D} must be in 1..--max-prediction - 1 = {maxp - 1} (1.. in lockstep mode): "
+                         "the engine's contract (include/ggrs_amd.h, ggrs_p2p_config_t.remote_latency), else the "
+                         "prediction threshold stalls the session (p2p_session.rs:393-423)")
     frames = (args.warmup + args.steps) * calls
     # --peers: rank r and rank r + world/2 are the two machines of the same matches (local player
     # 0 on one, 1 on the other, the same inputs); their checksum reports (desync detection,
@@ -977,6 +978,7 @@ def run_requests(args):
     if form in ("native", "p2p"):
         from ggrs_amd import build as gbuild
         drv = ctypes.CDLL(gbuild.build_driver())
+        drv.handler_last_error.restype = ctypes.c_char_p
     if form == "p2p":
         fx = load_p2p_fixture()
         P, maxp = fx["P"], fx["maxp"]
@@ -1033,7 +1035,7 @@ def run_requests(args):
                                               ptr(fx["adv_off"]), ptr(fx["inputs"]), ptr(fx["status"]),
                                               ptr(fx["shape"]), ptr(lane_frames), c, n, args.session_us,
                                               int(args.req_deferred), T, ctypes.byref(s), ctypes.byref(sec), ph)
-            assert rc == 0, (rc, eng._L.ggrs_last_error())
+            assert rc == 0, (rc, drv.handler_last_error() or eng._L.ggrs_last_error())
             phases[:] = list(ph)
             sink[0] += s.value
     elif form == "batch":

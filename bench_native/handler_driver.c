@@ -24,6 +24,11 @@
 
 #include "ggrs_amd.h"
 
+/* the rejection message of a failed encode on an OpenMP worker: ggrs_last_error() is thread-local
+ * in the engine, so the worker's message is copied here for the calling thread (handler_last_error) */
+static char g_drv_error[512];
+const char* handler_last_error(void) { return g_drv_error; }
+
 static double now_s(void) {
   struct timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
@@ -311,7 +316,13 @@ int handler_drive_p2p_groups(ggrs_engine_t** engs, int32_t G, int32_t L, int32_t
                                   lane_frames[lane], &bad);
         if (rc) {
 #pragma omp critical
-          enc_rc = rc; /* the fixture's lists are valid: any rejection is an error here */
+          { /* the fixture's lists are valid: any rejection is an error here */
+            if (!enc_rc) {
+              strncpy(g_drv_error, ggrs_last_error(), sizeof g_drv_error - 1);
+              g_drv_error[sizeof g_drv_error - 1] = 0;
+            }
+            enc_rc = rc;
+          }
         }
       }
       if (enc_rc) return enc_rc;

@@ -288,20 +288,14 @@ __host__ __device__ inline void glibc_sincosf_domain_raw_k(float y, float* sr, f
   const double x6 = x4 * x2;
   const double cc = __builtin_fma(x4, K.c2, c1);
   const uint32_t C = __builtin_bit_cast(uint32_t, (float)__builtin_fma(x6, c2, cc));
-#if defined(__HIP_DEVICE_COMPILE__)
-  // one v_bfe_i32 (all ones in odd quadrants) and two v_bfi_b32 (the compiler expanded the
-  // equivalent and/or form into nine instructions)
-  uint32_t m, srb, crb;
-  asm("v_bfe_i32 %0, %1, 0, 1" : "=v"(m) : "v"(n));
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(srb) : "v"(m), "v"(C), "v"(S));
-  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(crb) : "v"(m), "v"(S), "v"(C));
-  *sr = __builtin_bit_cast(float, srb);
-  *cr = __builtin_bit_cast(float, crb);
-#else
+  // the swap as xor-selects: gfx950 codegen is one v_bfe_i32 (all ones in odd quadrants) and two
+  // v_bitop3_b32 -- the instruction count of the round-4 inline asm (v_bfe_i32 + two v_bfi_b32),
+  // with every consumer visible to the compiler's hazard recognizer (box_game.h,
+  // fletcher_from_doubled, says why that matters)
   const uint32_t m = 0u - (n & 1u);  // all ones in odd quadrants
-  *sr = __builtin_bit_cast(float, (m & C) | (~m & S));
-  *cr = __builtin_bit_cast(float, (m & S) | (~m & C));
-#endif
+  const uint32_t sc = S ^ C;
+  *sr = __builtin_bit_cast(float, S ^ (sc & m));
+  *cr = __builtin_bit_cast(float, C ^ (sc & m));
   const uint32_t l30 = n << 30, l31 = n << 31;
   *qs = l30 & 0x80000000u;
   *qc = (l30 ^ l31) & 0x80000000u;

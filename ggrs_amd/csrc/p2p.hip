@@ -773,9 +773,13 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_canon_kernel(P2PParams p) {
   const int ring_pieces = p.R * PC;
   // Only the cells the launch may read before it Saves them come in: a rollback at call f loads
   // frame f - D, the desync history reads frame f - 1 - D, and every frame >= f0 is saved by its
-  // own call first, so the cells of frames f0 - 1 - D .. f0 - 1 (from frame 0; D + 1 < R).  Only
-  // the cells the launch saves go back (frames f0 .. f0 + n - 1, the last R of them); the other
-  // cells stay as they are in HBM.
+  // own call first, so the cells of frames f0 - 1 - D .. f0 - 1 (from frame 0; D + 1 < R).  The
+  // cells the launch may have written go back: its own frames f0 .. f0 + n - 1 and, because a
+  // rollback at call f re-saves frames f - D + 1 .. f - 1 (adjust_gamestate saves every replayed
+  // frame but the loaded one, p2p_session.rs:696-706), the frames f0 - D + 1 .. f0 - 1 a rollback
+  // in the launch's first D - 1 calls rewrites -- the newest R of frames max(0, f0 - D + 1) ..
+  // f0 + n - 1 (every one of them is in LDS: copied in, or saved by the launch).  The other cells
+  // stay as they are in HBM.
   const uint4* const gring = reinterpret_cast<const uint4*>(p.ring) + sess0 * ring_pieces;
   {
     const int32_t first_in = max(0, p.f0 - 1 - p.D);
@@ -892,7 +896,9 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_canon_kernel(P2PParams p) {
   }
   __syncthreads();
   {
-    const int saved = p.n < p.R ? p.n : p.R;  // frames f_end - saved .. f_end - 1
+    // frames f_end - saved .. f_end - 1: the launch's own and those its early rollbacks re-saved
+    const int32_t first_out = max(max(0, p.f0 - p.D + 1), f_end - p.R);
+    const int saved = f_end - first_out;
     const int out_pieces = saved * PC;
     const int slot_out = (f_end - saved) % p.R;
     const int n = nb * out_pieces;

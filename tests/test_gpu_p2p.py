@@ -302,6 +302,29 @@ def test_p2p_chains_form_rejects_non_plain(oracle):
         eng.advance_frames(8)
 
 
+@pytest.mark.parametrize("P,local,delay,mp,D,form", [(2, (0,), 0, 8, 3, "canonical"), (2, (1,), 1, 7, 5, "canonical"),
+                                                     (4, (0, 2), 0, 8, 4, "canonical"), (2, (0,), 0, 8, 3, "default")])
+def test_p2p_single_call_launches_match_oracle(oracle, P, local, delay, mp, D, form):
+    """advance_frames(1) per tick on the canonical flat kernel with remote_latency >= 2 and uniform
+    inputs (a misprediction at almost every call): a rollback in a launch's first calls re-saves
+    frames before the launch's first frame (adjust_gamestate saves every replayed frame but the
+    loaded one, p2p_session.rs:696-706), and those cells must reach HBM -- the next launch loads
+    them.  State, whole ring and stats bit-exact with the oracle after every launch."""
+    from ggrs_amd import P2PEngine
+    S, frames = 130, 36
+    rows = stream(S, frames, P, 0, seed_base=0x5151)
+    eng = P2PEngine(S, num_players=P, local_players=local, input_delay=delay, max_prediction=mp,
+                    remote_latency=D, input_capacity=frames + 8)
+    eng.set_kernel_form(form)
+    eng.add_inputs(0, rows)
+    for done in range(1, frames + 1):
+        eng.advance_frames(1)
+        if done >= D:
+            check_against_oracle(eng, rows[:done], [0, 64, 129], done, trace=False)
+    rb, _ = eng.stats()
+    assert (rb > frames // 2).all()  # uniform inputs: rollbacks at most calls
+
+
 def test_p2p_forms_interleave_with_equal_queues(oracle):
     """Every plain form leaves the InputQueue state the others continue from: launches alternate
     between the queue-stepping flat kernel, the canonical flat kernel and the chains form, with
