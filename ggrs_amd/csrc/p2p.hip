@@ -39,6 +39,7 @@
 #include <vector>
 
 #include "common.h"
+#include "p2p_engine.h"
 
 #pragma clang fp contract(off)
 
@@ -1609,43 +1610,6 @@ __global__ void init_queue_kernel(int32_t* queue, int64_t n_per_field, int32_t P
 
 }  // namespace
 
-struct ggrs_p2p_engine {
-  ggrs_p2p_config_t cfg{};
-  int Pp = 1, F = 1, R = 2, cap = 256;
-  int num_cus = 256;                 // the device's CUs (LDS-ring occupancy rule)
-  hipStream_t stream = nullptr;
-  uint32_t* cur = nullptr;
-  uint32_t* ring = nullptr;
-  uint8_t* inputs = nullptr;
-  int32_t* queue = nullptr;
-  int32_t* rollbacks = nullptr;
-  int64_t* resim = nullptr;
-  uint16_t* trace = nullptr;
-  uint8_t* staging = nullptr;
-  size_t staging_bytes = 0;
-  int32_t current_frame = 0;
-  int32_t next_input_frame = 0;
-  int32_t desync_interval = 0;
-  uint16_t* hist = nullptr;     // [kHist][S] local checksum history
-  uint64_t* cmp_mask = nullptr; // [ceil(S/64)] compare result
-  int32_t* cmp_count = nullptr;
-  int64_t dbg_sess = -1;
-  int32_t dbg_frame = -1;
-  int32_t sparse = 0;
-  int32_t form = 0;  // ggrs_p2p_set_unstaged: 0 default (canonical flat, or chains for few sessions),
-                     // 1 global input reads, 2 lockstep staged, 3 flat with HBM rings, 4 chains,
-                     // 5 flat with LDS rings and the queue bookkeeping, 6 canonical flat
-  bool dbg_ever = false;  // a debug flip was armed: the states may no longer be the canonical ones
-  int32_t* last_saved = nullptr;  // [S], sparse saving only
-  int32_t* ring_frame = nullptr;  // [R][S], sparse saving only
-  // lockstep mode (max_prediction 0): the session-uniform control flow, replayed on the host
-  int32_t ls_frame = 0;                     // SyncLayer::current_frame
-  int32_t ls_local_last = kNull;            // local players' last queue frame (local_connect_status)
-  std::vector<int32_t> ls_row_of;           // queue frame q -> the call (input row) that added it, q % size
-  int32_t* ls_prog = nullptr;               // device copy of a launch's (local row, remote row) pairs
-  int32_t ls_prog_cap = 0;
-  SpanTimer timer;
-};
 
 namespace {
 

@@ -1406,6 +1406,123 @@ int oracle_p2p_stream(const OracleP2PCfg* cfg, int32_t frames, const uint8_t* in
   return rc;
 }
 
+/* ---------------------------------------------------------------- arrival schedules (f1)
+ * One peer's P2P session under an arbitrary remote-arrival schedule, with the prediction
+ * threshold and disconnects: what the device engine's scheduled mode (ggrs_p2p_add_arrivals)
+ * must reproduce.  Call c (c = 0 .. calls - 1):
+ *   1. poll_remote_clients (p2p_session.rs:430-478): every remote frame g in (delivered,
+ *      arrive_upto[c]] arrives as Event::Input for each remote player not yet disconnected
+ *      (handle_event :880-895 -> add_remote_input -> InputQueue::add_input), then, for each player k
+ *      with bit k of events[c] (ascending k; the reference polls its endpoints in HashMap order,
+ *      which is unspecified), Event::Disconnected (:866-878 -> disconnect_player_at_frame :618-655:
+ *      disconnected, and disconnect_frame = last_frame + 1 when the session is past it);
+ *   2. add_local_input of every local player with row c's byte (PlayerInput{current_frame, input},
+ *      :219-246; a call that does not advance keeps its frame, so the next call's input for the same
+ *      frame is the one InputQueue::add_input drops, input_queue.rs:170-186);
+ *   3. advance_frame (:265-426) with the prediction threshold: a call with frames_ahead >=
+ *      max_prediction saves (and rolls back) but emits no AdvanceFrame (:393-423);
+ *   4. Game::handle_requests over the list.
+ * Row g of inputs: local players' add_local_input of call g, remote players' input of frame g.
+ * arrive_upto[c] <= c (the remote peer has sent at most its frame c); a value at or below what
+ * already arrived delivers nothing.  update_player_disconnects (:748-783) changes nothing here: no
+ * running endpoint reports a third player's disconnect.  Per call: advanced[c] (1 if an AdvanceFrame
+ * of the current frame was emitted), rb_frame[c] (the first LoadGameState's frame, -1 for none).
+ * Returns 0; -1 bad arguments or schedule; -4 a condition on which the reference panics (an input
+ * queue over INPUT_QUEUE_LENGTH, no connected player, a rollback to a frame not in the past). */
+int oracle_p2p_sched_run(const OracleP2PCfg* cfg, int32_t calls, const uint8_t* inputs, const int32_t* arrive_upto,
+                         const uint8_t* events, uint8_t* advanced, int32_t* rb_frame, uint16_t* cksum_trace,
+                         uint8_t* final_state, int32_t* ring_frames, uint16_t* ring_cksums, uint8_t* ring_states,
+                         OracleP2PResult* res) {
+  memset(res, 0, sizeof *res);
+  const size_t P = (size_t)cfg->num_players;
+  if (P < 1 || P > MAX_PLAYERS || cfg->max_prediction < 1 || cfg->input_delay < 0 ||
+      (cfg->local_mask & ~((1 << P) - 1)) != 0 || cfg->local_mask == (1 << P) - 1) {
+    res->status = -1;
+    return -1;
+  }
+  P2PSession s; memset(&s, 0, sizeof s);
+  s.num_players = P; s.max_prediction = (size_t)cfg->max_prediction;
+  s.local_mask = (uint32_t)cfg->local_mask;
+  sl_new(&s.sl, P, s.max_prediction, cfg->predictor);
+  for (size_t i = 0; i < P; i++) {
+    s.last_frame[i] = NULL_FRAME;
+    if ((s.local_mask >> i) & 1u) s.sl.queues[i].frame_delay = (size_t)cfg->input_delay;
+  }
+  s.disconnect_frame = NULL_FRAME;
+  s.sparse_saving = cfg->sparse_saving;
+  Game game; memset(&game, 0, sizeof game);
+  game.desync_frame = -1;
+  state_new(&game.game_state, (uint64_t)P);
+  game.last_checksum_frame = NULL_FRAME;
+  RequestVec rv = {0};
+  int32_t delivered = NULL_FRAME;
+  int rc = 0;
+  for (int32_t c = 0; c < calls && rc == 0; c++) {
+    const int32_t upto = arrive_upto[c];
+    if (upto > c) { rc = -1; break; }
+    for (int32_t g = delivered + 1; g <= upto && rc == 0; g++)   /* the burst */
+      for (size_t i = 0; i < P; i++) {
+        if (((s.local_mask >> i) & 1u) || s.disconnected[i]) continue;
+        if (s.sl.queues[i].length + 1 > INPUT_QUEUE_LENGTH) { rc = -4; break; }
+        p2p_on_remote_input(&s, i, g, inputs[(size_t)g * P + i]);
+      }
+    if (rc) break;
+    if (upto > delivered) delivered = upto;
+    const uint8_t ev = events ? events[c] : 0;
+    for (size_t i = 0; i < P; i++)                        /* Event::Disconnected */
+      if (((ev >> i) & 1u) && !((s.local_mask >> i) & 1u) && !s.disconnected[i]) {
+        s.disconnected[i] = 1;
+        if (s.sl.current_frame > s.last_frame[i]) s.disconnect_frame = s.last_frame[i] + 1;
+      }
+    int any_connected = 0;
+    for (size_t i = 0; i < P; i++) any_connected |= !s.disconnected[i];
+    if (!any_connected) { rc = -4; break; }
+    {  /* a rollback to a frame that is not in the past panics in load_frame (sync_layer.rs:231-237):
+        * a disconnect whose last_frame is current_frame - 1 sets disconnect_frame = current_frame */
+      const int32_t fi = sl_check_simulation_consistency(&s.sl, s.disconnect_frame);
+      if (fi != NULL_FRAME && fi >= s.sl.current_frame) { rc = -4; break; }
+    }
+    for (size_t i = 0; i < P; i++)
+      if ((s.local_mask >> i) & 1u) {
+        s.local[i].frame = s.sl.current_frame; s.local[i].input = inputs[(size_t)c * P + i]; s.has_local[i] = 1;
+      }
+    int64_t rb0 = s.rollbacks;
+    int adv = 0;
+    if (p2p_advance_frame(&s, &rv, &adv) < 0) { rc = -1; break; }
+    if (advanced) advanced[c] = (uint8_t)adv;
+    if (rb_frame) {
+      rb_frame[c] = -1;
+      for (size_t k = 0; k < rv.n && s.rollbacks != rb0; k++)
+        if (rv.v[k].kind == REQ_LOAD) { rb_frame[c] = rv.v[k].frame; break; }
+    }
+    for (size_t k = 0; k < rv.n; k++) {
+      if (rv.v[k].kind == REQ_LOAD) res->n_load++;
+      else if (rv.v[k].kind == REQ_SAVE) res->n_save++;
+      else res->n_advance++;
+    }
+    game_handle_requests(&game, &s.sl, &rv, 0);
+    if (cksum_trace) cksum_trace[c] = game.last_checksum;
+    res->frames_done = c + 1;
+  }
+  res->rollbacks = s.rollbacks;
+  res->resim = s.resim;
+  res->status = rc;
+  if (final_state) oracle_state_serialize(&game.game_state, final_state);
+  for (size_t i = 0; i < s.sl.num_cells; i++) {
+    const Cell* cl = &s.sl.cells[i];
+    if (ring_frames) ring_frames[i] = cl->frame;
+    if (ring_cksums) ring_cksums[i] = cl->has_checksum ? cl->checksum : 0;
+    if (ring_states) {
+      uint8_t* dst = ring_states + i * (36 + 20 * P);
+      if (cl->has_data) oracle_state_serialize(&cl->data, dst); else memset(dst, 0, 36 + 20 * P);
+    }
+  }
+  free(rv.v);
+  state_free(&game.game_state);
+  sl_free(&s.sl);
+  return rc;
+}
+
 /* The ex_game request handler alone (Game::handle_requests, ex_game.rs:79-127, over its own
  * SavedStates ring of max_prediction + 1 cells, sync_layer.rs:144-166): executes n requests
  * (kind, frame, per-advance inputs[P] and status[P]) in order from State::new and records every

@@ -301,6 +301,65 @@ def p2p_stream(inputs, arrive_upto, num_players=2, local_mask=0b01, input_delay=
                 frame=frame[:n], inputs=inp[:n], status=st[:n])
 
 
+def stall_schedule(calls, max_prediction, seed, max_lag=None, stall_every=40, stall_len=None):
+    """arrive_upto[c] for oracle_p2p_sched_run: jittered lags in [1, max_lag] (default max_prediction
+    - 1) with, every ~stall_every calls, a network stall of stall_len calls (default max_prediction
+    + 4) in which nothing arrives -- so sessions hit the prediction threshold and skip calls, then
+    the burst arrives at once (a rollback as deep as the window).  Non-decreasing, <= c."""
+    rng = np.random.default_rng(seed)
+    max_lag = max_lag or max(1, max_prediction - 1)
+    stall_len = stall_len or max_prediction + 4
+    lag = rng.integers(1, max_lag + 1, calls)
+    upto = np.arange(calls) - lag
+    c = int(rng.integers(stall_every // 2, stall_every + 1))
+    while c < calls:
+        hold = upto[c - 1] if c > 0 else -1
+        upto[c:c + stall_len] = np.minimum(upto[c:c + stall_len], hold)
+        c += stall_len + int(rng.integers(stall_every // 2, stall_every + 1))
+    upto = np.maximum.accumulate(np.maximum(upto, -1))
+    return upto.astype(np.int32)
+
+
+def p2p_sched_run(inputs, arrive_upto, events=None, num_players=2, local_mask=0b01, input_delay=0,
+                  max_prediction=8, predictor=0, sparse_saving=False):
+    """One peer's P2P session under an arrival schedule, with the prediction threshold and
+    disconnects (oracle_p2p_sched_run): inputs[c] = local add_local_input of call c / remote input of
+    frame c; arrive_upto[c] = newest remote frame delivered by call c; events[c] bit k = player k's
+    Event::Disconnected at call c.  Returns rc, result, per-call advanced / rb_frame / ck_trace, the
+    final state and the ring; current_frame and skips derived from the counts."""
+    inputs = np.ascontiguousarray(inputs, np.uint8).reshape(-1, num_players)
+    calls = inputs.shape[0]
+    upto = np.ascontiguousarray(arrive_upto, np.int32)
+    assert upto.shape[0] >= calls
+    ev = None if events is None else np.ascontiguousarray(events, np.uint8)
+    R, sb = max_prediction + 1, state_bytes(num_players)
+    cfg = P2PCfg(num_players, max_prediction, input_delay, 1, local_mask, predictor, int(sparse_saving))
+    res = P2PResult()
+    out = dict(advanced=np.zeros(calls, np.uint8), rb_frame=np.zeros(calls, np.int32),
+               ck_trace=np.zeros(calls, np.uint16), final_state=np.zeros(sb, np.uint8),
+               ring_frames=np.zeros(R, np.int32), ring_cksums=np.zeros(R, np.uint16),
+               ring_states=np.zeros((R, sb), np.uint8))
+    L = lib()
+    if not getattr(L, "_sched_bound", False):
+        P = ctypes.POINTER
+        u8p, u16p, i32p = P(ctypes.c_uint8), P(ctypes.c_uint16), P(ctypes.c_int32)
+        L.oracle_p2p_sched_run.argtypes = [P(P2PCfg), ctypes.c_int32, u8p, i32p, u8p, u8p, i32p, u16p, u8p, i32p,
+                                           u16p, u8p, P(P2PResult)]
+        L.oracle_p2p_sched_run.restype = ctypes.c_int
+        L._sched_bound = True
+    rc = L.oracle_p2p_sched_run(
+        ctypes.byref(cfg), calls, _ptr(inputs, ctypes.c_uint8), _ptr(upto, ctypes.c_int32), _ptr(ev, ctypes.c_uint8),
+        _ptr(out["advanced"], ctypes.c_uint8), _ptr(out["rb_frame"], ctypes.c_int32),
+        _ptr(out["ck_trace"], ctypes.c_uint16), _ptr(out["final_state"], ctypes.c_uint8),
+        _ptr(out["ring_frames"], ctypes.c_int32), _ptr(out["ring_cksums"], ctypes.c_uint16),
+        _ptr(out["ring_states"], ctypes.c_uint8), ctypes.byref(res))
+    out["rc"] = rc
+    out["result"] = res
+    out["current_frame"] = int(res.n_advance - res.resim)
+    out["skips"] = int(res.frames_done - out["current_frame"])
+    return out
+
+
 def handler_run(kind, frame, inputs, status=None, num_players=2, max_prediction=8):
     """Game::handle_requests over one lane's request stream (oracle_handler_run): dict with rc
     (0, or -(1 + k) at the request that would panic), the checksum of every Save in order, the
