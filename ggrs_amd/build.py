@@ -16,9 +16,11 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "_obj")
 LIB = os.path.join(HERE, "libggrs_amd.so")
-UNITS = ("engine.hip", "requests.hip", "branch.hip", "particles.hip", "p2p.hip", "codec.hip", "lane_encode.cpp")
+UNITS = ("engine.hip", "requests.hip", "branch.hip", "particles.hip", "p2p.hip", "p2p_sched.hip", "codec.hip",
+         "lane_encode.cpp")
 SOURCES = [os.path.join(CSRC, f) for f in UNITS]
-HEADERS = [os.path.join(CSRC, h) for h in ("box_game.h", "glibc_sincosf.h", "common.h", "particles.h")] + [
+HEADERS = [os.path.join(CSRC, h) for h in ("box_game.h", "glibc_sincosf.h", "common.h", "particles.h", "p2p_engine.h",
+                                           "engine.h")] + [
     os.path.join(ROOT, "include", "ggrs_amd.h")]
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -44,7 +46,7 @@ FLAGS = ["-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC", "-std=c++
 # every unit (profiles/r04w): max-memory-clause, config 2 and the P2P chains 3 % slower, config 3
 # equal; iterative-ilp crashes this hipcc on particles.hip.
 ILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
-UNIT_FLAGS = {"engine.hip": ILP, "p2p.hip": ILP}
+UNIT_FLAGS = {"engine.hip": ILP, "p2p.hip": ILP, "p2p_sched.hip": ILP}
 
 
 def needs_build():

@@ -1626,6 +1626,9 @@ int p2p_launch_timed(ggrs_p2p_engine* e, K&& launch) {
 // players' replay, and the remote input f - D; with sparse saving a replay starts at the last
 // save, up to max_prediction frames back
 int32_t oldest_row(const ggrs_p2p_engine* e, int32_t f) {
+  // scheduled arrivals: the local rows of the calls still to run (a remote row is checked against
+  // its tag on the device when it arrives)
+  if (e->sched) return f;
   if (e->cfg.max_prediction == 0) {  // lockstep: the current frame's remote row, the next local rows
     int32_t oldest = std::min(f, e->ls_frame);
     const int32_t q = std::max(e->ls_frame, e->cfg.input_delay);
@@ -1680,6 +1683,7 @@ int ggrs_p2p_engine_destroy(ggrs_p2p_engine_t* e) {
   if (!e) return GGRS_OK;
   (void)hipSetDevice(e->cfg.device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
+  p2p_sched_free(e);
   void* bufs[] = {e->cur, e->ring, e->inputs, e->queue, e->rollbacks, e->resim, e->trace, e->staging,
                   e->hist, e->cmp_mask, e->cmp_count, e->last_saved, e->ring_frame, e->ls_prog};
   for (void* b : bufs)
@@ -1788,6 +1792,11 @@ int ggrs_p2p_add_inputs(ggrs_p2p_engine_t* e, int32_t first_frame, int32_t n, co
   pack_inputs_kernel<<<grid_of((int64_t)n * S, 256), 256, 0, e->stream>>>(e->staging, e->inputs, S, P, e->Pp, n,
                                                                           first_frame % e->cap, e->cap);
   HIP_TRY(hipGetLastError());
+  if (e->sched) {  // the frame each row slot now holds (a remote row is checked against it on arrival)
+    for (int32_t k = 0; k < n; k++) e->row_tag_host[(size_t)((first_frame + k) % e->cap)] = first_frame + k;
+    HIP_TRY(hipMemcpyAsync(e->row_tag, e->row_tag_host.data(), sizeof(int32_t) * e->cap, hipMemcpyHostToDevice,
+                           e->stream));
+  }
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->next_input_frame = first_frame + n;
   return GGRS_OK;
@@ -1801,6 +1810,7 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
     return set_error(GGRS_E_INVALID, "Missing local input: inputs are queued up to frame %d, calls need up to %d",
                      e->next_input_frame - 1, e->current_frame + n - 1);
   HIP_TRY(hipSetDevice(e->cfg.device));
+  if (e->sched) return p2p_sched_advance(e, n);  // per-session arrival schedules (p2p_sched.hip)
   P2PParams p;
   p.S = e->cfg.num_sessions;
   p.R = e->R;
@@ -2005,6 +2015,7 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
 int ggrs_p2p_set_desync_detection(ggrs_p2p_engine_t* e, int32_t interval) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
   if (interval < 0) return set_error(GGRS_E_INVALID, "interval must be >= 0 (0 = DesyncDetection::Off)");
+  if (interval > 0 && e->sched) return set_error(GGRS_E_STATE, "desync detection is not supported with arrival schedules");
   if (interval > 0 && e->sparse)
     return set_error(GGRS_E_STATE, "desync detection with sparse saving is not supported: the reference sends a "
                                    "report only for a frame it saved (p2p_session.rs:948-962, sync_layer.rs:323-326)");
@@ -2121,6 +2132,8 @@ int ggrs_p2p_current_frame(const ggrs_p2p_engine_t* e, int32_t* out) {
   if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
   // P2PSession::current_frame (:555-558): every call advances in rollback mode; in lockstep mode
   // calls wait for confirmed inputs
+  if (e->sched)
+    return set_error(GGRS_E_STATE, "with arrival schedules every session has its own frame (ggrs_p2p_read_sessions)");
   *out = e->cfg.max_prediction == 0 ? e->ls_frame : e->current_frame;
   return GGRS_OK;
 }
@@ -2169,7 +2182,7 @@ int ggrs_p2p_read_ring(ggrs_p2p_engine_t* e, int32_t session, int32_t* frames, u
     int32_t fr = kNull;
     if (e->cfg.max_prediction == 0) {
       // lockstep mode never saves
-    } else if (e->sparse) {
+    } else if (e->sparse || e->sched) {
       HIP_TRY(hipMemcpy(&fr, e->ring_frame + (int64_t)slot * S + session, 4, hipMemcpyDeviceToHost));
     } else {
       for (int32_t g = f - 1; g >= 0 && g >= f - R; g--)
@@ -2207,6 +2220,7 @@ int ggrs_p2p_read_stats(ggrs_p2p_engine_t* e, int32_t* rollbacks, int64_t* resim
 
 int ggrs_p2p_read_queues(ggrs_p2p_engine_t* e, int32_t* out) {
   if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
+  if (e->sched) return set_error(GGRS_E_STATE, "the queue words of scheduled mode are per session (ggrs_p2p_read_sessions)");
   HIP_TRY(hipSetDevice(e->cfg.device));
   const size_t bytes = sizeof(int32_t) * 4 * e->cfg.num_players * (size_t)e->cfg.num_sessions;
   HIP_TRY(hipMemcpyAsync(out, e->queue, bytes, hipMemcpyDeviceToHost, e->stream));

@@ -54,7 +54,7 @@ struct ggrs_p2p_engine {
   std::vector<int32_t> row_tag_host;
   uint32_t* iq = nullptr;         // [kSchedQueue][S] every player's queued input of frame q, q % kSchedQueue
   int32_t* sst = nullptr;         // [sched_fields(P)][S] SyncLayer / InputQueue / connect-status words
-  SpanTimer timer;
+  ggrs::SpanTimer timer;
 };
 
 namespace ggrs {

@@ -64,6 +64,9 @@ def _bind(L):
     L.ggrs_p2p_debug_desync.argtypes = [vp, i32, i32]
     L.ggrs_p2p_set_sparse_saving.argtypes = [vp, i32]
     L.ggrs_p2p_set_unstaged.argtypes = [vp, i32]
+    L.ggrs_p2p_set_arrival_schedule.argtypes = [vp, i32]
+    L.ggrs_p2p_add_arrivals.argtypes = [vp, i32, i32, vp, vp]
+    L.ggrs_p2p_read_sessions.argtypes = [vp, vp, vp, vp]
     for name in _lib.EXPORTS:
         if name.startswith("ggrs_p2p_"):
             getattr(L, name).restype = ctypes.c_int
@@ -215,6 +218,35 @@ class P2PEngine:
         """SessionBuilder::with_sparse_saving_mode for every session; before the first call."""
         _lib.check(self._L.ggrs_p2p_set_sparse_saving(self._h, int(bool(on))))
         self.sparse_saving = bool(on)
+
+    # ---- arrival schedules (include/ggrs_amd.h, ggrs_p2p_*arrival*; p2p_sched.hip)
+    def set_arrival_schedule(self, on=True):
+        """Per-session remote-arrival tables instead of the fixed remote_latency (before the first
+        call): each session rolls back to its own earliest misprediction, stops advancing at the
+        prediction threshold (p2p_session.rs:393-423), and handles disconnects (:618-655)."""
+        _lib.check(self._L.ggrs_p2p_set_arrival_schedule(self._h, int(bool(on))))
+        self.arrival_schedule = bool(on)
+
+    def add_arrivals(self, first_call, arrive_upto, events=None):
+        """arrive_upto [n][S] int32: the newest remote frame each session's poll delivered at calls
+        first_call .. first_call + n - 1; events [n][S] uint8 (bit k: Event::Disconnected for
+        remote player k at that call, after its arrivals) or None."""
+        a = np.ascontiguousarray(arrive_upto, np.int32)
+        if a.ndim != 2 or a.shape[1] != self.num_sessions:
+            raise InvalidRequest(-1, f"arrive_upto must be [n][{self.num_sessions}]")
+        ev = None
+        if events is not None:
+            ev = np.ascontiguousarray(events, np.uint8)
+            if ev.shape != a.shape:
+                raise InvalidRequest(-1, "events must have arrive_upto's shape")
+        _lib.check(self._L.ggrs_p2p_add_arrivals(self._h, first_call, a.shape[0], _vp(a), _vp(ev)))
+
+    def sessions(self):
+        """(frames, skipped, errors) [S] int32 each: every session's current frame, its calls that
+        did not advance (prediction threshold), and its error (0, or where the reference panics)."""
+        out = [np.zeros(self.num_sessions, np.int32) for _ in range(3)]
+        _lib.check(self._L.ggrs_p2p_read_sessions(self._h, *(_vp(a) for a in out)))
+        return tuple(out)
 
     KERNEL_FORMS = {"default": 0, "unstaged": 1, "lockstep": 2, "flat": 3, "chains": 4, "flat_queues": 5,
                     "canonical": 6}

@@ -49,8 +49,12 @@ extern "C" {
 #endif
 
 /* 2: GGRS_PATH_* renumbered (2, 3 = the pipelined forms), lane batches submitted and waited for
- * separately, host-side lane encoding, branch round forms */
-#define GGRS_ABI_VERSION 3
+ * separately, host-side lane encoding, branch round forms
+ * 3: ggrs_branch_set_stream(e, NULL) binds HIP's null stream (it used to select the engine's own
+ * stream); ggrs_branch_use_own_stream returns to the engine's own
+ * 4: P2P arrival schedules (ggrs_p2p_set_arrival_schedule, ggrs_p2p_add_arrivals,
+ * ggrs_p2p_read_sessions) */
+#define GGRS_ABI_VERSION 4
 
 #define GGRS_OK 0
 #define GGRS_E_INVALID (-1)      /* GgrsError::InvalidRequest: bad argument or configuration */
@@ -521,6 +525,38 @@ int ggrs_p2p_set_unstaged(ggrs_p2p_engine_t* eng, int32_t form);
 /* test hook: the AdvanceFrame from `frame` of `session` flips the lowest bit of player 0's x on
  * every (re)simulation -- a deterministic desync of this peer (session -1: off) */
 int ggrs_p2p_debug_desync(ggrs_p2p_engine_t* eng, int32_t session, int32_t frame);
+
+/* ---- Arrival schedules: the network of a real match, per session.
+ * Replaces the fixed remote_latency model by each session's own remote-arrival table, so every
+ * session rolls back to its own earliest misprediction (InputQueue::add_input_by_frame's
+ * first_incorrect_frame, src/input_queue.rs:190-230 -> check_simulation_consistency,
+ * src/sync_layer.rs:343-353) with its own depth, a call at the prediction threshold saves but does
+ * not advance (frames_ahead >= max_prediction, p2p_session.rs:393-423), and a disconnected remote
+ * player (handle_event Event::Disconnected :866-878 -> disconnect_player_at_frame :618-655) rolls
+ * the session back to its last frame + 1 and is replayed with InputStatus::Disconnected (ex_game
+ * input 4, src/sync_layer.rs:280-293).  Call c: (1) the remote frames (delivered, arrive_upto[c]]
+ * arrive, in order, for every remote player not disconnected; (2) Event::Disconnected for each
+ * remote player k with bit k of events[c] (ascending k); (3) add_local_input of every local player
+ * with input row c's byte, for the session's current frame (a call that did not advance repeats its
+ * frame, and InputQueue::add_input drops the repeat, input_queue.rs:170-186); (4) advance_frame.
+ * Input row g (ggrs_p2p_add_inputs) = the local players' input of call g and the remote players'
+ * input of frame g, as in the fixed-latency model.  Rollback mode only (max_prediction >= 1),
+ * sparse saving allowed, no desync detection or trace; remote_latency is ignored.  A session whose
+ * call would make the reference panic (a remote input no longer in the input rows or more than
+ * 126 - max_prediction frames ahead of the session, a rollback to a frame that is not in the past,
+ * no connected player) or whose arrival row names a frame after its call (GGRS_E_INVALID) stops
+ * there with that error (ggrs_p2p_read_sessions); the other sessions run on.  Kernel:
+ * p2p_sched.hip. */
+/* on = 1 switches the engine to arrival schedules; part of the configuration: before the first call */
+int ggrs_p2p_set_arrival_schedule(ggrs_p2p_engine_t* eng, int32_t on);
+/* arrive_upto [n_calls][num_sessions] i32: the newest remote frame delivered by each call (<= the
+ * call's index; at or below what already arrived delivers nothing); events [n_calls][num_sessions]
+ * u8 (NULL: none).  Calls in order from 0, at most input_capacity calls ahead of the next call. */
+int ggrs_p2p_add_arrivals(ggrs_p2p_engine_t* eng, int32_t first_call, int32_t n_calls, const int32_t* arrive_upto,
+                          const uint8_t* events);
+/* per session: SyncLayer::current_frame, the calls that did not advance (prediction threshold),
+ * and the session's error (0, GGRS_E_PRECONDITION or GGRS_E_INVALID); any pointer may be NULL */
+int ggrs_p2p_read_sessions(ggrs_p2p_engine_t* eng, int32_t* frames, int32_t* skipped, int32_t* errors);
 
 /* ---- Input wire codec, batched (src/network/compression.rs:14-182; bitfield-rle 0.2.1 runs,
  * bincode 1.3 fixint framing of EncodedInputSequence).  Replaces compression::encode / decode as

@@ -18,6 +18,7 @@ fn main() {
         .arg(csrc.join("branch.hip"))
         .arg(csrc.join("particles.hip"))
         .arg(csrc.join("p2p.hip"))
+        .arg(csrc.join("p2p_sched.hip"))
         .arg(csrc.join("codec.hip"))
         .arg(csrc.join("lane_encode.cpp"))
         .status()

@@ -4,7 +4,7 @@
 #![allow(non_camel_case_types)]
 use std::os::raw::{c_char, c_void};
 
-pub const GGRS_ABI_VERSION: i32 = 3;
+pub const GGRS_ABI_VERSION: i32 = 4;
 
 pub const GGRS_OK: i32 = 0;
 pub const GGRS_E_INVALID: i32 = -1;
@@ -271,6 +271,20 @@ extern "C" {
     pub fn ggrs_p2p_set_sparse_saving(eng: *mut ggrs_p2p_engine_t, on: i32) -> i32;
     pub fn ggrs_p2p_set_unstaged(eng: *mut ggrs_p2p_engine_t, form: i32) -> i32;
     pub fn ggrs_p2p_debug_desync(eng: *mut ggrs_p2p_engine_t, session: i32, frame: i32) -> i32;
+    pub fn ggrs_p2p_set_arrival_schedule(eng: *mut ggrs_p2p_engine_t, on: i32) -> i32;
+    pub fn ggrs_p2p_add_arrivals(
+        eng: *mut ggrs_p2p_engine_t,
+        first_call: i32,
+        n_calls: i32,
+        arrive_upto: *const i32,
+        events: *const u8,
+    ) -> i32;
+    pub fn ggrs_p2p_read_sessions(
+        eng: *mut ggrs_p2p_engine_t,
+        frames: *mut i32,
+        skipped: *mut i32,
+        errors: *mut i32,
+    ) -> i32;
 
     // ---- input wire codec, batched (src/network/compression.rs:14-182); device pointers
     pub fn ggrs_codec_encode(ref_: *const u8, pending: *const u8, count: *const i32, n_packets: i64,

@@ -24,6 +24,18 @@ fn check(rc: i32) -> Result<(), EngineError> {
     if rc == GGRS_OK { Ok(()) } else { Err(EngineError(rc, last_error())) }
 }
 
+/// The library this crate links must implement the ABI its declarations describe (ffi.rs); checked
+/// before any engine is created, so a stale libggrs_amd.so fails loudly instead of misreading a
+/// changed signature (ABI 3 changed what ggrs_branch_set_stream(NULL) means).
+fn check_abi() -> Result<(), EngineError> {
+    let v = unsafe { ggrs_abi_version() };
+    if v == GGRS_ABI_VERSION {
+        Ok(())
+    } else {
+        Err(EngineError(GGRS_E_STATE, format!("libggrs_amd ABI {} but this crate declares ABI {}", v, GGRS_ABI_VERSION)))
+    }
+}
+
 /// Turns a game input into the byte the box game reads (`Input.inp`, ex_game.rs:28-32).
 pub trait InputByte {
     fn input_byte(&self) -> u8;
@@ -90,6 +102,7 @@ impl BatchedBoxGame {
     /// One engine lane per session: SessionBuilder's max_prediction / check_distance / input delay.
     pub fn new(lanes: usize, players: usize, max_prediction: usize, check_distance: usize,
                input_delay: usize, device: i32) -> Result<Self, EngineError> {
+        check_abi()?;
         let cfg = ggrs_config_t {
             num_lanes: lanes as i32,
             num_players: players as i32,

@@ -1,0 +1,160 @@
+"""GPU parity of the P2P engine under arrival schedules (ggrs_p2p_set_arrival_schedule / add_arrivals,
+p2p_sched.hip) against the oracle's P2PSession stepped call by call under the same schedule
+(oracle_p2p_sched_run): jittered remote arrivals, network stalls longer than max_prediction (calls
+at the prediction threshold skip their AdvanceFrame, p2p_session.rs:393-423, then a burst as deep
+as the window arrives), and disconnects (a rollback to the player's last frame + 1 and
+InputStatus::Disconnected replays, :618-655, sync_layer.rs:280-293).  Every checked session's final
+state, saved-state ring with its frame tags, rollback / resimulation counts, skipped calls, current
+frame and error are bit-exact -- including the sessions where the reference would panic."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")  # loads torch's HIP runtime before the engine library
+
+pytestmark = pytest.mark.gpu
+
+
+def schedules(S, calls, mp, seed, local_mask, P, disconnect_every=5):
+    """[calls][S] arrivals and events: per session its own network -- stalls with bursts (2 of 3
+    sessions), plain jitter, or a fixed latency -- and a disconnect of one remote player in every
+    `disconnect_every`-th session."""
+    from oracle import oracle as o
+    arrive = np.zeros((calls, S), np.int32)
+    events = np.zeros((calls, S), np.uint8)
+    remote = [k for k in range(P) if not (local_mask >> k) & 1]
+    rng = np.random.default_rng(seed)
+    for s in range(S):
+        kind = s % 3
+        if kind == 2:
+            arrive[:, s] = np.maximum(np.arange(calls) - int(rng.integers(1, mp)), -1)
+        else:
+            arrive[:, s] = o.stall_schedule(calls, mp, seed * 1000 + s, stall_every=40 if kind == 0 else 10 ** 9)
+        if disconnect_every and s % disconnect_every == 0:
+            events[int(rng.integers(calls // 4, 3 * calls // 4)), s] = 1 << remote[s % len(remote)]
+    return arrive, events
+
+
+def check_sessions(eng, rows, arrive, events, sessions, calls, **kw):
+    from oracle import oracle as o
+    from ggrs_amd._lib import GGRS_E_PRECONDITION
+    frames, skipped, errors = eng.sessions()
+    rb, rs = eng.stats()
+    for s in sessions:
+        out = o.p2p_sched_run(rows[:calls, s], arrive[:calls, s], events[:calls, s], num_players=eng.num_players,
+                              local_mask=eng.local_mask, input_delay=eng.input_delay,
+                              max_prediction=eng.max_prediction, predictor=eng.predictor, **kw)
+        res = out["result"]
+        if out["rc"] == -4:  # the reference panics at this call: the device stops the session there
+            assert errors[s] == GGRS_E_PRECONDITION, (s, errors[s])
+        else:
+            assert out["rc"] == 0 and errors[s] == 0, (s, out["rc"], errors[s])
+            assert frames[s] == out["current_frame"] and skipped[s] == out["skips"], (s, frames[s], out["current_frame"])
+        assert bytes(eng.state(s)) == bytes(out["final_state"]), s
+        fr, cks, states = eng.ring(s)
+        assert (fr == out["ring_frames"]).all(), (s, fr, out["ring_frames"])
+        assert (cks == out["ring_cksums"]).all(), s
+        assert (states == out["ring_states"]).all(), s
+        assert rb[s] == res.rollbacks and rs[s] == res.resim, (s, rb[s], res.rollbacks, rs[s], res.resim)
+
+
+CASES = [
+    # P, local players, delay, max_prediction, predictor, input model, sparse saving
+    (2, (0,), 0, 8, 0, 0, False),
+    (2, (1,), 2, 6, 0, 1, False),
+    (4, (0, 2), 1, 7, 1, 0, False),
+    (3, (0,), 0, 12, 0, 0, False),
+    (2, (0,), 0, 8, 0, 0, True),
+    (4, (1,), 1, 9, 0, 0, True),
+    (2, (), 1, 8, 0, 0, False),
+]
+
+
+@pytest.mark.parametrize("P,local,delay,mp,pred,model,sparse", CASES)
+def test_p2p_arrival_schedules_match_oracle(oracle, P, local, delay, mp, pred, model, sparse):
+    from ggrs_amd import P2PEngine
+    S, calls = 200, 240
+    mask = sum(1 << k for k in local)
+    rows = np.stack([oracle.gen_inputs(oracle.session_seed(s, 0x5C4E), calls, P, model) for s in range(S)], axis=1)
+    arrive, events = schedules(S, calls, mp, 11 + P, mask, P)
+    eng = P2PEngine(S, num_players=P, local_players=local, input_delay=delay, max_prediction=mp, remote_latency=1,
+                    predictor=pred, input_capacity=calls)
+    if sparse:
+        eng.set_sparse_saving(True)
+    eng.set_arrival_schedule(True)
+    eng.add_inputs(0, rows)
+    eng.add_arrivals(0, arrive, events)
+    done = 0
+    for n in (1, 3, 60, 17, 159):
+        eng.advance_frames(n)
+        done += n
+        if done in (4, 81):
+            check_sessions(eng, rows, arrive, events, [0, 1, 5, 63, 64, 199], done, sparse_saving=sparse)
+    assert done == calls
+    check_sessions(eng, rows, arrive, events, range(0, S, 3), calls, sparse_saving=sparse)
+    frames, skipped, errors = eng.sessions()
+    assert skipped.sum() > 0  # stalls past max_prediction: calls at the prediction threshold
+    rb, _ = eng.stats()
+    assert rb.sum() > S
+
+
+def test_p2p_arrival_schedule_streamed_and_uniform(oracle):
+    """Inputs and arrivals streamed through small rings in chunks; a uniform schedule (every
+    session's remote input of frame g at call g + 4) equals the fixed-latency engine's states."""
+    from ggrs_amd import P2PEngine
+    S, calls, chunk, P = 130, 200, 20, 2
+    rows = np.stack([oracle.gen_inputs(oracle.session_seed(s, 0x77), calls, P, 0) for s in range(S)], axis=1)
+    arrive = np.repeat(np.maximum(np.arange(calls) - 4, -1)[:, None], S, axis=1).astype(np.int32)
+    eng = P2PEngine(S, num_players=P, local_players=(0,), max_prediction=8, remote_latency=1, input_capacity=48)
+    eng.set_arrival_schedule(True)
+    ref = P2PEngine(S, num_players=P, local_players=(0,), max_prediction=8, remote_latency=4, input_capacity=48)
+    for c0 in range(0, calls, chunk):
+        eng.add_inputs(c0, rows[c0:c0 + chunk])
+        eng.add_arrivals(c0, arrive[c0:c0 + chunk])
+        eng.advance_frames(chunk)
+        ref.add_inputs(c0, rows[c0:c0 + chunk])
+        ref.advance_frames(chunk)
+    frames, skipped, errors = eng.sessions()
+    assert (frames == calls).all() and (skipped == 0).all() and (errors == 0).all()
+    rb, rs = eng.stats()
+    rb2, rs2 = ref.stats()
+    assert (rb == rb2).all() and (rs == rs2).all()
+    for s in (0, 64, 129):
+        assert bytes(eng.state(s)) == bytes(ref.state(s))
+        a, b = eng.ring(s), ref.ring(s)
+        assert all((x == y).all() for x, y in zip(a, b))
+
+
+def test_p2p_arrival_schedule_rejects(oracle):
+    """Arrivals naming a frame after their call, and remote rows overwritten before they arrive,
+    stop only the offending sessions (GGRS_E_INVALID / GGRS_E_PRECONDITION); API misuse raises."""
+    from ggrs_amd import InvalidRequest, P2PEngine
+    from ggrs_amd._lib import GGRS_E_INVALID, GGRS_E_PRECONDITION, GgrsError
+    S, P = 70, 2
+    eng = P2PEngine(S, num_players=P, local_players=(0,), max_prediction=8, remote_latency=1, input_capacity=16)
+    with pytest.raises(GgrsError):
+        eng.add_arrivals(0, np.zeros((1, S), np.int32))  # not in scheduled mode
+    eng.set_arrival_schedule(True)
+    rows = np.zeros((16, S, P), np.uint8)
+    eng.add_inputs(0, rows)
+    arrive = np.repeat(np.arange(16)[:, None] - 2, S, axis=1).astype(np.int32)
+    arrive[3, 5] = 4  # frame 4 at call 3: later than the call
+    eng.add_arrivals(0, arrive)
+    with pytest.raises(InvalidRequest):
+        eng.advance_frames(17)  # missing local input / arrivals
+    eng.advance_frames(16)
+    frames, skipped, errors = eng.sessions()
+    assert errors[5] == GGRS_E_INVALID and frames[5] == 3
+    assert (np.delete(errors, 5) == 0).all() and (np.delete(frames, 5) == 16).all()
+    # session 9 receives nothing for 24 calls: its rows are overwritten before they arrive
+    eng.add_inputs(16, np.zeros((16, S, P), np.uint8))
+    late = np.repeat(np.arange(16, 32)[:, None] - 2, S, axis=1).astype(np.int32)
+    late[:, 9] = 13
+    eng.add_arrivals(16, late)
+    eng.advance_frames(16)
+    eng.add_inputs(32, np.zeros((16, S, P), np.uint8))
+    late2 = np.repeat(np.arange(32, 48)[:, None] - 2, S, axis=1).astype(np.int32)
+    eng.add_arrivals(32, late2)
+    eng.advance_frames(16)
+    frames, skipped, errors = eng.sessions()
+    assert errors[9] == GGRS_E_PRECONDITION
+    assert errors[10] == 0 and frames[10] == 48
