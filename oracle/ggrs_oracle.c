@@ -1478,9 +1478,11 @@ int oracle_p2p_sched_run(const OracleP2PCfg* cfg, int32_t calls, const uint8_t* 
     for (size_t i = 0; i < P; i++) any_connected |= !s.disconnected[i];
     if (!any_connected) { rc = -4; break; }
     {  /* a rollback to a frame that is not in the past panics in load_frame (sync_layer.rs:231-237):
-        * a disconnect whose last_frame is current_frame - 1 sets disconnect_frame = current_frame */
+        * a disconnect whose last_frame is current_frame - 1 sets disconnect_frame = current_frame
+        * (sparse saving loads the last save instead, p2p_session.rs:666-673) */
       const int32_t fi = sl_check_simulation_consistency(&s.sl, s.disconnect_frame);
-      if (fi != NULL_FRAME && fi >= s.sl.current_frame) { rc = -4; break; }
+      const int32_t load = s.sparse_saving ? s.sl.last_saved_frame : fi;
+      if (fi != NULL_FRAME && load >= s.sl.current_frame) { rc = -4; break; }
     }
     for (size_t i = 0; i < P; i++)
       if ((s.local_mask >> i) & 1u) {
