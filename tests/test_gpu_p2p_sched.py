@@ -130,31 +130,31 @@ def test_p2p_arrival_schedule_rejects(oracle):
     from ggrs_amd import InvalidRequest, P2PEngine
     from ggrs_amd._lib import GGRS_E_INVALID, GGRS_E_PRECONDITION, GgrsError
     S, P = 70, 2
-    eng = P2PEngine(S, num_players=P, local_players=(0,), max_prediction=8, remote_latency=1, input_capacity=16)
+    eng = P2PEngine(S, num_players=P, local_players=(0,), max_prediction=8, remote_latency=1, input_capacity=32)
     with pytest.raises(GgrsError):
         eng.add_arrivals(0, np.zeros((1, S), np.int32))  # not in scheduled mode
     eng.set_arrival_schedule(True)
-    rows = np.zeros((16, S, P), np.uint8)
-    eng.add_inputs(0, rows)
+    eng.add_inputs(0, np.zeros((32, S, P), np.uint8))
     arrive = np.repeat(np.arange(16)[:, None] - 2, S, axis=1).astype(np.int32)
     arrive[3, 5] = 4  # frame 4 at call 3: later than the call
     eng.add_arrivals(0, arrive)
     with pytest.raises(InvalidRequest):
-        eng.advance_frames(17)  # missing local input / arrivals
+        eng.advance_frames(17)  # missing arrivals
     eng.advance_frames(16)
     frames, skipped, errors = eng.sessions()
     assert errors[5] == GGRS_E_INVALID and frames[5] == 3
     assert (np.delete(errors, 5) == 0).all() and (np.delete(frames, 5) == 16).all()
-    # session 9 receives nothing for 24 calls: its rows are overwritten before they arrive
-    eng.add_inputs(16, np.zeros((16, S, P), np.uint8))
+    # session 9 receives nothing for 16 calls: the rows of its frames 14, 15 are overwritten by
+    # frames 46, 47 before they arrive (the prediction threshold stalls it meanwhile)
     late = np.repeat(np.arange(16, 32)[:, None] - 2, S, axis=1).astype(np.int32)
     late[:, 9] = 13
     eng.add_arrivals(16, late)
     eng.advance_frames(16)
+    frames, skipped, errors = eng.sessions()
+    assert skipped[9] > 0 and errors[9] == 0
     eng.add_inputs(32, np.zeros((16, S, P), np.uint8))
-    late2 = np.repeat(np.arange(32, 48)[:, None] - 2, S, axis=1).astype(np.int32)
-    eng.add_arrivals(32, late2)
+    eng.add_arrivals(32, np.repeat(np.arange(32, 48)[:, None] - 2, S, axis=1).astype(np.int32))
     eng.advance_frames(16)
     frames, skipped, errors = eng.sessions()
     assert errors[9] == GGRS_E_PRECONDITION
-    assert errors[10] == 0 and frames[10] == 48
+    assert errors[10] == 0 and frames[10] == 48 and skipped[10] == 0
