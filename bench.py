@@ -558,7 +558,10 @@ def run_p2p(args):
     from ggrs_amd import P2PEngine, synth
     S = args.sessions or 65536
     P, D, maxp, calls = 2, args.latency, args.max_prediction, 64
-    if not (1 <= D <= maxp - 1 or (maxp == 0 and D >= 1)):
+    sched = args.arrivals != "fixed"
+    if sched and (maxp < 2 or args.peers or args.p2p_form != "default"):
+        raise SystemExit("--arrivals jitter/stall: rollback mode (--max-prediction >= 2), no --peers, default form")
+    if not sched and not (1 <= D <= maxp - 1 or (maxp == 0 and D >= 1)):
         raise SystemExit(f"--latency {D} must be in 1..--max-prediction - 1 = {maxp - 1} (1.. in lockstep mode): "
                          "the engine's contract (include/ggrs_amd.h, ggrs_p2p_config_t.remote_latency), else the "
                          "prediction threshold stalls the session (p2p_session.rs:393-423)")
@@ -571,10 +574,15 @@ def run_p2p(args):
     local = (1,) if peers and rank >= world // 2 else (0,)
     rows = synth.gen_inputs(pair * S, S, frames, P, synth.MODEL_HELD)
     eng = P2PEngine(S, num_players=P, local_players=local, input_delay=0, max_prediction=maxp,
-                    remote_latency=D, input_capacity=frames + D + 2, device=local_rank)
+                    remote_latency=1 if sched else D, input_capacity=frames + D + 2, device=local_rank)
     eng.set_kernel_form(args.p2p_form)
     if args.sparse:
         eng.set_sparse_saving(True)  # builder.rs:160-169
+    arrive = None
+    if sched:  # every session its own network (p2p_sched.hip): jittered lags, optionally stalls
+        arrive = synth.jitter_arrivals(pair * S, S, frames, maxp, stalls=args.arrivals == "stall")
+        eng.set_arrival_schedule(True)
+        eng.add_arrivals(0, arrive)
     det, events = None, []
     if peers:
         from ggrs_amd import exchange
@@ -618,6 +626,10 @@ def run_p2p(args):
     rollbacks = int((rb1 - rb0).sum())
     value = total / elapsed
     F = 5 * P + 1
+    skipped = errors = None
+    if sched:
+        fr1, sk1, er1 = eng.sessions()
+        skipped, errors = int(sk1.sum()), int((er1 != 0).sum())
     # HBM bytes per launch: the state in/out, every save (state + checksum), every rollback load,
     # the queue words in/out and the input rows each call reads (arrival + its own, + replays)
     # (sparse saving: about one save per call, at min_confirmed, and replays save nothing)
@@ -626,6 +638,10 @@ def run_p2p(args):
     bytes_launch = (2 * 4 * F * S + (session_calls // args.steps) * (4 * F + 2) * 1
                     + (rollbacks // args.steps) * 4 * F + replay_saves
                     + 2 * 16 * P * S + (session_calls // args.steps) * 2 * 2 + (resim // args.steps) * 2 * 2)
+    if sched:  # + per call its arrival word, the queue word of the frame that arrives and of the
+        # local input (read-modify-write), each save's frame tag; the session words in and out
+        per_call = session_calls // args.steps
+        bytes_launch += per_call * (4 + 2 * 8) + (per_call + (resim - rollbacks) // args.steps) * 4 + 2 * 4 * (9 + 5 * P) * S
     avg_s = kernel_ms / 1e3 / max(launches, 1)
     achieved = bytes_launch / avg_s / 1e9
     parity = cpu_baseline = None
@@ -635,14 +651,20 @@ def run_p2p(args):
             O.build()
             ok = True
             for s in (0, 1, S // 2, S - 1):
-                r = O.p2p_run(rows[:, s], num_players=P, local_mask=0b01, max_prediction=maxp, latency=D,
-                              sparse_saving=bool(args.sparse))
+                if sched:
+                    r = O.p2p_sched_run(rows[:, s], arrive[:, s], num_players=P, local_mask=0b01, max_prediction=maxp,
+                                        sparse_saving=bool(args.sparse))
+                    ok &= r["rc"] == 0 and int(fr1[s]) == r["current_frame"] and int(sk1[s]) == r["skips"]
+                else:
+                    r = O.p2p_run(rows[:, s], num_players=P, local_mask=0b01, max_prediction=maxp, latency=D,
+                                  sparse_saving=bool(args.sparse))
                 ok &= bytes(eng.state(s)) == bytes(r["final_state"]) and int(rb1[s]) == r["result"].rollbacks
             parity = {"sessions_0_1_mid_last_bit_exact": bool(ok)}
             if peers:
                 parity["peers_desync_events"] = n_desync
             if world == 1 and not args.no_cpu_baseline:
-                cpu_baseline = p2p_cpu_baseline(args, O, synth, P, D, maxp)
+                cpu_baseline = (p2p_sched_cpu_baseline(args, O, synth, P, maxp) if sched
+                                else p2p_cpu_baseline(args, O, synth, P, D, maxp))
         except Exception as exc:
             parity = {"error": repr(exc)}
         line = {
@@ -650,8 +672,12 @@ def run_p2p(args):
             "unit": "session-frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": f"p2p: {S} sessions per GPU, 2 players (1 remote, inputs {D} frames "
-                                   f"late), max_prediction {maxp}, held-key inputs, {calls} calls per step",
+            "config": {"workload": f"p2p: {S} sessions per GPU, 2 players (1 remote, " + (
+                                       f"inputs {D} frames late" if not sched else
+                                       "per-session jittered arrivals, lag 1..max_prediction-1"
+                                       + (", network stalls of max_prediction + 4 calls every 48" if args.arrivals == "stall" else ""))
+                                   + f"), max_prediction {maxp}, held-key inputs, {calls} calls per step",
+                       "arrivals": args.arrivals,
                        "sessions_per_gpu": S, "peers": peers, "sparse_saving": bool(args.sparse),
                        "parallelism": f"sessions sharded over {world} GPU(s)"
                                       + (f", peer ranks exchange checksum reports over {dist.get_backend()}" if peers else "")},
@@ -661,9 +687,11 @@ def run_p2p(args):
             "resimulated_session_frames_per_s": round(resim * world / elapsed, 1),
             "resimulated_per_session_frame": round(resim / session_calls, 5),
             "advances_per_sec": round((session_calls + resim) * world / elapsed, 1),
+            "skipped_calls": skipped, "sessions_in_error": errors,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                         "traffic": pmc_traffic(f"p2p_s{S}" + ("" if (D, maxp) == (4, 8) else f"_d{D}_m{maxp}")
+                         "traffic": pmc_traffic(f"p2p_s{S}" + (f"_{args.arrivals}_m{maxp}" if sched else
+                                                               ("" if (D, maxp) == (4, 8) else f"_d{D}_m{maxp}"))
                                                + ("_sparse" if args.sparse else "")),
                          "algorithmic_bytes_per_launch": bytes_launch,
                          "avg_launch_ms": round(avg_s * 1e3, 4)},
@@ -886,6 +914,27 @@ def p2p_cpu_baseline(args, O, synth, P, D, maxp):
             "sample": f"{T} threads x {frames} P2P advance_frame calls (1 session/thread, same game, "
                       f"latency {D}, held-key inputs{', sparse saving' if args.sparse else ''}), C restatement "
                       f"oracle/ggrs_oracle.c oracle_p2p_run",
+            "wall_s": round(wall, 3), "all_ok": all(r == 0 for r in res)}
+
+
+def p2p_sched_cpu_baseline(args, O, synth, P, maxp):
+    """The oracle's P2P session under the same arrival-schedule model (oracle_p2p_sched_run: the
+    InputQueue / SyncLayer / P2PSession restatement stepped call by call) on T host threads, one
+    session per thread."""
+    from concurrent.futures import ThreadPoolExecutor
+    T = cpu_threads(args)
+    calls = 1_000_000
+    per = [(O.gen_inputs(synth.SEED_BASE + t, calls, P, O.MODEL_HELD),
+            synth.jitter_arrivals(t, 1, calls, maxp, stalls=args.arrivals == "stall")[:, 0].copy()) for t in range(T)]
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(T) as ex:
+        res = list(ex.map(lambda a: O.p2p_sched_run(a[0], a[1], num_players=P, local_mask=0b01, max_prediction=maxp,
+                                                    sparse_saving=bool(args.sparse))["rc"], per))
+    wall = time.perf_counter() - t0
+    return {"value": round(T * calls / wall, 1), "unit": "session-frames/s", "cores": T, "kind": "port",
+            "sample": f"{T} threads x {calls} P2P advance_frame calls (1 session/thread, {args.arrivals} arrivals, "
+                      f"max_prediction {maxp}, held-key inputs{', sparse saving' if args.sparse else ''}), "
+                      "C restatement oracle/ggrs_oracle.c oracle_p2p_sched_run",
             "wall_s": round(wall, 3), "all_ok": all(r == 0 for r in res)}
 
 
@@ -1246,6 +1295,9 @@ def main():
                     default="default",
                     help="p2p: kernel form (DESIGN.md section 3)")
     ap.add_argument("--sparse", action="store_true", help="p2p: sparse saving (SURVEY.md 8f row 4)")
+    ap.add_argument("--arrivals", choices=["fixed", "jitter", "stall"], default="fixed",
+                    help="p2p: the network -- every remote input --latency frames late (fixed), or per-session "
+                         "arrival schedules (ggrs_p2p_add_arrivals): jittered lags, plus network stalls")
     ap.add_argument("--latency", type=int, default=4, help="p2p: frames the remote player's inputs arrive late")
     ap.add_argument("--max-prediction", type=int, default=8, help="p2p: max_prediction (builder.rs:130-147)")
     ap.add_argument("--req-form", choices=["native", "p2p", "batch", "lanes", "lockstep"], default="native",

@@ -34,3 +34,22 @@ def gen_inputs(first_session, sessions, frames, players, model=MODEL_UNIFORM, ba
                 prev[:, p] = v
                 out[f, :, p] = v
     return out
+
+
+def jitter_arrivals(first_session, sessions, calls, max_prediction, stalls=False, seed=0x5C4E,
+                    stall_every=48, stall_len=None):
+    """[calls][sessions] int32 remote-arrival schedules (ggrs_p2p_add_arrivals): per session and call
+    a lag drawn uniformly from [1, max_prediction - 1], made non-decreasing, so the remote inputs
+    come in bursts of differing size and sessions roll back to differing depths; with `stalls`,
+    every session also loses its network for stall_len calls (default max_prediction + 4) once per
+    stall_every calls at its own phase, so it reaches the prediction threshold and skips calls
+    (p2p_session.rs:393-423) before the burst arrives.  Deterministic in (seed, first_session)."""
+    rng = np.random.default_rng([seed, first_session])
+    c = np.arange(calls, dtype=np.int32)[:, None]
+    upto = c - rng.integers(1, max(2, max_prediction), size=(calls, sessions), dtype=np.int32)
+    if stalls:
+        stall_len = stall_len or max_prediction + 4
+        phase = rng.integers(0, stall_every, size=sessions, dtype=np.int32)[None, :]
+        upto[(c + phase) % stall_every < stall_len] = -1
+    np.maximum(upto, -1, out=upto)
+    return np.maximum.accumulate(upto, axis=0)
