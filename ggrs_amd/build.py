@@ -58,6 +58,11 @@ def needs_build():
 
 def _compile(src, extra, verbose, obj_dir=OBJ, csrc=CSRC):
     obj = os.path.join(obj_dir, os.path.basename(src) + ".o")
+    # an unchanged unit keeps its object (same source, headers, flags and this script)
+    if not extra and csrc == CSRC and os.path.exists(obj):
+        t = os.path.getmtime(obj)
+        if all(os.path.getmtime(f) <= t for f in [src] + HEADERS + [os.path.abspath(__file__)]):
+            return obj
     cmd = [HIPCC, *FLAGS, *UNIT_FLAGS.get(os.path.basename(src), []), *extra, "-I", os.path.join(ROOT, "include"), "-I", csrc, "-c", "-o", obj, src]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

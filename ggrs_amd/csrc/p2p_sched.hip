@@ -16,9 +16,11 @@
 // Per-session device state (between launches, HBM):
 //   cur   [F][S] u32        the game state after the last call (the handler's State)
 //   ring  [S][R][C] u32     saved cells (p2p.hip's session-major layout), ring_frame [R][S] their frames
-//   iq    [Q][S] u32        the InputQueues' inputs: byte k = player k's input of frame q (slot q % Q,
-//                           Q = INPUT_QUEUE_LENGTH = 128, input_queue.rs:6); local bytes written by
-//                           add_local_input, remote bytes by the poll
+//   lq    [WL][S] u32       the local players' InputQueues: their input of frame q in slot q % WL
+//                           (WL >= max_prediction + input_delay + 2); the remote players' inputs are
+//                           read from the input rows themselves (row g = frame g), whose slots carry
+//                           the frame they hold (row_tag), so a remote input no longer queued is an
+//                           error rather than a stale byte
 //   sst   [fields][S] i32   SyncLayer current/last_confirmed/last_saved frames, disconnect_frame,
 //                           the newest delivered remote frame, local players' last queued frame,
 //                           skipped calls, the session's error, the disconnected mask, and per
@@ -51,6 +53,7 @@ __host__ __device__ constexpr int cell_dwords_s(int p) { return (state_fields(p)
 struct SchedParams {
   int64_t S;
   int32_t R, delay, cap, maxp, c0, n, predictor, sparse;
+  int32_t K, B, WL;  // calls per stage, rows kept behind a stage's first call, local-queue frames (2^k)
   uint32_t local_mask;
   uint32_t* cur;
   uint32_t* ring;
@@ -59,54 +62,78 @@ struct SchedParams {
   const int32_t* row_tag;
   const int32_t* arrive;
   const uint8_t* events;
-  uint32_t* iq;
+  uint32_t* lq;  // [WL][S] the local players' queued inputs by frame (slot frame % WL)
   int32_t* sst;
   int32_t* rollbacks;
   int64_t* resim;
 };
 
-template <int P>
-__device__ inline uint4* sched_cell(const SchedParams& p, int32_t slot, int64_t s) {
-  return reinterpret_cast<uint4*>(p.ring + ((int64_t)s * p.R + slot) * cell_dwords_s(P));
+// The block's LDS (dynamic): its 64 sessions' rings [R][PC][64] uint4 (+ frame tags [R][64] with
+// sparse saving; without it every frame 0 .. last save has been saved, so a cell's frame is the
+// newest one <= the last save in its slot), local queues [WL][64], and per stage of K calls the
+// arrival deltas + Event::Disconnected bits [K][64] u16 and the input rows [B + K][64] of frames /
+// calls [stage start - B, stage end) with their row tags.
+struct SchedLds {
+  size_t o_tags, o_lq, o_arr, o_rowtag, o_rows, total;
+};
+__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+__host__ __device__ inline int input_word_bytes(int P) { return P <= 1 ? 1 : (P == 2 ? 2 : 4); }
+__host__ __device__ inline SchedLds sched_lds(int P, int R, int sparse, int WL, int K, int B) {
+  SchedLds l;
+  const size_t ring = (size_t)R * (cell_dwords_s(P) / 4) * kBlock * 16;
+  l.o_tags = ring;
+  l.o_lq = align16(l.o_tags + (sparse ? (size_t)R * kBlock * 4 : 0));
+  l.o_arr = align16(l.o_lq + (size_t)WL * kBlock * input_word_bytes(P));
+  l.o_rowtag = align16(l.o_arr + (size_t)K * kBlock * 2);
+  l.o_rows = align16(l.o_rowtag + (size_t)(K + B) * 4);
+  l.total = align16(l.o_rows + (size_t)(K + B) * kBlock * input_word_bytes(P));
+  return l;
 }
-
-template <int P>
-__device__ inline void load_cell_s(BoxState<P>& st, const uint4* c) {
-  constexpr int F = state_fields(P);
-#pragma unroll
-  for (int k = 0; k < cell_dwords_s(P) / 4; k++) {
-    const uint4 v = c[k];
-    const uint32_t x[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-      if (4 * k + i < F) st.w[4 * k + i] = x[i];
-  }
-}
-// a cell = the state's F fields, then the fletcher16 handed to GameStateCell::save, zero padding
-template <int P>
-__device__ inline void store_cell_s(const BoxState<P>& st, uint32_t ck, uint4* c) {
-  constexpr int F = state_fields(P);
-#pragma unroll
-  for (int k = 0; k < cell_dwords_s(P) / 4; k++) {
-    uint32_t x[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) x[i] = 4 * k + i < F ? st.w[4 * k + i] : (4 * k + i == F ? ck : 0u);
-    c[k] = make_uint4(x[0], x[1], x[2], x[3]);
-  }
-}
+constexpr int kArrInvalid = 0xff;  // arrival code: a frame after its call (GGRS_E_INVALID)
+constexpr int kArrTooFar = 0xfe;   // a burst of >= 254 frames: past the device queue (GGRS_E_PRECONDITION)
 
 template <int P>
 __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
+  using T = typename InputWord<P>::T;
+  constexpr int F = state_fields(P);
+  constexpr int PC = cell_dwords_s(P) / 4;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const SchedLds L = sched_lds(P, p.R, p.sparse, p.WL, p.K, p.B);
+  // LDS regions addressed from the extern array itself at each use (pointer variables into dynamic
+  // LDS captured by the lambdas below become generic pointers, which this hipcc miscompiles)
+#define lring (reinterpret_cast<uint4*>(lds))
+#define ltag (reinterpret_cast<int32_t*>(lds + L.o_tags))
+#define llq (reinterpret_cast<T*>(lds + L.o_lq))
+#define larr (reinterpret_cast<uint16_t*>(lds + L.o_arr))
+#define lrowtag (reinterpret_cast<int32_t*>(lds + L.o_rowtag))
+#define lrows (reinterpret_cast<T*>(lds + L.o_rows))
+
   const int64_t S = p.S;
-  const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (s >= S) return;  // (no block-level synchronisation in this kernel)
+  const int64_t sess0 = (int64_t)blockIdx.x * kBlock;
+  const int lt = threadIdx.x;
+  const bool live = sess0 + lt < S;
+  const int64_t s = live ? sess0 + lt : sess0;  // idle lanes shadow the block's first session, never store
+  const int nb = (int)min((int64_t)kBlock, S - sess0);
   const uint32_t lmask = p.local_mask;
   uint32_t lbytes = 0;
 #pragma unroll
   for (int k = 0; k < P; k++) lbytes |= ((lmask >> k) & 1u) ? 0xffu << (8 * k) : 0u;
-  const int32_t maxp = p.maxp, R = p.R;
+  const int32_t maxp = p.maxp, R = p.R, WL = p.WL;
+  const int ring_pieces = R * PC;
 
-  // ---- the session's state
+  // ---- copy in: rings (the block's sessions are contiguous in HBM), tags, local queues
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(p.ring) + sess0 * ring_pieces;
+    const int n = nb * ring_pieces;
+    for (int i = lt; i < n; i += kBlock) {
+      const int sl = i / ring_pieces, rem = i - sl * ring_pieces;
+      lring[rem * kBlock + sl] = src[i];
+    }
+  }
+  if (p.sparse)
+    for (int q = 0; q < R; q++) ltag[q * kBlock + lt] = live ? p.ring_frame[(int64_t)q * S + s] : kNull;
+  for (int q = 0; q < WL; q++) llq[q * kBlock + lt] = live ? (T)p.lq[(int64_t)q * S + s] : (T)0;
+
   BoxState<P> st;
   load_state<P>(st, p.cur + s, S);
   auto fld = [&](int f) -> int32_t& { return p.sst[(int64_t)f * S + s]; };
@@ -122,44 +149,78 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
     finc[k] = fld(kPl0 + kPlFields * k + 3);
     lreq[k] = fld(kPl0 + kPlFields * k + 4);
   }
+  if (!live) err = 1;  // idle lanes run no call
   int32_t rollbacks = 0;
   int64_t resim = 0;
   // every state the launch steps descends from cur or from a ring cell this engine wrote, all in the
   // lean step's rotation domain: one wave-wide test instead of one per player per step
   const bool lean_ok = __all(rot_in_domain<P>(st));
+  __syncthreads();
 
-  uint32_t* const iq = p.iq + s;
-  auto iq_at = [&](int32_t q) -> uint32_t& { return iq[(int64_t)(q & (kQ - 1)) * S]; };
   auto next_slot = [&](int32_t x) { return x + 1 == R ? 0 : x + 1; };
   int32_t slot_f = cur % R;  // ring slot of the current frame
-
+  auto cell_load = [&](int32_t slot) {
+#pragma unroll
+    for (int k = 0; k < PC; k++) {
+      const uint4 v = lring[(slot * PC + k) * kBlock + lt];
+      const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        if (4 * k + i < F) st.w[4 * k + i] = x[i];
+    }
+  };
   // SaveGameState(h) into `slot` (sync_layer.rs:208-215 + ex_game.rs:103-108)
   auto save = [&](int32_t h, int32_t slot) {
-    store_cell_s<P>(st, fletcher16_state<P>(st), sched_cell<P>(p, slot, s));
-    p.ring_frame[(int64_t)slot * S + s] = h;
+    const uint32_t ck = fletcher16_state<P>(st);
+#pragma unroll
+    for (int k = 0; k < PC; k++) {
+      uint32_t x[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) x[i] = 4 * k + i < F ? st.w[4 * k + i] : (4 * k + i == F ? ck : 0u);
+      lring[(slot * PC + k) * kBlock + lt] = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+    if (p.sparse) ltag[slot * kBlock + lt] = h;
     last_saved = h;
   };
 
+  const int32_t c_end = p.c0 + p.n;
+  int32_t runmax = delivered;  // the arrivals staged so far
+  int32_t lo = 0, ce = 0;      // the stage's rows: frames / calls [lo, ce)
+  bool bad = false;            // a row read whose frame the input ring no longer holds
+  // input row g (frame g's remote inputs, call g's local ones): staged, or (older than the stage's
+  // window: a session far behind its calls) from the input ring
+  auto row = [&](int32_t g) -> uint32_t {
+    if (g >= lo) {
+      bad |= lrowtag[g - lo] != g;
+      return (uint32_t)lrows[(g - lo) * kBlock + lt];
+    }
+    const int32_t gi = g % p.cap;
+    bad |= p.row_tag[gi] != g;
+    return load_inputs<P>(p.inputs, (int64_t)gi * S + s);
+  };
   // synchronized_inputs(h) (sync_layer.rs:280-293) with InputQueue::input (input_queue.rs:104-167)
   auto sync_inputs = [&](int32_t h) -> uint32_t {
-    const uint32_t w = iq_at(h);
-    uint32_t in = 0;
+    uint32_t in = lbytes ? (uint32_t)llq[(h & (WL - 1)) * kBlock + lt] & lbytes : 0u;
+    uint32_t hrow = 0;
+    bool have_h = false;
 #pragma unroll
     for (int k = 0; k < P; k++) {
+      if ((lmask >> k) & 1u) continue;
       uint32_t v;
-      if ((lmask >> k) & 1u) {
-        v = (w >> (8 * k)) & 0xffu;  // local queues hold every frame <= current + delay
-      } else if (((disc >> k) & 1u) && lf[k] < h) {
+      if (((disc >> k) & 1u) && lf[k] < h) {
         v = 4u;  // InputStatus::Disconnected: ex_game spins the ship (ex_game.rs:280)
       } else {
         lreq[k] = h;
-        if (pf[k] < 0 && h <= lf[k]) {
-          v = (w >> (8 * k)) & 0xffu;  // confirmed
+        if (pf[k] < 0 && h <= lf[k]) {  // confirmed
+          if (!have_h) {
+            hrow = row(h);
+            have_h = true;
+          }
+          v = (hrow >> (8 * k)) & 0xffu;
         } else {
-          if (pf[k] < 0) {  // a new prediction from the last added input
+          if (pf[k] < 0) {  // a new prediction from the last added input (lib.rs:390-406)
             const bool prev = !(h == 0 || lf[k] == kNull);
-            const uint32_t last = prev ? (iq_at(lf[k]) >> (8 * k)) & 0xffu : 0u;
-            pin[k] = (int32_t)(prev ? (p.predictor == 0 ? last : 0u) : 0u);  // lib.rs:390-406
+            pin[k] = (prev && p.predictor == 0) ? (int32_t)((row(lf[k]) >> (8 * k)) & 0xffu) : 0;
             pf[k] = (prev ? lf[k] : kNull) + 1;
           }
           v = (uint32_t)pin[k];
@@ -170,8 +231,6 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
     return in;
   };
 
-  const int32_t c_end = p.c0 + p.n;
-  int32_t c = err ? c_end : p.c0;
   bool at_start = true, replaying = false, window_done = false, save_own = false;
   int32_t h = 0, load = 0, slot_h = 0, confirmed = kNull;
   // adjust_gamestate's LoadGameState + reset_prediction (p2p_session.rs:658-714)
@@ -179,8 +238,8 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
     if (from == kNull || from >= cur || from < cur - maxp) return false;  // load_frame's asserts
     const int32_t sh = slot_f - (cur - from);
     slot_h = sh < 0 ? sh + R : sh;
-    if (p.ring_frame[(int64_t)slot_h * S + s] != from) return false;  // cell.frame == frame_to_load
-    load_cell_s<P>(st, sched_cell<P>(p, slot_h, s));
+    if (p.sparse && ltag[slot_h * kBlock + lt] != from) return false;  // cell.frame == frame_to_load
+    cell_load(slot_h);
 #pragma unroll
     for (int k = 0; k < P; k++) {
       pf[k] = kNull;
@@ -195,135 +254,188 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
     return true;
   };
 
-  while (c < c_end) {
-    if (at_start) {
-      const int32_t ci = c % p.cap;
-      // 1. poll_remote_clients: the burst of remote frames (delivered, arrive_upto[c]]
-      const int32_t up = p.arrive[(int64_t)ci * S + s];
-      if (up > c) { err = GGRS_E_INVALID; break; }  // the remote peer cannot have sent a later frame
-      uint32_t cbytes = 0;  // bytes of the remote players still connected
+  for (int32_t cs = p.c0; cs < c_end; cs += p.K) {
+    ce = min(c_end, cs + p.K);
+    lo = max(0, cs - p.B);
+    const int nrows = ce - lo;
+    __syncthreads();  // every lane is done with the previous stage
+    {  // input rows [lo, ce) and their tags; row r of the block is 64 input words
+      int32_t ri = lo % p.cap;
+      const T* src = reinterpret_cast<const T*>(p.inputs) + sess0 + lt;
+      for (int r = 0; r < nrows; r++) {
+        if (lt < nb) lrows[r * kBlock + lt] = src[(int64_t)ri * S];
+        if (lt == 0) lrowtag[r] = p.row_tag[ri];
+        ri = ri + 1 == p.cap ? 0 : ri + 1;
+      }
+    }
+    {  // this session's arrivals and Event::Disconnected bits for calls [cs, ce)
+      int32_t ci = cs % p.cap;
+      for (int32_t c = cs; c < ce; c++) {
+        const int32_t up = live ? p.arrive[(int64_t)ci * S + s] : kNull;
+        const uint32_t ev = (live && p.events) ? p.events[(int64_t)ci * S + s] : 0u;
+        int32_t code;
+        if (up > c) {
+          code = kArrInvalid;
+        } else {
+          code = up > runmax ? min(up - runmax, kArrTooFar) : 0;
+          runmax = max(runmax, up);
+        }
+        larr[(c - cs) * kBlock + lt] = (uint16_t)(code | (ev << 8));
+        ci = ci + 1 == p.cap ? 0 : ci + 1;
+      }
+    }
+    __syncthreads();
+    int32_t c = err ? ce : cs;
+    while (c < ce) {
+      if (at_start) {
+        const uint32_t a = larr[(c - cs) * kBlock + lt];
+        const int32_t code = (int32_t)(a & 0xffu);
+        if (code == kArrInvalid) { err = GGRS_E_INVALID; break; }  // the remote peer cannot have sent it yet
+        if (code == kArrTooFar) { err = GGRS_E_PRECONDITION; break; }
+        // 1. poll_remote_clients: the burst of remote frames (delivered, delivered + code]
+        uint32_t cbytes = 0;  // bytes of the remote players still connected
 #pragma unroll
-      for (int k = 0; k < P; k++)
-        if (!((lmask >> k) & 1u) && !((disc >> k) & 1u)) cbytes |= 0xffu << (8 * k);
-      for (int32_t g = delivered + 1; g <= up; ++g) {
-        // the device queue keeps 128 frames (INPUT_QUEUE_LENGTH); a frame this far ahead of the
-        // session would overwrite one a rollback may still read (the reference's queue panics)
-        if (g >= cur - maxp + kQ - 1) { err = GGRS_E_PRECONDITION; break; }
-        const int32_t gi = g % p.cap;
-        if (p.row_tag[gi] != g) { err = GGRS_E_PRECONDITION; break; }  // input row no longer queued
-        const uint32_t row = load_inputs<P>(p.inputs, (int64_t)gi * S + s);
-        uint32_t& q = iq_at(g);
-        q = (q & ~cbytes) | (row & cbytes);
+        for (int k = 0; k < P; k++)
+          if (!((lmask >> k) & 1u) && !((disc >> k) & 1u)) cbytes |= 0xffu << (8 * k);
+        const int32_t up = delivered + code;
+        for (int32_t g = delivered + 1; g <= up; ++g) {
+          // the reference's InputQueue holds 128 inputs (input_queue.rs:6) and panics past them;
+          // the device keeps the same bound on how far the remote inputs may run ahead
+          if (g >= cur - maxp + kQ - 1) { err = GGRS_E_PRECONDITION; break; }
+          const uint32_t rw = row(g);
 #pragma unroll
-        for (int k = 0; k < P; k++) {  // Event::Input -> add_remote_input (p2p_session.rs:880-895)
-          if (!((cbytes >> (8 * k)) & 1u)) continue;
-          const int32_t v = (int32_t)((row >> (8 * k)) & 0xffu);
-          if (pf[k] != kNull) {  // add_input_by_frame (input_queue.rs:190-230)
-            if (finc[k] == kNull && pin[k] != v) finc[k] = g;
-            if (pf[k] == lreq[k] && finc[k] == kNull) pf[k] = kNull;
-            else pf[k] += 1;
+          for (int k = 0; k < P; k++) {  // Event::Input -> add_remote_input (p2p_session.rs:880-895)
+            if (!((cbytes >> (8 * k)) & 1u)) continue;
+            const int32_t v = (int32_t)((rw >> (8 * k)) & 0xffu);
+            if (pf[k] != kNull) {  // add_input_by_frame (input_queue.rs:190-230)
+              if (finc[k] == kNull && pin[k] != v) finc[k] = g;
+              if (pf[k] == lreq[k] && finc[k] == kNull) pf[k] = kNull;
+              else pf[k] += 1;
+            }
+            lf[k] = g;
           }
-          lf[k] = g;
+        }
+        if (bad && !err) err = GGRS_E_PRECONDITION;  // a remote input no longer in the input rows
+        if (err) break;
+        delivered = up;
+        // Event::Disconnected (p2p_session.rs:866-878 -> disconnect_player_at_frame :618-655)
+        const uint32_t ev = a >> 8;
+#pragma unroll
+        for (int k = 0; k < P; k++) {
+          if (!((ev >> k) & 1u) || ((lmask >> k) & 1u) || ((disc >> k) & 1u)) continue;
+          disc |= 1u << k;
+          if (cur > lf[k]) dframe = lf[k] + 1;
+        }
+        // 2. the first frame's save (:305-308)
+        if (cur == 0) save(0, slot_f);
+        // confirmed_frame (:542-553): the newest frame every connected player has sent
+        confirmed = INT32_MAX;
+#pragma unroll
+        for (int k = 0; k < P; k++) {
+          if ((disc >> k) & 1u) continue;
+          confirmed = min(confirmed, ((lmask >> k) & 1u) ? local_last : lf[k]);
+        }
+        if (confirmed == INT32_MAX) { err = GGRS_E_PRECONDITION; break; }  // assert!(confirmed < i32::MAX)
+        // 3. check_simulation_consistency(disconnect_frame) (sync_layer.rs:343-353) + adjust_gamestate
+        int32_t first_inc = dframe;
+#pragma unroll
+        for (int k = 0; k < P; k++)
+          if (finc[k] != kNull && (first_inc == kNull || finc[k] < first_inc)) first_inc = finc[k];
+        if (first_inc != kNull) {
+          if (!begin_replay(p.sparse ? last_saved : first_inc)) { err = GGRS_E_PRECONDITION; break; }
+          dframe = kNull;
+        }
+        window_done = false;
+        save_own = false;
+        at_start = false;
+      }
+      // sparse saving: check_last_saved_state (:819-843) once the rollback's replay is done
+      if (p.sparse && !replaying && !window_done) {
+        window_done = true;
+        if (cur - last_saved >= maxp) {
+          if (confirmed >= cur) save_own = true;
+          else if (!begin_replay(last_saved)) { err = GGRS_E_PRECONDITION; break; }
         }
       }
-      if (err) break;
-      delivered = max(delivered, up);
-      // Event::Disconnected (p2p_session.rs:866-878 -> disconnect_player_at_frame :618-655)
-      const uint32_t ev = p.events ? p.events[(int64_t)ci * S + s] : 0u;
-#pragma unroll
-      for (int k = 0; k < P; k++) {
-        if (!((ev >> k) & 1u) || ((lmask >> k) & 1u) || ((disc >> k) & 1u)) continue;
-        disc |= 1u << k;
-        if (cur > lf[k]) dframe = lf[k] + 1;
-      }
-      // 2. the first frame's save (:305-308)
-      if (cur == 0) save(0, slot_f);
-      // confirmed_frame (:542-553): the newest frame every connected player has sent
-      confirmed = INT32_MAX;
-#pragma unroll
-      for (int k = 0; k < P; k++) {
-        if ((disc >> k) & 1u) continue;
-        confirmed = min(confirmed, ((lmask >> k) & 1u) ? local_last : lf[k]);
-      }
-      if (confirmed == INT32_MAX) { err = GGRS_E_PRECONDITION; break; }  // assert!(confirmed < i32::MAX)
-      // 3. check_simulation_consistency(disconnect_frame) (sync_layer.rs:343-353) + adjust_gamestate
-      int32_t first_inc = dframe;
-#pragma unroll
-      for (int k = 0; k < P; k++)
-        if (finc[k] != kNull && (first_inc == kNull || finc[k] < first_inc)) first_inc = finc[k];
-      if (first_inc != kNull) {
-        if (!begin_replay(p.sparse ? last_saved : first_inc)) { err = GGRS_E_PRECONDITION; break; }
-        dframe = kNull;
-      }
-      window_done = false;
-      save_own = false;
-      at_start = false;
-    }
-    // sparse saving: check_last_saved_state (:819-843) once the rollback's replay is done
-    if (p.sparse && !replaying && !window_done) {
-      window_done = true;
-      if (cur - last_saved >= maxp) {
-        if (confirmed >= cur) save_own = true;
-        else if (!begin_replay(last_saved)) { err = GGRS_E_PRECONDITION; break; }
-      }
-    }
-    bool do_save, adv;
-    int32_t fr, sslot;
-    if (replaying) {
-      fr = h;
-      sslot = slot_h;
-      do_save = p.sparse ? h == confirmed : h > load;  // (:692-702)
-      adv = true;
-    } else {
-      fr = cur;
-      sslot = slot_f;
-      do_save = p.sparse ? save_own : true;  // SaveGameState(current) (:337)
-      // set_last_confirmed_frame (sync_layer.rs:313-340), after this call's saves
-      int32_t lc = confirmed;
-      const int32_t ls = do_save ? cur : last_saved;
-      if (p.sparse && ls < lc) lc = ls;
-      if (cur < lc) lc = cur;
-      lconf = lc;
-      // add_local_input for every local player (:362-377, input_queue.rs:170-186): queue frame
-      // current + delay, dropped unless it is the next one; the first fills the frames below the
-      // delay with the default input
-      if (lbytes) {
-        const int32_t qf = cur + p.delay;
-        if (local_last == kNull || qf == local_last + 1) {
-          if (local_last == kNull)
-            for (int32_t q = 0; q < p.delay; q++) iq_at(q) &= ~lbytes;
-          const uint32_t row = load_inputs<P>(p.inputs, (int64_t)(c % p.cap) * S + s);
-          uint32_t& w = iq_at(qf);
-          w = (w & ~lbytes) | (row & lbytes);
-          local_last = qf;
-        }
-      }
-      // the prediction threshold (:393-423)
-      const int32_t ahead = lconf == kNull ? cur : cur - lconf;
-      adv = ahead < maxp;
-    }
-    uint32_t in = 0;
-    if (adv) in = sync_inputs(fr);
-    if (do_save) save(fr, sslot);
-    if (adv) {
-      if (lean_ok) advance_state_lean<P>(st, in);
-      else advance_state<P>(st, in, 0u);
-    }
-    if (replaying) {
-      ++h;
-      slot_h = next_slot(slot_h);
-      replaying = h != cur;
-    } else {
-      if (adv) {
-        ++cur;
-        slot_f = next_slot(slot_f);
+      bool do_save, adv;
+      int32_t fr, sslot;
+      if (replaying) {
+        fr = h;
+        sslot = slot_h;
+        do_save = p.sparse ? h == confirmed : h > load;  // (:692-702)
+        adv = true;
       } else {
-        ++skips;
+        fr = cur;
+        sslot = slot_f;
+        do_save = p.sparse ? save_own : true;  // SaveGameState(current) (:337)
+        // set_last_confirmed_frame (sync_layer.rs:313-340), after this call's saves
+        int32_t lc = confirmed;
+        const int32_t ls = do_save ? cur : last_saved;
+        if (p.sparse && ls < lc) lc = ls;
+        if (cur < lc) lc = cur;
+        lconf = lc;
+        // add_local_input for every local player (:362-377, input_queue.rs:170-186): queue frame
+        // current + delay, dropped unless it is the next one; the first fills the frames below the
+        // delay with the default input
+        if (lbytes) {
+          const int32_t qf = cur + p.delay;
+          if (local_last == kNull || qf == local_last + 1) {
+            if (local_last == kNull)
+              for (int32_t q = 0; q < p.delay; q++) llq[(q & (WL - 1)) * kBlock + lt] = (T)0;
+            llq[(qf & (WL - 1)) * kBlock + lt] = (T)(row(c) & lbytes);
+            local_last = qf;
+          }
+        }
+        // the prediction threshold (:393-423)
+        const int32_t ahead = lconf == kNull ? cur : cur - lconf;
+        adv = ahead < maxp;
       }
-      ++c;
-      at_start = true;
+      uint32_t in = 0;
+      if (adv) in = sync_inputs(fr);
+      if (bad) { err = GGRS_E_PRECONDITION; break; }
+      if (do_save) save(fr, sslot);
+      if (adv) {
+        if (lean_ok) advance_state_lean<P>(st, in);
+        else advance_state<P>(st, in, 0u);
+      }
+      if (replaying) {
+        ++h;
+        slot_h = next_slot(slot_h);
+        replaying = h != cur;
+      } else {
+        if (adv) {
+          ++cur;
+          slot_f = next_slot(slot_f);
+        } else {
+          ++skips;
+        }
+        ++c;
+        at_start = true;
+      }
     }
   }
+  __syncthreads();
+  {  // rings back to HBM
+    uint4* dst = reinterpret_cast<uint4*>(p.ring) + sess0 * ring_pieces;
+    const int n = nb * ring_pieces;
+    for (int i = lt; i < n; i += kBlock) {
+      const int sl = i / ring_pieces, rem = i - sl * ring_pieces;
+      dst[i] = lring[rem * kBlock + sl];
+    }
+  }
+  if (!live) return;
+  for (int q = 0; q < R; q++) {  // the cells' frames
+    int32_t fr = kNull;
+    if (p.sparse) {
+      fr = ltag[q * kBlock + lt];
+    } else if (last_saved != kNull) {  // the newest frame <= the last save in slot q
+      const int32_t d = (last_saved - q) % R;
+      fr = last_saved - (d < 0 ? d + R : d);
+      if (fr < 0) fr = kNull;
+    }
+    p.ring_frame[(int64_t)q * S + s] = fr;
+  }
+  for (int q = 0; q < WL; q++) p.lq[(int64_t)q * S + s] = (uint32_t)llq[q * kBlock + lt];
   store_state<P>(st, p.cur + s, S);
   fld(kCur) = cur;
   fld(kLconf) = lconf;
@@ -344,6 +456,12 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
   }
   p.rollbacks[s] += rollbacks;
   p.resim[s] += resim;
+#undef lring
+#undef ltag
+#undef llq
+#undef larr
+#undef lrowtag
+#undef lrows
 }
 
 // every session at frame 0, nothing arrived, every player connected (SyncLayer::new,
@@ -410,7 +528,21 @@ int p2p_sched_advance(ggrs_p2p_engine* e, int32_t n) {
     if (rc) return rc;
     return p2p_sched_advance(e, n - e->cap);
   }
+  // stage geometry: B rows behind a stage's first call (a rollback's confirmed inputs reach back
+  // max_prediction frames, a burst after a stall a few more), K calls per stage as many as keep the
+  // block's LDS within 40 KB (four blocks, one per SIMD, per CU) -- at least 8
+  const int P = e->cfg.num_players;
+  int WL = 2;
+  while (WL < e->cfg.max_prediction + e->cfg.input_delay + 2) WL *= 2;
+  const int B = 2 * e->cfg.max_prediction + 4;
+  int K = 64;
+  while (K > 8 && sched_lds(P, e->R, e->sparse, WL, K, B).total > 40 * 1024) K -= 4;
+  const size_t shm = sched_lds(P, e->R, e->sparse, WL, K, B).total;
+  if (shm > 160 * 1024) return set_error(GGRS_E_INVALID, "max_prediction too large for the scheduled kernel's LDS");
   SchedParams p;
+  p.K = K;
+  p.B = B;
+  p.WL = WL;
   p.S = e->cfg.num_sessions;
   p.R = e->R;
   p.delay = e->cfg.input_delay;
@@ -428,15 +560,21 @@ int p2p_sched_advance(ggrs_p2p_engine* e, int32_t n) {
   p.row_tag = e->row_tag;
   p.arrive = e->arrive;
   p.events = e->events;
-  p.iq = e->iq;
+  p.lq = e->iq;
   p.sst = e->sst;
   p.rollbacks = e->rollbacks;
   p.resim = e->resim;
   if (int rc = e->timer.before(e->stream)) return rc;
-  dispatch_players(e->cfg.num_players, [&](auto PC) {
+  hipError_t attr = hipSuccess;
+  dispatch_players(P, [&](auto PC) {
     constexpr int PP = decltype(PC)::value;
-    p2p_sched_kernel<PP><<<(unsigned)grid_of(p.S, kBlock), kBlock, 0, e->stream>>>(p);
+    if (shm > 64 * 1024)
+      attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&p2p_sched_kernel<PP>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    if (attr == hipSuccess)
+      p2p_sched_kernel<PP><<<(unsigned)grid_of(p.S, kBlock), kBlock, shm, e->stream>>>(p);
   });
+  HIP_TRY(attr);
   HIP_TRY(hipGetLastError());
   e->timer.count();
   e->current_frame += n;
