@@ -130,8 +130,11 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
       lring[rem * kBlock + sl] = src[i];
     }
   }
-  if (p.sparse)
+  if (p.sparse) {
+#pragma unroll 8
     for (int q = 0; q < R; q++) ltag[q * kBlock + lt] = live ? p.ring_frame[(int64_t)q * S + s] : kNull;
+  }
+#pragma unroll 8
   for (int q = 0; q < WL; q++) llq[q * kBlock + lt] = live ? (T)p.lq[(int64_t)q * S + s] : (T)0;
 
   BoxState<P> st;
@@ -259,29 +262,71 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
     lo = max(0, cs - p.B);
     const int nrows = ce - lo;
     __syncthreads();  // every lane is done with the previous stage
-    {  // input rows [lo, ce) and their tags; row r of the block is 64 input words
-      int32_t ri = lo % p.cap;
+    // Staging: every load of a batch is issued before the first is used (one wave per SIMD: a
+    // load-use chain per row or call would cost a full memory latency each).
+    const int32_t lo_i = lo % p.cap;  // ring slot of row lo
+    constexpr int kUnitT = 16 / sizeof(T);  // input words per 16-byte unit
+    if (nb == kBlock && ((S * (int64_t)sizeof(T)) & 15) == 0) {  // rows [lo, ce) as 16-byte units
+      constexpr int kUpr = kBlock / kUnitT;  // units per row
+      const int units = nrows * kUpr;
+      for (int u0 = 0; u0 < units; u0 += 8 * kBlock) {
+        uint4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          const int u = u0 + j * kBlock + lt;
+          if (u < units) {
+            const int r = u / kUpr, k = u - r * kUpr;
+            int32_t ri = lo_i + r;
+            ri = ri >= p.cap ? ri - p.cap : ri;
+            v[j] = reinterpret_cast<const uint4*>(p.inputs + ((int64_t)ri * S + sess0) * sizeof(T))[k];
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          const int u = u0 + j * kBlock + lt;
+          if (u < units) reinterpret_cast<uint4*>(lrows)[u] = v[j];
+        }
+      }
+    } else {  // a partial last block: word by word
       const T* src = reinterpret_cast<const T*>(p.inputs) + sess0 + lt;
+#pragma unroll 8
       for (int r = 0; r < nrows; r++) {
+        int32_t ri = lo_i + r;
+        ri = ri >= p.cap ? ri - p.cap : ri;
         if (lt < nb) lrows[r * kBlock + lt] = src[(int64_t)ri * S];
-        if (lt == 0) lrowtag[r] = p.row_tag[ri];
-        ri = ri + 1 == p.cap ? 0 : ri + 1;
       }
     }
-    {  // this session's arrivals and Event::Disconnected bits for calls [cs, ce)
-      int32_t ci = cs % p.cap;
-      for (int32_t c = cs; c < ce; c++) {
-        const int32_t up = live ? p.arrive[(int64_t)ci * S + s] : kNull;
-        const uint32_t ev = (live && p.events) ? p.events[(int64_t)ci * S + s] : 0u;
-        int32_t code;
-        if (up > c) {
-          code = kArrInvalid;
-        } else {
-          code = up > runmax ? min(up - runmax, kArrTooFar) : 0;
-          runmax = max(runmax, up);
+    for (int r = lt; r < nrows; r += kBlock) {
+      int32_t ri = lo_i + r;
+      ri = ri >= p.cap ? ri - p.cap : ri;
+      lrowtag[r] = p.row_tag[ri];
+    }
+    {  // this session's arrivals and Event::Disconnected bits for calls [cs, ce), eight at a time
+      const int32_t ci0 = cs % p.cap;
+      for (int32_t cb = cs; cb < ce; cb += 8) {
+        int32_t up[8];
+        uint32_t ev[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          int32_t ci = ci0 + (cb - cs) + j;
+          ci = ci >= p.cap ? ci - p.cap : ci;
+          const bool in = live && cb + j < ce;
+          up[j] = in ? p.arrive[(int64_t)ci * S + s] : kNull;
+          ev[j] = (in && p.events) ? p.events[(int64_t)ci * S + s] : 0u;
         }
-        larr[(c - cs) * kBlock + lt] = (uint16_t)(code | (ev << 8));
-        ci = ci + 1 == p.cap ? 0 : ci + 1;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          const int32_t c = cb + j;
+          if (c >= ce) break;
+          int32_t code;
+          if (up[j] > c) {
+            code = kArrInvalid;
+          } else {
+            code = up[j] > runmax ? min(up[j] - runmax, kArrTooFar) : 0;
+            runmax = max(runmax, up[j]);
+          }
+          larr[(c - cs) * kBlock + lt] = (uint16_t)(code | (ev[j] << 8));
+        }
       }
     }
     __syncthreads();
