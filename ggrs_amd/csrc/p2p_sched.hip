@@ -24,8 +24,8 @@
 //   sst   [fields][S] i32   SyncLayer current/last_confirmed/last_saved frames, disconnect_frame,
 //                           the newest delivered remote frame, local players' last queued frame,
 //                           skipped calls, the session's error, the disconnected mask, and per
-//                           player last_frame (local_connect_status), prediction frame / input,
-//                           first_incorrect_frame, last_requested_frame (input_queue.rs:10-37)
+//                           player last_frame (local_connect_status); the remote InputQueues'
+//                           prediction state is implied (the canonical form, in the kernel)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -46,7 +46,7 @@ constexpr int kQ = 128;  // INPUT_QUEUE_LENGTH (input_queue.rs:6)
 constexpr int kBlock = 64;
 
 enum : int { kCur = 0, kLconf, kDframe, kLastSaved, kDelivered, kLocalLast, kSkips, kErr, kDisc, kPl0 };
-constexpr int kPlFields = 5;  // per player: last_frame, prediction.frame, prediction.input, first_incorrect, last_requested
+constexpr int kPlFields = 1;  // per player: last_frame (local_connect_status; remote players)
 __host__ __device__ constexpr int sched_fields(int P) { return kPl0 + kPlFields * P; }
 __host__ __device__ constexpr int cell_dwords_s(int p) { return (state_fields(p) + 1 + 3) & ~3; }
 
@@ -118,6 +118,7 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
   uint32_t lbytes = 0;
 #pragma unroll
   for (int k = 0; k < P; k++) lbytes |= ((lmask >> k) & 1u) ? 0xffu << (8 * k) : 0u;
+  const uint32_t rbytes = (P == 4 ? 0xffffffffu : ((1u << (8 * P)) - 1u)) & ~lbytes;  // remote players' bytes
   const int32_t maxp = p.maxp, R = p.R, WL = p.WL;
   const int ring_pieces = R * PC;
 
@@ -143,15 +144,11 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
   int32_t cur = fld(kCur), lconf = fld(kLconf), dframe = fld(kDframe), last_saved = fld(kLastSaved);
   int32_t delivered = fld(kDelivered), local_last = fld(kLocalLast), skips = fld(kSkips), err = fld(kErr);
   uint32_t disc = (uint32_t)fld(kDisc);
-  int32_t lf[P], pf[P], pin[P], finc[P], lreq[P];
+  // the remote players' last frames (local_connect_status[k].last_frame): the newest delivered frame
+  // for a connected player, frozen at its disconnect
+  int32_t lf[P];
 #pragma unroll
-  for (int k = 0; k < P; k++) {
-    lf[k] = fld(kPl0 + kPlFields * k + 0);
-    pf[k] = fld(kPl0 + kPlFields * k + 1);
-    pin[k] = fld(kPl0 + kPlFields * k + 2);
-    finc[k] = fld(kPl0 + kPlFields * k + 3);
-    lreq[k] = fld(kPl0 + kPlFields * k + 4);
-  }
+  for (int k = 0; k < P; k++) lf[k] = fld(kPl0 + kPlFields * k + 0);
   if (!live) err = 1;  // idle lanes run no call
   int32_t rollbacks = 0;
   int64_t resim = 0;
@@ -201,39 +198,38 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
     bad |= p.row_tag[gi] != g;
     return load_inputs<P>(p.inputs, (int64_t)gi * S + s);
   };
-  // synchronized_inputs(h) (sync_layer.rs:280-293) with InputQueue::input (input_queue.rs:104-167)
-  auto sync_inputs = [&](int32_t h) -> uint32_t {
+  // The remote InputQueues in their canonical form.  Every frame a session has simulated used, for
+  // a connected remote player, its input if it had arrived (frame <= lf) and otherwise the
+  // prediction made from the newest arrived one (repeat-last: its input; PredictDefault, or nothing
+  // arrived yet: 0; lib.rs:390-406, input_queue.rs:128-161): a prediction, once made, is kept until
+  // an arrival contradicts it (add_input_by_frame's first_incorrect_frame, input_queue.rs:190-230),
+  // and an arrival that confirms it leaves "the newest input" equal to it, so the value predicted for
+  // every simulated frame past lf IS the newest input.  Hence a burst (lf, up] is mispredicted at the
+  // first g < current_frame whose input differs from the newest input before the burst, a rollback's
+  // replay (reset_prediction, then synchronized_inputs per frame) uses the confirmed inputs up to lf
+  // and the newest input after, and no per-frame prediction / last_requested bookkeeping is needed.
+  // pbase: the connected remote players' prediction (their bytes of the newest delivered row).
+  uint32_t pbase = 0;
+  auto base_of = [&](int32_t d, uint32_t cb) -> uint32_t {
+    return (p.predictor == 0 && d != kNull) ? row(d) & cb : 0u;
+  };
+  // synchronized_inputs(h) (sync_layer.rs:280-293): local players from their queues, connected
+  // remote players confirmed or predicted, disconnected ones InputStatus::Disconnected past their
+  // last frame (ex_game spins the ship: input 4, ex_game.rs:280)
+  auto sync_inputs = [&](int32_t h, uint32_t cb) -> uint32_t {
     uint32_t in = lbytes ? (uint32_t)llq[(h & (WL - 1)) * kBlock + lt] & lbytes : 0u;
-    uint32_t hrow = 0;
-    bool have_h = false;
+    const bool conf = h <= delivered;  // (a disconnected player's last frame is <= delivered too)
+    const uint32_t hrow = conf ? row(h) : 0u;
+    in |= conf ? hrow & cb : pbase;
+    if (disc) {
 #pragma unroll
-    for (int k = 0; k < P; k++) {
-      if ((lmask >> k) & 1u) continue;
-      uint32_t v;
-      if (((disc >> k) & 1u) && lf[k] < h) {
-        v = 4u;  // InputStatus::Disconnected: ex_game spins the ship (ex_game.rs:280)
-      } else {
-        lreq[k] = h;
-        if (pf[k] < 0 && h <= lf[k]) {  // confirmed
-          if (!have_h) {
-            hrow = row(h);
-            have_h = true;
-          }
-          v = (hrow >> (8 * k)) & 0xffu;
-        } else {
-          if (pf[k] < 0) {  // a new prediction from the last added input (lib.rs:390-406)
-            const bool prev = !(h == 0 || lf[k] == kNull);
-            pin[k] = (prev && p.predictor == 0) ? (int32_t)((row(lf[k]) >> (8 * k)) & 0xffu) : 0;
-            pf[k] = (prev ? lf[k] : kNull) + 1;
-          }
-          v = (uint32_t)pin[k];
-        }
-      }
-      in |= v << (8 * k);
+      for (int k = 0; k < P; k++)
+        if ((disc >> k) & 1u) in |= (h <= lf[k] ? (hrow >> (8 * k)) & 0xffu : 4u) << (8 * k);
     }
     return in;
   };
 
+  uint32_t conn = 0;  // the connected remote players' bytes (set at each call start)
   bool at_start = true, replaying = false, window_done = false, save_own = false;
   int32_t h = 0, load = 0, slot_h = 0, confirmed = kNull;
   // adjust_gamestate's LoadGameState + reset_prediction (p2p_session.rs:658-714)
@@ -242,13 +238,7 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
     const int32_t sh = slot_f - (cur - from);
     slot_h = sh < 0 ? sh + R : sh;
     if (p.sparse && ltag[slot_h * kBlock + lt] != from) return false;  // cell.frame == frame_to_load
-    cell_load(slot_h);
-#pragma unroll
-    for (int k = 0; k < P; k++) {
-      pf[k] = kNull;
-      finc[k] = kNull;
-      lreq[k] = kNull;
-    }
+    cell_load(slot_h);  // (reset_prediction: nothing to reset in the canonical form)
     load = from;
     h = from;
     replaying = true;
@@ -337,40 +327,45 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
         const int32_t code = (int32_t)(a & 0xffu);
         if (code == kArrInvalid) { err = GGRS_E_INVALID; break; }  // the remote peer cannot have sent it yet
         if (code == kArrTooFar) { err = GGRS_E_PRECONDITION; break; }
-        // 1. poll_remote_clients: the burst of remote frames (delivered, delivered + code]
-        uint32_t cbytes = 0;  // bytes of the remote players still connected
+        // 1. poll_remote_clients: the burst of remote frames (delivered, delivered + code] for the
+        //    remote players still connected (handle_event Event::Input, p2p_session.rs:880-895)
+        uint32_t cb = rbytes;  // bytes of the remote players still connected
 #pragma unroll
         for (int k = 0; k < P; k++)
-          if (!((lmask >> k) & 1u) && !((disc >> k) & 1u)) cbytes |= 0xffu << (8 * k);
+          if ((disc >> k) & 1u) cb &= ~(0xffu << (8 * k));
         const int32_t up = delivered + code;
-        for (int32_t g = delivered + 1; g <= up; ++g) {
-          // the reference's InputQueue holds 128 inputs (input_queue.rs:6) and panics past them;
-          // the device keeps the same bound on how far the remote inputs may run ahead
-          if (g >= cur - maxp + kQ - 1) { err = GGRS_E_PRECONDITION; break; }
-          const uint32_t rw = row(g);
-#pragma unroll
-          for (int k = 0; k < P; k++) {  // Event::Input -> add_remote_input (p2p_session.rs:880-895)
-            if (!((cbytes >> (8 * k)) & 1u)) continue;
-            const int32_t v = (int32_t)((rw >> (8 * k)) & 0xffu);
-            if (pf[k] != kNull) {  // add_input_by_frame (input_queue.rs:190-230)
-              if (finc[k] == kNull && pin[k] != v) finc[k] = g;
-              if (pf[k] == lreq[k] && finc[k] == kNull) pf[k] = kNull;
-              else pf[k] += 1;
+        // the reference's InputQueue holds 128 inputs (input_queue.rs:6) and panics past them; the
+        // device keeps the same bound on how far the remote inputs may run ahead of the session
+        if (up >= cur - maxp + kQ - 1) { err = GGRS_E_PRECONDITION; break; }
+        // add_input_by_frame's first_incorrect_frame: the first frame of the burst the session has
+        // simulated whose inputs differ from the prediction (the canonical form above)
+        int32_t mis = kNull;
+        if (cb) {
+          pbase = base_of(delivered, cb);
+          const int32_t last = min(up, cur - 1);
+          for (int32_t g = delivered + 1; g <= last; ++g)
+            if ((row(g) & cb) != pbase) {
+              mis = g;
+              break;
             }
-            lf[k] = g;
-          }
         }
-        if (bad && !err) err = GGRS_E_PRECONDITION;  // a remote input no longer in the input rows
-        if (err) break;
+        if (bad) { err = GGRS_E_PRECONDITION; break; }  // a remote input no longer in the input rows
         delivered = up;
+#pragma unroll
+        for (int k = 0; k < P; k++)
+          if ((cb >> (8 * k)) & 1u) lf[k] = up;
         // Event::Disconnected (p2p_session.rs:866-878 -> disconnect_player_at_frame :618-655)
         const uint32_t ev = a >> 8;
 #pragma unroll
         for (int k = 0; k < P; k++) {
           if (!((ev >> k) & 1u) || ((lmask >> k) & 1u) || ((disc >> k) & 1u)) continue;
           disc |= 1u << k;
+          cb &= ~(0xffu << (8 * k));
           if (cur > lf[k]) dframe = lf[k] + 1;
         }
+        pbase = base_of(delivered, cb);  // the prediction from the newest input
+        if (bad) { err = GGRS_E_PRECONDITION; break; }
+        conn = cb;
         // 2. the first frame's save (:305-308)
         if (cur == 0) save(0, slot_f);
         // confirmed_frame (:542-553): the newest frame every connected player has sent
@@ -383,9 +378,7 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
         if (confirmed == INT32_MAX) { err = GGRS_E_PRECONDITION; break; }  // assert!(confirmed < i32::MAX)
         // 3. check_simulation_consistency(disconnect_frame) (sync_layer.rs:343-353) + adjust_gamestate
         int32_t first_inc = dframe;
-#pragma unroll
-        for (int k = 0; k < P; k++)
-          if (finc[k] != kNull && (first_inc == kNull || finc[k] < first_inc)) first_inc = finc[k];
+        if (mis != kNull && (first_inc == kNull || mis < first_inc)) first_inc = mis;
         if (first_inc != kNull) {
           if (!begin_replay(p.sparse ? last_saved : first_inc)) { err = GGRS_E_PRECONDITION; break; }
           dframe = kNull;
@@ -436,7 +429,7 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
         adv = ahead < maxp;
       }
       uint32_t in = 0;
-      if (adv) in = sync_inputs(fr);
+      if (adv) in = sync_inputs(fr, conn);
       if (bad) { err = GGRS_E_PRECONDITION; break; }
       if (do_save) save(fr, sslot);
       if (adv) {
@@ -492,13 +485,7 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
   fld(kErr) = err;
   fld(kDisc) = (int32_t)disc;
 #pragma unroll
-  for (int k = 0; k < P; k++) {
-    fld(kPl0 + kPlFields * k + 0) = lf[k];
-    fld(kPl0 + kPlFields * k + 1) = pf[k];
-    fld(kPl0 + kPlFields * k + 2) = pin[k];
-    fld(kPl0 + kPlFields * k + 3) = finc[k];
-    fld(kPl0 + kPlFields * k + 4) = lreq[k];
-  }
+  for (int k = 0; k < P; k++) fld(kPl0 + kPlFields * k + 0) = lf[k];
   p.rollbacks[s] += rollbacks;
   p.resim[s] += resim;
 #undef lring
@@ -517,7 +504,6 @@ __global__ void sched_init_kernel(int32_t* sst, int64_t S, int32_t P) {
   const int f = (int)(i / S);
   int32_t v = kNull;
   if (f == kCur || f == kSkips || f == kErr || f == kDisc) v = 0;
-  if (f >= kPl0 && (f - kPl0) % kPlFields == 2) v = 0;  // prediction.input
   sst[i] = v;
 }
 
