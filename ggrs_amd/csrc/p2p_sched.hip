@@ -74,31 +74,44 @@ struct SchedParams {
 // arrival deltas + Event::Disconnected bits [K][64] u16 and the input rows [B + K][64] of frames /
 // calls [stage start - B, stage end) with their row tags.
 struct SchedLds {
-  size_t o_tags, o_lq, o_arr, o_rowtag, o_rows, total;
+  uint32_t o_tags, o_lq, o_arr, o_rowtag, o_rows, total;  // byte offsets (32-bit: scalar registers are scarce)
 };
-__host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+__host__ __device__ inline uint32_t align16(uint32_t x) { return (x + 15) & ~15u; }
 __host__ __device__ inline int input_word_bytes(int P) { return P <= 1 ? 1 : (P == 2 ? 2 : 4); }
 __host__ __device__ inline SchedLds sched_lds(int P, int R, int sparse, int WL, int K, int B) {
   SchedLds l;
-  const size_t ring = (size_t)R * (cell_dwords_s(P) / 4) * kBlock * 16;
+  const uint32_t ring = (uint32_t)R * (cell_dwords_s(P) / 4) * kBlock * 16;
   l.o_tags = ring;
-  l.o_lq = align16(l.o_tags + (sparse ? (size_t)R * kBlock * 4 : 0));
-  l.o_arr = align16(l.o_lq + (size_t)WL * kBlock * input_word_bytes(P));
-  l.o_rowtag = align16(l.o_arr + (size_t)K * kBlock * 2);
-  l.o_rows = align16(l.o_rowtag + (size_t)(K + B) * 4);
-  l.total = align16(l.o_rows + (size_t)(K + B) * kBlock * input_word_bytes(P));
+  l.o_lq = align16(l.o_tags + (sparse ? (uint32_t)R * kBlock * 4 : 0u));
+  l.o_arr = align16(l.o_lq + (uint32_t)WL * kBlock * input_word_bytes(P));
+  l.o_rowtag = align16(l.o_arr + (uint32_t)K * kBlock * 2);
+  l.o_rows = align16(l.o_rowtag + (uint32_t)(K + B) * 4);
+  l.total = align16(l.o_rows + (uint32_t)(K + B) * kBlock * input_word_bytes(P));
   return l;
 }
 constexpr int kArrInvalid = 0xff;  // arrival code: a frame after its call (GGRS_E_INVALID)
 constexpr int kArrTooFar = 0xfe;   // a burst of >= 254 frames: past the device queue (GGRS_E_PRECONDITION)
 
-template <int P>
+// A pointer held in vector registers: the kernel's uniform values exceed the scalar register file
+// (102 SGPRs) and the compiler spills them to VGPR lanes, reloading each with a v_readlane at every
+// use; the buffers touched only at a launch's start and end and by rare paths live in VGPRs instead
+// (an empty asm statement: it emits no instruction).
+template <typename T>
+__device__ inline T* in_vgpr_ptr(T* ptr) {
+  uint64_t u = reinterpret_cast<uint64_t>(ptr);
+  asm volatile("" : "+v"(u));
+  return reinterpret_cast<T*>(u);
+}
+
+// kSparse: sparse saving; kPred: the predictor (0 repeat-last, 1 PredictDefault) -- compile-time, so
+// their tests leave the step loop and its scalar registers
+template <int P, bool kSparse, int kPred>
 __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
   using T = typename InputWord<P>::T;
   constexpr int F = state_fields(P);
   constexpr int PC = cell_dwords_s(P) / 4;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const SchedLds L = sched_lds(P, p.R, p.sparse, p.WL, p.K, p.B);
+  const SchedLds L = sched_lds(P, p.R, kSparse, p.WL, p.K, p.B);
   // LDS regions addressed from the extern array itself at each use (pointer variables into dynamic
   // LDS captured by the lambdas below become generic pointers, which this hipcc miscompiles)
 #define lring (reinterpret_cast<uint4*>(lds))
@@ -108,6 +121,15 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
 #define lrowtag (reinterpret_cast<int32_t*>(lds + L.o_rowtag))
 #define lrows (reinterpret_cast<T*>(lds + L.o_rows))
 
+  p.cur = in_vgpr_ptr(p.cur);
+  p.ring = in_vgpr_ptr(p.ring);
+  p.ring_frame = in_vgpr_ptr(p.ring_frame);
+  p.lq = in_vgpr_ptr(p.lq);
+  p.sst = in_vgpr_ptr(p.sst);
+  p.rollbacks = in_vgpr_ptr(p.rollbacks);
+  p.resim = in_vgpr_ptr(p.resim);
+  p.row_tag = in_vgpr_ptr(p.row_tag);
+  p.events = in_vgpr_ptr(p.events);
   const int64_t S = p.S;
   const int64_t sess0 = (int64_t)blockIdx.x * kBlock;
   const int lt = threadIdx.x;
@@ -131,7 +153,7 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
       lring[rem * kBlock + sl] = src[i];
     }
   }
-  if (p.sparse) {
+  if (kSparse) {
 #pragma unroll 8
     for (int q = 0; q < R; q++) ltag[q * kBlock + lt] = live ? p.ring_frame[(int64_t)q * S + s] : kNull;
   }
@@ -155,6 +177,9 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
   // every state the launch steps descends from cur or from a ring cell this engine wrote, all in the
   // lean step's rotation domain: one wave-wide test instead of one per player per step
   const bool lean_ok = __all(rot_in_domain<P>(st));
+  // the glibc sinf/cosf constants in vector registers: beside this kernel's many uniform values
+  // they would otherwise take 20 scalar registers and spill (glibc_sincosf.h, SincosConsts)
+  const SincosConsts K = sincos_consts_vgpr();
   __syncthreads();
 
   auto next_slot = [&](int32_t x) { return x + 1 == R ? 0 : x + 1; };
@@ -179,7 +204,7 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
       for (int i = 0; i < 4; i++) x[i] = 4 * k + i < F ? st.w[4 * k + i] : (4 * k + i == F ? ck : 0u);
       lring[(slot * PC + k) * kBlock + lt] = make_uint4(x[0], x[1], x[2], x[3]);
     }
-    if (p.sparse) ltag[slot * kBlock + lt] = h;
+    if (kSparse) ltag[slot * kBlock + lt] = h;
     last_saved = h;
   };
 
@@ -211,7 +236,7 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
   // pbase: the connected remote players' prediction (their bytes of the newest delivered row).
   uint32_t pbase = 0;
   auto base_of = [&](int32_t d, uint32_t cb) -> uint32_t {
-    return (p.predictor == 0 && d != kNull) ? row(d) & cb : 0u;
+    return (kPred == 0 && d != kNull) ? row(d) & cb : 0u;
   };
   // synchronized_inputs(h) (sync_layer.rs:280-293): local players from their queues, connected
   // remote players confirmed or predicted, disconnected ones InputStatus::Disconnected past their
@@ -237,7 +262,7 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
     if (from == kNull || from >= cur || from < cur - maxp) return false;  // load_frame's asserts
     const int32_t sh = slot_f - (cur - from);
     slot_h = sh < 0 ? sh + R : sh;
-    if (p.sparse && ltag[slot_h * kBlock + lt] != from) return false;  // cell.frame == frame_to_load
+    if (kSparse && ltag[slot_h * kBlock + lt] != from) return false;  // cell.frame == frame_to_load
     cell_load(slot_h);  // (reset_prediction: nothing to reset in the canonical form)
     load = from;
     h = from;
@@ -380,7 +405,7 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
         int32_t first_inc = dframe;
         if (mis != kNull && (first_inc == kNull || mis < first_inc)) first_inc = mis;
         if (first_inc != kNull) {
-          if (!begin_replay(p.sparse ? last_saved : first_inc)) { err = GGRS_E_PRECONDITION; break; }
+          if (!begin_replay(kSparse ? last_saved : first_inc)) { err = GGRS_E_PRECONDITION; break; }
           dframe = kNull;
         }
         window_done = false;
@@ -388,7 +413,7 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
         at_start = false;
       }
       // sparse saving: check_last_saved_state (:819-843) once the rollback's replay is done
-      if (p.sparse && !replaying && !window_done) {
+      if (kSparse && !replaying && !window_done) {
         window_done = true;
         if (cur - last_saved >= maxp) {
           if (confirmed >= cur) save_own = true;
@@ -400,16 +425,16 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
       if (replaying) {
         fr = h;
         sslot = slot_h;
-        do_save = p.sparse ? h == confirmed : h > load;  // (:692-702)
+        do_save = kSparse ? h == confirmed : h > load;  // (:692-702)
         adv = true;
       } else {
         fr = cur;
         sslot = slot_f;
-        do_save = p.sparse ? save_own : true;  // SaveGameState(current) (:337)
+        do_save = kSparse ? save_own : true;  // SaveGameState(current) (:337)
         // set_last_confirmed_frame (sync_layer.rs:313-340), after this call's saves
         int32_t lc = confirmed;
         const int32_t ls = do_save ? cur : last_saved;
-        if (p.sparse && ls < lc) lc = ls;
+        if (kSparse && ls < lc) lc = ls;
         if (cur < lc) lc = cur;
         lconf = lc;
         // add_local_input for every local player (:362-377, input_queue.rs:170-186): queue frame
@@ -433,8 +458,30 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
       if (bad) { err = GGRS_E_PRECONDITION; break; }
       if (do_save) save(fr, sslot);
       if (adv) {
-        if (lean_ok) advance_state_lean<P>(st, in);
-        else advance_state<P>(st, in, 0u);
+        if (lean_ok) {  // State::advance: the players' lean steps side by side, constants in VGPRs
+          uint32_t v[P][5], pin[P];
+#pragma unroll
+          for (int k = 0; k < P; k++) {
+            v[k][0] = st.w[fld_x(P, k)];
+            v[k][1] = st.w[fld_y(P, k)];
+            v[k][2] = st.w[fld_vx(P, k)];
+            v[k][3] = st.w[fld_vy(P, k)];
+            v[k][4] = st.w[fld_rot(P, k)];
+            pin[k] = (in >> (8 * k)) & 0xffu;
+          }
+          advance_players_lean<P>(v, pin, K);
+          st.w[0] = (uint32_t)((int32_t)st.w[0] + 1);
+#pragma unroll
+          for (int k = 0; k < P; k++) {
+            st.w[fld_x(P, k)] = v[k][0];
+            st.w[fld_y(P, k)] = v[k][1];
+            st.w[fld_vx(P, k)] = v[k][2];
+            st.w[fld_vy(P, k)] = v[k][3];
+            st.w[fld_rot(P, k)] = v[k][4];
+          }
+        } else {
+          advance_state<P>(st, in, 0u);
+        }
       }
       if (replaying) {
         ++h;
@@ -464,7 +511,7 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
   if (!live) return;
   for (int q = 0; q < R; q++) {  // the cells' frames
     int32_t fr = kNull;
-    if (p.sparse) {
+    if (kSparse) {
       fr = ltag[q * kBlock + lt];
     } else if (last_saved != kNull) {  // the newest frame <= the last save in slot q
       const int32_t d = (last_saved - q) % R;
@@ -599,11 +646,19 @@ int p2p_sched_advance(ggrs_p2p_engine* e, int32_t n) {
   hipError_t attr = hipSuccess;
   dispatch_players(P, [&](auto PC) {
     constexpr int PP = decltype(PC)::value;
-    if (shm > 64 * 1024)
-      attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&p2p_sched_kernel<PP>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    if (attr == hipSuccess)
-      p2p_sched_kernel<PP><<<(unsigned)grid_of(p.S, kBlock), kBlock, shm, e->stream>>>(p);
+    auto go = [&](auto kern) {
+      if (shm > 64 * 1024)
+        attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)shm);
+      if (attr == hipSuccess) kern<<<(unsigned)grid_of(p.S, kBlock), kBlock, shm, e->stream>>>(p);
+    };
+    if (p.sparse) {
+      if (p.predictor == 0) go(&p2p_sched_kernel<PP, true, 0>);
+      else go(&p2p_sched_kernel<PP, true, 1>);
+    } else {
+      if (p.predictor == 0) go(&p2p_sched_kernel<PP, false, 0>);
+      else go(&p2p_sched_kernel<PP, false, 1>);
+    }
   });
   HIP_TRY(attr);
   HIP_TRY(hipGetLastError());
