@@ -720,7 +720,6 @@ def run_codec(args):
     dev = torch.device("cuda", local_rank)
     d_ref, d_pend, d_cnt = (torch.from_numpy(x).to(dev) for x in (ref, pend, count))
     stride = codec.max_packet_bytes(B, W)
-    codec.set_kernels(args.codec_kernels)
     chunked = args.codec_layout == "chunked"  # each 256-packet block's packets back to back
     dec_buf = torch.empty((N, W, B), dtype=torch.uint8, device=dev)  # decoded inputs, reused per step
     evs = []
@@ -1303,8 +1302,6 @@ def main():
     ap.add_argument("--max-prediction", type=int, default=8, help="p2p: max_prediction (builder.rs:130-147)")
     ap.add_argument("--req-form", choices=["native", "p2p", "batch", "lanes", "lockstep"], default="native",
                     help="requests: the boundary form (run_requests docstring)")
-    ap.add_argument("--codec-kernels", choices=["default", "staged", "reg1"], default="default",
-                    help="codec: kernel form (ggrs_amd.codec.set_kernels; comparison)")
     ap.add_argument("--codec-layout", choices=["chunked", "strided"], default="chunked",
                     help="codec: packet layout (chunked: each 256-packet block's packets back to back)")
     ap.add_argument("--req-groups", type=int, default=2,

@@ -106,7 +106,7 @@ def chunk_offsets(lengths, stride):
     return out
 
 
-KERNEL_FORMS = {"default": 0, "direct": 1, "staged": 2, "reg1": 3}
+KERNEL_FORMS = {"default": 0, "direct": 1, "staged": 2}
 
 
 def set_direct(on):
@@ -115,10 +115,8 @@ def set_direct(on):
 
 
 def set_kernels(form):
-    """Kernel form for later calls: "default" (run-level forms where W*B <= 64: the chunked decode
-    parses four packets per lane from registers, one wave per 256-packet block), "direct" or
-    "staged" (thread-per-packet forms; "staged" also selects the LDS-row chunked decode), "reg1"
-    (the register chunked decode with one packet per thread)."""
+    """Kernel form for later calls: "default" (lane-cooperative where W*B <= 64, else LDS-staged),
+    "direct" or "staged" (thread-per-packet forms)."""
     L = _lib.lib()
     _bind(L)
     _lib.check(L.ggrs_codec_set_direct(KERNEL_FORMS[form]))

@@ -864,10 +864,6 @@ __device__ inline void fill_ff(uint32_t (&x)[NDW], int a, int n) {
 }
 
 template <int B, int NDW>
-__device__ inline void decode_reg_one(const DecodeParams& p, int64_t pk, int64_t len, uint32_t rw, const uint32_t (&w)[8],
-                                      const uint8_t* d, int W, int WB, int stride);
-
-template <int B, int NDW>
 __global__ __launch_bounds__(256) void decode_reg_kernel(DecodeParams p) {
   const int T = blockDim.x, W = p.W, WB = W * B, stride = p.stride;
   const int64_t pk0 = (int64_t)blockIdx.x * T;
@@ -894,13 +890,6 @@ __global__ __launch_bounds__(256) void decode_reg_kernel(DecodeParams p) {
 #pragma unroll
     for (int k = 0; k < 8; k++) w[k] = 4 * k < cb ? d32[k] : 0u;
   }
-  decode_reg_one<B, NDW>(p, pk, len, rw, w, d, W, WB, stride);
-}
-
-// one packet: len, reference rw, its first 32 bytes w, its bytes d in global memory
-template <int B, int NDW>
-__device__ inline void decode_reg_one(const DecodeParams& p, int64_t pk, int64_t len, uint32_t rw, const uint32_t (&w)[8],
-                                      const uint8_t* d, int W, int WB, int stride) {
   constexpr int kCap = 4 * NDW;  // stream bytes kept: any valid packet expands to <= W * B of them
   uint32_t x[NDW];
 #pragma unroll
@@ -1010,76 +999,8 @@ __device__ inline void decode_reg_one(const DecodeParams& p, int64_t pk, int64_t
   p.status[pk] = status;
 }
 
-// The register form, one wave per 256-packet block: lane l decodes packets l, l + 64, l + 128 and
-// l + 192 of the block.  Every global load of the four packets (lengths, references, then the
-// packets' dwords) is issued before the first is used, the block's chunk offsets come from one
-// wave-level scan (no barrier), and the four parses are independent chains the scheduler
-// interleaves.
-constexpr int kRegPk = 4;  // packets per lane
-template <int B, int NDW>
-__global__ __launch_bounds__(64) void decode_reg4_kernel(DecodeParams p) {
-  const int W = p.W, WB = W * B, stride = p.stride;
-  const int64_t pk0 = (int64_t)blockIdx.x * 256;
-  const int np = (int)((p.N - pk0) < 256 ? (p.N - pk0) : 256);
-  const int t = threadIdx.x;
-  int64_t len[kRegPk];
-  uint32_t rw[kRegPk];
-#pragma unroll
-  for (int j = 0; j < kRegPk; j++) {
-    const int i = t + 64 * j;
-    len[j] = i < np ? p.len[pk0 + i] : 0;
-    rw[j] = 0;
-    if (i < np) {
-      const uint8_t* rp = p.ref + (pk0 + i) * B;
-#pragma unroll
-      for (int b = 0; b < B; b++) rw[j] |= (uint32_t)rp[b] << (8 * b);
-    }
-  }
-  // chunk offsets: packet i of the block starts at the sum of the padded lengths before it; the
-  // block's packets are in order l + 64 j, so offset(l + 64 j) = (rows j' < j) + (lanes < l in row j)
-  int off[kRegPk];
-  {
-    int rowbase = 0;
-#pragma unroll
-    for (int j = 0; j < kRegPk; j++) {
-      const int cb = (t + 64 * j) < np ? chunk_bytes(len[j], stride) : 0;
-      int x = cb;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int y = __shfl_up(x, d, 64);
-        if (t >= d) x += y;
-      }
-      off[j] = rowbase + x - cb;
-      rowbase += __shfl(x, 63, 64);
-    }
-  }
-  uint32_t w[kRegPk][8];
-#pragma unroll
-  for (int j = 0; j < kRegPk; j++) {
-    const int cb = (t + 64 * j) < np ? chunk_bytes(len[j], stride) : 0;
-    const uint32_t* d32 = reinterpret_cast<const uint32_t*>(p.packets + pk0 * stride + off[j]);
-#pragma unroll
-    for (int k = 0; k < 8; k++) w[j][k] = 4 * k < cb ? d32[k] : 0u;
-  }
-#pragma unroll
-  for (int j = 0; j < kRegPk; j++) {
-    const int i = t + 64 * j;
-    if (i < np) decode_reg_one<B, NDW>(p, pk0 + i, len[j], rw[j], w[j], p.packets + pk0 * stride + off[j], W, WB, stride);
-  }
-}
-
 template <int B>
-void launch_decode_reg(int ndw, int64_t grid, hipStream_t s, const DecodeParams& p, bool four) {
-  if (four) {  // one wave per 256-packet block
-    switch (ndw) {
-      case 1: decode_reg4_kernel<B, 1><<<grid, 64, 0, s>>>(p); break;
-      case 2: decode_reg4_kernel<B, 2><<<grid, 64, 0, s>>>(p); break;
-      case 4: decode_reg4_kernel<B, 4><<<grid, 64, 0, s>>>(p); break;
-      case 8: decode_reg4_kernel<B, 8><<<grid, 64, 0, s>>>(p); break;
-      default: decode_reg4_kernel<B, 16><<<grid, 64, 0, s>>>(p); break;
-    }
-    return;
-  }
+void launch_decode_reg(int ndw, int64_t grid, hipStream_t s, const DecodeParams& p) {
   switch (ndw) {
     case 1: decode_reg_kernel<B, 1><<<grid, 256, 0, s>>>(p); break;
     case 2: decode_reg_kernel<B, 2><<<grid, 256, 0, s>>>(p); break;
@@ -1232,16 +1153,15 @@ int ggrs_codec_decode_chunked(const uint8_t* ref, const uint8_t* packets, const 
   const int ndw = swar_ndw(input_bytes, max_inputs, packet_stride);
   const size_t lds = ndw ? decode_swar_bytes(ndw, input_bytes, max_inputs, packet_stride) : 0;
   // (the register form needs no LDS; the LDS-row form of mode 2 its rows within the budget)
-  if (!ndw || !aligned4(packets) || !aligned4(out) || ((g_codec_mode == 1 || g_codec_mode == 2) && lds > kLdsBudget))
+  if (!ndw || !aligned4(packets) || !aligned4(out) || (g_codec_mode != 0 && lds > kLdsBudget))
     return set_error(GGRS_E_INVALID, "codec: the chunked layout needs 1-, 2- or 4-byte inputs, W * B <= 64 and "
                                      "multiple of 4, a stride multiple of 4 and dword-aligned buffers");
   DecodeParams p{ref, packets, packet_len, out, count, status, n_packets, input_bytes, max_inputs, packet_stride};
-  if (g_codec_mode == 0 || g_codec_mode == 3) {  // the register forms (mode 2: the LDS-row form)
+  if (g_codec_mode == 0) {  // the register form (mode 2: the LDS-row form, for comparison)
     const hipStream_t s = (hipStream_t)stream;
-    const bool four = g_codec_mode == 0;
-    if (input_bytes == 1) launch_decode_reg<1>(ndw, grid_of(n_packets, 256), s, p, four);
-    else if (input_bytes == 2) launch_decode_reg<2>(ndw, grid_of(n_packets, 256), s, p, four);
-    else launch_decode_reg<4>(ndw, grid_of(n_packets, 256), s, p, four);
+    if (input_bytes == 1) launch_decode_reg<1>(ndw, grid_of(n_packets, 256), s, p);
+    else if (input_bytes == 2) launch_decode_reg<2>(ndw, grid_of(n_packets, 256), s, p);
+    else launch_decode_reg<4>(ndw, grid_of(n_packets, 256), s, p);
   } else {
     decode_swar_any<true>(input_bytes, ndw, grid_of(n_packets, 256), lds, (hipStream_t)stream, p);
   }
@@ -1259,8 +1179,7 @@ int32_t ggrs_codec_max_packet_bytes(int32_t input_bytes, int32_t max_inputs) {
 }
 
 int ggrs_codec_set_direct(int32_t mode) {
-  if (mode < 0 || mode > 3)
-    return set_error(GGRS_E_INVALID, "codec mode %d (0 default, 1 direct, 2 staged, 3 one packet per thread)", mode);
+  if (mode < 0 || mode > 2) return set_error(GGRS_E_INVALID, "codec mode %d (0 default, 1 direct, 2 staged)", mode);
   g_codec_mode = mode;
   return GGRS_OK;
 }
