@@ -1152,8 +1152,7 @@ int ggrs_codec_decode_chunked(const uint8_t* ref, const uint8_t* packets, const 
   if (!ref || !packets || !packet_len || !out || !count || !status) return set_error(GGRS_E_INVALID, "null argument");
   const int ndw = swar_ndw(input_bytes, max_inputs, packet_stride);
   const size_t lds = ndw ? decode_swar_bytes(ndw, input_bytes, max_inputs, packet_stride) : 0;
-  // (the register form needs no LDS; the LDS-row form of mode 2 its rows within the budget)
-  if (!ndw || !aligned4(packets) || !aligned4(out) || (g_codec_mode != 0 && lds > kLdsBudget))
+  if (!ndw || !aligned4(packets) || !aligned4(out) || lds > kLdsBudget)
     return set_error(GGRS_E_INVALID, "codec: the chunked layout needs 1-, 2- or 4-byte inputs, W * B <= 64 and "
                                      "multiple of 4, a stride multiple of 4 and dword-aligned buffers");
   DecodeParams p{ref, packets, packet_len, out, count, status, n_packets, input_bytes, max_inputs, packet_stride};
