@@ -825,191 +825,6 @@ __global__ __launch_bounds__(256) void decode_swar_kernel(DecodeParams p) {
   lds_to_block(p.out + pk0 * (int64_t)WB, l_out, out_pitch, np, WB);
 }
 
-// ------------------------------------------------------------------------------------------
-// Register form of the chunked decode (the default for ggrs_codec_decode_chunked): no LDS rows.
-// Each thread loads its packet's first 32 bytes straight into eight registers -- the block's
-// packets are back to back, so a wave's loads cover one contiguous stretch -- and parses the
-// bincode framing and the bitfield-rle runs out of those registers (a byte at a data-dependent
-// position is a three-level select, not a dependent LDS read); the XOR-delta stream is built in
-// NDW registers by byte / 0xFF-range inserts, prefix-XORed as in decode_swar_kernel, and stored
-// as whole output rows.  Packets the register path does not cover (longer than 32 bytes, a tag
-// other than None, a length outside [1, stride]) take the general checks (validate_packet, the
-// same order as decode_kernel) on the packet in global memory.  Same results, status codes and
-// whole-row writes as decode_swar_kernel.
-__device__ inline uint32_t sel8(const uint32_t (&w)[8], uint32_t i) {  // w[i & 7]
-  const uint32_t a = (i & 1) ? w[1] : w[0], b = (i & 1) ? w[3] : w[2];
-  const uint32_t c = (i & 1) ? w[5] : w[4], d = (i & 1) ? w[7] : w[6];
-  const uint32_t e = (i & 2) ? b : a, f = (i & 2) ? d : c;
-  return (i & 4) ? f : e;
-}
-__device__ inline uint32_t byte_at32(const uint32_t (&w)[8], uint32_t i) {  // byte i < 32
-  return (sel8(w, i >> 2) >> (8 * (i & 3))) & 0xffu;
-}
-// byte v at position i of the NDW-dword stream x (positions past it are dropped)
-template <int NDW>
-__device__ inline void insert_byte(uint32_t (&x)[NDW], uint32_t i, uint32_t v) {
-  const uint32_t j = i >> 2, sh = 8 * (i & 3);
-#pragma unroll
-  for (int k = 0; k < NDW; k++) x[k] |= (j == (uint32_t)k) ? v << sh : 0u;
-}
-// bytes [a, a + n) of the stream set to 0xFF (clipped to its 4 * NDW bytes)
-template <int NDW>
-__device__ inline void fill_ff(uint32_t (&x)[NDW], int a, int n) {
-  const int e = a + n;
-#pragma unroll
-  for (int k = 0; k < NDW; k++) {
-    const int lo = max(a - 4 * k, 0), hi = min(e - 4 * k, 4);  // the dword's byte range [lo, hi)
-    if (hi > lo) x[k] |= (hi >= 4 ? 0xFFFFFFFFu : (1u << (8 * hi)) - 1u) & ~((1u << (8 * lo)) - 1u);
-  }
-}
-
-template <int B, int NDW>
-__global__ __launch_bounds__(256) void decode_reg_kernel(DecodeParams p) {
-  const int T = blockDim.x, W = p.W, WB = W * B, stride = p.stride;
-  const int64_t pk0 = (int64_t)blockIdx.x * T;
-  const int np = (int)((p.N - pk0) < T ? (p.N - pk0) : T);
-  const int t = threadIdx.x;
-  const int64_t pk = pk0 + t;
-  int64_t len = 0;
-  uint32_t rw = 0;
-  if (t < np) {
-    len = p.len[pk];
-    const uint8_t* rp = p.ref + pk * B;  // (byte loads: the caller's pointer may be unaligned)
-#pragma unroll
-    for (int b = 0; b < B; b++) rw |= (uint32_t)rp[b] << (8 * b);
-  }
-  __shared__ int wsum[4];
-  int total;
-  const int cb = t < np ? chunk_bytes(len, stride) : 0;
-  const int d_off = block_excl_scan(cb, wsum, &total);
-  if (t >= np) return;
-  const uint8_t* d = p.packets + pk0 * stride + d_off;  // the packet's bytes (dword aligned)
-  uint32_t w[8];
-  {
-    const uint32_t* d32 = reinterpret_cast<const uint32_t*>(d);
-#pragma unroll
-    for (int k = 0; k < 8; k++) w[k] = 4 * k < cb ? d32[k] : 0u;
-  }
-  constexpr int kCap = 4 * NDW;  // stream bytes kept: any valid packet expands to <= W * B of them
-  uint32_t x[NDW];
-#pragma unroll
-  for (int k = 0; k < NDW; k++) x[k] = 0;  // 0x00 runs need no writes
-  int64_t cnt = 0;
-  int32_t status = GGRS_CODEC_OK;
-  if (len >= 1 && len <= stride && len <= 32 && (w[0] & 0xffu) == 0) {
-    // input_sizes = None: the checks of decode_kernel in the same order, the runs expanded during
-    // the measuring pass, every byte from the registers
-    if (len - 1 < 8) {
-      status = GGRS_CODEC_E_BINCODE;
-    } else {
-      const uint64_t m = (uint64_t)alignbyte(w[1], w[0], 1) | (uint64_t)alignbyte(w[2], w[1], 1) << 32;
-      if (m > (uint64_t)(len - 9)) {
-        status = GGRS_CODEC_E_BINCODE;
-      } else {
-        const int mm = (int)m;  // <= 23
-        int xl = 0;             // < 2^24 (kMaxDecoded) while the runs stay in bounds
-        for (int q = 0; q < mm;) {
-          // get_varint over the stream's bytes 9 + q ..
-          uint64_t h = 0;
-          bool ok = false;
-          for (int shift = 0; shift < 64; shift += 7) {
-            if (q >= mm) break;
-            const uint32_t b = byte_at32(w, 9 + q);
-            ++q;
-            h |= (uint64_t)(b & 0x7fu) << shift;
-            if (!(b & 0x80u)) {
-              ok = true;
-              break;
-            }
-          }
-          if (!ok) { status = GGRS_CODEC_E_RLE; break; }
-          const uint64_t rl = (h & 1) ? h >> 2 : h >> 1;
-          if (rl > (uint64_t)kMaxDecoded || (uint64_t)xl + rl > (uint64_t)kMaxDecoded) { status = GGRS_CODEC_E_RLE; break; }
-          const bool fits = xl + (int64_t)rl <= kCap;
-          if (!(h & 1)) {
-            if ((uint64_t)(mm - q) < rl) { status = GGRS_CODEC_E_RLE; break; }
-            if (fits)
-              for (int k = 0; k < (int)rl; k++) insert_byte<NDW>(x, (uint32_t)(xl + k), byte_at32(w, 9 + q + k));
-            q += (int)rl;
-          } else if ((h & 2) && fits) {
-            fill_ff<NDW>(x, xl, (int)rl);
-          }
-          xl += (int)rl;
-        }
-        if (status == GGRS_CODEC_OK) {
-          cnt = xl / B;
-          if (cnt * B != xl) status = GGRS_CODEC_E_DELTA;
-          else if (cnt > W) status = GGRS_CODEC_E_CAP;
-        }
-      }
-    }
-  } else {
-    // the general checks on the packet in global memory, then the runs expanded from there
-    int64_t rle_at = 0;
-    uint64_t m = 0;
-    status = validate_packet(d, len, stride, B, W, &cnt, &m, &rle_at);
-    if (status == GGRS_CODEC_OK) {
-      const uint8_t* rle = d + rle_at;
-      int at = 0;
-      for (int64_t q = 0; q < (int64_t)m;) {
-        uint64_t h;
-        get_varint(rle, (int64_t)m, q, h);
-        const int rl = (int)((h & 1) ? h >> 2 : h >> 1);
-        if (h & 1) {
-          if (h & 2) fill_ff<NDW>(x, at, rl);
-        } else {
-          for (int k = 0; k < rl; k++) insert_byte<NDW>(x, (uint32_t)(at + k), rle[q + k]);
-          q += rl;
-        }
-        at += rl;
-      }
-    }
-  }
-  uint32_t* orow = reinterpret_cast<uint32_t*>(p.out + pk * (int64_t)WB);
-  if (status == GGRS_CODEC_OK) {
-    const int xl = (int)cnt * B;
-    const uint32_t refpat = B == 1 ? rw * 0x01010101u : (B == 2 ? rw * 0x00010001u : rw);
-    uint32_t carry = 0;  // the previous dword's last input, repeated
-    uint32_t o[NDW];
-#pragma unroll
-    for (int k = 0; k < NDW; k++) {
-      const int live_bytes = xl - 4 * k;
-      const uint32_t keep = live_bytes >= 4 ? 0xFFFFFFFFu : (live_bytes <= 0 ? 0u : (1u << (8 * live_bytes)) - 1u);
-      uint32_t y = x[k] & keep;
-      if constexpr (B == 1) {
-        y ^= y << 8;
-        y ^= y << 16;
-      } else if constexpr (B == 2) {
-        y ^= y << 16;
-      }
-      y ^= carry;
-      carry = B == 1 ? (y >> 24) * 0x01010101u : (B == 2 ? (y >> 16) * 0x00010001u : y);
-      o[k] = (y ^ refpat) & keep;
-    }
-#pragma unroll
-    for (int k = 0; k < NDW; k++)
-      if (4 * k < WB) orow[k] = o[k];
-    p.count[pk] = (int32_t)cnt;
-  } else {
-#pragma unroll
-    for (int k = 0; k < NDW; k++)
-      if (4 * k < WB) orow[k] = 0;
-    p.count[pk] = 0;
-  }
-  p.status[pk] = status;
-}
-
-template <int B>
-void launch_decode_reg(int ndw, int64_t grid, hipStream_t s, const DecodeParams& p) {
-  switch (ndw) {
-    case 1: decode_reg_kernel<B, 1><<<grid, 256, 0, s>>>(p); break;
-    case 2: decode_reg_kernel<B, 2><<<grid, 256, 0, s>>>(p); break;
-    case 4: decode_reg_kernel<B, 4><<<grid, 256, 0, s>>>(p); break;
-    case 8: decode_reg_kernel<B, 8><<<grid, 256, 0, s>>>(p); break;
-    default: decode_reg_kernel<B, 16><<<grid, 256, 0, s>>>(p); break;
-  }
-}
-
 size_t encode_swar_bytes(int ndw, int stride, bool chunked = false) {
   return (size_t)256 * (swar_out_pitch(stride, ndw) + odd_dword_pitch(4 * ndw) + (chunked ? stride : 0));
 }
@@ -1156,14 +971,7 @@ int ggrs_codec_decode_chunked(const uint8_t* ref, const uint8_t* packets, const 
     return set_error(GGRS_E_INVALID, "codec: the chunked layout needs 1-, 2- or 4-byte inputs, W * B <= 64 and "
                                      "multiple of 4, a stride multiple of 4 and dword-aligned buffers");
   DecodeParams p{ref, packets, packet_len, out, count, status, n_packets, input_bytes, max_inputs, packet_stride};
-  if (g_codec_mode == 0) {  // the register form (mode 2: the LDS-row form, for comparison)
-    const hipStream_t s = (hipStream_t)stream;
-    if (input_bytes == 1) launch_decode_reg<1>(ndw, grid_of(n_packets, 256), s, p);
-    else if (input_bytes == 2) launch_decode_reg<2>(ndw, grid_of(n_packets, 256), s, p);
-    else launch_decode_reg<4>(ndw, grid_of(n_packets, 256), s, p);
-  } else {
-    decode_swar_any<true>(input_bytes, ndw, grid_of(n_packets, 256), lds, (hipStream_t)stream, p);
-  }
+  decode_swar_any<true>(input_bytes, ndw, grid_of(n_packets, 256), lds, (hipStream_t)stream, p);
   HIP_TRY(hipGetLastError());
   return GGRS_OK;
 }
