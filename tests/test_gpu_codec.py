@@ -188,19 +188,36 @@ def test_chunked_layout_matches_oracle(oracle, N, W, B, held):
         assert (dec[p, :count[p]] == pend[p, :count[p]]).all(), p
 
 
-def test_chunked_decode_hostile_lengths_match_strided(oracle):
+@pytest.mark.parametrize("mode", ["mutated", "random", "truncated"])
+@pytest.mark.parametrize("W,B", [(16, 2), (8, 1), (16, 4)])
+def test_chunked_decode_hostile_lengths_match_strided(oracle, mode, W, B):
     """Lengths outside [1, stride] take no bytes in the chunked layout and give the strided decode's
-    error codes; mutated packets at their chunk offsets decode as the strided form of the same bytes."""
+    error codes; hostile packets at their chunk offsets -- mutated bytes, random runs inside valid
+    bincode framing, packets cut short -- decode as the strided form of the same bytes (the chunked
+    decode stages the block's packets in LDS from their packed offsets, the strided one whole rows)."""
     from ggrs_amd import codec
-    rng = np.random.default_rng(77)
-    N, W, B = 3000, 16, 2
+    rng = np.random.default_rng(77 + W + B + {"mutated": 0, "random": 1000, "truncated": 2000}[mode])
+    N = 3000
     ref, pend, count = batch(rng, N, W, B)
     out, ln = codec.encode(gpu(ref), gpu(pend), gpu(count))  # strided
     pk, lh = out.cpu().numpy().copy(), ln.cpu().numpy().copy()
     stride = pk.shape[1]
-    for p in range(N):
-        if rng.random() < 0.3:
-            pk[p, int(rng.integers(0, max(lh[p], 1)))] = rng.integers(0, 256)
+    if mode == "mutated":
+        for p in range(N):
+            if rng.random() < 0.3:
+                pk[p, int(rng.integers(0, max(lh[p], 1)))] = rng.integers(0, 256)
+    elif mode == "random":
+        pk[:] = rng.integers(0, 256, pk.shape, dtype=np.uint8)
+        pk[:, 9:][rng.random((N, stride - 9)) < 0.5] &= 0x7F  # short varints: runs that parse
+        lh = rng.integers(1, stride + 1, N).astype(np.int32)
+        framed = (rng.random(N) < 0.8) & (lh >= 9)
+        pk[framed, 0] = 0
+        for p in np.nonzero(framed)[0]:
+            pk[p, 1:9] = np.frombuffer(int(lh[p] - 9).to_bytes(8, "little"), np.uint8)
+    else:
+        lh = (lh * rng.random(N)).astype(np.int32)
+        for p in np.nonzero(lh >= 9)[0]:
+            pk[p, 1:9] = np.frombuffer(int(lh[p] - 9).to_bytes(8, "little"), np.uint8)
     bad = rng.random(N) < 0.1
     lh[bad] = rng.choice([-5, 0, stride + 4, 10 ** 6], int(bad.sum())).astype(np.int32)
     # the same packets in the chunked layout
