@@ -1221,8 +1221,9 @@ def run_requests(args):
                        "session_us_per_group_call":
                            args.session_us, "lane_server": not args.no_lane_server,
                        "us_per_call": round(elapsed / n_calls * 1e6, 2),
-                       **({"us_per_call_host_encode_device_handback_session": [round(x / n_calls * 1e6, 2)
-                                                                              for x in phases]}
+                       **({("us_per_call_encode_handback_submit_wait_session" if form == "p2p" else
+                            "us_per_call_host_encode_device_handback_session"): [round(x / n_calls * 1e6, 2)
+                                                                                 for x in phases]}
                           if drv is not None else {}),
                        "parallelism": f"sessions sharded over {world} GPU(s)"},
             "dist": dist_info(dist, per_rank),
@@ -1332,6 +1333,9 @@ def main():
     if args.workload == "codec":
         return run_codec(args)
     if args.workload == "requests":
+        # the host handler's worker threads meet at barriers twice per lane group and call: spin
+        # there (before torch loads libgomp, which reads this once)
+        os.environ.setdefault("OMP_WAIT_POLICY", "active")
         return run_requests(args)
     if args.config == 5:
         return run_particles(args)

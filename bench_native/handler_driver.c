@@ -23,6 +23,7 @@
 #include <time.h>
 
 #include "ggrs_amd.h"
+#include <omp.h>
 
 /* the rejection message of a failed encode on an OpenMP worker: ggrs_last_error() is thread-local
  * in the engine, so the worker's message is copied here for the calling thread (handler_last_error) */
@@ -271,81 +272,96 @@ int handler_drive_p2p_groups(ggrs_engine_t** engs, int32_t G, int32_t L, int32_t
     g[q].base = q * Lg;
     g[q].lanes = Lg;
   }
-  double t_enc = 0, t_dev = 0, t_back = 0, t_sess = 0;
+  /* phases (the master thread's clock): encode + hand-back of a group's lanes (the threads' shares
+   * between two barriers), submit, wait, session logic; the barriers themselves are in the first */
+  double t_work = 0, t_submit = 0, t_wait = 0, t_sess = 0;
   uint64_t acc = 0;
   int32_t prev_call[MAX_GROUPS];
+  int err = 0;
   const double t0 = now_s();
-  for (int32_t c = c_begin; c <= c_begin + n_calls; c++) {
-    for (int q = 0; q < G; q++) {
-      group_t* gq = &g[q];
-      if (gq->pending) {
-        const double ta = now_s();
-        int32_t failed = 0;
-        int rc = ggrs_lane_batch_wait(engs[q], &failed);
-        if (rc) return rc;
-        const double tb = now_s();
-        const int32_t pc = prev_call[q];
-        uint64_t part = 0;
-#pragma omp parallel for num_threads(threads) schedule(static) reduction(+ : part) if (threads > 1)
-        for (int32_t l = 0; l < Lg; l++) { /* every Save's checksum of the lane's list */
-          const int32_t lane = gq->base + l, m = lane % M;
-          const int64_t a = req_off[(int64_t)m * (C + 1) + pc], b = req_off[(int64_t)m * (C + 1) + pc + 1];
-          int si = 0;
-          for (int64_t k = a; k < b; k++)
-            if (reqs[k].kind == GGRS_REQ_SAVE) part += gq->b.checksums[(size_t)si++ * Lg + l];
-          lane_frames[lane] = gq->b.lane_result[l];
+  /* One parallel region for the whole run: the threads persist across calls and meet at barriers
+   * (a fork/join per group and call cost more than the encoding itself).  Per
+   * call and group: the master collects the group's previous batch, every thread hands back the
+   * checksums of its share of the lanes and encodes their next lists (one pass over each lane),
+   * the master submits. */
+#pragma omp parallel num_threads(threads) reduction(+ : acc) if (threads > 1)
+  {
+    const int tid = omp_get_thread_num(), nt = omp_get_num_threads();
+    for (int32_t c = c_begin; c <= c_begin + n_calls; c++) {
+      for (int q = 0; q < G; q++) {
+        group_t* gq = &g[q];
+#pragma omp master
+        {
+          if (gq->pending && !err) {
+            const double ta = now_s();
+            int32_t failed = 0;
+            int rc = ggrs_lane_batch_wait(engs[q], &failed);
+            if (rc) err = rc;
+            t_wait += now_s() - ta;
+            if (!deferred) spin_us(session_us); /* the session logic after the checksums are back */
+          }
         }
-        acc += part;
-        const double tc = now_s();
-        if (!deferred) spin_us(session_us); /* the session logic after the call returned its checksums */
-        t_dev += tb - ta;
-        t_back += tc - tb;
-        t_sess += now_s() - tc;
-        gq->pending = 0;
-      }
-      if (c == c_begin + n_calls) continue;
-      const double ta = now_s();
-      int enc_rc = 0;
-#pragma omp parallel for num_threads(threads) schedule(static) if (threads > 1)
-      for (int32_t l = 0; l < Lg; l++) {
-        const int32_t lane = gq->base + l, m = lane % M;
-        const int64_t a = req_off[(int64_t)m * (C + 1) + c], b = req_off[(int64_t)m * (C + 1) + c + 1];
-        const int64_t ad = adv_off[(int64_t)m * (C + 1) + c];
-        int32_t bad = -1;
-        int rc = ggrs_lane_encode(&gq->b, Lg, P, l, reqs + a, (int32_t)(b - a), inputs + ad * P, status + ad * P,
-                                  lane_frames[lane], &bad);
-        if (rc) {
+#pragma omp barrier
+        const double tw = now_s();
+        const int32_t l0 = (int32_t)((int64_t)Lg * tid / nt), l1 = (int32_t)((int64_t)Lg * (tid + 1) / nt);
+        const int handback = gq->pending && !err, encode = c < c_begin + n_calls && !err;
+        const int32_t pc = prev_call[q];
+        for (int32_t l = l0; l < l1; l++) {
+          const int32_t lane = gq->base + l, m = lane % M;
+          if (handback) { /* every Save's checksum of the lane's previous list */
+            const int64_t a = req_off[(int64_t)m * (C + 1) + pc], b = req_off[(int64_t)m * (C + 1) + pc + 1];
+            int si = 0;
+            for (int64_t k = a; k < b; k++)
+              if (reqs[k].kind == GGRS_REQ_SAVE) acc += gq->b.checksums[(size_t)si++ * Lg + l];
+            lane_frames[lane] = gq->b.lane_result[l];
+          }
+          if (encode) {
+            const int64_t a = req_off[(int64_t)m * (C + 1) + c], b = req_off[(int64_t)m * (C + 1) + c + 1];
+            const int64_t ad = adv_off[(int64_t)m * (C + 1) + c];
+            int32_t bad = -1;
+            int rc = ggrs_lane_encode(&gq->b, Lg, P, l, reqs + a, (int32_t)(b - a), inputs + ad * P, status + ad * P,
+                                      lane_frames[lane], &bad);
+            if (rc) {
 #pragma omp critical
-          { /* the fixture's lists are valid: any rejection is an error here */
-            if (!enc_rc) {
-              strncpy(g_drv_error, ggrs_last_error(), sizeof g_drv_error - 1);
-              g_drv_error[sizeof g_drv_error - 1] = 0;
+              { /* the fixture's lists are valid: any rejection is an error here */
+                if (!err) {
+                  strncpy(g_drv_error, ggrs_last_error(), sizeof g_drv_error - 1);
+                  g_drv_error[sizeof g_drv_error - 1] = 0;
+                  err = rc;
+                }
+              }
             }
-            enc_rc = rc;
+          }
+        }
+#pragma omp barrier
+#pragma omp master
+        {
+          t_work += now_s() - tw;
+          gq->pending = 0;
+          if (encode && !err) {
+            gq->run = gq->b;
+            const double tb = now_s();
+            int rc = ggrs_lane_batch_submit(engs[q], &gq->run, GGRS_BATCH_STATUS);
+            if (rc) err = rc;
+            gq->pending = rc == 0;
+            prev_call[q] = c;
+            t_submit += now_s() - tb;
+            if (deferred) { /* the call has returned: the session logic overlaps the batch on the device */
+              const double td = now_s();
+              spin_us(session_us);
+              t_sess += now_s() - td;
+            }
           }
         }
       }
-      if (enc_rc) return enc_rc;
-      gq->run = gq->b;
-      const double tb = now_s();
-      int rc = ggrs_lane_batch_submit(engs[q], &gq->run, GGRS_BATCH_STATUS);
-      if (rc) return rc;
-      gq->pending = 1;
-      prev_call[q] = c;
-      t_enc += tb - ta;
-      t_dev += now_s() - tb;
-      if (deferred) { /* the call has returned: the session logic overlaps the batch on the device */
-        const double td = now_s();
-        spin_us(session_us);
-        t_sess += now_s() - td;
-      }
     }
   }
+  if (err) return err;
   *seconds = now_s() - t0;
-  if (phases) {
-    phases[0] = t_enc;
-    phases[1] = t_dev;
-    phases[2] = t_back;
+  if (phases) { /* encode + hand-back (barriers included), submit, wait, session logic */
+    phases[0] = t_work;
+    phases[1] = t_submit;
+    phases[2] = t_wait;
     phases[3] = t_sess;
   }
   *sink = acc;
