@@ -24,6 +24,7 @@
 
 #include "ggrs_amd.h"
 #include <omp.h>
+#include <stdatomic.h>
 
 /* the rejection message of a failed encode on an OpenMP worker: ggrs_last_error() is thread-local
  * in the engine, so the worker's message is copied here for the calling thread (handler_last_error) */
@@ -279,78 +280,84 @@ int handler_drive_p2p_groups(ggrs_engine_t** engs, int32_t G, int32_t L, int32_t
   int32_t prev_call[MAX_GROUPS];
   int err = 0;
   const double t0 = now_s();
-  /* One parallel region for the whole run: the threads persist across calls and meet at barriers
-   * (a fork/join per group and call cost more than the encoding itself).  Per
-   * call and group: the master collects the group's previous batch, every thread hands back the
-   * checksums of its share of the lanes and encodes their next lists (one pass over each lane),
-   * the master submits. */
+  /* One parallel region for the whole run: the threads persist across calls (a fork/join per group
+   * and call cost more than the encoding itself).  Step e = (call, group): the
+   * master collects the group's previous batch and releases the step (ready = e), every thread
+   * hands back the checksums of its share of the lanes and encodes their next lists (one pass over
+   * each lane) and counts itself done, the master submits once all have.  A release flag and an
+   * arrival counter instead of two full barriers per step. */
+  _Atomic int64_t ready = -1, done = 0;
+  const int64_t n_steps = (int64_t)(n_calls + 1) * G;
 #pragma omp parallel num_threads(threads) reduction(+ : acc) if (threads > 1)
   {
     const int tid = omp_get_thread_num(), nt = omp_get_num_threads();
-    for (int32_t c = c_begin; c <= c_begin + n_calls; c++) {
-      for (int q = 0; q < G; q++) {
-        group_t* gq = &g[q];
-#pragma omp master
-        {
-          if (gq->pending && !err) {
-            const double ta = now_s();
-            int32_t failed = 0;
-            int rc = ggrs_lane_batch_wait(engs[q], &failed);
-            if (rc) err = rc;
-            t_wait += now_s() - ta;
-            if (!deferred) spin_us(session_us); /* the session logic after the checksums are back */
-          }
+    for (int64_t e = 0; e < n_steps; e++) {
+      const int32_t c = c_begin + (int32_t)(e / G);
+      const int q = (int)(e % G);
+      group_t* gq = &g[q];
+      if (tid == 0) {
+        if (gq->pending && !err) {
+          const double ta = now_s();
+          int32_t failed = 0;
+          int rc = ggrs_lane_batch_wait(engs[q], &failed);
+          if (rc) err = rc;
+          t_wait += now_s() - ta;
+          if (!deferred) spin_us(session_us); /* the session logic after the checksums are back */
         }
-#pragma omp barrier
-        const double tw = now_s();
-        const int32_t l0 = (int32_t)((int64_t)Lg * tid / nt), l1 = (int32_t)((int64_t)Lg * (tid + 1) / nt);
-        const int handback = gq->pending && !err, encode = c < c_begin + n_calls && !err;
-        const int32_t pc = prev_call[q];
-        for (int32_t l = l0; l < l1; l++) {
-          const int32_t lane = gq->base + l, m = lane % M;
-          if (handback) { /* every Save's checksum of the lane's previous list */
-            const int64_t a = req_off[(int64_t)m * (C + 1) + pc], b = req_off[(int64_t)m * (C + 1) + pc + 1];
-            int si = 0;
-            for (int64_t k = a; k < b; k++)
-              if (reqs[k].kind == GGRS_REQ_SAVE) acc += gq->b.checksums[(size_t)si++ * Lg + l];
-            lane_frames[lane] = gq->b.lane_result[l];
-          }
-          if (encode) {
-            const int64_t a = req_off[(int64_t)m * (C + 1) + c], b = req_off[(int64_t)m * (C + 1) + c + 1];
-            const int64_t ad = adv_off[(int64_t)m * (C + 1) + c];
-            int32_t bad = -1;
-            int rc = ggrs_lane_encode(&gq->b, Lg, P, l, reqs + a, (int32_t)(b - a), inputs + ad * P, status + ad * P,
-                                      lane_frames[lane], &bad);
-            if (rc) {
+        atomic_store_explicit(&ready, e, memory_order_release);
+      } else {
+        while (atomic_load_explicit(&ready, memory_order_acquire) < e) __builtin_ia32_pause();
+      }
+      const double tw = now_s();
+      const int32_t l0 = (int32_t)((int64_t)Lg * tid / nt), l1 = (int32_t)((int64_t)Lg * (tid + 1) / nt);
+      const int handback = gq->pending && !err, encode = c < c_begin + n_calls && !err;
+      const int32_t pc = prev_call[q];
+      for (int32_t l = l0; l < l1; l++) {
+        const int32_t lane = gq->base + l, m = lane % M;
+        if (handback) { /* every Save's checksum of the lane's previous list */
+          const int64_t a = req_off[(int64_t)m * (C + 1) + pc], b = req_off[(int64_t)m * (C + 1) + pc + 1];
+          int si = 0;
+          for (int64_t k = a; k < b; k++)
+            if (reqs[k].kind == GGRS_REQ_SAVE) acc += gq->b.checksums[(size_t)si++ * Lg + l];
+          lane_frames[lane] = gq->b.lane_result[l];
+        }
+        if (encode) {
+          const int64_t a = req_off[(int64_t)m * (C + 1) + c], b = req_off[(int64_t)m * (C + 1) + c + 1];
+          const int64_t ad = adv_off[(int64_t)m * (C + 1) + c];
+          int32_t bad = -1;
+          int rc = ggrs_lane_encode(&gq->b, Lg, P, l, reqs + a, (int32_t)(b - a), inputs + ad * P, status + ad * P,
+                                    lane_frames[lane], &bad);
+          if (rc) {
 #pragma omp critical
-              { /* the fixture's lists are valid: any rejection is an error here */
-                if (!err) {
-                  strncpy(g_drv_error, ggrs_last_error(), sizeof g_drv_error - 1);
-                  g_drv_error[sizeof g_drv_error - 1] = 0;
-                  err = rc;
-                }
+            { /* the fixture's lists are valid: any rejection is an error here */
+              if (!err) {
+                strncpy(g_drv_error, ggrs_last_error(), sizeof g_drv_error - 1);
+                g_drv_error[sizeof g_drv_error - 1] = 0;
+                err = rc;
               }
             }
           }
         }
-#pragma omp barrier
-#pragma omp master
-        {
-          t_work += now_s() - tw;
-          gq->pending = 0;
-          if (encode && !err) {
-            gq->run = gq->b;
-            const double tb = now_s();
-            int rc = ggrs_lane_batch_submit(engs[q], &gq->run, GGRS_BATCH_STATUS);
-            if (rc) err = rc;
-            gq->pending = rc == 0;
-            prev_call[q] = c;
-            t_submit += now_s() - tb;
-            if (deferred) { /* the call has returned: the session logic overlaps the batch on the device */
-              const double td = now_s();
-              spin_us(session_us);
-              t_sess += now_s() - td;
-            }
+      }
+      if (tid != 0) {
+        atomic_fetch_add_explicit(&done, 1, memory_order_release);
+      } else {
+        const int64_t want = (e + 1) * (nt - 1);
+        while (atomic_load_explicit(&done, memory_order_acquire) < want) __builtin_ia32_pause();
+        t_work += now_s() - tw;
+        gq->pending = 0;
+        if (encode && !err) {
+          gq->run = gq->b;
+          const double tb = now_s();
+          int rc = ggrs_lane_batch_submit(engs[q], &gq->run, GGRS_BATCH_STATUS);
+          if (rc) err = rc;
+          gq->pending = rc == 0;
+          prev_call[q] = c;
+          t_submit += now_s() - tb;
+          if (deferred) { /* the call has returned: the session logic overlaps the batch on the device */
+            const double td = now_s();
+            spin_us(session_us);
+            t_sess += now_s() - td;
           }
         }
       }
