@@ -35,16 +35,12 @@ FLAGS = ["-O3", "--offload-arch=gfx950", "-ffp-contract=off", "-fPIC", "-std=c++
 # (profiles/r04o, the whole library A/B twice): the default scheduler cost config 2 3 %, the P2P
 # kernels 4-6 %, and gained config 3's pipelined prefix kernel (lane-pair trunk split,
 # write-through saves) 3 %: 25.8 -> 25.0 us per 16-round step, so branch.hip keeps the default.
-# max-ilp on every unit (profiles/r04q, r04r): codec and the request boundary unchanged, and the
-# particle unit's checksums CHANGE (its GPU parity tests fail: the ring states and checksums differ
-# from frame ~50 on), so particles.hip must stay on the default scheduler.  The failure follows
-# particles.h's two inline-asm 24-bit multiply-adds: with them written as __umul24 / __mul24 the
-# max-ilp build passes every particle test (profiles/r04v), so the product now writes them that
-# way (config 5 unchanged at 5.90e6, profiles/r04y).  The engine and P2P units, which use
-# inline asm too (fletcher_from_doubled, the sincosf quadrant select), pass all their parity tests
-# under max-ilp; their kernels are re-verified by the GPU suite on every build.  Also measured on
-# every unit (profiles/r04w): max-memory-clause, config 2 and the P2P chains 3 % slower, config 3
-# equal; iterative-ilp crashes this hipcc on particles.hip.
+# max-ilp on every unit (round 4): codec and the request boundary unchanged; the particle unit's
+# checksums changed, which round 5 traced to inline asm (DESIGN.md §3 "No inline asm": LLVM's
+# hazard recognizer does not see an asm statement as the reader of a v_dot result, so the 3 wait
+# states gfx950 needs were missing).  No unit contains instruction-emitting inline asm any more
+# (tests/test_no_inline_asm.py).  Also measured on every unit: max-memory-clause, config 2 and
+# the P2P chains 3 % slower, config 3 equal; iterative-ilp crashes this hipcc on particles.hip.
 ILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
 UNIT_FLAGS = {"engine.hip": ILP, "p2p.hip": ILP, "p2p_sched.hip": ILP}
 
