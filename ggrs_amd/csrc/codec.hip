@@ -690,10 +690,8 @@ __global__ __launch_bounds__(256) void decode_swar_kernel(DecodeParams p) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const int T = blockDim.x, W = p.W, WB = W * B, stride = p.stride;
   const int in_pitch = odd_dword_pitch(stride), x_pitch = odd_dword_pitch(4 * NDW);
-  const int out_pitch = odd_dword_pitch(WB);
   uint8_t* l_in = smem;                     // [T][in_pitch] packets
-  uint8_t* l_x = l_in + T * in_pitch;       // [T][x_pitch] expanded runs
-  uint8_t* l_out = l_x + T * x_pitch;       // [T][out_pitch] decoded inputs
+  uint8_t* l_x = l_in + T * in_pitch;       // [T][x_pitch] expanded runs, then (in place) the decoded inputs
   const int64_t pk0 = (int64_t)blockIdx.x * T;
   const int np = (int)((p.N - pk0) < T ? (p.N - pk0) : T);
   const int t = threadIdx.x;
@@ -729,6 +727,7 @@ __global__ __launch_bounds__(256) void decode_swar_kernel(DecodeParams p) {
     for (int k = 0; k < NDW; k++) xr32[k] = 0;  // 0x00 runs need no writes
     int64_t cnt = 0;
     int32_t status = GGRS_CODEC_OK;
+    uint64_t ffm = 0;  // fast path: one bit per scratch byte inside a 0xFF run
     if (len < 0 || len > stride || len < 1 || d[0] != 0) {
       // a length outside the row, or input_sizes = Some(..) (or a bad tag): the general checks
       // (validate_packet, the same order as decode_kernel), then the runs are expanded
@@ -766,22 +765,36 @@ __global__ __launch_bounds__(256) void decode_swar_kernel(DecodeParams p) {
           status = GGRS_CODEC_E_BINCODE;
         } else {
           const uint8_t* rle = d + 9;
-          int64_t xl = 0;
-          for (int64_t q = 0; q < (int64_t)m;) {
-            uint64_t h;
-            if (!get_varint(rle, (int64_t)m, q, h)) { status = GGRS_CODEC_E_RLE; break; }
-            const uint64_t rl = (h & 1) ? h >> 2 : h >> 1;
-            if (rl > (uint64_t)kMaxDecoded || (uint64_t)xl + rl > (uint64_t)kMaxDecoded) { status = GGRS_CODEC_E_RLE; break; }
-            const bool fits = xl + (int64_t)rl <= kCap;
-            if (!(h & 1)) {
-              if ((uint64_t)((int64_t)m - q) < rl) { status = GGRS_CODEC_E_RLE; break; }
-              if (fits)
-                for (int k = 0; k < (int)rl; k++) xb[xl + k] = rle[q + k];
-              q += (int64_t)rl;
-            } else if ((h & 2) && fits) {
-              for (int k = 0; k < (int)rl; k++) xb[xl + k] = 0xFF;
+          const int mm = (int)m;  // <= len - 9 < stride
+          int q = 0, xl = 0;      // xl <= kMaxDecoded
+          while (q < mm) {
+            // one-byte headers (every run of <= 31 fill / 63 literal bytes) without the varint loop
+            uint32_t h = rle[q];
+            int rl;
+            if (h < 0x80u) {
+              q++;
+              rl = (int)((h & 1) ? h >> 2 : h >> 1);
+              if (xl + rl > kMaxDecoded) { status = GGRS_CODEC_E_RLE; break; }
+            } else {
+              int64_t q64 = q;
+              uint64_t h64;
+              if (!get_varint(rle, mm, q64, h64)) { status = GGRS_CODEC_E_RLE; break; }
+              const uint64_t rl64 = (h64 & 1) ? h64 >> 2 : h64 >> 1;
+              if (rl64 > (uint64_t)kMaxDecoded || (uint64_t)xl + rl64 > (uint64_t)kMaxDecoded) { status = GGRS_CODEC_E_RLE; break; }
+              q = (int)q64;
+              h = (uint32_t)h64;
+              rl = (int)rl64;
             }
-            xl += (int64_t)rl;
+            const bool fits = xl + rl <= kCap;
+            if (!(h & 1)) {
+              if (mm - q < rl) { status = GGRS_CODEC_E_RLE; break; }
+              if (fits)
+                for (int k = 0; k < rl; k++) xb[xl + k] = rle[q + k];
+              q += rl;
+            } else if ((h & 2) && fits && rl > 0) {
+              ffm |= (rl >= 64 ? ~0ull : (1ull << rl) - 1) << xl;  // 0xFF bytes, expanded below
+            }
+            xl += rl;
           }
           if (status == GGRS_CODEC_OK) {
             cnt = xl / B;
@@ -791,7 +804,7 @@ __global__ __launch_bounds__(256) void decode_swar_kernel(DecodeParams p) {
         }
       }
     }
-    uint32_t* orow = reinterpret_cast<uint32_t*>(l_out + t * out_pitch);
+    uint32_t* orow = xr32;  // dword k of the output replaces dword k of the runs, in order
     if (status == GGRS_CODEC_OK) {
       const int xl = (int)cnt * B;
       const uint32_t refpat = B == 1 ? rw * 0x01010101u : (B == 2 ? rw * 0x00010001u : rw);
@@ -802,7 +815,8 @@ __global__ __launch_bounds__(256) void decode_swar_kernel(DecodeParams p) {
         if (4 * k >= WB) break;
         const int live_bytes = xl - 4 * k;
         const uint32_t keep = live_bytes >= 4 ? 0xFFFFFFFFu : (live_bytes <= 0 ? 0u : (1u << (8 * live_bytes)) - 1u);
-        uint32_t y = xr[k] & keep;
+        const uint32_t ffb = (uint32_t)(ffm >> (4 * k)) & 0xFu;
+        uint32_t y = (xr[k] | (((ffb * 0x00204081u) & 0x01010101u) * 0xFFu)) & keep;
         // prefix XOR of stride B inside the dword, then the carry from the dwords before
         if constexpr (B == 1) {
           y ^= y << 8;
@@ -822,14 +836,14 @@ __global__ __launch_bounds__(256) void decode_swar_kernel(DecodeParams p) {
     p.status[pk] = status;
   }
   __syncthreads();
-  lds_to_block(p.out + pk0 * (int64_t)WB, l_out, out_pitch, np, WB);
+  lds_to_block(p.out + pk0 * (int64_t)WB, l_x, x_pitch, np, WB);
 }
 
 size_t encode_swar_bytes(int ndw, int stride, bool chunked = false) {
   return (size_t)256 * (swar_out_pitch(stride, ndw) + odd_dword_pitch(4 * ndw) + (chunked ? stride : 0));
 }
 size_t decode_swar_bytes(int ndw, int B, int W, int stride) {
-  return (size_t)256 * (odd_dword_pitch(stride) + odd_dword_pitch(4 * ndw) + odd_dword_pitch(W * B));
+  return (size_t)256 * (odd_dword_pitch(stride) + odd_dword_pitch(4 * ndw));
 }
 // dwords of the run-level forms' register stream (a power of two >= W*B/4), or 0 when they do
 // not apply
