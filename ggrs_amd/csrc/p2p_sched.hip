@@ -30,6 +30,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "common.h"
@@ -71,8 +72,8 @@ struct SchedParams {
 // The block's LDS (dynamic): its 64 sessions' rings [R][PC][64] uint4 (+ frame tags [R][64] with
 // sparse saving; without it every frame 0 .. last save has been saved, so a cell's frame is the
 // newest one <= the last save in its slot), local queues [WL][64], and per stage of K calls the
-// arrival deltas + Event::Disconnected bits [K][64] u16 and the input rows [B + K][64] of frames /
-// calls [stage start - B, stage end) with their row tags.
+// calls' records [K][64] (u32, sparse saving u64) and the input rows [B + K][64] of frames / calls
+// [stage start - B, stage end) with their row tags.
 struct SchedLds {
   uint32_t o_tags, o_lq, o_arr, o_rowtag, o_rows, total;  // byte offsets (32-bit: scalar registers are scarce)
 };
@@ -84,13 +85,12 @@ __host__ __device__ inline SchedLds sched_lds(int P, int R, int sparse, int WL, 
   l.o_tags = ring;
   l.o_lq = align16(l.o_tags + (sparse ? (uint32_t)R * kBlock * 4 : 0u));
   l.o_arr = align16(l.o_lq + (uint32_t)WL * kBlock * input_word_bytes(P));
-  l.o_rowtag = align16(l.o_arr + (uint32_t)K * kBlock * 2);
+  l.o_rowtag = align16(l.o_arr + (uint32_t)K * kBlock * (sparse ? 8 : 4));  // the calls' records
   l.o_rows = align16(l.o_rowtag + (uint32_t)(K + B) * 4);
   l.total = align16(l.o_rows + (uint32_t)(K + B) * kBlock * input_word_bytes(P));
   return l;
 }
-constexpr int kArrInvalid = 0xff;  // arrival code: a frame after its call (GGRS_E_INVALID)
-constexpr int kArrTooFar = 0xfe;   // a burst of >= 254 frames: past the device queue (GGRS_E_PRECONDITION)
+constexpr int kArrTooFar = 0xfe;  // a burst of >= 254 frames: past the device queue (GGRS_E_PRECONDITION)
 
 // A pointer held in vector registers: the kernel's uniform values exceed the scalar register file
 // (102 SGPRs) and the compiler spills them to VGPR lanes, reloading each with a v_readlane at every
@@ -103,11 +103,22 @@ __device__ inline T* in_vgpr_ptr(T* ptr) {
   return reinterpret_cast<T*>(u);
 }
 
+// A call's record, written by the control pass and read by the step loop (bits):
+//   0-6 d1: replay depth of the rollback (0: none) | 7 adv: the own frame advances | 8-9 stop |
+//   10 save_own (sparse saving) | 16-23 code: remote frames delivered | 24-27 Event::Disconnected
+// and with sparse saving a second word: 0-6 d2: depth of check_last_saved_state's replay |
+//   8-14 s1, 16-22 s2: 1 + the replayed frame saved (h == confirmed) in replay 1 / 2, 0 none.
+// stop: where the session stops at this call with its error (the reference panics there, or an input
+// row it needs is no longer held): 1 before the call's work, 2 after the first frame's save, 3 after
+// the first replay.
+enum : uint32_t { kStopNone = 0, kStopBefore = 1, kStopAfterSave0 = 2, kStopAfterReplay1 = 3 };
+
 // kSparse: sparse saving; kPred: the predictor (0 repeat-last, 1 PredictDefault) -- compile-time, so
 // their tests leave the step loop and its scalar registers
 template <int P, bool kSparse, int kPred>
 __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
   using T = typename InputWord<P>::T;
+  using Rec = typename std::conditional<kSparse, uint2, uint32_t>::type;
   constexpr int F = state_fields(P);
   constexpr int PC = cell_dwords_s(P) / 4;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -117,7 +128,7 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
 #define lring (reinterpret_cast<uint4*>(lds))
 #define ltag (reinterpret_cast<int32_t*>(lds + L.o_tags))
 #define llq (reinterpret_cast<T*>(lds + L.o_lq))
-#define larr (reinterpret_cast<uint16_t*>(lds + L.o_arr))
+#define lrec (reinterpret_cast<Rec*>(lds + L.o_arr))
 #define lrowtag (reinterpret_cast<int32_t*>(lds + L.o_rowtag))
 #define lrows (reinterpret_cast<T*>(lds + L.o_rows))
 
@@ -163,6 +174,8 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
   BoxState<P> st;
   load_state<P>(st, p.cur + s, S);
   auto fld = [&](int f) -> int32_t& { return p.sst[(int64_t)f * S + s]; };
+  // The control state (SyncLayer / InputQueue / connect status), advanced call by call by the control
+  // pass; the step loop keeps its own copies of what the inputs of a frame depend on.
   int32_t cur = fld(kCur), lconf = fld(kLconf), dframe = fld(kDframe), last_saved = fld(kLastSaved);
   int32_t delivered = fld(kDelivered), local_last = fld(kLocalLast), skips = fld(kSkips), err = fld(kErr);
   uint32_t disc = (uint32_t)fld(kDisc);
@@ -172,6 +185,11 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
 #pragma unroll
   for (int k = 0; k < P; k++) lf[k] = fld(kPl0 + kPlFields * k + 0);
   if (!live) err = 1;  // idle lanes run no call
+  int32_t s_cur = cur, s_delivered = delivered, s_local_last = local_last, s_lf[P];
+  uint32_t s_disc = disc;
+  bool s_done = err != 0;
+#pragma unroll
+  for (int k = 0; k < P; k++) s_lf[k] = lf[k];
   int32_t rollbacks = 0;
   int64_t resim = 0;
   // every state the launch steps descends from cur or from a ring cell this engine wrote, all in the
@@ -183,7 +201,9 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
   __syncthreads();
 
   auto next_slot = [&](int32_t x) { return x + 1 == R ? 0 : x + 1; };
-  int32_t slot_f = cur % R;  // ring slot of the current frame
+  auto back_slot = [&](int32_t x, int32_t d) { const int32_t y = x - d; return y < 0 ? y + R : y; };
+  int32_t slot_f = cur % R;    // control: ring slot of the current frame
+  int32_t s_slot_f = slot_f;   // step loop: the same
   auto cell_load = [&](int32_t slot) {
 #pragma unroll
     for (int k = 0; k < PC; k++) {
@@ -194,8 +214,9 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
         if (4 * k + i < F) st.w[4 * k + i] = x[i];
     }
   };
-  // SaveGameState(h) into `slot` (sync_layer.rs:208-215 + ex_game.rs:103-108)
-  auto save = [&](int32_t h, int32_t slot) {
+  // SaveGameState into `slot` (sync_layer.rs:208-215 + ex_game.rs:103-108); the frame tags and
+  // last_saved are the control pass's
+  auto save = [&](int32_t slot) {
     const uint32_t ck = fletcher16_state<P>(st);
 #pragma unroll
     for (int k = 0; k < PC; k++) {
@@ -204,24 +225,18 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
       for (int i = 0; i < 4; i++) x[i] = 4 * k + i < F ? st.w[4 * k + i] : (4 * k + i == F ? ck : 0u);
       lring[(slot * PC + k) * kBlock + lt] = make_uint4(x[0], x[1], x[2], x[3]);
     }
-    if (kSparse) ltag[slot * kBlock + lt] = h;
-    last_saved = h;
   };
 
   const int32_t c_end = p.c0 + p.n;
-  int32_t runmax = delivered;  // the arrivals staged so far
-  int32_t lo = 0, ce = 0;      // the stage's rows: frames / calls [lo, ce)
-  bool bad = false;            // a row read whose frame the input ring no longer holds
-  // input row g (frame g's remote inputs, call g's local ones): staged, or (older than the stage's
-  // window: a session far behind its calls) from the input ring
+  int32_t lo = 0;  // the stage's rows: frames / calls [lo, ce)
+  // a row's frame tag: staged, or (older than the stage's window: a session far behind its calls)
+  // from the input ring
+  auto row_ok = [&](int32_t g) -> bool { return g >= lo ? lrowtag[g - lo] == g : p.row_tag[g % p.cap] == g; };
+  // input row g (frame g's remote inputs, call g's local ones); the control pass has checked that
+  // every row the step loop reads is held
   auto row = [&](int32_t g) -> uint32_t {
-    if (g >= lo) {
-      bad |= lrowtag[g - lo] != g;
-      return (uint32_t)lrows[(g - lo) * kBlock + lt];
-    }
-    const int32_t gi = g % p.cap;
-    bad |= p.row_tag[gi] != g;
-    return load_inputs<P>(p.inputs, (int64_t)gi * S + s);
+    if (g >= lo) return (uint32_t)lrows[(g - lo) * kBlock + lt];
+    return load_inputs<P>(p.inputs, (int64_t)(g % p.cap) * S + s);
   };
   // The remote InputQueues in their canonical form.  Every frame a session has simulated used, for
   // a connected remote player, its input if it had arrived (frame <= lf) and otherwise the
@@ -233,47 +248,23 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
   // first g < current_frame whose input differs from the newest input before the burst, a rollback's
   // replay (reset_prediction, then synchronized_inputs per frame) uses the confirmed inputs up to lf
   // and the newest input after, and no per-frame prediction / last_requested bookkeeping is needed.
-  // pbase: the connected remote players' prediction (their bytes of the newest delivered row).
-  uint32_t pbase = 0;
   auto base_of = [&](int32_t d, uint32_t cb) -> uint32_t {
     return (kPred == 0 && d != kNull) ? row(d) & cb : 0u;
   };
-  // synchronized_inputs(h) (sync_layer.rs:280-293): local players from their queues, connected
-  // remote players confirmed or predicted, disconnected ones InputStatus::Disconnected past their
-  // last frame (ex_game spins the ship: input 4, ex_game.rs:280)
-  auto sync_inputs = [&](int32_t h, uint32_t cb) -> uint32_t {
-    uint32_t in = lbytes ? (uint32_t)llq[(h & (WL - 1)) * kBlock + lt] & lbytes : 0u;
-    const bool conf = h <= delivered;  // (a disconnected player's last frame is <= delivered too)
-    const uint32_t hrow = conf ? row(h) : 0u;
-    in |= conf ? hrow & cb : pbase;
-    if (disc) {
-#pragma unroll
-      for (int k = 0; k < P; k++)
-        if ((disc >> k) & 1u) in |= (h <= lf[k] ? (hrow >> (8 * k)) & 0xffu : 4u) << (8 * k);
-    }
-    return in;
+  // the rows [a, b] all held (a replay's confirmed inputs)
+  auto rows_ok = [&](int32_t a, int32_t b) -> bool {
+    bool ok = true;
+    for (int32_t g = a; g <= b; ++g) ok &= row_ok(g);
+    return ok;
   };
-
-  uint32_t conn = 0;  // the connected remote players' bytes (set at each call start)
-  bool at_start = true, replaying = false, window_done = false, save_own = false;
-  int32_t h = 0, load = 0, slot_h = 0, confirmed = kNull;
-  // adjust_gamestate's LoadGameState + reset_prediction (p2p_session.rs:658-714)
-  auto begin_replay = [&](int32_t from) -> bool {
-    if (from == kNull || from >= cur || from < cur - maxp) return false;  // load_frame's asserts
-    const int32_t sh = slot_f - (cur - from);
-    slot_h = sh < 0 ? sh + R : sh;
-    if (kSparse && ltag[slot_h * kBlock + lt] != from) return false;  // cell.frame == frame_to_load
-    cell_load(slot_h);  // (reset_prediction: nothing to reset in the canonical form)
-    load = from;
-    h = from;
-    replaying = true;
-    rollbacks += 1;
-    resim += cur - from;
-    return true;
+  // load_frame's asserts (sync_layer.rs:218-241) and, with sparse saving, cell.frame == frame_to_load
+  auto replay_ok = [&](int32_t from) -> bool {
+    if (from == kNull || from >= cur || from < cur - maxp) return false;
+    return !kSparse || ltag[back_slot(slot_f, cur - from) * kBlock + lt] == from;
   };
 
   for (int32_t cs = p.c0; cs < c_end; cs += p.K) {
-    ce = min(c_end, cs + p.K);
+    const int32_t ce = min(c_end, cs + p.K);
     lo = max(0, cs - p.B);
     const int nrows = ce - lo;
     __syncthreads();  // every lane is done with the previous stage
@@ -311,113 +302,344 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
         if (lt < nb) lrows[r * kBlock + lt] = src[(int64_t)ri * S];
       }
     }
+    bool tags_ok = true;
     for (int r = lt; r < nrows; r += kBlock) {
       int32_t ri = lo_i + r;
       ri = ri >= p.cap ? ri - p.cap : ri;
-      lrowtag[r] = p.row_tag[ri];
-    }
-    {  // this session's arrivals and Event::Disconnected bits for calls [cs, ce), eight at a time
-      const int32_t ci0 = cs % p.cap;
-      for (int32_t cb = cs; cb < ce; cb += 8) {
-        int32_t up[8];
-        uint32_t ev[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-          int32_t ci = ci0 + (cb - cs) + j;
-          ci = ci >= p.cap ? ci - p.cap : ci;
-          const bool in = live && cb + j < ce;
-          up[j] = in ? p.arrive[(int64_t)ci * S + s] : kNull;
-          ev[j] = (in && p.events) ? p.events[(int64_t)ci * S + s] : 0u;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-          const int32_t c = cb + j;
-          if (c >= ce) break;
-          int32_t code;
-          if (up[j] > c) {
-            code = kArrInvalid;
-          } else {
-            code = up[j] > runmax ? min(up[j] - runmax, kArrTooFar) : 0;
-            runmax = max(runmax, up[j]);
-          }
-          larr[(c - cs) * kBlock + lt] = (uint16_t)(code | (ev[j] << 8));
-        }
-      }
+      const int32_t tag = p.row_tag[ri];
+      lrowtag[r] = tag;
+      tags_ok &= tag == lo + r;
     }
     __syncthreads();
-    int32_t c = err ? ce : cs;
+    // The control pass's fast form (below): every staged row held, and at most 64 of them, so that a
+    // lane's "where do the remote inputs change" is one 64-bit mask over the stage's rows (repeat-last:
+    // row g differs from row g - 1; PredictDefault: row g is not 0).
+    const bool mask_ok = !kSparse && nrows <= 64 && __all(tags_ok);
+    uint64_t cm = 0;
+    if (mask_ok) {
+      uint32_t prev = 0;
+      for (int r = 0; r < nrows; r++) {
+        const uint32_t v = (uint32_t)lrows[r * kBlock + lt] & rbytes;
+        if (kPred == 0 ? (r > 0 && v != prev) : v != 0u) cm |= 1ull << r;
+        prev = v;
+      }
+    }
+
+    // ---- control pass: P2PSession::advance_frame's decisions for calls [cs, ce), call by call
+    // (every lane at the same call), without the game state; one record per call
+    {
+      const int32_t ci0 = cs % p.cap;
+      for (int32_t cb8 = cs; cb8 < ce; cb8 += 8) {
+        int32_t up8[8];
+        uint32_t ev8[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {  // this session's arrivals and Event::Disconnected bits, eight calls at a time
+          int32_t ci = ci0 + (cb8 - cs) + j;
+          ci = ci >= p.cap ? ci - p.cap : ci;
+          const bool in = !err && cb8 + j < ce;
+          up8[j] = in ? p.arrive[(int64_t)ci * S + s] : kNull;
+          ev8[j] = (in && p.events) ? p.events[(int64_t)ci * S + s] : 0u;
+        }
+        for (int j = 0; j < 8; j++) {
+          const int32_t c = cb8 + j;
+          if (c >= ce) break;
+          uint32_t rec = 0, rec2 = 0, stop = kStopNone;
+          // Fast form: a lane with every player connected, no disconnect pending, its rows staged,
+          // and nothing in this call that the reference would panic at -- the common call, branch-free.
+          bool fast = false;
+          if (mask_ok && !err) {
+            const int32_t a = up8[j];
+            const int32_t up = max(a, delivered);
+            const int32_t last = min(up, cur - 1);
+            int32_t mis = kNull;
+            if (last > delivered) {  // the burst's simulated frames (delivered, last]: bits lo_b .. hi_b
+              const int lo_b = delivered - lo + 1, hi_b = last - lo;
+              const uint64_t win = (hi_b >= 63 ? ~0ull : (2ull << hi_b) - 1) & ~((1ull << lo_b) - 1);
+              const uint64_t hit = cm & win;
+              if (hit) mis = lo + (int32_t)__builtin_ctzll(hit);
+            }
+            fast = a <= c && disc == 0 && ev8[j] == 0 && dframe == kNull && cur >= 1 && cur >= lo &&
+                   delivered >= (kPred == 0 ? lo : lo - 1) && (lbytes == 0 || local_last != kNull) &&
+                   up - delivered < kArrTooFar && up < cur - maxp + kQ - 1 && (mis == kNull || mis >= cur - maxp);
+            if (fast) {
+              const int32_t code = up - delivered;
+              delivered = up;
+#pragma unroll
+              for (int k = 0; k < P; k++)
+                if ((rbytes >> (8 * k)) & 1u) lf[k] = up;
+              int32_t confirmed = INT32_MAX;  // confirmed_frame (:542-553), every player connected
+              if (lbytes) confirmed = local_last;
+              if (rbytes) confirmed = min(confirmed, up);
+              uint32_t d = 0;
+              if (mis != kNull) {  // adjust_gamestate from the first misprediction
+                d = (uint32_t)(cur - mis);
+                rollbacks += 1;
+                resim += d;
+                if (d >= 2) last_saved = cur - 1;  // the replay's saves (:692-702)
+              }
+              const int32_t lc = min(confirmed, cur);  // set_last_confirmed_frame
+              if (lbytes && cur + p.delay == local_last + 1) local_last = cur + p.delay;  // add_local_input
+              const bool adv = cur - lc < maxp;  // the prediction threshold (:393-423)
+              lconf = lc;
+              last_saved = cur;
+              if (adv) {
+                ++cur;
+                slot_f = next_slot(slot_f);
+              } else {
+                ++skips;
+              }
+              rec = d | (adv ? 1u << 7 : 0u) | 1u << 10 | (uint32_t)code << 16;
+            }
+          }
+          if (fast) {
+          } else if (err) {
+            stop = kStopBefore;
+          } else {
+            // 1. poll_remote_clients: the burst of remote frames (delivered, up] for the remote players
+            //    still connected (handle_event Event::Input, p2p_session.rs:880-895)
+            const int32_t code = up8[j] > c ? -1 : (up8[j] > delivered ? min(up8[j] - delivered, kArrTooFar) : 0);
+            uint32_t cb = rbytes;  // bytes of the remote players still connected
+#pragma unroll
+            for (int k = 0; k < P; k++)
+              if ((disc >> k) & 1u) cb &= ~(0xffu << (8 * k));
+            const int32_t up = delivered + code;
+            bool bad = false;
+            if (code < 0) {  // a frame after its call: the remote peer cannot have sent it yet
+              err = GGRS_E_INVALID;
+            } else if (code == kArrTooFar || up >= cur - maxp + kQ - 1) {
+              // the reference's InputQueue holds 128 inputs (input_queue.rs:6) and panics past them; the
+              // device keeps the same bound on how far the remote inputs may run ahead of the session
+              err = GGRS_E_PRECONDITION;
+            } else {
+              // add_input_by_frame's first_incorrect_frame: the first frame of the burst the session
+              // has simulated whose inputs differ from the prediction (the canonical form above)
+              int32_t mis = kNull;
+              if (cb) {
+                if (kPred == 0 && delivered != kNull) bad |= !row_ok(delivered);
+                const uint32_t pb = base_of(delivered, cb);
+                const int32_t last = min(up, cur - 1);
+                for (int32_t g = delivered + 1; g <= last; ++g) {
+                  bad |= !row_ok(g);
+                  if ((row(g) & cb) != pb) {
+                    mis = g;
+                    break;
+                  }
+                }
+              }
+              if (bad) {
+                err = GGRS_E_PRECONDITION;  // a remote input no longer in the input rows
+                goto call_done;
+              }
+              delivered = up;
+#pragma unroll
+              for (int k = 0; k < P; k++)
+                if ((cb >> (8 * k)) & 1u) lf[k] = up;
+              // Event::Disconnected (p2p_session.rs:866-878 -> disconnect_player_at_frame :618-655)
+              const uint32_t ev = ev8[j] & ((1u << P) - 1u);
+#pragma unroll
+              for (int k = 0; k < P; k++) {
+                if (!((ev >> k) & 1u) || ((lmask >> k) & 1u) || ((disc >> k) & 1u)) continue;
+                disc |= 1u << k;
+                cb &= ~(0xffu << (8 * k));
+                if (cur > lf[k]) dframe = lf[k] + 1;
+              }
+              if (kPred == 0 && delivered != kNull) bad |= !row_ok(delivered);  // the prediction's row
+              rec = (uint32_t)code << 16 | ev << 24;
+              if (bad) {
+                err = GGRS_E_PRECONDITION;  // a remote input no longer in the input rows
+              } else {
+                // 2. the first frame's save (:305-308)
+                if (cur == 0) {
+                  last_saved = 0;
+                  if (kSparse) ltag[slot_f * kBlock + lt] = 0;
+                }
+                // confirmed_frame (:542-553): the newest frame every connected player has sent
+                int32_t confirmed = INT32_MAX;
+#pragma unroll
+                for (int k = 0; k < P; k++) {
+                  if ((disc >> k) & 1u) continue;
+                  confirmed = min(confirmed, ((lmask >> k) & 1u) ? local_last : lf[k]);
+                }
+                stop = kStopAfterSave0;
+                if (confirmed == INT32_MAX) {  // assert!(confirmed < i32::MAX)
+                  err = GGRS_E_PRECONDITION;
+                } else {
+                  // 3. check_simulation_consistency(disconnect_frame) (sync_layer.rs:343-353) +
+                  //    adjust_gamestate (p2p_session.rs:658-714)
+                  int32_t first_inc = dframe;
+                  if (mis != kNull && (first_inc == kNull || mis < first_inc)) first_inc = mis;
+                  if (first_inc != kNull) {
+                    const int32_t from = kSparse ? last_saved : first_inc;
+                    if (!replay_ok(from) || !rows_ok(from, min(cur - 1, delivered))) {
+                      err = GGRS_E_PRECONDITION;
+                    } else {
+                      const int32_t d = cur - from;
+                      rec |= (uint32_t)d;
+                      rollbacks += 1;
+                      resim += d;
+                      dframe = kNull;
+                      // the replay's saves (:692-702)
+                      if (kSparse) {
+                        if (confirmed >= from && confirmed < cur) {
+                          rec2 |= (uint32_t)(confirmed - from + 1) << 8;
+                          last_saved = confirmed;
+                          ltag[back_slot(slot_f, cur - confirmed) * kBlock + lt] = confirmed;
+                        }
+                      } else if (d >= 2) {
+                        last_saved = cur - 1;
+                      }
+                    }
+                  }
+                  bool save_own = !kSparse;
+                  // sparse saving: check_last_saved_state (:819-843) once the rollback's replay is done
+                  if (!err && kSparse && cur - last_saved >= maxp) {
+                    if (confirmed >= cur) {
+                      save_own = true;
+                    } else if (!replay_ok(last_saved)) {
+                      err = GGRS_E_PRECONDITION;
+                      stop = kStopAfterReplay1;
+                    } else if (!rows_ok(last_saved, min(cur - 1, delivered))) {
+                      err = GGRS_E_PRECONDITION;
+                    } else {
+                      const int32_t d2 = cur - last_saved;
+                      rec2 |= (uint32_t)d2;
+                      rollbacks += 1;
+                      resim += d2;
+                      if (confirmed >= last_saved && confirmed < cur) {
+                        rec2 |= (uint32_t)(confirmed - last_saved + 1) << 16;
+                        ltag[back_slot(slot_f, cur - confirmed) * kBlock + lt] = confirmed;
+                        last_saved = confirmed;
+                      }
+                    }
+                  }
+                  if (!err) {
+                    // set_last_confirmed_frame (sync_layer.rs:313-340), after this call's saves
+                    int32_t lc = confirmed;
+                    const int32_t ls = save_own ? cur : last_saved;
+                    if (kSparse && ls < lc) lc = ls;
+                    if (cur < lc) lc = cur;
+                    // add_local_input for every local player (:362-377, input_queue.rs:170-186): queue
+                    // frame current + delay, dropped unless it is the next one
+                    int32_t ll = local_last;
+                    if (lbytes) {
+                      const int32_t qf = cur + p.delay;
+                      if (local_last == kNull || qf == local_last + 1) ll = qf;
+                    }
+                    // the prediction threshold (:393-423)
+                    const int32_t ahead = lc == kNull ? cur : cur - lc;
+                    const bool adv = ahead < maxp;
+                    if ((lbytes && !row_ok(c)) || (adv && cur <= delivered && !row_ok(cur))) {
+                      err = GGRS_E_PRECONDITION;
+                    } else {
+                      lconf = lc;
+                      local_last = ll;
+                      if (save_own) {
+                        last_saved = cur;
+                        if (kSparse) ltag[slot_f * kBlock + lt] = cur;
+                      }
+                      rec |= (adv ? 1u << 7 : 0u) | (save_own ? 1u << 10 : 0u);
+                      if (adv) {
+                        ++cur;
+                        slot_f = next_slot(slot_f);
+                      } else {
+                        ++skips;
+                      }
+                      stop = kStopNone;
+                    }
+                  }
+                }
+              }
+            }
+          call_done:
+            if (err && stop == kStopNone) stop = kStopBefore;
+          }
+          rec |= stop << 8;
+          Rec r;
+          if constexpr (kSparse) r = make_uint2(rec, rec2);
+          else r = rec;
+          lrec[(c - cs) * kBlock + lt] = r;
+        }
+      }
+    }
+
+    // ---- step loop: the game states.  One thread per session, each its own step sequence: an
+    // iteration is one AdvanceFrame of the lane's current work -- a replayed frame, or its call's own
+    // frame -- or a call that does not advance.
+    uint32_t conn = 0, pbase = 0;  // the connected remote players' bytes; their prediction
+    // synchronized_inputs(h) (sync_layer.rs:280-293): local players from their queues, connected
+    // remote players confirmed or predicted, disconnected ones InputStatus::Disconnected past their
+    // last frame (ex_game spins the ship: input 4, ex_game.rs:280)
+    auto sync_inputs = [&](int32_t h) -> uint32_t {
+      uint32_t in = lbytes ? (uint32_t)llq[(h & (WL - 1)) * kBlock + lt] & lbytes : 0u;
+      const bool conf = h <= s_delivered;  // (a disconnected player's last frame is <= delivered too)
+      const uint32_t hrow = conf ? row(h) : 0u;
+      in |= conf ? hrow & conn : pbase;
+      if (s_disc) {
+#pragma unroll
+        for (int k = 0; k < P; k++)
+          if ((s_disc >> k) & 1u) in |= (h <= s_lf[k] ? (hrow >> (8 * k)) & 0xffu : 4u) << (8 * k);
+      }
+      return in;
+    };
+    int32_t c = s_done ? ce : cs;
+    bool at_start = true, replaying = false, second = false;
+    int32_t h = 0, load = 0, slot_h = 0, save_at = 0;  // save_at: sparse, the replayed frame saved
+    uint32_t rec = 0, rec2 = 0;
     while (c < ce) {
       if (at_start) {
-        const uint32_t a = larr[(c - cs) * kBlock + lt];
-        const int32_t code = (int32_t)(a & 0xffu);
-        if (code == kArrInvalid) { err = GGRS_E_INVALID; break; }  // the remote peer cannot have sent it yet
-        if (code == kArrTooFar) { err = GGRS_E_PRECONDITION; break; }
-        // 1. poll_remote_clients: the burst of remote frames (delivered, delivered + code] for the
-        //    remote players still connected (handle_event Event::Input, p2p_session.rs:880-895)
-        uint32_t cb = rbytes;  // bytes of the remote players still connected
+        const Rec r = lrec[(c - cs) * kBlock + lt];
+        if constexpr (kSparse) {
+          rec = r.x;
+          rec2 = r.y;
+        } else {
+          rec = r;
+        }
+        const uint32_t stop = (rec >> 8) & 3u;
+        if (stop == kStopBefore) break;
+        uint32_t cb = rbytes;
 #pragma unroll
         for (int k = 0; k < P; k++)
-          if ((disc >> k) & 1u) cb &= ~(0xffu << (8 * k));
-        const int32_t up = delivered + code;
-        // the reference's InputQueue holds 128 inputs (input_queue.rs:6) and panics past them; the
-        // device keeps the same bound on how far the remote inputs may run ahead of the session
-        if (up >= cur - maxp + kQ - 1) { err = GGRS_E_PRECONDITION; break; }
-        // add_input_by_frame's first_incorrect_frame: the first frame of the burst the session has
-        // simulated whose inputs differ from the prediction (the canonical form above)
-        int32_t mis = kNull;
-        if (cb) {
-          pbase = base_of(delivered, cb);
-          const int32_t last = min(up, cur - 1);
-          for (int32_t g = delivered + 1; g <= last; ++g)
-            if ((row(g) & cb) != pbase) {
-              mis = g;
-              break;
-            }
-        }
-        if (bad) { err = GGRS_E_PRECONDITION; break; }  // a remote input no longer in the input rows
-        delivered = up;
+          if ((s_disc >> k) & 1u) cb &= ~(0xffu << (8 * k));
+        s_delivered += (int32_t)((rec >> 16) & 0xffu);
 #pragma unroll
         for (int k = 0; k < P; k++)
-          if ((cb >> (8 * k)) & 1u) lf[k] = up;
-        // Event::Disconnected (p2p_session.rs:866-878 -> disconnect_player_at_frame :618-655)
-        const uint32_t ev = a >> 8;
+          if ((cb >> (8 * k)) & 1u) s_lf[k] = s_delivered;
+        const uint32_t ev = (rec >> 24) & ~lmask & ~s_disc;
+        if (ev) {
+          s_disc |= ev;
 #pragma unroll
-        for (int k = 0; k < P; k++) {
-          if (!((ev >> k) & 1u) || ((lmask >> k) & 1u) || ((disc >> k) & 1u)) continue;
-          disc |= 1u << k;
-          cb &= ~(0xffu << (8 * k));
-          if (cur > lf[k]) dframe = lf[k] + 1;
+          for (int k = 0; k < P; k++)
+            if ((ev >> k) & 1u) cb &= ~(0xffu << (8 * k));
         }
-        pbase = base_of(delivered, cb);  // the prediction from the newest input
-        if (bad) { err = GGRS_E_PRECONDITION; break; }
         conn = cb;
-        // 2. the first frame's save (:305-308)
-        if (cur == 0) save(0, slot_f);
-        // confirmed_frame (:542-553): the newest frame every connected player has sent
-        confirmed = INT32_MAX;
-#pragma unroll
-        for (int k = 0; k < P; k++) {
-          if ((disc >> k) & 1u) continue;
-          confirmed = min(confirmed, ((lmask >> k) & 1u) ? local_last : lf[k]);
+        pbase = base_of(s_delivered, cb);  // the prediction from the newest input
+        if (s_cur == 0) save(s_slot_f);    // the first frame's save
+        if (stop == kStopAfterSave0) break;
+        const int32_t d = (int32_t)(rec & 0x7fu);
+        second = false;
+        if (d) {  // adjust_gamestate's LoadGameState (reset_prediction: nothing to reset in the canonical form)
+          load = s_cur - d;
+          h = load;
+          slot_h = back_slot(s_slot_f, d);
+          cell_load(slot_h);
+          save_at = kSparse ? (int32_t)((rec2 >> 8) & 0x7fu) : 0;
+          replaying = true;
         }
-        if (confirmed == INT32_MAX) { err = GGRS_E_PRECONDITION; break; }  // assert!(confirmed < i32::MAX)
-        // 3. check_simulation_consistency(disconnect_frame) (sync_layer.rs:343-353) + adjust_gamestate
-        int32_t first_inc = dframe;
-        if (mis != kNull && (first_inc == kNull || mis < first_inc)) first_inc = mis;
-        if (first_inc != kNull) {
-          if (!begin_replay(kSparse ? last_saved : first_inc)) { err = GGRS_E_PRECONDITION; break; }
-          dframe = kNull;
-        }
-        window_done = false;
-        save_own = false;
         at_start = false;
       }
-      // sparse saving: check_last_saved_state (:819-843) once the rollback's replay is done
-      if (kSparse && !replaying && !window_done) {
-        window_done = true;
-        if (cur - last_saved >= maxp) {
-          if (confirmed >= cur) save_own = true;
-          else if (!begin_replay(last_saved)) { err = GGRS_E_PRECONDITION; break; }
+      if (!replaying && !second) {  // the first replay is done (or there was none)
+        if ((rec >> 8 & 3u) == kStopAfterReplay1) break;
+        second = true;
+        if (kSparse) {
+          const int32_t d2 = (int32_t)(rec2 & 0x7fu);
+          if (d2) {  // check_last_saved_state's rollback to the last save
+            load = s_cur - d2;
+            h = load;
+            slot_h = back_slot(s_slot_f, d2);
+            cell_load(slot_h);
+            save_at = (int32_t)((rec2 >> 16) & 0x7fu);
+            replaying = true;
+          }
         }
       }
       bool do_save, adv;
@@ -425,38 +647,28 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
       if (replaying) {
         fr = h;
         sslot = slot_h;
-        do_save = kSparse ? h == confirmed : h > load;  // (:692-702)
+        do_save = kSparse ? h - load + 1 == save_at : h > load;  // (:692-702)
         adv = true;
       } else {
-        fr = cur;
-        sslot = slot_f;
-        do_save = kSparse ? save_own : true;  // SaveGameState(current) (:337)
-        // set_last_confirmed_frame (sync_layer.rs:313-340), after this call's saves
-        int32_t lc = confirmed;
-        const int32_t ls = do_save ? cur : last_saved;
-        if (kSparse && ls < lc) lc = ls;
-        if (cur < lc) lc = cur;
-        lconf = lc;
-        // add_local_input for every local player (:362-377, input_queue.rs:170-186): queue frame
-        // current + delay, dropped unless it is the next one; the first fills the frames below the
-        // delay with the default input
+        fr = s_cur;
+        sslot = s_slot_f;
+        do_save = !kSparse || ((rec >> 10) & 1u);  // SaveGameState(current) (:337)
+        adv = (rec >> 7) & 1u;
+        // add_local_input (:362-377): queue frame current + delay, dropped unless it is the next
+        // one; the first fills the frames below the delay with the default input
         if (lbytes) {
-          const int32_t qf = cur + p.delay;
-          if (local_last == kNull || qf == local_last + 1) {
-            if (local_last == kNull)
+          const int32_t qf = s_cur + p.delay;
+          if (s_local_last == kNull || qf == s_local_last + 1) {
+            if (s_local_last == kNull)
               for (int32_t q = 0; q < p.delay; q++) llq[(q & (WL - 1)) * kBlock + lt] = (T)0;
             llq[(qf & (WL - 1)) * kBlock + lt] = (T)(row(c) & lbytes);
-            local_last = qf;
+            s_local_last = qf;
           }
         }
-        // the prediction threshold (:393-423)
-        const int32_t ahead = lconf == kNull ? cur : cur - lconf;
-        adv = ahead < maxp;
       }
       uint32_t in = 0;
-      if (adv) in = sync_inputs(fr, conn);
-      if (bad) { err = GGRS_E_PRECONDITION; break; }
-      if (do_save) save(fr, sslot);
+      if (adv) in = sync_inputs(fr);
+      if (do_save) save(sslot);
       if (adv) {
         if (lean_ok) {  // State::advance: the players' lean steps side by side, constants in VGPRs
           uint32_t v[P][5], pin[P];
@@ -486,18 +698,17 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
       if (replaying) {
         ++h;
         slot_h = next_slot(slot_h);
-        replaying = h != cur;
+        replaying = h != s_cur;
       } else {
         if (adv) {
-          ++cur;
-          slot_f = next_slot(slot_f);
-        } else {
-          ++skips;
+          ++s_cur;
+          s_slot_f = next_slot(s_slot_f);
         }
         ++c;
         at_start = true;
       }
     }
+    if (c < ce) s_done = true;  // stopped at an error
   }
   __syncthreads();
   {  // rings back to HBM
@@ -538,7 +749,7 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
 #undef lring
 #undef ltag
 #undef llq
-#undef larr
+#undef lrec
 #undef lrowtag
 #undef lrows
 }
