@@ -565,15 +565,16 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
     // ---- step loop: the game states.  One thread per session, each its own step sequence: an
     // iteration is one AdvanceFrame of the lane's current work -- a replayed frame, or its call's own
     // frame -- or a call that does not advance.
-    uint32_t conn = 0, pbase = 0;  // the connected remote players' bytes; their prediction
+    uint32_t conn = 0;  // the connected remote players' bytes
     // synchronized_inputs(h) (sync_layer.rs:280-293): local players from their queues, connected
-    // remote players confirmed or predicted, disconnected ones InputStatus::Disconnected past their
-    // last frame (ex_game spins the ship: input 4, ex_game.rs:280)
+    // remote players confirmed or predicted -- the input of frame min(h, delivered) in the canonical
+    // form (repeat-last; PredictDefault: 0 past delivered) --, disconnected ones
+    // InputStatus::Disconnected past their last frame (ex_game spins the ship: input 4, ex_game.rs:280)
     auto sync_inputs = [&](int32_t h) -> uint32_t {
       uint32_t in = lbytes ? (uint32_t)llq[(h & (WL - 1)) * kBlock + lt] & lbytes : 0u;
       const bool conf = h <= s_delivered;  // (a disconnected player's last frame is <= delivered too)
-      const uint32_t hrow = conf ? row(h) : 0u;
-      in |= conf ? hrow & conn : pbase;
+      const uint32_t hrow = s_delivered == kNull ? 0u : row(conf ? h : s_delivered);
+      in |= (kPred == 1 && !conf) ? 0u : hrow & conn;
       if (s_disc) {
 #pragma unroll
         for (int k = 0; k < P; k++)
@@ -612,8 +613,7 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
             if ((ev >> k) & 1u) cb &= ~(0xffu << (8 * k));
         }
         conn = cb;
-        pbase = base_of(s_delivered, cb);  // the prediction from the newest input
-        if (s_cur == 0) save(s_slot_f);    // the first frame's save
+        if (s_cur == 0) save(s_slot_f);  // the first frame's save
         if (stop == kStopAfterSave0) break;
         const int32_t d = (int32_t)(rec & 0x7fu);
         second = false;
@@ -627,10 +627,10 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
         }
         at_start = false;
       }
-      if (!replaying && !second) {  // the first replay is done (or there was none)
+      if (kSparse && !replaying && !second) {  // the first replay is done (or there was none)
         if ((rec >> 8 & 3u) == kStopAfterReplay1) break;
         second = true;
-        if (kSparse) {
+        {
           const int32_t d2 = (int32_t)(rec2 & 0x7fu);
           if (d2) {  // check_last_saved_state's rollback to the last save
             load = s_cur - d2;
@@ -642,18 +642,14 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
           }
         }
       }
-      bool do_save, adv;
-      int32_t fr, sslot;
-      if (replaying) {
-        fr = h;
-        sslot = slot_h;
-        do_save = kSparse ? h - load + 1 == save_at : h > load;  // (:692-702)
-        adv = true;
-      } else {
-        fr = s_cur;
-        sslot = s_slot_f;
-        do_save = !kSparse || ((rec >> 10) & 1u);  // SaveGameState(current) (:337)
-        adv = (rec >> 7) & 1u;
+      // SaveGameState of the replayed frames after the loaded one (:692-702) and of the current
+      // frame (:337); without sparse saving every step saves -- the first replay step rewrites the
+      // loaded cell with its own bytes -- so the save needs no branch
+      const int32_t fr = replaying ? h : s_cur;
+      const int32_t sslot = replaying ? slot_h : s_slot_f;
+      const bool do_save = !kSparse || (replaying ? h - load + 1 == save_at : ((rec >> 10) & 1u) != 0u);
+      const bool adv = replaying || ((rec >> 7) & 1u);
+      if (!replaying) {
         // add_local_input (:362-377): queue frame current + delay, dropped unless it is the next
         // one; the first fills the frames below the delay with the default input
         if (lbytes) {
@@ -666,9 +662,12 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
           }
         }
       }
-      uint32_t in = 0;
-      if (adv) in = sync_inputs(fr);
-      if (do_save) save(sslot);
+      const uint32_t in = sync_inputs(fr);
+      if (kSparse) {
+        if (do_save) save(sslot);
+      } else {
+        save(sslot);
+      }
       if (adv) {
         if (lean_ok) {  // State::advance: the players' lean steps side by side, constants in VGPRs
           uint32_t v[P][5], pin[P];
@@ -695,18 +694,15 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
           advance_state<P>(st, in, 0u);
         }
       }
-      if (replaying) {
-        ++h;
-        slot_h = next_slot(slot_h);
-        replaying = h != s_cur;
-      } else {
-        if (adv) {
-          ++s_cur;
-          s_slot_f = next_slot(s_slot_f);
-        }
-        ++c;
-        at_start = true;
-      }
+      const bool rep = replaying;
+      h = rep ? h + 1 : h;
+      slot_h = rep ? next_slot(slot_h) : slot_h;
+      replaying = rep && h != s_cur;
+      const bool own_adv = !rep && adv;
+      s_cur = own_adv ? s_cur + 1 : s_cur;
+      s_slot_f = own_adv ? next_slot(s_slot_f) : s_slot_f;
+      c = rep ? c : c + 1;
+      at_start = !rep;
     }
     if (c < ce) s_done = true;  // stopped at an error
   }
