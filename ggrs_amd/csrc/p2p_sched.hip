@@ -102,6 +102,10 @@ __device__ inline T* in_vgpr_ptr(T* ptr) {
   asm volatile("" : "+v"(u));
   return reinterpret_cast<T*>(u);
 }
+__device__ inline int32_t in_vgpr_i32(int32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
 
 // A call's record, written by the control pass and read by the step loop (bits):
 //   0-6 d1: replay depth of the rollback (0: none) | 7 adv: the own frame advances | 8-9 stop |
@@ -115,7 +119,9 @@ enum : uint32_t { kStopNone = 0, kStopBefore = 1, kStopAfterSave0 = 2, kStopAfte
 
 // kSparse: sparse saving; kPred: the predictor (0 repeat-last, 1 PredictDefault) -- compile-time, so
 // their tests leave the step loop and its scalar registers
-template <int P, bool kSparse, int kPred>
+// kLocal: the local-player mask when it is a compile-time one (two players, one of them local: the
+// usual peer), else -1
+template <int P, bool kSparse, int kPred, int kLocal>
 __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
   using T = typename InputWord<P>::T;
   using Rec = typename std::conditional<kSparse, uint2, uint32_t>::type;
@@ -141,13 +147,17 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
   p.resim = in_vgpr_ptr(p.resim);
   p.row_tag = in_vgpr_ptr(p.row_tag);
   p.events = in_vgpr_ptr(p.events);
+  p.inputs = in_vgpr_ptr(p.inputs);
+  p.arrive = in_vgpr_ptr(p.arrive);
+  p.cap = in_vgpr_i32(p.cap);
+  p.delay = in_vgpr_i32(p.delay);
   const int64_t S = p.S;
   const int64_t sess0 = (int64_t)blockIdx.x * kBlock;
   const int lt = threadIdx.x;
   const bool live = sess0 + lt < S;
   const int64_t s = live ? sess0 + lt : sess0;  // idle lanes shadow the block's first session, never store
   const int nb = (int)min((int64_t)kBlock, S - sess0);
-  const uint32_t lmask = p.local_mask;
+  const uint32_t lmask = kLocal >= 0 ? (uint32_t)kLocal : p.local_mask;
   uint32_t lbytes = 0;
 #pragma unroll
   for (int k = 0; k < P; k++) lbytes |= ((lmask >> k) & 1u) ? 0xffu << (8 * k) : 0u;
@@ -275,23 +285,13 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
     if (nb == kBlock && ((S * (int64_t)sizeof(T)) & 15) == 0) {  // rows [lo, ce) as 16-byte units
       constexpr int kUpr = kBlock / kUnitT;  // units per row
       const int units = nrows * kUpr;
-      for (int u0 = 0; u0 < units; u0 += 8 * kBlock) {
-        uint4 v[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-          const int u = u0 + j * kBlock + lt;
-          if (u < units) {
-            const int r = u / kUpr, k = u - r * kUpr;
-            int32_t ri = lo_i + r;
-            ri = ri >= p.cap ? ri - p.cap : ri;
-            v[j] = reinterpret_cast<const uint4*>(p.inputs + ((int64_t)ri * S + sess0) * sizeof(T))[k];
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-          const int u = u0 + j * kBlock + lt;
-          if (u < units) reinterpret_cast<uint4*>(lrows)[u] = v[j];
-        }
+#pragma unroll 8
+      for (int u = lt; u < units; u += kBlock) {  // (unrolled: the global loads issue back to back)
+        const int r = u / kUpr, k = u - r * kUpr;
+        int32_t ri = lo_i + r;
+        ri = ri >= p.cap ? ri - p.cap : ri;
+        reinterpret_cast<uint4*>(lrows)[u] =
+            reinterpret_cast<const uint4*>(p.inputs + ((int64_t)ri * S + sess0) * sizeof(T))[k];
       }
     } else {  // a partial last block: word by word
       const T* src = reinterpret_cast<const T*>(p.inputs) + sess0 + lt;
@@ -343,12 +343,21 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
         for (int j = 0; j < 8; j++) {
           const int32_t c = cb8 + j;
           if (c >= ce) break;
+          // this call's arrival and events: the front of the batch, which shifts down a call per
+          // iteration (indexing it by j would put it in scratch memory)
+          const int32_t a_c = up8[0];
+          const uint32_t e_c = ev8[0];
+#pragma unroll
+          for (int k = 0; k < 7; k++) {
+            up8[k] = up8[k + 1];
+            ev8[k] = ev8[k + 1];
+          }
           uint32_t rec = 0, rec2 = 0, stop = kStopNone;
           // Fast form: a lane with every player connected, no disconnect pending, its rows staged,
           // and nothing in this call that the reference would panic at -- the common call, branch-free.
           bool fast = false;
           if (mask_ok && !err) {
-            const int32_t a = up8[j];
+            const int32_t a = a_c;
             const int32_t up = max(a, delivered);
             const int32_t last = min(up, cur - 1);
             int32_t mis = kNull;
@@ -358,7 +367,7 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
               const uint64_t hit = cm & win;
               if (hit) mis = lo + (int32_t)__builtin_ctzll(hit);
             }
-            fast = a <= c && disc == 0 && ev8[j] == 0 && dframe == kNull && cur >= 1 && cur >= lo &&
+            fast = a <= c && disc == 0 && e_c == 0 && dframe == kNull && cur >= 1 && cur >= lo &&
                    delivered >= (kPred == 0 ? lo : lo - 1) && (lbytes == 0 || local_last != kNull) &&
                    up - delivered < kArrTooFar && up < cur - maxp + kQ - 1 && (mis == kNull || mis >= cur - maxp);
             if (fast) {
@@ -397,7 +406,7 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
           } else {
             // 1. poll_remote_clients: the burst of remote frames (delivered, up] for the remote players
             //    still connected (handle_event Event::Input, p2p_session.rs:880-895)
-            const int32_t code = up8[j] > c ? -1 : (up8[j] > delivered ? min(up8[j] - delivered, kArrTooFar) : 0);
+            const int32_t code = a_c > c ? -1 : (a_c > delivered ? min(a_c - delivered, kArrTooFar) : 0);
             uint32_t cb = rbytes;  // bytes of the remote players still connected
 #pragma unroll
             for (int k = 0; k < P; k++)
@@ -435,7 +444,7 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
               for (int k = 0; k < P; k++)
                 if ((cb >> (8 * k)) & 1u) lf[k] = up;
               // Event::Disconnected (p2p_session.rs:866-878 -> disconnect_player_at_frame :618-655)
-              const uint32_t ev = ev8[j] & ((1u << P) - 1u);
+              const uint32_t ev = e_c & ((1u << P) - 1u);
 #pragma unroll
               for (int k = 0; k < P; k++) {
                 if (!((ev >> k) & 1u) || ((lmask >> k) & 1u) || ((disc >> k) & 1u)) continue;
@@ -860,11 +869,21 @@ int p2p_sched_advance(ggrs_p2p_engine* e, int32_t n) {
       if (attr == hipSuccess) kern<<<(unsigned)grid_of(p.S, kBlock), kBlock, shm, e->stream>>>(p);
     };
     if (p.sparse) {
-      if (p.predictor == 0) go(&p2p_sched_kernel<PP, true, 0>);
-      else go(&p2p_sched_kernel<PP, true, 1>);
+      if (p.predictor == 0) go(&p2p_sched_kernel<PP, true, 0, -1>);
+      else go(&p2p_sched_kernel<PP, true, 1, -1>);
     } else {
-      if (p.predictor == 0) go(&p2p_sched_kernel<PP, false, 0>);
-      else go(&p2p_sched_kernel<PP, false, 1>);
+      bool done = false;
+      if constexpr (PP == 2) {  // one local player of two, repeat-last: the usual peer, masks compile-time
+        if (p.predictor == 0 && (p.local_mask == 1u || p.local_mask == 2u)) {
+          if (p.local_mask == 1u) go(&p2p_sched_kernel<PP, false, 0, 1>);
+          else go(&p2p_sched_kernel<PP, false, 0, 2>);
+          done = true;
+        }
+      }
+      if (!done) {
+        if (p.predictor == 0) go(&p2p_sched_kernel<PP, false, 0, -1>);
+        else go(&p2p_sched_kernel<PP, false, 1, -1>);
+      }
     }
   });
   HIP_TRY(attr);
