@@ -360,16 +360,15 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
             const int32_t a = a_c;
             const int32_t up = max(a, delivered);
             const int32_t last = min(up, cur - 1);
-            int32_t mis = kNull;
-            if (last > delivered) {  // the burst's simulated frames (delivered, last]: bits lo_b .. hi_b
-              const int lo_b = delivered - lo + 1, hi_b = last - lo;
-              const uint64_t win = (hi_b >= 63 ? ~0ull : (2ull << hi_b) - 1) & ~((1ull << lo_b) - 1);
-              const uint64_t hit = cm & win;
-              if (hit) mis = lo + (int32_t)__builtin_ctzll(hit);
-            }
-            fast = a <= c && disc == 0 && e_c == 0 && dframe == kNull && cur >= 1 && cur >= lo &&
-                   delivered >= (kPred == 0 ? lo : lo - 1) && (lbytes == 0 || local_last != kNull) &&
-                   up - delivered < kArrTooFar && up < cur - maxp + kQ - 1 && (mis == kNull || mis >= cur - maxp);
+            // the burst's simulated frames (delivered, last]: bits lo_b .. hi_b of the change mask
+            const int lo_b = (delivered - lo + 1) & 63, hi_b = (last - lo) & 63;
+            const uint64_t win = (last - lo >= 63 ? ~0ull : (2ull << hi_b) - 1) & ~((1ull << lo_b) - 1);
+            const uint64_t hit = last > delivered ? cm & win : 0ull;
+            const int32_t mis = hit ? lo + (int32_t)__builtin_ctzll(hit) : kNull;
+            // (bitwise: every test evaluated, no branch per test)
+            fast = (a <= c) & (disc == 0u) & (e_c == 0u) & (dframe == kNull) & (cur >= 1) & (cur >= lo) &
+                   (delivered >= (kPred == 0 ? lo : lo - 1)) & (lbytes == 0u || local_last != kNull) &
+                   (up - delivered < kArrTooFar) & (up < cur - maxp + kQ - 1) & (mis == kNull || mis >= cur - maxp);
             if (fast) {
               const int32_t code = up - delivered;
               delivered = up;
@@ -379,24 +378,20 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
               int32_t confirmed = INT32_MAX;  // confirmed_frame (:542-553), every player connected
               if (lbytes) confirmed = local_last;
               if (rbytes) confirmed = min(confirmed, up);
-              uint32_t d = 0;
-              if (mis != kNull) {  // adjust_gamestate from the first misprediction
-                d = (uint32_t)(cur - mis);
-                rollbacks += 1;
-                resim += d;
-                if (d >= 2) last_saved = cur - 1;  // the replay's saves (:692-702)
-              }
+              // adjust_gamestate from the first misprediction (its replay's saves end below the
+              // current frame's, which becomes the last save)
+              const bool rb = mis != kNull;
+              const uint32_t d = rb ? (uint32_t)(cur - mis) : 0u;
+              rollbacks += rb ? 1 : 0;
+              resim += d;
               const int32_t lc = min(confirmed, cur);  // set_last_confirmed_frame
-              if (lbytes && cur + p.delay == local_last + 1) local_last = cur + p.delay;  // add_local_input
+              if (lbytes) local_last = cur + p.delay == local_last + 1 ? cur + p.delay : local_last;  // add_local_input
               const bool adv = cur - lc < maxp;  // the prediction threshold (:393-423)
               lconf = lc;
               last_saved = cur;
-              if (adv) {
-                ++cur;
-                slot_f = next_slot(slot_f);
-              } else {
-                ++skips;
-              }
+              cur = adv ? cur + 1 : cur;
+              slot_f = adv ? next_slot(slot_f) : slot_f;
+              skips += adv ? 0 : 1;
               rec = d | (adv ? 1u << 7 : 0u) | 1u << 10 | (uint32_t)code << 16;
             }
           }
