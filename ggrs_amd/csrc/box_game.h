@@ -491,6 +491,33 @@ __device__ inline void advance_state_lean(BoxState<P>& s, uint32_t inputs) {
   }
 }
 
+// The same with the players' steps side by side (advance_players_lean: one clamp branch) and the
+// sin/cos constants the caller hoisted into vector registers (sincos_consts_vgpr): for step loops
+// whose many uniform values would otherwise spill the constants' scalar registers.
+template <int P>
+__device__ inline void advance_state_lean_k(BoxState<P>& st, uint32_t inputs, const SincosConsts& K) {
+  uint32_t v[P][5], pin[P];
+#pragma unroll
+  for (int k = 0; k < P; k++) {
+    v[k][0] = st.w[fld_x(P, k)];
+    v[k][1] = st.w[fld_y(P, k)];
+    v[k][2] = st.w[fld_vx(P, k)];
+    v[k][3] = st.w[fld_vy(P, k)];
+    v[k][4] = st.w[fld_rot(P, k)];
+    pin[k] = (inputs >> (8 * k)) & 0xffu;
+  }
+  advance_players_lean<P>(v, pin, K);
+  st.w[0] = (uint32_t)((int32_t)st.w[0] + 1);
+#pragma unroll
+  for (int k = 0; k < P; k++) {
+    st.w[fld_x(P, k)] = v[k][0];
+    st.w[fld_y(P, k)] = v[k][1];
+    st.w[fld_vx(P, k)] = v[k][2];
+    st.w[fld_vy(P, k)] = v[k][3];
+    st.w[fld_rot(P, k)] = v[k][4];
+  }
+}
+
 template <int P>
 __device__ inline bool rot_in_domain(const BoxState<P>& s) {
   bool ok = true;

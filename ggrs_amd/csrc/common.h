@@ -200,6 +200,21 @@ inline void dispatch_players(int p, F&& f) {
   }
 }
 
+// A pointer held in vector registers: the kernel's uniform values exceed the scalar register file
+// (102 SGPRs) and the compiler spills them to VGPR lanes, reloading each with a v_readlane at every
+// use; the buffers touched only at a launch's start and end and by rare paths live in VGPRs instead
+// (an empty asm statement: it emits no instruction).
+template <typename T>
+__device__ inline T* in_vgpr_ptr(T* ptr) {
+  uint64_t u = reinterpret_cast<uint64_t>(ptr);
+  asm volatile("" : "+v"(u));
+  return reinterpret_cast<T*>(u);
+}
+__device__ inline int32_t in_vgpr_i32(int32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
 }  // namespace
 
 }  // namespace ggrs

@@ -92,20 +92,6 @@ __host__ __device__ inline SchedLds sched_lds(int P, int R, int sparse, int WL, 
 }
 constexpr int kArrTooFar = 0xfe;  // a burst of >= 254 frames: past the device queue (GGRS_E_PRECONDITION)
 
-// A pointer held in vector registers: the kernel's uniform values exceed the scalar register file
-// (102 SGPRs) and the compiler spills them to VGPR lanes, reloading each with a v_readlane at every
-// use; the buffers touched only at a launch's start and end and by rare paths live in VGPRs instead
-// (an empty asm statement: it emits no instruction).
-template <typename T>
-__device__ inline T* in_vgpr_ptr(T* ptr) {
-  uint64_t u = reinterpret_cast<uint64_t>(ptr);
-  asm volatile("" : "+v"(u));
-  return reinterpret_cast<T*>(u);
-}
-__device__ inline int32_t in_vgpr_i32(int32_t x) {
-  asm volatile("" : "+v"(x));
-  return x;
-}
 
 // A call's record, written by the control pass and read by the step loop (bits):
 //   0-6 d1: replay depth of the rollback (0: none) | 7 adv: the own frame advances | 8-9 stop |
@@ -674,26 +660,7 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
       }
       if (adv) {
         if (lean_ok) {  // State::advance: the players' lean steps side by side, constants in VGPRs
-          uint32_t v[P][5], pin[P];
-#pragma unroll
-          for (int k = 0; k < P; k++) {
-            v[k][0] = st.w[fld_x(P, k)];
-            v[k][1] = st.w[fld_y(P, k)];
-            v[k][2] = st.w[fld_vx(P, k)];
-            v[k][3] = st.w[fld_vy(P, k)];
-            v[k][4] = st.w[fld_rot(P, k)];
-            pin[k] = (in >> (8 * k)) & 0xffu;
-          }
-          advance_players_lean<P>(v, pin, K);
-          st.w[0] = (uint32_t)((int32_t)st.w[0] + 1);
-#pragma unroll
-          for (int k = 0; k < P; k++) {
-            st.w[fld_x(P, k)] = v[k][0];
-            st.w[fld_y(P, k)] = v[k][1];
-            st.w[fld_vx(P, k)] = v[k][2];
-            st.w[fld_vy(P, k)] = v[k][3];
-            st.w[fld_rot(P, k)] = v[k][4];
-          }
+          advance_state_lean_k<P>(st, in, K);
         } else {
           advance_state<P>(st, in, 0u);
         }
