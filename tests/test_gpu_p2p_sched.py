@@ -158,3 +158,27 @@ def test_p2p_arrival_schedule_rejects(oracle):
     frames, skipped, errors = eng.sessions()
     assert errors[9] == GGRS_E_PRECONDITION
     assert errors[10] == 0 and frames[10] == 48 and skipped[10] == 0
+
+
+@pytest.mark.parametrize("stalls,delay,local", [(False, 0, (0,)), (True, 0, (0,)), (False, 2, (1,))])
+def test_p2p_synth_schedules_every_session(oracle, stalls, delay, local):
+    """The bench's schedules (synth.jitter_arrivals: jittered lags, optionally network stalls past
+    max_prediction) for every one of 640 sessions, in launches that cross the kernel's stages at
+    different calls -- the control pass's branch-free fast form (every player connected, the rows
+    staged) decides nearly every call here -- state, ring, counts, skips and frames bit-exact."""
+    from ggrs_amd import P2PEngine, synth
+    S, calls, P, mp = 640, 200, 2, 8
+    rows = synth.gen_inputs(0, S, calls, P, synth.MODEL_HELD)
+    arrive = synth.jitter_arrivals(0, S, calls, mp, stalls=stalls)
+    eng = P2PEngine(S, num_players=P, local_players=local, input_delay=delay, max_prediction=mp, remote_latency=1,
+                    input_capacity=calls)
+    eng.set_arrival_schedule(True)
+    eng.add_inputs(0, rows)
+    eng.add_arrivals(0, arrive)
+    for n in (37, 64, 99):
+        eng.advance_frames(n)
+    events = np.zeros((calls, S), np.uint8)
+    check_sessions(eng, rows, arrive, events, range(S), calls)
+    frames, skipped, errors = eng.sessions()
+    assert (errors == 0).all()
+    assert (skipped.sum() > 0) == stalls
