@@ -555,7 +555,10 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
     // ---- step loop: the game states.  One thread per session, each its own step sequence: an
     // iteration is one AdvanceFrame of the lane's current work -- a replayed frame, or its call's own
     // frame -- or a call that does not advance.
-    uint32_t conn = 0;  // the connected remote players' bytes
+    uint32_t conn = rbytes;  // the connected remote players' bytes
+#pragma unroll
+    for (int k = 0; k < P; k++)
+      if ((s_disc >> k) & 1u) conn &= ~(0xffu << (8 * k));
     // synchronized_inputs(h) (sync_layer.rs:280-293): local players from their queues, connected
     // remote players confirmed or predicted -- the input of frame min(h, delivered) in the canonical
     // form (repeat-last; PredictDefault: 0 past delivered) --, disconnected ones
@@ -585,26 +588,23 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
         } else {
           rec = r;
         }
-        const uint32_t stop = (rec >> 8) & 3u;
-        if (stop == kStopBefore) break;
-        uint32_t cb = rbytes;
-#pragma unroll
-        for (int k = 0; k < P; k++)
-          if ((s_disc >> k) & 1u) cb &= ~(0xffu << (8 * k));
         s_delivered += (int32_t)((rec >> 16) & 0xffu);
-#pragma unroll
-        for (int k = 0; k < P; k++)
-          if ((cb >> (8 * k)) & 1u) s_lf[k] = s_delivered;
-        const uint32_t ev = (rec >> 24) & ~lmask & ~s_disc;
-        if (ev) {
-          s_disc |= ev;
+        // the rare call starts in one branch: a stop, a disconnect (the player's last frame is the
+        // newest delivered one, ex_game spins it from the next), or the first call
+        if ((rec & 0x0f000300u) != 0u || s_cur == 0) {
+          const uint32_t stop = (rec >> 8) & 3u;
+          if (stop == kStopBefore) break;
+          const uint32_t ev = (rec >> 24) & ~lmask & ~s_disc;
 #pragma unroll
           for (int k = 0; k < P; k++)
-            if ((ev >> k) & 1u) cb &= ~(0xffu << (8 * k));
+            if ((ev >> k) & 1u) {
+              s_lf[k] = s_delivered;
+              conn &= ~(0xffu << (8 * k));
+            }
+          s_disc |= ev;
+          if (s_cur == 0) save(s_slot_f);  // the first frame's save
+          if (stop == kStopAfterSave0) break;
         }
-        conn = cb;
-        if (s_cur == 0) save(s_slot_f);  // the first frame's save
-        if (stop == kStopAfterSave0) break;
         const int32_t d = (int32_t)(rec & 0x7fu);
         second = false;
         if (d) {  // adjust_gamestate's LoadGameState (reset_prediction: nothing to reset in the canonical form)
