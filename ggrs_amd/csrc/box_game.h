@@ -554,10 +554,9 @@ __device__ inline uint32_t dot4_u8(uint32_t a, uint32_t b, uint32_t c) {
 // Fletcher-16 from DOUBLED sums d1 = 2*sum1, d2 = 2*sum2 (< 2^22; accumulated with doubled byte
 // weights, all <= 2*116 = 232 so they still fit v_dot4's u8 lanes).  Doubling lets the mod-255
 // run on full-rate instructions: q = floor(x/255) = (2x * 0x808081) >> 32 for x < 2^31/127
-// (0x808081 * 255 = 2^31 + 127), one v_mul_hi_u32_u24; 2r = 2x - 510 q, one v_dot2c_i32_i16
-// (d + q * -510 over the 16-bit lanes (q, 0) x (-510, 0): exact while q < 2^15, and here q <
-// 2^22 / 255 < 2^14); then (r2 << 8) | r1 = (2 r2 << 7) | (2 r1 >> 1).  Replaces four quarter-rate
-// 32-bit multiplies.
+// (0x808081 * 255 = 2^31 + 127), one v_mul_hi_u32_u24; 2r = 2x - 510 q, one multiply-add (exact:
+// q < 2^22 / 255 < 2^14); then (r2 << 8) | r1 = (2 r2 << 7) | (2 r1 >> 1).  Replaces four
+// quarter-rate 32-bit multiplies.
 //
 // No inline asm (round 5): these multiply-adds were `v_mad_i32_i24` inline asm until round 4, and
 // the same construct in particles.h gave wrong checksums under LLVM's max-ilp scheduler.  The
@@ -569,18 +568,29 @@ __device__ inline uint32_t dot4_u8(uint32_t a, uint32_t b, uint32_t c) {
 //     v_mad_u32_u24 v32, v59, v27, v84         ; inline asm: reads v27 0 wait states later
 // and the asm read a stale accumulator.  Builtins keep every consumer visible to the hazard
 // recognizer (tools/asm_hazards.py checks every unit's ISA for the pattern).
-typedef short ggrs_short2 __attribute__((ext_vector_type(2)));
 __device__ inline uint32_t mulhi_u24(uint32_t a, uint32_t b) {
   return (uint32_t)(((uint64_t)(a & 0xffffffu) * (uint64_t)(b & 0xffffffu)) >> 32);
 }
-// 2x - 510 q for q < 2^15: q's register holds the 16-bit lanes (q, 0)
+// 2x - 510 q (q < 2^14), two exact forms: kMad24 a signed 24-bit multiply-add; else v_dot2c_i32_i16
+// over the 16-bit lanes (q, 0) x (-510, 0).  Which one is faster depends on the kernel around it
+// (profiles/r05ac, r05ad: the dot form's readers need the three DOT wait states, the mad form the
+// integer multiply pipe): config 3's prefix kernel 24.3 us per launch with the mad against 26.4
+// with the dot, config 4's rounds kernel 300 against 290 us, configs 2 / P2P within 1 %; the
+// prefix kernel takes kMad24, the rest the dot form.
+typedef short ggrs_short2 __attribute__((ext_vector_type(2)));
+template <bool kMad24>
 __device__ inline uint32_t sub510_small(uint32_t x2, uint32_t q) {
-  const ggrs_short2 m = {(short)-510, (short)0};
-  return (uint32_t)__builtin_amdgcn_sdot2(__builtin_bit_cast(ggrs_short2, q), m, (int32_t)x2, false);
+  if constexpr (kMad24) {
+    return (uint32_t)((int32_t)x2 + __mul24((int32_t)q, -510));
+  } else {
+    const ggrs_short2 m = {(short)-510, (short)0};
+    return (uint32_t)__builtin_amdgcn_sdot2(__builtin_bit_cast(ggrs_short2, q), m, (int32_t)x2, false);
+  }
 }
+template <bool kMad24 = false>
 __device__ inline uint32_t fletcher_from_doubled(uint32_t d1, uint32_t d2) {
   const uint32_t q1 = mulhi_u24(d1, 0x808081u), q2 = mulhi_u24(d2, 0x808081u);
-  const uint32_t r1 = sub510_small(d1, q1), r2 = sub510_small(d2, q2);
+  const uint32_t r1 = sub510_small<kMad24>(d1, q1), r2 = sub510_small<kMad24>(d2, q2);
   return (r2 << 7) | (r1 >> 1);
 }
 

