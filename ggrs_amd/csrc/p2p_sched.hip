@@ -786,13 +786,19 @@ int p2p_sched_advance(ggrs_p2p_engine* e, int32_t n) {
   }
   // stage geometry: B rows behind a stage's first call (a rollback's confirmed inputs reach back
   // max_prediction frames, a burst after a stall a few more), K calls per stage as many as keep the
-  // block's LDS within 40 KB (four blocks, one per SIMD, per CU) -- at least 8
+  // block's LDS within its share of the CU -- at least 8
   const int P = e->cfg.num_players;
   int WL = 2;
   while (WL < e->cfg.max_prediction + e->cfg.input_delay + 2) WL *= 2;
   const int B = 2 * e->cfg.max_prediction + 4;
-  int K = 64;
-  while (K > 8 && sched_lds(P, e->R, e->sparse, WL, K, B).total > 40 * 1024) K -= 4;
+  // the LDS a block may take without costing residency: 160 KB per CU shared by the blocks each CU
+  // must hold at once (65,536 sessions: four, one per SIMD -> 40 KB; 4,096 sessions: one -> all of it)
+  const int64_t blocks = grid_of(e->cfg.num_sessions, kBlock);
+  const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(4, (blocks + e->num_cus - 1) / e->num_cus));
+  const uint32_t budget = (uint32_t)(160 * 1024 / per_cu) - 1024;
+  // and at most 64 - B, so that a stage's rows fit the control pass's 64-bit change masks (its fast form)
+  int K = std::max(8, std::min(64, 64 - B));
+  while (K > 8 && sched_lds(P, e->R, e->sparse, WL, K, B).total > budget) K -= 4;
   const size_t shm = sched_lds(P, e->R, e->sparse, WL, K, B).total;
   if (shm > 160 * 1024) return set_error(GGRS_E_INVALID, "max_prediction too large for the scheduled kernel's LDS");
   SchedParams p;
