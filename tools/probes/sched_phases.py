@@ -21,9 +21,9 @@ for _ in range(launches):
 eng.synchronize()
 rb, rs = eng.stats()
 import os
-seg = "stamps2" in os.environ.get("GGRS_AMD_EXP_LIB", "")
+seg = "stamps3" in os.environ.get("GGRS_AMD_EXP_LIB", "")
 blocks = np.asarray(rs).reshape(-1, 64)[:, :8].astype(np.float64)
-names = (["call start", "replay switch", "decisions + local input", "inputs", "save", "advance", "-", "iterations"]
+names = (["staging", "control", "call start", "decisions + local input", "inputs + save", "advance", "step loop", "iterations"]
          if seg else ["staging", "control", "step loop", "stage loop total"])
 for k, n in enumerate(names):
     col = blocks[:, k]
