@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <type_traits>
 #include <vector>
@@ -76,18 +77,24 @@ struct SchedParams {
 // [stage start - B, stage end) with their row tags.
 struct SchedLds {
   uint32_t o_tags, o_lq, o_arr, o_rowtag, o_rows, total;  // byte offsets (32-bit: scalar registers are scarce)
+  uint32_t rec_b, rowtag_b, rows_b;                       // bytes of one stage buffer of each
 };
 __host__ __device__ inline uint32_t align16(uint32_t x) { return (x + 15) & ~15u; }
 __host__ __device__ inline int input_word_bytes(int P) { return P <= 1 ? 1 : (P == 2 ? 2 : 4); }
-__host__ __device__ inline SchedLds sched_lds(int P, int R, int sparse, int WL, int K, int B) {
+// nbuf: stage buffers (records, row tags, rows): 2 when the control pass of stage i + 1 runs on a
+// second wave beside stage i's step loop
+__host__ __device__ inline SchedLds sched_lds(int P, int R, int sparse, int WL, int K, int B, int nbuf = 1) {
   SchedLds l;
   const uint32_t ring = (uint32_t)R * (cell_dwords_s(P) / 4) * kBlock * 16;
   l.o_tags = ring;
   l.o_lq = align16(l.o_tags + (sparse ? (uint32_t)R * kBlock * 4 : 0u));
   l.o_arr = align16(l.o_lq + (uint32_t)WL * kBlock * input_word_bytes(P));
-  l.o_rowtag = align16(l.o_arr + (uint32_t)K * kBlock * (sparse ? 8 : 4));  // the calls' records
-  l.o_rows = align16(l.o_rowtag + (uint32_t)(K + B) * 4);
-  l.total = align16(l.o_rows + (uint32_t)(K + B) * kBlock * input_word_bytes(P));
+  l.rec_b = align16((uint32_t)K * kBlock * (sparse ? 8 : 4));  // the calls' records
+  l.o_rowtag = l.o_arr + (uint32_t)nbuf * l.rec_b;
+  l.rowtag_b = align16((uint32_t)(K + B) * 4);
+  l.o_rows = l.o_rowtag + (uint32_t)nbuf * l.rowtag_b;
+  l.rows_b = align16((uint32_t)(K + B) * kBlock * input_word_bytes(P));
+  l.total = l.o_rows + (uint32_t)nbuf * l.rows_b;
   return l;
 }
 constexpr int kArrTooFar = 0xfe;  // a burst of >= 254 frames: past the device queue (GGRS_E_PRECONDITION)
@@ -106,23 +113,27 @@ enum : uint32_t { kStopNone = 0, kStopBefore = 1, kStopAfterSave0 = 2, kStopAfte
 // kSparse: sparse saving; kPred: the predictor (0 repeat-last, 1 PredictDefault) -- compile-time, so
 // their tests leave the step loop and its scalar registers
 // kLocal: the local-player mask when it is a compile-time one (two players, one of them local: the
-// usual peer), else -1
-template <int P, bool kSparse, int kPred, int kLocal>
-__global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
+// usual peer), else -1.  kSplit: two waves per block of 64 sessions -- wave 1 stages the input rows
+// of stage i + 1 and runs its control pass while wave 0 runs stage i's step loop (double-buffered
+// records and rows; one barrier per stage); chosen when a CU holds one block (few sessions), where
+// the two waves sit on two SIMDs of an otherwise idle CU.
+template <int P, bool kSparse, int kPred, int kLocal, bool kSplit>
+__global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel(SchedParams p) {
   using T = typename InputWord<P>::T;
   using Rec = typename std::conditional<kSparse, uint2, uint32_t>::type;
   constexpr int F = state_fields(P);
   constexpr int PC = cell_dwords_s(P) / 4;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const SchedLds L = sched_lds(P, p.R, kSparse, p.WL, p.K, p.B);
+  const SchedLds L = sched_lds(P, p.R, kSparse, p.WL, p.K, p.B, kSplit ? 2 : 1);
+  int buf = 0;  // this wave's stage buffer
   // LDS regions addressed from the extern array itself at each use (pointer variables into dynamic
   // LDS captured by the lambdas below become generic pointers, which this hipcc miscompiles)
 #define lring (reinterpret_cast<uint4*>(lds))
 #define ltag (reinterpret_cast<int32_t*>(lds + L.o_tags))
 #define llq (reinterpret_cast<T*>(lds + L.o_lq))
-#define lrec (reinterpret_cast<Rec*>(lds + L.o_arr))
-#define lrowtag (reinterpret_cast<int32_t*>(lds + L.o_rowtag))
-#define lrows (reinterpret_cast<T*>(lds + L.o_rows))
+#define lrec (reinterpret_cast<Rec*>(lds + L.o_arr + buf * L.rec_b))
+#define lrowtag (reinterpret_cast<int32_t*>(lds + L.o_rowtag + buf * L.rowtag_b))
+#define lrows (reinterpret_cast<T*>(lds + L.o_rows + buf * L.rows_b))
 
   p.cur = in_vgpr_ptr(p.cur);
   p.ring = in_vgpr_ptr(p.ring);
@@ -139,7 +150,9 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
   p.delay = in_vgpr_i32(p.delay);
   const int64_t S = p.S;
   const int64_t sess0 = (int64_t)blockIdx.x * kBlock;
-  const int lt = threadIdx.x;
+  const int lt = threadIdx.x & (kBlock - 1);
+  const bool ctl_w = !kSplit || threadIdx.x >= kBlock;  // this wave stages and decides
+  const bool stp_w = !kSplit || threadIdx.x < kBlock;   // this wave steps the game states
   const bool live = sess0 + lt < S;
   const int64_t s = live ? sess0 + lt : sess0;  // idle lanes shadow the block's first session, never store
   const int nb = (int)min((int64_t)kBlock, S - sess0);
@@ -155,7 +168,7 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
   {
     const uint4* src = reinterpret_cast<const uint4*>(p.ring) + sess0 * ring_pieces;
     const int n = nb * ring_pieces;
-    for (int i = lt; i < n; i += kBlock) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
       const int sl = i / ring_pieces, rem = i - sl * ring_pieces;
       lring[rem * kBlock + sl] = src[i];
     }
@@ -259,11 +272,15 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
     return !kSparse || ltag[back_slot(slot_f, cur - from) * kBlock + lt] == from;
   };
 
-  for (int32_t cs = p.c0; cs < c_end; cs += p.K) {
+  const int nst = (p.n + p.K - 1) / p.K;
+  for (int it = 0; it < nst + (kSplit ? 1 : 0); ++it) {
+   if (ctl_w && it < nst) {
+    const int32_t cs = p.c0 + it * p.K;
     const int32_t ce = min(c_end, cs + p.K);
+    buf = kSplit ? (it & 1) : 0;
     lo = max(0, cs - p.B);
     const int nrows = ce - lo;
-    __syncthreads();  // every lane is done with the previous stage
+    if (!kSplit) __syncthreads();  // every lane is done with the previous stage
     // Staging: every load of a batch is issued before the first is used (one wave per SIMD: a
     // load-use chain per row or call would cost a full memory latency each).
     const int32_t lo_i = lo % p.cap;  // ring slot of row lo
@@ -296,7 +313,13 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
       lrowtag[r] = tag;
       tags_ok &= tag == lo + r;
     }
-    __syncthreads();
+    if (kSplit) {  // this wave's rows in LDS before its lanes read each other's (no block barrier: one wave)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    } else {
+      __syncthreads();
+    }
     // The control pass's fast form (below): every staged row held, and at most 64 of them, so that a
     // lane's "where do the remote inputs change" is one 64-bit mask over the stage's rows (repeat-last:
     // row g differs from row g - 1; PredictDefault: row g is not 0).
@@ -552,6 +575,13 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
       }
     }
 
+   }
+   if (stp_w && it >= (kSplit ? 1 : 0)) {
+    const int si = kSplit ? it - 1 : it;
+    const int32_t cs = p.c0 + si * p.K;
+    const int32_t ce = min(c_end, cs + p.K);
+    buf = kSplit ? (si & 1) : 0;
+    lo = max(0, cs - p.B);
     // ---- step loop: the game states.  One thread per session, each its own step sequence: an
     // iteration is one AdvanceFrame of the lane's current work -- a replayed frame, or its call's own
     // frame -- or a call that does not advance.
@@ -676,17 +706,24 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
       at_start = !rep;
     }
     if (c < ce) s_done = true;  // stopped at an error
+   }
+   if (kSplit) __syncthreads();  // stage it + 1's records ready, stage it's buffers free
   }
   __syncthreads();
   {  // rings back to HBM
     uint4* dst = reinterpret_cast<uint4*>(p.ring) + sess0 * ring_pieces;
     const int n = nb * ring_pieces;
-    for (int i = lt; i < n; i += kBlock) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
       const int sl = i / ring_pieces, rem = i - sl * ring_pieces;
       dst[i] = lring[rem * kBlock + sl];
     }
   }
   if (!live) return;
+  if (stp_w) {  // the step loop's: the local queues and the game state
+    for (int q = 0; q < WL; q++) p.lq[(int64_t)q * S + s] = (uint32_t)llq[q * kBlock + lt];
+    store_state<P>(st, p.cur + s, S);
+  }
+  if (!ctl_w) return;
   for (int q = 0; q < R; q++) {  // the cells' frames
     int32_t fr = kNull;
     if (kSparse) {
@@ -698,8 +735,6 @@ __global__ __launch_bounds__(kBlock) void p2p_sched_kernel(SchedParams p) {
     }
     p.ring_frame[(int64_t)q * S + s] = fr;
   }
-  for (int q = 0; q < WL; q++) p.lq[(int64_t)q * S + s] = (uint32_t)llq[q * kBlock + lt];
-  store_state<P>(st, p.cur + s, S);
   fld(kCur) = cur;
   fld(kLconf) = lconf;
   fld(kDframe) = dframe;
@@ -797,9 +832,17 @@ int p2p_sched_advance(ggrs_p2p_engine* e, int32_t n) {
   const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(4, (blocks + e->num_cus - 1) / e->num_cus));
   const uint32_t budget = (uint32_t)(160 * 1024 / per_cu) - 1024;
   // and at most 64 - B, so that a stage's rows fit the control pass's 64-bit change masks (its fast form)
+  // Two waves per block (the control pass of the next stage beside the step loop) when each CU holds
+  // one block: its second wave runs on a SIMD that would idle (GGRS_SCHED_SPLIT=0 turns it off)
+  const char* split_env = getenv("GGRS_SCHED_SPLIT");
+  const bool split = !e->sparse && per_cu == 1 && blocks <= e->num_cus && !(split_env && split_env[0] == '0');
+  const int nbuf = split ? 2 : 1;
+  // (the two-wave form overlaps all but the first stage's control pass, but shorter stages cost the
+  // step wave more than they hide: 4,096 sessions 180 / 170 / 158 / 156 / 156 us at 8 / 12 / 16 / 24
+  // / 42 calls per stage, profiles/r05ak_k*)
   int K = std::max(8, std::min(64, 64 - B));
-  while (K > 8 && sched_lds(P, e->R, e->sparse, WL, K, B).total > budget) K -= 4;
-  const size_t shm = sched_lds(P, e->R, e->sparse, WL, K, B).total;
+  while (K > 8 && sched_lds(P, e->R, e->sparse, WL, K, B, nbuf).total > budget) K -= 4;
+  const size_t shm = sched_lds(P, e->R, e->sparse, WL, K, B, nbuf).total;
   if (shm > 160 * 1024) return set_error(GGRS_E_INVALID, "max_prediction too large for the scheduled kernel's LDS");
   SchedParams p;
   p.K = K;
@@ -834,23 +877,28 @@ int p2p_sched_advance(ggrs_p2p_engine* e, int32_t n) {
       if (shm > 64 * 1024)
         attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)shm);
-      if (attr == hipSuccess) kern<<<(unsigned)grid_of(p.S, kBlock), kBlock, shm, e->stream>>>(p);
+      if (attr == hipSuccess)
+        kern<<<(unsigned)grid_of(p.S, kBlock), split ? 2 * kBlock : kBlock, shm, e->stream>>>(p);
+    };
+    auto go2 = [&](auto kern1, auto kern2) {
+      if (split) go(kern2);
+      else go(kern1);
     };
     if (p.sparse) {
-      if (p.predictor == 0) go(&p2p_sched_kernel<PP, true, 0, -1>);
-      else go(&p2p_sched_kernel<PP, true, 1, -1>);
+      if (p.predictor == 0) go(&p2p_sched_kernel<PP, true, 0, -1, false>);
+      else go(&p2p_sched_kernel<PP, true, 1, -1, false>);
     } else {
       bool done = false;
       if constexpr (PP == 2) {  // one local player of two, repeat-last: the usual peer, masks compile-time
         if (p.predictor == 0 && (p.local_mask == 1u || p.local_mask == 2u)) {
-          if (p.local_mask == 1u) go(&p2p_sched_kernel<PP, false, 0, 1>);
-          else go(&p2p_sched_kernel<PP, false, 0, 2>);
+          if (p.local_mask == 1u) go2(&p2p_sched_kernel<PP, false, 0, 1, false>, &p2p_sched_kernel<PP, false, 0, 1, true>);
+          else go2(&p2p_sched_kernel<PP, false, 0, 2, false>, &p2p_sched_kernel<PP, false, 0, 2, true>);
           done = true;
         }
       }
       if (!done) {
-        if (p.predictor == 0) go(&p2p_sched_kernel<PP, false, 0, -1>);
-        else go(&p2p_sched_kernel<PP, false, 1, -1>);
+        if (p.predictor == 0) go2(&p2p_sched_kernel<PP, false, 0, -1, false>, &p2p_sched_kernel<PP, false, 0, -1, true>);
+        else go2(&p2p_sched_kernel<PP, false, 1, -1, false>, &p2p_sched_kernel<PP, false, 1, -1, true>);
       }
     }
   });

@@ -160,12 +160,16 @@ def test_p2p_arrival_schedule_rejects(oracle):
     assert errors[10] == 0 and frames[10] == 48 and skipped[10] == 0
 
 
+@pytest.mark.parametrize("split", ["1", "0"])
 @pytest.mark.parametrize("stalls,delay,local", [(False, 0, (0,)), (True, 0, (0,)), (False, 2, (1,))])
-def test_p2p_synth_schedules_every_session(oracle, stalls, delay, local):
+def test_p2p_synth_schedules_every_session(oracle, monkeypatch, stalls, delay, local, split):
     """The bench's schedules (synth.jitter_arrivals: jittered lags, optionally network stalls past
     max_prediction) for every one of 640 sessions, in launches that cross the kernel's stages at
     different calls -- the control pass's branch-free fast form (every player connected, the rows
-    staged) decides nearly every call here -- state, ring, counts, skips and frames bit-exact."""
+    staged) decides nearly every call here -- state, ring, counts, skips and frames bit-exact; with
+    the two-wave form (control pass of the next stage beside the step loop: the default when every
+    CU holds one block, as here) and the one-wave form (GGRS_SCHED_SPLIT=0, the many-session form)."""
+    monkeypatch.setenv("GGRS_SCHED_SPLIT", split)
     from ggrs_amd import P2PEngine, synth
     S, calls, P, mp = 640, 200, 2, 8
     rows = synth.gen_inputs(0, S, calls, P, synth.MODEL_HELD)
