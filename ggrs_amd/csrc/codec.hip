@@ -767,8 +767,35 @@ __global__ __launch_bounds__(256) void decode_swar_kernel(DecodeParams p) {
           const uint8_t* rle = d + 9;
           const int mm = (int)m;  // <= len - 9 < stride
           int q = 0, xl = 0;      // xl <= kMaxDecoded
+          // one-byte headers (every run of <= 31 fill / 63 literal bytes), the loop left only through
+          // its condition (a break per error costs every iteration exec-mask bookkeeping); a multi-byte
+          // header sends the packet to the general loop below, from the start
+          bool multi = false;
           while (q < mm) {
-            // one-byte headers (every run of <= 31 fill / 63 literal bytes) without the varint loop
+            const uint32_t h = rle[q];
+            const bool one = h < 0x80u, lit = !(h & 1u);
+            const int rl = (int)(lit ? (h >> 1) & 0x3fu : (h >> 2) & 0x1fu);
+            const bool over = one && lit && mm - (q + 1) < rl;
+            if (one && !over) {
+              const bool fits = xl + rl <= kCap;
+              if (lit) {
+                if (fits)
+                  for (int k = 0; k < rl; k++) xb[xl + k] = rle[q + 1 + k];
+              } else if ((h & 2) && fits && rl > 0) {
+                ffm |= ((1ull << rl) - 1) << xl;  // 0xFF bytes, expanded below
+              }
+            }
+            if (over) status = GGRS_CODEC_E_RLE;
+            multi |= !one;
+            xl += rl;
+            q = (!one || over) ? mm : q + 1 + (lit ? rl : 0);
+          }
+          if (multi) {
+            q = 0;
+            xl = 0;
+            ffm = 0;
+          }
+          while (multi && q < mm) {
             uint32_t h = rle[q];
             int rl;
             if (h < 0x80u) {
