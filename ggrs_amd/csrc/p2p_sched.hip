@@ -8,10 +8,13 @@
 // for that uniform network; this is the general one.  Checked against oracle_p2p_sched_run
 // (oracle/ggrs_oracle.c), which steps the restated InputQueue / SyncLayer / P2PSession.
 //
-// One thread per session, each its own step sequence (as p2p_flat_kernel): an iteration is one
-// AdvanceFrame of the lane's current work -- a replayed frame, or its call's own frame -- or a call
-// that does not advance; the call start (poll, disconnect events, first save, rollback decision)
-// runs in the iteration that begins the call.
+// One thread per session.  Per stage of K calls: the input rows are staged in LDS, a control pass
+// takes every decision of the stage's calls (poll, disconnect events, confirmed frame, rollback and
+// its depth, check_last_saved_state, the threshold, the saves' frames, errors) without the game
+// state, call by call, and writes one record per call; then the step loop replays and advances, each
+// lane its own step sequence (an iteration is one AdvanceFrame -- a replayed frame or the call's own
+// -- or a call that does not advance).  With one block per CU the control pass of stage i + 1 runs
+// on a second wave beside stage i's step loop.
 //
 // Per-session device state (between launches, HBM):
 //   cur   [F][S] u32        the game state after the last call (the handler's State)
