@@ -652,8 +652,12 @@ __global__ __launch_bounds__(256) void encode_swar_kernel(EncodeParams p) {
         const uint32_t len = (uint32_t)(nx - i);
         const bool fill = ((zm | fm) >> i) & 1;
         const uint32_t h = fill ? (len << 2) | (uint32_t)((fm >> i) & 1) << 1 | 1u : len << 1;  // < 2^14
-        o[pos++] = (uint8_t)((h & 0x7fu) | (h >= 0x80u ? 0x80u : 0u));
-        if (h >= 0x80u) o[pos++] = (uint8_t)(h >> 7);
+        if constexpr (4 * NDW <= 31) {  // runs of <= 31 bytes: every header is one LEB128 byte
+          o[pos++] = (uint8_t)h;
+        } else {
+          o[pos++] = (uint8_t)((h & 0x7fu) | (h >= 0x80u ? 0x80u : 0u));
+          if (h >= 0x80u) o[pos++] = (uint8_t)(h >> 7);
+        }
         if (!fill)
           for (int q = i; q < nx; q++) o[pos++] = xb[q];
       }
