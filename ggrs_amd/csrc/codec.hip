@@ -658,8 +658,10 @@ __global__ __launch_bounds__(256) void encode_swar_kernel(EncodeParams p) {
           o[pos++] = (uint8_t)((h & 0x7fu) | (h >= 0x80u ? 0x80u : 0u));
           if (h >= 0x80u) o[pos++] = (uint8_t)(h >> 7);
         }
-        if (!fill)
-          for (int q = i; q < nx; q++) o[pos++] = xb[q];
+        if (!fill) {  // (a literal run has >= 1 byte; most have exactly one: no loop for them)
+          o[pos++] = xb[i];
+          for (int q = i + 1; q < nx; q++) o[pos++] = xb[q];
+        }
       }
       const int rle = pos - 9;
       code = pos > stride ? GGRS_CODEC_E_CAP : pos;
@@ -783,8 +785,10 @@ __global__ __launch_bounds__(256) void decode_swar_kernel(DecodeParams p) {
             if (one && !over) {
               const bool fits = xl + rl <= kCap;
               if (lit) {
-                if (fits)
-                  for (int k = 0; k < rl; k++) xb[xl + k] = rle[q + 1 + k];
+                if (fits && rl > 0) {  // (most literal runs are one byte: no loop for them)
+                  xb[xl] = rle[q + 1];
+                  for (int k = 1; k < rl; k++) xb[xl + k] = rle[q + 1 + k];
+                }
               } else if ((h & 2) && fits && rl > 0) {
                 ffm |= ((1ull << rl) - 1) << xl;  // 0xFF bytes, expanded below
               }
