@@ -23,6 +23,8 @@
 //   decode out: inputs [N][W][B], count [N], status [N]
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 using namespace ggrs;
@@ -629,26 +631,33 @@ __global__ __launch_bounds__(256) void encode_swar_kernel(EncodeParams p) {
       code = GGRS_CODEC_E_INVALID;
     } else {
       const int L = n * B;
-      uint64_t zm = 0, fm = 0;
+      // byte-class masks, one bit per delta byte: 32-bit when the stream has at most 32 bytes
+      using Mk = typename std::conditional<(4 * NDW <= 32), uint32_t, uint64_t>::type;
+      constexpr int kMb = 8 * (int)sizeof(Mk);
+      auto ctzm = [](Mk v) -> int {
+        if constexpr (sizeof(Mk) == 4) return (int)__builtin_ctz(v);
+        else return (int)__builtin_ctzll(v);
+      };
+      Mk zm = 0, fm = 0;
       uint32_t* xrow = reinterpret_cast<uint32_t*>(l_x + t * x_pitch);
 #pragma unroll
       for (int k = 0; k < NDW; k++) {
-        zm |= (uint64_t)zero_byte_bits(xw[k]) << (4 * k);
-        fm |= (uint64_t)zero_byte_bits(~xw[k]) << (4 * k);
+        zm |= (Mk)zero_byte_bits(xw[k]) << (4 * k);
+        fm |= (Mk)zero_byte_bits(~xw[k]) << (4 * k);
         xrow[k] = xw[k];
       }
-      const uint64_t valid = L >= 64 ? ~0ull : ((1ull << L) - 1);
+      const Mk valid = L >= kMb ? ~(Mk)0 : (((Mk)1 << L) - 1);
       zm &= valid;
       fm &= valid;
       // a run starts where the class (0x00 / 0xFF / literal) changes
-      uint64_t starts = ((zm ^ (zm << 1)) | (fm ^ (fm << 1)) | 1ull) & valid;
+      Mk starts = ((zm ^ (zm << 1)) | (fm ^ (fm << 1)) | (Mk)1) & valid;
       uint8_t* o = l_out + t * out_pitch;
       const uint8_t* xb = l_x + t * x_pitch;
       int pos = 9;
       while (starts) {
-        const int i = (int)__builtin_ctzll(starts);
+        const int i = ctzm(starts);
         starts &= starts - 1;
-        const int nx = starts ? (int)__builtin_ctzll(starts) : L;
+        const int nx = starts ? ctzm(starts) : L;
         const uint32_t len = (uint32_t)(nx - i);
         const bool fill = ((zm | fm) >> i) & 1;
         const uint32_t h = fill ? (len << 2) | (uint32_t)((fm >> i) & 1) << 1 | 1u : len << 1;  // < 2^14
@@ -733,7 +742,10 @@ __global__ __launch_bounds__(256) void decode_swar_kernel(DecodeParams p) {
     for (int k = 0; k < NDW; k++) xr32[k] = 0;  // 0x00 runs need no writes
     int64_t cnt = 0;
     int32_t status = GGRS_CODEC_OK;
-    uint64_t ffm = 0;  // fast path: one bit per scratch byte inside a 0xFF run
+    // one bit per scratch byte inside a 0xFF run (32-bit when the scratch row has at most 32 bytes)
+    using Mf = typename std::conditional<(kCap <= 32), uint32_t, uint64_t>::type;
+    constexpr int kFb = 8 * (int)sizeof(Mf);
+    Mf ffm = 0;
     if (len < 0 || len > stride || len < 1 || d[0] != 0) {
       // a length outside the row, or input_sizes = Some(..) (or a bad tag): the general checks
       // (validate_packet, the same order as decode_kernel), then the runs are expanded
@@ -790,7 +802,7 @@ __global__ __launch_bounds__(256) void decode_swar_kernel(DecodeParams p) {
                   for (int k = 1; k < rl; k++) xb[xl + k] = rle[q + 1 + k];
                 }
               } else if ((h & 2) && fits && rl > 0) {
-                ffm |= ((1ull << rl) - 1) << xl;  // 0xFF bytes, expanded below
+                ffm |= (((Mf)1 << rl) - 1) << xl;  // 0xFF bytes, expanded below (rl <= 31, xl + rl <= kCap)
               }
             }
             if (over) status = GGRS_CODEC_E_RLE;
@@ -827,7 +839,7 @@ __global__ __launch_bounds__(256) void decode_swar_kernel(DecodeParams p) {
                 for (int k = 0; k < rl; k++) xb[xl + k] = rle[q + k];
               q += rl;
             } else if ((h & 2) && fits && rl > 0) {
-              ffm |= (rl >= 64 ? ~0ull : (1ull << rl) - 1) << xl;  // 0xFF bytes, expanded below
+              ffm |= (rl >= kFb ? ~(Mf)0 : ((Mf)1 << rl) - 1) << xl;  // 0xFF bytes, expanded below
             }
             xl += rl;
           }
