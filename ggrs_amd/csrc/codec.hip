@@ -675,8 +675,9 @@ __global__ __launch_bounds__(256) void encode_swar_kernel(EncodeParams p) {
       const int rle = pos - 9;
       code = pos > stride ? GGRS_CODEC_E_CAP : pos;
       if (code > 0) {
-        o[0] = 0;  // input_sizes: None, then the u64 length of encoded_bytes
-        for (int b = 0; b < 8; b++) o[1 + b] = b < 4 ? (uint8_t)((uint32_t)rle >> (8 * b)) : 0;
+        // input_sizes: None (byte 0), then the u64 length of encoded_bytes (bytes 1..8): the row
+        // was zeroed and rle < 2^24, so one dword store (the row starts dword-aligned)
+        *reinterpret_cast<uint32_t*>(o) = (uint32_t)rle << 8;
       } else {
         for (int q = 0; q < pos; q++) o[q] = 0;  // an error row is stored as zeros
       }
