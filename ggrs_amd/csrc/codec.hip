@@ -561,6 +561,9 @@ __host__ __device__ inline int swar_out_pitch(int stride, int ndw) {
   return odd_dword_pitch(stride > 9 + 12 * ndw ? stride : 9 + 12 * ndw);
 }
 
+// the chunked encode compacts its packets in place of the output rows when a row fits in 16 dwords
+__host__ __device__ constexpr bool encode_in_place(int ndw) { return (9 + 12 * ndw + 3) / 4 <= 16; }
+
 // Chunked packet layout (ggrs_codec_encode_chunked / _decode_chunked): the packets of the 256-packet
 // block b lie back to back from byte b * 256 * stride, each padded to whole dwords (a packet whose
 // length is outside [1, stride] -- an error code -- takes no bytes), so a block's packets are one
@@ -598,8 +601,7 @@ __global__ __launch_bounds__(256) void encode_swar_kernel(EncodeParams p) {
   const int out_pitch = swar_out_pitch(stride, NDW), x_pitch = odd_dword_pitch(4 * NDW);
   uint8_t* l_out = smem;                    // [T][out_pitch]
   uint8_t* l_x = l_out + T * out_pitch;     // [T][x_pitch] delta bytes, for literal copies
-  uint8_t* l_chunk = l_x + T * x_pitch;     // kChunked: [T * stride] the block's packets back to back
-  __shared__ int wsum[4];
+  uint8_t* l_chunk = l_x + T * x_pitch;     // kChunked, NDW > 4: [T * stride] the block's packets back to back
   const int64_t pk0 = (int64_t)blockIdx.x * T;
   const int np = (int)((p.N - pk0) < T ? (p.N - pk0) : T);
   for (int q = threadIdx.x; q < np * out_pitch / 4; q += T) reinterpret_cast<uint32_t*>(l_out)[q] = 0;
@@ -684,7 +686,30 @@ __global__ __launch_bounds__(256) void encode_swar_kernel(EncodeParams p) {
     }
     p.out_len[pk] = code;
   }
-  if constexpr (kChunked) {
+  if constexpr (kChunked && encode_in_place(NDW)) {
+    // the block's packets compacted in place of the output rows (a packet's chunk offset is at most
+    // its row's): no staging area, so twice the blocks per CU.  A row has at most kRowDw dwords.
+    constexpr int kRowDw = (9 + 12 * NDW + 3) / 4;
+    int* wsum = reinterpret_cast<int*>(l_x);  // the delta rows, no longer read after this barrier
+    __syncthreads();
+    int total;
+    const int cb = t < np ? chunk_bytes(code, stride) : 0;
+    const int off = block_excl_scan(cb, wsum, &total);  // (its barrier also orders the row writes)
+    const uint32_t* row = reinterpret_cast<const uint32_t*>(l_out + t * out_pitch);
+    uint32_t rr[kRowDw];
+#pragma unroll
+    for (int k = 0; k < kRowDw; k++) rr[k] = 4 * k < cb ? row[k] : 0u;
+    __syncthreads();
+    uint32_t* dst = reinterpret_cast<uint32_t*>(l_out + off);
+#pragma unroll
+    for (int k = 0; k < kRowDw; k++)
+      if (4 * k < cb) dst[k] = rr[k];
+    __syncthreads();
+    uint32_t* out32 = reinterpret_cast<uint32_t*>(p.out + pk0 * stride);
+    const uint32_t* c32 = reinterpret_cast<const uint32_t*>(l_out);
+    for (int q = t; q < total / 4; q += T) out32[q] = c32[q];
+  } else if constexpr (kChunked) {
+    __shared__ int wsum[4];
     int total;
     const int cb = t < np ? chunk_bytes(code, stride) : 0;
     const int off = block_excl_scan(cb, wsum, &total);  // (its barrier also orders the row writes)
@@ -888,7 +913,8 @@ __global__ __launch_bounds__(256) void decode_swar_kernel(DecodeParams p) {
 }
 
 size_t encode_swar_bytes(int ndw, int stride, bool chunked = false) {
-  return (size_t)256 * (swar_out_pitch(stride, ndw) + odd_dword_pitch(4 * ndw) + (chunked ? stride : 0));
+  return (size_t)256 * (swar_out_pitch(stride, ndw) + odd_dword_pitch(4 * ndw) +
+                        (chunked && !encode_in_place(ndw) ? stride : 0));
 }
 size_t decode_swar_bytes(int ndw, int B, int W, int stride) {
   return (size_t)256 * (odd_dword_pitch(stride) + odd_dword_pitch(4 * ndw));
