@@ -278,7 +278,12 @@ int handler_drive_p2p_groups(ggrs_engine_t** engs, int32_t G, int32_t L, int32_t
   double t_work = 0, t_submit = 0, t_wait = 0, t_sess = 0;
   uint64_t acc = 0;
   int32_t prev_call[MAX_GROUPS];
-  int err = 0;
+  /* err: the first failure; written under `omp critical` by workers and by the master, so atomic.
+   * step_err: its value when the master released step e -- every thread of the step reads that
+   * one (ordered by the release/acquire chain on `ready`), so no two threads of a step disagree
+   * on whether to hand back or encode */
+  _Atomic int err = 0;
+  int step_err = 0;
   const double t0 = now_s();
   /* One parallel region for the whole run: the threads persist across calls (a fork/join per group
    * and call cost more than the encoding itself).  Step e = (call, group): the
@@ -296,21 +301,22 @@ int handler_drive_p2p_groups(ggrs_engine_t** engs, int32_t G, int32_t L, int32_t
       const int q = (int)(e % G);
       group_t* gq = &g[q];
       if (tid == 0) {
-        if (gq->pending && !err) {
+        if (gq->pending && !atomic_load_explicit(&err, memory_order_relaxed)) {
           const double ta = now_s();
           int32_t failed = 0;
           int rc = ggrs_lane_batch_wait(engs[q], &failed);
-          if (rc) err = rc;
+          if (rc) atomic_store_explicit(&err, rc, memory_order_relaxed);
           t_wait += now_s() - ta;
           if (!deferred) spin_us(session_us); /* the session logic after the checksums are back */
         }
+        step_err = atomic_load_explicit(&err, memory_order_relaxed);
         atomic_store_explicit(&ready, e, memory_order_release);
       } else {
         while (atomic_load_explicit(&ready, memory_order_acquire) < e) __builtin_ia32_pause();
       }
       const double tw = now_s();
       const int32_t l0 = (int32_t)((int64_t)Lg * tid / nt), l1 = (int32_t)((int64_t)Lg * (tid + 1) / nt);
-      const int handback = gq->pending && !err, encode = c < c_begin + n_calls && !err;
+      const int handback = gq->pending && !step_err, encode = c < c_begin + n_calls && !step_err;
       const int32_t pc = prev_call[q];
       for (int32_t l = l0; l < l1; l++) {
         const int32_t lane = gq->base + l, m = lane % M;
@@ -330,10 +336,10 @@ int handler_drive_p2p_groups(ggrs_engine_t** engs, int32_t G, int32_t L, int32_t
           if (rc) {
 #pragma omp critical
             { /* the fixture's lists are valid: any rejection is an error here */
-              if (!err) {
+              if (!atomic_load_explicit(&err, memory_order_relaxed)) {
                 strncpy(g_drv_error, ggrs_last_error(), sizeof g_drv_error - 1);
                 g_drv_error[sizeof g_drv_error - 1] = 0;
-                err = rc;
+                atomic_store_explicit(&err, rc, memory_order_relaxed);
               }
             }
           }
@@ -346,11 +352,11 @@ int handler_drive_p2p_groups(ggrs_engine_t** engs, int32_t G, int32_t L, int32_t
         while (atomic_load_explicit(&done, memory_order_acquire) < want) __builtin_ia32_pause();
         t_work += now_s() - tw;
         gq->pending = 0;
-        if (encode && !err) {
+        if (encode && !atomic_load_explicit(&err, memory_order_relaxed)) {
           gq->run = gq->b;
           const double tb = now_s();
           int rc = ggrs_lane_batch_submit(engs[q], &gq->run, GGRS_BATCH_STATUS);
-          if (rc) err = rc;
+          if (rc) atomic_store_explicit(&err, rc, memory_order_relaxed);
           gq->pending = rc == 0;
           prev_call[q] = c;
           t_submit += now_s() - tb;
@@ -363,7 +369,7 @@ int handler_drive_p2p_groups(ggrs_engine_t** engs, int32_t G, int32_t L, int32_t
       }
     }
   }
-  if (err) return err;
+  if (atomic_load_explicit(&err, memory_order_relaxed)) return atomic_load_explicit(&err, memory_order_relaxed);
   *seconds = now_s() - t0;
   if (phases) { /* encode + hand-back (barriers included), submit, wait, session logic */
     phases[0] = t_work;

@@ -2045,7 +2045,8 @@ int ggrs_p2p_set_sparse_saving(ggrs_p2p_engine_t* e, int32_t on) {
   if (on && !e->last_saved) {
     HIP_TRY(hipMalloc(&e->last_saved, sizeof(int32_t) * S));
     HIP_TRY(hipMemsetAsync(e->last_saved, 0xff, sizeof(int32_t) * S, e->stream));  // NULL_FRAME
-    HIP_TRY(hipMalloc(&e->ring_frame, sizeof(int32_t) * e->R * S));
+    // (scheduled mode may have allocated the cell frames already: p2p_sched_enable)
+    if (!e->ring_frame) HIP_TRY(hipMalloc(&e->ring_frame, sizeof(int32_t) * e->R * S));
     HIP_TRY(hipMemsetAsync(e->ring_frame, 0xff, sizeof(int32_t) * e->R * S, e->stream));
   }
   // ignored in lockstep mode, as the reference does (p2p_session.rs:187-197)

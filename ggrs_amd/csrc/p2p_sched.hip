@@ -398,7 +398,9 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
               resim += d;
               const int32_t lc = min(confirmed, cur);  // set_last_confirmed_frame
               if (lbytes) local_last = cur + p.delay == local_last + 1 ? cur + p.delay : local_last;  // add_local_input
-              const bool adv = cur - lc < maxp;  // the prediction threshold (:393-423)
+              // the prediction threshold (:393-423): frames_ahead is current_frame while nothing is
+              // confirmed (PredictDefault lets a session with nothing delivered take this form)
+              const bool adv = (lc == kNull ? cur : cur - lc) < maxp;
               lconf = lc;
               last_saved = cur;
               cur = adv ? cur + 1 : cur;

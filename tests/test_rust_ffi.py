@@ -138,10 +138,25 @@ def test_constants_match():
         assert rs[k] == v, k
 
 
-def test_build_rs_compiles_every_unit():
+def test_build_rs_compiles_every_unit_with_build_py_flags():
     """build.rs hands hipcc the same translation units as ggrs_amd/build.py (a unit missing there
-    leaves its symbols undefined in the crate's library)."""
+    leaves its symbols undefined in the crate's library), with the same common flags and the same
+    per-unit flags (max-ilp on the step-kernel units), so the crate links the library bench.py
+    measures."""
     from ggrs_amd import build
     src = open(os.path.join(ROOT, "rust", "ggrs-mi355x", "build.rs")).read()
-    units = set(re.findall(r'csrc\.join\("(\w+\.(?:hip|cpp))"\)', src))
-    assert units == set(build.UNITS)
+
+    def str_list(name):
+        m = re.search(r"const %s: &\[&str\] = &\[(.*?)\];" % name, src, re.S)
+        assert m, name
+        return re.findall(r'"([^"]*)"', m.group(1))
+
+    assert str_list("FLAGS") == build.FLAGS
+    lists = {"ILP": str_list("ILP"), "NONE": str_list("NONE")}
+    assert lists["ILP"] == build.ILP and lists["NONE"] == []
+    m = re.search(r"const UNITS: &\[\(&str, &\[&str\]\)\] = &\[(.*?)\];", src, re.S)
+    assert m
+    units = re.findall(r'\("(\w+\.(?:hip|cpp))",\s*(\w+)\)', m.group(1))
+    assert [u for u, _ in units] == list(build.UNITS)
+    for unit, flags in units:
+        assert lists[flags] == build.UNIT_FLAGS.get(unit, []), unit
