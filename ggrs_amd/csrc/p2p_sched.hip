@@ -59,6 +59,7 @@ struct SchedParams {
   int64_t S;
   int32_t R, delay, cap, maxp, c0, n, predictor, sparse;
   int32_t K, B, WL;  // calls per stage, rows kept behind a stage's first call, local-queue frames (2^k)
+  int32_t TW;        // the time-aligned form's table frames (2^k)
   uint32_t local_mask;
   uint32_t* cur;
   uint32_t* ring;
@@ -112,6 +113,320 @@ constexpr int kArrTooFar = 0xfe;  // a burst of >= 254 frames: past the device q
 // row it needs is no longer held): 1 before the call's work, 2 after the first frame's save, 3 after
 // the first replay.
 enum : uint32_t { kStopNone = 0, kStopBefore = 1, kStopAfterSave0 = 2, kStopAfterReplay1 = 3 };
+
+// The dynamic LDS of both scheduled kernels (regions addressed by byte offset at each use:
+// pointer variables into dynamic LDS captured by lambdas become generic pointers, which this hipcc
+// miscompiles)
+extern __shared__ __attribute__((aligned(16))) uint8_t sched_lds_base[];
+
+// One session's control state (SyncLayer / InputQueue / connect status), advanced call by call by
+// the control pass; the step loops keep their own copies of what the inputs of a frame depend on.
+template <int P>
+struct SchedCtl {
+  int32_t cur, lconf, dframe, last_saved, delivered, local_last, skips, err;
+  uint32_t disc;
+  int32_t lf[P];  // the remote players' last frames (local_connect_status[k].last_frame): the newest
+                  // delivered frame for a connected player, frozen at its disconnect
+  int32_t slot_f;  // ring slot of the current frame
+  int32_t rollbacks;
+  int64_t resim;
+};
+
+// What a call of the control pass reads besides the session's state: the stage's staged rows
+// (LDS byte offsets of this stage's row tags and rows, `ns` sessions per row), the input ring, the
+// sparse cell tags.
+struct SchedCtlEnv {
+  int32_t lo, maxp, R, delay, cap;
+  int64_t S, s;
+  uint32_t lmask, lbytes, rbytes;
+  uint32_t o_rowtag, o_rows, o_tags;
+  int ns, col;  // sessions per LDS row and this session's column
+  const uint8_t* inputs;
+  const int32_t* row_tag;
+};
+
+// P2PSession::advance_frame's decisions for call c (p2p_session.rs:265-426) without the game state:
+// updates `q` and returns the call's record (word 0; word 1 with sparse saving, see below).
+// a_c: the newest remote frame this call's poll delivered; e_c: its Event::Disconnected bits;
+// mask_ok / cm: the fast form's precondition and change mask over the stage's rows.
+template <int P, bool kSparse, int kPred>
+__device__ __forceinline__ uint2 sched_control_call(SchedCtl<P>& q, const SchedCtlEnv& x, bool mask_ok, uint64_t cm,
+                                                    int32_t c, int32_t a_c, uint32_t e_c) {
+  using T = typename InputWord<P>::T;
+  const int32_t lo = x.lo, maxp = x.maxp, R = x.R;
+  const uint32_t lmask = x.lmask, lbytes = x.lbytes, rbytes = x.rbytes;
+  auto next_slot = [&](int32_t v) { return v + 1 == R ? 0 : v + 1; };
+  auto back_slot = [&](int32_t v, int32_t d) { const int32_t y = v - d; return y < 0 ? y + R : y; };
+  // a row's frame tag: staged, or (older than the stage's window: a session far behind its calls)
+  // from the input ring
+  auto row_ok = [&](int32_t g) -> bool {
+    return g >= lo ? reinterpret_cast<const int32_t*>(sched_lds_base + x.o_rowtag)[g - lo] == g
+                   : x.row_tag[g % x.cap] == g;
+  };
+  auto row = [&](int32_t g) -> uint32_t {
+    if (g >= lo) return (uint32_t)reinterpret_cast<const T*>(sched_lds_base + x.o_rows)[(g - lo) * x.ns + x.col];
+    return load_inputs<P>(x.inputs, (int64_t)(g % x.cap) * x.S + x.s);
+  };
+  auto tag = [&](int32_t slot) -> int32_t& {
+    return reinterpret_cast<int32_t*>(sched_lds_base + x.o_tags)[slot * x.ns + x.col];
+  };
+  // the remote InputQueues in canonical form (the kernel comment): the prediction from frame d
+  auto base_of = [&](int32_t d, uint32_t cb) -> uint32_t { return (kPred == 0 && d != kNull) ? row(d) & cb : 0u; };
+  // the rows [a, b] all held (a replay's confirmed inputs)
+  auto rows_ok = [&](int32_t a, int32_t b) -> bool {
+    bool ok = true;
+    for (int32_t g = a; g <= b; ++g) ok &= row_ok(g);
+    return ok;
+  };
+  // load_frame's asserts (sync_layer.rs:218-241) and, with sparse saving, cell.frame == frame_to_load
+  auto replay_ok = [&](int32_t from) -> bool {
+    if (from == kNull || from >= q.cur || from < q.cur - maxp) return false;
+    return !kSparse || tag(back_slot(q.slot_f, q.cur - from)) == from;
+  };
+
+  uint32_t rec = 0, rec2 = 0, stop = kStopNone;
+  // Fast form: a lane with every player connected, no disconnect pending, its rows staged, and
+  // nothing in this call that the reference would panic at -- the common call, branch-free.
+  bool fast = false;
+  if (mask_ok && !q.err) {
+    const int32_t a = a_c;
+    const int32_t up = max(a, q.delivered);
+    const int32_t last = min(up, q.cur - 1);
+    // the burst's simulated frames (delivered, last]: bits lo_b .. hi_b of the change mask
+    const int lo_b = (q.delivered - lo + 1) & 63, hi_b = (last - lo) & 63;
+    const uint64_t win = (last - lo >= 63 ? ~0ull : (2ull << hi_b) - 1) & ~((1ull << lo_b) - 1);
+    const uint64_t hit = last > q.delivered ? cm & win : 0ull;
+    const int32_t mis = hit ? lo + (int32_t)__builtin_ctzll(hit) : kNull;
+    // (bitwise: every test evaluated, no branch per test)
+    fast = (a <= c) & (q.disc == 0u) & (e_c == 0u) & (q.dframe == kNull) & (q.cur >= 1) & (q.cur >= lo) &
+           (q.delivered >= (kPred == 0 ? lo : lo - 1)) & (lbytes == 0u || q.local_last != kNull) &
+           (up - q.delivered < kArrTooFar) & (up < q.cur - maxp + kQ - 1) & (mis == kNull || mis >= q.cur - maxp);
+    if (fast) {
+      const int32_t code = up - q.delivered;
+      q.delivered = up;
+#pragma unroll
+      for (int k = 0; k < P; k++)
+        if ((rbytes >> (8 * k)) & 1u) q.lf[k] = up;
+      int32_t confirmed = INT32_MAX;  // confirmed_frame (:542-553), every player connected
+      if (lbytes) confirmed = q.local_last;
+      if (rbytes) confirmed = min(confirmed, up);
+      // adjust_gamestate from the first misprediction (its replay's saves end below the current
+      // frame's, which becomes the last save)
+      const bool rb = mis != kNull;
+      const uint32_t d = rb ? (uint32_t)(q.cur - mis) : 0u;
+      q.rollbacks += rb ? 1 : 0;
+      q.resim += d;
+      const int32_t lc = min(confirmed, q.cur);  // set_last_confirmed_frame
+      if (lbytes) q.local_last = q.cur + x.delay == q.local_last + 1 ? q.cur + x.delay : q.local_last;  // add_local_input
+      // the prediction threshold (:393-423): frames_ahead is current_frame while nothing is
+      // confirmed (PredictDefault lets a session with nothing delivered take this form)
+      const bool adv = (lc == kNull ? q.cur : q.cur - lc) < maxp;
+      q.lconf = lc;
+      q.last_saved = q.cur;
+      q.cur = adv ? q.cur + 1 : q.cur;
+      q.slot_f = adv ? next_slot(q.slot_f) : q.slot_f;
+      q.skips += adv ? 0 : 1;
+      rec = d | (adv ? 1u << 7 : 0u) | 1u << 10 | (uint32_t)code << 16;
+    }
+  }
+  if (fast) {
+  } else if (q.err) {
+    stop = kStopBefore;
+  } else {
+    // 1. poll_remote_clients: the burst of remote frames (delivered, up] for the remote players
+    //    still connected (handle_event Event::Input, p2p_session.rs:880-895)
+    const int32_t code = a_c > c ? -1 : (a_c > q.delivered ? min(a_c - q.delivered, kArrTooFar) : 0);
+    uint32_t cb = rbytes;  // bytes of the remote players still connected
+#pragma unroll
+    for (int k = 0; k < P; k++)
+      if ((q.disc >> k) & 1u) cb &= ~(0xffu << (8 * k));
+    const int32_t up = q.delivered + code;
+    bool bad = false;
+    if (code < 0) {  // a frame after its call: the remote peer cannot have sent it yet
+      q.err = GGRS_E_INVALID;
+    } else if (code == kArrTooFar || up >= q.cur - maxp + kQ - 1) {
+      // the reference's InputQueue holds 128 inputs (input_queue.rs:6) and panics past them; the
+      // device keeps the same bound on how far the remote inputs may run ahead of the session
+      q.err = GGRS_E_PRECONDITION;
+    } else {
+      // add_input_by_frame's first_incorrect_frame: the first frame of the burst the session has
+      // simulated whose inputs differ from the prediction (the canonical form)
+      int32_t mis = kNull;
+      if (cb) {
+        if (kPred == 0 && q.delivered != kNull) bad |= !row_ok(q.delivered);
+        const uint32_t pb = base_of(q.delivered, cb);
+        const int32_t last = min(up, q.cur - 1);
+        for (int32_t g = q.delivered + 1; g <= last; ++g) {
+          bad |= !row_ok(g);
+          if ((row(g) & cb) != pb) {
+            mis = g;
+            break;
+          }
+        }
+      }
+      if (bad) {
+        q.err = GGRS_E_PRECONDITION;  // a remote input no longer in the input rows
+        goto call_done;
+      }
+      q.delivered = up;
+#pragma unroll
+      for (int k = 0; k < P; k++)
+        if ((cb >> (8 * k)) & 1u) q.lf[k] = up;
+      // Event::Disconnected (p2p_session.rs:866-878 -> disconnect_player_at_frame :618-655)
+      const uint32_t ev = e_c & ((1u << P) - 1u);
+#pragma unroll
+      for (int k = 0; k < P; k++) {
+        if (!((ev >> k) & 1u) || ((lmask >> k) & 1u) || ((q.disc >> k) & 1u)) continue;
+        q.disc |= 1u << k;
+        cb &= ~(0xffu << (8 * k));
+        if (q.cur > q.lf[k]) q.dframe = q.lf[k] + 1;
+      }
+      if (kPred == 0 && q.delivered != kNull) bad |= !row_ok(q.delivered);  // the prediction's row
+      rec = (uint32_t)code << 16 | ev << 24;
+      if (bad) {
+        q.err = GGRS_E_PRECONDITION;  // a remote input no longer in the input rows
+      } else {
+        // 2. the first frame's save (:305-308)
+        if (q.cur == 0) {
+          q.last_saved = 0;
+          if (kSparse) tag(q.slot_f) = 0;
+        }
+        // confirmed_frame (:542-553): the newest frame every connected player has sent
+        int32_t confirmed = INT32_MAX;
+#pragma unroll
+        for (int k = 0; k < P; k++) {
+          if ((q.disc >> k) & 1u) continue;
+          confirmed = min(confirmed, ((lmask >> k) & 1u) ? q.local_last : q.lf[k]);
+        }
+        stop = kStopAfterSave0;
+        if (confirmed == INT32_MAX) {  // assert!(confirmed < i32::MAX)
+          q.err = GGRS_E_PRECONDITION;
+        } else {
+          // 3. check_simulation_consistency(disconnect_frame) (sync_layer.rs:343-353) +
+          //    adjust_gamestate (p2p_session.rs:658-714)
+          int32_t first_inc = q.dframe;
+          if (mis != kNull && (first_inc == kNull || mis < first_inc)) first_inc = mis;
+          if (first_inc != kNull) {
+            const int32_t from = kSparse ? q.last_saved : first_inc;
+            if (!replay_ok(from) || !rows_ok(from, min(q.cur - 1, q.delivered))) {
+              q.err = GGRS_E_PRECONDITION;
+            } else {
+              const int32_t d = q.cur - from;
+              rec |= (uint32_t)d;
+              q.rollbacks += 1;
+              q.resim += d;
+              q.dframe = kNull;
+              // the replay's saves (:692-702)
+              if (kSparse) {
+                if (confirmed >= from && confirmed < q.cur) {
+                  rec2 |= (uint32_t)(confirmed - from + 1) << 8;
+                  q.last_saved = confirmed;
+                  tag(back_slot(q.slot_f, q.cur - confirmed)) = confirmed;
+                }
+              } else if (d >= 2) {
+                q.last_saved = q.cur - 1;
+              }
+            }
+          }
+          bool save_own = !kSparse;
+          // sparse saving: check_last_saved_state (:819-843) once the rollback's replay is done
+          if (!q.err && kSparse && q.cur - q.last_saved >= maxp) {
+            if (confirmed >= q.cur) {
+              save_own = true;
+            } else if (!replay_ok(q.last_saved)) {
+              q.err = GGRS_E_PRECONDITION;
+              stop = kStopAfterReplay1;
+            } else if (!rows_ok(q.last_saved, min(q.cur - 1, q.delivered))) {
+              q.err = GGRS_E_PRECONDITION;
+            } else {
+              const int32_t d2 = q.cur - q.last_saved;
+              rec2 |= (uint32_t)d2;
+              q.rollbacks += 1;
+              q.resim += d2;
+              if (confirmed >= q.last_saved && confirmed < q.cur) {
+                rec2 |= (uint32_t)(confirmed - q.last_saved + 1) << 16;
+                tag(back_slot(q.slot_f, q.cur - confirmed)) = confirmed;
+                q.last_saved = confirmed;
+              }
+            }
+          }
+          if (!q.err) {
+            // set_last_confirmed_frame (sync_layer.rs:313-340), after this call's saves
+            int32_t lc = confirmed;
+            const int32_t ls = save_own ? q.cur : q.last_saved;
+            if (kSparse && ls < lc) lc = ls;
+            if (q.cur < lc) lc = q.cur;
+            // add_local_input for every local player (:362-377, input_queue.rs:170-186): queue
+            // frame current + delay, dropped unless it is the next one
+            int32_t ll = q.local_last;
+            if (lbytes) {
+              const int32_t qf = q.cur + x.delay;
+              if (q.local_last == kNull || qf == q.local_last + 1) ll = qf;
+            }
+            // the prediction threshold (:393-423)
+            const int32_t ahead = lc == kNull ? q.cur : q.cur - lc;
+            const bool adv = ahead < maxp;
+            if ((lbytes && !row_ok(c)) || (adv && q.cur <= q.delivered && !row_ok(q.cur))) {
+              q.err = GGRS_E_PRECONDITION;
+            } else {
+              q.lconf = lc;
+              q.local_last = ll;
+              if (save_own) {
+                q.last_saved = q.cur;
+                if (kSparse) tag(q.slot_f) = q.cur;
+              }
+              rec |= (adv ? 1u << 7 : 0u) | (save_own ? 1u << 10 : 0u);
+              if (adv) {
+                ++q.cur;
+                q.slot_f = next_slot(q.slot_f);
+              } else {
+                ++q.skips;
+              }
+              stop = kStopNone;
+            }
+          }
+        }
+      }
+    }
+  call_done:
+    if (q.err && stop == kStopNone) stop = kStopBefore;
+  }
+  rec |= stop << 8;
+  return make_uint2(rec, rec2);
+}
+
+// A launch's end: the control state back to HBM (sst), the counts, and -- without sparse saving,
+// where every frame 0 .. last save has been saved -- each cell's frame, the newest one <= the last
+// save in its slot.
+template <int P>
+__device__ inline void sched_store_ctl(const SchedParams& p, const SchedCtl<P>& q, int64_t s, bool cell_frames) {
+  const int64_t S = p.S;
+  if (cell_frames) {
+    for (int r = 0; r < p.R; r++) {
+      int32_t fr = kNull;
+      if (q.last_saved != kNull) {
+        const int32_t d = (q.last_saved - r) % p.R;
+        fr = q.last_saved - (d < 0 ? d + p.R : d);
+        if (fr < 0) fr = kNull;
+      }
+      p.ring_frame[(int64_t)r * S + s] = fr;
+    }
+  }
+  auto fld = [&](int f) -> int32_t& { return p.sst[(int64_t)f * S + s]; };
+  fld(kCur) = q.cur;
+  fld(kLconf) = q.lconf;
+  fld(kDframe) = q.dframe;
+  fld(kLastSaved) = q.last_saved;
+  fld(kDelivered) = q.delivered;
+  fld(kLocalLast) = q.local_last;
+  fld(kSkips) = q.skips;
+  fld(kErr) = q.err;
+  fld(kDisc) = (int32_t)q.disc;
+#pragma unroll
+  for (int k = 0; k < P; k++) fld(kPl0 + kPlFields * k + 0) = q.lf[k];
+  p.rollbacks[s] += q.rollbacks;
+  p.resim[s] += q.resim;
+}
 
 // kSparse: sparse saving; kPred: the predictor (0 repeat-last, 1 PredictDefault) -- compile-time, so
 // their tests leave the step loop and its scalar registers
@@ -186,24 +501,29 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
   BoxState<P> st;
   load_state<P>(st, p.cur + s, S);
   auto fld = [&](int f) -> int32_t& { return p.sst[(int64_t)f * S + s]; };
-  // The control state (SyncLayer / InputQueue / connect status), advanced call by call by the control
-  // pass; the step loop keeps its own copies of what the inputs of a frame depend on.
-  int32_t cur = fld(kCur), lconf = fld(kLconf), dframe = fld(kDframe), last_saved = fld(kLastSaved);
-  int32_t delivered = fld(kDelivered), local_last = fld(kLocalLast), skips = fld(kSkips), err = fld(kErr);
-  uint32_t disc = (uint32_t)fld(kDisc);
-  // the remote players' last frames (local_connect_status[k].last_frame): the newest delivered frame
-  // for a connected player, frozen at its disconnect
-  int32_t lf[P];
+  // The control state, advanced call by call by the control pass (sched_control_call); the step loop
+  // keeps its own copies of what the inputs of a frame depend on.
+  SchedCtl<P> q;
+  q.cur = fld(kCur);
+  q.lconf = fld(kLconf);
+  q.dframe = fld(kDframe);
+  q.last_saved = fld(kLastSaved);
+  q.delivered = fld(kDelivered);
+  q.local_last = fld(kLocalLast);
+  q.skips = fld(kSkips);
+  q.err = fld(kErr);
+  q.disc = (uint32_t)fld(kDisc);
 #pragma unroll
-  for (int k = 0; k < P; k++) lf[k] = fld(kPl0 + kPlFields * k + 0);
-  if (!live) err = 1;  // idle lanes run no call
-  int32_t s_cur = cur, s_delivered = delivered, s_local_last = local_last, s_lf[P];
-  uint32_t s_disc = disc;
-  bool s_done = err != 0;
+  for (int k = 0; k < P; k++) q.lf[k] = fld(kPl0 + kPlFields * k + 0);
+  if (!live) q.err = 1;  // idle lanes run no call
+  q.slot_f = q.cur % R;
+  q.rollbacks = 0;
+  q.resim = 0;
+  int32_t s_cur = q.cur, s_delivered = q.delivered, s_local_last = q.local_last, s_lf[P];
+  uint32_t s_disc = q.disc;
+  bool s_done = q.err != 0;
 #pragma unroll
-  for (int k = 0; k < P; k++) s_lf[k] = lf[k];
-  int32_t rollbacks = 0;
-  int64_t resim = 0;
+  for (int k = 0; k < P; k++) s_lf[k] = q.lf[k];
   // every state the launch steps descends from cur or from a ring cell this engine wrote, all in the
   // lean step's rotation domain: one wave-wide test instead of one per player per step
   const bool lean_ok = __all(rot_in_domain<P>(st));
@@ -214,8 +534,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
 
   auto next_slot = [&](int32_t x) { return x + 1 == R ? 0 : x + 1; };
   auto back_slot = [&](int32_t x, int32_t d) { const int32_t y = x - d; return y < 0 ? y + R : y; };
-  int32_t slot_f = cur % R;    // control: ring slot of the current frame
-  int32_t s_slot_f = slot_f;   // step loop: the same
+  int32_t s_slot_f = q.slot_f;  // step loop: ring slot of the current frame
   auto cell_load = [&](int32_t slot) {
 #pragma unroll
     for (int k = 0; k < PC; k++) {
@@ -241,40 +560,12 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
 
   const int32_t c_end = p.c0 + p.n;
   int32_t lo = 0;  // the stage's rows: frames / calls [lo, ce)
-  // a row's frame tag: staged, or (older than the stage's window: a session far behind its calls)
-  // from the input ring
-  auto row_ok = [&](int32_t g) -> bool { return g >= lo ? lrowtag[g - lo] == g : p.row_tag[g % p.cap] == g; };
   // input row g (frame g's remote inputs, call g's local ones); the control pass has checked that
   // every row the step loop reads is held
   auto row = [&](int32_t g) -> uint32_t {
     if (g >= lo) return (uint32_t)lrows[(g - lo) * kBlock + lt];
     return load_inputs<P>(p.inputs, (int64_t)(g % p.cap) * S + s);
   };
-  // The remote InputQueues in their canonical form.  Every frame a session has simulated used, for
-  // a connected remote player, its input if it had arrived (frame <= lf) and otherwise the
-  // prediction made from the newest arrived one (repeat-last: its input; PredictDefault, or nothing
-  // arrived yet: 0; lib.rs:390-406, input_queue.rs:128-161): a prediction, once made, is kept until
-  // an arrival contradicts it (add_input_by_frame's first_incorrect_frame, input_queue.rs:190-230),
-  // and an arrival that confirms it leaves "the newest input" equal to it, so the value predicted for
-  // every simulated frame past lf IS the newest input.  Hence a burst (lf, up] is mispredicted at the
-  // first g < current_frame whose input differs from the newest input before the burst, a rollback's
-  // replay (reset_prediction, then synchronized_inputs per frame) uses the confirmed inputs up to lf
-  // and the newest input after, and no per-frame prediction / last_requested bookkeeping is needed.
-  auto base_of = [&](int32_t d, uint32_t cb) -> uint32_t {
-    return (kPred == 0 && d != kNull) ? row(d) & cb : 0u;
-  };
-  // the rows [a, b] all held (a replay's confirmed inputs)
-  auto rows_ok = [&](int32_t a, int32_t b) -> bool {
-    bool ok = true;
-    for (int32_t g = a; g <= b; ++g) ok &= row_ok(g);
-    return ok;
-  };
-  // load_frame's asserts (sync_layer.rs:218-241) and, with sparse saving, cell.frame == frame_to_load
-  auto replay_ok = [&](int32_t from) -> bool {
-    if (from == kNull || from >= cur || from < cur - maxp) return false;
-    return !kSparse || ltag[back_slot(slot_f, cur - from) * kBlock + lt] == from;
-  };
-
   const int nst = (p.n + p.K - 1) / p.K;
   for (int it = 0; it < nst + (kSplit ? 1 : 0); ++it) {
    if (ctl_w && it < nst) {
@@ -294,8 +585,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
 #pragma unroll 8
       for (int u = lt; u < units; u += kBlock) {  // (unrolled: the global loads issue back to back)
         const int r = u / kUpr, k = u - r * kUpr;
-        int32_t ri = lo_i + r;
-        ri = ri >= p.cap ? ri - p.cap : ri;
+        const int32_t ri = (lo_i + r) % p.cap;  // (a stage may span more rows than the ring holds)
         reinterpret_cast<uint4*>(lrows)[u] =
             reinterpret_cast<const uint4*>(p.inputs + ((int64_t)ri * S + sess0) * sizeof(T))[k];
       }
@@ -303,15 +593,13 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
       const T* src = reinterpret_cast<const T*>(p.inputs) + sess0 + lt;
 #pragma unroll 8
       for (int r = 0; r < nrows; r++) {
-        int32_t ri = lo_i + r;
-        ri = ri >= p.cap ? ri - p.cap : ri;
+        const int32_t ri = (lo_i + r) % p.cap;  // (a stage may span more rows than the ring holds)
         if (lt < nb) lrows[r * kBlock + lt] = src[(int64_t)ri * S];
       }
     }
     bool tags_ok = true;
     for (int r = lt; r < nrows; r += kBlock) {
-      int32_t ri = lo_i + r;
-      ri = ri >= p.cap ? ri - p.cap : ri;
+      const int32_t ri = (lo_i + r) % p.cap;
       const int32_t tag = p.row_tag[ri];
       lrowtag[r] = tag;
       tags_ok &= tag == lo + r;
@@ -340,15 +628,32 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
     // ---- control pass: P2PSession::advance_frame's decisions for calls [cs, ce), call by call
     // (every lane at the same call), without the game state; one record per call
     {
+      SchedCtlEnv env;
+      env.lo = lo;
+      env.maxp = maxp;
+      env.R = R;
+      env.delay = p.delay;
+      env.cap = p.cap;
+      env.S = S;
+      env.s = s;
+      env.lmask = lmask;
+      env.lbytes = lbytes;
+      env.rbytes = rbytes;
+      env.o_rowtag = L.o_rowtag + buf * L.rowtag_b;
+      env.o_rows = L.o_rows + buf * L.rows_b;
+      env.o_tags = L.o_tags;
+      env.ns = kBlock;
+      env.col = lt;
+      env.inputs = p.inputs;
+      env.row_tag = p.row_tag;
       const int32_t ci0 = cs % p.cap;
       for (int32_t cb8 = cs; cb8 < ce; cb8 += 8) {
         int32_t up8[8];
         uint32_t ev8[8];
 #pragma unroll
         for (int j = 0; j < 8; j++) {  // this session's arrivals and Event::Disconnected bits, eight calls at a time
-          int32_t ci = ci0 + (cb8 - cs) + j;
-          ci = ci >= p.cap ? ci - p.cap : ci;
-          const bool in = !err && cb8 + j < ce;
+          const int32_t ci = (ci0 + (cb8 - cs) + j) % p.cap;
+          const bool in = !q.err && cb8 + j < ce;
           up8[j] = in ? p.arrive[(int64_t)ci * S + s] : kNull;
           ev8[j] = (in && p.events) ? p.events[(int64_t)ci * S + s] : 0u;
         }
@@ -364,217 +669,10 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
             up8[k] = up8[k + 1];
             ev8[k] = ev8[k + 1];
           }
-          uint32_t rec = 0, rec2 = 0, stop = kStopNone;
-          // Fast form: a lane with every player connected, no disconnect pending, its rows staged,
-          // and nothing in this call that the reference would panic at -- the common call, branch-free.
-          bool fast = false;
-          if (mask_ok && !err) {
-            const int32_t a = a_c;
-            const int32_t up = max(a, delivered);
-            const int32_t last = min(up, cur - 1);
-            // the burst's simulated frames (delivered, last]: bits lo_b .. hi_b of the change mask
-            const int lo_b = (delivered - lo + 1) & 63, hi_b = (last - lo) & 63;
-            const uint64_t win = (last - lo >= 63 ? ~0ull : (2ull << hi_b) - 1) & ~((1ull << lo_b) - 1);
-            const uint64_t hit = last > delivered ? cm & win : 0ull;
-            const int32_t mis = hit ? lo + (int32_t)__builtin_ctzll(hit) : kNull;
-            // (bitwise: every test evaluated, no branch per test)
-            fast = (a <= c) & (disc == 0u) & (e_c == 0u) & (dframe == kNull) & (cur >= 1) & (cur >= lo) &
-                   (delivered >= (kPred == 0 ? lo : lo - 1)) & (lbytes == 0u || local_last != kNull) &
-                   (up - delivered < kArrTooFar) & (up < cur - maxp + kQ - 1) & (mis == kNull || mis >= cur - maxp);
-            if (fast) {
-              const int32_t code = up - delivered;
-              delivered = up;
-#pragma unroll
-              for (int k = 0; k < P; k++)
-                if ((rbytes >> (8 * k)) & 1u) lf[k] = up;
-              int32_t confirmed = INT32_MAX;  // confirmed_frame (:542-553), every player connected
-              if (lbytes) confirmed = local_last;
-              if (rbytes) confirmed = min(confirmed, up);
-              // adjust_gamestate from the first misprediction (its replay's saves end below the
-              // current frame's, which becomes the last save)
-              const bool rb = mis != kNull;
-              const uint32_t d = rb ? (uint32_t)(cur - mis) : 0u;
-              rollbacks += rb ? 1 : 0;
-              resim += d;
-              const int32_t lc = min(confirmed, cur);  // set_last_confirmed_frame
-              if (lbytes) local_last = cur + p.delay == local_last + 1 ? cur + p.delay : local_last;  // add_local_input
-              // the prediction threshold (:393-423): frames_ahead is current_frame while nothing is
-              // confirmed (PredictDefault lets a session with nothing delivered take this form)
-              const bool adv = (lc == kNull ? cur : cur - lc) < maxp;
-              lconf = lc;
-              last_saved = cur;
-              cur = adv ? cur + 1 : cur;
-              slot_f = adv ? next_slot(slot_f) : slot_f;
-              skips += adv ? 0 : 1;
-              rec = d | (adv ? 1u << 7 : 0u) | 1u << 10 | (uint32_t)code << 16;
-            }
-          }
-          if (fast) {
-          } else if (err) {
-            stop = kStopBefore;
-          } else {
-            // 1. poll_remote_clients: the burst of remote frames (delivered, up] for the remote players
-            //    still connected (handle_event Event::Input, p2p_session.rs:880-895)
-            const int32_t code = a_c > c ? -1 : (a_c > delivered ? min(a_c - delivered, kArrTooFar) : 0);
-            uint32_t cb = rbytes;  // bytes of the remote players still connected
-#pragma unroll
-            for (int k = 0; k < P; k++)
-              if ((disc >> k) & 1u) cb &= ~(0xffu << (8 * k));
-            const int32_t up = delivered + code;
-            bool bad = false;
-            if (code < 0) {  // a frame after its call: the remote peer cannot have sent it yet
-              err = GGRS_E_INVALID;
-            } else if (code == kArrTooFar || up >= cur - maxp + kQ - 1) {
-              // the reference's InputQueue holds 128 inputs (input_queue.rs:6) and panics past them; the
-              // device keeps the same bound on how far the remote inputs may run ahead of the session
-              err = GGRS_E_PRECONDITION;
-            } else {
-              // add_input_by_frame's first_incorrect_frame: the first frame of the burst the session
-              // has simulated whose inputs differ from the prediction (the canonical form above)
-              int32_t mis = kNull;
-              if (cb) {
-                if (kPred == 0 && delivered != kNull) bad |= !row_ok(delivered);
-                const uint32_t pb = base_of(delivered, cb);
-                const int32_t last = min(up, cur - 1);
-                for (int32_t g = delivered + 1; g <= last; ++g) {
-                  bad |= !row_ok(g);
-                  if ((row(g) & cb) != pb) {
-                    mis = g;
-                    break;
-                  }
-                }
-              }
-              if (bad) {
-                err = GGRS_E_PRECONDITION;  // a remote input no longer in the input rows
-                goto call_done;
-              }
-              delivered = up;
-#pragma unroll
-              for (int k = 0; k < P; k++)
-                if ((cb >> (8 * k)) & 1u) lf[k] = up;
-              // Event::Disconnected (p2p_session.rs:866-878 -> disconnect_player_at_frame :618-655)
-              const uint32_t ev = e_c & ((1u << P) - 1u);
-#pragma unroll
-              for (int k = 0; k < P; k++) {
-                if (!((ev >> k) & 1u) || ((lmask >> k) & 1u) || ((disc >> k) & 1u)) continue;
-                disc |= 1u << k;
-                cb &= ~(0xffu << (8 * k));
-                if (cur > lf[k]) dframe = lf[k] + 1;
-              }
-              if (kPred == 0 && delivered != kNull) bad |= !row_ok(delivered);  // the prediction's row
-              rec = (uint32_t)code << 16 | ev << 24;
-              if (bad) {
-                err = GGRS_E_PRECONDITION;  // a remote input no longer in the input rows
-              } else {
-                // 2. the first frame's save (:305-308)
-                if (cur == 0) {
-                  last_saved = 0;
-                  if (kSparse) ltag[slot_f * kBlock + lt] = 0;
-                }
-                // confirmed_frame (:542-553): the newest frame every connected player has sent
-                int32_t confirmed = INT32_MAX;
-#pragma unroll
-                for (int k = 0; k < P; k++) {
-                  if ((disc >> k) & 1u) continue;
-                  confirmed = min(confirmed, ((lmask >> k) & 1u) ? local_last : lf[k]);
-                }
-                stop = kStopAfterSave0;
-                if (confirmed == INT32_MAX) {  // assert!(confirmed < i32::MAX)
-                  err = GGRS_E_PRECONDITION;
-                } else {
-                  // 3. check_simulation_consistency(disconnect_frame) (sync_layer.rs:343-353) +
-                  //    adjust_gamestate (p2p_session.rs:658-714)
-                  int32_t first_inc = dframe;
-                  if (mis != kNull && (first_inc == kNull || mis < first_inc)) first_inc = mis;
-                  if (first_inc != kNull) {
-                    const int32_t from = kSparse ? last_saved : first_inc;
-                    if (!replay_ok(from) || !rows_ok(from, min(cur - 1, delivered))) {
-                      err = GGRS_E_PRECONDITION;
-                    } else {
-                      const int32_t d = cur - from;
-                      rec |= (uint32_t)d;
-                      rollbacks += 1;
-                      resim += d;
-                      dframe = kNull;
-                      // the replay's saves (:692-702)
-                      if (kSparse) {
-                        if (confirmed >= from && confirmed < cur) {
-                          rec2 |= (uint32_t)(confirmed - from + 1) << 8;
-                          last_saved = confirmed;
-                          ltag[back_slot(slot_f, cur - confirmed) * kBlock + lt] = confirmed;
-                        }
-                      } else if (d >= 2) {
-                        last_saved = cur - 1;
-                      }
-                    }
-                  }
-                  bool save_own = !kSparse;
-                  // sparse saving: check_last_saved_state (:819-843) once the rollback's replay is done
-                  if (!err && kSparse && cur - last_saved >= maxp) {
-                    if (confirmed >= cur) {
-                      save_own = true;
-                    } else if (!replay_ok(last_saved)) {
-                      err = GGRS_E_PRECONDITION;
-                      stop = kStopAfterReplay1;
-                    } else if (!rows_ok(last_saved, min(cur - 1, delivered))) {
-                      err = GGRS_E_PRECONDITION;
-                    } else {
-                      const int32_t d2 = cur - last_saved;
-                      rec2 |= (uint32_t)d2;
-                      rollbacks += 1;
-                      resim += d2;
-                      if (confirmed >= last_saved && confirmed < cur) {
-                        rec2 |= (uint32_t)(confirmed - last_saved + 1) << 16;
-                        ltag[back_slot(slot_f, cur - confirmed) * kBlock + lt] = confirmed;
-                        last_saved = confirmed;
-                      }
-                    }
-                  }
-                  if (!err) {
-                    // set_last_confirmed_frame (sync_layer.rs:313-340), after this call's saves
-                    int32_t lc = confirmed;
-                    const int32_t ls = save_own ? cur : last_saved;
-                    if (kSparse && ls < lc) lc = ls;
-                    if (cur < lc) lc = cur;
-                    // add_local_input for every local player (:362-377, input_queue.rs:170-186): queue
-                    // frame current + delay, dropped unless it is the next one
-                    int32_t ll = local_last;
-                    if (lbytes) {
-                      const int32_t qf = cur + p.delay;
-                      if (local_last == kNull || qf == local_last + 1) ll = qf;
-                    }
-                    // the prediction threshold (:393-423)
-                    const int32_t ahead = lc == kNull ? cur : cur - lc;
-                    const bool adv = ahead < maxp;
-                    if ((lbytes && !row_ok(c)) || (adv && cur <= delivered && !row_ok(cur))) {
-                      err = GGRS_E_PRECONDITION;
-                    } else {
-                      lconf = lc;
-                      local_last = ll;
-                      if (save_own) {
-                        last_saved = cur;
-                        if (kSparse) ltag[slot_f * kBlock + lt] = cur;
-                      }
-                      rec |= (adv ? 1u << 7 : 0u) | (save_own ? 1u << 10 : 0u);
-                      if (adv) {
-                        ++cur;
-                        slot_f = next_slot(slot_f);
-                      } else {
-                        ++skips;
-                      }
-                      stop = kStopNone;
-                    }
-                  }
-                }
-              }
-            }
-          call_done:
-            if (err && stop == kStopNone) stop = kStopBefore;
-          }
-          rec |= stop << 8;
+          const uint2 rr = sched_control_call<P, kSparse, kPred>(q, env, mask_ok, cm, c, a_c, e_c);
           Rec r;
-          if constexpr (kSparse) r = make_uint2(rec, rec2);
-          else r = rec;
+          if constexpr (kSparse) r = rr;
+          else r = rr.x;
           lrec[(c - cs) * kBlock + lt] = r;
         }
       }
@@ -725,40 +823,564 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
   }
   if (!live) return;
   if (stp_w) {  // the step loop's: the local queues and the game state
-    for (int q = 0; q < WL; q++) p.lq[(int64_t)q * S + s] = (uint32_t)llq[q * kBlock + lt];
+    for (int w = 0; w < WL; w++) p.lq[(int64_t)w * S + s] = (uint32_t)llq[w * kBlock + lt];
     store_state<P>(st, p.cur + s, S);
   }
   if (!ctl_w) return;
-  for (int q = 0; q < R; q++) {  // the cells' frames
-    int32_t fr = kNull;
-    if (kSparse) {
-      fr = ltag[q * kBlock + lt];
-    } else if (last_saved != kNull) {  // the newest frame <= the last save in slot q
-      const int32_t d = (last_saved - q) % R;
-      fr = last_saved - (d < 0 ? d + R : d);
-      if (fr < 0) fr = kNull;
-    }
-    p.ring_frame[(int64_t)q * S + s] = fr;
+  if (kSparse) {
+    for (int r = 0; r < R; r++) p.ring_frame[(int64_t)r * S + s] = ltag[r * kBlock + lt];
+    sched_store_ctl<P>(p, q, s, false);
+  } else {
+    sched_store_ctl<P>(p, q, s, true);
   }
-  fld(kCur) = cur;
-  fld(kLconf) = lconf;
-  fld(kDframe) = dframe;
-  fld(kLastSaved) = last_saved;
-  fld(kDelivered) = delivered;
-  fld(kLocalLast) = local_last;
-  fld(kSkips) = skips;
-  fld(kErr) = err;
-  fld(kDisc) = (int32_t)disc;
-#pragma unroll
-  for (int k = 0; k < P; k++) fld(kPl0 + kPlFields * k + 0) = lf[k];
-  p.rollbacks[s] += rollbacks;
-  p.resim[s] += resim;
 #undef lring
 #undef ltag
 #undef llq
 #undef lrec
 #undef lrowtag
 #undef lrows
+}
+
+// ---------------------------------------------------------------------------------------------
+// The time-aligned form (few sessions): a session's calls spread over 16 lanes.
+//
+// After call c every state a session holds -- its current state and every saved cell -- is S_c(h),
+// the state at frame h under the inputs the session knows after call c (the remote players' inputs
+// up to the newest delivered frame, the prediction after; the canonical form above).  A call that
+// rolls back to frame m replays the frames m .. cur - 1 from S_{c-1}(m); every other call saves and
+// advances its own frame.  Those replays are the reference's work (adjust_gamestate,
+// p2p_session.rs:658-714), and they are independent of each other except through the states they
+// start from: so each replay runs as a CHAIN on a lane of its own, and every chain advances frame h
+// at time step h.  At time step h:
+//   * slot 0 (the lineage) holds the session's state at frame h as the calls whose current frame is
+//     h see it, saves the cell of h and advances it with the advancing call's inputs;
+//   * a chain (slots 1..15) holds S_c(h) of its call c: it saves the cell of h and advances;
+//   * a chain starts at its frame m by copying S_{c-1}(m) from the slot that holds it before the
+//     step's exchange -- the newest chain covering m (started before m, ending at or after it),
+//     else the lineage, else (m before the launch's first frame) the ring cell -- and at its call's
+//     current frame hands its state to the lineage (the newest chain ending there);
+//   * of the lanes saving frame h's cell only the newest call's write lands (all compute it).
+// "Newest" is the chain's key -- its rank among the session's rollbacks, i.e. call order -- taken
+// as a max-reduction over the session's 16 lanes (DPP within a row).  The control pass (a fifth
+// wave) takes every call's decisions as in p2p_sched_kernel and only stores, per frame: whether a
+// call has it as its current frame, whether that call advances and with which delivered frame /
+// disconnect mask, the local players' queued input, and the chains starting there (slot, depth,
+// key, inputs).  The step waves run one stage behind it and process frame h once no later call can
+// start a chain at or before h (h < current frame - max_prediction).  A launch thus takes about as
+// many time steps as frames it advances, instead of frames + replays in sequence; the replays cost
+// idle lanes, not time.  Bit-exact with p2p_sched_kernel (the same control pass, the same cells,
+// counts and states; tests/test_gpu_p2p_sched.py runs both forms).
+//
+// Requirements (the host picks p2p_sched_kernel otherwise): no sparse saving, max_prediction <= 12
+// and at most two remote players.  Then chain slots can be dealt round-robin: the chains active at
+// frame h start in [h - max_prediction, h] at strictly increasing frames except a disconnect's
+// rollback to the player's last frame + 1 (at most one per remote player), so at most
+// max_prediction + 3 <= 15 are in flight and the chain 15 ranks later starts after this one ended;
+// and at most two start at one frame.
+constexpr int kCS = 16;          // sessions per block
+constexpr int kSL = 16;          // lanes per session: slot 0 the lineage, slots 1..15 chains
+constexpr int kChainThreads = kCS * kSL + 64;  // four step waves + the control wave
+constexpr int kMaxChainDepth = 12;              // max_prediction of the time-aligned form
+constexpr int kChainMaxK = 32;                  // calls per stage (the control wave's prefetch registers)
+
+// per (frame % TW, session): two uint4
+//   e0.x  the delivered frame of the call at this current frame that advances (the last one there)
+//   e0.y  bit 0 a call has this current frame | 1 it advances | 2-5 its disconnect mask
+//   e0.zw chain 0 starting here: delivered frame, flags (bit 0 valid | 4-7 slot | 8-11 depth |
+//         12-15 disconnect mask | 16-31 key)
+//   e1.xy chain 1 (a second chain starting at the same frame), e1.z the local players' input
+struct ChainLds {
+  uint32_t o_tab, o_rowtag, o_rows, o_arr, o_ev, o_range, o_lf, total;
+  uint32_t rowtag_b, rows_b, arr_b, ev_b;
+};
+__host__ __device__ inline ChainLds chain_lds(int P, int R, int TW, int K, int B) {
+  ChainLds l;
+  l.o_tab = (uint32_t)R * (cell_dwords_s(P) / 4) * kCS * 16;
+  l.rowtag_b = align16((uint32_t)(K + B) * 4);
+  l.rows_b = align16((uint32_t)(K + B) * kCS * input_word_bytes(P));
+  l.arr_b = align16((uint32_t)K * kCS * 4);
+  l.ev_b = align16((uint32_t)K * kCS);
+  l.o_rowtag = l.o_tab + (uint32_t)TW * kCS * 32;
+  l.o_rows = l.o_rowtag + 3 * l.rowtag_b;  // three stage buffers: the control's, the steps', the prefetch's
+  l.o_arr = l.o_rows + 3 * l.rows_b;
+  l.o_ev = l.o_arr + 2 * l.arr_b;
+  l.o_range = l.o_ev + 2 * l.ev_b;
+  l.o_lf = l.o_range + 2 * kCS * 8;
+  l.total = l.o_lf + kCS * 4 * 4;
+  return l;
+}
+
+// max over the 16 lanes of a DPP row, in every lane of it
+__device__ inline int32_t rowmax16(int32_t v) {
+  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
+  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
+  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x141, 0xf, 0xf, false));  // row_half_mirror
+  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x140, 0xf, 0xf, false));  // row_mirror
+  return v;
+}
+
+// A stage's global reads for the control wave (input rows and their tags, arrivals, events), held
+// in registers from their issue to their store into LDS -- one stage ahead, behind the control pass
+template <int P>
+struct ChainStage {
+  static constexpr int kUnitT = 16 / (int)sizeof(typename InputWord<P>::T);
+  static constexpr int kUpr = kCS / kUnitT;  // 16-byte units of one row of the block's sessions
+  uint4 rows[kUpr];
+  int32_t tag;
+  uint4 arr[(kChainMaxK * 4 + 63) / 64];
+  uint4 ev;
+};
+
+template <int P, int kPred, int kLocal>
+__global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedParams p) {
+  using T = typename InputWord<P>::T;
+  constexpr int F = state_fields(P);
+  constexpr int PC = cell_dwords_s(P) / 4;
+  const int TW = p.TW;  // table frames (a power of two)
+  const ChainLds L = chain_lds(P, p.R, TW, p.K, p.B);
+#define lring (reinterpret_cast<uint4*>(sched_lds_base))
+#define ltab (reinterpret_cast<uint4*>(sched_lds_base + L.o_tab))
+#define lrange (reinterpret_cast<int2*>(sched_lds_base + L.o_range))
+#define llf (reinterpret_cast<int32_t*>(sched_lds_base + L.o_lf))
+
+  const int64_t S = p.S;
+  const int64_t sess0 = (int64_t)blockIdx.x * kCS;
+  const int nb = (int)min((int64_t)kCS, S - sess0);
+  const bool ctl_w = threadIdx.x >= kCS * kSL;
+  const uint32_t lmask = kLocal >= 0 ? (uint32_t)kLocal : p.local_mask;
+  uint32_t lbytes = 0;
+#pragma unroll
+  for (int k = 0; k < P; k++) lbytes |= ((lmask >> k) & 1u) ? 0xffu << (8 * k) : 0u;
+  const uint32_t rbytes = (P == 4 ? 0xffffffffu : ((1u << (8 * P)) - 1u)) & ~lbytes;
+  const int32_t maxp = p.maxp, R = p.R;
+  const int ring_pieces = R * PC;
+  const int32_t c_end = p.c0 + p.n;
+  const int nst = (p.n + p.K - 1) / p.K;
+  auto tab0 = [&](int32_t f, int col) -> uint4& { return ltab[((f & (TW - 1)) * kCS + col) * 2]; };
+  auto tab1 = [&](int32_t f, int col) -> uint4& { return ltab[((f & (TW - 1)) * kCS + col) * 2 + 1]; };
+  auto stage_lo = [&](int st) { return max(0, p.c0 + st * p.K - p.B); };
+  auto stage_rows = [&](int st) -> T* { return reinterpret_cast<T*>(sched_lds_base + L.o_rows + (st % 3) * L.rows_b); };
+
+  // ---- copy in: the block's rings
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(p.ring) + sess0 * ring_pieces;
+    const int n = nb * ring_pieces;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const int sl = i / ring_pieces, rem = i - sl * ring_pieces;
+      lring[rem * kCS + sl] = src[i];
+    }
+  }
+
+  if (ctl_w) {
+    // ================= the control wave: lanes 0..15 are the block's sessions =================
+    const int lt = threadIdx.x - kCS * kSL;
+    const int col = lt < kCS ? lt : 0;
+    const bool live = lt < nb;
+    const int64_t s = live ? sess0 + lt : sess0;
+    auto fld = [&](int f) -> int32_t { return p.sst[(int64_t)f * S + s]; };
+    SchedCtl<P> q;
+    q.cur = fld(kCur);
+    q.lconf = fld(kLconf);
+    q.dframe = fld(kDframe);
+    q.last_saved = fld(kLastSaved);
+    q.delivered = fld(kDelivered);
+    q.local_last = fld(kLocalLast);
+    q.skips = fld(kSkips);
+    q.err = fld(kErr);
+    q.disc = (uint32_t)fld(kDisc);
+#pragma unroll
+    for (int k = 0; k < P; k++) q.lf[k] = fld(kPl0 + kPlFields * k + 0);
+    if (!live) q.err = 1;  // idle lanes run no call
+    q.slot_f = q.cur % R;
+    q.rollbacks = 0;
+    q.resim = 0;
+    const int32_t cur0 = q.cur;
+    int32_t own_hi = cur0 - 1, minpre = INT32_MAX, tn = 0, nchain = 0, last_m = kNull, dups = 0;
+    bool started = false;
+    if (lt < kCS) {
+      // the frames before the launch's first one: no call of this launch, no chain yet
+      for (int32_t f = max(0, cur0 - maxp); f < cur0; f++) {
+        tab0(f, col) = make_uint4(0u, 0u, 0u, 0u);
+        *reinterpret_cast<uint2*>(&tab1(f, col)) = make_uint2(0u, 0u);
+      }
+      // the local players' queued inputs still read: frames cur - max_prediction - 1 .. local_last
+      if (q.local_last != kNull)
+        for (int32_t f = max(0, cur0 - maxp - 1); f <= q.local_last; f++)
+          tab1(f, col).z = p.lq[(int64_t)(f & (p.WL - 1)) * S + s];
+#pragma unroll
+      for (int k = 0; k < P; k++) llf[col * 4 + k] = q.lf[k];
+    }
+    // Staging of stage st: its input rows [lo, ce) and their tags, its calls' arrivals and events.
+    // issue() starts the global reads into registers; store() writes them to the stage's buffers.
+    const bool full = nb == kCS && ((S * (int64_t)sizeof(T)) & 15) == 0;
+    ChainStage<P> pf;
+    auto issue = [&](int st) {
+      const int32_t cs = p.c0 + st * p.K, ce = min(c_end, cs + p.K), lo = stage_lo(st);
+      const int nrows = ce - lo, ncalls = ce - cs;
+      const int32_t lo_i = lo % p.cap, ci0 = cs % p.cap;
+#pragma unroll
+      for (int k = 0; k < ChainStage<P>::kUpr; k++) {
+        const int u = lt + 64 * k, r = u / ChainStage<P>::kUpr, kk = u - r * ChainStage<P>::kUpr;
+        const int32_t ri = (lo_i + r) % p.cap;  // (a stage may span more rows than the ring holds)
+        pf.rows[k] = (full && r < nrows)
+                         ? reinterpret_cast<const uint4*>(p.inputs + ((int64_t)ri * S + sess0) * sizeof(T))[kk]
+                         : make_uint4(0u, 0u, 0u, 0u);
+      }
+      {
+        const int32_t ri = (lo_i + lt) % p.cap;
+        pf.tag = lt < nrows ? p.row_tag[ri] : kNull;
+      }
+#pragma unroll
+      for (int k = 0; k < (kChainMaxK * 4 + 63) / 64; k++) {
+        const int u = lt + 64 * k, r = u / 4, kk = u - r * 4;
+        const int32_t ci = (ci0 + min(r, ncalls - 1)) % p.cap;
+        pf.arr[k] = (full && r < ncalls) ? reinterpret_cast<const uint4*>(p.arrive + (int64_t)ci * S + sess0)[kk]
+                                         : make_uint4(0u, 0u, 0u, 0u);
+      }
+      {
+        const int32_t ci = (ci0 + min(lt, ncalls - 1)) % p.cap;
+        pf.ev = (full && lt < ncalls) ? *reinterpret_cast<const uint4*>(p.events + (int64_t)ci * S + sess0)
+                                      : make_uint4(0u, 0u, 0u, 0u);
+      }
+    };
+    auto store = [&](int st) -> bool {
+      const int32_t cs = p.c0 + st * p.K, ce = min(c_end, cs + p.K), lo = stage_lo(st);
+      const int nrows = ce - lo, ncalls = ce - cs;
+      T* lrows = stage_rows(st);
+      int32_t* lrowtag = reinterpret_cast<int32_t*>(sched_lds_base + L.o_rowtag + (st % 3) * L.rowtag_b);
+      int32_t* larr = reinterpret_cast<int32_t*>(sched_lds_base + L.o_arr + (st & 1) * L.arr_b);
+      uint8_t* lev = sched_lds_base + L.o_ev + (st & 1) * L.ev_b;
+      if (full) {
+#pragma unroll
+        for (int k = 0; k < ChainStage<P>::kUpr; k++) {
+          const int u = lt + 64 * k;
+          if (u / ChainStage<P>::kUpr < nrows) reinterpret_cast<uint4*>(lrows)[u] = pf.rows[k];
+        }
+#pragma unroll
+        for (int k = 0; k < (kChainMaxK * 4 + 63) / 64; k++) {
+          const int u = lt + 64 * k;
+          if (u / 4 < ncalls) reinterpret_cast<uint4*>(larr)[u] = pf.arr[k];
+        }
+        if (lt < ncalls) reinterpret_cast<uint4*>(lev)[lt] = pf.ev;
+      } else {  // a partial last block: word by word, read here
+        const int32_t lo_i = lo % p.cap, ci0 = cs % p.cap;
+        for (int r = 0; r < nrows; r++) {
+          const int32_t ri = (lo_i + r) % p.cap;
+          if (lt < nb) lrows[r * kCS + col] = reinterpret_cast<const T*>(p.inputs)[(int64_t)ri * S + sess0 + col];
+        }
+        for (int r = 0; r < ncalls; r++) {
+          int32_t ci = ci0 + r;
+          ci = ci >= p.cap ? ci - p.cap : ci;
+          if (lt < nb) {
+            larr[r * kCS + col] = p.arrive[(int64_t)ci * S + sess0 + col];
+            lev[r * kCS + col] = p.events[(int64_t)ci * S + sess0 + col];
+          }
+        }
+      }
+      if (lt < nrows) lrowtag[lt] = pf.tag;
+      return lt >= nrows || pf.tag == lo + lt;
+    };
+    issue(0);
+    bool tags_ok = store(0);
+    __syncthreads();  // (1) tables and rings in
+
+    for (int it = 0; it <= nst; ++it) {
+      if (it < nst) {
+        const int32_t cs = p.c0 + it * p.K;
+        const int32_t ce = min(c_end, cs + p.K);
+        const int32_t lo = stage_lo(it);
+        const int nrows = ce - lo;
+        const uint32_t o_rowtag = L.o_rowtag + (it % 3) * L.rowtag_b, o_rows = L.o_rows + (it % 3) * L.rows_b;
+        const T* lrows = stage_rows(it);
+        const int32_t* larr = reinterpret_cast<const int32_t*>(sched_lds_base + L.o_arr + (it & 1) * L.arr_b);
+        const uint8_t* lev = sched_lds_base + L.o_ev + (it & 1) * L.ev_b;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // this stage's staging visible to the wave
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (it + 1 < nst) issue(it + 1);  // the next stage's reads fly behind this stage's calls
+        const bool mask_ok = nrows <= 64 && __all(tags_ok);
+        uint64_t cm = 0;
+        if (mask_ok) {
+          uint32_t prev = 0;
+          for (int r = 0; r < nrows; r++) {
+            const uint32_t v = (uint32_t)lrows[r * kCS + col] & rbytes;
+            if (kPred == 0 ? (r > 0 && v != prev) : v != 0u) cm |= 1ull << r;
+            prev = v;
+          }
+        }
+        SchedCtlEnv env;
+        env.lo = lo;
+        env.maxp = maxp;
+        env.R = R;
+        env.delay = p.delay;
+        env.cap = p.cap;
+        env.S = S;
+        env.s = s;
+        env.lmask = lmask;
+        env.lbytes = lbytes;
+        env.rbytes = rbytes;
+        env.o_rowtag = o_rowtag;
+        env.o_rows = o_rows;
+        env.o_tags = 0;
+        env.ns = kCS;
+        env.col = col;
+        env.inputs = p.inputs;
+        env.row_tag = p.row_tag;
+        for (int32_t cb8 = cs; cb8 < ce; cb8 += 8) {
+          // eight calls' arrivals, events and input rows (the local players' input each call queues),
+          // all read before the first is used
+          int32_t up8[8];
+          uint32_t ev8[8], rw8[8];
+#pragma unroll
+          for (int j = 0; j < 8; j++) {
+            const int r = min(cb8 + j, ce - 1) - cs;
+            up8[j] = larr[r * kCS + col];
+            ev8[j] = lev[r * kCS + col];
+            rw8[j] = (uint32_t)lrows[(r + cs - lo) * kCS + col];
+          }
+          for (int j = 0; j < 8; j++) {
+            const int32_t c = cb8 + j;
+            if (c >= ce) break;
+            // the front of the batch, which shifts down a call per iteration (indexing it by j would
+            // put it in scratch memory)
+            const int32_t a_c = q.err ? kNull : up8[0];
+            const uint32_t e_c = q.err ? 0u : ev8[0], rw_c = rw8[0];
+#pragma unroll
+            for (int k = 0; k < 7; k++) {
+              up8[k] = up8[k + 1];
+              ev8[k] = ev8[k + 1];
+              rw8[k] = rw8[k + 1];
+            }
+            const int32_t tau = q.cur, ll0 = q.local_last;
+            const uint32_t disc0 = q.disc;
+            const uint32_t rec = sched_control_call<P, false, kPred>(q, env, mask_ok, cm, c, a_c, e_c).x;
+            if (!live) continue;
+            const uint32_t stop = (rec >> 8) & 3u;
+            // add_local_input: the local players' input of the queued frame (and, the first time,
+            // the default input below the delay)
+            if (lbytes && q.local_last != ll0) {
+              if (ll0 == kNull)
+                for (int32_t f = 0; f < p.delay; f++) tab1(f, col).z = 0u;
+              tab1(q.local_last, col).z = rw_c & lbytes;
+            }
+            if (q.disc != disc0) {  // the disconnected players' last frames, frozen now
+#pragma unroll
+              for (int k = 0; k < P; k++)
+                if (((q.disc ^ disc0) >> k) & 1u) llf[col * 4 + k] = q.lf[k];
+            }
+            if (stop == kStopBefore || (stop == kStopAfterSave0 && tau != 0)) continue;
+            const int32_t d = stop == kStopNone ? (int32_t)(rec & 0x7fu) : 0;
+            if (d) {
+              // the replay of frames m .. tau - 1 as a chain, on the next slot in round-robin order
+              const int32_t m = tau - d;
+              dups = m == last_m ? dups + 1 : 0;
+              if (dups > 1) {
+                q.err = GGRS_E_STATE;  // a third chain at one frame (cannot happen within the requirements)
+                continue;
+              }
+              const uint32_t cf = 1u | (uint32_t)(1 + nchain % (kSL - 1)) << 4 | (uint32_t)d << 8 | q.disc << 12 |
+                                  (uint32_t)nchain << 16;
+              uint2* ce2 = dups ? reinterpret_cast<uint2*>(&tab1(m, col)) : reinterpret_cast<uint2*>(&tab0(m, col)) + 1;
+              *ce2 = make_uint2((uint32_t)q.delivered, cf);
+              ++nchain;
+              last_m = m;
+              if (m < cur0) minpre = min(minpre, m);
+            }
+            // the lineage's work at frame tau (the first call there opens the frame: no chain starts
+            // there yet; a later call at the same frame overwrites the advance and inputs)
+            const uint32_t y = 1u | (stop == kStopNone ? ((rec & 0x80u) ? 2u : 0u) | q.disc << 2 : 0u);
+            const uint32_t x = stop == kStopNone ? (uint32_t)q.delivered : 0u;
+            if (tau > own_hi) {
+              own_hi = tau;
+              tab0(tau, col) = make_uint4(x, y, 0u, 0u);
+              *reinterpret_cast<uint2*>(&tab1(tau, col)) = make_uint2(0u, 0u);
+            } else {
+              *reinterpret_cast<uint2*>(&tab0(tau, col)) = make_uint2(x, y);
+            }
+          }
+        }
+        if (it + 1 < nst) tags_ok = store(it + 1);
+        // the frames the step waves may process: every chain that can still start has m >= cur - max_prediction
+        if (lt < kCS) {
+          const bool last = it == nst - 1 || q.err;
+          const int32_t Tn = last ? own_hi + 1 : q.cur - maxp;
+          if (!started && (last || Tn >= cur0)) {
+            started = true;
+            tn = min(cur0, minpre);
+          }
+          int2 rg = make_int2(0, 0);
+          if (started) {
+            rg = make_int2(tn, max(tn, Tn));
+            tn = rg.y;
+          }
+          lrange[(it & 1) * kCS + col] = rg;
+        }
+      }
+      __syncthreads();  // (2) stage it's tables ready; stage it - 1's steps done
+    }
+    __syncthreads();  // (3) every step done
+    // rings back (every thread), then this session's control state and local queue
+    {
+      uint4* dst = reinterpret_cast<uint4*>(p.ring) + sess0 * ring_pieces;
+      const int n = nb * ring_pieces;
+      for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int sl = i / ring_pieces, rem = i - sl * ring_pieces;
+        dst[i] = lring[rem * kCS + sl];
+      }
+    }
+    if (!live || lt >= kCS) return;
+    if (q.local_last != kNull)
+      for (int32_t f = max(0, q.cur - maxp - 1); f <= q.local_last; f++)
+        p.lq[(int64_t)(f & (p.WL - 1)) * S + s] = tab1(f, col).z;
+    sched_store_ctl<P>(p, q, s, true);
+    return;
+  }
+
+  // ================= the step waves: lane = session (4 per wave) x slot =================
+  const int lane = threadIdx.x;
+  const int j = lane & (kSL - 1), sib = lane / kSL;
+  const bool live = sib < nb;
+  const int64_t s = live ? sess0 + sib : sess0;
+  const int sbase = lane & ~(kSL - 1) & 63;  // the session's first lane in the wave
+  const int32_t cur0 = p.sst[(int64_t)kCur * S + s];  // the launch's first frame (the lineage's)
+  BoxState<P> st;
+  if (j == 0) {
+    load_state<P>(st, p.cur + s, S);
+  } else {
+#pragma unroll
+    for (int k = 0; k < F; k++) st.w[k] = 0u;
+  }
+  const bool lean_ok = __all(j != 0 || rot_in_domain<P>(st));
+  const SincosConsts K = sincos_consts_vgpr();
+  // this slot's chain: active, its first frame, its call's current frame, key (rank), inputs
+  bool act = false;
+  int32_t cm = 0, cend = 0, ckey = 0, cdlv = kNull;
+  uint32_t cdisc = 0;
+  __syncthreads();  // (1)
+  for (int it = 0; it <= nst; ++it) {
+    if (it >= 1) {
+      const int32_t lo = stage_lo(it - 1);
+      const uint32_t o_rows = L.o_rows + ((it - 1) % 3) * L.rows_b;  // (an offset: see sched_lds_base)
+      const int2 rg = lrange[((it - 1) & 1) * kCS + sib];
+      int32_t tau = live ? rg.x : 0;
+      const int32_t te = live ? rg.y : 0;
+      int32_t slot_tau = tau % R;
+      auto row = [&](int32_t g) -> uint32_t {
+        if (g >= lo) return (uint32_t)reinterpret_cast<const T*>(sched_lds_base + o_rows)[(g - lo) * kCS + sib];
+        return load_inputs<P>(p.inputs, (int64_t)(g % p.cap) * S + s);
+      };
+      uint4 e0 = tab0(tau, sib), e1 = tab1(tau, sib);
+      while (__any(tau < te)) {
+        // (every decision by selects, gated by `on`: the wave iterates while any of its sessions has
+        // a frame left)
+        const bool on = tau < te;
+        const int32_t tau1 = on ? tau + 1 : tau;
+        const uint4 n0 = tab0(tau1, sib), n1 = tab1(tau1, sib);  // the next step's entries, read ahead
+        // who holds S(tau) before the exchange (the newest chain started before tau and ending at or
+        // after it) and which chain ends here (the newest), by key over the session's 16 lanes
+        const int32_t me = ckey << 4 | j;
+        const bool hold_c = on & act & (cm < tau) & (tau <= cend);
+        const bool hand_c = on & act & (cend == tau);
+        // a chain starting on this slot at this frame
+        const bool s0 = on & ((e0.w & 1u) != 0u) & (((e0.w >> 4) & 15u) == (uint32_t)j);
+        const bool s1 = on & ((e1.y & 1u) != 0u) & (((e1.y >> 4) & 15u) == (uint32_t)j);
+        const bool sn = s0 | s1;
+        const int32_t hmax = __builtin_amdgcn_ballot_w64(sn) ? rowmax16(hold_c ? me : -1) : -1;
+        const int32_t hdmax = __builtin_amdgcn_ballot_w64(hand_c) ? rowmax16(hand_c ? me : -1) : -1;
+        const uint32_t cf = s0 ? e0.w : e1.y;
+        act = act | sn;
+        cm = sn ? tau : cm;
+        cend = sn ? tau + (int32_t)((cf >> 8) & 15u) : cend;
+        ckey = sn ? (int32_t)(cf >> 16) : ckey;
+        cdlv = sn ? (int32_t)(s0 ? e0.z : e1.x) : cdlv;
+        cdisc = sn ? (cf >> 12) & 15u : cdisc;
+        const bool ring_ld = sn & (hmax < 0) & (tau < cur0);
+        // the lineage: a call has this current frame; it takes the newest chain ending here
+        const bool own = (j == 0) & on & ((e0.y & 1u) != 0u);
+        const int src = sn ? (hmax >= 0 ? (sbase | (hmax & 15)) : sbase)
+                           : ((own & (hdmax >= 0)) ? (sbase | (hdmax & 15)) : (lane & 63));
+        const bool rep = on & (j != 0) & act & (tau < cend);
+        const bool adv = rep | (own & ((e0.y & 2u) != 0u));
+        // the cell of frame tau: the newest replaying chain writes it last, else the lineage
+        const int32_t lwmax = __builtin_amdgcn_ballot_w64(rep) ? rowmax16(rep ? (ckey << 4 | j) : -1) : -1;
+        const bool wr = (rep & ((ckey << 4 | j) == lwmax)) | (own & (lwmax < 0));
+        // synchronized_inputs(tau) (sync_layer.rs:280-293) as the lane's call sees it -- before the
+        // exchange, whose latency its row read shares (computed on every lane, used where it advances)
+        const int32_t dlv = own ? (int32_t)e0.x : cdlv;
+        const uint32_t disc = own ? (e0.y >> 2) & 15u : cdisc;
+        const bool conf = tau <= dlv;
+        const int32_t g = (adv & (dlv != kNull)) ? (conf ? tau : dlv) : lo;
+        uint32_t hrow;
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(g < lo) != 0, 0)) hrow = row(g);  // far behind: the input ring
+        else hrow = (uint32_t)reinterpret_cast<const T*>(sched_lds_base + o_rows)[(g - lo) * kCS + sib];
+        hrow = dlv == kNull ? 0u : hrow;
+        uint32_t conn = rbytes;
+#pragma unroll
+        for (int k = 0; k < P; k++) conn &= ((disc >> k) & 1u) ? ~(0xffu << (8 * k)) : 0xffffffffu;
+        uint32_t in = (lbytes ? e1.z & lbytes : 0u) | ((kPred == 1 && !conf) ? 0u : hrow & conn);
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(adv & (disc != 0u)) != 0, 0)) {
+          // InputStatus::Disconnected past the player's last frame (ex_game spins it: input 4)
+#pragma unroll
+          for (int k = 0; k < P; k++)
+            if ((disc >> k) & 1u) in |= (tau <= llf[sib * 4 + k] ? (hrow >> (8 * k)) & 0xffu : 4u) << (8 * k);
+        }
+        // the exchange: every lane reads its source's state from before it
+        if (__builtin_amdgcn_ballot_w64(src != (lane & 63))) {
+#pragma unroll
+          for (int k = 0; k < F; k++) st.w[k] = (uint32_t)__builtin_amdgcn_ds_bpermute(src << 2, (int)st.w[k]);
+        }
+        if (__builtin_amdgcn_ballot_w64(ring_ld)) {
+          if (ring_ld) {
+#pragma unroll
+            for (int k = 0; k < PC; k++) {
+              const uint4 v = lring[(slot_tau * PC + k) * kCS + sib];
+              const uint32_t x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+              for (int i = 0; i < 4; i++)
+                if (4 * k + i < F) st.w[4 * k + i] = x[i];
+            }
+          }
+        }
+        // SaveGameState of frame tau (sync_layer.rs:208-215, ex_game.rs:103-108)
+        {
+          const uint32_t ck = fletcher16_state<P>(st);
+          if (wr) {
+#pragma unroll
+            for (int k = 0; k < PC; k++) {
+              uint32_t x[4];
+#pragma unroll
+              for (int i = 0; i < 4; i++) x[i] = 4 * k + i < F ? st.w[4 * k + i] : (4 * k + i == F ? ck : 0u);
+              lring[(slot_tau * PC + k) * kCS + sib] = make_uint4(x[0], x[1], x[2], x[3]);
+            }
+          }
+        }
+        if (adv) {
+          if (lean_ok) advance_state_lean_k<P>(st, in, K);
+          else advance_state<P>(st, in, 0u);
+        }
+        e0 = n0;
+        e1 = n1;
+        act = act & !(on & (tau >= cend));  // handed off this step (the lineage read it above)
+        tau = tau1;
+        slot_tau = on ? (slot_tau + 1 == R ? 0 : slot_tau + 1) : slot_tau;
+      }
+    }
+    __syncthreads();  // (2)
+  }
+  __syncthreads();  // (3)
+  {
+    uint4* dst = reinterpret_cast<uint4*>(p.ring) + sess0 * ring_pieces;
+    const int n = nb * ring_pieces;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const int sl = i / ring_pieces, rem = i - sl * ring_pieces;
+      dst[i] = lring[rem * kCS + sl];
+    }
+  }
+  if (live && j == 0) store_state<P>(st, p.cur + s, S);
+#undef lring
+#undef ltab
+#undef lrange
+#undef llf
 }
 
 // every session at frame 0, nothing arrived, every player connected (SyncLayer::new,
@@ -874,8 +1496,50 @@ int p2p_sched_advance(ggrs_p2p_engine* e, int32_t n) {
   p.sst = e->sst;
   p.rollbacks = e->rollbacks;
   p.resim = e->resim;
+  p.TW = 0;
   if (int rc = e->timer.before(e->stream)) return rc;
   hipError_t attr = hipSuccess;
+  // The time-aligned form (a session's replays on 16 lanes) for few sessions: when its blocks of 16
+  // sessions fill at most two per CU.  GGRS_SCHED_CHAINS=0 keeps the one-thread-per-session form.
+  int remote = 0;
+  for (int k = 0; k < P; k++) remote += !((e->cfg.local_mask >> k) & 1);
+  const char* chains_env = getenv("GGRS_SCHED_CHAINS");
+  const int64_t cblocks = grid_of(e->cfg.num_sessions, kCS);
+  const bool chains = !e->sparse && e->cfg.max_prediction <= kMaxChainDepth && remote <= 2 && !(chains_env && chains_env[0] == '0') &&
+                      (cblocks <= 2 * (int64_t)e->num_cus || (chains_env && chains_env[0] == '1'));
+  if (chains) {
+    // K calls per stage: the step waves trail the control wave by a stage, so shorter stages overlap
+    // more of the two; the tables hold the frames of two stages + max_prediction + the delay
+    const char* k_env = getenv("GGRS_SCHED_K");
+    int Kc = k_env ? atoi(k_env) : 16;
+    Kc = std::max(4, std::min(std::min(Kc, 64 - B), kChainMaxK));
+    int TW = 16;
+    while (TW < 2 * Kc + e->cfg.max_prediction + e->cfg.input_delay + 8) TW *= 2;
+    const ChainLds cl = chain_lds(P, e->R, TW, Kc, B);
+    if (cl.total > 160 * 1024) return set_error(GGRS_E_INVALID, "input_delay too large for the scheduled kernel's LDS");
+    p.K = Kc;
+    p.TW = TW;
+    dispatch_players(P, [&](auto PC) {
+      constexpr int PP = decltype(PC)::value;
+      auto go = [&](auto kern) {
+        if (cl.total > 64 * 1024)
+          attr = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)cl.total);
+        if (attr == hipSuccess) kern<<<(unsigned)cblocks, kChainThreads, cl.total, e->stream>>>(p);
+      };
+      if constexpr (PP == 2) {
+        if (p.predictor == 0 && p.local_mask == 1u) return go(&p2p_sched_chains_kernel<PP, 0, 1>);
+        if (p.predictor == 0 && p.local_mask == 2u) return go(&p2p_sched_chains_kernel<PP, 0, 2>);
+      }
+      if (p.predictor == 0) go(&p2p_sched_chains_kernel<PP, 0, -1>);
+      else go(&p2p_sched_chains_kernel<PP, 1, -1>);
+    });
+    HIP_TRY(attr);
+    HIP_TRY(hipGetLastError());
+    e->timer.count();
+    e->current_frame += n;
+    return GGRS_OK;
+  }
   dispatch_players(P, [&](auto PC) {
     constexpr int PP = decltype(PC)::value;
     auto go = [&](auto kern) {

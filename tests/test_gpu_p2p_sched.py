@@ -69,8 +69,19 @@ CASES = [
 ]
 
 
+FORMS = ["chains", "flat"]
+
+
+def set_form(monkeypatch, form):
+    """chains: the time-aligned kernel (a session's replays on 16 lanes; the default for few
+    sessions), flat: one thread per session (GGRS_SCHED_CHAINS=0; the many-session form)."""
+    monkeypatch.setenv("GGRS_SCHED_CHAINS", "1" if form == "chains" else "0")
+
+
+@pytest.mark.parametrize("form", FORMS)
 @pytest.mark.parametrize("P,local,delay,mp,pred,model,sparse", CASES)
-def test_p2p_arrival_schedules_match_oracle(oracle, P, local, delay, mp, pred, model, sparse):
+def test_p2p_arrival_schedules_match_oracle(oracle, monkeypatch, form, P, local, delay, mp, pred, model, sparse):
+    set_form(monkeypatch, form)
     from ggrs_amd import P2PEngine
     S, calls = 200, 240
     mask = sum(1 << k for k in local)
@@ -97,12 +108,14 @@ def test_p2p_arrival_schedules_match_oracle(oracle, P, local, delay, mp, pred, m
     assert rb.sum() > S
 
 
+@pytest.mark.parametrize("form", FORMS)
 @pytest.mark.parametrize("P,local,mp", [(2, (0,), 6), (2, (1,), 9), (3, (0,), 4)])
-def test_p2p_predict_default_silent_start_matches_oracle(oracle, P, local, mp):
+def test_p2p_predict_default_silent_start_matches_oracle(oracle, monkeypatch, form, P, local, mp):
     """PredictDefault sessions that receive nothing for their first 0 .. 2 max_prediction + 3 calls:
     while nothing is confirmed frames_ahead is current_frame (p2p_session.rs:399-405), so the session
     stops advancing at call max_prediction, not one call later.  Lets the control pass's fast form
     (which PredictDefault with nothing delivered may take) meet the NULL confirmed frame."""
+    set_form(monkeypatch, form)
     from ggrs_amd import P2PEngine
     S, calls = 96, 120
     mask = sum(1 << k for k in local)
@@ -189,7 +202,7 @@ def test_p2p_arrival_schedule_rejects(oracle):
     assert errors[10] == 0 and frames[10] == 48 and skipped[10] == 0
 
 
-@pytest.mark.parametrize("split", ["1", "0"])
+@pytest.mark.parametrize("split", ["chains", "1", "0"])
 @pytest.mark.parametrize("stalls,delay,local", [(False, 0, (0,)), (True, 0, (0,)), (False, 2, (1,))])
 def test_p2p_synth_schedules_every_session(oracle, monkeypatch, stalls, delay, local, split):
     """The bench's schedules (synth.jitter_arrivals: jittered lags, optionally network stalls past
@@ -197,8 +210,10 @@ def test_p2p_synth_schedules_every_session(oracle, monkeypatch, stalls, delay, l
     different calls -- the control pass's branch-free fast form (every player connected, the rows
     staged) decides nearly every call here -- state, ring, counts, skips and frames bit-exact; with
     the two-wave form (control pass of the next stage beside the step loop: the default when every
-    CU holds one block, as here) and the one-wave form (GGRS_SCHED_SPLIT=0, the many-session form)."""
-    monkeypatch.setenv("GGRS_SCHED_SPLIT", split)
+    CU holds one block, as here) and the one-wave form (GGRS_SCHED_SPLIT=0, the many-session form),
+    and with the time-aligned form (a session's replays on 16 lanes, the default for few sessions)."""
+    set_form(monkeypatch, "chains" if split == "chains" else "flat")
+    monkeypatch.setenv("GGRS_SCHED_SPLIT", "1" if split == "chains" else split)
     from ggrs_amd import P2PEngine, synth
     S, calls, P, mp = 640, 200, 2, 8
     rows = synth.gen_inputs(0, S, calls, P, synth.MODEL_HELD)
