@@ -145,6 +145,59 @@ struct SchedCtlEnv {
   const int32_t* row_tag;
 };
 
+// The control pass's fast form of call c (see sched_control_call): every player connected, no
+// disconnect pending, the stage's rows staged and held (the change mask cm), nothing the reference
+// would panic at.  Returns whether the call takes it; only then are q and rec updated (by selects:
+// no branch).
+template <int P, int kPred>
+__device__ __forceinline__ bool sched_fast_call(SchedCtl<P>& q, const SchedCtlEnv& x, uint64_t cm, int32_t c,
+                                                int32_t a_c, uint32_t e_c, uint32_t& rec, bool en = true) {
+  const int32_t lo = x.lo, maxp = x.maxp;
+  const uint32_t lbytes = x.lbytes, rbytes = x.rbytes;
+  const int32_t a = a_c;
+  const int32_t up = max(a, q.delivered);
+  const int32_t last = min(up, q.cur - 1);
+  // the burst's simulated frames (delivered, last]: bits lo_b .. hi_b of the change mask
+  const int lo_b = (q.delivered - lo + 1) & 63, hi_b = (last - lo) & 63;
+  const uint64_t win = (last - lo >= 63 ? ~0ull : (2ull << hi_b) - 1) & ~((1ull << lo_b) - 1);
+  const uint64_t hit = last > q.delivered ? cm & win : 0ull;
+  const int32_t mis = hit ? lo + (int32_t)__builtin_ctzll(hit) : kNull;
+  // (bitwise: every test evaluated, no branch per test)
+  const bool fast = en & (a <= c) & (q.disc == 0u) & (e_c == 0u) & (q.dframe == kNull) & (q.cur >= 1) & (q.cur >= lo) &
+                    (q.delivered >= (kPred == 0 ? lo : lo - 1)) & (lbytes == 0u || q.local_last != kNull) &
+                    (up - q.delivered < kArrTooFar) & (up < q.cur - maxp + kQ - 1) & (mis == kNull || mis >= q.cur - maxp);
+  const int32_t code = up - q.delivered;
+  int32_t confirmed = INT32_MAX;  // confirmed_frame (:542-553), every player connected
+  if (lbytes) confirmed = q.local_last;
+  if (rbytes) confirmed = min(confirmed, up);
+  // adjust_gamestate from the first misprediction (its replay's saves end below the current frame's,
+  // which becomes the last save)
+  const bool rb = mis != kNull;
+  const uint32_t d = rb ? (uint32_t)(q.cur - mis) : 0u;
+  const int32_t lc = min(confirmed, q.cur);  // set_last_confirmed_frame
+  const int32_t ll = (lbytes && q.cur + x.delay == q.local_last + 1) ? q.cur + x.delay : q.local_last;  // add_local_input
+  // the prediction threshold (:393-423): frames_ahead is current_frame while nothing is confirmed
+  // (PredictDefault lets a session with nothing delivered take this form)
+  const bool adv = (lc == kNull ? q.cur : q.cur - lc) < maxp;
+  const int32_t nslot = q.slot_f + 1 == x.R ? 0 : q.slot_f + 1;
+  if (fast) {
+    q.delivered = up;
+#pragma unroll
+    for (int k = 0; k < P; k++)
+      if ((rbytes >> (8 * k)) & 1u) q.lf[k] = up;
+    q.rollbacks += rb ? 1 : 0;
+    q.resim += d;
+    q.local_last = ll;
+    q.lconf = lc;
+    q.last_saved = q.cur;
+    q.slot_f = adv ? nslot : q.slot_f;
+    q.cur = adv ? q.cur + 1 : q.cur;
+    q.skips += adv ? 0 : 1;
+    rec = d | (adv ? 1u << 7 : 0u) | 1u << 10 | (uint32_t)code << 16;
+  }
+  return fast;
+}
+
 // P2PSession::advance_frame's decisions for call c (p2p_session.rs:265-426) without the game state:
 // updates `q` and returns the call's record (word 0; word 1 with sparse saving, see below).
 // a_c: the newest remote frame this call's poll delivered; e_c: its Event::Disconnected bits;
@@ -188,47 +241,7 @@ __device__ __forceinline__ uint2 sched_control_call(SchedCtl<P>& q, const SchedC
   // Fast form: a lane with every player connected, no disconnect pending, its rows staged, and
   // nothing in this call that the reference would panic at -- the common call, branch-free.
   bool fast = false;
-  if (mask_ok && !q.err) {
-    const int32_t a = a_c;
-    const int32_t up = max(a, q.delivered);
-    const int32_t last = min(up, q.cur - 1);
-    // the burst's simulated frames (delivered, last]: bits lo_b .. hi_b of the change mask
-    const int lo_b = (q.delivered - lo + 1) & 63, hi_b = (last - lo) & 63;
-    const uint64_t win = (last - lo >= 63 ? ~0ull : (2ull << hi_b) - 1) & ~((1ull << lo_b) - 1);
-    const uint64_t hit = last > q.delivered ? cm & win : 0ull;
-    const int32_t mis = hit ? lo + (int32_t)__builtin_ctzll(hit) : kNull;
-    // (bitwise: every test evaluated, no branch per test)
-    fast = (a <= c) & (q.disc == 0u) & (e_c == 0u) & (q.dframe == kNull) & (q.cur >= 1) & (q.cur >= lo) &
-           (q.delivered >= (kPred == 0 ? lo : lo - 1)) & (lbytes == 0u || q.local_last != kNull) &
-           (up - q.delivered < kArrTooFar) & (up < q.cur - maxp + kQ - 1) & (mis == kNull || mis >= q.cur - maxp);
-    if (fast) {
-      const int32_t code = up - q.delivered;
-      q.delivered = up;
-#pragma unroll
-      for (int k = 0; k < P; k++)
-        if ((rbytes >> (8 * k)) & 1u) q.lf[k] = up;
-      int32_t confirmed = INT32_MAX;  // confirmed_frame (:542-553), every player connected
-      if (lbytes) confirmed = q.local_last;
-      if (rbytes) confirmed = min(confirmed, up);
-      // adjust_gamestate from the first misprediction (its replay's saves end below the current
-      // frame's, which becomes the last save)
-      const bool rb = mis != kNull;
-      const uint32_t d = rb ? (uint32_t)(q.cur - mis) : 0u;
-      q.rollbacks += rb ? 1 : 0;
-      q.resim += d;
-      const int32_t lc = min(confirmed, q.cur);  // set_last_confirmed_frame
-      if (lbytes) q.local_last = q.cur + x.delay == q.local_last + 1 ? q.cur + x.delay : q.local_last;  // add_local_input
-      // the prediction threshold (:393-423): frames_ahead is current_frame while nothing is
-      // confirmed (PredictDefault lets a session with nothing delivered take this form)
-      const bool adv = (lc == kNull ? q.cur : q.cur - lc) < maxp;
-      q.lconf = lc;
-      q.last_saved = q.cur;
-      q.cur = adv ? q.cur + 1 : q.cur;
-      q.slot_f = adv ? next_slot(q.slot_f) : q.slot_f;
-      q.skips += adv ? 0 : 1;
-      rec = d | (adv ? 1u << 7 : 0u) | 1u << 10 | (uint32_t)code << 16;
-    }
-  }
+  if (mask_ok && !q.err) fast = sched_fast_call<P, kPred>(q, x, cm, c, a_c, e_c, rec);
   if (fast) {
   } else if (q.err) {
     stop = kStopBefore;
@@ -911,13 +924,30 @@ __host__ __device__ inline ChainLds chain_lds(int P, int R, int TW, int K, int B
 }
 
 // max over the 16 lanes of a DPP row, in every lane of it
+// (mov_dpp with every row and bank enabled and bound_ctrl: the DPP combiner folds each move into
+// its max as one v_max_i32_dpp; every lane of these patterns reads a lane of its own row)
 __device__ inline int32_t rowmax16(int32_t v) {
-  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
-  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
-  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x141, 0xf, 0xf, false));  // row_half_mirror
-  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x140, 0xf, 0xf, false));  // row_mirror
+  v = max(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, true));   // quad_perm [1,0,3,2]
+  v = max(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, true));   // quad_perm [2,3,0,1]
+  v = max(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xf, 0xf, true));  // row_half_mirror
+  v = max(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xf, 0xf, true));  // row_mirror
   return v;
 }
+
+// the same for two 16-bit signed values at once (v_pk_max_i16 per DPP step)
+typedef short ggrs_s2v __attribute__((ext_vector_type(2)));
+__device__ inline uint32_t rowmax16_pk(uint32_t v) {
+  ggrs_s2v x = __builtin_bit_cast(ggrs_s2v, v);
+#define GGRS_PK_STEP(ctrl) \
+  x = __builtin_elementwise_max(x, __builtin_bit_cast(ggrs_s2v, __builtin_amdgcn_mov_dpp((int)__builtin_bit_cast(uint32_t, x), ctrl, 0xf, 0xf, true)))
+  GGRS_PK_STEP(0xB1);
+  GGRS_PK_STEP(0x4E);
+  GGRS_PK_STEP(0x141);
+  GGRS_PK_STEP(0x140);
+#undef GGRS_PK_STEP
+  return __builtin_bit_cast(uint32_t, x);
+}
+constexpr int kChainMaxCalls = 2000;  // calls per launch: chain keys (ranks) << 4 | slot fit 15 bits
 
 // A stage's global reads for the control wave (input rows and their tags, arrivals, events), held
 // in registers from their issue to their store into LDS -- one stage ahead, behind the control pass
@@ -1080,6 +1110,47 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
       if (lt < nrows) lrowtag[lt] = pf.tag;
       return lt >= nrows || pf.tag == lo + lt;
     };
+    // One call's table entries (its record, the frame it was at, the local players' last queued
+    // frame before / after it, its delivered frame and disconnect mask, its input row).
+    auto emit = [&](int32_t tau, int32_t ll0, int32_t ll1, uint32_t rec, int32_t dlv, uint32_t disc, uint32_t rw_c) {
+      const uint32_t stop = (rec >> 8) & 3u;
+      // add_local_input: the local players' input of the queued frame (and, the first time, the
+      // default input below the delay)
+      if (lbytes && ll1 != ll0) {
+        if (ll0 == kNull)
+          for (int32_t f = 0; f < p.delay; f++) tab1(f, col).z = 0u;
+        tab1(ll1, col).z = rw_c & lbytes;
+      }
+      if (stop == kStopBefore || (stop == kStopAfterSave0 && tau != 0)) return;
+      const int32_t d = stop == kStopNone ? (int32_t)(rec & 0x7fu) : 0;
+      if (d) {
+        // the replay of frames m .. tau - 1 as a chain, on the next slot in round-robin order
+        const int32_t m = tau - d;
+        dups = m == last_m ? dups + 1 : 0;
+        if (dups > 1) {
+          q.err = GGRS_E_STATE;  // a third chain at one frame (cannot happen within the requirements)
+          return;
+        }
+        const uint32_t cf = 1u | (uint32_t)(1 + nchain % (kSL - 1)) << 4 | (uint32_t)d << 8 | disc << 12 |
+                            (uint32_t)nchain << 16;
+        uint2* ce2 = dups ? reinterpret_cast<uint2*>(&tab1(m, col)) : reinterpret_cast<uint2*>(&tab0(m, col)) + 1;
+        *ce2 = make_uint2((uint32_t)dlv, cf);
+        ++nchain;
+        last_m = m;
+        if (m < cur0) minpre = min(minpre, m);
+      }
+      // the lineage's work at frame tau (the first call there opens the frame: no chain starts there
+      // yet; a later call at the same frame overwrites the advance and inputs)
+      const uint32_t y = 1u | (stop == kStopNone ? ((rec & 0x80u) ? 2u : 0u) | disc << 2 : 0u);
+      const uint32_t xx = stop == kStopNone ? (uint32_t)dlv : 0u;
+      if (tau > own_hi) {
+        own_hi = tau;
+        tab0(tau, col) = make_uint4(xx, y, 0u, 0u);
+        *reinterpret_cast<uint2*>(&tab1(tau, col)) = make_uint2(0u, 0u);
+      } else {
+        *reinterpret_cast<uint2*>(&tab0(tau, col)) = make_uint2(xx, y);
+      }
+    };
     issue(0);
     bool tags_ok = store(0);
     __syncthreads();  // (1) tables and rings in
@@ -1102,6 +1173,7 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
         uint64_t cm = 0;
         if (mask_ok) {
           uint32_t prev = 0;
+#pragma unroll 8
           for (int r = 0; r < nrows; r++) {
             const uint32_t v = (uint32_t)lrows[r * kCS + col] & rbytes;
             if (kPred == 0 ? (r > 0 && v != prev) : v != 0u) cm |= 1ull << r;
@@ -1138,6 +1210,34 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
             ev8[j] = lev[r * kCS + col];
             rw8[j] = (uint32_t)lrows[(r + cs - lo) * kCS + col];
           }
+          // The batch's calls through the fast form first, back to back (they depend on each other
+          // only through a few scalars of q); their table entries after.  A batch where some session
+          // needs the general form runs call by call from the state before it.
+          const int nj = min(8, ce - cb8);
+          const bool idle = !live | (q.err != 0);  // runs no call (a stopped session: kStopBefore, no entry)
+          const bool en = !idle & mask_ok;
+          const SchedCtl<P> q0 = q;
+          bool ok = true;
+          uint32_t recs[8];
+          int32_t taus[8], dlvs[8], lls0[8], lls1[8];
+#pragma unroll
+          for (int j = 0; j < 8; j++) {
+            recs[j] = 0u;
+            taus[j] = q.cur;
+            lls0[j] = q.local_last;
+            if (j < nj) ok &= sched_fast_call<P, kPred>(q, env, cm, cb8 + j, up8[j], ev8[j], recs[j], en);
+            dlvs[j] = q.delivered;
+            lls1[j] = q.local_last;
+          }
+          if (__builtin_expect(__all(ok | idle), 1)) {
+            if (en) {
+#pragma unroll
+              for (int j = 0; j < 8; j++)
+                if (j < nj) emit(taus[j], lls0[j], lls1[j], recs[j], dlvs[j], 0u, rw8[j]);
+            }
+            continue;
+          }
+          q = q0;
           for (int j = 0; j < 8; j++) {
             const int32_t c = cb8 + j;
             if (c >= ce) break;
@@ -1155,48 +1255,12 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
             const uint32_t disc0 = q.disc;
             const uint32_t rec = sched_control_call<P, false, kPred>(q, env, mask_ok, cm, c, a_c, e_c).x;
             if (!live) continue;
-            const uint32_t stop = (rec >> 8) & 3u;
-            // add_local_input: the local players' input of the queued frame (and, the first time,
-            // the default input below the delay)
-            if (lbytes && q.local_last != ll0) {
-              if (ll0 == kNull)
-                for (int32_t f = 0; f < p.delay; f++) tab1(f, col).z = 0u;
-              tab1(q.local_last, col).z = rw_c & lbytes;
-            }
             if (q.disc != disc0) {  // the disconnected players' last frames, frozen now
 #pragma unroll
               for (int k = 0; k < P; k++)
                 if (((q.disc ^ disc0) >> k) & 1u) llf[col * 4 + k] = q.lf[k];
             }
-            if (stop == kStopBefore || (stop == kStopAfterSave0 && tau != 0)) continue;
-            const int32_t d = stop == kStopNone ? (int32_t)(rec & 0x7fu) : 0;
-            if (d) {
-              // the replay of frames m .. tau - 1 as a chain, on the next slot in round-robin order
-              const int32_t m = tau - d;
-              dups = m == last_m ? dups + 1 : 0;
-              if (dups > 1) {
-                q.err = GGRS_E_STATE;  // a third chain at one frame (cannot happen within the requirements)
-                continue;
-              }
-              const uint32_t cf = 1u | (uint32_t)(1 + nchain % (kSL - 1)) << 4 | (uint32_t)d << 8 | q.disc << 12 |
-                                  (uint32_t)nchain << 16;
-              uint2* ce2 = dups ? reinterpret_cast<uint2*>(&tab1(m, col)) : reinterpret_cast<uint2*>(&tab0(m, col)) + 1;
-              *ce2 = make_uint2((uint32_t)q.delivered, cf);
-              ++nchain;
-              last_m = m;
-              if (m < cur0) minpre = min(minpre, m);
-            }
-            // the lineage's work at frame tau (the first call there opens the frame: no chain starts
-            // there yet; a later call at the same frame overwrites the advance and inputs)
-            const uint32_t y = 1u | (stop == kStopNone ? ((rec & 0x80u) ? 2u : 0u) | q.disc << 2 : 0u);
-            const uint32_t x = stop == kStopNone ? (uint32_t)q.delivered : 0u;
-            if (tau > own_hi) {
-              own_hi = tau;
-              tab0(tau, col) = make_uint4(x, y, 0u, 0u);
-              *reinterpret_cast<uint2*>(&tab1(tau, col)) = make_uint2(0u, 0u);
-            } else {
-              *reinterpret_cast<uint2*>(&tab0(tau, col)) = make_uint2(x, y);
-            }
+            emit(tau, ll0, q.local_last, rec, q.delivered, q.disc, rw_c);
           }
         }
         if (it + 1 < nst) tags_ok = store(it + 1);
@@ -1269,6 +1333,9 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
         if (g >= lo) return (uint32_t)reinterpret_cast<const T*>(sched_lds_base + o_rows)[(g - lo) * kCS + sib];
         return load_inputs<P>(p.inputs, (int64_t)(g % p.cap) * S + s);
       };
+      // (the loop compiled once per advance form: the general one never runs on states this engine made)
+      auto steps = [&](auto lean_c) {
+      constexpr bool kLean = decltype(lean_c)::value;
       uint4 e0 = tab0(tau, sib), e1 = tab1(tau, sib);
       while (__any(tau < te)) {
         // (every decision by selects, gated by `on`: the wave iterates while any of its sessions has
@@ -1277,7 +1344,8 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
         const int32_t tau1 = on ? tau + 1 : tau;
         const uint4 n0 = tab0(tau1, sib), n1 = tab1(tau1, sib);  // the next step's entries, read ahead
         // who holds S(tau) before the exchange (the newest chain started before tau and ending at or
-        // after it) and which chain ends here (the newest), by key over the session's 16 lanes
+        // after it), which chain ends here (the newest), and which replaying chain writes the cell of
+        // tau last (the newest, a chain starting here included), by key over the session's 16 lanes
         const int32_t me = ckey << 4 | j;
         const bool hold_c = on & act & (cm < tau) & (tau <= cend);
         const bool hand_c = on & act & (cend == tau);
@@ -1285,7 +1353,6 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
         const bool s0 = on & ((e0.w & 1u) != 0u) & (((e0.w >> 4) & 15u) == (uint32_t)j);
         const bool s1 = on & ((e1.y & 1u) != 0u) & (((e1.y >> 4) & 15u) == (uint32_t)j);
         const bool sn = s0 | s1;
-        const int32_t hmax = __builtin_amdgcn_ballot_w64(sn) ? rowmax16(hold_c ? me : -1) : -1;
         const int32_t hdmax = __builtin_amdgcn_ballot_w64(hand_c) ? rowmax16(hand_c ? me : -1) : -1;
         const uint32_t cf = s0 ? e0.w : e1.y;
         act = act | sn;
@@ -1294,25 +1361,28 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
         ckey = sn ? (int32_t)(cf >> 16) : ckey;
         cdlv = sn ? (int32_t)(s0 ? e0.z : e1.x) : cdlv;
         cdisc = sn ? (cf >> 12) & 15u : cdisc;
+        const bool rep = on & (j != 0) & act & (tau < cend);
+        const int32_t me1 = ckey << 4 | j;
+        const uint32_t red = rowmax16_pk((uint32_t)(hold_c ? me : 0xffff) | (uint32_t)(rep ? me1 : 0xffff) << 16);
+        const int32_t hmax = (int32_t)(int16_t)(red & 0xffffu), lwmax = (int32_t)(int16_t)(red >> 16);
         const bool ring_ld = sn & (hmax < 0) & (tau < cur0);
         // the lineage: a call has this current frame; it takes the newest chain ending here
         const bool own = (j == 0) & on & ((e0.y & 1u) != 0u);
         const int src = sn ? (hmax >= 0 ? (sbase | (hmax & 15)) : sbase)
                            : ((own & (hdmax >= 0)) ? (sbase | (hdmax & 15)) : (lane & 63));
-        const bool rep = on & (j != 0) & act & (tau < cend);
         const bool adv = rep | (own & ((e0.y & 2u) != 0u));
         // the cell of frame tau: the newest replaying chain writes it last, else the lineage
-        const int32_t lwmax = __builtin_amdgcn_ballot_w64(rep) ? rowmax16(rep ? (ckey << 4 | j) : -1) : -1;
-        const bool wr = (rep & ((ckey << 4 | j) == lwmax)) | (own & (lwmax < 0));
+        const bool wr = (rep & (me1 == lwmax)) | (own & (lwmax < 0));
         // synchronized_inputs(tau) (sync_layer.rs:280-293) as the lane's call sees it -- before the
         // exchange, whose latency its row read shares (computed on every lane, used where it advances)
         const int32_t dlv = own ? (int32_t)e0.x : cdlv;
         const uint32_t disc = own ? (e0.y >> 2) & 15u : cdisc;
         const bool conf = tau <= dlv;
         const int32_t g = (adv & (dlv != kNull)) ? (conf ? tau : dlv) : lo;
-        uint32_t hrow;
-        if (__builtin_expect(__builtin_amdgcn_ballot_w64(g < lo) != 0, 0)) hrow = row(g);  // far behind: the input ring
-        else hrow = (uint32_t)reinterpret_cast<const T*>(sched_lds_base + o_rows)[(g - lo) * kCS + sib];
+        uint32_t hrow = (uint32_t)reinterpret_cast<const T*>(sched_lds_base + o_rows)[(max(g, lo) - lo) * kCS + sib];
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(g < lo) != 0, 0)) {
+          if (g < lo) hrow = row(g);  // far behind its calls: the input ring
+        }
         hrow = dlv == kNull ? 0u : hrow;
         uint32_t conn = rbytes;
 #pragma unroll
@@ -1355,7 +1425,7 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
           }
         }
         if (adv) {
-          if (lean_ok) advance_state_lean_k<P>(st, in, K);
+          if (kLean) advance_state_lean_k<P>(st, in, K);
           else advance_state<P>(st, in, 0u);
         }
         e0 = n0;
@@ -1364,6 +1434,9 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
         tau = tau1;
         slot_tau = on ? (slot_tau + 1 == R ? 0 : slot_tau + 1) : slot_tau;
       }
+      };
+      if (lean_ok) steps(std::true_type());
+      else steps(std::false_type());
     }
     __syncthreads();  // (2)
   }
@@ -1507,6 +1580,11 @@ int p2p_sched_advance(ggrs_p2p_engine* e, int32_t n) {
   const int64_t cblocks = grid_of(e->cfg.num_sessions, kCS);
   const bool chains = !e->sparse && e->cfg.max_prediction <= kMaxChainDepth && remote <= 2 && !(chains_env && chains_env[0] == '0') &&
                       (cblocks <= 2 * (int64_t)e->num_cus || (chains_env && chains_env[0] == '1'));
+  if (chains && n > kChainMaxCalls) {
+    int rc = p2p_sched_advance(e, kChainMaxCalls);
+    if (rc) return rc;
+    return p2p_sched_advance(e, n - kChainMaxCalls);
+  }
   if (chains) {
     // K calls per stage: the step waves trail the control wave by a stage, so shorter stages overlap
     // more of the two; the tables hold the frames of two stages + max_prediction + the delay

@@ -1783,3 +1783,105 @@ int oracle_particles_synctest_run(int32_t N, int32_t P, int32_t max_prediction, 
   synctest_free(&s);
   return 0;
 }
+
+/* ---------------------------------------------------------------- batches for every-lane parity
+ * Many independent sessions / branches at once, for the GPU tests and bench.py's parity leg to
+ * compare EVERY lane of a full-size run (test infrastructure: the restatements above, run per lane
+ * on `threads` threads).  Nothing here is new semantics. */
+typedef struct {
+  const OracleSyncTestCfg* cfg;
+  int32_t frames;
+  int64_t lanes, a, b;
+  const uint8_t* inputs;
+  uint16_t* cksum_trace;
+  uint8_t* final_states;
+  int32_t* ring_frames;
+  uint16_t* ring_cksums;
+  int32_t* status;
+} SyncBatchJob;
+static void* synctest_batch_worker(void* arg) {
+  SyncBatchJob* j = (SyncBatchJob*)arg;
+  const size_t P = (size_t)j->cfg->num_players, R = (size_t)j->cfg->max_prediction + 1, sb = 36 + 20 * P;
+  uint8_t* in = (uint8_t*)malloc((size_t)j->frames * P);
+  uint16_t* tr = (uint16_t*)malloc((size_t)j->frames * 2);
+  uint8_t* rs = (uint8_t*)malloc(R * sb);
+  for (int64_t l = j->a; l < j->b; l++) {
+    for (int32_t f = 0; f < j->frames; f++)
+      memcpy(in + (size_t)f * P, j->inputs + ((size_t)f * j->lanes + l) * P, P);
+    OracleSyncTestResult res;
+    oracle_synctest_run(j->cfg, j->frames, in, tr, NULL, 0, NULL, j->final_states ? j->final_states + l * sb : NULL,
+                        j->ring_frames ? j->ring_frames + l * R : NULL, j->ring_cksums ? j->ring_cksums + l * R : NULL,
+                        rs, &res);
+    if (j->cksum_trace)
+      for (int32_t f = 0; f < j->frames; f++) j->cksum_trace[(size_t)f * j->lanes + l] = tr[f];
+    if (j->status) j->status[l] = res.status;
+  }
+  free(in); free(tr); free(rs);
+  return NULL;
+}
+/* oracle_synctest_run for every lane of an engine-layout input block inputs[frames][lanes][P]:
+ * cksum_trace [frames][lanes], final_states [lanes][36+20P], ring_frames / ring_cksums [lanes][R],
+ * status [lanes] (any output may be NULL). */
+int oracle_synctest_batch(const OracleSyncTestCfg* cfg, int32_t frames, int64_t lanes, const uint8_t* inputs,
+                          int32_t threads, uint16_t* cksum_trace, uint8_t* final_states, int32_t* ring_frames,
+                          uint16_t* ring_cksums, int32_t* status) {
+  if (threads < 1) threads = 1;
+  if (threads > 64) threads = 64;
+  pthread_t th[64]; SyncBatchJob jobs[64];
+  const int64_t per = (lanes + threads - 1) / threads;
+  int used = 0;
+  for (int t = 0; t < threads; t++) {
+    const int64_t a = (int64_t)t * per, b = a + per < lanes ? a + per : lanes;
+    if (a >= b) break;
+    jobs[t] = (SyncBatchJob){cfg, frames, lanes, a, b, inputs, cksum_trace, final_states, ring_frames, ring_cksums, status};
+    pthread_create(&th[t], NULL, synctest_batch_worker, &jobs[t]);
+    used++;
+  }
+  for (int t = 0; t < used; t++) pthread_join(th[t], NULL);
+  return 0;
+}
+
+typedef struct {
+  int32_t P, load_frame, count, max_prediction;
+  int64_t a, b;
+  const uint8_t* start_states;
+  const int32_t* start_index;
+  const uint8_t* inputs;
+  uint16_t* cksums;
+  uint8_t* states;
+  int32_t rc;
+} ReplayBatchJob;
+static void* replay_batch_worker(void* arg) {
+  ReplayBatchJob* j = (ReplayBatchJob*)arg;
+  const size_t sb = 36 + 20 * (size_t)j->P;
+  for (int64_t l = j->a; l < j->b; l++) {
+    const int rc = oracle_p2p_replay(j->P, j->start_states + (size_t)j->start_index[l] * sb, j->load_frame, j->count,
+                                     j->max_prediction, j->inputs + (size_t)l * j->count * j->P, NULL,
+                                     j->states ? j->states + (size_t)l * j->count * sb : NULL,
+                                     j->cksums ? j->cksums + (size_t)l * j->count : NULL, NULL);
+    if (rc) j->rc = rc;
+  }
+  return NULL;
+}
+/* oracle_p2p_replay for many lanes: lane l loads start_states[start_index[l]] (saved at load_frame)
+ * and replays `count` frames with inputs[l][count][P]; its saved cells' checksums go to
+ * cksums[l][count] and states to states[l][count][36+20P] (either may be NULL). */
+int oracle_p2p_replay_batch(int32_t P, int64_t lanes, const uint8_t* start_states, const int32_t* start_index,
+                            int32_t load_frame, int32_t count, const uint8_t* inputs, int32_t threads,
+                            uint16_t* cksums, uint8_t* states) {
+  if (threads < 1) threads = 1;
+  if (threads > 64) threads = 64;
+  pthread_t th[64]; ReplayBatchJob jobs[64];
+  const int64_t per = (lanes + threads - 1) / threads;
+  int used = 0;
+  for (int t = 0; t < threads; t++) {
+    const int64_t a = (int64_t)t * per, b = a + per < lanes ? a + per : lanes;
+    if (a >= b) break;
+    jobs[t] = (ReplayBatchJob){P, load_frame, count, count, a, b, start_states, start_index, inputs, cksums, states, 0};
+    pthread_create(&th[t], NULL, replay_batch_worker, &jobs[t]);
+    used++;
+  }
+  int rc = 0;
+  for (int t = 0; t < used; t++) { pthread_join(th[t], NULL); if (jobs[t].rc) rc = jobs[t].rc; }
+  return rc;
+}

@@ -559,3 +559,63 @@ def codec_bench(ref, pending, count, passes=1):
     if n < 0:
         raise RuntimeError("codec round trip failed")
     return n, wall.value
+
+
+def default_threads():
+    """Threads for the batch entries: the CPU share a one-GPU job gets on the GPU box (its
+    OMP_NUM_THREADS is 16 there), else this machine's CPUs."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(64, int(env) if env and env.isdigit() else (os.cpu_count() or 1)))
+
+
+def synctest_batch(inputs, num_players=2, max_prediction=8, check_distance=2, input_delay=0, threads=None,
+                   trace=True):
+    """oracle_synctest_run for every lane of inputs[frames][lanes][P] (the engine's layout), on
+    `threads` threads: dict of cksum [frames][lanes] (the display checksum after every call),
+    final_states [lanes][sb], ring_frames / ring_cksums [lanes][R], status [lanes]."""
+    inputs = np.ascontiguousarray(inputs, np.uint8)
+    frames, lanes = inputs.shape[0], inputs.shape[1]
+    R, sb = max_prediction + 1, state_bytes(num_players)
+    cfg = SyncTestCfg(num_players, max_prediction, check_distance, input_delay, 0, 0, 1, -1, 0)
+    out = dict(cksum=np.zeros((frames, lanes), np.uint16) if trace else None,
+               final_states=np.zeros((lanes, sb), np.uint8), ring_frames=np.zeros((lanes, R), np.int32),
+               ring_cksums=np.zeros((lanes, R), np.uint16), status=np.zeros(lanes, np.int32))
+    L = lib()
+    if not getattr(L, "_batch_bound", False):
+        P = ctypes.POINTER
+        u8p, u16p, i32p = P(ctypes.c_uint8), P(ctypes.c_uint16), P(ctypes.c_int32)
+        L.oracle_synctest_batch.argtypes = [P(SyncTestCfg), ctypes.c_int32, ctypes.c_int64, u8p, ctypes.c_int32,
+                                            u16p, u8p, i32p, u16p, i32p]
+        L.oracle_synctest_batch.restype = ctypes.c_int
+        L.oracle_p2p_replay_batch.argtypes = [ctypes.c_int32, ctypes.c_int64, u8p, i32p, ctypes.c_int32,
+                                              ctypes.c_int32, u8p, ctypes.c_int32, u16p, u8p]
+        L.oracle_p2p_replay_batch.restype = ctypes.c_int
+        L._batch_bound = True
+    L.oracle_synctest_batch(ctypes.byref(cfg), frames, lanes, _ptr(inputs, ctypes.c_uint8), threads or default_threads(),
+                            _ptr(out["cksum"], ctypes.c_uint16), _ptr(out["final_states"], ctypes.c_uint8),
+                            _ptr(out["ring_frames"], ctypes.c_int32), _ptr(out["ring_cksums"], ctypes.c_uint16),
+                            _ptr(out["status"], ctypes.c_int32))
+    return out
+
+
+def p2p_replay_batch(start_states, start_index, load_frame, inputs, threads=None, states=False):
+    """p2p_replay for many lanes at once: lane l from start_states[start_index[l]] (the cell of
+    load_frame) over inputs[l][count][P]; returns (checksums [lanes][count], states
+    [lanes][count][sb] or None)."""
+    start_states = np.ascontiguousarray(start_states, np.uint8)
+    sb = start_states.shape[-1]
+    P = (sb - 36) // 20
+    idx = np.ascontiguousarray(start_index, np.int32)
+    inp = np.ascontiguousarray(inputs, np.uint8)
+    lanes, count = inp.shape[0], inp.shape[1]
+    cks = np.zeros((lanes, count), np.uint16)
+    st = np.zeros((lanes, count, sb), np.uint8) if states else None
+    L = lib()
+    if not getattr(L, "_batch_bound", False):
+        synctest_batch(np.zeros((1, 1, P), np.uint8), P, 2, 1, 0, threads=1)  # binds the batch entries
+    rc = L.oracle_p2p_replay_batch(P, lanes, _ptr(start_states, ctypes.c_uint8), _ptr(idx, ctypes.c_int32), load_frame,
+                                   count, _ptr(inp, ctypes.c_uint8), threads or default_threads(),
+                                   _ptr(cks, ctypes.c_uint16), _ptr(st, ctypes.c_uint8))
+    if rc != 0:
+        raise ValueError("bad p2p replay batch arguments")
+    return cks, st
