@@ -2015,7 +2015,6 @@ int ggrs_p2p_advance_frames(ggrs_p2p_engine_t* e, int32_t n) {
 int ggrs_p2p_set_desync_detection(ggrs_p2p_engine_t* e, int32_t interval) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
   if (interval < 0) return set_error(GGRS_E_INVALID, "interval must be >= 0 (0 = DesyncDetection::Off)");
-  if (interval > 0 && e->sched) return set_error(GGRS_E_STATE, "desync detection is not supported with arrival schedules");
   if (interval > 0 && e->sparse)
     return set_error(GGRS_E_STATE, "desync detection with sparse saving is not supported: the reference sends a "
                                    "report only for a frame it saved (p2p_session.rs:948-962, sync_layer.rs:323-326)");
@@ -2030,6 +2029,7 @@ int ggrs_p2p_set_desync_detection(ggrs_p2p_engine_t* e, int32_t interval) {
     HIP_TRY(hipMalloc(&e->cmp_count, sizeof(int32_t)));
   }
   e->desync_interval = interval;
+  if (interval > 0 && e->sched) return p2p_sched_desync_alloc(e);
   return GGRS_OK;
 }
 
@@ -2089,6 +2089,7 @@ static int hist_row(ggrs_p2p_engine_t* e, int32_t frame, const uint16_t** row) {
 }
 
 int ggrs_p2p_local_checksums(ggrs_p2p_engine_t* e, int32_t frame, uint16_t* out, int32_t out_on_device) {
+  if (e && e->sched) return set_error(GGRS_E_STATE, "arrival schedules report per session: ggrs_p2p_read_reports");
   if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
   const uint16_t* row = nullptr;
   int rc = hist_row(e, frame, &row);
@@ -2102,6 +2103,7 @@ int ggrs_p2p_local_checksums(ggrs_p2p_engine_t* e, int32_t frame, uint16_t* out,
 
 int ggrs_p2p_compare_checksums(ggrs_p2p_engine_t* e, int32_t frame, const uint16_t* remote, int32_t remote_on_device,
                                uint64_t* mask, int32_t* n_differ) {
+  if (e && e->sched) return set_error(GGRS_E_STATE, "arrival schedules report per session: ggrs_p2p_read_reports");
   if (!e || !remote || !mask || !n_differ) return set_error(GGRS_E_INVALID, "null argument");
   const uint16_t* row = nullptr;
   int rc = hist_row(e, frame, &row);

@@ -54,6 +54,15 @@ struct ggrs_p2p_engine {
   std::vector<int32_t> row_tag_host;
   uint32_t* iq = nullptr;         // [kSchedQueue][S] every player's queued input of frame q, q % kSchedQueue
   int32_t* sst = nullptr;         // [sched_fields(P)][S] SyncLayer / InputQueue / connect-status words
+  // scheduled desync detection: per call (row c % cap) the report sent, its checksum, the
+  // last_confirmed_frame compared against, the last queued local frame; every frame's final cell
+  // checksum [sched_hf][S]
+  int32_t* rep_frame = nullptr;
+  uint16_t* rep_ck = nullptr;
+  int32_t* rep_lconf = nullptr;
+  int32_t* rep_ll = nullptr;
+  uint16_t* fck = nullptr;
+  int32_t sched_hf = 0;
   ggrs::SpanTimer timer;
 };
 
@@ -62,4 +71,5 @@ namespace ggrs {
 int p2p_sched_enable(ggrs_p2p_engine* e);
 int p2p_sched_advance(ggrs_p2p_engine* e, int32_t n);
 int p2p_sched_free(ggrs_p2p_engine* e);
+int p2p_sched_desync_alloc(ggrs_p2p_engine* e);  // desync detection's buffers (scheduled mode)
 }  // namespace ggrs

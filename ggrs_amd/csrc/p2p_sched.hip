@@ -50,7 +50,7 @@ constexpr int32_t kNull = GGRS_NULL_FRAME;
 constexpr int kQ = 128;  // INPUT_QUEUE_LENGTH (input_queue.rs:6)
 constexpr int kBlock = 64;
 
-enum : int { kCur = 0, kLconf, kDframe, kLastSaved, kDelivered, kLocalLast, kSkips, kErr, kDisc, kPl0 };
+enum : int { kCur = 0, kLconf, kDframe, kLastSaved, kDelivered, kLocalLast, kSkips, kErr, kDisc, kLastSent, kPl0 };
 constexpr int kPlFields = 1;  // per player: last_frame (local_connect_status; remote players)
 __host__ __device__ constexpr int sched_fields(int P) { return kPl0 + kPlFields * P; }
 __host__ __device__ constexpr int cell_dwords_s(int p) { return (state_fields(p) + 1 + 3) & ~3; }
@@ -72,6 +72,16 @@ struct SchedParams {
   int32_t* sst;
   int32_t* rollbacks;
   int64_t* resim;
+  // desync detection (interval > 0): per call c (row c % cap) and session the checksum report sent
+  // (frame, NULL_FRAME for none; its checksum), last_confirmed_frame when the call compared, and the
+  // local players' last queued frame after it; fck [HF][S] the checksum of every frame's final cell
+  // (slot frame & (HF - 1)), from which a report's checksum is read after the launch
+  int32_t interval, HF;
+  int32_t* rep_frame;
+  uint16_t* rep_ck;
+  int32_t* rep_lconf;
+  int32_t* rep_ll;
+  uint16_t* fck;
 };
 
 // The block's LDS (dynamic): its 64 sessions' rings [R][PC][64] uint4 (+ frame tags [R][64] with
@@ -124,6 +134,7 @@ extern __shared__ __attribute__((aligned(16))) uint8_t sched_lds_base[];
 template <int P>
 struct SchedCtl {
   int32_t cur, lconf, dframe, last_saved, delivered, local_last, skips, err;
+  int32_t last_sent;  // last_sent_checksum_frame (desync detection, p2p_session.rs:939-975)
   uint32_t disc;
   int32_t lf[P];  // the remote players' last frames (local_connect_status[k].last_frame): the newest
                   // delivered frame for a connected player, frozen at its disconnect
@@ -137,6 +148,7 @@ struct SchedCtl {
 // sparse cell tags.
 struct SchedCtlEnv {
   int32_t lo, maxp, R, delay, cap;
+  int32_t interval;  // desync detection interval (0: off)
   int64_t S, s;
   uint32_t lmask, lbytes, rbytes;
   uint32_t o_rowtag, o_rows, o_tags;
@@ -151,7 +163,8 @@ struct SchedCtlEnv {
 // no branch).
 template <int P, int kPred>
 __device__ __forceinline__ bool sched_fast_call(SchedCtl<P>& q, const SchedCtlEnv& x, uint64_t cm, int32_t c,
-                                                int32_t a_c, uint32_t e_c, uint32_t& rec, bool en = true) {
+                                                int32_t a_c, uint32_t e_c, uint32_t& rec, int32_t& rep,
+                                                bool en = true) {
   const int32_t lo = x.lo, maxp = x.maxp;
   const uint32_t lbytes = x.lbytes, rbytes = x.rbytes;
   const int32_t a = a_c;
@@ -163,9 +176,15 @@ __device__ __forceinline__ bool sched_fast_call(SchedCtl<P>& q, const SchedCtlEn
   const uint64_t hit = last > q.delivered ? cm & win : 0ull;
   const int32_t mis = hit ? lo + (int32_t)__builtin_ctzll(hit) : kNull;
   // (bitwise: every test evaluated, no branch per test)
+  // check_checksum_send_interval (p2p_session.rs:939-975), before the call's rollback: the report of
+  // frame_to_send once it is confirmed and saved; its cell must still be in the ring (else the
+  // reference panics: the general form stops the session)
+  const int32_t fts = q.last_sent == kNull ? x.interval : q.last_sent + x.interval;
+  const bool send = x.interval > 0 && fts <= q.lconf && fts <= q.last_saved;
   const bool fast = en & (a <= c) & (q.disc == 0u) & (e_c == 0u) & (q.dframe == kNull) & (q.cur >= 1) & (q.cur >= lo) &
                     (q.delivered >= (kPred == 0 ? lo : lo - 1)) & (lbytes == 0u || q.local_last != kNull) &
-                    (up - q.delivered < kArrTooFar) & (up < q.cur - maxp + kQ - 1) & (mis == kNull || mis >= q.cur - maxp);
+                    (up - q.delivered < kArrTooFar) & (up < q.cur - maxp + kQ - 1) & (mis == kNull || mis >= q.cur - maxp) &
+                    (!send || fts >= q.last_saved - maxp);
   const int32_t code = up - q.delivered;
   int32_t confirmed = INT32_MAX;  // confirmed_frame (:542-553), every player connected
   if (lbytes) confirmed = q.local_last;
@@ -181,6 +200,8 @@ __device__ __forceinline__ bool sched_fast_call(SchedCtl<P>& q, const SchedCtlEn
   const bool adv = (lc == kNull ? q.cur : q.cur - lc) < maxp;
   const int32_t nslot = q.slot_f + 1 == x.R ? 0 : q.slot_f + 1;
   if (fast) {
+    rep = send ? fts : kNull;
+    q.last_sent = send ? fts : q.last_sent;
     q.delivered = up;
 #pragma unroll
     for (int k = 0; k < P; k++)
@@ -204,7 +225,7 @@ __device__ __forceinline__ bool sched_fast_call(SchedCtl<P>& q, const SchedCtlEn
 // mask_ok / cm: the fast form's precondition and change mask over the stage's rows.
 template <int P, bool kSparse, int kPred>
 __device__ __forceinline__ uint2 sched_control_call(SchedCtl<P>& q, const SchedCtlEnv& x, bool mask_ok, uint64_t cm,
-                                                    int32_t c, int32_t a_c, uint32_t e_c) {
+                                                    int32_t c, int32_t a_c, uint32_t e_c, int32_t& rep) {
   using T = typename InputWord<P>::T;
   const int32_t lo = x.lo, maxp = x.maxp, R = x.R;
   const uint32_t lmask = x.lmask, lbytes = x.lbytes, rbytes = x.rbytes;
@@ -241,7 +262,8 @@ __device__ __forceinline__ uint2 sched_control_call(SchedCtl<P>& q, const SchedC
   // Fast form: a lane with every player connected, no disconnect pending, its rows staged, and
   // nothing in this call that the reference would panic at -- the common call, branch-free.
   bool fast = false;
-  if (mask_ok && !q.err) fast = sched_fast_call<P, kPred>(q, x, cm, c, a_c, e_c, rec);
+  rep = kNull;
+  if (mask_ok && !q.err) fast = sched_fast_call<P, kPred>(q, x, cm, c, a_c, e_c, rec, rep);
   if (fast) {
   } else if (q.err) {
     stop = kStopBefore;
@@ -296,6 +318,16 @@ __device__ __forceinline__ uint2 sched_control_call(SchedCtl<P>& q, const SchedC
       }
       if (kPred == 0 && q.delivered != kNull) bad |= !row_ok(q.delivered);  // the prediction's row
       rec = (uint32_t)code << 16 | ev << 24;
+      // check_checksum_send_interval (p2p_session.rs:939-975): after the poll, before the rollback
+      const int32_t fts = q.last_sent == kNull ? x.interval : q.last_sent + x.interval;
+      if (!bad && x.interval > 0 && fts <= q.lconf && fts <= q.last_saved) {
+        if (fts < q.last_saved - maxp) {
+          q.err = GGRS_E_PRECONDITION;  // "cell not found!" (:951-954): the reference panics
+          goto call_done;
+        }
+        q.last_sent = fts;
+        rep = fts;
+      }
       if (bad) {
         q.err = GGRS_E_PRECONDITION;  // a remote input no longer in the input rows
       } else {
@@ -408,6 +440,26 @@ __device__ __forceinline__ uint2 sched_control_call(SchedCtl<P>& q, const SchedC
   return make_uint2(rec, rec2);
 }
 
+// Desync detection: a call's report row (the frame sent or NULL_FRAME, last_confirmed_frame at the
+// comparison, the local players' last queued frame after the call)
+__device__ inline void sched_store_report(const SchedParams& p, int32_t c, int64_t s, int32_t rep, int32_t lconf,
+                                          int32_t ll) {
+  const int64_t i = (int64_t)(c % p.cap) * p.S + s;
+  p.rep_frame[i] = rep;
+  p.rep_lconf[i] = lconf;
+  p.rep_ll[i] = ll;
+}
+// ... and after the launch (every cell final): each report's checksum, the final cell checksum of its
+// frame -- a confirmed frame's cell is never saved again (a rollback starts after every confirmed
+// frame), so this is the checksum the reference read from the cell when it sent the report
+__device__ inline void sched_report_checksums(const SchedParams& p, int64_t s) {
+  for (int32_t c = p.c0; c < p.c0 + p.n; c++) {
+    const int64_t i = (int64_t)(c % p.cap) * p.S + s;
+    const int32_t f = p.rep_frame[i];
+    p.rep_ck[i] = f == kNull ? (uint16_t)0 : p.fck[(int64_t)(f & (p.HF - 1)) * p.S + s];
+  }
+}
+
 // A launch's end: the control state back to HBM (sst), the counts, and -- without sparse saving,
 // where every frame 0 .. last save has been saved -- each cell's frame, the newest one <= the last
 // save in its slot.
@@ -435,6 +487,7 @@ __device__ inline void sched_store_ctl(const SchedParams& p, const SchedCtl<P>& 
   fld(kSkips) = q.skips;
   fld(kErr) = q.err;
   fld(kDisc) = (int32_t)q.disc;
+  fld(kLastSent) = q.last_sent;
 #pragma unroll
   for (int k = 0; k < P; k++) fld(kPl0 + kPlFields * k + 0) = q.lf[k];
   p.rollbacks[s] += q.rollbacks;
@@ -526,6 +579,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
   q.skips = fld(kSkips);
   q.err = fld(kErr);
   q.disc = (uint32_t)fld(kDisc);
+  q.last_sent = fld(kLastSent);
 #pragma unroll
   for (int k = 0; k < P; k++) q.lf[k] = fld(kPl0 + kPlFields * k + 0);
   if (!live) q.err = 1;  // idle lanes run no call
@@ -562,6 +616,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
   // last_saved are the control pass's
   auto save = [&](int32_t slot) {
     const uint32_t ck = fletcher16_state<P>(st);
+    if (!kSparse && p.interval > 0) p.fck[(int64_t)((int32_t)st.w[0] & (p.HF - 1)) * S + s] = (uint16_t)ck;
 #pragma unroll
     for (int k = 0; k < PC; k++) {
       uint32_t x[4];
@@ -659,6 +714,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
       env.col = lt;
       env.inputs = p.inputs;
       env.row_tag = p.row_tag;
+      env.interval = p.interval;
       const int32_t ci0 = cs % p.cap;
       for (int32_t cb8 = cs; cb8 < ce; cb8 += 8) {
         int32_t up8[8];
@@ -682,7 +738,10 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
             up8[k] = up8[k + 1];
             ev8[k] = ev8[k + 1];
           }
-          const uint2 rr = sched_control_call<P, kSparse, kPred>(q, env, mask_ok, cm, c, a_c, e_c);
+          const int32_t lconf0 = q.lconf;
+          int32_t rep;
+          const uint2 rr = sched_control_call<P, kSparse, kPred>(q, env, mask_ok, cm, c, a_c, e_c, rep);
+          if (p.interval > 0 && live) sched_store_report(p, c, s, rep, lconf0, q.local_last);
           Rec r;
           if constexpr (kSparse) r = rr;
           else r = rr.x;
@@ -845,6 +904,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
     sched_store_ctl<P>(p, q, s, false);
   } else {
     sched_store_ctl<P>(p, q, s, true);
+    if (p.interval > 0) sched_report_checksums(p, s);  // (every save of the launch done: the barrier above)
   }
 #undef lring
 #undef ltag
@@ -1018,6 +1078,7 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
     q.skips = fld(kSkips);
     q.err = fld(kErr);
     q.disc = (uint32_t)fld(kDisc);
+    q.last_sent = fld(kLastSent);
 #pragma unroll
     for (int k = 0; k < P; k++) q.lf[k] = fld(kPl0 + kPlFields * k + 0);
     if (!live) q.err = 1;  // idle lanes run no call
@@ -1198,6 +1259,7 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
         env.col = col;
         env.inputs = p.inputs;
         env.row_tag = p.row_tag;
+        env.interval = p.interval;
         for (int32_t cb8 = cs; cb8 < ce; cb8 += 8) {
           // eight calls' arrivals, events and input rows (the local players' input each call queues),
           // all read before the first is used
@@ -1219,21 +1281,28 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
           const SchedCtl<P> q0 = q;
           bool ok = true;
           uint32_t recs[8];
-          int32_t taus[8], dlvs[8], lls0[8], lls1[8];
+          int32_t taus[8], dlvs[8], lls0[8], lls1[8], reps[8], lcs[8];
 #pragma unroll
           for (int j = 0; j < 8; j++) {
             recs[j] = 0u;
+            reps[j] = kNull;
             taus[j] = q.cur;
             lls0[j] = q.local_last;
-            if (j < nj) ok &= sched_fast_call<P, kPred>(q, env, cm, cb8 + j, up8[j], ev8[j], recs[j], en);
+            lcs[j] = q.lconf;
+            if (j < nj) ok &= sched_fast_call<P, kPred>(q, env, cm, cb8 + j, up8[j], ev8[j], recs[j], reps[j], en);
             dlvs[j] = q.delivered;
             lls1[j] = q.local_last;
           }
           if (__builtin_expect(__all(ok | idle), 1)) {
             if (en) {
 #pragma unroll
-              for (int j = 0; j < 8; j++)
+              for (int j = 0; j < 8; j++) {
                 if (j < nj) emit(taus[j], lls0[j], lls1[j], recs[j], dlvs[j], 0u, rw8[j]);
+                if (j < nj && p.interval > 0) sched_store_report(p, cb8 + j, s, reps[j], lcs[j], lls1[j]);
+              }
+            }
+            if (p.interval > 0 && live && !en) {  // (a stopped session: no report)
+              for (int j = 0; j < nj; j++) sched_store_report(p, cb8 + j, s, kNull, q.lconf, q.local_last);
             }
             continue;
           }
@@ -1251,10 +1320,12 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
               ev8[k] = ev8[k + 1];
               rw8[k] = rw8[k + 1];
             }
-            const int32_t tau = q.cur, ll0 = q.local_last;
+            const int32_t tau = q.cur, ll0 = q.local_last, lconf0 = q.lconf;
             const uint32_t disc0 = q.disc;
-            const uint32_t rec = sched_control_call<P, false, kPred>(q, env, mask_ok, cm, c, a_c, e_c).x;
+            int32_t rep;
+            const uint32_t rec = sched_control_call<P, false, kPred>(q, env, mask_ok, cm, c, a_c, e_c, rep).x;
             if (!live) continue;
+            if (p.interval > 0) sched_store_report(p, c, s, rep, lconf0, q.local_last);
             if (q.disc != disc0) {  // the disconnected players' last frames, frozen now
 #pragma unroll
               for (int k = 0; k < P; k++)
@@ -1297,6 +1368,7 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
       for (int32_t f = max(0, q.cur - maxp - 1); f <= q.local_last; f++)
         p.lq[(int64_t)(f & (p.WL - 1)) * S + s] = tab1(f, col).z;
     sched_store_ctl<P>(p, q, s, true);
+    if (p.interval > 0) sched_report_checksums(p, s);  // (every step done: barrier (3))
     return;
   }
 
@@ -1414,6 +1486,7 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
         // SaveGameState of frame tau (sync_layer.rs:208-215, ex_game.rs:103-108)
         {
           const uint32_t ck = fletcher16_state<P>(st);
+          if (wr && p.interval > 0) p.fck[(int64_t)(tau & (p.HF - 1)) * S + s] = (uint16_t)ck;
           if (wr) {
 #pragma unroll
             for (int k = 0; k < PC; k++) {
@@ -1463,7 +1536,7 @@ __global__ void sched_init_kernel(int32_t* sst, int64_t S, int32_t P) {
   if (i >= (int64_t)sched_fields(P) * S) return;
   const int f = (int)(i / S);
   int32_t v = kNull;
-  if (f == kCur || f == kSkips || f == kErr || f == kDisc) v = 0;
+  if (f == kCur || f == kSkips || f == kErr || f == kDisc) v = 0;  // (kLastSent: NULL_FRAME)
   sst[i] = v;
 }
 
@@ -1472,7 +1545,7 @@ __global__ void sched_init_kernel(int32_t* sst, int64_t S, int32_t P) {
 namespace ggrs {
 
 int p2p_sched_free(ggrs_p2p_engine* e) {
-  void* bufs[] = {e->arrive, e->events, e->row_tag, e->iq, e->sst};
+  void* bufs[] = {e->arrive, e->events, e->row_tag, e->iq, e->sst, e->rep_frame, e->rep_ck, e->rep_lconf, e->rep_ll, e->fck};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   e->arrive = nullptr;
@@ -1480,6 +1553,33 @@ int p2p_sched_free(ggrs_p2p_engine* e) {
   e->row_tag = nullptr;
   e->iq = nullptr;
   e->sst = nullptr;
+  e->rep_frame = nullptr;
+  e->rep_ck = nullptr;
+  e->rep_lconf = nullptr;
+  e->rep_ll = nullptr;
+  e->fck = nullptr;
+  return GGRS_OK;
+}
+
+// desync detection under arrival schedules: the per-call report rows and the frames' final cell
+// checksums (a launch of n <= cap calls reports frames >= its first frame - max_prediction - 1, so
+// cap + max_prediction + 2 frames of them suffice)
+int p2p_sched_desync_alloc(ggrs_p2p_engine* e) {
+  if (e->rep_frame) return GGRS_OK;
+  const int64_t S = e->cfg.num_sessions;
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  int hf = 2;
+  while (hf < e->cap + e->cfg.max_prediction + 2) hf *= 2;
+  e->sched_hf = hf;
+  HIP_TRY(hipMalloc(&e->rep_frame, sizeof(int32_t) * (size_t)e->cap * S));
+  HIP_TRY(hipMalloc(&e->rep_ck, sizeof(uint16_t) * (size_t)e->cap * S));
+  HIP_TRY(hipMalloc(&e->rep_lconf, sizeof(int32_t) * (size_t)e->cap * S));
+  HIP_TRY(hipMalloc(&e->rep_ll, sizeof(int32_t) * (size_t)e->cap * S));
+  HIP_TRY(hipMalloc(&e->fck, sizeof(uint16_t) * (size_t)hf * S));
+  HIP_TRY(hipMemsetAsync(e->rep_frame, 0xff, sizeof(int32_t) * (size_t)e->cap * S, e->stream));
+  HIP_TRY(hipMemsetAsync(e->rep_ck, 0, sizeof(uint16_t) * (size_t)e->cap * S, e->stream));
+  HIP_TRY(hipMemsetAsync(e->fck, 0, sizeof(uint16_t) * (size_t)hf * S, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
   return GGRS_OK;
 }
 
@@ -1570,6 +1670,13 @@ int p2p_sched_advance(ggrs_p2p_engine* e, int32_t n) {
   p.rollbacks = e->rollbacks;
   p.resim = e->resim;
   p.TW = 0;
+  p.interval = e->desync_interval;
+  p.HF = e->sched_hf;
+  p.rep_frame = e->rep_frame;
+  p.rep_ck = e->rep_ck;
+  p.rep_lconf = e->rep_lconf;
+  p.rep_ll = e->rep_ll;
+  p.fck = e->fck;
   if (int rc = e->timer.before(e->stream)) return rc;
   hipError_t attr = hipSuccess;
   // The time-aligned form (a session's replays on 16 lanes) for few sessions: when its blocks of 16
@@ -1672,9 +1779,9 @@ int ggrs_p2p_set_arrival_schedule(ggrs_p2p_engine_t* e, int32_t on) {
     return set_error(GGRS_E_INVALID, "scheduled arrivals need rollback mode (max_prediction >= 1)");
   if (e->cfg.max_prediction + e->cfg.input_delay + 2 >= kQ)
     return set_error(GGRS_E_INVALID, "max_prediction + input_delay must be < %d (the device input queue)", kQ - 2);
-  if (e->desync_interval > 0 || e->trace)
-    return set_error(GGRS_E_STATE, "scheduled arrivals support neither desync detection nor the display-checksum trace");
-  return p2p_sched_enable(e);
+  if (e->trace) return set_error(GGRS_E_STATE, "scheduled arrivals do not support the display-checksum trace");
+  if (int rc = p2p_sched_enable(e)) return rc;
+  return e->desync_interval > 0 ? p2p_sched_desync_alloc(e) : GGRS_OK;
 }
 
 int ggrs_p2p_add_arrivals(ggrs_p2p_engine_t* e, int32_t first_call, int32_t n, const int32_t* arrive_upto,
@@ -1705,6 +1812,32 @@ int ggrs_p2p_add_arrivals(ggrs_p2p_engine_t* e, int32_t first_call, int32_t n, c
   }
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->next_arrival_call = first_call + n;
+  return GGRS_OK;
+}
+
+int ggrs_p2p_read_reports(ggrs_p2p_engine_t* e, int32_t first_call, int32_t n, int32_t* frames, uint16_t* checksums,
+                          int32_t* last_confirmed, int32_t* local_last) {
+  if (!e) return set_error(GGRS_E_INVALID, "null engine");
+  if (!e->sched || e->desync_interval <= 0 || !e->rep_frame)
+    return set_error(GGRS_E_STATE, "per-session reports exist with arrival schedules and desync detection only");
+  if (n < 0 || first_call < 0 || first_call + n > e->current_frame || first_call < e->current_frame - e->cap)
+    return set_error(GGRS_E_INVALID, "calls %d .. %d are not among the last %d calls run (%d run)", first_call,
+                     first_call + n - 1, e->cap, e->current_frame);
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const int64_t S = e->cfg.num_sessions;
+  for (int32_t k = 0; k < n;) {  // rows wrap at cap: at most two pieces
+    const int32_t slot = (first_call + k) % e->cap;
+    const int32_t m = std::min(n - k, e->cap - slot);
+    const size_t off = (size_t)slot * S, dst = (size_t)k * S, cnt = (size_t)m * S;
+    if (frames) HIP_TRY(hipMemcpyAsync(frames + dst, e->rep_frame + off, 4 * cnt, hipMemcpyDeviceToHost, e->stream));
+    if (checksums)
+      HIP_TRY(hipMemcpyAsync(checksums + dst, e->rep_ck + off, 2 * cnt, hipMemcpyDeviceToHost, e->stream));
+    if (last_confirmed)
+      HIP_TRY(hipMemcpyAsync(last_confirmed + dst, e->rep_lconf + off, 4 * cnt, hipMemcpyDeviceToHost, e->stream));
+    if (local_last) HIP_TRY(hipMemcpyAsync(local_last + dst, e->rep_ll + off, 4 * cnt, hipMemcpyDeviceToHost, e->stream));
+    k += m;
+  }
+  HIP_TRY(hipStreamSynchronize(e->stream));
   return GGRS_OK;
 }
 

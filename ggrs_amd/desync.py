@@ -128,3 +128,110 @@ def exchange(a, b):
         b.receive(call, frame, report)
     for call, frame, report in b.outgoing():
         a.receive(call, frame, report)
+
+
+class SchedDesyncDetector:
+    """Desync detection for every session of a P2PEngine under arrival schedules
+    (ggrs_p2p_set_arrival_schedule): each session sends its checksum reports at its own calls, for
+    its own frames (check_checksum_send_interval on the device, ggrs_p2p_read_reports), and this
+    class keeps the rest of the reference's bookkeeping per session:
+      * a report the remote peer sent in its call g travels with the inputs it sent in that call
+        (its last queued frame, `local_last`), so it is received at the first local call c > g whose
+        poll delivers that frame (the arrival rows handed to the engine, `note_arrivals`);
+      * UdpProtocol::on_checksum_report (protocol.rs:663-682) keeps it in pending_checksums;
+      * the local report of a call enters local_checksum_history (pruned to 32 reports);
+      * compare_local_checksums_against_peers (p2p_session.rs:904-937) compares every pending report
+        older than the call's last_confirmed_frame that is in the history, raises DesyncDetected when
+        they differ, and drops it -- pending reports are visited in frame order.
+    """
+
+    def __init__(self, engine, interval, addr=None):
+        import numpy as np
+        self.np = np
+        self.engine = engine
+        self.interval = interval
+        self.addr = addr
+        engine.set_desync_detection(interval)
+        S = engine.num_sessions
+        self.local = [dict() for _ in range(S)]     # local_checksum_history per session
+        self.pending = [dict() for _ in range(S)]   # remote pending_checksums per session
+        self.arrive = {}                            # call -> [S] newest remote frame delivered
+        self.remote = []                            # remote report rows: (call, frame[S], cs[S], local_last[S])
+        self.next_remote = np.zeros(S, np.int64)    # per session: remote rows delivered so far
+        self.processed = 0
+        self.sent = 0
+
+    def note_arrivals(self, first_call, arrive_upto):
+        """The arrival rows given to the engine (ggrs_p2p_add_arrivals), for the report delivery."""
+        for k, row in enumerate(self.np.asarray(arrive_upto)):
+            self.arrive[first_call + k] = self.np.asarray(row, self.np.int32)
+
+    def outgoing(self):
+        """The report rows of the calls run since the last outgoing(): (first_call, engine.reports)."""
+        current = self.engine.calls()
+        first, n = self.sent, current - self.sent
+        self.sent = current
+        return first, self.engine.reports(first, n) if n > 0 else None
+
+    def receive(self, first_call, rows):
+        """The remote peer's outgoing() rows (its calls first_call ..)."""
+        if rows is None:
+            return
+        assert first_call == len(self.remote), "remote report rows must be received in order"
+        for k in range(rows["frame"].shape[0]):
+            self.remote.append((first_call + k, rows["frame"][k], rows["checksum"][k], rows["local_last"][k]))
+
+    def _on_checksum_report(self, s, frame, cs):
+        pend = self.pending[s]
+        if len(pend) >= MAX_CHECKSUM_HISTORY_SIZE:
+            oldest = frame - (MAX_CHECKSUM_HISTORY_SIZE - 1) * self.interval
+            self.pending[s] = pend = {f: c for f, c in pend.items() if f >= oldest}
+        pend[frame] = cs
+
+    def poll(self):
+        """Replay the desync steps of every call run so far (report arrivals, the local report, the
+        comparison) and return the DesyncDetected events they raise, in call order."""
+        np = self.np
+        events = []
+        current = self.engine.calls()
+        if current <= self.processed:
+            return events
+        first = self.processed
+        own = self.engine.reports(first, current - first)
+        for c in range(first, current):
+            arrive = self.arrive[c]
+            # poll_remote_clients: remote reports whose inputs this call's poll delivers, in order
+            for s in range(len(self.local)):
+                g = int(self.next_remote[s])
+                while g < len(self.remote) and g < c:
+                    _, fr, cs, ll = self.remote[g]
+                    if ll[s] > arrive[s]:
+                        break
+                    if fr[s] >= 0:
+                        self._on_checksum_report(s, int(fr[s]), int(cs[s]))
+                    g += 1
+                self.next_remote[s] = g
+            row = c - first
+            fr, cs, lc = own["frame"][row], own["checksum"][row], own["last_confirmed"][row]
+            for s in np.nonzero(fr >= 0)[0]:           # check_checksum_send_interval
+                hist = self.local[s]
+                hist[int(fr[s])] = int(cs[s])
+                if len(hist) > MAX_CHECKSUM_HISTORY_SIZE:
+                    oldest = int(fr[s]) - (MAX_CHECKSUM_HISTORY_SIZE - 1) * self.interval
+                    self.local[s] = {f: v for f, v in hist.items() if f >= oldest}
+            for s in range(len(self.local)):           # compare_local_checksums_against_peers
+                pend = self.pending[s]
+                if not pend:
+                    continue
+                hist = self.local[s]
+                checked = []
+                for frame in sorted(pend):
+                    if frame >= lc[s] or frame not in hist:
+                        continue
+                    if hist[frame] != pend[frame]:
+                        events.append(DesyncDetected(frame, s, hist[frame], pend[frame], self.addr, c))
+                    checked.append(frame)
+                for frame in checked:
+                    del pend[frame]
+        self.processed = current
+        return events

@@ -108,6 +108,32 @@ def exchange_p2p_reports(detector, group=None):
     return len(out)
 
 
+def exchange_sched_reports(detector, group=None):
+    """The same for P2P engines under arrival schedules (desync.SchedDesyncDetector): each rank's
+    report rows of the calls run since the last exchange -- per call and session the report frame,
+    checksum and the local players' last queued frame (the report travels with those inputs) -- are
+    all-gathered over the process group as one int32 block, and the peer's rows go to
+    SchedDesyncDetector.receive.  Every rank runs the same calls.  Returns the number of calls."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    peer = peer_of(rank, world)
+    first, rows = detector.outgoing()
+    if rows is None:
+        return 0
+    block = np.stack([rows["frame"], rows["checksum"].astype(np.int32), rows["local_last"]], axis=1)
+    local = torch.from_numpy(np.ascontiguousarray(block, np.int32))
+    if dist.get_backend(group) == "nccl":
+        local = local.cuda()
+    parts = [torch.empty_like(local) for _ in range(world)]
+    dist.all_gather(parts, local, group=group)
+    theirs = parts[peer].cpu().numpy()
+    detector.receive(first, dict(frame=theirs[:, 0], checksum=theirs[:, 1].astype(np.uint16),
+                                 local_last=theirs[:, 2]))
+    return theirs.shape[0]
+
+
 class ReportExchange:
     """Stream-ordered exchange of branch-engine reports (configs 3/4 across GPUs): one all-gather
     per batch of `batch` confirmations (default 1: one per confirmation) with no host

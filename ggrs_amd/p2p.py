@@ -67,6 +67,7 @@ def _bind(L):
     L.ggrs_p2p_set_arrival_schedule.argtypes = [vp, i32]
     L.ggrs_p2p_add_arrivals.argtypes = [vp, i32, i32, vp, vp]
     L.ggrs_p2p_read_sessions.argtypes = [vp, vp, vp, vp]
+    L.ggrs_p2p_read_reports.argtypes = [vp, i32, i32, vp, vp, vp, vp]
     for name in _lib.EXPORTS:
         if name.startswith("ggrs_p2p_"):
             getattr(L, name).restype = ctypes.c_int
@@ -247,6 +248,19 @@ class P2PEngine:
         out = [np.zeros(self.num_sessions, np.int32) for _ in range(3)]
         _lib.check(self._L.ggrs_p2p_read_sessions(self._h, *(_vp(a) for a in out)))
         return tuple(out)
+
+    def reports(self, first_call, n_calls):
+        """Desync detection under arrival schedules: dict of [n][S] arrays for calls first_call ..
+        first_call + n - 1 -- frame (the checksum report check_checksum_send_interval sent, -1
+        none), checksum, last_confirmed (the frame compare_local_checksums_against_peers compared
+        against) and local_last (the local players' last queued frame after the call)."""
+        shape = (n_calls, self.num_sessions)
+        out = dict(frame=np.zeros(shape, np.int32), checksum=np.zeros(shape, np.uint16),
+                   last_confirmed=np.zeros(shape, np.int32), local_last=np.zeros(shape, np.int32))
+        _lib.check(self._L.ggrs_p2p_read_reports(self._h, first_call, n_calls, _vp(out["frame"]),
+                                                  _vp(out["checksum"]), _vp(out["last_confirmed"]),
+                                                  _vp(out["local_last"])))
+        return out
 
     KERNEL_FORMS = {"default": 0, "unstaged": 1, "lockstep": 2, "flat": 3, "chains": 4, "flat_queues": 5,
                     "canonical": 6}

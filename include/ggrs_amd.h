@@ -53,8 +53,9 @@ extern "C" {
  * 3: ggrs_branch_set_stream(e, NULL) binds HIP's null stream (it used to select the engine's own
  * stream); ggrs_branch_use_own_stream returns to the engine's own
  * 4: P2P arrival schedules (ggrs_p2p_set_arrival_schedule, ggrs_p2p_add_arrivals,
- * ggrs_p2p_read_sessions) */
-#define GGRS_ABI_VERSION 4
+ * ggrs_p2p_read_sessions)
+ * 5: desync detection under arrival schedules (ggrs_p2p_read_reports) */
+#define GGRS_ABI_VERSION 5
 
 #define GGRS_OK 0
 #define GGRS_E_INVALID (-1)      /* GgrsError::InvalidRequest: bad argument or configuration */
@@ -541,7 +542,8 @@ int ggrs_p2p_debug_desync(ggrs_p2p_engine_t* eng, int32_t session, int32_t frame
  * frame, and InputQueue::add_input drops the repeat, input_queue.rs:170-186); (4) advance_frame.
  * Input row g (ggrs_p2p_add_inputs) = the local players' input of call g and the remote players'
  * input of frame g, as in the fixed-latency model.  Rollback mode only (max_prediction >= 1),
- * sparse saving allowed, no desync detection or trace; remote_latency is ignored.  A session whose
+ * sparse saving allowed, no trace; desync detection (ggrs_p2p_set_desync_detection, without sparse
+ * saving) per session: ggrs_p2p_read_reports; remote_latency is ignored.  A session whose
  * call would make the reference panic (a remote input no longer in the input rows or more than
  * 126 - max_prediction frames ahead of the session, a rollback to a frame that is not in the past,
  * no connected player) or whose arrival row names a frame after its call (GGRS_E_INVALID) stops
@@ -557,6 +559,18 @@ int ggrs_p2p_add_arrivals(ggrs_p2p_engine_t* eng, int32_t first_call, int32_t n_
 /* per session: SyncLayer::current_frame, the calls that did not advance (prediction threshold),
  * and the session's error (0, GGRS_E_PRECONDITION or GGRS_E_INVALID); any pointer may be NULL */
 int ggrs_p2p_read_sessions(ggrs_p2p_engine_t* eng, int32_t* frames, int32_t* skipped, int32_t* errors);
+/* Desync detection under arrival schedules (p2p_session.rs:281-291, 904-975): for calls
+ * first_call .. first_call + n_calls - 1 (run, and among the last input_capacity calls), per call and
+ * session [n_calls][num_sessions]: the frame of the checksum report check_checksum_send_interval
+ * sent (NULL_FRAME: none) and its checksum (the cell's, as read when sent), the
+ * last_confirmed_frame compare_local_checksums_against_peers compared against in that call, and
+ * the local players' last queued frame after the call (the reports travel with those inputs).
+ * The pending-report bookkeeping and comparison are the caller's (ggrs_amd/desync.py
+ * SchedDesyncDetector: UdpProtocol::on_checksum_report, protocol.rs:663-682).  A session whose
+ * report cell is gone (the reference panics, :951-954) stops with GGRS_E_PRECONDITION.  Any output
+ * pointer may be NULL. */
+int ggrs_p2p_read_reports(ggrs_p2p_engine_t* eng, int32_t first_call, int32_t n_calls, int32_t* frames,
+                          uint16_t* checksums, int32_t* last_confirmed, int32_t* local_last);
 
 /* ---- Input wire codec, batched (src/network/compression.rs:14-182; bitfield-rle 0.2.1 runs,
  * bincode 1.3 fixint framing of EncodedInputSequence).  Replaces compression::encode / decode as

@@ -1406,6 +1406,64 @@ int oracle_p2p_stream(const OracleP2PCfg* cfg, int32_t frames, const uint8_t* in
   return rc;
 }
 
+/* One call of a scheduled session (the body of oracle_p2p_sched_run's loop, shared with the
+ * two-peer run below): poll_remote_clients' burst of remote frames (delivered, upto] whose inputs
+ * are remote_rows[g][P] and its Event::Disconnected bits, then advance_frame with the local
+ * players' inputs local_row[P] and Game::handle_requests.  With desync detection on, the checksum
+ * report the call would send is checked first: the reference panics when the cell is gone.
+ * Returns 0, -1 (a schedule error) or -4 (the reference panics). */
+static int sched_session_call(P2PSession* s, Game* game, RequestVec* rv, int32_t c, const uint8_t* local_row,
+                              const uint8_t* remote_rows, int32_t* delivered, int32_t upto, uint8_t ev, int* adv,
+                              int32_t* rb_frame, OracleP2PResult* res) {
+  const size_t P = s->num_players;
+  if (upto > c) return -1;
+  for (int32_t g = *delivered + 1; g <= upto; g++)   /* the burst */
+    for (size_t i = 0; i < P; i++) {
+      if (((s->local_mask >> i) & 1u) || s->disconnected[i]) continue;
+      if (s->sl.queues[i].length + 1 > INPUT_QUEUE_LENGTH) return -4;
+      p2p_on_remote_input(s, i, g, remote_rows[(size_t)g * P + i]);
+    }
+  if (upto > *delivered) *delivered = upto;
+  for (size_t i = 0; i < P; i++)                        /* Event::Disconnected */
+    if (((ev >> i) & 1u) && !((s->local_mask >> i) & 1u) && !s->disconnected[i]) {
+      s->disconnected[i] = 1;
+      if (s->sl.current_frame > s->last_frame[i]) s->disconnect_frame = s->last_frame[i] + 1;
+    }
+  int any_connected = 0;
+  for (size_t i = 0; i < P; i++) any_connected |= !s->disconnected[i];
+  if (!any_connected) return -4;
+  if (s->ds && s->ds->interval > 0) {  /* check_checksum_send_interval's cell lookup (p2p_session.rs:951-954) */
+    const int32_t fts = s->ds->last_sent == NULL_FRAME ? s->ds->interval : s->ds->last_sent + s->ds->interval;
+    if (fts <= s->sl.last_confirmed_frame && fts <= s->sl.last_saved_frame && !sl_saved_state_by_frame(&s->sl, fts))
+      return -4;
+  }
+  {  /* a rollback to a frame that is not in the past panics in load_frame (sync_layer.rs:231-237):
+      * a disconnect whose last_frame is current_frame - 1 sets disconnect_frame = current_frame
+      * (sparse saving loads the last save instead, p2p_session.rs:666-673) */
+    const int32_t fi = sl_check_simulation_consistency(&s->sl, s->disconnect_frame);
+    const int32_t load = s->sparse_saving ? s->sl.last_saved_frame : fi;
+    if (fi != NULL_FRAME && load >= s->sl.current_frame) return -4;
+  }
+  for (size_t i = 0; i < P; i++)
+    if ((s->local_mask >> i) & 1u) {
+      s->local[i].frame = s->sl.current_frame; s->local[i].input = local_row[i]; s->has_local[i] = 1;
+    }
+  int64_t rb0 = s->rollbacks;
+  if (p2p_advance_frame(s, rv, adv) < 0) return -1;
+  if (rb_frame) {
+    *rb_frame = -1;
+    for (size_t k = 0; k < rv->n && s->rollbacks != rb0; k++)
+      if (rv->v[k].kind == REQ_LOAD) { *rb_frame = rv->v[k].frame; break; }
+  }
+  for (size_t k = 0; k < rv->n; k++) {
+    if (rv->v[k].kind == REQ_LOAD) res->n_load++;
+    else if (rv->v[k].kind == REQ_SAVE) res->n_save++;
+    else res->n_advance++;
+  }
+  game_handle_requests(game, &s->sl, rv, 0);
+  return 0;
+}
+
 /* ---------------------------------------------------------------- arrival schedules (f1)
  * One peer's P2P session under an arbitrary remote-arrival schedule, with the prediction
  * threshold and disconnects: what the device engine's scheduled mode (ggrs_p2p_add_arrivals)
@@ -1458,51 +1516,11 @@ int oracle_p2p_sched_run(const OracleP2PCfg* cfg, int32_t calls, const uint8_t* 
   int32_t delivered = NULL_FRAME;
   int rc = 0;
   for (int32_t c = 0; c < calls && rc == 0; c++) {
-    const int32_t upto = arrive_upto[c];
-    if (upto > c) { rc = -1; break; }
-    for (int32_t g = delivered + 1; g <= upto && rc == 0; g++)   /* the burst */
-      for (size_t i = 0; i < P; i++) {
-        if (((s.local_mask >> i) & 1u) || s.disconnected[i]) continue;
-        if (s.sl.queues[i].length + 1 > INPUT_QUEUE_LENGTH) { rc = -4; break; }
-        p2p_on_remote_input(&s, i, g, inputs[(size_t)g * P + i]);
-      }
-    if (rc) break;
-    if (upto > delivered) delivered = upto;
-    const uint8_t ev = events ? events[c] : 0;
-    for (size_t i = 0; i < P; i++)                        /* Event::Disconnected */
-      if (((ev >> i) & 1u) && !((s.local_mask >> i) & 1u) && !s.disconnected[i]) {
-        s.disconnected[i] = 1;
-        if (s.sl.current_frame > s.last_frame[i]) s.disconnect_frame = s.last_frame[i] + 1;
-      }
-    int any_connected = 0;
-    for (size_t i = 0; i < P; i++) any_connected |= !s.disconnected[i];
-    if (!any_connected) { rc = -4; break; }
-    {  /* a rollback to a frame that is not in the past panics in load_frame (sync_layer.rs:231-237):
-        * a disconnect whose last_frame is current_frame - 1 sets disconnect_frame = current_frame
-        * (sparse saving loads the last save instead, p2p_session.rs:666-673) */
-      const int32_t fi = sl_check_simulation_consistency(&s.sl, s.disconnect_frame);
-      const int32_t load = s.sparse_saving ? s.sl.last_saved_frame : fi;
-      if (fi != NULL_FRAME && load >= s.sl.current_frame) { rc = -4; break; }
-    }
-    for (size_t i = 0; i < P; i++)
-      if ((s.local_mask >> i) & 1u) {
-        s.local[i].frame = s.sl.current_frame; s.local[i].input = inputs[(size_t)c * P + i]; s.has_local[i] = 1;
-      }
-    int64_t rb0 = s.rollbacks;
     int adv = 0;
-    if (p2p_advance_frame(&s, &rv, &adv) < 0) { rc = -1; break; }
+    rc = sched_session_call(&s, &game, &rv, c, inputs + (size_t)c * P, inputs, &delivered, arrive_upto[c],
+                            events ? events[c] : 0, &adv, rb_frame ? &rb_frame[c] : NULL, res);
+    if (rc) break;
     if (advanced) advanced[c] = (uint8_t)adv;
-    if (rb_frame) {
-      rb_frame[c] = -1;
-      for (size_t k = 0; k < rv.n && s.rollbacks != rb0; k++)
-        if (rv.v[k].kind == REQ_LOAD) { rb_frame[c] = rv.v[k].frame; break; }
-    }
-    for (size_t k = 0; k < rv.n; k++) {
-      if (rv.v[k].kind == REQ_LOAD) res->n_load++;
-      else if (rv.v[k].kind == REQ_SAVE) res->n_save++;
-      else res->n_advance++;
-    }
-    game_handle_requests(&game, &s.sl, &rv, 0);
     if (cksum_trace) cksum_trace[c] = game.last_checksum;
     res->frames_done = c + 1;
   }
@@ -1884,4 +1902,131 @@ int oracle_p2p_replay_batch(int32_t P, int64_t lanes, const uint8_t* start_state
   int rc = 0;
   for (int t = 0; t < used; t++) { pthread_join(th[t], NULL); if (jobs[t].rc) rc = jobs[t].rc; }
   return rc;
+}
+
+/* ---------------------------------------------------------------- two peers under arrival schedules
+ * Both machines of one match with desync detection (interval > 0), each under its own network:
+ * arrive[k][c] is the newest frame of the OTHER peer's players that peer k's call c polls (clamped
+ * here to what the other peer had queued by its previous call: a peer cannot receive a frame
+ * before it is sent).  Peer k's local players play inputs[k][c][P] (their columns of row c) at call
+ * c; what the other peer receives as their input of frame f is what peer k queued as frame f
+ * (add_local_input, input_queue.rs:170-186: with skipped calls that is the input of the call that
+ * first reached f), except that the input peer `corrupt_peer` queues at call `corrupt_call` reaches
+ * the other peer with bit 0 flipped (a corruption in flight: the two machines then simulate
+ * different matches, which their checksum reports must reveal).  Checksum reports travel with the
+ * inputs sent in the same call: peer k's report of call g reaches the other peer at the first of its
+ * calls c > g whose poll delivers peer k's last queued frame of call g.
+ * Outputs per peer k and call c: eff_inputs[k][c][P] (the input rows a device engine of peer k
+ * needs: its local players' input of call c, the remote players' input of frame c as received),
+ * eff_arrive[k][c], local_last[k][c] (after the call), the report sent (rep_frame, -1 none; rep_cs)
+ * and the frame last_confirmed_frame had when the call compared its pending reports (lconf[k][c]);
+ * the DesyncDetected events raised (ev_*: peer, call, frame, local and remote checksum; n_ev total);
+ * rc[k] (0, or -4 where the reference panics: that peer stops there).  desync_peer / desync_frame:
+ * as oracle_p2p_desync_pair_run (a game-state desync on one machine, Game.desync_frame). */
+int oracle_p2p_sched_desync_pair_run(int32_t num_players, int32_t max_prediction, int32_t predictor, int32_t interval,
+                                     const int32_t* local_mask, int32_t calls, const uint8_t* inputs,
+                                     const int32_t* arrive, int32_t corrupt_peer, int32_t corrupt_call,
+                                     int32_t desync_peer, int32_t desync_frame, uint8_t* eff_inputs, int32_t* eff_arrive, int32_t* local_last, int32_t* rep_frame,
+                                     uint16_t* rep_cs, int32_t* lconf, int32_t ev_cap, int32_t* ev_peer,
+                                     int32_t* ev_call, int32_t* ev_frame, uint16_t* ev_local, uint16_t* ev_remote,
+                                     int32_t* n_ev, int32_t* rc_out) {
+  const size_t P = (size_t)num_players;
+  *n_ev = 0;
+  if (P < 2 || P > MAX_PLAYERS || max_prediction < 1 || interval < 1 || calls < 1) return -1;
+  for (int k = 0; k < 2; k++)
+    if ((local_mask[k] & ~((1 << P) - 1)) != 0 || local_mask[k] == 0 || local_mask[k] == (1 << P) - 1) return -1;
+  if ((local_mask[0] | local_mask[1]) != (1 << P) - 1 || (local_mask[0] & local_mask[1])) return -1;
+  P2PSession s[2];
+  Game g[2];
+  Desync ds[2];
+  OracleP2PResult res[2];
+  RequestVec rv = {0};
+  memset(s, 0, sizeof s); memset(g, 0, sizeof g); memset(ds, 0, sizeof ds); memset(res, 0, sizeof res);
+  /* frame-indexed rows of what each peer queued (its local players' columns; as received by the other) */
+  uint8_t* sent_rows = (uint8_t*)calloc(2 * (size_t)calls * P, 1);
+  int32_t delivered[2] = {NULL_FRAME, NULL_FRAME}, ll_prev[2] = {NULL_FRAME, NULL_FRAME};
+  /* reports in flight to peer k: (sent call, frame, checksum, sender's last queued frame) */
+  int32_t* fl = (int32_t*)malloc(sizeof(int32_t) * 4 * 2 * (size_t)calls);
+  size_t fl_head[2] = {0, 0}, fl_tail[2] = {0, 0};
+  int32_t rc[2] = {0, 0};
+  for (int k = 0; k < 2; k++) {
+    s[k].num_players = P; s[k].max_prediction = (size_t)max_prediction;
+    s[k].local_mask = (uint32_t)local_mask[k];
+    sl_new(&s[k].sl, P, s[k].max_prediction, predictor);
+    for (size_t i = 0; i < P; i++) s[k].last_frame[i] = NULL_FRAME;
+    s[k].disconnect_frame = NULL_FRAME;
+    ds[k].interval = interval; ds[k].last_sent = NULL_FRAME;
+    s[k].ds = &ds[k];
+    state_new(&g[k].game_state, (uint64_t)P);
+    g[k].last_checksum_frame = NULL_FRAME;
+    g[k].desync_frame = k == desync_peer ? desync_frame : -1;
+  }
+  for (int32_t c = 0; c < calls; c++) {
+    const int32_t ll_snap[2] = {ll_prev[0], ll_prev[1]};  /* queued by the previous call */
+    for (int k = 0; k < 2; k++) {
+      const int o = 1 - k;
+      P2PSession* me = &s[k];
+      int32_t up = arrive[(size_t)k * calls + c];
+      if (up > ll_snap[o]) up = ll_snap[o];
+      if (up < delivered[k]) up = delivered[k];
+      eff_arrive[(size_t)k * calls + c] = up;
+      uint8_t* eff = eff_inputs + ((size_t)k * calls + c) * P;
+      for (size_t i = 0; i < P; i++) eff[i] = ((local_mask[k] >> i) & 1u) ? inputs[((size_t)k * calls + c) * P + i] : 0;
+      rep_frame[(size_t)k * calls + c] = -1; rep_cs[(size_t)k * calls + c] = 0;
+      lconf[(size_t)k * calls + c] = me->sl.last_confirmed_frame;
+      local_last[(size_t)k * calls + c] = ll_prev[k];
+      if (rc[k]) continue;
+      /* poll_remote_clients: the reports that travel with the inputs delivered now, in order */
+      while (fl_head[k] < fl_tail[k]) {
+        const int32_t* r = fl + 4 * ((size_t)k * calls + fl_head[k]);
+        if (r[0] >= c || r[3] > up) break;
+        ds_on_checksum_report(&ds[k], r[1], (uint16_t)r[2]);
+        fl_head[k]++;
+      }
+      int adv = 0;
+      const int32_t d0 = delivered[k];
+      rc[k] = sched_session_call(me, &g[k], &rv, c, eff, sent_rows + (size_t)o * calls * P, &delivered[k], up, 0, &adv,
+                                 NULL, &res[k]);
+      (void)d0;
+      if (rc[k]) continue;
+      if (me->sent) {
+        rep_frame[(size_t)k * calls + c] = me->sent_frame; rep_cs[(size_t)k * calls + c] = me->sent_cs;
+      }
+      for (size_t e = 0; e < me->n_events; e++) {
+        if (*n_ev < ev_cap) {
+          ev_peer[*n_ev] = k; ev_call[*n_ev] = c; ev_frame[*n_ev] = me->events[e].frame;
+          ev_local[*n_ev] = me->events[e].local_cs; ev_remote[*n_ev] = me->events[e].remote_cs;
+        }
+        *n_ev += 1;
+      }
+      /* what this call queued for its local players (the frame it reached, the input of this call) */
+      int32_t ll = NULL_FRAME;
+      for (size_t i = 0; i < P; i++)
+        if ((local_mask[k] >> i) & 1u) ll = me->last_frame[i];
+      if (ll != ll_prev[k] && ll >= 0 && ll < calls) {
+        for (int32_t f = ll_prev[k] + 1; f <= ll; f++)  /* (frames below the input delay: the default input) */
+          for (size_t i = 0; i < P; i++)
+            if ((local_mask[k] >> i) & 1u) {
+              uint8_t v = f == ll ? eff[i] : 0;
+              if (k == corrupt_peer && c == corrupt_call && f == ll) v ^= 1u;
+              sent_rows[((size_t)k * calls + f) * P + i] = v;
+            }
+      }
+      ll_prev[k] = ll;
+      local_last[(size_t)k * calls + c] = ll;
+      if (me->sent) {  /* in flight to the other peer with this call's inputs */
+        int32_t* r = fl + 4 * ((size_t)o * calls + fl_tail[o]);
+        r[0] = c; r[1] = me->sent_frame; r[2] = me->sent_cs; r[3] = ll;
+        fl_tail[o]++;
+      }
+    }
+  }
+  /* the remote players' columns of each peer's rows: the frames as the other peer queued them */
+  for (int k = 0; k < 2; k++)
+    for (int32_t f = 0; f < calls; f++)
+      for (size_t i = 0; i < P; i++)
+        if (!((local_mask[k] >> i) & 1u)) eff_inputs[((size_t)k * calls + f) * P + i] = sent_rows[((size_t)(1 - k) * calls + f) * P + i];
+  for (int k = 0; k < 2; k++) { rc_out[k] = rc[k]; state_free(&g[k].game_state); sl_free(&s[k].sl); }
+  free(rv.v); free(sent_rows); free(fl);
+  return 0;
 }

@@ -619,3 +619,50 @@ def p2p_replay_batch(start_states, start_index, load_frame, inputs, threads=None
     if rc != 0:
         raise ValueError("bad p2p replay batch arguments")
     return cks, st
+
+
+def p2p_sched_desync_pair_run(inputs, arrive, num_players=2, max_prediction=8, local_masks=(0b01, 0b10),
+                              predictor=0, interval=10, corrupt_peer=-1, corrupt_call=-1, desync_peer=-1,
+                              desync_frame=-1, ev_cap=4096):
+    """Both peers of one match under their own arrival schedules with DesyncDetection::On{interval}
+    (oracle_p2p_sched_desync_pair_run): inputs[2][calls][P] each peer's local players' inputs per
+    call, arrive[2][calls] the newest frame of the other peer each call polls.  Returns the rows a
+    device engine of each peer needs (eff_inputs [2][calls][P], eff_arrive [2][calls]), per call the
+    report sent (rep_frame / rep_cs), last_confirmed_frame at the comparison (lconf) and the last
+    queued local frame (local_last), the DesyncDetected events (peer, call, frame, local, remote) in
+    call order, and each peer's rc."""
+    inputs = np.ascontiguousarray(inputs, np.uint8)
+    calls = inputs.shape[1]
+    arrive = np.ascontiguousarray(arrive, np.int32)
+    masks = np.array(local_masks, np.int32)
+    out = dict(eff_inputs=np.zeros((2, calls, num_players), np.uint8), eff_arrive=np.zeros((2, calls), np.int32),
+               local_last=np.zeros((2, calls), np.int32), rep_frame=np.zeros((2, calls), np.int32),
+               rep_cs=np.zeros((2, calls), np.uint16), lconf=np.zeros((2, calls), np.int32))
+    ev = {k: np.zeros(ev_cap, t) for k, t in (("peer", np.int32), ("call", np.int32), ("frame", np.int32),
+                                              ("local", np.uint16), ("remote", np.uint16))}
+    n_ev = ctypes.c_int32(0)
+    rc = np.zeros(2, np.int32)
+    L = lib()
+    P_ = ctypes.POINTER
+    u8p, u16p, i32p, i32 = P_(ctypes.c_uint8), P_(ctypes.c_uint16), P_(ctypes.c_int32), ctypes.c_int32
+    L.oracle_p2p_sched_desync_pair_run.argtypes = [i32, i32, i32, i32, i32p, i32, u8p, i32p, i32, i32, i32, i32,
+                                                   u8p, i32p, i32p, i32p, u16p, i32p, i32, i32p, i32p, i32p, u16p,
+                                                   u16p, i32p, i32p]
+    L.oracle_p2p_sched_desync_pair_run.restype = ctypes.c_int
+    r = L.oracle_p2p_sched_desync_pair_run(
+        num_players, max_prediction, predictor, interval, _ptr(masks, ctypes.c_int32), calls,
+        _ptr(inputs, ctypes.c_uint8), _ptr(arrive, ctypes.c_int32), corrupt_peer, corrupt_call, desync_peer,
+        desync_frame, _ptr(out["eff_inputs"], ctypes.c_uint8), _ptr(out["eff_arrive"], ctypes.c_int32),
+        _ptr(out["local_last"], ctypes.c_int32), _ptr(out["rep_frame"], ctypes.c_int32),
+        _ptr(out["rep_cs"], ctypes.c_uint16), _ptr(out["lconf"], ctypes.c_int32), ev_cap,
+        _ptr(ev["peer"], ctypes.c_int32), _ptr(ev["call"], ctypes.c_int32), _ptr(ev["frame"], ctypes.c_int32),
+        _ptr(ev["local"], ctypes.c_uint16), _ptr(ev["remote"], ctypes.c_uint16), ctypes.byref(n_ev),
+        _ptr(rc, ctypes.c_int32))
+    if r != 0:
+        raise ValueError("bad pair-run arguments")
+    n = min(n_ev.value, ev_cap)
+    out["events"] = [(int(ev["peer"][i]), int(ev["call"][i]), int(ev["frame"][i]), int(ev["local"][i]),
+                      int(ev["remote"][i])) for i in range(n)]
+    out["n_events"] = n_ev.value
+    out["rc"] = rc
+    return out

@@ -4,7 +4,7 @@
 #![allow(non_camel_case_types)]
 use std::os::raw::{c_char, c_void};
 
-pub const GGRS_ABI_VERSION: i32 = 4;
+pub const GGRS_ABI_VERSION: i32 = 5;
 
 pub const GGRS_OK: i32 = 0;
 pub const GGRS_E_INVALID: i32 = -1;
@@ -284,6 +284,15 @@ extern "C" {
         frames: *mut i32,
         skipped: *mut i32,
         errors: *mut i32,
+    ) -> i32;
+    pub fn ggrs_p2p_read_reports(
+        eng: *mut ggrs_p2p_engine_t,
+        first_call: i32,
+        n_calls: i32,
+        frames: *mut i32,
+        checksums: *mut u16,
+        last_confirmed: *mut i32,
+        local_last: *mut i32,
     ) -> i32;
 
     // ---- input wire codec, batched (src/network/compression.rs:14-182); device pointers
