@@ -454,13 +454,15 @@ def run_branch(args):
         try:
             from oracle import oracle as O
             O.build()
-            st = O.state_new(P)
-            for f in range(eng.trunk_frame()):
-                st = O.state_advance(st, truth[f, 0])
-            ck, _ = eng.report()
-            parity = {"session0_trunk_bit_exact": bytes(eng.trunk(0)) == bytes(st),
-                      "session0_checksum": int(ck[0]) == O.fletcher16(bytes(st)),
-                      "desyncs": int((eng.desync() >= 0).sum()) + n_desync}
+            from oracle import every_lane
+            # EVERY lane's last speculated window (cells and states), every report checksum and
+            # survival bit against the oracle's replay (oracle_p2p_replay_batch)
+            r = every_lane.branch(eng, truth)
+            parity = {k: v for k, v in r.items() if k != "trunk_states"}
+            parity["session0_trunk_bit_exact"] = bytes(eng.trunk(0)) == bytes(r["trunk_states"][0])
+            parity["desyncs"] += n_desync
+            parity["every_lane_bit_exact"] = (all(v == 0 for k, v in parity.items() if k.endswith("_mismatched"))
+                                              and parity["session0_trunk_bit_exact"])
         except Exception as exc:
             parity = {"error": repr(exc)}
         cpu_baseline = None
@@ -689,17 +691,12 @@ def run_p2p(args):
         try:
             from oracle import oracle as O
             O.build()
-            ok = True
-            for s in (0, 1, S // 2, S - 1):
-                if sched:
-                    r = O.p2p_sched_run(rows[:, s], arrive[:, s], num_players=P, local_mask=0b01, max_prediction=maxp,
-                                        sparse_saving=bool(args.sparse))
-                    ok &= r["rc"] == 0 and int(fr1[s]) == r["current_frame"] and int(sk1[s]) == r["skips"]
-                else:
-                    r = O.p2p_run(rows[:, s], num_players=P, local_mask=0b01, max_prediction=maxp, latency=D,
-                                  sparse_saving=bool(args.sparse))
-                ok &= bytes(eng.state(s)) == bytes(r["final_state"]) and int(rb1[s]) == r["result"].rollbacks
-            parity = {"sessions_0_1_mid_last_bit_exact": bool(ok)}
+            from oracle import every_lane
+            # EVERY session against the oracle's P2PSession (oracle_p2p_batch): final state, rollbacks,
+            # and under a schedule the current frame and skipped calls
+            parity = every_lane.p2p(eng, rows, arrive, P=P, local_mask=eng.local_mask, maxp=maxp, latency=D,
+                                    sparse=bool(args.sparse))
+            parity["every_session_bit_exact"] = all(v == 0 for k, v in parity.items() if k.endswith("_mismatched"))
             if peers:
                 parity["peers_desync_events"] = n_desync
             if world == 1 and not args.no_cpu_baseline:
@@ -1449,11 +1446,12 @@ def main():
         try:
             from oracle import oracle as O  # checker + CPU baseline only
             O.build()
-            ref = O.synctest_run(inputs[:, 0, :], P, maxp, cd, delay)
-            parity = {"lane0_final_state_bit_exact": bytes(eng.state(0)) == bytes(ref["final_state"]),
-                      "lane0_trace_bit_exact": bool(
-                          (eng.trace(total_frames - trace_cap, trace_cap)[:, 0] ==
-                           ref["cksum"][total_frames - trace_cap:]).all())}
+            from oracle import every_lane
+            # EVERY lane against the oracle's SyncTestSession (oracle_synctest_batch on the job's
+            # CPU share): final state, ring checksums, the trace's last trace_cap frames
+            parity = every_lane.synctest(eng, inputs, P, maxp, cd, delay, trace_first=total_frames - trace_cap,
+                                         trace_n=trace_cap)
+            parity["every_lane_bit_exact"] = all(v == 0 for k, v in parity.items() if k.endswith("_mismatched"))
             if world == 1 and not args.no_cpu_baseline:
                 threads = cpu_threads(args)
                 frames = max(args.cpu_frames, total_frames)

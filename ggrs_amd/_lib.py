@@ -12,7 +12,7 @@ _EXP = os.environ.get("GGRS_AMD_EXP_LIB")
 if _EXP:
     LIB_PATH = os.path.join(HERE, "exp", os.path.basename(_EXP))
 
-ABI_VERSION = 5  # include/ggrs_amd.h GGRS_ABI_VERSION
+ABI_VERSION = 6  # include/ggrs_amd.h GGRS_ABI_VERSION
 GGRS_OK = 0
 GGRS_E_INVALID = -1
 GGRS_E_PRECONDITION = -2
@@ -32,7 +32,7 @@ EXPORTS = (
     "ggrs_abi_version", "ggrs_last_error", "ggrs_engine_create", "ggrs_engine_destroy",
     "ggrs_engine_config", "ggrs_add_local_inputs", "ggrs_add_local_inputs_device",
     "ggrs_synctest_advance_frames", "ggrs_handle_requests", "ggrs_synchronize",
-    "ggrs_current_frame", "ggrs_read_mismatches", "ggrs_read_save_checksums", "ggrs_read_save_checksums_frames", "ggrs_read_state",
+    "ggrs_current_frame", "ggrs_read_mismatches", "ggrs_read_save_checksums", "ggrs_read_save_checksums_frames", "ggrs_read_state", "ggrs_read_states",
     "ggrs_read_ring", "ggrs_read_trace", "ggrs_debug_corrupt_on_load", "ggrs_last_launch_ms",
     "ggrs_timing_reset", "ggrs_timing_stop", "ggrs_timing_read", "ggrs_set_synctest_path",
     "ggrs_lane_batch_map", "ggrs_lane_batch_run", "ggrs_handle_requests_lanes", "ggrs_read_lane_frames",
@@ -42,7 +42,7 @@ EXPORTS = (
     "ggrs_branch_add_inputs", "ggrs_branch_speculate", "ggrs_branch_confirm",
     "ggrs_branch_report_bytes", "ggrs_branch_synchronize", "ggrs_branch_trunk_frame",
     "ggrs_branch_read_report", "ggrs_branch_read_desync", "ggrs_branch_read_trunk",
-    "ggrs_branch_read_lane", "ggrs_branch_timing_reset", "ggrs_branch_timing_stop", "ggrs_branch_timing_read",
+    "ggrs_branch_read_lane", "ggrs_branch_read_cells", "ggrs_branch_timing_reset", "ggrs_branch_timing_stop", "ggrs_branch_timing_read",
     "ggrs_branch_rounds", "ggrs_branch_set_round_launches", "ggrs_branch_set_stream", "ggrs_branch_use_own_stream",
     "ggrs_branch_round", "ggrs_branch_rounds_reports", "ggrs_branch_compare_peer", "ggrs_branch_compare_peer_rows",
     "ggrs_particle_engine_create", "ggrs_particle_engine_destroy", "ggrs_particle_add_local_inputs",
@@ -56,7 +56,7 @@ EXPORTS = (
     "ggrs_p2p_read_trace", "ggrs_p2p_timing_reset", "ggrs_p2p_timing_stop", "ggrs_p2p_timing_read",
     "ggrs_p2p_set_desync_detection", "ggrs_p2p_local_checksums", "ggrs_p2p_compare_checksums",
     "ggrs_p2p_debug_desync", "ggrs_p2p_set_sparse_saving", "ggrs_p2p_set_unstaged",
-    "ggrs_p2p_set_arrival_schedule", "ggrs_p2p_add_arrivals", "ggrs_p2p_read_sessions", "ggrs_p2p_read_reports",
+    "ggrs_p2p_set_arrival_schedule", "ggrs_p2p_add_arrivals", "ggrs_p2p_read_sessions", "ggrs_p2p_read_reports", "ggrs_p2p_read_states",
     "ggrs_codec_encode", "ggrs_codec_decode", "ggrs_codec_encode_chunked", "ggrs_codec_decode_chunked", "ggrs_codec_max_packet_bytes", "ggrs_codec_set_direct",
 )
 
@@ -141,6 +141,7 @@ def lib():
         L.ggrs_read_save_checksums.argtypes = [vp, ctypes.c_int32, vp]
         L.ggrs_read_save_checksums_frames.argtypes = [vp, vp, ctypes.c_int32, vp]
         L.ggrs_read_state.argtypes = [vp, ctypes.c_int32, vp]
+        L.ggrs_read_states.argtypes = [vp, vp]
         L.ggrs_read_ring.argtypes = [vp, ctypes.c_int32, vp, vp, vp]
         L.ggrs_read_trace.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, vp]
         L.ggrs_debug_corrupt_on_load.argtypes = [vp, ctypes.c_int32, ctypes.c_int32]

@@ -50,6 +50,7 @@ def _bind(L):
     L.ggrs_branch_read_desync.argtypes = [vp, vp]
     L.ggrs_branch_read_trunk.argtypes = [vp, ctypes.c_int32, vp]
     L.ggrs_branch_read_lane.argtypes = [vp, ctypes.c_int64, ctypes.c_int32, P(ctypes.c_uint16), vp]
+    L.ggrs_branch_read_cells.argtypes = [vp, ctypes.c_int32, vp, vp]
     L.ggrs_branch_timing_reset.argtypes = [vp]
     L.ggrs_branch_timing_stop.argtypes = [vp]
     L.ggrs_branch_timing_read.argtypes = [vp, P(ctypes.c_float), P(ctypes.c_int32)]
@@ -223,6 +224,13 @@ class BranchEngine:
         ck = ctypes.c_uint16()
         _lib.check(self._L.ggrs_branch_read_lane(self._h, lane, frame, ctypes.byref(ck), _vp(out)))
         return int(ck.value), out
+
+    def cells(self, frame, states=True):
+        """lane_state for every lane: (checksums [num_lanes], states [num_lanes][sb] or None)."""
+        ck = np.zeros(self.num_lanes, np.uint16)
+        st = np.zeros((self.num_lanes, self.state_bytes), np.uint8) if states else None
+        _lib.check(self._L.ggrs_branch_read_cells(self._h, frame, _vp(ck), _vp(st) if states else None))
+        return ck, st
 
     def timing_reset(self):
         _lib.check(self._L.ggrs_branch_timing_reset(self._h))

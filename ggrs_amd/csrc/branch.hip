@@ -1058,6 +1058,39 @@ int ggrs_branch_read_lane(ggrs_branch_engine_t* e, int64_t lane, int32_t frame, 
   return GGRS_OK;
 }
 
+int ggrs_branch_read_cells(ggrs_branch_engine_t* e, int32_t frame, uint16_t* checksums, uint8_t* states) {
+  if (!e || !checksums) return set_error(GGRS_E_INVALID, "null argument");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const int slot = ((frame % e->R) + e->R) % e->R;
+  const int64_t L = e->L, B = e->cfg.branches;
+  std::vector<uint16_t> ck((size_t)L);
+  std::vector<uint32_t> soa(states ? (size_t)e->F * L : 0);
+  HIP_TRY(hipMemcpyAsync(ck.data(), e->ring_ck + (size_t)slot * L, (size_t)L * 2, hipMemcpyDeviceToHost, e->stream));
+  if (states)
+    HIP_TRY(hipMemcpyAsync(soa.data(), e->ring + (size_t)slot * e->F * L, soa.size() * 4, hipMemcpyDeviceToHost,
+                           e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  // resolved as ggrs_branch_read_lane: a prefix-shared cell is held by the prefix's representative
+  const bool shared = e->E > 0 && e->last_spec_fc >= 0 && frame >= e->last_spec_fc &&
+                      frame <= e->last_spec_fc + e->cfg.window;
+  const int k = shared && frame > e->last_spec_fc ? frame - e->last_spec_fc - 1 : 0;
+  const int sb = 36 + 20 * e->cfg.num_players;
+  uint32_t w[64];
+  for (int64_t lane = 0; lane < L; lane++) {
+    int64_t cell = lane;
+    if (shared) {
+      const int64_t sess = lane / B;
+      cell = sess * B + rep_branch(lane - sess * B, k, e->cfg.alphabet, e->E);
+    }
+    checksums[lane] = ck[(size_t)cell];
+    if (states) {
+      for (int j = 0; j < e->F; j++) w[j] = soa[(size_t)j * L + cell];
+      serialize_state_bytes(w, e->cfg.num_players, states + (size_t)lane * sb);
+    }
+  }
+  return GGRS_OK;
+}
+
 int ggrs_branch_timing_reset(ggrs_branch_engine_t* e) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
   HIP_TRY(hipSetDevice(e->cfg.device));

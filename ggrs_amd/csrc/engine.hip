@@ -1676,6 +1676,23 @@ int ggrs_read_state(ggrs_engine_t* e, int32_t lane, uint8_t* out) {
   return GGRS_OK;
 }
 
+int ggrs_read_states(ggrs_engine_t* e, uint8_t* out) {
+  if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
+  { int rc_ = resolve(e); if (rc_) return rc_; }
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const size_t L = e->cfg.num_lanes;
+  const int sb = bincode_bytes(e->cfg.num_players);
+  std::vector<uint32_t> soa((size_t)e->F * L);  // word k of every lane, one copy
+  HIP_TRY(hipMemcpyAsync(soa.data(), e->cur, soa.size() * 4, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  uint32_t w[32];
+  for (size_t l = 0; l < L; l++) {
+    for (int k = 0; k < e->F; k++) w[k] = soa[(size_t)k * L + l];
+    serialize_state_bytes(w, e->cfg.num_players, out + l * sb);
+  }
+  return GGRS_OK;
+}
+
 int ggrs_read_ring(ggrs_engine_t* e, int32_t lane, int32_t* frames, uint16_t* cks, uint8_t* states) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
   { int rc_ = resolve(e); if (rc_) return rc_; }

@@ -2172,6 +2172,22 @@ int ggrs_p2p_read_state(ggrs_p2p_engine_t* e, int32_t session, uint8_t* out) {
   return read_record(e, e->cur + session, e->cfg.num_sessions, out);
 }
 
+int ggrs_p2p_read_states(ggrs_p2p_engine_t* e, uint8_t* out) {
+  if (!e || !out) return set_error(GGRS_E_INVALID, "null argument");
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  const int64_t S = e->cfg.num_sessions;
+  const size_t sb = 36 + 20 * (size_t)e->cfg.num_players;
+  std::vector<uint32_t> soa((size_t)e->F * S);  // field k of every session, one copy
+  HIP_TRY(hipMemcpyAsync(soa.data(), e->cur, soa.size() * 4, hipMemcpyDeviceToHost, e->stream));
+  HIP_TRY(hipStreamSynchronize(e->stream));
+  std::vector<uint32_t> w(e->F);
+  for (int64_t s = 0; s < S; s++) {
+    for (int k = 0; k < e->F; k++) w[k] = soa[(size_t)k * S + s];
+    serialize_state_bytes(w.data(), e->cfg.num_players, out + (size_t)s * sb);
+  }
+  return GGRS_OK;
+}
+
 int ggrs_p2p_read_ring(ggrs_p2p_engine_t* e, int32_t session, int32_t* frames, uint16_t* checksums, uint8_t* states) {
   if (!e) return set_error(GGRS_E_INVALID, "null engine");
   if (session < 0 || session >= e->cfg.num_sessions) return set_error(GGRS_E_INVALID, "session out of range");

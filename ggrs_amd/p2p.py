@@ -51,6 +51,7 @@ def _bind(L):
     L.ggrs_p2p_calls.argtypes = [vp, P(i32)]
     L.ggrs_p2p_synchronize.argtypes = [vp]
     L.ggrs_p2p_read_state.argtypes = [vp, i32, vp]
+    L.ggrs_p2p_read_states.argtypes = [vp, vp]
     L.ggrs_p2p_read_ring.argtypes = [vp, i32, vp, vp, vp]
     L.ggrs_p2p_read_stats.argtypes = [vp, vp, vp]
     L.ggrs_p2p_read_queues.argtypes = [vp, vp]
@@ -140,6 +141,12 @@ class P2PEngine:
     def state(self, session):
         out = np.zeros(self.state_bytes, np.uint8)
         _lib.check(self._L.ggrs_p2p_read_state(self._h, session, _vp(out)))
+        return out
+
+    def states(self):
+        """state(session) for every session, one transfer: [num_sessions][state_bytes]."""
+        out = np.zeros((self.num_sessions, self.state_bytes), np.uint8)
+        _lib.check(self._L.ggrs_p2p_read_states(self._h, _vp(out)))
         return out
 
     def ring(self, session):

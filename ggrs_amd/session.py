@@ -203,6 +203,12 @@ class Engine:
         _lib.check(self._L.ggrs_read_state(self._h, lane, _vp(out)))
         return out
 
+    def states(self):
+        """state(lane) for every lane, one transfer: [num_lanes][state_bytes]."""
+        out = np.zeros((self.num_lanes, self.state_bytes), np.uint8)
+        _lib.check(self._L.ggrs_read_states(self._h, _vp(out)))
+        return out
+
     def ring(self, lane):
         fr = np.zeros(self.ring_len, np.int32)
         ck = np.zeros(self.ring_len, np.uint16)

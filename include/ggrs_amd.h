@@ -54,8 +54,9 @@ extern "C" {
  * stream); ggrs_branch_use_own_stream returns to the engine's own
  * 4: P2P arrival schedules (ggrs_p2p_set_arrival_schedule, ggrs_p2p_add_arrivals,
  * ggrs_p2p_read_sessions)
- * 5: desync detection under arrival schedules (ggrs_p2p_read_reports) */
-#define GGRS_ABI_VERSION 5
+ * 5: desync detection under arrival schedules (ggrs_p2p_read_reports)
+ * 6: bulk reads for every-lane checks (ggrs_read_states, ggrs_p2p_read_states, ggrs_branch_read_cells) */
+#define GGRS_ABI_VERSION 6
 
 #define GGRS_OK 0
 #define GGRS_E_INVALID (-1)      /* GgrsError::InvalidRequest: bad argument or configuration */
@@ -261,6 +262,8 @@ int ggrs_read_save_checksums(ggrs_engine_t* eng, int32_t frame, uint16_t* out);
 int ggrs_read_save_checksums_frames(ggrs_engine_t* eng, const int32_t* frames, int32_t n, uint16_t* out);
 /* Current game state of one lane as bincode bytes (36 + 20 * num_players). */
 int ggrs_read_state(ggrs_engine_t* eng, int32_t lane, uint8_t* out);
+/* ggrs_read_state for every lane, one transfer: out[num_lanes][36 + 20 * num_players]. */
+int ggrs_read_states(ggrs_engine_t* eng, uint8_t* out);
 /* Saved-state ring of one lane: frames[R], checksums[R], states[R][36 + 20 * num_players]. */
 int ggrs_read_ring(ggrs_engine_t* eng, int32_t lane, int32_t* frames, uint16_t* checksums,
                    uint8_t* states);
@@ -337,6 +340,9 @@ int ggrs_branch_read_trunk(ggrs_branch_engine_t* eng, int32_t session, uint8_t* 
  * the cell of the lane's prefix representative, which holds the same state) */
 int ggrs_branch_read_lane(ggrs_branch_engine_t* eng, int64_t lane, int32_t frame, uint16_t* checksum,
                           uint8_t* out);
+/* ggrs_branch_read_lane for every lane at once (checking every lane against a CPU replay):
+ * checksums [num_sessions * branches], states [num_sessions * branches][36 + 20 P] or NULL */
+int ggrs_branch_read_cells(ggrs_branch_engine_t* eng, int32_t frame, uint16_t* checksums, uint8_t* states);
 int ggrs_branch_timing_reset(ggrs_branch_engine_t* eng);
 int ggrs_branch_timing_stop(ggrs_branch_engine_t* eng); /* as ggrs_timing_stop */
 int ggrs_branch_timing_read(ggrs_branch_engine_t* eng, float* total_ms, int32_t* launches);
@@ -464,6 +470,8 @@ int ggrs_p2p_current_frame(const ggrs_p2p_engine_t* eng, int32_t* out);
 int ggrs_p2p_calls(const ggrs_p2p_engine_t* eng, int32_t* out);
 int ggrs_p2p_synchronize(ggrs_p2p_engine_t* eng);
 int ggrs_p2p_read_state(ggrs_p2p_engine_t* eng, int32_t session, uint8_t* out);
+/* ggrs_p2p_read_state for every session, one transfer: out[num_sessions][36 + 20 * num_players] */
+int ggrs_p2p_read_states(ggrs_p2p_engine_t* eng, uint8_t* out);
 /* the session's saved-state ring (SavedStates, sync_layer.rs:144-166): per slot frame, checksum,
  * bincode state (36 + 20 P bytes) */
 int ggrs_p2p_read_ring(ggrs_p2p_engine_t* eng, int32_t session, int32_t* frames, uint16_t* checksums,

@@ -1904,6 +1904,68 @@ int oracle_p2p_replay_batch(int32_t P, int64_t lanes, const uint8_t* start_state
   return rc;
 }
 
+typedef struct {
+  const OracleP2PCfg* cfg;
+  int32_t calls;
+  int64_t lanes, a, b;
+  const uint8_t* inputs;
+  const int32_t* arrive;
+  uint8_t* final_states;
+  int64_t* rollbacks;
+  int64_t* resim;
+  int32_t* current_frame;
+  int32_t* skips;
+  int32_t* rc;
+} P2PBatchJob;
+static void* p2p_batch_worker(void* arg) {
+  P2PBatchJob* j = (P2PBatchJob*)arg;
+  const size_t P = (size_t)j->cfg->num_players, sb = 36 + 20 * P;
+  uint8_t* in = (uint8_t*)malloc((size_t)j->calls * P);
+  int32_t* up = (int32_t*)malloc((size_t)j->calls * 4);
+  for (int64_t l = j->a; l < j->b; l++) {
+    for (int32_t c = 0; c < j->calls; c++) {
+      memcpy(in + (size_t)c * P, j->inputs + ((size_t)c * j->lanes + l) * P, P);
+      if (j->arrive) up[c] = j->arrive[(size_t)c * j->lanes + l];
+    }
+    OracleP2PResult res;
+    uint8_t* fs = j->final_states ? j->final_states + l * sb : NULL;
+    const int rc = j->arrive ? oracle_p2p_sched_run(j->cfg, j->calls, in, up, NULL, NULL, NULL, NULL, fs, NULL, NULL,
+                                                    NULL, &res)
+                             : oracle_p2p_run(j->cfg, j->calls, in, NULL, NULL, NULL, 0, NULL, fs, NULL, NULL, NULL, &res);
+    if (j->rc) j->rc[l] = rc ? rc : res.status;
+    if (j->rollbacks) j->rollbacks[l] = res.rollbacks;
+    if (j->resim) j->resim[l] = res.resim;
+    const int32_t cur = (int32_t)(res.n_advance - res.resim);
+    if (j->current_frame) j->current_frame[l] = cur;
+    if (j->skips) j->skips[l] = res.frames_done - cur;
+  }
+  free(in); free(up);
+  return NULL;
+}
+/* One peer's P2P session per lane of an engine-layout block inputs[calls][lanes][P]: with arrive
+ * ([calls][lanes], the newest remote frame each call polls) oracle_p2p_sched_run, else
+ * oracle_p2p_run at cfg->latency.  Per lane: final state, rollbacks, resimulated frames, current
+ * frame, skipped calls and rc (any output may be NULL). */
+int oracle_p2p_batch(const OracleP2PCfg* cfg, int32_t calls, int64_t lanes, const uint8_t* inputs,
+                     const int32_t* arrive, int32_t threads, uint8_t* final_states, int64_t* rollbacks, int64_t* resim,
+                     int32_t* current_frame, int32_t* skips, int32_t* rc) {
+  if (threads < 1) threads = 1;
+  if (threads > 64) threads = 64;
+  pthread_t th[64]; P2PBatchJob jobs[64];
+  const int64_t per = (lanes + threads - 1) / threads;
+  int used = 0;
+  for (int t = 0; t < threads; t++) {
+    const int64_t a = (int64_t)t * per, b = a + per < lanes ? a + per : lanes;
+    if (a >= b) break;
+    jobs[t] = (P2PBatchJob){cfg, calls, lanes, a, b, inputs, arrive, final_states, rollbacks, resim, current_frame,
+                            skips, rc};
+    pthread_create(&th[t], NULL, p2p_batch_worker, &jobs[t]);
+    used++;
+  }
+  for (int t = 0; t < used; t++) pthread_join(th[t], NULL);
+  return 0;
+}
+
 /* ---------------------------------------------------------------- two peers under arrival schedules
  * Both machines of one match with desync detection (interval > 0), each under its own network:
  * arrive[k][c] is the newest frame of the OTHER peer's players that peer k's call c polls (clamped

@@ -621,6 +621,35 @@ def p2p_replay_batch(start_states, start_index, load_frame, inputs, threads=None
     return cks, st
 
 
+def p2p_batch(inputs, arrive=None, num_players=2, local_mask=0b01, input_delay=0, max_prediction=8, latency=4,
+              predictor=0, sparse_saving=False, threads=None):
+    """p2p_run (arrive None, fixed latency) or p2p_sched_run (arrive[calls][lanes]) for every lane of
+    inputs[calls][lanes][P] on `threads` threads: dict of final_states [lanes][sb], rollbacks,
+    resim, current_frame, skips, rc [lanes]."""
+    inputs = np.ascontiguousarray(inputs, np.uint8)
+    calls, lanes = inputs.shape[0], inputs.shape[1]
+    arr = None if arrive is None else np.ascontiguousarray(arrive, np.int32)
+    if arr is not None:
+        assert arr.shape[:2] == (calls, lanes)
+        latency = 1
+    cfg = P2PCfg(num_players, max_prediction, input_delay, latency, local_mask, predictor, int(sparse_saving))
+    out = dict(final_states=np.zeros((lanes, state_bytes(num_players)), np.uint8),
+               rollbacks=np.zeros(lanes, np.int64), resim=np.zeros(lanes, np.int64),
+               current_frame=np.zeros(lanes, np.int32), skips=np.zeros(lanes, np.int32), rc=np.zeros(lanes, np.int32))
+    L = lib()
+    P_ = ctypes.POINTER
+    u8p, i32p, i64p = P_(ctypes.c_uint8), P_(ctypes.c_int32), P_(ctypes.c_int64)
+    L.oracle_p2p_batch.argtypes = [P_(P2PCfg), ctypes.c_int32, ctypes.c_int64, u8p, i32p, ctypes.c_int32, u8p, i64p,
+                                   i64p, i32p, i32p, i32p]
+    L.oracle_p2p_batch.restype = ctypes.c_int
+    L.oracle_p2p_batch(ctypes.byref(cfg), calls, lanes, _ptr(inputs, ctypes.c_uint8), _ptr(arr, ctypes.c_int32),
+                       threads or default_threads(), _ptr(out["final_states"], ctypes.c_uint8),
+                       _ptr(out["rollbacks"], ctypes.c_int64), _ptr(out["resim"], ctypes.c_int64),
+                       _ptr(out["current_frame"], ctypes.c_int32), _ptr(out["skips"], ctypes.c_int32),
+                       _ptr(out["rc"], ctypes.c_int32))
+    return out
+
+
 def p2p_sched_desync_pair_run(inputs, arrive, num_players=2, max_prediction=8, local_masks=(0b01, 0b10),
                               predictor=0, interval=10, corrupt_peer=-1, corrupt_call=-1, desync_peer=-1,
                               desync_frame=-1, ev_cap=4096):

@@ -4,7 +4,7 @@
 #![allow(non_camel_case_types)]
 use std::os::raw::{c_char, c_void};
 
-pub const GGRS_ABI_VERSION: i32 = 5;
+pub const GGRS_ABI_VERSION: i32 = 6;
 
 pub const GGRS_OK: i32 = 0;
 pub const GGRS_E_INVALID: i32 = -1;
@@ -186,6 +186,7 @@ extern "C" {
     pub fn ggrs_read_save_checksums(eng: *mut ggrs_engine_t, frame: i32, out: *mut u16) -> i32;
     pub fn ggrs_read_save_checksums_frames(eng: *mut ggrs_engine_t, frames: *const i32, n: i32, out: *mut u16) -> i32;
     pub fn ggrs_read_state(eng: *mut ggrs_engine_t, lane: i32, out: *mut u8) -> i32;
+    pub fn ggrs_read_states(eng: *mut ggrs_engine_t, out: *mut u8) -> i32;
     pub fn ggrs_read_ring(eng: *mut ggrs_engine_t, lane: i32, frames: *mut i32, checksums: *mut u16,
                           states: *mut u8) -> i32;
     pub fn ggrs_read_trace(eng: *mut ggrs_engine_t, first_frame: i32, n_frames: i32, out: *mut u16) -> i32;
@@ -211,6 +212,8 @@ extern "C" {
     pub fn ggrs_branch_read_trunk(eng: *mut ggrs_branch_engine_t, session: i32, out: *mut u8) -> i32;
     pub fn ggrs_branch_read_lane(eng: *mut ggrs_branch_engine_t, lane: i64, frame: i32, checksum: *mut u16,
                                  out: *mut u8) -> i32;
+    pub fn ggrs_branch_read_cells(eng: *mut ggrs_branch_engine_t, frame: i32, checksums: *mut u16, states: *mut u8)
+                                  -> i32;
     pub fn ggrs_branch_timing_reset(eng: *mut ggrs_branch_engine_t) -> i32;
     pub fn ggrs_branch_timing_stop(eng: *mut ggrs_branch_engine_t) -> i32;
     pub fn ggrs_branch_timing_read(eng: *mut ggrs_branch_engine_t, total_ms: *mut f32, launches: *mut i32) -> i32;
@@ -256,6 +259,7 @@ extern "C" {
     pub fn ggrs_p2p_calls(eng: *const ggrs_p2p_engine_t, out: *mut i32) -> i32;
     pub fn ggrs_p2p_synchronize(eng: *mut ggrs_p2p_engine_t) -> i32;
     pub fn ggrs_p2p_read_state(eng: *mut ggrs_p2p_engine_t, session: i32, out: *mut u8) -> i32;
+    pub fn ggrs_p2p_read_states(eng: *mut ggrs_p2p_engine_t, out: *mut u8) -> i32;
     pub fn ggrs_p2p_read_ring(eng: *mut ggrs_p2p_engine_t, session: i32, frames: *mut i32, checksums: *mut u16,
                               states: *mut u8) -> i32;
     pub fn ggrs_p2p_read_stats(eng: *mut ggrs_p2p_engine_t, rollbacks: *mut i32, resim_frames: *mut i64) -> i32;

@@ -23,7 +23,7 @@ def test_library_exports_every_symbol(engine_lib):
     import ctypes
     for name in header_symbols():
         assert hasattr(engine_lib, name), name
-    assert engine_lib.ggrs_abi_version() == 5
+    assert engine_lib.ggrs_abi_version() == 6
 
 
 def test_nm_exports(engine_lib):

@@ -24,6 +24,17 @@ def branch_inputs(eng, truth, f_c, lane, W):
     return np.array(rows, np.uint8)
 
 
+def check_every_lane(oracle, eng, truth):
+    """Every lane's last speculated window, every report checksum and survival bit, no desync
+    (oracle/every_lane.py: oracle_p2p_replay_batch from the oracle's confirmed trunk)."""
+    from oracle import every_lane
+    r = every_lane.branch(eng, truth)
+    assert r["cells_mismatched"] == 0, (r["cells_mismatched"], r["first_bad_lane"])
+    assert r["report_mismatched"] == 0 and r["survivors_mismatched"] == 0 and r["desyncs"] == 0
+    for s in (0, eng.num_sessions - 1):
+        assert bytes(eng.trunk(s)) == bytes(r["trunk_states"][s])
+
+
 def run_rounds(oracle, eng, truth, rounds, lanes_to_check):
     S, P, W = eng.num_sessions, eng.num_players, eng.window
     trunks = {s: oracle.state_new(P) for s in set(l // eng.branches for l in lanes_to_check) | {0}}
@@ -136,8 +147,8 @@ def test_report_to_device_buffer(oracle):
 def test_full_size_config4(oracle):
     """Config 4 at full per-GPU size: 8192 four-player sessions x 16 branches = 131,072 lanes,
     window 8.  Single rounds checked lane by lane against the oracle's adjust_gamestate replay on
-    sampled lanes, every sampled session's trunk and report; then the fused rounds launch (the bench
-    path) leaves every session's trunk checksum and survival word equal to the single rounds'."""
+    sampled lanes each round; then EVERY lane of the single-round engine and of the fused rounds
+    launch (the bench path) against the oracle (check_every_lane)."""
     from ggrs_amd import BranchEngine, synth
     S, B, P, mask, W, rounds = 8192, 16, 4, 0b1110, 8, 3
     truth = synth.gen_inputs(5, S, 2 * rounds + W + 2, P, synth.MODEL_HELD)
@@ -147,18 +158,12 @@ def test_full_size_config4(oracle):
     rng = np.random.default_rng(4)
     lanes = sorted(set([0, 1, 15, 16, L // 2, L - 17, L - 1] + rng.integers(0, L, 9).tolist()))
     run_rounds(oracle, eng, truth, rounds, lanes)
+    check_every_lane(oracle, eng, truth)
     fused = BranchEngine(S, num_players=P, remote_mask=mask, window=W, branches=B, alphabet=16)
     fused.add_inputs(0, truth)
     fused.rounds(rounds)
     fused.synchronize()
-    a, b = fused.report(), eng.report()
-    assert (a[0] == b[0]).all() and (a[1] == b[1]).all()
-    for s in (0, S // 3, S - 1):
-        st = oracle.state_new(P)
-        for f in range(rounds):
-            st = oracle.state_advance(st, truth[f, s])
-        assert bytes(fused.trunk(s)) == bytes(st)
-        assert int(a[0][s]) == oracle.fletcher16(bytes(st))
+    check_every_lane(oracle, fused, truth)
 
 
 @pytest.mark.parametrize("S,B,A,P,mask,W", [(1, 16 ** 4, 16, 2, 0b10, 4), (200, 16, 16, 2, 0b01, 6),
@@ -243,8 +248,9 @@ def test_prefix_pipe_ramp_forms(splits):
 
 
 def test_config3_fused_rounds_full_size(oracle):
-    """Config 3 through the bench's path (fused prefix-shared rounds): 16 rounds, then sampled
-    lanes of the last window against the oracle's replay, the trunk and the survivor count."""
+    """Config 3 through the bench's path (fused prefix-shared rounds): 16 rounds, then EVERY one of
+    the 65,536 lanes' last window (4 cells each, depth-4 cells included) against the oracle's
+    replay, the trunk, the report and the 16^3 survivors."""
     from ggrs_amd import BranchEngine, synth
     eng = BranchEngine(1, num_players=2, remote_mask=0b10, window=4, branches=16 ** 4, alphabet=16)
     n = 16
@@ -252,21 +258,8 @@ def test_config3_fused_rounds_full_size(oracle):
     eng.add_inputs(0, truth)
     eng.rounds(n)
     eng.synchronize()
-    st = oracle.state_new(2)
-    for fr in range(n - 1):
-        st = oracle.state_advance(st, truth[fr, 0])
-    rng = np.random.default_rng(9)
-    for lane in sorted(set([0, 15, 16, 255, 256, 4095, 4096, 65535] + rng.integers(0, 65536, 8).tolist())):
-        states, cks, _ = oracle.p2p_replay(st, n - 1, branch_inputs(eng, truth, n - 1, lane, 4))
-        for k in range(4):
-            ck, got = eng.lane_state(lane, n + k)
-            assert ck == int(cks[k]) and bytes(got) == bytes(states[k]), (lane, k)
-    st = oracle.state_advance(st, truth[n - 1, 0])
-    assert bytes(eng.trunk(0)) == bytes(st)
-    ck, _ = eng.report()
-    assert int(ck[0]) == oracle.fletcher16(bytes(st))
+    check_every_lane(oracle, eng, truth)
     assert eng.survivors().sum() == 16 ** 3
-    assert (eng.desync() == -1).all()
 
 
 def test_prefix_rounds_chunked_launches_and_reports(oracle):

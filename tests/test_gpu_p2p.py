@@ -210,6 +210,10 @@ def test_full_size_p2p_bench_config(oracle):
     check_against_oracle(eng, rows, sessions, frames, trace=False)
     rb, _ = eng.stats()
     assert rb.sum() > S  # rollbacks happen throughout
+    # EVERY session's final state and rollback count (oracle_p2p_batch)
+    from oracle import every_lane
+    r = every_lane.p2p(eng, rows, P=P, maxp=8, latency=4)
+    assert r["rc_mismatched"] == r["final_state_mismatched"] == r["rollbacks_mismatched"] == 0, r
 
 
 @pytest.mark.parametrize("form", ["default", "flat", "chains"])
@@ -233,6 +237,9 @@ def test_config2_p2p_shape(oracle, form):
     check_against_oracle(eng, rows, sessions, frames, trace=False)
     rb, rs = eng.stats()
     assert rb.sum() > 0 and rs.sum() >= 8 * rb.sum() - 8 * S  # rollbacks of up to 8 frames
+    from oracle import every_lane
+    r = every_lane.p2p(eng, rows, P=P, maxp=9, latency=8)  # every session
+    assert r["rc_mismatched"] == r["final_state_mismatched"] == r["rollbacks_mismatched"] == 0, r
 
 
 @pytest.mark.parametrize("P,local,delay,mp,D,pred,model", CASES)

@@ -230,3 +230,28 @@ def test_p2p_synth_schedules_every_session(oracle, monkeypatch, stalls, delay, l
     frames, skipped, errors = eng.sessions()
     assert (errors == 0).all()
     assert (skipped.sum() > 0) == stalls
+
+
+@pytest.mark.parametrize("form", FORMS)
+@pytest.mark.parametrize("stalls", [False, True])
+def test_p2p_bench_schedule_full_size_every_session(oracle, monkeypatch, form, stalls):
+    """The bench's any-network configuration at full size (`bench.py --workload p2p --arrivals
+    jitter|stall --sessions 4096 --max-prediction 9`: 4096 sessions, 64-call launches): EVERY
+    session's final state, rollback count, current frame and skipped calls against the oracle's
+    P2PSession under the same schedule (oracle_p2p_batch)."""
+    from ggrs_amd import P2PEngine, synth
+    from oracle import every_lane
+    set_form(monkeypatch, form)
+    S, calls, P, mp = 4096, 6 * 64, 2, 9
+    rows = synth.gen_inputs(0, S, calls, P, synth.MODEL_HELD)
+    arrive = synth.jitter_arrivals(0, S, calls, mp, stalls=stalls)
+    eng = P2PEngine(S, num_players=P, local_players=(0,), max_prediction=mp, remote_latency=1, input_capacity=calls)
+    eng.set_arrival_schedule(True)
+    eng.add_inputs(0, rows)
+    eng.add_arrivals(0, arrive)
+    for _ in range(calls // 64):
+        eng.advance_frames(64)
+    r = every_lane.p2p(eng, rows, arrive, P=P, maxp=mp)
+    assert r["rc_mismatched"] == r["final_state_mismatched"] == r["rollbacks_mismatched"] == 0, r
+    assert r["frame_skips_mismatched"] == 0, r
+    check_sessions(eng, rows, arrive, np.zeros((calls, S), np.uint8), (0, 1, S // 2, S - 1), calls)

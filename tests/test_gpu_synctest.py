@@ -196,15 +196,29 @@ def test_mismatch_restore_when_grid_exceeds_residency(oracle, lanes, bad_lane, c
 @pytest.mark.parametrize("path", PATHS_CD8)
 def test_full_size_config2(oracle, path):
     """Config 2 at full size: 4096 sessions, 8-frame rollback every frame (SyncTest cd 8,
-    max_prediction 9), held-key inputs; sampled lanes bit-exact."""
+    max_prediction 9), held-key inputs.  EVERY lane bit-exact against the oracle's SyncTestSession
+    (oracle_synctest_batch): the display checksum after every frame, the final state and the
+    saved-state ring's frames and checksums; sampled lanes' ring state bytes too."""
     from ggrs_amd import synth
     P, maxp, cd, d, F, lanes = 2, 9, 8, 0, 400, 4096
     inputs = synth.gen_inputs(0, lanes, F, P, synth.MODEL_HELD)
     eng = make_engine(lanes, P, maxp, cd, d, F, path=path)
     run_chunks(eng, inputs, [F])
+    ref = oracle.synctest_batch(inputs, P, maxp, cd, d)
+    assert (ref["status"] == 0).all()
     tr = eng.trace(0, F)
-    rng = np.random.default_rng(0)
-    for lane in sorted(set([0, 1, 6, 7, 2047, 4095] + rng.integers(0, lanes, 12).tolist())):
+    bad = np.nonzero((tr != ref["cksum"]).any(axis=0))[0]
+    assert bad.size == 0, f"{bad.size} lanes' traces differ, first {bad[:8].tolist()}"
+    states = eng.states()
+    bad = np.nonzero((states != ref["final_states"]).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} lanes' final states differ, first {bad[:8].tolist()}"
+    ring_frames = ref["ring_frames"][0]
+    assert (ref["ring_frames"] == ring_frames).all()  # SyncTest lanes step in lockstep
+    held = [(slot, int(f)) for slot, f in enumerate(ring_frames) if f >= 0]
+    cks = eng.save_checksums_frames([f for _, f in held])
+    for i, (slot, f) in enumerate(held):
+        assert (cks[i] == ref["ring_cksums"][:, slot]).all(), f"ring checksum of frame {f}"
+    for lane in (0, 4095):
         check_lane(oracle, eng, inputs, lane, P, maxp, cd, d, F, tr)
     st, _, _ = eng.mismatches()
     assert (st == 0).all()
