@@ -56,7 +56,7 @@ EXPORTS = (
     "ggrs_p2p_read_trace", "ggrs_p2p_timing_reset", "ggrs_p2p_timing_stop", "ggrs_p2p_timing_read",
     "ggrs_p2p_set_desync_detection", "ggrs_p2p_local_checksums", "ggrs_p2p_compare_checksums",
     "ggrs_p2p_debug_desync", "ggrs_p2p_set_sparse_saving", "ggrs_p2p_set_unstaged",
-    "ggrs_p2p_set_arrival_schedule", "ggrs_p2p_add_arrivals", "ggrs_p2p_read_sessions", "ggrs_p2p_read_reports", "ggrs_p2p_read_states",
+    "ggrs_p2p_set_arrival_schedule", "ggrs_p2p_add_arrivals", "ggrs_p2p_read_sessions", "ggrs_p2p_read_reports", "ggrs_p2p_read_states", "ggrs_p2p_add_peer_reports",
     "ggrs_codec_encode", "ggrs_codec_decode", "ggrs_codec_encode_chunked", "ggrs_codec_decode_chunked", "ggrs_codec_max_packet_bytes", "ggrs_codec_set_direct",
 )
 

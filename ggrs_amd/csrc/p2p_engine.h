@@ -50,6 +50,7 @@ struct ggrs_p2p_engine {
   int32_t next_arrival_call = 0;
   int32_t* arrive = nullptr;      // [cap][S] newest remote frame delivered by call c, row c % cap
   uint8_t* events = nullptr;      // [cap][S] Event::Disconnected bits of call c
+  int32_t* peer_reports = nullptr;  // [cap][S] the peers' disconnect reports of call c (ggrs_p2p_add_peer_reports)
   int32_t* row_tag = nullptr;     // [cap] the frame whose input row each row slot holds
   std::vector<int32_t> row_tag_host;
   uint32_t* iq = nullptr;         // [kSchedQueue][S] every player's queued input of frame q, q % kSchedQueue

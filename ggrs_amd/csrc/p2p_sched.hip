@@ -50,9 +50,13 @@ constexpr int32_t kNull = GGRS_NULL_FRAME;
 constexpr int kQ = 128;  // INPUT_QUEUE_LENGTH (input_queue.rs:6)
 constexpr int kBlock = 64;
 
-enum : int { kCur = 0, kLconf, kDframe, kLastSaved, kDelivered, kLocalLast, kSkips, kErr, kDisc, kLastSent, kPl0 };
+enum : int { kCur = 0, kLconf, kDframe, kLastSaved, kDelivered, kLocalLast, kSkips, kErr, kDisc, kLastSent, kRmask, kPl0 };
 constexpr int kPlFields = 1;  // per player: last_frame (local_connect_status; remote players)
-__host__ __device__ constexpr int sched_fields(int P) { return kPl0 + kPlFields * P; }
+// then the peers' disconnect reports: [reporter r][player k] the last frame r's endpoint reports
+// (valid where bit 4r + k of kRmask is set)
+__host__ __device__ constexpr int sched_rep0(int P) { return kPl0 + kPlFields * P; }
+__host__ __device__ constexpr int sched_fields(int P) { return sched_rep0(P) + P * P; }
+constexpr uint32_t kEvPeerReport = 0x10u;  // an events byte's flag: the call carries a peer report
 __host__ __device__ constexpr int cell_dwords_s(int p) { return (state_fields(p) + 1 + 3) & ~3; }
 
 struct SchedParams {
@@ -68,6 +72,7 @@ struct SchedParams {
   const int32_t* row_tag;
   const int32_t* arrive;
   const uint8_t* events;
+  const int32_t* reports;  // [cap][S] peers' disconnect reports (GGRS_PEER_REPORT), NULL when none were added
   uint32_t* lq;  // [WL][S] the local players' queued inputs by frame (slot frame % WL)
   int32_t* sst;
   int32_t* rollbacks;
@@ -136,6 +141,7 @@ struct SchedCtl {
   int32_t cur, lconf, dframe, last_saved, delivered, local_last, skips, err;
   int32_t last_sent;  // last_sent_checksum_frame (desync detection, p2p_session.rs:939-975)
   uint32_t disc;
+  uint32_t rmask;  // the peers' standing disconnect reports (bit 4 r + k: r's endpoint reports k)
   int32_t lf[P];  // the remote players' last frames (local_connect_status[k].last_frame): the newest
                   // delivered frame for a connected player, frozen at its disconnect
   int32_t slot_f;  // ring slot of the current frame
@@ -155,6 +161,8 @@ struct SchedCtlEnv {
   int ns, col;  // sessions per LDS row and this session's column
   const uint8_t* inputs;
   const int32_t* row_tag;
+  const int32_t* reports;  // the peers' reports ([cap][S]) and the session's table of them (sst)
+  int32_t* rtab;
 };
 
 // The control pass's fast form of call c (see sched_control_call): every player connected, no
@@ -181,7 +189,8 @@ __device__ __forceinline__ bool sched_fast_call(SchedCtl<P>& q, const SchedCtlEn
   // reference panics: the general form stops the session)
   const int32_t fts = q.last_sent == kNull ? x.interval : q.last_sent + x.interval;
   const bool send = x.interval > 0 && fts <= q.lconf && fts <= q.last_saved;
-  const bool fast = en & (a <= c) & (q.disc == 0u) & (e_c == 0u) & (q.dframe == kNull) & (q.cur >= 1) & (q.cur >= lo) &
+  const bool fast = en & (maxp > 0) & (a <= c) & (q.disc == 0u) & (q.rmask == 0u) & (e_c == 0u) & (q.dframe == kNull) &
+                    (q.cur >= 1) & (q.cur >= lo) &
                     (q.delivered >= (kPred == 0 ? lo : lo - 1)) & (lbytes == 0u || q.local_last != kNull) &
                     (up - q.delivered < kArrTooFar) & (up < q.cur - maxp + kQ - 1) & (mis == kNull || mis >= q.cur - maxp) &
                     (!send || fts >= q.last_saved - maxp);
@@ -316,8 +325,41 @@ __device__ __forceinline__ uint2 sched_control_call(SchedCtl<P>& q, const SchedC
         cb &= ~(0xffu << (8 * k));
         if (q.cur > q.lf[k]) q.dframe = q.lf[k] + 1;
       }
+      // update_player_disconnects (p2p_session.rs:748-783) over the peers' reports (the call's new
+      // one joins the session's table): for each player k, the endpoints still running that report k
+      // disconnected bound queue_min_confirmed (the others are taken to have seen every reported
+      // frame), with the local last frame while k is connected here; then disconnect_player_at_frame
+      // (:618-655) while k is connected here or its local last frame is newer -- on every call that
+      // holds, as the reference (local_connect_status[k].last_frame stays)
+      uint32_t rdisc = 0;
+      if (e_c & kEvPeerReport) {
+        const int32_t v = x.reports[(int64_t)(c % x.cap) * x.S + x.s];
+        const int k = v & 3, r = (v >> 2) & 3;
+        x.rtab[(int64_t)(r * P + k) * x.S + x.s] = (v >> 5) - 1;
+        q.rmask |= 1u << (4 * r + k);
+      }
+      if (q.rmask) {
+        for (int k = 0; k < P; k++) {
+          bool reported = false;
+          int32_t qmin = INT32_MAX;
+          for (int r = 0; r < P; r++) {
+            if (!((q.rmask >> (4 * r + k)) & 1u) || ((q.disc >> r) & 1u)) continue;  // (!endpoint.is_running())
+            reported = true;
+            qmin = min(qmin, x.rtab[(int64_t)(r * P + k) * x.S + x.s]);
+          }
+          if (!reported) continue;
+          const bool here = !((q.disc >> k) & 1u);
+          if (here) qmin = min(qmin, q.lf[k]);
+          if (here || q.lf[k] > qmin) {
+            rdisc |= here ? 1u << k : 0u;
+            q.disc |= 1u << k;
+            cb &= ~(0xffu << (8 * k));
+            if (q.cur > qmin) q.dframe = qmin + 1;
+          }
+        }
+      }
       if (kPred == 0 && q.delivered != kNull) bad |= !row_ok(q.delivered);  // the prediction's row
-      rec = (uint32_t)code << 16 | ev << 24;
+      rec = (uint32_t)code << 16 | (ev | rdisc) << 24;
       // check_checksum_send_interval (p2p_session.rs:939-975): after the poll, before the rollback
       const int32_t fts = q.last_sent == kNull ? x.interval : q.last_sent + x.interval;
       if (!bad && x.interval > 0 && fts <= q.lconf && fts <= q.last_saved) {
@@ -331,8 +373,9 @@ __device__ __forceinline__ uint2 sched_control_call(SchedCtl<P>& q, const SchedC
       if (bad) {
         q.err = GGRS_E_PRECONDITION;  // a remote input no longer in the input rows
       } else {
-        // 2. the first frame's save (:305-308)
-        if (q.cur == 0) {
+        // 2. the first frame's save (:305-308; lockstep mode, max_prediction 0, never saves)
+        const bool lockstep = maxp == 0;
+        if (q.cur == 0 && !lockstep) {
           q.last_saved = 0;
           if (kSparse) tag(q.slot_f) = 0;
         }
@@ -349,11 +392,19 @@ __device__ __forceinline__ uint2 sched_control_call(SchedCtl<P>& q, const SchedC
         } else {
           // 3. check_simulation_consistency(disconnect_frame) (sync_layer.rs:343-353) +
           //    adjust_gamestate (p2p_session.rs:658-714)
-          int32_t first_inc = q.dframe;
-          if (mis != kNull && (first_inc == kNull || mis < first_inc)) first_inc = mis;
+          //    (not in lockstep mode: no rollback)
+          int32_t first_inc = lockstep ? kNull : q.dframe;
+          if (!lockstep && mis != kNull && (first_inc == kNull || mis < first_inc)) first_inc = mis;
           if (first_inc != kNull) {
             const int32_t from = kSparse ? q.last_saved : first_inc;
-            if (!replay_ok(from) || !rows_ok(from, min(q.cur - 1, q.delivered))) {
+            // the replay reads every read player's InputQueue from `from`, which the last
+            // set_last_confirmed_frame trimmed to last_confirmed - 1 (input_queue.rs:83-101): older is
+            // the reference's "requested frame no longer exists" panic (:104-110) -- a peer's report
+            // of an old frame; a misprediction or a local disconnect is never behind it
+            // (sparse saving: adjust_gamestate's assert!(frame_to_load <= first_incorrect), :675 --
+            // again a report's rollback behind the last save)
+            if (!replay_ok(from) || (kSparse && from > first_inc) || (q.lconf > 0 && from < q.lconf - 1) ||
+                !rows_ok(from, min(q.cur - 1, q.delivered))) {
               q.err = GGRS_E_PRECONDITION;
             } else {
               const int32_t d = q.cur - from;
@@ -373,7 +424,7 @@ __device__ __forceinline__ uint2 sched_control_call(SchedCtl<P>& q, const SchedC
               }
             }
           }
-          bool save_own = !kSparse;
+          bool save_own = !kSparse && !lockstep;
           // sparse saving: check_last_saved_state (:819-843) once the rollback's replay is done
           if (!q.err && kSparse && q.cur - q.last_saved >= maxp) {
             if (confirmed >= q.cur) {
@@ -408,9 +459,10 @@ __device__ __forceinline__ uint2 sched_control_call(SchedCtl<P>& q, const SchedC
               const int32_t qf = q.cur + x.delay;
               if (q.local_last == kNull || qf == q.local_last + 1) ll = qf;
             }
-            // the prediction threshold (:393-423)
+            // the prediction threshold (:393-423); lockstep mode: advance only at last_confirmed ==
+            // current (:393-397)
             const int32_t ahead = lc == kNull ? q.cur : q.cur - lc;
-            const bool adv = ahead < maxp;
+            const bool adv = lockstep ? lc == q.cur : ahead < maxp;
             if ((lbytes && !row_ok(c)) || (adv && q.cur <= q.delivered && !row_ok(q.cur))) {
               q.err = GGRS_E_PRECONDITION;
             } else {
@@ -488,6 +540,7 @@ __device__ inline void sched_store_ctl(const SchedParams& p, const SchedCtl<P>& 
   fld(kErr) = q.err;
   fld(kDisc) = (int32_t)q.disc;
   fld(kLastSent) = q.last_sent;
+  fld(kRmask) = (int32_t)q.rmask;
 #pragma unroll
   for (int k = 0; k < P; k++) fld(kPl0 + kPlFields * k + 0) = q.lf[k];
   p.rollbacks[s] += q.rollbacks;
@@ -580,6 +633,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
   q.err = fld(kErr);
   q.disc = (uint32_t)fld(kDisc);
   q.last_sent = fld(kLastSent);
+  q.rmask = (uint32_t)fld(kRmask);
 #pragma unroll
   for (int k = 0; k < P; k++) q.lf[k] = fld(kPl0 + kPlFields * k + 0);
   if (!live) q.err = 1;  // idle lanes run no call
@@ -715,6 +769,8 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
       env.inputs = p.inputs;
       env.row_tag = p.row_tag;
       env.interval = p.interval;
+      env.reports = p.reports;
+      env.rtab = p.sst + (int64_t)sched_rep0(P) * S;
       const int32_t ci0 = cs % p.cap;
       for (int32_t cb8 = cs; cb8 < ce; cb8 += 8) {
         int32_t up8[8];
@@ -725,6 +781,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
           const bool in = !q.err && cb8 + j < ce;
           up8[j] = in ? p.arrive[(int64_t)ci * S + s] : kNull;
           ev8[j] = (in && p.events) ? p.events[(int64_t)ci * S + s] : 0u;
+          if (in && p.reports && p.reports[(int64_t)ci * S + s] != 0) ev8[j] |= kEvPeerReport;
         }
         for (int j = 0; j < 8; j++) {
           const int32_t c = cb8 + j;
@@ -1079,6 +1136,7 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
     q.err = fld(kErr);
     q.disc = (uint32_t)fld(kDisc);
     q.last_sent = fld(kLastSent);
+    q.rmask = (uint32_t)fld(kRmask);
 #pragma unroll
     for (int k = 0; k < P; k++) q.lf[k] = fld(kPl0 + kPlFields * k + 0);
     if (!live) q.err = 1;  // idle lanes run no call
@@ -1260,6 +1318,8 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
         env.inputs = p.inputs;
         env.row_tag = p.row_tag;
         env.interval = p.interval;
+        env.reports = nullptr;  // (this form runs only without peer reports: the host's choice)
+        env.rtab = p.sst + (int64_t)sched_rep0(P) * S;
         for (int32_t cb8 = cs; cb8 < ce; cb8 += 8) {
           // eight calls' arrivals, events and input rows (the local players' input each call queues),
           // all read before the first is used
@@ -1536,7 +1596,7 @@ __global__ void sched_init_kernel(int32_t* sst, int64_t S, int32_t P) {
   if (i >= (int64_t)sched_fields(P) * S) return;
   const int f = (int)(i / S);
   int32_t v = kNull;
-  if (f == kCur || f == kSkips || f == kErr || f == kDisc) v = 0;  // (kLastSent: NULL_FRAME)
+  if (f == kCur || f == kSkips || f == kErr || f == kDisc || f == kRmask) v = 0;  // (kLastSent: NULL_FRAME)
   sst[i] = v;
 }
 
@@ -1545,7 +1605,8 @@ __global__ void sched_init_kernel(int32_t* sst, int64_t S, int32_t P) {
 namespace ggrs {
 
 int p2p_sched_free(ggrs_p2p_engine* e) {
-  void* bufs[] = {e->arrive, e->events, e->row_tag, e->iq, e->sst, e->rep_frame, e->rep_ck, e->rep_lconf, e->rep_ll, e->fck};
+  void* bufs[] = {e->arrive, e->events, e->row_tag, e->iq, e->sst, e->rep_frame, e->rep_ck, e->rep_lconf, e->rep_ll, e->fck,
+                  e->peer_reports};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   e->arrive = nullptr;
@@ -1558,6 +1619,7 @@ int p2p_sched_free(ggrs_p2p_engine* e) {
   e->rep_lconf = nullptr;
   e->rep_ll = nullptr;
   e->fck = nullptr;
+  e->peer_reports = nullptr;
   return GGRS_OK;
 }
 
@@ -1665,6 +1727,7 @@ int p2p_sched_advance(ggrs_p2p_engine* e, int32_t n) {
   p.row_tag = e->row_tag;
   p.arrive = e->arrive;
   p.events = e->events;
+  p.reports = e->peer_reports;
   p.lq = e->iq;
   p.sst = e->sst;
   p.rollbacks = e->rollbacks;
@@ -1685,7 +1748,9 @@ int p2p_sched_advance(ggrs_p2p_engine* e, int32_t n) {
   for (int k = 0; k < P; k++) remote += !((e->cfg.local_mask >> k) & 1);
   const char* chains_env = getenv("GGRS_SCHED_CHAINS");
   const int64_t cblocks = grid_of(e->cfg.num_sessions, kCS);
-  const bool chains = !e->sparse && e->cfg.max_prediction <= kMaxChainDepth && remote <= 2 && !(chains_env && chains_env[0] == '0') &&
+  // (lockstep mode and peer reports take the one-thread-per-session form)
+  const bool chains = !e->sparse && e->cfg.max_prediction >= 1 && e->cfg.max_prediction <= kMaxChainDepth && remote <= 2 &&
+                      !e->peer_reports && !(chains_env && chains_env[0] == '0') &&
                       (cblocks <= 2 * (int64_t)e->num_cus || (chains_env && chains_env[0] == '1'));
   if (chains && n > kChainMaxCalls) {
     int rc = p2p_sched_advance(e, kChainMaxCalls);
@@ -1775,8 +1840,6 @@ int ggrs_p2p_set_arrival_schedule(ggrs_p2p_engine_t* e, int32_t on) {
     e->sched = 0;
     return GGRS_OK;
   }
-  if (e->cfg.max_prediction < 1)
-    return set_error(GGRS_E_INVALID, "scheduled arrivals need rollback mode (max_prediction >= 1)");
   if (e->cfg.max_prediction + e->cfg.input_delay + 2 >= kQ)
     return set_error(GGRS_E_INVALID, "max_prediction + input_delay must be < %d (the device input queue)", kQ - 2);
   if (e->trace) return set_error(GGRS_E_STATE, "scheduled arrivals do not support the display-checksum trace");
@@ -1808,10 +1871,52 @@ int ggrs_p2p_add_arrivals(ggrs_p2p_engine_t* e, int32_t first_call, int32_t n, c
                              hipMemcpyHostToDevice, e->stream));
     else
       HIP_TRY(hipMemsetAsync(e->events + (int64_t)slot * S, 0, (size_t)m * S, e->stream));
+    if (e->peer_reports)  // (a slot's report from cap calls ago is not this call's)
+      HIP_TRY(hipMemsetAsync(e->peer_reports + (int64_t)slot * S, 0, sizeof(int32_t) * m * S, e->stream));
     k += m;
   }
   HIP_TRY(hipStreamSynchronize(e->stream));
   e->next_arrival_call = first_call + n;
+  return GGRS_OK;
+}
+
+int ggrs_p2p_add_peer_reports(ggrs_p2p_engine_t* e, int32_t first_call, int32_t n, const int32_t* reports) {
+  if (!e || (!reports && n > 0)) return set_error(GGRS_E_INVALID, "null argument");
+  if (!e->sched) return set_error(GGRS_E_STATE, "peer reports need ggrs_p2p_set_arrival_schedule(e, 1)");
+  if (n < 0 || first_call < e->current_frame || first_call + n > e->next_arrival_call)
+    return set_error(GGRS_E_INVALID, "peer reports are for calls not yet run whose arrivals were added (calls %d .. %d)",
+                     e->current_frame, e->next_arrival_call - 1);
+  if (e->cfg.predictor != 0)
+    return set_error(GGRS_E_INVALID, "peer reports need the repeat-last predictor (a disconnected player's trimmed "
+                                     "queue answers with its prediction, input_queue.rs:104-167)");
+  const int P = e->cfg.num_players;
+  const int64_t S = e->cfg.num_sessions;
+  const uint32_t lm = (uint32_t)e->cfg.local_mask;
+  for (int32_t c = 0; c < n; c++)
+    for (int64_t s = 0; s < S; s++) {
+      const int32_t v = reports[(int64_t)c * S + s];
+      if (v == 0) continue;
+      const int k = v & 3, r = (v >> 2) & 3;
+      const int32_t f = (v >> 5) - 1;
+      if (!(v & 16) || k >= P || r >= P || k == r || ((lm >> k) & 1u) || ((lm >> r) & 1u) || f < kNull ||
+          f > first_call + c)
+        return set_error(GGRS_E_INVALID, "bad peer report %d (call %d, session %lld): GGRS_PEER_REPORT(player, "
+                         "reporter, frame) of two remote players, frame <= the call", v, first_call + c, (long long)s);
+    }
+  if (n == 0) return GGRS_OK;
+  HIP_TRY(hipSetDevice(e->cfg.device));
+  if (!e->peer_reports) {
+    HIP_TRY(hipMalloc(&e->peer_reports, sizeof(int32_t) * (size_t)e->cap * S));
+    HIP_TRY(hipMemsetAsync(e->peer_reports, 0, sizeof(int32_t) * (size_t)e->cap * S, e->stream));
+  }
+  for (int32_t k = 0; k < n;) {  // rows wrap at cap: at most two pieces
+    const int32_t slot = (first_call + k) % e->cap;
+    const int32_t m = std::min(n - k, e->cap - slot);
+    HIP_TRY(hipMemcpyAsync(e->peer_reports + (int64_t)slot * S, reports + (int64_t)k * S, sizeof(int32_t) * m * S,
+                           hipMemcpyHostToDevice, e->stream));
+    k += m;
+  }
+  HIP_TRY(hipStreamSynchronize(e->stream));
   return GGRS_OK;
 }
 

@@ -67,12 +67,19 @@ def _bind(L):
     L.ggrs_p2p_set_unstaged.argtypes = [vp, i32]
     L.ggrs_p2p_set_arrival_schedule.argtypes = [vp, i32]
     L.ggrs_p2p_add_arrivals.argtypes = [vp, i32, i32, vp, vp]
+    L.ggrs_p2p_add_peer_reports.argtypes = [vp, i32, i32, vp]
     L.ggrs_p2p_read_sessions.argtypes = [vp, vp, vp, vp]
     L.ggrs_p2p_read_reports.argtypes = [vp, i32, i32, vp, vp, vp, vp]
     for name in _lib.EXPORTS:
         if name.startswith("ggrs_p2p_"):
             getattr(L, name).restype = ctypes.c_int
     _bound = True
+
+
+def peer_report(player, reporter, frame):
+    """GGRS_PEER_REPORT: remote player `reporter`'s endpoint reports remote player `player`
+    disconnected with last frame `frame`."""
+    return 16 | player | reporter << 2 | (frame + 1) << 5
 
 
 def _vp(a):
@@ -248,6 +255,15 @@ class P2PEngine:
             if ev.shape != a.shape:
                 raise InvalidRequest(-1, "events must have arrive_upto's shape")
         _lib.check(self._L.ggrs_p2p_add_arrivals(self._h, first_call, a.shape[0], _vp(a), _vp(ev)))
+
+    def add_peer_reports(self, first_call, reports):
+        """reports [n][S] int32 (peer_report(player, reporter, frame) or 0): the peers' disconnect
+        reports received by calls first_call .. first_call + n - 1 (after their add_arrivals); each
+        stands until its reporter disconnects (update_player_disconnects, p2p_session.rs:748-783)."""
+        r = np.ascontiguousarray(reports, np.int32)
+        if r.ndim != 2 or r.shape[1] != self.num_sessions:
+            raise InvalidRequest(-1, f"reports must be [n][{self.num_sessions}]")
+        _lib.check(self._L.ggrs_p2p_add_peer_reports(self._h, first_call, r.shape[0], _vp(r)))
 
     def sessions(self):
         """(frames, skipped, errors) [S] int32 each: every session's current frame, its calls that

@@ -55,7 +55,8 @@ extern "C" {
  * 4: P2P arrival schedules (ggrs_p2p_set_arrival_schedule, ggrs_p2p_add_arrivals,
  * ggrs_p2p_read_sessions)
  * 5: desync detection under arrival schedules (ggrs_p2p_read_reports)
- * 6: bulk reads for every-lane checks (ggrs_read_states, ggrs_p2p_read_states, ggrs_branch_read_cells) */
+ * 6: bulk reads for every-lane checks (ggrs_read_states, ggrs_p2p_read_states, ggrs_branch_read_cells);
+ * lockstep mode under arrival schedules, peers' disconnect reports (ggrs_p2p_add_peer_reports) */
 #define GGRS_ABI_VERSION 6
 
 #define GGRS_OK 0
@@ -549,12 +550,14 @@ int ggrs_p2p_debug_desync(ggrs_p2p_engine_t* eng, int32_t session, int32_t frame
  * with input row c's byte, for the session's current frame (a call that did not advance repeats its
  * frame, and InputQueue::add_input drops the repeat, input_queue.rs:170-186); (4) advance_frame.
  * Input row g (ggrs_p2p_add_inputs) = the local players' input of call g and the remote players'
- * input of frame g, as in the fixed-latency model.  Rollback mode only (max_prediction >= 1),
- * sparse saving allowed, no trace; desync detection (ggrs_p2p_set_desync_detection, without sparse
+ * input of frame g, as in the fixed-latency model.  max_prediction 0 is lockstep mode (no saves,
+ * no rollbacks, a call advances only when last_confirmed_frame == current_frame, :301-304,
+ * 393-397); sparse saving allowed in rollback mode, no trace; peers' disconnect reports
+ * (ggrs_p2p_add_peer_reports) after (2); desync detection (ggrs_p2p_set_desync_detection, without sparse
  * saving) per session: ggrs_p2p_read_reports; remote_latency is ignored.  A session whose
  * call would make the reference panic (a remote input no longer in the input rows or more than
- * 126 - max_prediction frames ahead of the session, a rollback to a frame that is not in the past,
- * no connected player) or whose arrival row names a frame after its call (GGRS_E_INVALID) stops
+ * 126 - max_prediction frames ahead of the session, a rollback to a frame that is not in the past
+ * or older than the input queues hold, no connected player) or whose arrival row names a frame after its call (GGRS_E_INVALID) stops
  * there with that error (ggrs_p2p_read_sessions); the other sessions run on.  Kernel:
  * p2p_sched.hip. */
 /* on = 1 switches the engine to arrival schedules; part of the configuration: before the first call */
@@ -564,6 +567,19 @@ int ggrs_p2p_set_arrival_schedule(ggrs_p2p_engine_t* eng, int32_t on);
  * u8 (NULL: none).  Calls in order from 0, at most input_capacity calls ahead of the next call. */
 int ggrs_p2p_add_arrivals(ggrs_p2p_engine_t* eng, int32_t first_call, int32_t n_calls, const int32_t* arrive_upto,
                           const uint8_t* events);
+/* A peer's connect status as its input messages carry it (peer_connect_status): remote player
+ * `reporter`'s endpoint reports remote player `player` disconnected with last frame `frame`
+ * (-1 <= frame <= the call).  0 = no report. */
+#define GGRS_PEER_REPORT(player, reporter, frame) (16 | (player) | (reporter) << 2 | ((frame) + 1) << 5)
+/* reports [n_calls][num_sessions] i32 (GGRS_PEER_REPORT or 0) received by calls first_call ..
+ * first_call + n_calls - 1, after their arrivals (ggrs_p2p_add_arrivals; calls not yet run).  A
+ * report stands until its reporter disconnects; each call runs update_player_disconnects
+ * (p2p_session.rs:748-783) over the standing ones: player k is disconnected at queue_min_confirmed
+ * -- the oldest frame a running reporter gives, and k's own last frame while it is connected here
+ * (endpoints that do not report k are taken to have seen every reported frame) -- when it is
+ * connected here or its last frame is newer (the rollback then repeats every call, as the
+ * reference's).  The repeat-last predictor only. */
+int ggrs_p2p_add_peer_reports(ggrs_p2p_engine_t* eng, int32_t first_call, int32_t n_calls, const int32_t* reports);
 /* per session: SyncLayer::current_frame, the calls that did not advance (prediction threshold),
  * and the session's error (0, GGRS_E_PRECONDITION or GGRS_E_INVALID); any pointer may be NULL */
 int ggrs_p2p_read_sessions(ggrs_p2p_engine_t* eng, int32_t* frames, int32_t* skipped, int32_t* errors);

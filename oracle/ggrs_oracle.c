@@ -32,6 +32,7 @@
  */
 #include <math.h>
 #include <pthread.h>
+#include <setjmp.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -209,9 +210,16 @@ typedef struct {
   int predictor;
 } InputQueue;
 
+/* A restated assert! is the reference's panic.  Inside a scheduled session's call (where the run
+ * reports the panic as rc -4) it unwinds to the call; elsewhere it aborts. */
+static __thread jmp_buf* oracle_panic_jmp;
 #define ORACLE_ASSERT(c, msg)                                                              \
   do {                                                                                     \
-    if (!(c)) { fprintf(stderr, "oracle panic (%s:%d): %s\n", __FILE__, __LINE__, msg); abort(); } \
+    if (!(c)) {                                                                            \
+      if (oracle_panic_jmp) longjmp(*oracle_panic_jmp, 1);                                 \
+      fprintf(stderr, "oracle panic (%s:%d): %s\n", __FILE__, __LINE__, msg);              \
+      abort();                                                                             \
+    }                                                                                      \
   } while (0)
 
 static void iq_new(InputQueue* q, int predictor) { /* :40-53 */
@@ -1107,6 +1115,11 @@ typedef struct {
   int32_t last_frame[MAX_PLAYERS]; /* local_connect_status[i].last_frame */
   int disconnected[MAX_PLAYERS];
   int32_t disconnect_frame;
+  /* the peers' connect-status reports (arrival schedules): peer_rep[r][k] the last frame of player k
+   * that remote player r's endpoint reports with k disconnected; bit r * MAX_PLAYERS + k of
+   * peer_rep_mask marks a report */
+  int32_t peer_rep[MAX_PLAYERS][MAX_PLAYERS];
+  uint32_t peer_rep_mask;
   PlayerInput local[MAX_PLAYERS];
   int has_local[MAX_PLAYERS];
   int64_t rollbacks, resim;
@@ -1174,6 +1187,34 @@ static void p2p_on_remote_input(P2PSession* s, size_t player, int32_t frame, uin
 }
 
 /* advance_frame (:265-426).  Returns 0, or -1 (InvalidRequest: missing local input). */
+/* update_player_disconnects (p2p_session.rs:748-783) over the peers' reports.  For each player k:
+ * the running endpoints (remote players not disconnected) that report k disconnected give
+ * queue_connected = false and queue_min_confirmed = the minimum of their reported last frames; the
+ * running endpoints that report k connected are taken to have received at least every frame any
+ * peer reported (they bound nothing -- the model's one assumption about frames it does not carry);
+ * the local last_frame joins the minimum while k is connected here.  Then, as the reference,
+ * disconnect_player_at_frame(k, queue_min_confirmed) (:618-655) when k is still connected here or
+ * its local last frame is newer -- again on every call for as long as that holds, since the
+ * reference leaves local_connect_status[k].last_frame where it was. */
+static void p2p_update_player_disconnects(P2PSession* s) {
+  if (!s->peer_rep_mask) return;
+  for (size_t k = 0; k < s->num_players; k++) {
+    int queue_connected = 1;
+    int32_t qmin = INT32_MAX;
+    for (size_t r = 0; r < s->num_players; r++) {
+      if (!((s->peer_rep_mask >> (r * MAX_PLAYERS + k)) & 1u) || s->disconnected[r]) continue;
+      queue_connected = 0;
+      if (s->peer_rep[r][k] < qmin) qmin = s->peer_rep[r][k];
+    }
+    const int local_connected = !s->disconnected[k];
+    if (local_connected && s->last_frame[k] < qmin) qmin = s->last_frame[k];
+    if (!queue_connected && (local_connected || s->last_frame[k] > qmin)) {
+      s->disconnected[k] = 1;
+      if (s->sl.current_frame > qmin) s->disconnect_frame = qmin + 1;
+    }
+  }
+}
+
 static int p2p_advance_frame(P2PSession* s, RequestVec* rv, int* advanced) {
   rv->n = 0;
   *advanced = 0;
@@ -1188,6 +1229,12 @@ static int p2p_advance_frame(P2PSession* s, RequestVec* rv, int* advanced) {
   /* lockstep mode (max_prediction 0, :301-304, in_lockstep_mode :565-571): no save, no rollback */
   const int lockstep = s->max_prediction == 0;
   if (s->sl.current_frame == 0 && !lockstep) rv_push(rv, sl_save_current_state(&s->sl)); /* :305-308 */
+  p2p_update_player_disconnects(s);                                          /* :311 */
+  {
+    int any = 0;
+    for (size_t i = 0; i < s->num_players; i++) any |= !s->disconnected[i];
+    if (!any) return -4;  /* confirmed_frame's assert! (:551) */
+  }
   int32_t confirmed = p2p_confirmed_frame(s);                                /* :314 */
   int32_t first_incorrect = lockstep ? NULL_FRAME : sl_check_simulation_consistency(&s->sl, s->disconnect_frame);
   if (first_incorrect != NULL_FRAME) {
@@ -1412,9 +1459,18 @@ int oracle_p2p_stream(const OracleP2PCfg* cfg, int32_t frames, const uint8_t* in
  * players' inputs local_row[P] and Game::handle_requests.  With desync detection on, the checksum
  * report the call would send is checked first: the reference panics when the cell is gone.
  * Returns 0, -1 (a schedule error) or -4 (the reference panics). */
+static int oracle_no_tail_check(void) {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ORACLE_SCHED_NO_TAIL_CHECK");
+    v = e && e[0] == '1';
+  }
+  return v;
+}
+
 static int sched_session_call(P2PSession* s, Game* game, RequestVec* rv, int32_t c, const uint8_t* local_row,
-                              const uint8_t* remote_rows, int32_t* delivered, int32_t upto, uint8_t ev, int* adv,
-                              int32_t* rb_frame, OracleP2PResult* res) {
+                              const uint8_t* remote_rows, int32_t* delivered, int32_t upto, uint8_t ev, int32_t report,
+                              int* adv, int32_t* rb_frame, OracleP2PResult* res) {
   const size_t P = s->num_players;
   if (upto > c) return -1;
   for (int32_t g = *delivered + 1; g <= upto; g++)   /* the burst */
@@ -1429,6 +1485,15 @@ static int sched_session_call(P2PSession* s, Game* game, RequestVec* rv, int32_t
       s->disconnected[i] = 1;
       if (s->sl.current_frame > s->last_frame[i]) s->disconnect_frame = s->last_frame[i] + 1;
     }
+  if (report) {  /* a peer's connect status: remote player r's endpoint reports k disconnected at n */
+    const uint32_t k = (uint32_t)report & 3u, r = ((uint32_t)report >> 2) & 3u;
+    const int32_t n = (report >> 5) - 1;
+    if (!(report & 16) || k >= P || r >= P || k == r || ((s->local_mask >> k) & 1u) || ((s->local_mask >> r) & 1u) ||
+        n < NULL_FRAME || n > c)
+      return -1;
+    s->peer_rep[r][k] = n;
+    s->peer_rep_mask |= 1u << (r * MAX_PLAYERS + k);
+  }
   int any_connected = 0;
   for (size_t i = 0; i < P; i++) any_connected |= !s->disconnected[i];
   if (!any_connected) return -4;
@@ -1440,16 +1505,47 @@ static int sched_session_call(P2PSession* s, Game* game, RequestVec* rv, int32_t
   {  /* a rollback to a frame that is not in the past panics in load_frame (sync_layer.rs:231-237):
       * a disconnect whose last_frame is current_frame - 1 sets disconnect_frame = current_frame
       * (sparse saving loads the last save instead, p2p_session.rs:666-673) */
-    const int32_t fi = sl_check_simulation_consistency(&s->sl, s->disconnect_frame);
-    const int32_t load = s->sparse_saving ? s->sl.last_saved_frame : fi;
-    if (fi != NULL_FRAME && load >= s->sl.current_frame) return -4;
+    if (s->max_prediction > 0) {  /* (lockstep mode never rolls back) */
+      int32_t dframe = s->disconnect_frame;
+      if (s->peer_rep_mask) {  /* the peers' reports apply before the rollback (update_player_disconnects) */
+        int disc[MAX_PLAYERS];
+        const int32_t dframe0 = s->disconnect_frame;
+        memcpy(disc, s->disconnected, sizeof disc);
+        p2p_update_player_disconnects(s);  /* (a dry run: advance_frame applies it) */
+        dframe = s->disconnect_frame;
+        memcpy(s->disconnected, disc, sizeof disc);
+        s->disconnect_frame = dframe0;
+      }
+      const int32_t fi = sl_check_simulation_consistency(&s->sl, dframe);
+      const int32_t load = s->sparse_saving ? s->sl.last_saved_frame : fi;
+      if (fi != NULL_FRAME && (load >= s->sl.current_frame || load < s->sl.current_frame - (int32_t)s->max_prediction))
+        return -4;
+      /* the replay reads the InputQueues from `load`; set_last_confirmed_frame trimmed them to
+       * last_confirmed - 1 (input_queue.rs:83-101): InputQueue::input's "requested frame no longer
+       * exists" (:104-110) -- only a peer's report of an old frame rolls back that far.  (The
+       * restated queues assert the same; ORACLE_SCHED_NO_TAIL_CHECK=1 leaves it to them, as the
+       * test that pins this condition does.) */
+      if (fi != NULL_FRAME && s->sl.last_confirmed_frame > 0 && load < s->sl.last_confirmed_frame - 1 &&
+          !oracle_no_tail_check())
+        return -4;
+    }
   }
   for (size_t i = 0; i < P; i++)
     if ((s->local_mask >> i) & 1u) {
       s->local[i].frame = s->sl.current_frame; s->local[i].input = local_row[i]; s->has_local[i] = 1;
     }
   int64_t rb0 = s->rollbacks;
-  if (p2p_advance_frame(s, rv, adv) < 0) return -1;
+  {
+    jmp_buf jb;
+    if (setjmp(jb)) {  /* a restated assert!: the reference panics in this call */
+      oracle_panic_jmp = NULL;
+      return -4;
+    }
+    oracle_panic_jmp = &jb;
+    const int rc = p2p_advance_frame(s, rv, adv);
+    oracle_panic_jmp = NULL;
+    if (rc < 0) return rc == -4 ? -4 : -1;
+  }
   if (rb_frame) {
     *rb_frame = -1;
     for (size_t k = 0; k < rv->n && s->rollbacks != rb0; k++)
@@ -1482,18 +1578,24 @@ static int sched_session_call(P2PSession* s, Game* game, RequestVec* rv, int32_t
  *   4. Game::handle_requests over the list.
  * Row g of inputs: local players' add_local_input of call g, remote players' input of frame g.
  * arrive_upto[c] <= c (the remote peer has sent at most its frame c); a value at or below what
- * already arrived delivers nothing.  update_player_disconnects (:748-783) changes nothing here: no
- * running endpoint reports a third player's disconnect.  Per call: advanced[c] (1 if an AdvanceFrame
+ * already arrived delivers nothing.  reports[c] (NULL: none; 0: none this call) is a peer's
+ * connect-status report received in call c's poll, GGRS_PEER_REPORT(k, r, n) = 16 | k | r << 2 |
+ * (n + 1) << 5: remote player r's endpoint reports remote player k disconnected with last frame n
+ * (-1 <= n <= c); reports persist, and update_player_disconnects (:748-783,
+ * p2p_update_player_disconnects) disconnects k at the reported frame.  max_prediction 0 is lockstep
+ * mode (:301-304, 393-397: no saves, no rollbacks, advance only at last_confirmed == current; sparse
+ * saving ignored).  Per call: advanced[c] (1 if an AdvanceFrame
  * of the current frame was emitted), rb_frame[c] (the first LoadGameState's frame, -1 for none).
  * Returns 0; -1 bad arguments or schedule; -4 a condition on which the reference panics (an input
  * queue over INPUT_QUEUE_LENGTH, no connected player, a rollback to a frame not in the past). */
 int oracle_p2p_sched_run(const OracleP2PCfg* cfg, int32_t calls, const uint8_t* inputs, const int32_t* arrive_upto,
-                         const uint8_t* events, uint8_t* advanced, int32_t* rb_frame, uint16_t* cksum_trace,
+                         const uint8_t* events, const int32_t* reports, uint8_t* advanced, int32_t* rb_frame,
+                         uint16_t* cksum_trace,
                          uint8_t* final_state, int32_t* ring_frames, uint16_t* ring_cksums, uint8_t* ring_states,
                          OracleP2PResult* res) {
   memset(res, 0, sizeof *res);
   const size_t P = (size_t)cfg->num_players;
-  if (P < 1 || P > MAX_PLAYERS || cfg->max_prediction < 1 || cfg->input_delay < 0 ||
+  if (P < 1 || P > MAX_PLAYERS || cfg->max_prediction < 0 || cfg->input_delay < 0 ||
       (cfg->local_mask & ~((1 << P) - 1)) != 0 || cfg->local_mask == (1 << P) - 1) {
     res->status = -1;
     return -1;
@@ -1507,7 +1609,7 @@ int oracle_p2p_sched_run(const OracleP2PCfg* cfg, int32_t calls, const uint8_t* 
     if ((s.local_mask >> i) & 1u) s.sl.queues[i].frame_delay = (size_t)cfg->input_delay;
   }
   s.disconnect_frame = NULL_FRAME;
-  s.sparse_saving = cfg->sparse_saving;
+  s.sparse_saving = cfg->max_prediction == 0 ? 0 : cfg->sparse_saving;  /* ignored in lockstep mode (:187-197) */
   Game game; memset(&game, 0, sizeof game);
   game.desync_frame = -1;
   state_new(&game.game_state, (uint64_t)P);
@@ -1518,7 +1620,8 @@ int oracle_p2p_sched_run(const OracleP2PCfg* cfg, int32_t calls, const uint8_t* 
   for (int32_t c = 0; c < calls && rc == 0; c++) {
     int adv = 0;
     rc = sched_session_call(&s, &game, &rv, c, inputs + (size_t)c * P, inputs, &delivered, arrive_upto[c],
-                            events ? events[c] : 0, &adv, rb_frame ? &rb_frame[c] : NULL, res);
+                            events ? events[c] : 0, reports ? reports[c] : 0, &adv, rb_frame ? &rb_frame[c] : NULL,
+                            res);
     if (rc) break;
     if (advanced) advanced[c] = (uint8_t)adv;
     if (cksum_trace) cksum_trace[c] = game.last_checksum;
@@ -1929,7 +2032,7 @@ static void* p2p_batch_worker(void* arg) {
     }
     OracleP2PResult res;
     uint8_t* fs = j->final_states ? j->final_states + l * sb : NULL;
-    const int rc = j->arrive ? oracle_p2p_sched_run(j->cfg, j->calls, in, up, NULL, NULL, NULL, NULL, fs, NULL, NULL,
+    const int rc = j->arrive ? oracle_p2p_sched_run(j->cfg, j->calls, in, up, NULL, NULL, NULL, NULL, NULL, fs, NULL, NULL,
                                                     NULL, &res)
                              : oracle_p2p_run(j->cfg, j->calls, in, NULL, NULL, NULL, 0, NULL, fs, NULL, NULL, NULL, &res);
     if (j->rc) j->rc[l] = rc ? rc : res.status;
@@ -2047,7 +2150,7 @@ int oracle_p2p_sched_desync_pair_run(int32_t num_players, int32_t max_prediction
       }
       int adv = 0;
       const int32_t d0 = delivered[k];
-      rc[k] = sched_session_call(me, &g[k], &rv, c, eff, sent_rows + (size_t)o * calls * P, &delivered[k], up, 0, &adv,
+      rc[k] = sched_session_call(me, &g[k], &rv, c, eff, sent_rows + (size_t)o * calls * P, &delivered[k], up, 0, 0, &adv,
                                  NULL, &res[k]);
       (void)d0;
       if (rc[k]) continue;

@@ -320,18 +320,26 @@ def stall_schedule(calls, max_prediction, seed, max_lag=None, stall_every=40, st
     return upto.astype(np.int32)
 
 
+def peer_report(player, reporter, frame):
+    """GGRS_PEER_REPORT: remote player `reporter`'s endpoint reports remote player `player`
+    disconnected with last frame `frame` (a reports[] entry of p2p_sched_run / the device engine)."""
+    return 16 | player | reporter << 2 | (frame + 1) << 5
+
+
 def p2p_sched_run(inputs, arrive_upto, events=None, num_players=2, local_mask=0b01, input_delay=0,
-                  max_prediction=8, predictor=0, sparse_saving=False):
+                  max_prediction=8, predictor=0, sparse_saving=False, reports=None):
     """One peer's P2P session under an arrival schedule, with the prediction threshold and
     disconnects (oracle_p2p_sched_run): inputs[c] = local add_local_input of call c / remote input of
     frame c; arrive_upto[c] = newest remote frame delivered by call c; events[c] bit k = player k's
-    Event::Disconnected at call c.  Returns rc, result, per-call advanced / rb_frame / ck_trace, the
-    final state and the ring; current_frame and skips derived from the counts."""
+    Event::Disconnected at call c; reports[c] a peer's disconnect report (peer_report, 0 none);
+    max_prediction 0 is lockstep mode.  Returns rc, result, per-call advanced / rb_frame / ck_trace,
+    the final state and the ring; current_frame and skips derived from the counts."""
     inputs = np.ascontiguousarray(inputs, np.uint8).reshape(-1, num_players)
     calls = inputs.shape[0]
     upto = np.ascontiguousarray(arrive_upto, np.int32)
     assert upto.shape[0] >= calls
     ev = None if events is None else np.ascontiguousarray(events, np.uint8)
+    rp = None if reports is None else np.ascontiguousarray(reports, np.int32)
     R, sb = max_prediction + 1, state_bytes(num_players)
     cfg = P2PCfg(num_players, max_prediction, input_delay, 1, local_mask, predictor, int(sparse_saving))
     res = P2PResult()
@@ -343,13 +351,13 @@ def p2p_sched_run(inputs, arrive_upto, events=None, num_players=2, local_mask=0b
     if not getattr(L, "_sched_bound", False):
         P = ctypes.POINTER
         u8p, u16p, i32p = P(ctypes.c_uint8), P(ctypes.c_uint16), P(ctypes.c_int32)
-        L.oracle_p2p_sched_run.argtypes = [P(P2PCfg), ctypes.c_int32, u8p, i32p, u8p, u8p, i32p, u16p, u8p, i32p,
-                                           u16p, u8p, P(P2PResult)]
+        L.oracle_p2p_sched_run.argtypes = [P(P2PCfg), ctypes.c_int32, u8p, i32p, u8p, i32p, u8p, i32p, u16p, u8p,
+                                           i32p, u16p, u8p, P(P2PResult)]
         L.oracle_p2p_sched_run.restype = ctypes.c_int
         L._sched_bound = True
     rc = L.oracle_p2p_sched_run(
         ctypes.byref(cfg), calls, _ptr(inputs, ctypes.c_uint8), _ptr(upto, ctypes.c_int32), _ptr(ev, ctypes.c_uint8),
-        _ptr(out["advanced"], ctypes.c_uint8), _ptr(out["rb_frame"], ctypes.c_int32),
+        _ptr(rp, ctypes.c_int32), _ptr(out["advanced"], ctypes.c_uint8), _ptr(out["rb_frame"], ctypes.c_int32),
         _ptr(out["ck_trace"], ctypes.c_uint16), _ptr(out["final_state"], ctypes.c_uint8),
         _ptr(out["ring_frames"], ctypes.c_int32), _ptr(out["ring_cksums"], ctypes.c_uint16),
         _ptr(out["ring_states"], ctypes.c_uint8), ctypes.byref(res))

@@ -260,6 +260,8 @@ extern "C" {
     pub fn ggrs_p2p_synchronize(eng: *mut ggrs_p2p_engine_t) -> i32;
     pub fn ggrs_p2p_read_state(eng: *mut ggrs_p2p_engine_t, session: i32, out: *mut u8) -> i32;
     pub fn ggrs_p2p_read_states(eng: *mut ggrs_p2p_engine_t, out: *mut u8) -> i32;
+    pub fn ggrs_p2p_add_peer_reports(eng: *mut ggrs_p2p_engine_t, first_call: i32, n_calls: i32, reports: *const i32)
+                                     -> i32;
     pub fn ggrs_p2p_read_ring(eng: *mut ggrs_p2p_engine_t, session: i32, frames: *mut i32, checksums: *mut u16,
                               states: *mut u8) -> i32;
     pub fn ggrs_p2p_read_stats(eng: *mut ggrs_p2p_engine_t, rollbacks: *mut i32, resim_frames: *mut i64) -> i32;

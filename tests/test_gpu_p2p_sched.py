@@ -34,7 +34,7 @@ def schedules(S, calls, mp, seed, local_mask, P, disconnect_every=5):
     return arrive, events
 
 
-def check_sessions(eng, rows, arrive, events, sessions, calls, **kw):
+def check_sessions(eng, rows, arrive, events, sessions, calls, reports=None, **kw):
     from oracle import oracle as o
     from ggrs_amd._lib import GGRS_E_PRECONDITION
     frames, skipped, errors = eng.sessions()
@@ -42,7 +42,8 @@ def check_sessions(eng, rows, arrive, events, sessions, calls, **kw):
     for s in sessions:
         out = o.p2p_sched_run(rows[:calls, s], arrive[:calls, s], events[:calls, s], num_players=eng.num_players,
                               local_mask=eng.local_mask, input_delay=eng.input_delay,
-                              max_prediction=eng.max_prediction, predictor=eng.predictor, **kw)
+                              max_prediction=eng.max_prediction, predictor=eng.predictor,
+                              reports=None if reports is None else reports[:calls, s], **kw)
         res = out["result"]
         if out["rc"] == -4:  # the reference panics at this call: the device stops the session there
             assert errors[s] == GGRS_E_PRECONDITION, (s, errors[s])
@@ -255,3 +256,106 @@ def test_p2p_bench_schedule_full_size_every_session(oracle, monkeypatch, form, s
     assert r["rc_mismatched"] == r["final_state_mismatched"] == r["rollbacks_mismatched"] == 0, r
     assert r["frame_skips_mismatched"] == 0, r
     check_sessions(eng, rows, arrive, np.zeros((calls, S), np.uint8), (0, 1, S // 2, S - 1), calls)
+
+
+@pytest.mark.parametrize("P,local,delay", [(2, (0,), 0), (2, (1,), 2), (4, (0, 2), 1), (3, (), 0)])
+def test_p2p_lockstep_schedules_match_oracle(oracle, P, local, delay):
+    """Lockstep mode under arrival schedules (max_prediction 0, p2p_session.rs:301-304, 393-397):
+    no saves, no rollbacks, a call advances only when last_confirmed_frame == current_frame --
+    jittered, stalled and fixed networks and disconnects; every session bit-exact against the
+    oracle (state, frames, skipped calls, counts), in launches of uneven length."""
+    from ggrs_amd import P2PEngine
+    S, calls = 300, 180
+    rows = np.stack([oracle.gen_inputs(oracle.session_seed(s, 77), calls, P, 1) for s in range(S)], axis=1)
+    lmask = sum(1 << k for k in local)
+    arrive, events = schedules(S, calls, 8, 13, lmask, P)
+    eng = P2PEngine(S, num_players=P, local_players=local, input_delay=delay, max_prediction=0, remote_latency=1,
+                    input_capacity=calls)
+    eng.set_arrival_schedule(True)
+    eng.add_inputs(0, rows)
+    eng.add_arrivals(0, arrive, events)
+    for n in (1, 30, 64, 85):
+        eng.advance_frames(n)
+    check_sessions(eng, rows, arrive, events, range(S), calls)
+    rb, _ = eng.stats()
+    assert (rb == 0).all()
+    frames, skipped, errors = eng.sessions()
+    assert skipped.sum() > 0 and frames.max() > 40
+
+
+def peer_report_schedules(S, calls, mp, seed, P, local_mask):
+    """Per session a network (schedules()) and peers' disconnect reports of several kinds: at the
+    frame the call delivered (the local Event::Disconnected's frame), older ones (repeated rollbacks
+    while the reporter runs; further back than the input queues hold: the reference panics), about a
+    player already disconnected here at the reported frame, and a reported player's peer reporting
+    its own reporter."""
+    from oracle import oracle as o
+    arrive, events = schedules(S, calls, mp, seed, local_mask, P, disconnect_every=0)
+    remote = [k for k in range(P) if not (local_mask >> k) & 1]
+    reports = np.zeros((calls, S), np.int32)
+    rng = np.random.default_rng(seed + 1)
+    for s in range(S):
+        kind = s % 6
+        k, r = (remote[0], remote[1]) if s % 2 == 0 else (remote[-1], remote[0])
+        c = int(rng.integers(calls // 4, calls // 2))
+        delivered = int(np.maximum.accumulate(arrive[:, s])[c])
+        if kind == 0:
+            reports[c, s] = o.peer_report(k, r, delivered)
+        elif kind == 1:
+            reports[c, s] = o.peer_report(k, r, max(delivered - 1, -1))
+            events[c + 3, s] |= 1 << r  # the reporter leaves: the repeated rollbacks stop
+        elif kind == 2:
+            reports[c, s] = o.peer_report(k, r, max(delivered - int(rng.integers(2, 12)), -1))
+        elif kind == 3:
+            events[c, s] |= 1 << k  # disconnected here first; a peer's report of the same frame changes nothing
+            reports[c + 2, s] = o.peer_report(k, r, delivered)
+        elif kind == 4:
+            reports[c, s] = o.peer_report(k, r, delivered)
+            reports[c + 5, s] = o.peer_report(r, k if k != r else remote[0], delivered)  # k's peer reports r
+        # kind 5: no report
+    return arrive, events, reports
+
+
+@pytest.mark.parametrize("sparse", [False, True])
+@pytest.mark.parametrize("P,local,mp", [(4, (0,), 8), (3, (1,), 6), (4, (0, 3), 9)])
+def test_p2p_peer_reported_disconnects_match_oracle(oracle, P, local, mp, sparse):
+    """update_player_disconnects (p2p_session.rs:748-783) over the peers' reports, with P > 2
+    (ggrs_p2p_add_peer_reports): every session's state, ring, counts, frames, skips and error --
+    including the sessions whose report rolls back further than the reference's input queues hold
+    (it panics there) -- bit-exact against the oracle."""
+    from ggrs_amd import P2PEngine
+    from ggrs_amd._lib import GGRS_E_PRECONDITION
+    S, calls = 360, 160
+    rows = np.stack([oracle.gen_inputs(oracle.session_seed(s, 91), calls, P, 1) for s in range(S)], axis=1)
+    lmask = sum(1 << k for k in local)
+    arrive, events, reports = peer_report_schedules(S, calls, mp, 29, P, lmask)
+    eng = P2PEngine(S, num_players=P, local_players=local, max_prediction=mp, remote_latency=1, input_capacity=calls)
+    eng.set_arrival_schedule(True)
+    if sparse:
+        eng.set_sparse_saving(True)
+    eng.add_inputs(0, rows)
+    eng.add_arrivals(0, arrive, events)
+    eng.add_peer_reports(0, reports)
+    for n in (37, 64, 59):
+        eng.advance_frames(n)
+    check_sessions(eng, rows, arrive, events, range(S), calls, reports=reports, sparse_saving=sparse)
+    frames, skipped, errors = eng.sessions()
+    assert (errors == GGRS_E_PRECONDITION).sum() > 0 and (errors == 0).sum() > S // 2
+
+
+def test_p2p_peer_reports_rejected(oracle):
+    from ggrs_amd import InvalidRequest, P2PEngine
+    from ggrs_amd.p2p import peer_report
+    S, calls, P = 8, 20, 3
+    eng = P2PEngine(S, num_players=P, local_players=(0,), max_prediction=8, remote_latency=1, input_capacity=calls)
+    eng.set_arrival_schedule(True)
+    eng.add_inputs(0, np.zeros((calls, S, P), np.uint8))
+    eng.add_arrivals(0, np.full((10, S), -1, np.int32))
+    for bad in (peer_report(0, 2, 3), peer_report(1, 0, 3), peer_report(1, 1, 3), peer_report(1, 2, 6)):
+        rep = np.zeros((10, S), np.int32)
+        rep[5, 3] = bad
+        with pytest.raises(InvalidRequest):
+            eng.add_peer_reports(0, rep)
+    with pytest.raises(InvalidRequest):  # calls whose arrivals are not added yet
+        eng.add_peer_reports(5, np.zeros((10, S), np.int32))
+    eng.add_peer_reports(0, np.zeros((10, S), np.int32))
