@@ -936,6 +936,73 @@ def requests_cpu_baseline(args, synth, P, maxp, cd):
             "wall_s": round(wall, 3), "all_ok": all(r == 0 for r in res)}
 
 
+def requests_p2p_cpu_baseline(args, fx):
+    """The request boundary with P2P lists on the host: ex_game's handler restatement
+    (oracle_handler_run: Save = clone + bincode + fletcher16, Load = clone, Advance = State::advance)
+    over the same committed fixture's lists, one session's whole stream per task on T threads --
+    what the Rust handler does per session without this engine.  Units: advance_frame calls."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import numpy as np
+    from ggrs_amd._lib import REQ_ADVANCE
+    from oracle import oracle as O
+    O.build()
+    T = cpu_threads(args)
+    M, C, P, maxp = fx["M"], fx["C"], fx["P"], fx["maxp"]
+    streams = []
+    for m in range(M):
+        a, b = int(fx["req_off"][m, 0]), int(fx["req_off"][m, C])
+        kind = np.ascontiguousarray(fx["kind"][a:b].astype(np.int32))
+        inp = np.zeros((b - a, P), np.uint8)
+        st = np.zeros((b - a, P), np.uint8)
+        adv = np.nonzero(kind == REQ_ADVANCE)[0]
+        a0 = int(fx["adv_off"][m, 0])
+        inp[adv] = fx["inputs"][a0:a0 + len(adv)]
+        st[adv] = fx["status"][a0:a0 + len(adv)]
+        streams.append((kind, np.ascontiguousarray(fx["frame"][a:b]), inp, st))
+    ok, one = O.handler_bench(streams, P, maxp, M, 1)  # every stream once, one thread: the size of a task
+    tasks = max(T, int(10.0 * T * M / max(one, 1e-6)))  # about 10 s of wall time on T threads
+    ok, wall = O.handler_bench(streams, P, maxp, tasks, T)
+    res = [0 if ok == tasks else -1]  # (every stream ran without a rejected request)
+    return {"value": round(tasks * C / wall, 1), "unit": "session-frames/s", "cores": T, "kind": "port",
+            "sample": f"{T} threads x {tasks} session streams of {C} advance_frame calls each (the committed P2P "
+                      f"fixture's {M} sessions' request lists) through the ex_game handler restatement "
+                      "(oracle_handler_run)",
+            "wall_s": round(wall, 3), "cpu": cpu_model(), "all_ok": all(r == 0 for r in res)}
+
+
+def read_host_profile(drv, T, n_calls, lanes_per_group, G):
+    """handler_profile_read after a profiled run: per call and per thread (mean over threads), the
+    time spinning / handing back / encoding, and per lane the counters of each pass."""
+    import ctypes
+
+    import numpy as np
+    nc = 5
+    w = 5 + 2 * nc
+    buf = np.zeros((max(T, 1), w), np.float64)
+    drv.handler_profile_read.restype = ctypes.c_int32
+    drv.handler_profile_read.argtypes = [ctypes.c_void_p, ctypes.c_int32]
+    n = drv.handler_profile_read(ctypes.c_void_p(buf.ctypes.data), buf.shape[0])
+    buf = buf[:n]
+    names = ["cycles", "instructions", "cache_references", "cache_misses", "l1d_read_misses"]
+    lanes_call = lanes_per_group * G  # every lane encoded once per call, its share on each thread
+    out = {"threads": int(n), "calls": int(n_calls),
+           "us_per_call_per_thread": {"spin": round(float(buf[:, 0].mean()) / n_calls * 1e6, 3),
+                                      "handback": round(float(buf[:, 1].mean()) / n_calls * 1e6, 3),
+                                      "encode": round(float(buf[:, 2].mean()) / n_calls * 1e6, 3)},
+           "ns_per_lane": {"handback": round(float(buf[:, 1].sum()) / (n_calls * lanes_call) * 1e9, 2),
+                           "encode": round(float(buf[:, 2].sum()) / (n_calls * lanes_call) * 1e9, 2)},
+           "counters_open": int(buf[:, 4 + 2 * nc].min()) if n else 0}
+    k = out["counters_open"]
+    if k:
+        for j, part in ((5, "handback"), (5 + nc, "encode")):
+            tot = buf[:, j - 2:j - 2 + nc].sum(axis=0)
+            out[f"{part}_per_lane"] = {names[i]: round(float(tot[i]) / (n_calls * lanes_call), 3) for i in range(k)}
+            if k >= 2 and tot[0] > 0:
+                out[f"{part}_per_lane"]["ipc"] = round(float(tot[1] / tot[0]), 3)
+    return out
+
+
 def p2p_cpu_baseline(args, O, synth, P, D, maxp):
     """The oracle's P2P session (C restatement of p2p_session.rs:265-426 + ex_game) on T host
     threads, one session per thread (ctypes drops the GIL for the call)."""
@@ -1176,7 +1243,18 @@ def run_requests(args):
                 call(f + k)
     # warm-up calls, then the timed ones (SyncTest lists: the first cd + 1 frames carry no rollback)
     f = (0 if form == "p2p" else cd + 1) + args.warmup * calls
-    run_calls(0, f)
+    host_profile = None
+    if form == "p2p" and args.req_profile and args.warmup >= 2:
+        # the encoder's profile over warm-up steps 2.. (instrumented: not the timed region)
+        run_calls(0, calls)
+        os.environ["GGRS_DRIVER_PROFILE"] = "1"
+        try:
+            run_calls(calls, f - calls)
+        finally:
+            os.environ.pop("GGRS_DRIVER_PROFILE", None)
+        host_profile = read_host_profile(drv, T, f - calls, L // G, G)
+    else:
+        run_calls(0, f)
     if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
@@ -1231,8 +1309,9 @@ def run_requests(args):
         except Exception as exc:
             parity = {"error": repr(exc)}
         cpu_baseline = None
-        if world == 1 and not args.no_cpu_baseline and form != "p2p":
-            cpu_baseline = requests_cpu_baseline(args, synth, P, maxp, cd)
+        if world == 1 and not args.no_cpu_baseline:
+            cpu_baseline = (requests_p2p_cpu_baseline(args, fx) if form == "p2p" else
+                            requests_cpu_baseline(args, synth, P, maxp, cd))
         # the device work of one call is the SyncTest frame's Load + cd x (Advance, Save) per lane:
         # its algorithmic HBM bytes over the call's wall time (PCIe round trip and host handler
         # included -- the call is latency-bound, so this is far below the HBM roofline)
@@ -1273,6 +1352,29 @@ def run_requests(args):
         if form == "p2p":
             line["resimulated_session_frames_per_s"] = round(total_resim / elapsed, 1)
             line["resimulated_per_session_frame"] = round(resim / units, 4)
+            # the bound: each call is a host encode + hand-back of every lane's list and one PCIe
+            # round trip per lane group; the device's own work per call (the lists' advances, saves,
+            # loads) is microseconds of HBM traffic, so the HBM figure is a floor, and the call's
+            # critical path is the host's -- achieved against the measured device round trip
+            m_of = np.arange(L) % fx["M"]
+            adv_c = int(fx["n_adv"][m_of][:, f_timed:f].sum()) / n_calls
+            Sp = 4 + 20 * P
+            dev_bytes = adv_c * (2 * Sp + P) + L * 2 * Sp  # per call: every advance's state in/out + inputs,
+            call_us = elapsed / n_calls * 1e6             # each lane's state loaded and stored once
+            wait_us = phases[2] / n_calls * 1e6
+            submit_us = phases[1] / n_calls * 1e6
+            line["roofline"] = {
+                "bound": "hbm", "achieved": round(dev_bytes / (call_us * 1e-6) / 1e9, 3), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(dev_bytes / (call_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 6), "traffic": None,
+                "algorithmic_bytes_per_call": int(dev_bytes),
+                "latency_bound": {"unit": "us", "us_per_call": round(call_us, 2),
+                                  "device_round_trip_us_per_call": round(wait_us + submit_us, 2),
+                                  "host_encode_handback_us_per_call": round(phases[0] / n_calls * 1e6, 2),
+                                  "frac_of_call_on_device_round_trip": round((wait_us + submit_us) / call_us, 4)},
+                "note": "host-bound: the call is the host encode + hand-back of every lane's list plus the lane "
+                        "groups' PCIe round trips; the device work per call is microseconds of HBM"}
+            if host_profile is not None:
+                line["host_profile"] = host_profile
         print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
@@ -1353,6 +1455,10 @@ def main():
     ap.add_argument("--req-deferred", action="store_true",
                     help="requests (p2p): deferred checksum hand-back (handle_requests_deferred): the session "
                          "logic (--session-us) overlaps the batch on the device")
+    ap.add_argument("--req-profile", action="store_true",
+                    help="requests (p2p): profile the host encoder over the warm-up calls after the first step "
+                         "(per thread: spin / hand-back / encode time, and user-space cache counters where the "
+                         "kernel allows them) -- reported as host_profile, outside the timed region")
     ap.add_argument("--session-us", type=float, default=0.0,
                     help="requests: modelled GGRS session-logic host time per lane group and call (us)")
     ap.add_argument("--workload", choices=["synctest", "p2p", "codec", "requests", "launch-selftest"],
@@ -1376,6 +1482,12 @@ def main():
         # the host handler's worker threads meet at barriers twice per lane group and call: spin
         # there (before torch loads libgomp, which reads this once)
         os.environ.setdefault("OMP_WAIT_POLICY", "active")
+        # one worker per physical core, bound: unbound, the workers of a job whose affinity spans the
+        # machine (a CPU quota, not a cpuset) share SMT siblings and migrate -- the P2P encoder then
+        # takes 204 cycles per lane at IPC 1.7 instead of 83 at IPC 4.1 for the same 342
+        # instructions (profiles/r06_reqp2p/plateau_threads_binding.txt)
+        os.environ.setdefault("OMP_PROC_BIND", "close")
+        os.environ.setdefault("OMP_PLACES", "cores")
         return run_requests(args)
     if args.config == 5:
         return run_particles(args)

@@ -18,9 +18,14 @@
  *   p2p       every lane its own P2PSession's lists (p2p_session.rs:265-426, rollbacks of differing
  *             depth) from a fixture the oracle generated (bench_native/make_p2p_fixture.py), each
  *             lane encoded by ggrs_lane_encode, the encoder the Rust crate uses. */
+#include <linux/perf_event.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
+#include <sys/ioctl.h>
+#include <sys/syscall.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "ggrs_amd.h"
 #include <omp.h>
@@ -35,6 +40,78 @@ static double now_s(void) {
   struct timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
   return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
+/* ---- the P2P encoder's profile (GGRS_DRIVER_PROFILE=1; bench.py --req-profile): per host thread
+ * the time spent waiting for the step's release / the workers (spin), handing checksums back and
+ * encoding lists -- the two as separate passes over the thread's lanes -- and, where the kernel
+ * lets a process count its own events (perf_event_open, user space only), cycles, instructions,
+ * cache references / misses and L1D read misses of each pass, read as one group per pass. */
+#define PROF_MAX_T 64
+#define PROF_NC 5
+typedef struct {
+  double t_spin, t_hb, t_enc;
+  uint64_t c_hb[PROF_NC], c_enc[PROF_NC];
+  int64_t lanes;
+  int32_t counters;  /* the events that opened (0: none) */
+} thread_prof_t;
+static thread_prof_t g_prof[PROF_MAX_T];
+static int32_t g_prof_threads;
+
+static int prof_open(uint32_t type, uint64_t config, int group) {
+  struct perf_event_attr a;
+  memset(&a, 0, sizeof a);
+  a.size = sizeof a;
+  a.type = type;
+  a.config = config;
+  a.disabled = group < 0;
+  a.exclude_kernel = 1;
+  a.exclude_hv = 1;
+  a.read_format = PERF_FORMAT_GROUP;
+  return (int)syscall(SYS_perf_event_open, &a, 0, -1, group, 0);
+}
+/* this thread's counter group: its leader's fd, or -1 */
+static int prof_group(int32_t* n_open) {
+  const uint64_t l1d_miss = PERF_COUNT_HW_CACHE_L1D | (PERF_COUNT_HW_CACHE_OP_READ << 8) |
+                            ((uint64_t)PERF_COUNT_HW_CACHE_RESULT_MISS << 16);
+  const int lead = prof_open(PERF_TYPE_HARDWARE, PERF_COUNT_HW_CPU_CYCLES, -1);
+  *n_open = 0;
+  if (lead < 0) return -1;
+  *n_open = 1;
+  const struct { uint32_t t; uint64_t c; } ev[PROF_NC - 1] = {{PERF_TYPE_HARDWARE, PERF_COUNT_HW_INSTRUCTIONS},
+                                                             {PERF_TYPE_HARDWARE, PERF_COUNT_HW_CACHE_REFERENCES},
+                                                             {PERF_TYPE_HARDWARE, PERF_COUNT_HW_CACHE_MISSES},
+                                                             {PERF_TYPE_HW_CACHE, l1d_miss}};
+  for (int i = 0; i < PROF_NC - 1; i++) {
+    if (prof_open(ev[i].t, ev[i].c, lead) < 0) break;
+    ++*n_open;
+  }
+  ioctl(lead, PERF_EVENT_IOC_ENABLE, PERF_IOC_FLAG_GROUP);
+  return lead;
+}
+static void prof_read(int fd, int32_t n, uint64_t* v) {
+  uint64_t buf[1 + PROF_NC];
+  memset(v, 0, sizeof(uint64_t) * PROF_NC);
+  if (fd < 0 || read(fd, buf, sizeof(uint64_t) * (1 + (size_t)n)) <= 0) return;
+  for (int i = 0; i < n && i < PROF_NC; i++) v[i] = buf[1 + i];
+}
+/* out[t][3 + 2 PROF_NC + 2]: t_spin, t_hb, t_enc (s), the handback counters, the encode counters,
+ * lanes encoded, counters open; returns the threads profiled */
+int32_t handler_profile_read(double* out, int32_t max_threads) {
+  const int32_t n = g_prof_threads < max_threads ? g_prof_threads : max_threads;
+  for (int32_t t = 0; t < n; t++) {
+    double* o = out + (size_t)t * (5 + 2 * PROF_NC);
+    o[0] = g_prof[t].t_spin;
+    o[1] = g_prof[t].t_hb;
+    o[2] = g_prof[t].t_enc;
+    for (int i = 0; i < PROF_NC; i++) {
+      o[3 + i] = (double)g_prof[t].c_hb[i];
+      o[3 + PROF_NC + i] = (double)g_prof[t].c_enc[i];
+    }
+    o[3 + 2 * PROF_NC] = (double)g_prof[t].lanes;
+    o[4 + 2 * PROF_NC] = g_prof[t].counters;
+  }
+  return n;
 }
 
 static void spin_us(double us) {
@@ -293,9 +370,20 @@ int handler_drive_p2p_groups(ggrs_engine_t** engs, int32_t G, int32_t L, int32_t
    * arrival counter instead of two full barriers per step. */
   _Atomic int64_t ready = -1, done = 0;
   const int64_t n_steps = (int64_t)(n_calls + 1) * G;
+  const char* prof_env = getenv("GGRS_DRIVER_PROFILE");
+  const int prof = prof_env && prof_env[0] == '1';
+  if (prof) {
+    memset(g_prof, 0, sizeof g_prof);
+    g_prof_threads = threads < PROF_MAX_T ? threads : PROF_MAX_T;
+  }
 #pragma omp parallel num_threads(threads) reduction(+ : acc) if (threads > 1)
   {
     const int tid = omp_get_thread_num(), nt = omp_get_num_threads();
+    thread_prof_t* tp = prof && tid < PROF_MAX_T ? &g_prof[tid] : NULL;
+    int32_t n_open = 0;
+    const int pfd = tp ? prof_group(&n_open) : -1;
+    if (tp) tp->counters = n_open;
+    uint64_t c0[PROF_NC], c1[PROF_NC], c2[PROF_NC];
     for (int64_t e = 0; e < n_steps; e++) {
       const int32_t c = c_begin + (int32_t)(e / G);
       const int q = (int)(e % G);
@@ -312,22 +400,33 @@ int handler_drive_p2p_groups(ggrs_engine_t** engs, int32_t G, int32_t L, int32_t
         step_err = atomic_load_explicit(&err, memory_order_relaxed);
         atomic_store_explicit(&ready, e, memory_order_release);
       } else {
+        const double ts = tp ? now_s() : 0;
         while (atomic_load_explicit(&ready, memory_order_acquire) < e) __builtin_ia32_pause();
+        if (tp) tp->t_spin += now_s() - ts;
       }
       const double tw = now_s();
       const int32_t l0 = (int32_t)((int64_t)Lg * tid / nt), l1 = (int32_t)((int64_t)Lg * (tid + 1) / nt);
       const int handback = gq->pending && !step_err, encode = c < c_begin + n_calls && !step_err;
       const int32_t pc = prev_call[q];
+      /* profiling: the hand-back and the encode as two passes, each timed and counted */
+      const int passes = tp ? 2 : 1;
+      for (int pass = 0; pass < passes; pass++) {
+      const int do_hb = handback && (!tp || pass == 0), do_enc = encode && (!tp || pass == 1);
+      double tp0 = 0;
+      if (tp) {
+        prof_read(pfd, n_open, pass == 0 ? c0 : c1);
+        tp0 = now_s();
+      }
       for (int32_t l = l0; l < l1; l++) {
         const int32_t lane = gq->base + l, m = lane % M;
-        if (handback) { /* every Save's checksum of the lane's previous list */
+        if (do_hb) { /* every Save's checksum of the lane's previous list */
           const int64_t a = req_off[(int64_t)m * (C + 1) + pc], b = req_off[(int64_t)m * (C + 1) + pc + 1];
           int si = 0;
           for (int64_t k = a; k < b; k++)
             if (reqs[k].kind == GGRS_REQ_SAVE) acc += gq->b.checksums[(size_t)si++ * Lg + l];
           lane_frames[lane] = gq->b.lane_result[l];
         }
-        if (encode) {
+        if (do_enc) {
           const int64_t a = req_off[(int64_t)m * (C + 1) + c], b = req_off[(int64_t)m * (C + 1) + c + 1];
           const int64_t ad = adv_off[(int64_t)m * (C + 1) + c];
           int32_t bad = -1;
@@ -345,11 +444,26 @@ int handler_drive_p2p_groups(ggrs_engine_t** engs, int32_t G, int32_t L, int32_t
           }
         }
       }
+      if (tp) {
+        const double dt = now_s() - tp0;
+        prof_read(pfd, n_open, pass == 0 ? c2 : c0);
+        if (pass == 0) {
+          tp->t_hb += dt;
+          for (int i = 0; i < PROF_NC; i++) tp->c_hb[i] += c2[i] - c0[i];
+        } else {
+          tp->t_enc += dt;
+          for (int i = 0; i < PROF_NC; i++) tp->c_enc[i] += c0[i] - c1[i];
+          if (encode) tp->lanes += l1 - l0;
+        }
+      }
+      }
       if (tid != 0) {
         atomic_fetch_add_explicit(&done, 1, memory_order_release);
       } else {
         const int64_t want = (e + 1) * (nt - 1);
+        const double ts = tp ? now_s() : 0;
         while (atomic_load_explicit(&done, memory_order_acquire) < want) __builtin_ia32_pause();
+        if (tp) tp->t_spin += now_s() - ts;
         t_work += now_s() - tw;
         gq->pending = 0;
         if (encode && !atomic_load_explicit(&err, memory_order_relaxed)) {
@@ -368,6 +482,7 @@ int handler_drive_p2p_groups(ggrs_engine_t** engs, int32_t G, int32_t L, int32_t
         }
       }
     }
+    if (pfd >= 0) close(pfd);
   }
   if (atomic_load_explicit(&err, memory_order_relaxed)) return atomic_load_explicit(&err, memory_order_relaxed);
   *seconds = now_s() - t0;

@@ -2069,6 +2069,57 @@ int oracle_p2p_batch(const OracleP2PCfg* cfg, int32_t calls, int64_t lanes, cons
   return 0;
 }
 
+/* The request boundary's CPU baseline: oracle_handler_run over M sessions' request streams (kind /
+ * frame / inputs / status back to back, stream m at [off[m], off[m + 1])), `tasks` streams in all
+ * (task k plays stream k % M) on `threads` threads; returns the streams run without error and the
+ * wall seconds (the first start to the last end). */
+typedef struct {
+  int32_t P, maxp, M;
+  const int64_t* off;
+  const int32_t *kind, *frame;
+  const uint8_t *inputs, *status;
+  int64_t t0, t1;  /* tasks [t0, t1) */
+  int64_t ok;
+  double start, end;
+} HandlerBenchJob;
+static void* handler_bench_worker(void* arg) {
+  HandlerBenchJob* j = (HandlerBenchJob*)arg;
+  j->start = now_s();
+  for (int64_t t = j->t0; t < j->t1; t++) {
+    const int m = (int)(t % j->M);
+    const int64_t a = j->off[m], b = j->off[m + 1];
+    j->ok += oracle_handler_run(j->P, j->maxp, b - a, j->kind + a, j->frame + a, j->inputs + a * j->P,
+                                j->status ? j->status + a * j->P : NULL, NULL, NULL, NULL, NULL, NULL) == 0;
+  }
+  j->end = now_s();
+  return NULL;
+}
+int64_t oracle_handler_bench(int32_t P, int32_t maxp, int32_t M, const int64_t* off, const int32_t* kind,
+                             const int32_t* frame, const uint8_t* inputs, const uint8_t* status, int64_t tasks,
+                             int32_t threads, double* wall) {
+  if (threads < 1) threads = 1;
+  if (threads > 64) threads = 64;
+  pthread_t th[64]; HandlerBenchJob jobs[64];
+  const int64_t per = (tasks + threads - 1) / threads;
+  int used = 0;
+  for (int t = 0; t < threads; t++) {
+    const int64_t a = (int64_t)t * per, b = a + per < tasks ? a + per : tasks;
+    if (a >= b) break;
+    jobs[t] = (HandlerBenchJob){P, maxp, M, off, kind, frame, inputs, status, a, b, 0, 0, 0};
+    pthread_create(&th[t], NULL, handler_bench_worker, &jobs[t]);
+    used++;
+  }
+  int64_t ok = 0; double t0 = 1e300, t1 = 0;
+  for (int t = 0; t < used; t++) {
+    pthread_join(th[t], NULL);
+    ok += jobs[t].ok;
+    if (jobs[t].start < t0) t0 = jobs[t].start;
+    if (jobs[t].end > t1) t1 = jobs[t].end;
+  }
+  *wall = t1 - t0;
+  return ok;
+}
+
 /* ---------------------------------------------------------------- two peers under arrival schedules
  * Both machines of one match with desync detection (interval > 0), each under its own network:
  * arrive[k][c] is the newest frame of the OTHER peer's players that peer k's call c polls (clamped

@@ -629,6 +629,30 @@ def p2p_replay_batch(start_states, start_index, load_frame, inputs, threads=None
     return cks, st
 
 
+def handler_bench(streams, num_players, max_prediction, tasks, threads=None):
+    """oracle_handler_bench: `tasks` runs of oracle_handler_run over the request streams (a list of
+    (kind, frame, inputs, status) per session; task k plays stream k % len(streams)) on `threads`
+    threads.  Returns (streams run without error, wall seconds)."""
+    M = len(streams)
+    off = np.zeros(M + 1, np.int64)
+    off[1:] = np.cumsum([len(st[0]) for st in streams])
+    kind = np.ascontiguousarray(np.concatenate([st[0] for st in streams]), np.int32)
+    frame = np.ascontiguousarray(np.concatenate([st[1] for st in streams]), np.int32)
+    inp = np.ascontiguousarray(np.concatenate([st[2] for st in streams]), np.uint8)
+    sta = np.ascontiguousarray(np.concatenate([st[3] for st in streams]), np.uint8)
+    L = lib()
+    P_ = ctypes.POINTER
+    L.oracle_handler_bench.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, P_(ctypes.c_int64),
+                                       P_(ctypes.c_int32), P_(ctypes.c_int32), P_(ctypes.c_uint8), P_(ctypes.c_uint8),
+                                       ctypes.c_int64, ctypes.c_int32, P_(ctypes.c_double)]
+    L.oracle_handler_bench.restype = ctypes.c_int64
+    wall = ctypes.c_double()
+    ok = L.oracle_handler_bench(num_players, max_prediction, M, _ptr(off, ctypes.c_int64), _ptr(kind, ctypes.c_int32),
+                                _ptr(frame, ctypes.c_int32), _ptr(inp, ctypes.c_uint8), _ptr(sta, ctypes.c_uint8),
+                                tasks, threads or default_threads(), ctypes.byref(wall))
+    return int(ok), wall.value
+
+
 def p2p_batch(inputs, arrive=None, num_players=2, local_mask=0b01, input_delay=0, max_prediction=8, latency=4,
               predictor=0, sparse_saving=False, threads=None):
     """p2p_run (arrive None, fixed latency) or p2p_sched_run (arrive[calls][lanes]) for every lane of
