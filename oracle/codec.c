@@ -157,9 +157,13 @@ int oracle_codec_decode(const uint8_t* ref, int32_t ref_len, const uint8_t* data
   for (int b = 0; b < 8; b++) m |= (uint64_t)data[pos + b] << (8 * b);
   pos += 8;
   if (m > (uint64_t)(len - pos)) return CODEC_E_BINCODE;
-  uint8_t* x = (uint8_t*)malloc(CODEC_MAX_DECODED);
+  /* the decoded bytes: a per-thread scratch of the decode cap, allocated once (a 16 MiB malloc per
+   * packet is an mmap + munmap: page faults that serialise threads) */
+  static __thread uint8_t* scratch;
+  if (!scratch) scratch = (uint8_t*)malloc(CODEC_MAX_DECODED);
+  uint8_t* x = scratch;
   const int64_t xl = oracle_rle_decode(data + pos, (int64_t)m, x, CODEC_MAX_DECODED);
-  if (xl < 0) { free(x); return CODEC_E_RLE; }
+  if (xl < 0) { return CODEC_E_RLE; }
   /* delta_decode (:97-182): the sizes first */
   int64_t count;
   if (tag == 1) {
@@ -170,20 +174,20 @@ int oracle_codec_decode(const uint8_t* ref, int32_t ref_len, const uint8_t* data
       for (int b = 0; b < 4; b++) u |= (uint32_t)data[sizes_at + 4 * k + b] << (8 * b);
       const int32_t rel = (int32_t)u;
       const int64_t sz = (int64_t)(int32_t)((uint32_t)bs + (uint32_t)rel); /* i32 arithmetic (:118) */
-      if (sz < 0) { free(x); return CODEC_E_DELTA; }
+      if (sz < 0) { return CODEC_E_DELTA; }
       if (k < lens_cap) lens[k] = (int32_t)sz;
       bs = sz;
       sum += sz;
-      if (sum > xl) { free(x); return CODEC_E_DELTA; }
+      if (sum > xl) { return CODEC_E_DELTA; }
     }
-    if (sum != xl) { free(x); return CODEC_E_DELTA; }
+    if (sum != xl) { return CODEC_E_DELTA; }
   } else {
-    if (ref_len == 0) { free(x); return CODEC_E_DELTA; }
+    if (ref_len == 0) { return CODEC_E_DELTA; }
     count = xl / ref_len;
     for (int64_t k = 0; k < count && k < lens_cap; k++) lens[k] = ref_len;
-    if (count * ref_len != xl) { free(x); return CODEC_E_DELTA; }
+    if (count * ref_len != xl) { return CODEC_E_DELTA; }
   }
-  if (count > lens_cap || xl > cap) { free(x); return CODEC_E_CAP; }
+  if (count > lens_cap || xl > cap) { return CODEC_E_CAP; }
   const uint8_t* base = ref; int64_t base_len = ref_len;
   int64_t p = 0;
   for (int64_t k = 0; k < count; k++) {
@@ -193,7 +197,6 @@ int oracle_codec_decode(const uint8_t* ref, int32_t ref_len, const uint8_t* data
     p += sz;
   }
   *n_out = (int32_t)count;
-  free(x);
   return CODEC_OK;
 }
 
@@ -227,4 +230,50 @@ int64_t oracle_codec_bench(const uint8_t* ref, const uint8_t* pending, const int
   *wall = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
   free(pkt); free(dec); free(lens);
   return done;
+}
+
+/* oracle_codec_bench on `threads` threads, each its own slice of the packets (the endpoints a game
+ * server's threads would serve), `passes` times.  Returns packets round-tripped (-1 on a mismatch);
+ * *wall = seconds from the first start to the last end. */
+#include <pthread.h>
+typedef struct {
+  const uint8_t *ref, *pending;
+  const int32_t* count;
+  int64_t n;
+  int32_t B, W, passes;
+  int64_t done;
+  double wall;
+} CodecJob;
+static void* codec_worker(void* arg) {
+  CodecJob* j = (CodecJob*)arg;
+  j->done = oracle_codec_bench(j->ref, j->pending, j->count, j->n, j->B, j->W, j->passes, &j->wall);
+  return NULL;
+}
+int64_t oracle_codec_bench_mt(const uint8_t* ref, const uint8_t* pending, const int32_t* count, int64_t n_packets,
+                              int32_t B, int32_t W, int32_t passes, int32_t threads, double* wall) {
+  if (threads < 1) threads = 1;
+  if (threads > 64) threads = 64;
+  pthread_t th[64];
+  CodecJob jobs[64];
+  const int64_t per = (n_packets + threads - 1) / threads;
+  int used = 0;
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (int t = 0; t < threads; t++) {
+    const int64_t a = (int64_t)t * per, b = a + per < n_packets ? a + per : n_packets;
+    if (a >= b) break;
+    jobs[t] = (CodecJob){ref + a * B, pending + a * (int64_t)W * B, count + a, b - a, B, W, passes, 0, 0};
+    pthread_create(&th[t], NULL, codec_worker, &jobs[t]);
+    used++;
+  }
+  int64_t done = 0;
+  int bad = 0;
+  for (int t = 0; t < used; t++) {
+    pthread_join(th[t], NULL);
+    if (jobs[t].done < 0) bad = 1;
+    else done += jobs[t].done;
+  }
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  *wall = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+  return bad ? -1 : done;
 }

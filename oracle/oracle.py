@@ -505,6 +505,8 @@ def _codec_bind(L):
     L.oracle_rle_decode.restype = i64
     L.oracle_codec_bench.argtypes = [u8p, u8p, i32p, i64, i32, i32, i32, ctypes.POINTER(ctypes.c_double)]
     L.oracle_codec_bench.restype = i64
+    L.oracle_codec_bench_mt.argtypes = [u8p, u8p, i32p, i64, i32, i32, i32, i32, ctypes.POINTER(ctypes.c_double)]
+    L.oracle_codec_bench_mt.restype = i64
     L._codec_bound = True
 
 
@@ -552,9 +554,10 @@ def codec_decode(reference, data, max_inputs=1 << 16):
     return 0, res
 
 
-def codec_bench(ref, pending, count, passes=1):
-    """CPU baseline: encode + decode every packet one by one (oracle_codec_bench).
-    Returns (packets round-tripped, wall seconds)."""
+def codec_bench(ref, pending, count, passes=1, threads=1):
+    """CPU baseline: encode + decode every packet one by one (oracle_codec_bench; threads > 1:
+    oracle_codec_bench_mt, each thread its slice of the packets).  Returns (packets round-tripped,
+    wall seconds)."""
     L = lib()
     _codec_bind(L)
     N, W, B = pending.shape
@@ -562,8 +565,12 @@ def codec_bench(ref, pending, count, passes=1):
     pending = np.ascontiguousarray(pending, np.uint8)
     count = np.ascontiguousarray(count, np.int32)
     wall = ctypes.c_double()
-    n = L.oracle_codec_bench(_ptr(ref, ctypes.c_uint8), _ptr(pending, ctypes.c_uint8), _ptr(count, ctypes.c_int32),
-                             N, B, W, passes, ctypes.byref(wall))
+    if threads > 1:
+        n = L.oracle_codec_bench_mt(_ptr(ref, ctypes.c_uint8), _ptr(pending, ctypes.c_uint8),
+                                    _ptr(count, ctypes.c_int32), N, B, W, passes, threads, ctypes.byref(wall))
+    else:
+        n = L.oracle_codec_bench(_ptr(ref, ctypes.c_uint8), _ptr(pending, ctypes.c_uint8), _ptr(count, ctypes.c_int32),
+                                 N, B, W, passes, ctypes.byref(wall))
     if n < 0:
         raise RuntimeError("codec round trip failed")
     return n, wall.value
