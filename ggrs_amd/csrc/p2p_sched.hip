@@ -335,7 +335,9 @@ __device__ __forceinline__ uint2 sched_control_call(SchedCtl<P>& q, const SchedC
       if (e_c & kEvPeerReport) {
         const int32_t v = x.reports[(int64_t)(c % x.cap) * x.S + x.s];
         const int k = v & 3, r = (v >> 2) & 3;
-        x.rtab[(int64_t)(r * P + k) * x.S + x.s] = (v >> 5) - 1;
+        int32_t& t = x.rtab[(int64_t)(r * P + k) * x.S + x.s];
+        // (the endpoint keeps the newest last_frame of every message, protocol.rs:576-584)
+        t = ((q.rmask >> (4 * r + k)) & 1u) ? max(t, (v >> 5) - 1) : (v >> 5) - 1;
         q.rmask |= 1u << (4 * r + k);
       }
       if (q.rmask) {

@@ -1491,8 +1491,10 @@ static int sched_session_call(P2PSession* s, Game* game, RequestVec* rv, int32_t
     if (!(report & 16) || k >= P || r >= P || k == r || ((s->local_mask >> k) & 1u) || ((s->local_mask >> r) & 1u) ||
         n < NULL_FRAME || n > c)
       return -1;
-    s->peer_rep[r][k] = n;
-    s->peer_rep_mask |= 1u << (r * MAX_PLAYERS + k);
+    /* the endpoint keeps the newest last_frame of every message (protocol.rs:576-584) */
+    const uint32_t bit = 1u << (r * MAX_PLAYERS + k);
+    s->peer_rep[r][k] = (s->peer_rep_mask & bit) && s->peer_rep[r][k] > n ? s->peer_rep[r][k] : n;
+    s->peer_rep_mask |= bit;
   }
   int any_connected = 0;
   for (size_t i = 0; i < P; i++) any_connected |= !s->disconnected[i];

@@ -301,6 +301,8 @@ def peer_report_schedules(S, calls, mp, seed, P, local_mask):
         delivered = int(np.maximum.accumulate(arrive[:, s])[c])
         if kind == 0:
             reports[c, s] = o.peer_report(k, r, delivered)
+            # the same endpoint later with an older frame: it keeps the newest (protocol.rs:576-584)
+            reports[c + 4, s] = o.peer_report(k, r, max(delivered - 3, -1))
         elif kind == 1:
             reports[c, s] = o.peer_report(k, r, max(delivered - 1, -1))
             events[c + 3, s] |= 1 << r  # the reporter leaves: the repeated rollbacks stop
