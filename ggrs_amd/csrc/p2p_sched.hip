@@ -50,7 +50,7 @@ constexpr int32_t kNull = GGRS_NULL_FRAME;
 constexpr int kQ = 128;  // INPUT_QUEUE_LENGTH (input_queue.rs:6)
 constexpr int kBlock = 64;
 
-enum : int { kCur = 0, kLconf, kDframe, kLastSaved, kDelivered, kLocalLast, kSkips, kErr, kDisc, kLastSent, kRmask, kPl0 };
+enum : int { kCur = 0, kLconf, kDframe, kLastSaved, kDelivered, kLocalLast, kSkips, kErr, kDisc, kLastSent, kRmask, kLastCk, kPl0 };
 constexpr int kPlFields = 1;  // per player: last_frame (local_connect_status; remote players)
 // then the peers' disconnect reports: [reporter r][player k] the last frame r's endpoint reports
 // (valid where bit 4r + k of kRmask is set)
@@ -87,6 +87,11 @@ struct SchedParams {
   int32_t* rep_lconf;
   int32_t* rep_ll;
   uint16_t* fck;
+  // the display trace (trace_cap > 0): per call c (row c % trace_cap) and session the checksum of the
+  // state after the call's last AdvanceFrame -- a replayed frame or its own -- as the handler keeps
+  // it (ex_game.rs:115-127), the previous call's when it advanced nothing
+  uint16_t* trace;
+  int32_t trace_cap;
 };
 
 // The block's LDS (dynamic): its 64 sessions' rings [R][PC][64] uint4 (+ frame tags [R][64] with
@@ -658,6 +663,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
   auto next_slot = [&](int32_t x) { return x + 1 == R ? 0 : x + 1; };
   auto back_slot = [&](int32_t x, int32_t d) { const int32_t y = x - d; return y < 0 ? y + R : y; };
   int32_t s_slot_f = q.slot_f;  // step loop: ring slot of the current frame
+  uint32_t s_last_ck = (uint32_t)fld(kLastCk);  // the display checksum (p.trace_cap > 0)
   auto cell_load = [&](int32_t slot) {
 #pragma unroll
     for (int k = 0; k < PC; k++) {
@@ -929,6 +935,10 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
           advance_state<P>(st, in, 0u);
         }
       }
+      if (p.trace_cap > 0) {  // (uniform: only engines with a display trace)
+        if (adv) s_last_ck = fletcher16_state<P>(st);
+        if (!replaying) p.trace[(int64_t)(c % p.trace_cap) * S + s] = (uint16_t)s_last_ck;
+      }
       const bool rep = replaying;
       h = rep ? h + 1 : h;
       slot_h = rep ? next_slot(slot_h) : slot_h;
@@ -953,9 +963,10 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
     }
   }
   if (!live) return;
-  if (stp_w) {  // the step loop's: the local queues and the game state
+  if (stp_w) {  // the step loop's: the local queues, the game state, the display checksum
     for (int w = 0; w < WL; w++) p.lq[(int64_t)w * S + s] = (uint32_t)llq[w * kBlock + lt];
     store_state<P>(st, p.cur + s, S);
+    if (p.trace_cap > 0) p.sst[(int64_t)kLastCk * S + s] = (int32_t)s_last_ck;
   }
   if (!ctl_w) return;
   if (kSparse) {
@@ -1598,7 +1609,7 @@ __global__ void sched_init_kernel(int32_t* sst, int64_t S, int32_t P) {
   if (i >= (int64_t)sched_fields(P) * S) return;
   const int f = (int)(i / S);
   int32_t v = kNull;
-  if (f == kCur || f == kSkips || f == kErr || f == kDisc || f == kRmask) v = 0;  // (kLastSent: NULL_FRAME)
+  if (f == kCur || f == kSkips || f == kErr || f == kDisc || f == kRmask || f == kLastCk) v = 0;  // (kLastSent: NULL_FRAME)
   sst[i] = v;
 }
 
@@ -1742,6 +1753,8 @@ int p2p_sched_advance(ggrs_p2p_engine* e, int32_t n) {
   p.rep_lconf = e->rep_lconf;
   p.rep_ll = e->rep_ll;
   p.fck = e->fck;
+  p.trace = e->trace;
+  p.trace_cap = e->trace ? e->cfg.trace_capacity : 0;
   if (int rc = e->timer.before(e->stream)) return rc;
   hipError_t attr = hipSuccess;
   // The time-aligned form (a session's replays on 16 lanes) for few sessions: when its blocks of 16
@@ -1750,9 +1763,9 @@ int p2p_sched_advance(ggrs_p2p_engine* e, int32_t n) {
   for (int k = 0; k < P; k++) remote += !((e->cfg.local_mask >> k) & 1);
   const char* chains_env = getenv("GGRS_SCHED_CHAINS");
   const int64_t cblocks = grid_of(e->cfg.num_sessions, kCS);
-  // (lockstep mode and peer reports take the one-thread-per-session form)
+  // (lockstep mode, peer reports and the display trace take the one-thread-per-session form)
   const bool chains = !e->sparse && e->cfg.max_prediction >= 1 && e->cfg.max_prediction <= kMaxChainDepth && remote <= 2 &&
-                      !e->peer_reports && !(chains_env && chains_env[0] == '0') &&
+                      !e->peer_reports && !e->trace && !(chains_env && chains_env[0] == '0') &&
                       (cblocks <= 2 * (int64_t)e->num_cus || (chains_env && chains_env[0] == '1'));
   if (chains && n > kChainMaxCalls) {
     int rc = p2p_sched_advance(e, kChainMaxCalls);
@@ -1844,7 +1857,6 @@ int ggrs_p2p_set_arrival_schedule(ggrs_p2p_engine_t* e, int32_t on) {
   }
   if (e->cfg.max_prediction + e->cfg.input_delay + 2 >= kQ)
     return set_error(GGRS_E_INVALID, "max_prediction + input_delay must be < %d (the device input queue)", kQ - 2);
-  if (e->trace) return set_error(GGRS_E_STATE, "scheduled arrivals do not support the display-checksum trace");
   if (int rc = p2p_sched_enable(e)) return rc;
   return e->desync_interval > 0 ? p2p_sched_desync_alloc(e) : GGRS_OK;
 }

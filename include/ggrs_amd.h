@@ -552,7 +552,8 @@ int ggrs_p2p_debug_desync(ggrs_p2p_engine_t* eng, int32_t session, int32_t frame
  * Input row g (ggrs_p2p_add_inputs) = the local players' input of call g and the remote players'
  * input of frame g, as in the fixed-latency model.  max_prediction 0 is lockstep mode (no saves,
  * no rollbacks, a call advances only when last_confirmed_frame == current_frame, :301-304,
- * 393-397); sparse saving allowed in rollback mode, no trace; peers' disconnect reports
+ * 393-397); sparse saving allowed in rollback mode; the display trace per call (trace_capacity > 0: the
+ * checksum after the call's last AdvanceFrame, ggrs_p2p_read_trace indexed by call); peers' disconnect reports
  * (ggrs_p2p_add_peer_reports) after (2); desync detection (ggrs_p2p_set_desync_detection, without sparse
  * saving) per session: ggrs_p2p_read_reports; remote_latency is ignored.  A session whose
  * call would make the reference panic (a remote input no longer in the input rows or more than

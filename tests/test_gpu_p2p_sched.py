@@ -361,3 +361,31 @@ def test_p2p_peer_reports_rejected(oracle):
     with pytest.raises(InvalidRequest):  # calls whose arrivals are not added yet
         eng.add_peer_reports(5, np.zeros((10, S), np.int32))
     eng.add_peer_reports(0, np.zeros((10, S), np.int32))
+
+
+@pytest.mark.parametrize("sparse,mp", [(False, 8), (True, 7), (False, 0)])
+def test_p2p_display_trace_under_schedules(oracle, sparse, mp):
+    """The display checksum after every call (the state after the call's last AdvanceFrame, replay
+    or own; the previous one when it advanced nothing: ex_game.rs:115-127) under arrival schedules with
+    stalls and disconnects, in rollback, sparse-saving and lockstep mode: every session's trace
+    equals the oracle's up to where the reference would panic."""
+    from ggrs_amd import P2PEngine
+    S, calls, P = 320, 160, 3
+    rows = np.stack([oracle.gen_inputs(oracle.session_seed(s, 55), calls, P, 1) for s in range(S)], axis=1)
+    arrive, events = schedules(S, calls, max(mp, 4), 31, 0b001, P)
+    eng = P2PEngine(S, num_players=P, local_players=(0,), max_prediction=mp, remote_latency=1, input_capacity=calls,
+                    trace_capacity=calls)
+    eng.set_arrival_schedule(True)
+    if sparse:
+        eng.set_sparse_saving(True)
+    eng.add_inputs(0, rows)
+    eng.add_arrivals(0, arrive, events)
+    for n in (41, 64, 55):
+        eng.advance_frames(n)
+    tr = eng.trace(0, calls)
+    for s in range(S):
+        out = oracle.p2p_sched_run(rows[:, s], arrive[:, s], events[:, s], num_players=P, local_mask=0b001,
+                                   max_prediction=mp, sparse_saving=sparse)
+        done = out["result"].frames_done
+        assert (tr[:done, s] == out["ck_trace"][:done]).all(), (s, int(np.argmax(tr[:done, s] != out["ck_trace"][:done])))
+    check_sessions(eng, rows, arrive, events, range(0, S, 7), calls, sparse_saving=sparse)
