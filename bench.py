@@ -599,7 +599,7 @@ def run_p2p(args):
     world, rank, local_rank, torch, dist = setup_dist(args)
     from ggrs_amd import P2PEngine, synth
     S = args.sessions or 65536
-    P, D, maxp, calls = 2, args.latency, args.max_prediction, 64
+    P, D, maxp, calls = 2, args.latency, args.max_prediction, args.p2p_calls
     sched = args.arrivals != "fixed"
     if sched and (maxp < 2 or args.peers or args.p2p_form != "default"):
         raise SystemExit("--arrivals jitter/stall: rollback mode (--max-prediction >= 2), no --peers, default form")
@@ -1445,6 +1445,8 @@ def main():
                          "arrival schedules (ggrs_p2p_add_arrivals): jittered lags, plus network stalls")
     ap.add_argument("--latency", type=int, default=4, help="p2p: frames the remote player's inputs arrive late")
     ap.add_argument("--max-prediction", type=int, default=8, help="p2p: max_prediction (builder.rs:130-147)")
+    ap.add_argument("--p2p-calls", type=int, default=64,
+                    help="p2p: advance_frame calls per session per step (one launch; default 64)")
     ap.add_argument("--req-form", choices=["native", "p2p", "batch", "lanes", "lockstep"], default="native",
                     help="requests: the boundary form (run_requests docstring)")
     ap.add_argument("--codec-layout", choices=["chunked", "strided"], default="chunked",
