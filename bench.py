@@ -34,6 +34,15 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# the process's CPU set before anything binds a thread: the requests workload binds the handler's
+# OpenMP workers (OMP_PROC_BIND), which pins the main thread too, and threads it creates inherit that
+# mask -- the CPU baselines restore it for theirs
+PROCESS_AFFINITY = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None
+
+
+def unbind_main_thread():
+    if PROCESS_AFFINITY is not None:
+        os.sched_setaffinity(0, PROCESS_AFFINITY)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -910,6 +919,7 @@ def requests_cpu_baseline(args, synth, P, maxp, cd):
     import numpy as np
     from oracle import oracle as O
     O.build()
+    unbind_main_thread()
     T = cpu_threads(args)
     frames = 300_000
     inputs = np.stack([O.gen_inputs(synth.SEED_BASE + t, frames, P, O.MODEL_HELD) for t in range(T)], 1)
@@ -949,6 +959,7 @@ def requests_p2p_cpu_baseline(args, fx):
     from ggrs_amd._lib import REQ_ADVANCE
     from oracle import oracle as O
     O.build()
+    unbind_main_thread()
     T = cpu_threads(args)
     M, C, P, maxp = fx["M"], fx["C"], fx["P"], fx["maxp"]
     streams = []
