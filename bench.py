@@ -1501,8 +1501,9 @@ def main():
         # machine (a CPU quota, not a cpuset) share SMT siblings and migrate -- the P2P encoder then
         # takes 204 cycles per lane at IPC 1.7 instead of 83 at IPC 4.1 for the same 342
         # instructions (profiles/r06_reqp2p/plateau_threads_binding.txt)
-        os.environ.setdefault("OMP_PROC_BIND", "close")
-        os.environ.setdefault("OMP_PLACES", "cores")
+        if args.req_form == "p2p" and args.req_threads > 1:
+            os.environ.setdefault("OMP_PROC_BIND", "close")
+            os.environ.setdefault("OMP_PLACES", "cores")
         return run_requests(args)
     if args.config == 5:
         return run_particles(args)
