@@ -157,6 +157,8 @@ class SchedDesyncDetector:
         self.pending = [dict() for _ in range(S)]   # remote pending_checksums per session
         self.arrive = {}                            # call -> [S] newest remote frame delivered
         self.remote = []                            # remote report rows: (call, frame[S], cs[S], local_last[S])
+        self.remote_base = 0                        # the call of self.remote[0] (earlier rows are delivered)
+        self.remote_in = 0                          # remote rows received so far
         self.next_remote = np.zeros(S, np.int64)    # per session: remote rows delivered so far
         self.processed = 0
         self.sent = 0
@@ -177,9 +179,10 @@ class SchedDesyncDetector:
         """The remote peer's outgoing() rows (its calls first_call ..)."""
         if rows is None:
             return
-        assert first_call == len(self.remote), "remote report rows must be received in order"
+        assert first_call == self.remote_in, "remote report rows must be received in order"
         for k in range(rows["frame"].shape[0]):
             self.remote.append((first_call + k, rows["frame"][k], rows["checksum"][k], rows["local_last"][k]))
+        self.remote_in += rows["frame"].shape[0]
 
     def _on_checksum_report(self, s, frame, cs):
         pend = self.pending[s]
@@ -203,8 +206,8 @@ class SchedDesyncDetector:
             # poll_remote_clients: remote reports whose inputs this call's poll delivers, in order
             for s in range(len(self.local)):
                 g = int(self.next_remote[s])
-                while g < len(self.remote) and g < c:
-                    _, fr, cs, ll = self.remote[g]
+                while g < self.remote_in and g < c:
+                    _, fr, cs, ll = self.remote[g - self.remote_base]
                     if ll[s] > arrive[s]:
                         break
                     if fr[s] >= 0:
@@ -234,4 +237,12 @@ class SchedDesyncDetector:
                 for frame in checked:
                     del pend[frame]
         self.processed = current
+        # drop what no later call reads: the arrival rows of the calls replayed, the remote rows
+        # every session has taken
+        for c in range(first, current):
+            del self.arrive[c]
+        done = int(self.next_remote.min()) if len(self.local) else self.remote_in
+        if done > self.remote_base:
+            del self.remote[:done - self.remote_base]
+            self.remote_base = done
         return events

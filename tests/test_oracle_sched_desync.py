@@ -80,3 +80,6 @@ def test_detector_bookkeeping_matches_oracle(oracle, stalls, interval, corrupt):
         want = [(c, f, l, r) for (p, c, f, l, r) in out["events"] if p == k]
         assert got == want
     assert (len(out["events"]) > 0) == (corrupt[0] >= 0)
+    for d in dets:  # the replayed calls' arrival rows and the delivered remote rows are dropped
+        assert not d.arrive and len(d.remote) == d.remote_in - d.remote_base <= calls
+        assert d.remote_base == int(d.next_remote.min())
