@@ -174,7 +174,7 @@ struct SchedCtlEnv {
 // disconnect pending, the stage's rows staged and held (the change mask cm), nothing the reference
 // would panic at.  Returns whether the call takes it; only then are q and rec updated (by selects:
 // no branch).
-template <int P, int kPred>
+template <int P, int kPred, bool kFeat = true>
 __device__ __forceinline__ bool sched_fast_call(SchedCtl<P>& q, const SchedCtlEnv& x, uint64_t cm, int32_t c,
                                                 int32_t a_c, uint32_t e_c, uint32_t& rec, int32_t& rep,
                                                 bool en = true) {
@@ -193,8 +193,8 @@ __device__ __forceinline__ bool sched_fast_call(SchedCtl<P>& q, const SchedCtlEn
   // frame_to_send once it is confirmed and saved; its cell must still be in the ring (else the
   // reference panics: the general form stops the session)
   const int32_t fts = q.last_sent == kNull ? x.interval : q.last_sent + x.interval;
-  const bool send = x.interval > 0 && fts <= q.lconf && fts <= q.last_saved;
-  const bool fast = en & (maxp > 0) & (a <= c) & (q.disc == 0u) & (q.rmask == 0u) & (e_c == 0u) & (q.dframe == kNull) &
+  const bool send = kFeat && x.interval > 0 && fts <= q.lconf && fts <= q.last_saved;
+  const bool fast = en & (maxp > 0) & (a <= c) & (q.disc == 0u) & (!kFeat || q.rmask == 0u) & (e_c == 0u) & (q.dframe == kNull) &
                     (q.cur >= 1) & (q.cur >= lo) &
                     (q.delivered >= (kPred == 0 ? lo : lo - 1)) & (lbytes == 0u || q.local_last != kNull) &
                     (up - q.delivered < kArrTooFar) & (up < q.cur - maxp + kQ - 1) & (mis == kNull || mis >= q.cur - maxp) &
@@ -237,7 +237,9 @@ __device__ __forceinline__ bool sched_fast_call(SchedCtl<P>& q, const SchedCtlEn
 // updates `q` and returns the call's record (word 0; word 1 with sparse saving, see below).
 // a_c: the newest remote frame this call's poll delivered; e_c: its Event::Disconnected bits;
 // mask_ok / cm: the fast form's precondition and change mask over the stage's rows.
-template <int P, bool kSparse, int kPred>
+// kFeat false: an engine without desync detection or peer reports (the host's choice: no report is
+// sent, none received, q.rmask stays 0), their code compiled out
+template <int P, bool kSparse, int kPred, bool kFeat = true>
 __device__ __forceinline__ uint2 sched_control_call(SchedCtl<P>& q, const SchedCtlEnv& x, bool mask_ok, uint64_t cm,
                                                     int32_t c, int32_t a_c, uint32_t e_c, int32_t& rep) {
   using T = typename InputWord<P>::T;
@@ -277,7 +279,7 @@ __device__ __forceinline__ uint2 sched_control_call(SchedCtl<P>& q, const SchedC
   // nothing in this call that the reference would panic at -- the common call, branch-free.
   bool fast = false;
   rep = kNull;
-  if (mask_ok && !q.err) fast = sched_fast_call<P, kPred>(q, x, cm, c, a_c, e_c, rec, rep);
+  if (mask_ok && !q.err) fast = sched_fast_call<P, kPred, kFeat>(q, x, cm, c, a_c, e_c, rec, rep);
   if (fast) {
   } else if (q.err) {
     stop = kStopBefore;
@@ -337,7 +339,7 @@ __device__ __forceinline__ uint2 sched_control_call(SchedCtl<P>& q, const SchedC
       // (:618-655) while k is connected here or its local last frame is newer -- on every call that
       // holds, as the reference (local_connect_status[k].last_frame stays)
       uint32_t rdisc = 0;
-      if (e_c & kEvPeerReport) {
+      if (kFeat && (e_c & kEvPeerReport)) {
         const int32_t v = x.reports[(int64_t)(c % x.cap) * x.S + x.s];
         const int k = v & 3, r = (v >> 2) & 3;
         int32_t& t = x.rtab[(int64_t)(r * P + k) * x.S + x.s];
@@ -345,7 +347,7 @@ __device__ __forceinline__ uint2 sched_control_call(SchedCtl<P>& q, const SchedC
         t = ((q.rmask >> (4 * r + k)) & 1u) ? max(t, (v >> 5) - 1) : (v >> 5) - 1;
         q.rmask |= 1u << (4 * r + k);
       }
-      if (q.rmask) {
+      if (kFeat && q.rmask) {
         for (int k = 0; k < P; k++) {
           bool reported = false;
           int32_t qmin = INT32_MAX;
@@ -369,7 +371,7 @@ __device__ __forceinline__ uint2 sched_control_call(SchedCtl<P>& q, const SchedC
       rec = (uint32_t)code << 16 | (ev | rdisc) << 24;
       // check_checksum_send_interval (p2p_session.rs:939-975): after the poll, before the rollback
       const int32_t fts = q.last_sent == kNull ? x.interval : q.last_sent + x.interval;
-      if (!bad && x.interval > 0 && fts <= q.lconf && fts <= q.last_saved) {
+      if (kFeat && !bad && x.interval > 0 && fts <= q.lconf && fts <= q.last_saved) {
         if (fts < q.last_saved - maxp) {
           q.err = GGRS_E_PRECONDITION;  // "cell not found!" (:951-954): the reference panics
           goto call_done;
@@ -560,8 +562,10 @@ __device__ inline void sched_store_ctl(const SchedParams& p, const SchedCtl<P>& 
 // usual peer), else -1.  kSplit: two waves per block of 64 sessions -- wave 1 stages the input rows
 // of stage i + 1 and runs its control pass while wave 0 runs stage i's step loop (double-buffered
 // records and rows; one barrier per stage); chosen when a CU holds one block (few sessions), where
-// the two waves sit on two SIMDs of an otherwise idle CU.
-template <int P, bool kSparse, int kPred, int kLocal, bool kSplit>
+// the two waves sit on two SIMDs of an otherwise idle CU.  kFeat: desync detection, peer reports or
+// the display trace may be on (false: the engine has none of them, and their code is compiled out of
+// the control pass and the step loop).
+template <int P, bool kSparse, int kPred, int kLocal, bool kSplit, bool kFeat>
 __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel(SchedParams p) {
   using T = typename InputWord<P>::T;
   using Rec = typename std::conditional<kSparse, uint2, uint32_t>::type;
@@ -678,7 +682,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
   // last_saved are the control pass's
   auto save = [&](int32_t slot) {
     const uint32_t ck = fletcher16_state<P>(st);
-    if (!kSparse && p.interval > 0) p.fck[(int64_t)((int32_t)st.w[0] & (p.HF - 1)) * S + s] = (uint16_t)ck;
+    if (!kSparse && kFeat && p.interval > 0) p.fck[(int64_t)((int32_t)st.w[0] & (p.HF - 1)) * S + s] = (uint16_t)ck;
 #pragma unroll
     for (int k = 0; k < PC; k++) {
       uint32_t x[4];
@@ -789,7 +793,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
           const bool in = !q.err && cb8 + j < ce;
           up8[j] = in ? p.arrive[(int64_t)ci * S + s] : kNull;
           ev8[j] = (in && p.events) ? p.events[(int64_t)ci * S + s] : 0u;
-          if (in && p.reports && p.reports[(int64_t)ci * S + s] != 0) ev8[j] |= kEvPeerReport;
+          if (kFeat && in && p.reports && p.reports[(int64_t)ci * S + s] != 0) ev8[j] |= kEvPeerReport;
         }
         for (int j = 0; j < 8; j++) {
           const int32_t c = cb8 + j;
@@ -805,8 +809,8 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
           }
           const int32_t lconf0 = q.lconf;
           int32_t rep;
-          const uint2 rr = sched_control_call<P, kSparse, kPred>(q, env, mask_ok, cm, c, a_c, e_c, rep);
-          if (p.interval > 0 && live) sched_store_report(p, c, s, rep, lconf0, q.local_last);
+          const uint2 rr = sched_control_call<P, kSparse, kPred, kFeat>(q, env, mask_ok, cm, c, a_c, e_c, rep);
+          if (kFeat && p.interval > 0 && live) sched_store_report(p, c, s, rep, lconf0, q.local_last);
           Rec r;
           if constexpr (kSparse) r = rr;
           else r = rr.x;
@@ -935,7 +939,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
           advance_state<P>(st, in, 0u);
         }
       }
-      if (p.trace_cap > 0) {  // (uniform: only engines with a display trace)
+      if (kFeat && p.trace_cap > 0) {  // (uniform: only engines with a display trace)
         if (adv) s_last_ck = fletcher16_state<P>(st);
         if (!replaying) p.trace[(int64_t)(c % p.trace_cap) * S + s] = (uint16_t)s_last_ck;
       }
@@ -966,7 +970,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
   if (stp_w) {  // the step loop's: the local queues, the game state, the display checksum
     for (int w = 0; w < WL; w++) p.lq[(int64_t)w * S + s] = (uint32_t)llq[w * kBlock + lt];
     store_state<P>(st, p.cur + s, S);
-    if (p.trace_cap > 0) p.sst[(int64_t)kLastCk * S + s] = (int32_t)s_last_ck;
+    if (kFeat && p.trace_cap > 0) p.sst[(int64_t)kLastCk * S + s] = (int32_t)s_last_ck;
   }
   if (!ctl_w) return;
   if (kSparse) {
@@ -974,7 +978,7 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
     sched_store_ctl<P>(p, q, s, false);
   } else {
     sched_store_ctl<P>(p, q, s, true);
-    if (p.interval > 0) sched_report_checksums(p, s);  // (every save of the launch done: the barrier above)
+    if (kFeat && p.interval > 0) sched_report_checksums(p, s);  // (every save of the launch done: the barrier above)
   }
 #undef lring
 #undef ltag
@@ -1755,6 +1759,9 @@ int p2p_sched_advance(ggrs_p2p_engine* e, int32_t n) {
   p.fck = e->fck;
   p.trace = e->trace;
   p.trace_cap = e->trace ? e->cfg.trace_capacity : 0;
+  // desync detection, peer reports or the display trace: the flat kernel with their code (a session's
+  // standing reports, q.rmask, can only come from an engine given reports)
+  const bool feat = p.interval > 0 || p.reports != nullptr || p.trace_cap > 0;
   if (int rc = e->timer.before(e->stream)) return rc;
   hipError_t attr = hipSuccess;
   // The time-aligned form (a session's replays on 16 lanes) for few sessions: when its blocks of 16
@@ -1814,25 +1821,34 @@ int p2p_sched_advance(ggrs_p2p_engine* e, int32_t n) {
       if (attr == hipSuccess)
         kern<<<(unsigned)grid_of(p.S, kBlock), split ? 2 * kBlock : kBlock, shm, e->stream>>>(p);
     };
-    auto go2 = [&](auto kern1, auto kern2) {
-      if (split) go(kern2);
-      else go(kern1);
+    // (split, features) -> the kernel; sparse saving keeps the features compiled in
+    auto go4 = [&](auto k00, auto k01, auto k10, auto k11) {
+      if (split) feat ? go(k11) : go(k10);
+      else feat ? go(k01) : go(k00);
     };
     if (p.sparse) {
-      if (p.predictor == 0) go(&p2p_sched_kernel<PP, true, 0, -1, false>);
-      else go(&p2p_sched_kernel<PP, true, 1, -1, false>);
+      if (p.predictor == 0) go(&p2p_sched_kernel<PP, true, 0, -1, false, true>);
+      else go(&p2p_sched_kernel<PP, true, 1, -1, false, true>);
     } else {
       bool done = false;
       if constexpr (PP == 2) {  // one local player of two, repeat-last: the usual peer, masks compile-time
         if (p.predictor == 0 && (p.local_mask == 1u || p.local_mask == 2u)) {
-          if (p.local_mask == 1u) go2(&p2p_sched_kernel<PP, false, 0, 1, false>, &p2p_sched_kernel<PP, false, 0, 1, true>);
-          else go2(&p2p_sched_kernel<PP, false, 0, 2, false>, &p2p_sched_kernel<PP, false, 0, 2, true>);
+          if (p.local_mask == 1u)
+            go4(&p2p_sched_kernel<PP, false, 0, 1, false, false>, &p2p_sched_kernel<PP, false, 0, 1, false, true>,
+                &p2p_sched_kernel<PP, false, 0, 1, true, false>, &p2p_sched_kernel<PP, false, 0, 1, true, true>);
+          else
+            go4(&p2p_sched_kernel<PP, false, 0, 2, false, false>, &p2p_sched_kernel<PP, false, 0, 2, false, true>,
+                &p2p_sched_kernel<PP, false, 0, 2, true, false>, &p2p_sched_kernel<PP, false, 0, 2, true, true>);
           done = true;
         }
       }
       if (!done) {
-        if (p.predictor == 0) go2(&p2p_sched_kernel<PP, false, 0, -1, false>, &p2p_sched_kernel<PP, false, 0, -1, true>);
-        else go2(&p2p_sched_kernel<PP, false, 1, -1, false>, &p2p_sched_kernel<PP, false, 1, -1, true>);
+        if (p.predictor == 0)
+          go4(&p2p_sched_kernel<PP, false, 0, -1, false, false>, &p2p_sched_kernel<PP, false, 0, -1, false, true>,
+              &p2p_sched_kernel<PP, false, 0, -1, true, false>, &p2p_sched_kernel<PP, false, 0, -1, true, true>);
+        else
+          go4(&p2p_sched_kernel<PP, false, 1, -1, false, false>, &p2p_sched_kernel<PP, false, 1, -1, false, true>,
+              &p2p_sched_kernel<PP, false, 1, -1, true, false>, &p2p_sched_kernel<PP, false, 1, -1, true, true>);
       }
     }
   });
