@@ -1095,7 +1095,9 @@ struct ChainStage {
   uint4 ev;
 };
 
-template <int P, int kPred, int kLocal>
+// kFeat: desync detection on (false: its code compiled out; this form never takes peer reports or a
+// trace)
+template <int P, int kPred, int kLocal, bool kFeat>
 __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedParams p) {
   using T = typename InputWord<P>::T;
   constexpr int F = state_fields(P);
@@ -1334,7 +1336,7 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
         env.col = col;
         env.inputs = p.inputs;
         env.row_tag = p.row_tag;
-        env.interval = p.interval;
+        env.interval = kFeat ? p.interval : 0;
         env.reports = nullptr;  // (this form runs only without peer reports: the host's choice)
         env.rtab = p.sst + (int64_t)sched_rep0(P) * S;
         for (int32_t cb8 = cs; cb8 < ce; cb8 += 8) {
@@ -1366,7 +1368,7 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
             taus[j] = q.cur;
             lls0[j] = q.local_last;
             lcs[j] = q.lconf;
-            if (j < nj) ok &= sched_fast_call<P, kPred>(q, env, cm, cb8 + j, up8[j], ev8[j], recs[j], reps[j], en);
+            if (j < nj) ok &= sched_fast_call<P, kPred, kFeat>(q, env, cm, cb8 + j, up8[j], ev8[j], recs[j], reps[j], en);
             dlvs[j] = q.delivered;
             lls1[j] = q.local_last;
           }
@@ -1375,10 +1377,10 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
 #pragma unroll
               for (int j = 0; j < 8; j++) {
                 if (j < nj) emit(taus[j], lls0[j], lls1[j], recs[j], dlvs[j], 0u, rw8[j]);
-                if (j < nj && p.interval > 0) sched_store_report(p, cb8 + j, s, reps[j], lcs[j], lls1[j]);
+                if (kFeat && j < nj && p.interval > 0) sched_store_report(p, cb8 + j, s, reps[j], lcs[j], lls1[j]);
               }
             }
-            if (p.interval > 0 && live && !en) {  // (a stopped session: no report)
+            if (kFeat && p.interval > 0 && live && !en) {  // (a stopped session: no report)
               for (int j = 0; j < nj; j++) sched_store_report(p, cb8 + j, s, kNull, q.lconf, q.local_last);
             }
             continue;
@@ -1400,9 +1402,9 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
             const int32_t tau = q.cur, ll0 = q.local_last, lconf0 = q.lconf;
             const uint32_t disc0 = q.disc;
             int32_t rep;
-            const uint32_t rec = sched_control_call<P, false, kPred>(q, env, mask_ok, cm, c, a_c, e_c, rep).x;
+            const uint32_t rec = sched_control_call<P, false, kPred, kFeat>(q, env, mask_ok, cm, c, a_c, e_c, rep).x;
             if (!live) continue;
-            if (p.interval > 0) sched_store_report(p, c, s, rep, lconf0, q.local_last);
+            if (kFeat && p.interval > 0) sched_store_report(p, c, s, rep, lconf0, q.local_last);
             if (q.disc != disc0) {  // the disconnected players' last frames, frozen now
 #pragma unroll
               for (int k = 0; k < P; k++)
@@ -1445,7 +1447,7 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
       for (int32_t f = max(0, q.cur - maxp - 1); f <= q.local_last; f++)
         p.lq[(int64_t)(f & (p.WL - 1)) * S + s] = tab1(f, col).z;
     sched_store_ctl<P>(p, q, s, true);
-    if (p.interval > 0) sched_report_checksums(p, s);  // (every step done: barrier (3))
+    if (kFeat && p.interval > 0) sched_report_checksums(p, s);  // (every step done: barrier (3))
     return;
   }
 
@@ -1563,7 +1565,7 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
         // SaveGameState of frame tau (sync_layer.rs:208-215, ex_game.rs:103-108)
         {
           const uint32_t ck = fletcher16_state<P>(st);
-          if (wr && p.interval > 0) p.fck[(int64_t)(tau & (p.HF - 1)) * S + s] = (uint16_t)ck;
+          if (kFeat && wr && p.interval > 0) p.fck[(int64_t)(tau & (p.HF - 1)) * S + s] = (uint16_t)ck;
           if (wr) {
 #pragma unroll
             for (int k = 0; k < PC; k++) {
@@ -1799,12 +1801,15 @@ int p2p_sched_advance(ggrs_p2p_engine* e, int32_t n) {
                                      (int)cl.total);
         if (attr == hipSuccess) kern<<<(unsigned)cblocks, kChainThreads, cl.total, e->stream>>>(p);
       };
+      auto go_f = [&](auto k0, auto k1) { feat ? go(k1) : go(k0); };  // (feat: desync detection here)
       if constexpr (PP == 2) {
-        if (p.predictor == 0 && p.local_mask == 1u) return go(&p2p_sched_chains_kernel<PP, 0, 1>);
-        if (p.predictor == 0 && p.local_mask == 2u) return go(&p2p_sched_chains_kernel<PP, 0, 2>);
+        if (p.predictor == 0 && p.local_mask == 1u)
+          return go_f(&p2p_sched_chains_kernel<PP, 0, 1, false>, &p2p_sched_chains_kernel<PP, 0, 1, true>);
+        if (p.predictor == 0 && p.local_mask == 2u)
+          return go_f(&p2p_sched_chains_kernel<PP, 0, 2, false>, &p2p_sched_chains_kernel<PP, 0, 2, true>);
       }
-      if (p.predictor == 0) go(&p2p_sched_chains_kernel<PP, 0, -1>);
-      else go(&p2p_sched_chains_kernel<PP, 1, -1>);
+      if (p.predictor == 0) go_f(&p2p_sched_chains_kernel<PP, 0, -1, false>, &p2p_sched_chains_kernel<PP, 0, -1, true>);
+      else go_f(&p2p_sched_chains_kernel<PP, 1, -1, false>, &p2p_sched_chains_kernel<PP, 1, -1, true>);
     });
     HIP_TRY(attr);
     HIP_TRY(hipGetLastError());
