@@ -1289,6 +1289,34 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
         *reinterpret_cast<uint2*>(&tab0(tau, col)) = make_uint2(xx, y);
       }
     };
+    // emit() for a call the fast form took: no stop, no disconnect, the local queue not empty (the
+    // form's preconditions) -- fewer branches in the batch's unrolled entries
+    auto emit_fast = [&](int32_t tau, int32_t ll0, int32_t ll1, uint32_t rec, int32_t dlv, uint32_t rw_c) {
+      if (lbytes && ll1 != ll0) tab1(ll1, col).z = rw_c & lbytes;
+      const int32_t d = (int32_t)(rec & 0x7fu);
+      if (d) {
+        const int32_t m = tau - d;
+        dups = m == last_m ? dups + 1 : 0;
+        if (dups > 1) {
+          q.err = GGRS_E_STATE;
+          return;
+        }
+        const uint32_t cf = 1u | (uint32_t)(1 + nchain % (kSL - 1)) << 4 | (uint32_t)d << 8 | (uint32_t)nchain << 16;
+        uint2* ce2 = dups ? reinterpret_cast<uint2*>(&tab1(m, col)) : reinterpret_cast<uint2*>(&tab0(m, col)) + 1;
+        *ce2 = make_uint2((uint32_t)dlv, cf);
+        ++nchain;
+        last_m = m;
+        if (m < cur0) minpre = min(minpre, m);
+      }
+      const uint32_t y = 1u | ((rec & 0x80u) ? 2u : 0u);
+      if (tau > own_hi) {
+        own_hi = tau;
+        tab0(tau, col) = make_uint4((uint32_t)dlv, y, 0u, 0u);
+        *reinterpret_cast<uint2*>(&tab1(tau, col)) = make_uint2(0u, 0u);
+      } else {
+        *reinterpret_cast<uint2*>(&tab0(tau, col)) = make_uint2((uint32_t)dlv, y);
+      }
+    };
     issue(0);
     bool tags_ok = store(0);
     __syncthreads();  // (1) tables and rings in
@@ -1376,7 +1404,7 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
             if (en) {
 #pragma unroll
               for (int j = 0; j < 8; j++) {
-                if (j < nj) emit(taus[j], lls0[j], lls1[j], recs[j], dlvs[j], 0u, rw8[j]);
+                if (j < nj) emit_fast(taus[j], lls0[j], lls1[j], recs[j], dlvs[j], rw8[j]);
                 if (kFeat && j < nj && p.interval > 0) sched_store_report(p, cb8 + j, s, reps[j], lcs[j], lls1[j]);
               }
             }
