@@ -795,6 +795,38 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
           ev8[j] = (in && p.events) ? p.events[(int64_t)ci * S + s] : 0u;
           if (kFeat && in && p.reports && p.reports[(int64_t)ci * S + s] != 0) ev8[j] |= kEvPeerReport;
         }
+        if constexpr (!kSparse) {
+          // The batch's calls through the fast form first, back to back, by selects (as the chains
+          // form's control wave); a batch where some session needs the general form runs call by
+          // call below from the state before it.  A stopped session (q.err) runs no call: its
+          // records say so.
+          const int nj = min(8, ce - cb8);
+          const bool idle = q.err != 0;
+          const bool en = !idle & mask_ok;
+          const SchedCtl<P> q0 = q;
+          bool ok = true;
+          uint32_t recs[8];
+          int32_t reps[8], lcs[8], lls1[8];
+#pragma unroll
+          for (int j = 0; j < 8; j++) {
+            recs[j] = 0u;
+            reps[j] = kNull;
+            lcs[j] = q.lconf;
+            if (j < nj) ok &= sched_fast_call<P, kPred, kFeat>(q, env, cm, cb8 + j, up8[j], ev8[j], recs[j], reps[j], en);
+            lls1[j] = q.local_last;
+          }
+          if (__builtin_expect(__all(ok | idle), 1)) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+              if (j < nj) {
+                lrec[(cb8 + j - cs) * kBlock + lt] = (Rec)(idle ? kStopBefore << 8 : recs[j]);
+                if (kFeat && p.interval > 0 && live) sched_store_report(p, cb8 + j, s, reps[j], lcs[j], lls1[j]);
+              }
+            }
+            continue;
+          }
+          q = q0;
+        }
         for (int j = 0; j < 8; j++) {
           const int32_t c = cb8 + j;
           if (c >= ce) break;
