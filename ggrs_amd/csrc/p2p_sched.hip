@@ -1352,6 +1352,11 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
     issue(0);
     bool tags_ok = store(0);
     __syncthreads();  // (1) tables and rings in
+    // the previous stage's change mask over its rows (its rows from lo_prev, n_prev of them)
+    uint64_t cm_prev = 0;
+    int32_t lo_prev = 0;
+    int n_prev = 0;
+    bool ok_prev = false;
 
     for (int it = 0; it <= nst; ++it) {
       if (it < nst) {
@@ -1370,14 +1375,27 @@ __global__ __launch_bounds__(kChainThreads) void p2p_sched_chains_kernel(SchedPa
         const bool mask_ok = nrows <= 64 && __all(tags_ok);
         uint64_t cm = 0;
         if (mask_ok) {
-          uint32_t prev = 0;
+          // the rows this stage shares with the previous one keep their bits (the same frames' rows):
+          // only the new rows are read
+          const int32_t sh = lo - lo_prev;
+          int r0 = 0;
+          if (ok_prev && sh > 0 && sh < n_prev) {
+            cm = cm_prev >> sh;
+            if (kPred == 0) cm &= ~1ull;  // (row 0 has no row before it in the stage)
+            r0 = n_prev - sh;
+          }
+          uint32_t prev = (kPred == 0 && r0 > 0) ? (uint32_t)lrows[(r0 - 1) * kCS + col] & rbytes : 0u;
 #pragma unroll 8
-          for (int r = 0; r < nrows; r++) {
+          for (int r = r0; r < nrows; r++) {
             const uint32_t v = (uint32_t)lrows[r * kCS + col] & rbytes;
             if (kPred == 0 ? (r > 0 && v != prev) : v != 0u) cm |= 1ull << r;
             prev = v;
           }
         }
+        cm_prev = cm;
+        lo_prev = lo;
+        n_prev = nrows;
+        ok_prev = mask_ok;
         SchedCtlEnv env;
         env.lo = lo;
         env.maxp = maxp;
