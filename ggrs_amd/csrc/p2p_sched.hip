@@ -885,9 +885,12 @@ __global__ __launch_bounds__(kSplit ? 2 * kBlock : kBlock) void p2p_sched_kernel
     bool at_start = true, replaying = false, second = false;
     int32_t h = 0, load = 0, slot_h = 0, save_at = 0;  // save_at: sparse, the replayed frame saved
     uint32_t rec = 0, rec2 = 0;
+    // the next call's record, read one call ahead (its LDS latency behind this call's steps)
+    Rec nrec = lrec[(min(c, ce - 1) - cs) * kBlock + lt];
     while (c < ce) {
       if (at_start) {
-        const Rec r = lrec[(c - cs) * kBlock + lt];
+        const Rec r = nrec;
+        nrec = lrec[(min(c + 1, ce - 1) - cs) * kBlock + lt];
         if constexpr (kSparse) {
           rec = r.x;
           rec2 = r.y;
