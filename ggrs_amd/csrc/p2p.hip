@@ -850,6 +850,8 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_canon_kernel(P2PParams p) {
     int32_t f = fs, h = 0, g = 0;
     bool at_start = true, replaying = false;
     uint32_t rem_conf = 0, rem_pred = 0;
+    // the next call's remote row, read one call ahead (its LDS latency behind this call's steps)
+    uint32_t next_rem = rows(fs - p.D) & rbytes;
     while (f < chunk_end) {
       if (at_start) {
         // check_checksum_send_interval (p2p_session.rs:939-975), before any rollback of this call
@@ -865,7 +867,8 @@ __global__ __launch_bounds__(kFlatBlock) void p2p_canon_kernel(P2PParams p) {
         }
         // poll of call f: the remote inputs of frame g = f - D against the prediction made for them
         g = f - p.D;
-        rem_conf = rows(g) & rbytes;
+        rem_conf = next_rem;
+        next_rem = rows(min(f + 1, chunk_end - 1) - p.D) & rbytes;
         const bool miss = rem_conf != (p.predictor == 0 ? prev_rem : 0u);
         prev_rem = rem_conf;
         rem_pred = p.predictor == 0 ? rem_conf : 0u;
